@@ -1,0 +1,250 @@
+"""Generate the golden vectors in tests/golden/ by running the REFERENCE itself.
+
+Run in the build container only (it reads /root/reference, which never travels):
+
+    python tests/golden/make_golden.py
+
+The reference (IseanB/SensorFusion-KalmanFilter) is imported with empty stub modules
+for ``numba`` (imported but unused, kf_workers.py:19) and ``utm`` (used only by the
+ingest step gps_to_modified_utm, kf_workers.py:319, which these vectors bypass by
+feeding pre-converted easting/northing). The imu_data.csv of the reference is absent
+(.MISSING_LARGE_BLOBS), so every stream here is synthetic and seeded.
+
+Fixtures written (inputs and the reference's outputs, nothing else):
+  ref15_full.npz    run_kalman_filter_full (kf_workers.py:623-728), cold start + warm
+                    start window, plus run_adaptive_threshold_kalman_filter (959-1058)
+  ref15_combos.npz  evaluate_combo_chunk_worker (kf_workers.py:22-97) on k=1..3 subsets
+  ref8_full.npz     hw5_2.run_kalman_filter (hw5_2.py:313-380)
+  cv_batch.npz      4/2 and 6/3 constant-velocity filters stepped with the reference's
+                    own predict_covariance (kf_workers.py:546-549) and
+                    calculate_kalman_gain (616-621), in the op order of 688-717
+"""
+import os
+import sys
+import types
+from itertools import combinations
+
+import numpy as np
+
+REF = '/root/reference'
+OUT = os.path.dirname(os.path.abspath(__file__))
+T0 = 1697739552.3362827  # first valid GPS stamp of gps_data.csv (KF_SensorFusion.ipynb:1331)
+
+
+def import_reference():
+    os.environ.setdefault('MPLBACKEND', 'Agg')
+    for name in ('numba', 'utm'):
+        if name not in sys.modules:
+            mod = types.ModuleType(name)
+            if name == 'numba':
+                mod.jit = lambda *a, **k: (lambda f: f)
+                mod.prange = range
+            sys.modules[name] = mod
+    sys.path.insert(0, REF)
+    import kf_workers  # noqa: E402
+    import hw5_2  # noqa: E402
+    return kf_workers, hw5_2
+
+
+def synth_events(seed, seconds=2.0, n_pre_imu=5, gps_hz=10.0, imu_hz=200.0, out_of_order=True):
+    """A GPS(10 Hz)+IMU(200 Hz) stream shaped like combine_sensor_data's output
+    (kf_workers.py:375-385): [(idx, 'GPS'|'IMU', t, payload)], sorted by t, GPS first
+    on ties. IMU payload = [t_str, roll, pitch, yaw, wx, wy, wz, ax, ay, az]
+    (kf_workers.py:367)."""
+    rng = np.random.RandomState(seed)
+    raw = []
+    # true motion: gentle accelerating drive
+    def truth(t):
+        tau = t - T0
+        p = np.array([3.0 * tau + 0.2 * tau ** 2, 1.5 * tau - 0.1 * tau ** 2, -32.6 + 0.05 * tau])
+        return p
+    t_imu = T0 - n_pre_imu / imu_hz
+    while t_imu < T0 + seconds:
+        acc = np.array([0.4, -0.2, 0.0]) + rng.normal(0, 0.05, 3)
+        payload = [repr(t_imu), *(rng.normal(0, 0.02, 3)), *(rng.normal(0, 0.01, 3)), *acc]
+        raw.append(('IMU', t_imu, payload))
+        t_imu += 1.0 / imu_hz + rng.uniform(-1e-4, 1e-4)
+    t_gps = T0
+    first = True
+    while t_gps < T0 + seconds:
+        p = truth(t_gps)
+        if first:
+            z = p.copy()
+            z[:2] = 0.0  # first fix is the UTM origin (kf_workers.py:327-328)
+            first = False
+        else:
+            z = p + rng.normal(0, np.sqrt(3.0), 3)
+        raw.append(('GPS', t_gps, {'time': t_gps, 'easting': float(z[0]), 'northing': float(z[1]),
+                                   'zone_number': 19, 'zone_letter': 'T', 'altitude': float(z[2])}))
+        t_gps += 1.0 / gps_hz + rng.uniform(-2e-3, 2e-3)
+    # stable sort with GPS entries first (kf_workers.py:378-384 appends GPS before IMU)
+    raw.sort(key=lambda e: (e[1], 0 if e[0] == 'GPS' else 1))
+    events = [(i, *e) for i, e in enumerate(raw)]
+    if out_of_order:
+        # exercise the dt<0 guard (kf_workers.py:683-685): swap two IMU entries late in the run
+        j = len(events) * 3 // 4
+        while events[j][1] != 'IMU' or events[j + 1][1] != 'IMU':
+            j += 1
+        a, b = events[j], events[j + 1]
+        events[j], events[j + 1] = (a[0], b[1], b[2], b[3]), (b[0], a[1], a[2], a[3])
+    return events
+
+
+def pack_events(events):
+    N = len(events)
+    etype = np.zeros(N, np.int8)
+    et = np.zeros(N)
+    gps = np.full((N, 3), np.nan)
+    imu = np.full((N, 9), np.nan)
+    for k, (_, s, t, d) in enumerate(events):
+        et[k] = t
+        if s == 'GPS':
+            gps[k] = [d['easting'], d['northing'], d['altitude']]
+        else:
+            etype[k] = 1
+            imu[k] = d[1:10]
+    return dict(ev_type=etype, ev_t=et, ev_gps=gps, ev_imu=imu)
+
+
+def ref15_full(kfw):
+    events = synth_events(seed=11)
+    sf = kfw.KF_SensorFusion('gps.csv', 'imu.csv')
+    sf.indexed_sensor_data = events
+    st, ld, P, prev = sf.run_kalman_filter_full(start_idx=0, end_idx=len(events))
+    out = pack_events(events)
+    out.update(cold_states=np.array(st), cold_logdets=np.array(ld), cold_P=np.array(P),
+               cold_prev_time=np.array(prev))
+    # warm-start window, as the experiment loop does (kf_workers.py:2316-2323)
+    s0 = len(events) // 3
+    st_a, ld_a, P_a, _ = sf.run_kalman_filter_full(start_idx=0, end_idx=s0)
+    st_w, ld_w, P_w, prev_w = sf.run_kalman_filter_full(start_idx=s0, end_idx=s0 + 60,
+                                                        initial_pt=P_a, initial_state=st_a[-1])
+    out.update(warm_start=np.array(s0), warm_init_P=np.array(P_a), warm_init_state=np.array(st_a[-1]),
+               warm_states=np.array(st_w), warm_logdets=np.array(ld_w), warm_P=np.array(P_w))
+    # adaptive threshold variant (kf_workers.py:959-1058)
+    thr = float(np.median(ld))
+    st_g, ld_g, P_g, prev_g, times_g = sf.run_adaptive_threshold_kalman_filter(
+        start_idx=0, end_idx=len(events), R_threshold=thr)
+    out.update(adapt_threshold=np.array(thr), adapt_states=np.array(st_g),
+               adapt_logdets=np.array(ld_g), adapt_P=np.array(P_g), adapt_times=np.array(times_g))
+    np.savez_compressed(os.path.join(OUT, 'ref15_full.npz'), **out)
+    print('ref15_full:', len(events), 'events; final logdet', ld[-1])
+
+
+def ref15_combos(kfw):
+    events = synth_events(seed=12, seconds=0.3, out_of_order=False)
+    sf = kfw.KF_SensorFusion('gps.csv', 'imu.csv')
+    sf.indexed_sensor_data = events
+    # warm start from a short full run, then 9 candidate measurements as in
+    # run_brute_force_kalman_filter_no_sampling_min_usage (kf_workers.py:1256-1263)
+    st, ld, P, prev = sf.run_kalman_filter_full(start_idx=0, end_idx=20)
+    cand = events[20:29]
+    target_end = events[28][2]
+    xt = np.zeros(15)
+    xt[0:6] = st[-1][1:7]
+    class_args = {
+        'get_state_transition_matrix': sf.get_state_transition_matrix,
+        'get_process_noise_covariance_matrix': sf.get_process_noise_covariance_matrix,
+        'predict_covariance': sf.predict_covariance,
+        'get_gps_observation_matrix': sf.get_gps_observation_matrix,
+        'get_gps_measurement_noise_covariance_matrix': sf.get_gps_measurement_noise_covariance_matrix,
+        'get_imu_observation_matrix': sf.get_imu_observation_matrix,
+        'get_imu_measurement_noise_covariance_matrix': sf.get_imu_measurement_noise_covariance_matrix,
+        'calculate_kalman_gain': sf.calculate_kalman_gain,
+    }
+    chunk = [c for k in (1, 2, 3) for c in combinations(cand, k)]
+    res = kfw.evaluate_combo_chunk_worker(chunk, xt, P, class_args, prev, target_end)
+    assert len(res) == len(chunk)
+    # ragged outputs -> flat + offsets
+    combo_pos = [[cand.index(e) for e in c] for c in chunk]
+    ld_flat, ld_off, tr_flat = [], [0], []
+    for r in res:
+        ld_flat.extend(r[5])
+        tr_flat.extend(r[1])
+        ld_off.append(len(ld_flat))
+    out = pack_events(cand)
+    ci = np.full((len(chunk), 3), -1, np.int32)
+    for i, c in enumerate(combo_pos):
+        ci[i, :len(c)] = c
+    out.update(x0=xt, P0=np.array(P), prev_time=np.array(prev), target_end=np.array(target_end),
+               combo_idx=ci, logdet_flat=np.array(ld_flat), offsets=np.array(ld_off),
+               traj_flat=np.array(tr_flat), x_final=np.array([r[3] for r in res]))
+    np.savez_compressed(os.path.join(OUT, 'ref15_combos.npz'), **out)
+    print('ref15_combos:', len(chunk), 'combos')
+
+
+def ref8_full(h5):
+    events = synth_events(seed=13, seconds=1.5, out_of_order=False)
+    sf = h5.KF_SensorFusion('gps.csv', 'imu.csv')
+    sf.indexed_sensor_data = events
+    st = sf.run_kalman_filter()
+    out = pack_events(events)
+    out.update(states=np.array(st, dtype=np.float64))
+    np.savez_compressed(os.path.join(OUT, 'ref8_full.npz'), **out)
+    print('ref8_full:', len(events), 'events')
+
+
+def cv_batch(kfw):
+    """4/2 and 6/3 constant-velocity filters stepped with the reference's own
+    predict_covariance / calculate_kalman_gain, in the op order of kf_workers.py:688-717.
+    The control term G u is the 15-state model's acceleration column applied to the IMU
+    acceleration (kf_workers.py:501-509)."""
+    sf = kfw.KF_SensorFusion('gps.csv', 'imu.csv')
+    rng = np.random.RandomState(14)
+    out = {}
+    for d, p0p, p0v in ((2, 1000.0, 100.0), (3, 10000.0, 1000.0)):
+        n = 2 * d
+        for k, T, dt0 in ((1, 48, 0.1), (5, 60, 0.01)):
+            B = 6
+            dt = np.full(T, dt0)
+            dt[3] = 0.0  # a zero-length step, like the re-processed initial GPS fix
+            dt[7] = dt0 * 1.7
+            u = rng.normal(0, 0.3, (T, d, B))
+            z = rng.normal(0, 50.0, (T // k, d, B)) + np.linspace(0, 30, T // k)[:, None, None]
+            x0 = np.zeros((B, n))
+            x0[:, :d] = rng.uniform(-1000, 1000, (B, d))
+            x0[:, d:] = rng.normal(0, 10, (B, d))
+            P0 = np.diag([p0p] * d + [p0v] * d)
+            traj = np.zeros((T, n, B))
+            logdet = np.zeros((T, B))
+            Pf = np.zeros((B, n, n))
+            H = np.eye(n)[:d]
+            R = np.diag([3.0] * d)
+            for b in range(B):
+                xt = x0[b].copy()
+                Pt = P0.copy()
+                for t in range(T):
+                    h = dt[t]
+                    F = np.eye(n)
+                    G = np.zeros((n, d))
+                    for i in range(d):
+                        F[i, d + i] = h
+                        G[i, i] = 0.5 * h ** 2
+                        G[d + i, i] = h
+                    Qt = np.diag([5.0 * h] * d + [1.0 * h] * d)
+                    xt = np.dot(F, xt) + np.dot(G, u[t, :, b])
+                    Pt = sf.predict_covariance(Pt, F, Qt)
+                    if (t + 1) % k == 0:
+                        K = sf.calculate_kalman_gain(Pt, H, R)
+                        y = np.array(z[t // k, :, b]) - np.dot(H, xt)
+                        xt = xt + np.dot(K, y)
+                        Pt = np.dot(np.eye(n) - np.dot(K, H), Pt)
+                    traj[t, :, b] = xt
+                    logdet[t, b] = np.linalg.slogdet(Pt)[1]
+                Pf[b] = Pt
+            key = f'cv{d}_k{k}'
+            out.update({f'{key}_dt': dt, f'{key}_u': u, f'{key}_z': z, f'{key}_x0': x0,
+                        f'{key}_P0': P0, f'{key}_traj': traj, f'{key}_logdet': logdet,
+                        f'{key}_Pfinal': Pf})
+    np.savez_compressed(os.path.join(OUT, 'cv_batch.npz'), **out)
+    print('cv_batch written')
+
+
+if __name__ == '__main__':
+    kfw, h5 = import_reference()
+    ref15_full(kfw)
+    ref15_combos(kfw)
+    ref8_full(h5)
+    cv_batch(kfw)
+    # analytic known answer: slogdet(P0) of kf_workers.py:651 = 6 ln 1e4 + 9 ln 1e3
+    print('KAT logdet(P0) =', np.linalg.slogdet(np.diag([1e4] * 3 + [1e3] * 9 + [1e4] * 3))[1])

@@ -1,0 +1,130 @@
+"""Pin the CPU oracle (oracle/ref_kf.py) against the reference's own outputs.
+
+The fixtures in tests/golden/ were produced by importing the reference
+(tests/golden/make_golden.py); these tests need no GPU and no reference checkout.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import ref_kf
+from golden_events import unpack_events
+
+RTOL = 1e-12
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def _rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1.0)))
+
+
+def test_kat_logdet_p0():
+    # slogdet of kf_workers.py:651's P0 = 6 ln 1e4 + 9 ln 1e3
+    ld = np.linalg.slogdet(ref_kf.P0_REF15)[1]
+    assert abs(ld - 117.43183974269634) < 1e-12
+    assert abs(ld - (6 * np.log(1e4) + 9 * np.log(1e3))) < 1e-12
+
+
+def test_ref15_full_cold_start(golden_dir):
+    g = _load(golden_dir, 'ref15_full.npz')
+    events = unpack_events(g)
+    st, ld, P, prev = ref_kf.run_kalman_filter_full(events, 0, len(events))
+    assert np.array(st).shape == g['cold_states'].shape
+    assert _rel(st, g['cold_states']) < RTOL
+    assert _rel(ld, g['cold_logdets']) < RTOL
+    assert _rel(P, g['cold_P']) < RTOL
+    assert prev == float(g['cold_prev_time'])
+
+
+def test_ref15_full_warm_start(golden_dir):
+    g = _load(golden_dir, 'ref15_full.npz')
+    events = unpack_events(g)
+    s0 = int(g['warm_start'])
+    st, ld, P, _ = ref_kf.run_kalman_filter_full(events, s0, s0 + 60, initial_pt=g['warm_init_P'].copy(),
+                                                 initial_state=tuple(g['warm_init_state']))
+    assert _rel(st, g['warm_states']) < RTOL
+    assert _rel(ld, g['warm_logdets']) < RTOL
+    assert _rel(P, g['warm_P']) < RTOL
+
+
+def test_ref15_adaptive_threshold(golden_dir):
+    g = _load(golden_dir, 'ref15_full.npz')
+    events = unpack_events(g)
+    st, ld, P, prev, times = ref_kf.run_adaptive_threshold(events, 0, len(events),
+                                                           R_threshold=float(g['adapt_threshold']))
+    assert _rel(st, g['adapt_states']) < RTOL
+    assert _rel(ld, g['adapt_logdets']) < RTOL
+    assert _rel(P, g['adapt_P']) < RTOL
+    np.testing.assert_array_equal(np.array(times), g['adapt_times'])
+
+
+def test_ref15_combo_worker(golden_dir):
+    g = _load(golden_dir, 'ref15_combos.npz')
+    cand = unpack_events(g)
+    chunk = [tuple(cand[i] for i in row if i >= 0) for row in g['combo_idx']]
+    res = ref_kf.evaluate_combo_chunk(chunk, g['x0'], g['P0'], float(g['prev_time']), float(g['target_end']))
+    ld_flat = [v for r in res for v in r[5]]
+    tr_flat = [v for r in res for v in r[1]]
+    assert _rel(ld_flat, g['logdet_flat']) < RTOL
+    assert _rel(tr_flat, g['traj_flat']) < RTOL
+    assert _rel([r[3] for r in res], g['x_final']) < RTOL
+    off = g['offsets']
+    assert [len(r[5]) for r in res] == list(np.diff(off))
+
+
+def test_ref8_full(golden_dir):
+    g = _load(golden_dir, 'ref8_full.npz')
+    events = unpack_events(g)
+    st, _ = ref_kf.run_kalman_filter_8state(events)
+    assert _rel(st, g['states']) < RTOL
+
+
+@pytest.mark.parametrize('d', [2, 3])
+@pytest.mark.parametrize('k', [1, 5])
+def test_cv_batch_and_loop(golden_dir, d, k):
+    g = _load(golden_dir, 'cv_batch.npz')
+    key = f'cv{d}_k{k}'
+    model = ref_kf.CVModel(d)
+    dt, u, z, x0, P0 = (g[f'{key}_{s}'] for s in ('dt', 'u', 'z', 'x0', 'P0'))
+    np.testing.assert_array_equal(P0, model.P0())
+    traj, ld, x, P = ref_kf.run_batch(model, x0, P0, dt, u, z, update_every=k)
+    assert _rel(traj, g[f'{key}_traj']) < RTOL
+    assert _rel(ld, g[f'{key}_logdet']) < RTOL
+    assert _rel(P, g[f'{key}_Pfinal']) < RTOL
+    for b in (0, x0.shape[0] - 1):
+        tl, ll, _, Pl = ref_kf.run_filter_loop(model, x0[b], P0, dt, u[:, :, b], z[:, :, b], update_every=k)
+        assert _rel(tl, g[f'{key}_traj'][:, :, b]) < RTOL
+        assert _rel(ll, g[f'{key}_logdet'][:, b]) < RTOL
+        assert _rel(Pl, g[f'{key}_Pfinal'][b]) < RTOL
+
+
+def test_tri_pack_roundtrip():
+    rng = np.random.default_rng(0)
+    A = rng.normal(size=(5, 6, 6))
+    P = A @ A.transpose(0, 2, 1)
+    back = ref_kf.tri_unpack(ref_kf.tri_pack(P), 6)
+    np.testing.assert_array_equal(back, P)
+
+
+def test_batch_mask_skips_update():
+    model = ref_kf.CV3
+    rng = np.random.default_rng(1)
+    B, T = 4, 6
+    x0 = rng.normal(size=(B, 6))
+    dt = np.full(T, 0.1)
+    u = rng.normal(size=(T, 3, B))
+    z = rng.normal(size=(T, 3, B))
+    mask = np.ones((T, B), bool)
+    mask[:, 2] = False
+    tr, ld, _, _ = ref_kf.run_batch(model, x0, model.P0(), dt, u, z, 1, mask=mask)
+    # a never-updated filter is pure prediction
+    tr_pred, ld_pred, _, _ = ref_kf.run_batch(model, x0[2:3], model.P0(), dt, u[:, :, 2:3], z[:, :, 2:3],
+                                              update_every=T + 1)
+    np.testing.assert_allclose(tr[:, :, 2], tr_pred[:, :, 0], rtol=1e-14)
+    np.testing.assert_allclose(ld[:, 2], ld_pred[:, 0], rtol=1e-14)
