@@ -1,0 +1,149 @@
+/*
+ * kf.h — C ABI of libkfmi.so, the MI355X (gfx950) batched Kalman-filter engine.
+ *
+ * One handle holds B independent filters of one model on one GPU.  State lives in HBM
+ * in structure-of-arrays form (filter index fastest):
+ *     x  [n][B]                 state estimate
+ *     P  [n(n+1)/2][B]          covariance, upper triangle packed row-major (i <= j)
+ *     status [B] int32          KF_OK, or KF_ENOTSPD once a filter lost positive-definiteness
+ * Per-step streams handed to the engine are device pointers in the same layout,
+ * with the time index slowest:  u [T][c][B], z [U][m][B], traj [T][n][B], logdet [T][B].
+ * Scalars are the handle's dtype (KF_F32 / KF_F64); time steps dt are always double
+ * (absolute epoch stamps ~1.7e9 s are differenced on the host in fp64).
+ *
+ * The reference (IseanB/SensorFusion-KalmanFilter) has no native boundary: its hot path
+ * is a per-event sequence of NumPy calls on KF_SensorFusion (kf_workers.py:493-621)
+ * driven by Python time loops (kf_workers.py:623-728, 22-97).  Each entry point below
+ * names the reference code it replaces.  The per-step math is
+ *     x = F x + G u;  P = F P F^T + Q;  K = P H^T (H P H^T + R)^-1;
+ *     x += K (z - H x);  P = (I - K H) P (I - K H)^T + K R K^T   (Joseph form)
+ * with S^-1 from an in-lane LDL^T factorisation and logdet(P) from an LDL^T of P.
+ *
+ * All functions return KF_OK (0) or a negative KF_E* code; kf_last_error() then
+ * describes the failure (thread-local).  Launching entry points are asynchronous on
+ * the given hipStream_t (NULL = the null stream) and never synchronise, allocate or
+ * free, so they can be captured into a hipGraph.
+ */
+#ifndef KFMI_KF_H
+#define KFMI_KF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KF_OK        0
+#define KF_EINVAL   (-1)  /* bad argument (shape, pointer, model, dtype)                      */
+#define KF_EHIP     (-2)  /* HIP runtime error                                                */
+#define KF_ENOTSPD  (-3)  /* per filter: S or P not positive definite; outputs become NaN.
+                             Mirrors the reference skipping a failing combo (kf_workers.py:88-91) */
+#define KF_ENODEV   (-4)  /* no usable gfx950 device                                          */
+#define KF_ENOMEM   (-5)  /* device allocation failed                                         */
+
+#define KF_F32 0
+#define KF_F64 1
+
+/* Models.  Both are restrictions of the reference models to [position, velocity] per axis,
+ * with the IMU acceleration moved from state to control input u:
+ *   KF_MODEL_CV2  n=4 m=2 c=2  [x, y, vx, vy]            hw5_2.py:219-304
+ *   KF_MODEL_CV3  n=6 m=3 c=3  [x, y, z, vx, vy, vz]     kf_workers.py:493-614
+ * F = [[I, dt I], [0, I]], G = [[dt^2/2 I], [dt I]], H = [I 0] (GPS position fix).       */
+#define KF_MODEL_CV2 2
+#define KF_MODEL_CV3 3
+
+/* Model constants; kf_default_params() fills the reference's values. */
+typedef struct kf_params {
+    double q_pos;   /* Q = diag(q_pos*dt I, q_vel*dt I): 5, 1   (kf_workers.py:521,523)        */
+    double q_vel;
+    double r[9];    /* R, m x m row-major, symmetric: 3 I       (kf_workers.py:581-585)        */
+    double p0_pos;  /* initial P = diag(p0_pos I, p0_vel I): CV3 1e4/1e3 (kf_workers.py:651), */
+    double p0_vel;  /*                                         CV2 1000/100 (hw5_2.py:317-326) */
+} kf_params;
+
+typedef struct kf_batch kf_batch;
+
+/* Library version string. */
+const char* kf_version(void);
+
+/* Thread-local description of the last failure on this thread ("" if none). */
+const char* kf_last_error(void);
+
+/* Reference constants for a model.  Replaces the hard-coded getters
+ * get_process_noise_covariance_matrix / get_gps_measurement_noise_covariance_matrix
+ * (kf_workers.py:519-544, 581-585) and the P0 literal (kf_workers.py:651). */
+int kf_default_params(int model, kf_params* out);
+
+/* Number of visible HIP devices (0 on a host without a GPU). */
+int kf_device_count(int* count);
+
+/* Select device `device` for the calling thread and check that it is gfx950.
+ * Idempotent.  No reference counterpart (the reference never leaves the CPU). */
+int kf_init(int device);
+
+/* Create a handle for `batch` filters of `model` in `dtype` on the current device, with
+ * x = 0, P = P0, status = KF_OK.  params may be NULL (reference constants).
+ * Replaces KF_SensorFusion.__init__ + the per-run initial state (kf_workers.py:641-651). */
+int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_params* params);
+int kf_free(kf_batch* handle);
+
+/* Dimensions of a handle (any pointer may be NULL). */
+int kf_dims(const kf_batch* handle, int* n, int* m, int* c, int64_t* batch, int* dtype);
+
+/* Re-initialise every filter: x = x0 (device [n][B]; NULL = zeros), P = P0, status = OK.
+ * The reference's cold start sets the position to the first GPS fix and everything else to
+ * zero (kf_workers.py:651-666). */
+int kf_reset(kf_batch* handle, const void* x0, void* stream);
+
+/* Copy state in/out.  on_device != 0: x/P are device pointers (async on stream);
+ * on_device == 0: host pointers (synchronous).  The warm start of the reference
+ * (initial_pt / initial_state, kf_workers.py:643-649) maps to kf_set_state. */
+int kf_set_state(kf_batch* handle, const void* x, const void* P, int on_device, void* stream);
+int kf_get_state(const kf_batch* handle, void* x, void* P, int on_device, void* stream);
+int kf_get_status(const kf_batch* handle, int32_t* status, int on_device, void* stream);
+
+/* One predict step for every filter: x = F(dt) x + G(dt) u, P = F P F^T + Q(dt).
+ * dt_per_filter: device [B] double (NULL = scalar dt for all filters; the brute-force caller
+ * has a different dt per combo, kf_workers.py:37).  u: device [c][B] (NULL = zero control).
+ * logdet_out: device [B] (NULL = skip), logdet of the predicted P, as the adaptive-threshold
+ * driver uses it (kf_workers.py:1023).
+ * Replaces get_state_transition_matrix + get_process_noise_covariance_matrix +
+ * x = np.dot(F, x) + predict_covariance (kf_workers.py:493-549, 688-691). */
+int kf_predict(kf_batch* handle, double dt, const double* dt_per_filter, const void* u,
+               void* logdet_out, void* stream);
+
+/* One GPS update for every filter: z device [m][B]; mask device [B] uint8 (NULL = all;
+ * 0 = skip this filter); logdet_out device [B] (NULL = skip).
+ * Replaces get_gps_observation_matrix + get_gps_measurement_noise_covariance_matrix +
+ * calculate_kalman_gain + the state/covariance update + slogdet
+ * (kf_workers.py:551-558, 581-585, 616-621, 694-717). */
+int kf_update(kf_batch* handle, const void* z, const uint8_t* mask, void* logdet_out, void* stream);
+
+/* The fused hot path: T steps for every filter in ONE launch, state held in registers.
+ * Step t predicts with dt_t (dt_steps device [T] double, or the scalar dt when NULL) and
+ * control u[t] (device [T][c][B]), then, when (t+1) % update_every == 0, updates with
+ * z[(t+1)/update_every - 1] (device [U][m][B], U = T / update_every) unless
+ * mask[(t+1)/update_every - 1][f] == 0 (mask device [U][B] uint8, NULL = all).
+ * traj (device [T][n][B]) and logdet (device [T][B]) receive x and logdet(P) after every
+ * step; either may be NULL.
+ * Replaces the time loop of run_kalman_filter_full (kf_workers.py:681-721) and the per-combo
+ * loop of evaluate_combo_chunk_worker (kf_workers.py:36-71), batched over filters. */
+int kf_run(kf_batch* handle, int T, double dt, const double* dt_steps, const void* u,
+           const void* z, const uint8_t* mask, int update_every, void* traj, void* logdet,
+           void* stream);
+
+/* Deterministic synthetic GPS+IMU streams for filters
+ * [filter_offset, filter_offset + B) of a global population: counter-based Philox4x32-10
+ * keyed by seed and the GLOBAL filter index, so any shard regenerates its own slice.
+ * Truth: p0 ~ U(-1000,1000) m, v0 ~ N(0,10^2) m/s, a_t ~ N(0,0.3^2); u_t = a_t + N(0,0.1^2);
+ * z = p_true + N(0,3).  x0_out [n][B] = (first fix, 0 velocity).  Outputs in the handle's
+ * dtype, computed in fp64 and rounded once.  Not a reference entry point: it replaces the
+ * missing imu_data.csv (.MISSING_LARGE_BLOBS) with a synthetic stream of the same shape. */
+int kf_synth(kf_batch* handle, uint64_t seed, int64_t filter_offset, int T, double dt,
+             int update_every, void* x0_out, void* u_out, void* z_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KFMI_KF_H */

@@ -1,0 +1,318 @@
+// C ABI of libkfmi.so (declared in include/kf.h): handle management, argument checking,
+// and dispatch to the gfx950 kernels in kf_cv.hip.  No compute happens here.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/kf.h"
+#include "kf_internal.h"
+
+struct kf_batch {
+    int model;
+    int axes;   // d: state n = 2d, measurement m = d, control c = d
+    int n, m, c;
+    int dtype;
+    int64_t B;
+    int device;
+    kf_params params;
+    void* x;          // [n][B]
+    void* P;          // [n(n+1)/2][B]
+    int32_t* status;  // [B]
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(KF_EHIP, "%s: %s (%d)", what, hipGetErrorString(e), static_cast<int>(e));
+}
+
+size_t elem(const kf_batch* h) { return h->dtype == KF_F64 ? 8 : 4; }
+int64_t ntri(const kf_batch* h) { return int64_t(h->n) * (h->n + 1) / 2; }
+
+kfmi::CvArgs base_args(const kf_batch* h) {
+    kfmi::CvArgs a{};
+    a.B = h->B;
+    a.T = 1;
+    a.update_every = 1;
+    a.x = h->x;
+    a.P = h->P;
+    a.status = h->status;
+    a.q_pos = h->params.q_pos;
+    a.q_vel = h->params.q_vel;
+    int k = 0;
+    for (int i = 0; i < h->m; ++i)
+        for (int j = i; j < h->m; ++j) a.r[k++] = h->params.r[i * h->m + j];
+    a.p0_pos = h->params.p0_pos;
+    a.p0_vel = h->params.p0_vel;
+    return a;
+}
+
+int launch(const kf_batch* h, kfmi::Op op, const kfmi::CvArgs& a, void* stream, const char* what) {
+    if (h->B == 0) return KF_OK;
+    hipError_t e = kfmi::launch_cv(h->axes, h->dtype == KF_F64, op, a, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, what);
+    return KF_OK;
+}
+
+int check_handle(const kf_batch* h) {
+    if (!h) return fail(KF_EINVAL, "null kf_batch handle");
+    return KF_OK;
+}
+
+int model_axes(int model) {
+    switch (model) {
+        case KF_MODEL_CV2: return 2;
+        case KF_MODEL_CV3: return 3;
+        default: return 0;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* kf_version(void) { return "kfmi 0.1.0 (gfx950)"; }
+
+const char* kf_last_error(void) { return g_err.c_str(); }
+
+int kf_default_params(int model, kf_params* out) {
+    const int d = model_axes(model);
+    if (!d) return fail(KF_EINVAL, "unknown model %d", model);
+    if (!out) return fail(KF_EINVAL, "null params");
+    std::memset(out, 0, sizeof *out);
+    out->q_pos = 5.0;  // position_noise = 5 * dt   (kf_workers.py:521)
+    out->q_vel = 1.0;  // velocity_noise = 1 * dt   (kf_workers.py:523)
+    for (int i = 0; i < d; ++i) out->r[i * d + i] = 3.0;  // gps variance 3 (kf_workers.py:583)
+    if (d == 3) {
+        out->p0_pos = 10000.0;  // kf_workers.py:651
+        out->p0_vel = 1000.0;
+    } else {
+        out->p0_pos = 1000.0;   // hw5_2.py:318-319
+        out->p0_vel = 100.0;    // hw5_2.py:321-322
+    }
+    return KF_OK;
+}
+
+int kf_device_count(int* count) {
+    if (!count) return fail(KF_EINVAL, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    *count = (e == hipSuccess) ? n : 0;
+    return KF_OK;
+}
+
+int kf_init(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(KF_ENODEV, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(KF_ENODEV, "device %d out of range [0,%d)", device, n);
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(KF_ENODEV, "device %d is %s; libkfmi is built for gfx950 only", device, prop.gcnArchName);
+    return KF_OK;
+}
+
+int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_params* params) {
+    if (!handle) return fail(KF_EINVAL, "null handle out-pointer");
+    *handle = nullptr;
+    const int d = model_axes(model);
+    if (!d) return fail(KF_EINVAL, "unknown model %d", model);
+    if (dtype != KF_F32 && dtype != KF_F64) return fail(KF_EINVAL, "unknown dtype %d", dtype);
+    if (batch < 0) return fail(KF_EINVAL, "negative batch %lld", static_cast<long long>(batch));
+    if (batch > (int64_t(1) << 40)) return fail(KF_EINVAL, "batch %lld too large", static_cast<long long>(batch));
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return fail(KF_ENODEV, "no current HIP device: %s", hipGetErrorString(e));
+    kf_batch* h = new kf_batch{};
+    h->model = model;
+    h->axes = d;
+    h->n = 2 * d;
+    h->m = d;
+    h->c = d;
+    h->dtype = dtype;
+    h->B = batch;
+    h->device = dev;
+    if (params) {
+        h->params = *params;
+    } else {
+        kf_default_params(model, &h->params);
+    }
+    const size_t w = elem(h);
+    const size_t nb = static_cast<size_t>(batch);
+    if (nb) {
+        if (hipMalloc(&h->x, w * h->n * nb) != hipSuccess ||
+            hipMalloc(&h->P, w * ntri(h) * nb) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&h->status), sizeof(int32_t) * nb) != hipSuccess) {
+            (void)hipGetLastError();
+            kf_free(h);
+            return fail(KF_ENOMEM, "hipMalloc of %zu filters failed", nb);
+        }
+    }
+    int rc = kf_reset(h, nullptr, nullptr);
+    if (rc == KF_OK && nb) {
+        e = hipStreamSynchronize(nullptr);
+        if (e != hipSuccess) rc = hip_fail(e, "kf_alloc reset");
+    }
+    if (rc != KF_OK) {
+        kf_free(h);
+        return rc;
+    }
+    *handle = h;
+    return KF_OK;
+}
+
+int kf_free(kf_batch* h) {
+    if (!h) return KF_OK;
+    if (h->x) (void)hipFree(h->x);
+    if (h->P) (void)hipFree(h->P);
+    if (h->status) (void)hipFree(h->status);
+    delete h;
+    return KF_OK;
+}
+
+int kf_dims(const kf_batch* h, int* n, int* m, int* c, int64_t* batch, int* dtype) {
+    if (int rc = check_handle(h)) return rc;
+    if (n) *n = h->n;
+    if (m) *m = h->m;
+    if (c) *c = h->c;
+    if (batch) *batch = h->B;
+    if (dtype) *dtype = h->dtype;
+    return KF_OK;
+}
+
+int kf_reset(kf_batch* h, const void* x0, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    kfmi::CvArgs a = base_args(h);
+    a.x0 = x0;
+    return launch(h, kfmi::Op::Reset, a, stream, "kf_reset");
+}
+
+int kf_set_state(kf_batch* h, const void* x, const void* P, int on_device, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (!x && !P) return fail(KF_EINVAL, "kf_set_state: x and P both null");
+    const hipMemcpyKind kind = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    const size_t w = elem(h), nb = static_cast<size_t>(h->B);
+    hipError_t e = hipSuccess;
+    if (x && nb) e = hipMemcpyAsync(h->x, x, w * h->n * nb, kind, static_cast<hipStream_t>(stream));
+    if (e == hipSuccess && P && nb)
+        e = hipMemcpyAsync(h->P, P, w * ntri(h) * nb, kind, static_cast<hipStream_t>(stream));
+    if (e == hipSuccess && nb)
+        e = hipMemsetAsync(h->status, 0, sizeof(int32_t) * nb, static_cast<hipStream_t>(stream));
+    if (e == hipSuccess && !on_device) e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "kf_set_state");
+    return KF_OK;
+}
+
+int kf_get_state(const kf_batch* h, void* x, void* P, int on_device, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    const hipMemcpyKind kind = on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    const size_t w = elem(h), nb = static_cast<size_t>(h->B);
+    hipError_t e = hipSuccess;
+    if (x && nb) e = hipMemcpyAsync(x, h->x, w * h->n * nb, kind, static_cast<hipStream_t>(stream));
+    if (e == hipSuccess && P && nb)
+        e = hipMemcpyAsync(P, h->P, w * ntri(h) * nb, kind, static_cast<hipStream_t>(stream));
+    if (e == hipSuccess && !on_device) e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "kf_get_state");
+    return KF_OK;
+}
+
+int kf_get_status(const kf_batch* h, int32_t* status, int on_device, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (!status) return fail(KF_EINVAL, "kf_get_status: null output");
+    const size_t nb = static_cast<size_t>(h->B);
+    if (!nb) return KF_OK;
+    hipError_t e = hipMemcpyAsync(status, h->status, sizeof(int32_t) * nb,
+                                  on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                                  static_cast<hipStream_t>(stream));
+    if (e == hipSuccess && !on_device) e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "kf_get_status");
+    return KF_OK;
+}
+
+int kf_predict(kf_batch* h, double dt, const double* dt_per_filter, const void* u, void* logdet_out,
+               void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (!dt_per_filter && !(dt >= 0.0)) return fail(KF_EINVAL, "kf_predict: dt must be >= 0 (got %g)", dt);
+    kfmi::CvArgs a = base_args(h);
+    a.dt = dt;
+    a.dt_filter = dt_per_filter;
+    a.u = u;
+    a.logdet = logdet_out;
+    return launch(h, kfmi::Op::Predict, a, stream, "kf_predict");
+}
+
+int kf_update(kf_batch* h, const void* z, const uint8_t* mask, void* logdet_out, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (!z && h->B) return fail(KF_EINVAL, "kf_update: null measurement stream z");
+    kfmi::CvArgs a = base_args(h);
+    a.z = z;
+    a.mask = mask;
+    a.logdet = logdet_out;
+    return launch(h, kfmi::Op::Update, a, stream, "kf_update");
+}
+
+int kf_run(kf_batch* h, int T, double dt, const double* dt_steps, const void* u, const void* z,
+           const uint8_t* mask, int update_every, void* traj, void* logdet, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (T < 0) return fail(KF_EINVAL, "kf_run: T = %d < 0", T);
+    if (update_every < 1) return fail(KF_EINVAL, "kf_run: update_every = %d < 1", update_every);
+    if (!dt_steps && !(dt >= 0.0)) return fail(KF_EINVAL, "kf_run: dt must be >= 0 (got %g)", dt);
+    const int U = T / update_every;
+    if (U > 0 && !z && h->B) return fail(KF_EINVAL, "kf_run: %d updates need a z stream", U);
+    if (T == 0) return KF_OK;
+    kfmi::CvArgs a = base_args(h);
+    a.T = T;
+    a.update_every = update_every;
+    a.dt = dt;
+    a.dt_steps = dt_steps;
+    a.u = u;
+    a.z = z;
+    a.mask = mask;
+    a.traj = traj;
+    a.logdet = logdet;
+    return launch(h, kfmi::Op::Run, a, stream, "kf_run");
+}
+
+int kf_synth(kf_batch* h, uint64_t seed, int64_t filter_offset, int T, double dt, int update_every,
+             void* x0_out, void* u_out, void* z_out, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (T < 0 || update_every < 1 || filter_offset < 0)
+        return fail(KF_EINVAL, "kf_synth: bad T/update_every/filter_offset");
+    if (h->B && (!x0_out || (T > 0 && !u_out) || (T / update_every > 0 && !z_out)))
+        return fail(KF_EINVAL, "kf_synth: null output stream");
+    if (h->B == 0) return KF_OK;
+    kfmi::SynthArgs a{};
+    a.B = h->B;
+    a.filter_offset = filter_offset;
+    a.seed = seed;
+    a.T = T;
+    a.update_every = update_every;
+    a.dt = dt;
+    a.x0 = x0_out;
+    a.u = u_out;
+    a.z = z_out;
+    hipError_t e = kfmi::launch_synth(h->axes, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "kf_synth");
+    return KF_OK;
+}
+
+}  // extern "C"

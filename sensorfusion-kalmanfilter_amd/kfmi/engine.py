@@ -1,0 +1,199 @@
+"""BatchedKF — the Python face of libkfmi.so: B independent Kalman filters on one MI355X.
+
+The per-step call shape follows the reference's fusion loop (kf_workers.py:688-717):
+``predict(dt, u)`` then ``update(z)`` per event, or the fused ``run(...)`` over T steps
+(the hot path, one kernel launch).  Device buffers are torch tensors (torch is only the
+allocator / stream provider here); all arithmetic happens in the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import KFError, check
+
+MODELS = {
+    # name: (model id, axes d); n = 2d, m = d, c = d
+    'cv2': (_lib.KF_MODEL_CV2, 2),   # 4-state/2-meas, hw5_2.py:219-304 restricted to [x,y,vx,vy]
+    'cv3': (_lib.KF_MODEL_CV3, 3),   # 6-state/3-meas, kf_workers.py:493-614 restricted to pos/vel
+}
+DTYPES = {'f32': (_lib.KF_F32, torch.float32, np.float32), 'f64': (_lib.KF_F64, torch.float64, np.float64)}
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def default_params(model):
+    p = _lib.kf_params()
+    check(_lib.lib().kf_default_params(MODELS[model][0], ctypes.byref(p)))
+    return p
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(_lib.lib().kf_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class BatchedKF:
+    """``batch`` independent filters of ``model`` ('cv2' | 'cv3') in ``dtype`` ('f32' | 'f64').
+
+    State layout in HBM (SoA, filter index fastest): x [n, B], P [n(n+1)/2, B] (upper
+    triangle packed row-major), status [B] int32.
+    """
+
+    def __init__(self, model='cv3', batch=1, dtype='f64', device=0, params=None):
+        if model not in MODELS:
+            raise ValueError(f'unknown model {model!r}; choose from {sorted(MODELS)}')
+        if dtype not in DTYPES:
+            raise ValueError(f'unknown dtype {dtype!r}; choose from {sorted(DTYPES)}')
+        self.model = model
+        self.dtype = dtype
+        self.batch = int(batch)
+        if self.batch < 0:
+            raise ValueError('batch must be >= 0')
+        self.device = torch.device('cuda', device)
+        self.axes = MODELS[model][1]
+        self.n, self.m, self.c = 2 * self.axes, self.axes, self.axes
+        self.ntri = self.n * (self.n + 1) // 2
+        self.torch_dtype = DTYPES[dtype][1]
+        L = _lib.lib()
+        check(L.kf_init(device))
+        torch.cuda.set_device(self.device)
+        self.params = params if params is not None else default_params(model)
+        h = ctypes.c_void_p()
+        check(L.kf_alloc(ctypes.byref(h), MODELS[model][0], self.batch, DTYPES[dtype][0],
+                         ctypes.byref(self.params)))
+        self._h = h
+
+    # -- lifecycle ---------------------------------------------------------------------
+    def close(self):
+        if getattr(self, '_h', None):
+            _lib.lib().kf_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        if not self._h:
+            raise KFError(_lib.KF_EINVAL, 'BatchedKF is closed')
+        return self._h
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # -- buffers -------------------------------------------------------------------------
+    def empty(self, *shape, dtype=None):
+        return torch.empty(shape, dtype=dtype or self.torch_dtype, device=self.device)
+
+    def _dev(self, a, shape, name, dtype=None):
+        """Validate (or move) an input stream to a contiguous device tensor of `shape`."""
+        dt = dtype or self.torch_dtype
+        if isinstance(a, np.ndarray):
+            a = torch.from_numpy(np.ascontiguousarray(a))
+        if not torch.is_tensor(a):
+            raise TypeError(f'{name}: expected a torch tensor or numpy array, got {type(a)}')
+        if tuple(a.shape) != tuple(shape):
+            raise ValueError(f'{name}: shape {tuple(a.shape)} != expected {tuple(shape)}')
+        if a.dtype != dt:
+            raise TypeError(f'{name}: dtype {a.dtype} != expected {dt}')
+        if a.device != self.device:
+            a = a.to(self.device)
+        return a.contiguous()
+
+    # -- state ---------------------------------------------------------------------------
+    def reset(self, x0=None):
+        """x = x0 ([n, B]; None = zeros), P = P0, status = OK (kf_workers.py:651-666)."""
+        x0d = self._dev(x0, (self.n, self.batch), 'x0') if x0 is not None else None
+        check(_lib.lib().kf_reset(self.handle, _ptr(x0d), self._stream()))
+
+    def set_state(self, x, P):
+        xd = self._dev(x, (self.n, self.batch), 'x')
+        Pd = self._dev(P, (self.ntri, self.batch), 'P')
+        check(_lib.lib().kf_set_state(self.handle, _ptr(xd), _ptr(Pd), 1, self._stream()))
+
+    def state(self):
+        """(x [n, B], P_packed [n(n+1)/2, B]) as new device tensors."""
+        x = self.empty(self.n, self.batch)
+        P = self.empty(self.ntri, self.batch)
+        check(_lib.lib().kf_get_state(self.handle, _ptr(x), _ptr(P), 1, self._stream()))
+        return x, P
+
+    def status(self):
+        s = torch.empty(self.batch, dtype=torch.int32, device=self.device)
+        check(_lib.lib().kf_get_status(self.handle, _ptr(s), 1, self._stream()))
+        return s
+
+    # -- per-step call shape (kf_workers.py:688-717) ----------------------------------------
+    def predict(self, dt, u=None, dt_per_filter=None, logdet=False):
+        """x = F(dt) x + G(dt) u, P = F P F^T + Q(dt).  Returns logdet(P_pred) [B] if asked."""
+        ud = self._dev(u, (self.c, self.batch), 'u') if u is not None else None
+        dtf = (self._dev(dt_per_filter, (self.batch,), 'dt_per_filter', torch.float64)
+               if dt_per_filter is not None else None)
+        ld = self.empty(self.batch) if logdet else None
+        check(_lib.lib().kf_predict(self.handle, float(dt if dt is not None else 0.0), _ptr(dtf),
+                                    _ptr(ud), _ptr(ld), self._stream()))
+        return ld
+
+    def update(self, z, mask=None, logdet=True):
+        """GPS update with z [m, B]; mask [B] (0 = skip).  Returns logdet(P) [B] if asked."""
+        zd = self._dev(z, (self.m, self.batch), 'z')
+        md = self._dev(mask, (self.batch,), 'mask', torch.uint8) if mask is not None else None
+        ld = self.empty(self.batch) if logdet else None
+        check(_lib.lib().kf_update(self.handle, _ptr(zd), _ptr(md), _ptr(ld), self._stream()))
+        return ld
+
+    # -- fused hot path -----------------------------------------------------------------
+    def run(self, u, z, dt=None, dt_steps=None, update_every=1, mask=None, traj=True, logdet=True,
+            out=None):
+        """T fused predict(+update) steps in one launch.
+
+        u [T, c, B]; z [T // update_every, m, B]; dt scalar or dt_steps [T] (float64);
+        mask [T // update_every, B] uint8 or None.  Returns (traj [T, n, B], logdet [T, B]);
+        pass ``out=(traj, logdet)`` to reuse buffers (either may be None to skip it)."""
+        T = int(u.shape[0])
+        U = T // update_every
+        ud = self._dev(u, (T, self.c, self.batch), 'u')
+        zd = self._dev(z, (U, self.m, self.batch), 'z') if U > 0 else None
+        md = self._dev(mask, (U, self.batch), 'mask', torch.uint8) if mask is not None else None
+        dts = self._dev(dt_steps, (T,), 'dt_steps', torch.float64) if dt_steps is not None else None
+        if dts is None and dt is None:
+            raise ValueError('run: give dt (scalar) or dt_steps [T]')
+        if out is not None:
+            tr, ld = out
+            if tr is not None:
+                tr = self._dev(tr, (T, self.n, self.batch), 'traj')
+            if ld is not None:
+                ld = self._dev(ld, (T, self.batch), 'logdet')
+        else:
+            tr = self.empty(T, self.n, self.batch) if traj else None
+            ld = self.empty(T, self.batch) if logdet else None
+        check(_lib.lib().kf_run(self.handle, T, float(dt or 0.0), _ptr(dts), _ptr(ud), _ptr(zd),
+                                _ptr(md), int(update_every), _ptr(tr), _ptr(ld), self._stream()))
+        return tr, ld
+
+    # -- synthetic streams -----------------------------------------------
+    def synth(self, T, dt, update_every=1, seed=20251015, filter_offset=0):
+        """Deterministic synthetic (x0 [n,B], u [T,c,B], z [U,m,B]) generated on the GPU."""
+        U = T // update_every
+        x0 = self.empty(self.n, self.batch)
+        u = self.empty(T, self.c, self.batch)
+        z = self.empty(max(U, 0), self.m, self.batch)
+        check(_lib.lib().kf_synth(self.handle, int(seed), int(filter_offset), int(T), float(dt),
+                                  int(update_every), _ptr(x0), _ptr(u), _ptr(z), self._stream()))
+        return x0, u, z

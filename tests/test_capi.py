@@ -1,0 +1,75 @@
+"""The C ABI library loads and exports what include/kf.h declares (no GPU needed).
+
+Only non-compute entry points are called here; on a host without a GPU they must fail
+cleanly (KF_ENODEV), never fall back to a CPU path.
+"""
+import ctypes
+import os
+
+import pytest
+
+import kfmi
+from kfmi import _lib
+
+
+def test_library_present_and_loads():
+    assert os.path.exists(_lib.LIB_PATH), 'libkfmi.so not built (run __graft_entry__.build())'
+    L = _lib.lib()
+    assert L.kf_version().decode().startswith('kfmi')
+
+
+def test_every_header_function_is_exported_and_bound():
+    names = _lib.header_functions()
+    assert len(names) >= 15
+    L = _lib.lib()
+    for n in names:
+        assert hasattr(L, n), f'{n} declared in include/kf.h but not exported'
+    # the ctypes signature table covers exactly the header
+    assert sorted(_lib.SIGNATURES) == names
+
+
+def test_header_constants_match_binding():
+    text = open(_lib.HEADER).read()
+    for name in ('KF_OK', 'KF_EINVAL', 'KF_EHIP', 'KF_ENOTSPD', 'KF_ENODEV', 'KF_ENOMEM',
+                 'KF_F32', 'KF_F64', 'KF_MODEL_CV2', 'KF_MODEL_CV3'):
+        import re
+        m = re.search(rf'#define {name}\s+\(?(-?\d+)\)?', text)
+        assert m, name
+        assert int(m.group(1)) == getattr(_lib, name), name
+
+
+def test_default_params_are_reference_constants():
+    p = kfmi.default_params('cv3')
+    assert (p.q_pos, p.q_vel) == (5.0, 1.0)             # kf_workers.py:521,523
+    assert list(p.r) == [3, 0, 0, 0, 3, 0, 0, 0, 3]     # kf_workers.py:583
+    assert (p.p0_pos, p.p0_vel) == (1e4, 1e3)           # kf_workers.py:651
+    p2 = kfmi.default_params('cv2')
+    assert list(p2.r)[:4] == [3, 0, 0, 3]
+    assert (p2.p0_pos, p2.p0_vel) == (1000.0, 100.0)    # hw5_2.py:317-326
+    L = _lib.lib()
+    assert L.kf_default_params(99, ctypes.byref(_lib.kf_params())) == _lib.KF_EINVAL
+    assert 'unknown model' in _lib.last_error()
+
+
+def test_null_handle_is_einval():
+    L = _lib.lib()
+    assert L.kf_run(None, 4, 0.1, None, None, None, None, 1, None, None, None) == _lib.KF_EINVAL
+    assert 'null' in _lib.last_error()
+    assert L.kf_free(None) == _lib.KF_OK
+
+
+def test_no_gpu_fails_loudly():
+    if kfmi.device_count() > 0:
+        pytest.skip('a GPU is visible; covered by the gpu tests')
+    L = _lib.lib()
+    assert L.kf_init(0) == _lib.KF_ENODEV
+    with pytest.raises(kfmi.KFError) as e:
+        kfmi.BatchedKF('cv3', 8, 'f64')
+    assert e.value.code == _lib.KF_ENODEV
+
+
+def test_bad_model_and_dtype_rejected_before_device():
+    with pytest.raises(ValueError):
+        kfmi.BatchedKF('cv9', 8, 'f64')
+    with pytest.raises(ValueError):
+        kfmi.BatchedKF('cv3', 8, 'bf16')
