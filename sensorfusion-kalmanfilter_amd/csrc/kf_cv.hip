@@ -16,7 +16,9 @@
 //            Joseph: P = (I-KH) P (I-KH)^T + K R K^T evaluated as Y + E K^T with
 //            Y = (I-KH) P and E = K R - Y H^T (the same polynomial in K, so the same
 //            first-order insensitivity to gain error; only the upper triangle is formed)
-//   logdet   LDL^T(P): sum of log pivots via frexp mantissa product (no sqrt, one log)
+//   logdet   LDL^T(P): log of the pivot product (no sqrt, one log per step)
+// A non-positive pivot of S turns its reciprocal into NaN, which poisons K, x and P of that
+// filter without a branch (status KF_ENOTSPD); the other lanes are unaffected.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -34,21 +36,8 @@ __host__ __device__ constexpr int tri(int i, int j) {
     return i <= j ? i * N - i * (i - 1) / 2 + (j - i) : j * N - j * (j - 1) / 2 + (i - j);
 }
 
-__device__ __forceinline__ double rcp(double d) {
-    double r = __builtin_amdgcn_rcp(d);  // v_rcp_f64, then two Newton steps -> ~1 ulp
-    double e = __builtin_fma(-d, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    e = __builtin_fma(-d, r, 1.0);
-    return __builtin_fma(r, e, r);
-}
-__device__ __forceinline__ float rcp(float d) {
-    float r = __builtin_amdgcn_rcpf(d);
-    float e = __builtin_fmaf(-d, r, 1.0f);
-    return __builtin_fmaf(r, e, r);
-}
-
-__device__ __forceinline__ double log_pos(double v) { return log(v); }
-__device__ __forceinline__ float log_pos(float v) { return __logf(v); }
+__device__ __forceinline__ double fmaT(double a, double b, double c) { return __builtin_fma(a, b, c); }
+__device__ __forceinline__ float fmaT(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
 template <typename T>
 __device__ __forceinline__ T quiet_nan();
@@ -57,16 +46,34 @@ __device__ __forceinline__ double quiet_nan<double>() { return __builtin_nan("")
 template <>
 __device__ __forceinline__ float quiet_nan<float>() { return __builtin_nanf(""); }
 
-// log det of an SPD N x N matrix (packed upper) via LDL^T.  Returns NaN if a pivot is
-// not > 0 (covariance lost positive definiteness).
+// 1/d refined by Newton steps (v_rcp_* is an approximation); NaN when !(d > 0).
+template <int NEWTON>
+__device__ __forceinline__ double rcp_pos(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+#pragma unroll
+    for (int i = 0; i < NEWTON; ++i) r = fmaT(r, fmaT(-d, r, 1.0), r);
+    return d > 0.0 ? r : quiet_nan<double>();
+}
+template <int NEWTON>
+__device__ __forceinline__ float rcp_pos(float d) {
+    float r = __builtin_amdgcn_rcpf(d);
+    r = fmaT(r, fmaT(-d, r, 1.0f), r);
+    return d > 0.0f ? r : quiet_nan<float>();
+}
+
+__device__ __forceinline__ double log_pos(double v) { return log(v); }
+__device__ __forceinline__ float log_pos(float v) { return __logf(v); }
+
+// log det of an SPD N x N matrix (packed upper) via LDL^T: log of the pivot product, with
+// the product renormalised by its binary exponent every 3 pivots so fp32 cannot overflow.
+// NaN if a pivot is not > 0 (covariance lost positive definiteness).
 template <int N, typename T>
 __device__ __forceinline__ T logdet_ldl(const T (&P)[N * (N + 1) / 2]) {
     T L[N][N];
     T d[N];
-    T dinv[N];
-    bool ok = true;
-    T mant = T(1);
+    T prod = T(1);
     int ex = 0;
+    bool ok = true;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         T v[N];
@@ -74,25 +81,28 @@ __device__ __forceinline__ T logdet_ldl(const T (&P)[N * (N + 1) / 2]) {
 #pragma unroll
         for (int k = 0; k < j; ++k) {
             v[k] = L[j][k] * d[k];
-            dj = __builtin_fma(-L[j][k], v[k], dj);
+            dj = fmaT(-L[j][k], v[k], dj);
         }
         ok = ok && (dj > T(0));
         d[j] = dj;
-        int e;
-        mant *= frexp(dj, &e);
-        ex += e;
+        prod *= dj;
+        if (j % 3 == 2 || j == N - 1) {
+            int e;
+            prod = frexp(prod, &e);
+            ex += e;
+        }
         if (j + 1 < N) {
-            dinv[j] = rcp(dj);
+            const T dinv = rcp_pos<1>(dj);
 #pragma unroll
             for (int i = j + 1; i < N; ++i) {
                 T s = P[tri<N>(i, j)];
 #pragma unroll
-                for (int k = 0; k < j; ++k) s = __builtin_fma(-L[i][k], v[k], s);
-                L[i][j] = s * dinv[j];
+                for (int k = 0; k < j; ++k) s = fmaT(-L[i][k], v[k], s);
+                L[i][j] = s * dinv;
             }
         }
     }
-    const T ld = log_pos(mant) + T(ex) * T(0.69314718055994530942);
+    const T ld = log_pos(prod) + T(ex) * T(0.69314718055994530942);
     return ok ? ld : quiet_nan<T>();
 }
 
@@ -109,8 +119,8 @@ struct Cv {
         const T hdt2 = T(0.5) * dt * dt;
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            x[i] = __builtin_fma(hdt2, u[i], __builtin_fma(dt, x[D + i], x[i]));
-            x[D + i] = __builtin_fma(dt, u[i], x[D + i]);
+            x[i] = fmaT(hdt2, u[i], fmaT(dt, x[D + i], x[i]));
+            x[D + i] = fmaT(dt, u[i], x[D + i]);
         }
         // With P = [[A, Bm], [Bm^T, C]]:  Bm' = Bm + dt C,  A' = A + dt (Bm' + Bm^T),  C' = C.
         T Bn[D][D];
@@ -118,12 +128,12 @@ struct Cv {
         for (int i = 0; i < D; ++i)
 #pragma unroll
             for (int j = 0; j < D; ++j)
-                Bn[i][j] = __builtin_fma(dt, P[tri<N>(D + i, D + j)], P[tri<N>(i, D + j)]);
+                Bn[i][j] = fmaT(dt, P[tri<N>(D + i, D + j)], P[tri<N>(i, D + j)]);
 #pragma unroll
         for (int i = 0; i < D; ++i)
 #pragma unroll
             for (int j = i; j < D; ++j)
-                P[tri<N>(i, j)] = __builtin_fma(dt, Bn[i][j] + P[tri<N>(j, D + i)], P[tri<N>(i, j)]);
+                P[tri<N>(i, j)] = fmaT(dt, Bn[i][j] + P[tri<N>(j, D + i)], P[tri<N>(i, j)]);
 #pragma unroll
         for (int i = 0; i < D; ++i)
 #pragma unroll
@@ -136,7 +146,9 @@ struct Cv {
     }
 
     // GPS update with H = [I 0] (kf_workers.py:551-558, 616-621, 708-711; Joseph form).
-    // Returns false when S is not positive definite.
+    // R is packed upper (m x m); DIAG_R skips its zero off-diagonal terms.
+    // Returns false when S is not positive definite (x and P are then NaN).
+    template <bool DIAG_R>
     __device__ static __forceinline__ bool update(T (&x)[N], T (&P)[NT], const T (&z)[M],
                                                   const T (&R)[MT]) {
         // LDL^T of S = H P H^T + R
@@ -151,16 +163,17 @@ struct Cv {
 #pragma unroll
             for (int k = 0; k < j; ++k) {
                 v[k] = L[j][k] * d[k];
-                dj = __builtin_fma(-L[j][k], v[k], dj);
+                dj = fmaT(-L[j][k], v[k], dj);
             }
             ok = ok && (dj > T(0));
             d[j] = dj;
-            dinv[j] = rcp(dj);
+            dinv[j] = rcp_pos<2>(dj);
 #pragma unroll
             for (int i = j + 1; i < M; ++i) {
-                T s = P[tri<N>(i, j)] + R[tri<M>(i, j)];
+                T s = P[tri<N>(i, j)];
+                if (!DIAG_R) s += R[tri<M>(i, j)];
 #pragma unroll
-                for (int k = 0; k < j; ++k) s = __builtin_fma(-L[i][k], v[k], s);
+                for (int k = 0; k < j; ++k) s = fmaT(-L[i][k], v[k], s);
                 L[i][j] = s * dinv[j];
             }
         }
@@ -173,14 +186,14 @@ struct Cv {
             for (int a = 0; a < M; ++a) {
                 T s = P[tri<N>(i, a)];
 #pragma unroll
-                for (int b = 0; b < a; ++b) s = __builtin_fma(-L[a][b], w[b], s);
+                for (int b = 0; b < a; ++b) s = fmaT(-L[a][b], w[b], s);
                 w[a] = s;
             }
 #pragma unroll
             for (int a = M - 1; a >= 0; --a) {
                 T s = w[a] * dinv[a];
 #pragma unroll
-                for (int b = a + 1; b < M; ++b) s = __builtin_fma(-L[b][a], K[i][b], s);
+                for (int b = a + 1; b < M; ++b) s = fmaT(-L[b][a], K[i][b], s);
                 K[i][a] = s;
             }
         }
@@ -192,7 +205,7 @@ struct Cv {
         for (int i = 0; i < N; ++i) {
             T s = x[i];
 #pragma unroll
-            for (int a = 0; a < M; ++a) s = __builtin_fma(K[i][a], y[a], s);
+            for (int a = 0; a < M; ++a) s = fmaT(K[i][a], y[a], s);
             x[i] = s;
         }
         // Joseph: E = K R - (I - K H) P H^T   (n x m)
@@ -202,11 +215,15 @@ struct Cv {
 #pragma unroll
             for (int a = 0; a < M; ++a) {
                 T yia = P[tri<N>(i, a)];
-                T kr = T(0);
 #pragma unroll
-                for (int b = 0; b < M; ++b) {
-                    yia = __builtin_fma(-K[i][b], P[tri<N>(b, a)], yia);
-                    kr = __builtin_fma(K[i][b], R[tri<M>(b, a)], kr);
+                for (int b = 0; b < M; ++b) yia = fmaT(-K[i][b], P[tri<N>(b, a)], yia);
+                T kr;
+                if (DIAG_R) {
+                    kr = K[i][a] * R[tri<M>(a, a)];
+                } else {
+                    kr = T(0);
+#pragma unroll
+                    for (int b = 0; b < M; ++b) kr = fmaT(K[i][b], R[tri<M>(b, a)], kr);
                 }
                 E[i][a] = kr - yia;
             }
@@ -220,9 +237,9 @@ struct Cv {
             for (int j = i; j < N; ++j) {
                 T s = P[tri<N>(i, j)];
 #pragma unroll
-                for (int b = 0; b < M; ++b) s = __builtin_fma(-K[i][b], P[tri<N>(b, j)], s);
+                for (int b = 0; b < M; ++b) s = fmaT(-K[i][b], P[tri<N>(b, j)], s);
 #pragma unroll
-                for (int a = 0; a < M; ++a) s = __builtin_fma(E[i][a], K[j][a], s);
+                for (int a = 0; a < M; ++a) s = fmaT(E[i][a], K[j][a], s);
                 if (i < M)
                     top[i][j] = s;
                 else
@@ -236,118 +253,191 @@ struct Cv {
     }
 };
 
+// Addressing: every access goes through a raw buffer descriptor built from wave-uniform
+// scalars — the base of one [B]-long row (component i of step t) and the row's byte length —
+// plus the lane's 32-bit byte offset (buffer_load ... offen).  No 64-bit address lives in
+// VGPRs, and the hardware range check turns an out-of-row access into a dropped store /
+// zero load instead of a fault.  B * sizeof(T) < 2^31 is enforced by kf_alloc.
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, int64_t r, uint32_t row_bytes) {
+    const char* p = reinterpret_cast<const char*>(base) + r * int64_t(row_bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(p), 0, row_bytes, 0x00020000);
+}
+
 template <typename T>
-__device__ __forceinline__ T ldg(const void* p, int64_t idx) {
-    return reinterpret_cast<const T*>(p)[idx];
+__device__ __forceinline__ T ldb(const void* base, int64_t r, uint32_t row_bytes, uint32_t off);
+template <>
+__device__ __forceinline__ double ldb<double>(const void* base, int64_t r, uint32_t row_bytes, uint32_t off) {
+    return __builtin_bit_cast(double, (v2u)__builtin_amdgcn_raw_buffer_load_b64(row_rsrc(base, r, row_bytes), off, 0, 0));
 }
-template <typename T>
-__device__ __forceinline__ void stg(void* p, int64_t idx, T v) {
-    reinterpret_cast<T*>(p)[idx] = v;
+template <>
+__device__ __forceinline__ float ldb<float>(const void* base, int64_t r, uint32_t row_bytes, uint32_t off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base, r, row_bytes), off, 0, 0));
 }
-
-template <int D, typename T>
-__device__ __forceinline__ void load_state(const CvArgs& a, int64_t f, T (&x)[2 * D],
-                                           T (&P)[Cv<D, T>::NT]) {
-#pragma unroll
-    for (int i = 0; i < 2 * D; ++i) x[i] = ldg<T>(a.x, i * a.B + f);
-#pragma unroll
-    for (int k = 0; k < Cv<D, T>::NT; ++k) P[k] = ldg<T>(a.P, k * a.B + f);
+__device__ __forceinline__ void stb(void* base, int64_t r, uint32_t row_bytes, uint32_t off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), row_rsrc(base, r, row_bytes), off, 0, 0);
 }
-
-template <int D, typename T>
-__device__ __forceinline__ void store_state(const CvArgs& a, int64_t f, const T (&x)[2 * D],
-                                            const T (&P)[Cv<D, T>::NT]) {
-#pragma unroll
-    for (int i = 0; i < 2 * D; ++i) stg<T>(a.x, i * a.B + f, x[i]);
-#pragma unroll
-    for (int k = 0; k < Cv<D, T>::NT; ++k) stg<T>(a.P, k * a.B + f, P[k]);
+__device__ __forceinline__ void stb(void* base, int64_t r, uint32_t row_bytes, uint32_t off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), row_rsrc(base, r, row_bytes), off, 0, 0);
 }
 
 template <int D, typename T>
-__device__ __forceinline__ void fill_nan(T (&x)[2 * D], T (&P)[D * (2 * D + 1)]) {
+__device__ __forceinline__ void load_state(const CvArgs& a, uint32_t rb, uint32_t off, T (&x)[2 * D],
+                                           T (&P)[D * (2 * D + 1)]) {
 #pragma unroll
-    for (int i = 0; i < 2 * D; ++i) x[i] = quiet_nan<T>();
+    for (int i = 0; i < 2 * D; ++i) x[i] = ldb<T>(a.x, i, rb, off);
 #pragma unroll
-    for (int k = 0; k < Cv<D, T>::NT; ++k) P[k] = quiet_nan<T>();
+    for (int k = 0; k < D * (2 * D + 1); ++k) P[k] = ldb<T>(a.P, k, rb, off);
 }
+
+template <int D, typename T>
+__device__ __forceinline__ void store_state(const CvArgs& a, uint32_t rb, uint32_t off, const T (&x)[2 * D],
+                                            const T (&P)[D * (2 * D + 1)]) {
+#pragma unroll
+    for (int i = 0; i < 2 * D; ++i) stb(a.x, i, rb, off, x[i]);
+#pragma unroll
+    for (int k = 0; k < D * (2 * D + 1); ++k) stb(a.P, k, rb, off, P[k]);
+}
+
+template <int D, typename T>
+__device__ __forceinline__ void load_R(const CvArgs& a, T (&R)[D * (D + 1) / 2]) {
+#pragma unroll
+    for (int k = 0; k < D * (D + 1) / 2; ++k) R[k] = T(a.r[k]);
+}
+
+// Inputs of one time step, double-buffered in registers by the run kernel.
+template <int D, typename T>
+struct StepIn {
+    T u[D];
+    T z[D];
+    uint8_t use;
+};
 
 // ------------------------------------------------------------------------------------
 // The fused hot path: T predict(+update) steps in one launch.
-// ------------------------------------------------------------------------------------
-// GENERAL = false: the bench / fusion configuration (scalar dt, control present, no mask,
-// trajectory and logdet written) with no runtime checks; GENERAL = true: every optional
+// GENERAL = false: scalar dt, control present, no mask, trajectory and logdet written (the
+// bench / fusion configuration) with no runtime checks; GENERAL = true: every optional
 // stream decided at run time by a wave-uniform branch.
-template <int D, typename T, bool GENERAL>
-__global__ __launch_bounds__(kBlock) void cv_run_kernel(const CvArgs a) {
+// The time loop is unrolled by two with statically named input buffers A and B: step t+1's
+// inputs are loaded before step t computes, and no loop-carried register copy forces the
+// wave to wait for its own trajectory stores (s_waitcnt counts loads and stores together).
+// Every step loads the z of the next update (clamped), so between GPS updates the same
+// line is re-read from L2 instead of a branch being taken around the load.
+// ------------------------------------------------------------------------------------
+// Minimum waves per SIMD requested from the register allocator for the run kernel (1 = let
+// the compiler choose).  Overridable at build time for occupancy experiments.
+#ifndef KF_OCC_CV3_F64
+#define KF_OCC_CV3_F64 1
+#endif
+#ifndef KF_OCC_CV3_F32
+#define KF_OCC_CV3_F32 1
+#endif
+#ifndef KF_OCC_CV2_F64
+#define KF_OCC_CV2_F64 1
+#endif
+#ifndef KF_OCC_CV2_F32
+#define KF_OCC_CV2_F32 1
+#endif
+template <int D, typename T>
+struct RunOcc {
+    static constexpr int value = D == 3 ? (sizeof(T) == 8 ? KF_OCC_CV3_F64 : KF_OCC_CV3_F32)
+                                        : (sizeof(T) == 8 ? KF_OCC_CV2_F64 : KF_OCC_CV2_F32);
+};
+
+template <int D, typename T, bool GENERAL, bool DIAG_R>
+__global__ __launch_bounds__(kBlock, (RunOcc<D, T>::value)) void cv_run_kernel(const CvArgs a) {
     using K = Cv<D, T>;
     constexpr int N = K::N, M = K::M;
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
     const int64_t B = a.B;
-    const bool HAS_DTS = GENERAL && a.dt_steps != nullptr;
-    const bool HAS_U = !GENERAL || a.u != nullptr;
-    const bool HAS_MASK = GENERAL && a.mask != nullptr;
-    const bool TRAJ = !GENERAL || a.traj != nullptr;
-    const bool LOGDET = !GENERAL || a.logdet != nullptr;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
+    const bool has_dts = GENERAL && a.dt_steps != nullptr;
+    const bool has_u = !GENERAL || a.u != nullptr;
+    const bool has_mask = GENERAL && a.mask != nullptr;
+    const bool has_traj = !GENERAL || a.traj != nullptr;
+    const bool has_ld = !GENERAL || a.logdet != nullptr;
 
     T x[N], P[K::NT];
-    load_state<D, T>(a, f, x, P);
+    load_state<D, T>(a, rb, off, x, P);
     int32_t st = a.status[f];
     T R[K::MT];
-#pragma unroll
-    for (int k = 0; k < K::MT; ++k) R[k] = T(a.r[k]);
+    load_R<D, T>(a, R);
 
+    const int T_ = a.T;
     const int k_upd = a.update_every;
-    const int U = a.T / k_upd;
-    // Software pipeline: the control of step t+1 and the fix of the next update are loaded
-    // before step t computes, so their HBM latency hides under a full step of VALU work.
-    T u_nxt[D], z_nxt[M];
+    const int U = T_ / k_upd;
+
+    // z index for the inputs of step t: the update at or after t (ceil((t+1)/k) - 1),
+    // tracked incrementally (load_in is called with t = 0, 1, 2, ...), clamped to U - 1.
+    int ld_upd_step = k_upd - 1;
+    int ld_s = 0;
+    auto load_in = [&](int t, StepIn<D, T>& in) {
+        const int tc = t < T_ ? t : T_ - 1;
+        if (tc > ld_upd_step) {
+            ld_upd_step += k_upd;
+            ++ld_s;
+        }
+        if (has_u) {
 #pragma unroll
-    for (int i = 0; i < D; ++i) u_nxt[i] = (HAS_U && a.T > 0) ? ldg<T>(a.u, i * B + f) : T(0);
+            for (int i = 0; i < D; ++i) in.u[i] = ldb<T>(a.u, int64_t(tc) * D + i, rb, off);
+        } else {
 #pragma unroll
-    for (int i = 0; i < M; ++i) z_nxt[i] = U > 0 ? ldg<T>(a.z, i * B + f) : T(0);
-    int s = 0;         // index of the next update
+            for (int i = 0; i < D; ++i) in.u[i] = T(0);
+        }
+        const int s = ld_s < U ? ld_s : U - 1;
+        if (U > 0) {
+#pragma unroll
+            for (int i = 0; i < M; ++i) in.z[i] = ldb<T>(a.z, int64_t(s) * M + i, rb, off);
+        } else {
+#pragma unroll
+            for (int i = 0; i < M; ++i) in.z[i] = T(0);
+        }
+        in.use = (has_mask && U > 0) ? a.mask[int64_t(s) * B + f] : uint8_t(1);
+    };
+
     int until_upd = k_upd;
-
-    for (int t = 0; t < a.T; ++t) {
-        T u[D];
-#pragma unroll
-        for (int i = 0; i < D; ++i) u[i] = u_nxt[i];
-        if (HAS_U) {
-            const int tn = t + 1 < a.T ? t + 1 : t;
-#pragma unroll
-            for (int i = 0; i < D; ++i) u_nxt[i] = ldg<T>(a.u, (int64_t(tn) * D + i) * B + f);
-        }
-        const double dtd = HAS_DTS ? a.dt_steps[t] : a.dt;
-        const T dt = T(dtd);
-        K::predict(x, P, dt, u, T(a.q_pos * dtd), T(a.q_vel * dtd));
-
-        if (--until_upd == 0) {
+    auto step = [&](int t, const StepIn<D, T>& in) {
+        const double dtd = has_dts ? a.dt_steps[t] : a.dt;
+        K::predict(x, P, T(dtd), in.u, T(a.q_pos * dtd), T(a.q_vel * dtd));
+        if (--until_upd == 0) {  // wave-uniform
             until_upd = k_upd;
-            T z[M];
-#pragma unroll
-            for (int i = 0; i < M; ++i) z[i] = z_nxt[i];
-            const bool use = !HAS_MASK || a.mask[int64_t(s) * B + f] != 0;
-            const int sn = s + 1 < U ? s + 1 : s;
-#pragma unroll
-            for (int i = 0; i < M; ++i) z_nxt[i] = ldg<T>(a.z, (int64_t(sn) * M + i) * B + f);
-            if (use && !K::update(x, P, z, R)) {
-                st = kNotSpd;
-                fill_nan<D, T>(x, P);
+            if (!has_mask) {
+                const bool ok = K::template update<DIAG_R>(x, P, in.z, R);
+                st = ok ? st : kNotSpd;
+            } else if (in.use) {
+                const bool ok = K::template update<DIAG_R>(x, P, in.z, R);
+                st = ok ? st : kNotSpd;
             }
-            ++s;
         }
-        if (TRAJ) {
+        if (has_traj) {
 #pragma unroll
-            for (int i = 0; i < N; ++i) stg<T>(a.traj, (int64_t(t) * N + i) * B + f, x[i]);
+            for (int i = 0; i < N; ++i) stb(a.traj, int64_t(t) * N + i, rb, off, x[i]);
         }
-        if (LOGDET) {
+        if (has_ld) {
             const T ld = logdet_ldl<N, T>(P);
-            if (!(ld == ld)) st = kNotSpd;
-            stg<T>(a.logdet, int64_t(t) * B + f, ld);
+            st = (ld == ld) ? st : kNotSpd;
+            stb(a.logdet, t, rb, off, ld);
         }
+    };
+
+    StepIn<D, T> A, Bf;
+    load_in(0, A);
+    // Drain the prologue loads (state + first inputs) once, so the compiler's wait analysis
+    // does not carry them into the loop header and stall every iteration on them.
+    __builtin_amdgcn_s_waitcnt(0);
+    int t = 0;
+    for (; t + 1 < T_; t += 2) {
+        load_in(t + 1, Bf);
+        step(t, A);
+        load_in(t + 2, A);
+        step(t + 1, Bf);
     }
-    store_state<D, T>(a, f, x, P);
+    if (t < T_) step(t, A);
+
+    store_state<D, T>(a, rb, off, x, P);
     a.status[f] = st;
 }
 
@@ -357,17 +447,19 @@ __global__ __launch_bounds__(kBlock) void cv_predict_kernel(const CvArgs a) {
     using K = Cv<D, T>;
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
     T x[K::N], P[K::NT];
-    load_state<D, T>(a, f, x, P);
+    load_state<D, T>(a, rb, off, x, P);
     T u[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) u[i] = a.u ? ldg<T>(a.u, i * a.B + f) : T(0);
+    for (int i = 0; i < D; ++i) u[i] = a.u ? ldb<T>(a.u, i, rb, off) : T(0);
     const double dtd = a.dt_filter ? a.dt_filter[f] : a.dt;
     K::predict(x, P, T(dtd), u, T(a.q_pos * dtd), T(a.q_vel * dtd));
-    store_state<D, T>(a, f, x, P);
+    store_state<D, T>(a, rb, off, x, P);
     if (a.logdet) {
         const T ld = logdet_ldl<K::N, T>(P);
-        stg<T>(a.logdet, f, ld);
+        stb(a.logdet, 0, rb, off, ld);
         if (!(ld == ld)) a.status[f] = kNotSpd;
     }
 }
@@ -378,26 +470,24 @@ __global__ __launch_bounds__(kBlock) void cv_update_kernel(const CvArgs a) {
     using K = Cv<D, T>;
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
     T x[K::N], P[K::NT];
-    load_state<D, T>(a, f, x, P);
+    load_state<D, T>(a, rb, off, x, P);
     T R[K::MT];
-#pragma unroll
-    for (int k = 0; k < K::MT; ++k) R[k] = T(a.r[k]);
+    load_R<D, T>(a, R);
     T z[K::M];
 #pragma unroll
-    for (int i = 0; i < K::M; ++i) z[i] = ldg<T>(a.z, i * a.B + f);
+    for (int i = 0; i < K::M; ++i) z[i] = ldb<T>(a.z, i, rb, off);
     int32_t st = a.status[f];
     if (!a.mask || a.mask[f] != 0) {
-        if (!K::update(x, P, z, R)) {
-            st = kNotSpd;
-            fill_nan<D, T>(x, P);
-        }
+        if (!K::template update<false>(x, P, z, R)) st = kNotSpd;
     }
-    store_state<D, T>(a, f, x, P);
+    store_state<D, T>(a, rb, off, x, P);
     if (a.logdet) {
         const T ld = logdet_ldl<K::N, T>(P);
         if (!(ld == ld)) st = kNotSpd;
-        stg<T>(a.logdet, f, ld);
+        stb(a.logdet, 0, rb, off, ld);
     }
     a.status[f] = st;
 }
@@ -408,9 +498,11 @@ __global__ __launch_bounds__(kBlock) void cv_reset_kernel(const CvArgs a) {
     using K = Cv<D, T>;
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
     T x[K::N], P[K::NT];
 #pragma unroll
-    for (int i = 0; i < K::N; ++i) x[i] = a.x0 ? ldg<T>(a.x0, i * a.B + f) : T(0);
+    for (int i = 0; i < K::N; ++i) x[i] = a.x0 ? ldb<T>(a.x0, i, rb, off) : T(0);
 #pragma unroll
     for (int k = 0; k < K::NT; ++k) P[k] = T(0);
 #pragma unroll
@@ -418,7 +510,7 @@ __global__ __launch_bounds__(kBlock) void cv_reset_kernel(const CvArgs a) {
         P[tri<K::N>(i, i)] = T(a.p0_pos);
         P[tri<K::N>(D + i, D + i)] = T(a.p0_vel);
     }
-    store_state<D, T>(a, f, x, P);
+    store_state<D, T>(a, rb, off, x, P);
     a.status[f] = 0;
 }
 
@@ -448,12 +540,15 @@ __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
     return U4{{c0, c1, c2, c3}};
 }
 
+__device__ __forceinline__ double u53(uint32_t hi, uint32_t lo) {
+    const uint64_t a = (uint64_t(hi) << 21) ^ (lo >> 11);
+    return (double(a & ((1ull << 53) - 1)) + 0.5) * 0x1.0p-53;  // (0, 1)
+}
+
 // Two independent N(0,1) from one Philox block (53-bit uniforms, Box-Muller).
 __device__ __forceinline__ void normal2(const U4& r, double& n0, double& n1) {
-    const uint64_t a = (uint64_t(r.v[0]) << 21) ^ (r.v[1] >> 11);
-    const uint64_t b = (uint64_t(r.v[2]) << 21) ^ (r.v[3] >> 11);
-    const double u1 = (double(a & ((1ull << 53) - 1)) + 0.5) * 0x1.0p-53;
-    const double u2 = (double(b & ((1ull << 53) - 1)) + 0.5) * 0x1.0p-53;
+    const double u1 = u53(r.v[0], r.v[1]);
+    const double u2 = u53(r.v[2], r.v[3]);
     const double rad = sqrt(-2.0 * log(u1));
     double sn, cs;
     sincos(6.283185307179586476925 * u2, &sn, &cs);
@@ -461,15 +556,12 @@ __device__ __forceinline__ void normal2(const U4& r, double& n0, double& n1) {
     n1 = rad * sn;
 }
 
-__device__ __forceinline__ double uniform01(const U4& r) {
-    const uint64_t a = (uint64_t(r.v[0]) << 21) ^ (r.v[1] >> 11);
-    return (double(a & ((1ull << 53) - 1)) + 0.5) * 0x1.0p-53;
-}
-
 template <int D, typename T>
 __global__ __launch_bounds__(kBlock) void cv_synth_kernel(const SynthArgs a) {
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
     const uint64_t g = uint64_t(a.filter_offset + f);
     const uint32_t g0 = uint32_t(g), g1 = uint32_t(g >> 32);
     const uint32_t k0 = uint32_t(a.seed), k1 = uint32_t(a.seed >> 32);
@@ -479,13 +571,13 @@ __global__ __launch_bounds__(kBlock) void cv_synth_kernel(const SynthArgs a) {
 #pragma unroll
     for (int i = 0; i < D; ++i) {
         const U4 ru = philox4x32_10(0xFFFFFFFFu, uint32_t(i), g0, g1, k0, k1);
-        p[i] = -1000.0 + 2000.0 * uniform01(ru);
+        p[i] = -1000.0 + 2000.0 * u53(ru.v[0], ru.v[1]);
         const U4 rn = philox4x32_10(0xFFFFFFFFu, uint32_t(8 + i), g0, g1, k0, k1);
         double n0, n1;
         normal2(rn, n0, n1);
         v[i] = 10.0 * n0;
-        stg<T>(a.x0, i * a.B + f, T(p[i] + sd_gps * n1));  // position = first GPS fix
-        stg<T>(a.x0, (D + i) * a.B + f, T(0));               // other states 0 (kf_workers.py:655-659)
+        stb(a.x0, i, rb, off, T(p[i] + sd_gps * n1));  // position = first GPS fix
+        stb(a.x0, D + i, rb, off, T(0));               // other states 0 (kf_workers.py:655-659)
     }
     int until = a.update_every;
     int s = 0;
@@ -503,7 +595,7 @@ __global__ __launch_bounds__(kBlock) void cv_synth_kernel(const SynthArgs a) {
             const double imu = 0.1 * n[2 * i + 1];
             p[i] += v[i] * dt + 0.5 * acc * dt * dt;
             v[i] += acc * dt;
-            stg<T>(a.u, (int64_t(t) * D + i) * a.B + f, T(acc + imu));
+            stb(a.u, int64_t(t) * D + i, rb, off, T(acc + imu));
         }
         if (--until == 0) {
             until = a.update_every;
@@ -514,7 +606,7 @@ __global__ __launch_bounds__(kBlock) void cv_synth_kernel(const SynthArgs a) {
             }
 #pragma unroll
             for (int i = 0; i < D; ++i)
-                stg<T>(a.z, (int64_t(s) * D + i) * a.B + f, T(p[i] + sd_gps * n[2 * D + i]));
+                stb(a.z, int64_t(s) * D + i, rb, off, T(p[i] + sd_gps * n[2 * D + i]));
             ++s;
         }
     }
@@ -524,10 +616,21 @@ template <int D, typename T>
 hipError_t launch_run(const CvArgs& a, dim3 grid, hipStream_t st) {
     const bool fast = a.dt_steps == nullptr && a.u != nullptr && a.mask == nullptr &&
                       a.traj != nullptr && a.logdet != nullptr;
-    if (fast)
-        cv_run_kernel<D, T, false><<<grid, kBlock, 0, st>>>(a);
+    bool diag = true;
+    {
+        int k = 0;
+        for (int i = 0; i < D; ++i)
+            for (int j = i; j < D; ++j, ++k)
+                if (i != j && a.r[k] != 0.0) diag = false;
+    }
+    if (fast && diag)
+        cv_run_kernel<D, T, false, true><<<grid, kBlock, 0, st>>>(a);
+    else if (fast)
+        cv_run_kernel<D, T, false, false><<<grid, kBlock, 0, st>>>(a);
+    else if (diag)
+        cv_run_kernel<D, T, true, true><<<grid, kBlock, 0, st>>>(a);
     else
-        cv_run_kernel<D, T, true><<<grid, kBlock, 0, st>>>(a);
+        cv_run_kernel<D, T, true, false><<<grid, kBlock, 0, st>>>(a);
     return hipGetLastError();
 }
 

@@ -10,7 +10,8 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libkfmi.so')
+# KFMI_LIB selects an alternative build (e.g. an occupancy variant); relative to the cwd.
+LIB_PATH = os.path.abspath(os.environ.get('KFMI_LIB') or os.path.join(HERE, 'libkfmi.so'))
 HEADER = os.path.normpath(os.path.join(HERE, '..', '..', 'include', 'kf.h'))
 
 KF_OK = 0
