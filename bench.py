@@ -65,7 +65,7 @@ def cpu_baseline(cfg, x0, u, z, budget_s=12.0):
     model = ref_kf.CV2 if cfg['model'] == 'cv2' else ref_kf.CV3
     T, k = cfg['T'], cfg['k']
     dt = np.full(T, cfg['dt'])
-    nf = 64
+    nf = min(4096, cfg['B'])
     idx = torch.linspace(0, cfg['B'] - 1, nf).long().to(u.device)
     xs = x0[:, idx].double().cpu().numpy().T
     us = u[:, :, idx].double().cpu().numpy()
@@ -101,11 +101,13 @@ def load_traffic(cfg_id, n_gpus):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=10)
-    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--config', type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument('--batch', type=int, default=None, help='override filters per GPU')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--ablate', choices=['none', 'no-traj', 'no-logdet', 'no-traj-no-logdet'], default='none',
+                    help='diagnostics only: skip an output stream (the JSON line says so)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -126,16 +128,22 @@ def main():
     B, T, k, dt = cfg['B'], cfg['T'], cfg['k'], cfg['dt']
     dev = torch.device('cuda', local)
 
+    from kfmi import dist as kdist
     kf = kfmi.BatchedKF(cfg['model'], B, cfg['dtype'], device=local)
-    # shard r owns global filters [r*B, (r+1)*B) and regenerates its own streams
-    x0, u, z = kf.synth(T=T, dt=dt, update_every=k, seed=SEED, filter_offset=rank * B)
+    # weak scaling: world*B filters in total; shard r owns a contiguous slice and regenerates
+    # its own streams from the counter-based generator (keyed by the global filter index)
+    offset, count = kdist.shard_range(world * B, rank, world)
+    assert count == B
+    x0, u, z = kf.synth(T=T, dt=dt, update_every=k, seed=SEED, filter_offset=offset)
     kf.reset(x0)
     traj = kf.empty(T, kf.n, B)
     logdet = kf.empty(T, B)
     stream = torch.cuda.current_stream(dev)
 
+    out = (None if 'no-traj' in args.ablate else traj, None if 'no-logdet' in args.ablate else logdet)
+
     def step():
-        kf.run(u, z, dt=dt, update_every=k, out=(traj, logdet))
+        kf.run(u, z, dt=dt, update_every=k, out=out)
 
     for _ in range(args.warmup):
         step()
@@ -159,18 +167,18 @@ def main():
     bad = int((kf.status() != 0).sum().item())
     gather_ms = None
     if dist:
-        t = torch.tensor([elapsed, kern_ms, float(bad)], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms, bad = float(t[0]), float(t[1]), int(t[2])
-        # reassemble the final states + logdets of every shard on every rank (RCCL over xGMI)
+        elapsed, kern_ms, bad = kdist.max_over_ranks([elapsed, kern_ms, bad], dev)
+        bad = int(bad)
+        # reassemble the final states + logdets of every shard on every rank (RCCL over xGMI);
+        # timed separately from the steps: it is a once-per-job reassembly, not the hot path
         xf, _ = kf.state()
         local_out = torch.cat([xf, logdet[-1:]], dim=0).contiguous()
-        gathered = torch.empty((world,) + tuple(local_out.shape), dtype=local_out.dtype, device=dev)
         torch.cuda.synchronize(dev)
         dist.barrier()
         g0 = time.perf_counter()
-        dist.all_gather_into_tensor(gathered, local_out)
+        gathered = kdist.gather_shards(local_out, world * B)
         torch.cuda.synchronize(dev)
+        assert gathered.shape == (kf.n + 1, world * B)
         gather_ms = (time.perf_counter() - g0) * 1e3
 
     if rank == 0:
@@ -207,6 +215,8 @@ def main():
                          'algorithmic_bytes_per_step': bytes_step},
             'failed_filters': bad,
         }
+        if args.ablate != 'none':
+            rec['ablation'] = args.ablate + ' (diagnostic run: NOT the benchmark workload)'
         if gather_ms is not None:
             rec['allgather_ms'] = gather_ms
         if world == 1 and not args.no_cpu_baseline:

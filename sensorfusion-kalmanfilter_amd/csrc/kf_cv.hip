@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "kf_internal.h"
 
@@ -46,23 +47,56 @@ __device__ __forceinline__ double quiet_nan<double>() { return __builtin_nan("")
 template <>
 __device__ __forceinline__ float quiet_nan<float>() { return __builtin_nanf(""); }
 
-// 1/d refined by Newton steps (v_rcp_* is an approximation); NaN when !(d > 0).
+// 1/d: the hardware approximation (v_rcp_f64 / v_rcp_f32) refined by NEWTON Newton steps.
 template <int NEWTON>
-__device__ __forceinline__ double rcp_pos(double d) {
+__device__ __forceinline__ double rcp_nr(double d) {
     double r = __builtin_amdgcn_rcp(d);
 #pragma unroll
     for (int i = 0; i < NEWTON; ++i) r = fmaT(r, fmaT(-d, r, 1.0), r);
-    return d > 0.0 ? r : quiet_nan<double>();
+    return r;
 }
 template <int NEWTON>
-__device__ __forceinline__ float rcp_pos(float d) {
+__device__ __forceinline__ float rcp_nr(float d) {
     float r = __builtin_amdgcn_rcpf(d);
-    r = fmaT(r, fmaT(-d, r, 1.0f), r);
-    return d > 0.0f ? r : quiet_nan<float>();
+#pragma unroll
+    for (int i = 0; i < NEWTON; ++i) r = fmaT(r, fmaT(-d, r, 1.0f), r);
+    return r;
+}
+// Same, but NaN unless d > 0: a non-positive pivot of S poisons everything derived from it.
+template <int NEWTON, typename T>
+__device__ __forceinline__ T rcp_pos(T d) {
+    const T r = rcp_nr<NEWTON>(d);
+    return d > T(0) ? r : quiet_nan<T>();
 }
 
-__device__ __forceinline__ double log_pos(double v) { return log(v); }
-__device__ __forceinline__ float log_pos(float v) { return __logf(v); }
+// log(m) + e ln 2 for a mantissa m in [0.5, 1) (the frexp-normalised pivot product).
+// fp64: reduce to m' in [sqrt(1/2), sqrt(2)), then log m' = 2 atanh(s), s = (m'-1)/(m'+1),
+// |s| < 0.1716, summed to s^21 (truncation < 1e-17) — ~25 VALU ops instead of the ~100 of
+// the general double-double log().  fp32: the hardware log (v_log_f32).
+__device__ __forceinline__ double log_mant(double m, int e) {
+    const bool lo = m < 0.70710678118654752440;
+    m = lo ? m + m : m;
+    e = lo ? e - 1 : e;
+    const double f = m - 1.0;
+    const double s = f * rcp_nr<2>(2.0 + f);
+    const double s2 = s * s;
+    double p = 1.0 / 21;
+    p = fmaT(p, s2, 1.0 / 19);
+    p = fmaT(p, s2, 1.0 / 17);
+    p = fmaT(p, s2, 1.0 / 15);
+    p = fmaT(p, s2, 1.0 / 13);
+    p = fmaT(p, s2, 1.0 / 11);
+    p = fmaT(p, s2, 1.0 / 9);
+    p = fmaT(p, s2, 1.0 / 7);
+    p = fmaT(p, s2, 1.0 / 5);
+    p = fmaT(p, s2, 1.0 / 3);
+    const double two_s = s + s;
+    const double lm = fmaT(two_s * s2, p, two_s);
+    return fmaT(double(e), 0.69314718055994530942, lm);
+}
+__device__ __forceinline__ float log_mant(float m, int e) {
+    return fmaT(float(e), 0.69314718055994530942f, __logf(m));
+}
 
 // log det of an SPD N x N matrix (packed upper) via LDL^T: log of the pivot product, with
 // the product renormalised by its binary exponent every 3 pivots so fp32 cannot overflow.
@@ -92,7 +126,7 @@ __device__ __forceinline__ T logdet_ldl(const T (&P)[N * (N + 1) / 2]) {
             ex += e;
         }
         if (j + 1 < N) {
-            const T dinv = rcp_pos<1>(dj);
+            const T dinv = rcp_nr<1>(dj);  // a bad pivot already makes `ok` false
 #pragma unroll
             for (int i = j + 1; i < N; ++i) {
                 T s = P[tri<N>(i, j)];
@@ -102,7 +136,7 @@ __device__ __forceinline__ T logdet_ldl(const T (&P)[N * (N + 1) / 2]) {
             }
         }
     }
-    const T ld = log_pos(prod) + T(ex) * T(0.69314718055994530942);
+    const T ld = log_mant(prod, ex);  // prod was frexp-normalised at the last pivot
     return ok ? ld : quiet_nan<T>();
 }
 
@@ -151,7 +185,13 @@ struct Cv {
     template <bool DIAG_R>
     __device__ static __forceinline__ bool update(T (&x)[N], T (&P)[NT], const T (&z)[M],
                                                   const T (&R)[MT]) {
-        // LDL^T of S = H P H^T + R
+        // S = H P H^T + R, then its LDL^T
+        T S[MT];
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+#pragma unroll
+            for (int j = i; j < M; ++j)
+                S[tri<M>(i, j)] = (i == j || !DIAG_R) ? P[tri<N>(i, j)] + R[tri<M>(i, j)] : P[tri<N>(i, j)];
         T L[M][M];
         T d[M];
         T dinv[M];
@@ -159,7 +199,7 @@ struct Cv {
 #pragma unroll
         for (int j = 0; j < M; ++j) {
             T v[M];
-            T dj = P[tri<N>(j, j)] + R[tri<M>(j, j)];
+            T dj = S[tri<M>(j, j)];
 #pragma unroll
             for (int k = 0; k < j; ++k) {
                 v[k] = L[j][k] * d[k];
@@ -170,8 +210,7 @@ struct Cv {
             dinv[j] = rcp_pos<2>(dj);
 #pragma unroll
             for (int i = j + 1; i < M; ++i) {
-                T s = P[tri<N>(i, j)];
-                if (!DIAG_R) s += R[tri<M>(i, j)];
+                T s = S[tri<M>(i, j)];
 #pragma unroll
                 for (int k = 0; k < j; ++k) s = fmaT(-L[i][k], v[k], s);
                 L[i][j] = s * dinv[j];
@@ -208,43 +247,36 @@ struct Cv {
             for (int a = 0; a < M; ++a) s = fmaT(K[i][a], y[a], s);
             x[i] = s;
         }
-        // Joseph: E = K R - (I - K H) P H^T   (n x m)
-        T E[N][M];
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-#pragma unroll
-            for (int a = 0; a < M; ++a) {
-                T yia = P[tri<N>(i, a)];
-#pragma unroll
-                for (int b = 0; b < M; ++b) yia = fmaT(-K[i][b], P[tri<N>(b, a)], yia);
-                T kr;
-                if (DIAG_R) {
-                    kr = K[i][a] * R[tri<M>(a, a)];
-                } else {
-                    kr = T(0);
-#pragma unroll
-                    for (int b = 0; b < M; ++b) kr = fmaT(K[i][b], R[tri<M>(b, a)], kr);
-                }
-                E[i][a] = kr - yia;
-            }
-        // P' = Y + E K^T with Y = (I - K H) P; upper triangle only.  Rows >= m are written in
-        // place (their old values are read only by themselves); rows < m are staged because
-        // every Y needs them.
+        // Joseph: P+ = (I-KH) P (I-KH)^T + K R K^T = (P - K G^T) + E K^T with G = P H^T and
+        // E = K S - G, an identity for ANY K (E is the residual of the gain equation K S = G,
+        // so an error dK in the gain enters P+ only as dK S dK^T).  Upper triangle only, row
+        // by row; row i's E is formed just before it is used so only m values of E are live.
+        // Rows >= m are written in place (their old values are read only by themselves); rows
+        // < m hold G and feed every row, so their new values are staged until the end.
         T top[M][N];
 #pragma unroll
-        for (int i = 0; i < N; ++i)
+        for (int i = 0; i < N; ++i) {
+            T E[M];
+#pragma unroll
+            for (int a = 0; a < M; ++a) {
+                T e = -P[tri<N>(i, a)];
+#pragma unroll
+                for (int b = 0; b < M; ++b) e = fmaT(K[i][b], S[tri<M>(b, a)], e);
+                E[a] = e;
+            }
 #pragma unroll
             for (int j = i; j < N; ++j) {
                 T s = P[tri<N>(i, j)];
 #pragma unroll
                 for (int b = 0; b < M; ++b) s = fmaT(-K[i][b], P[tri<N>(b, j)], s);
 #pragma unroll
-                for (int a = 0; a < M; ++a) s = fmaT(E[i][a], K[j][a], s);
+                for (int a = 0; a < M; ++a) s = fmaT(E[a], K[j][a], s);
                 if (i < M)
                     top[i][j] = s;
                 else
                     P[tri<N>(i, j)] = s;
             }
+        }
 #pragma unroll
         for (int i = 0; i < M; ++i)
 #pragma unroll
@@ -374,27 +406,23 @@ __global__ __launch_bounds__(kBlock, (RunOcc<D, T>::value)) void cv_run_kernel(c
     // tracked incrementally (load_in is called with t = 0, 1, 2, ...), clamped to U - 1.
     int ld_upd_step = k_upd - 1;
     int ld_s = 0;
+    // Optional streams cost no branch: a zero-length row descriptor makes the hardware range
+    // check return 0 for every load (no control / no update) without touching memory.
+    const uint32_t rb_u = has_u ? rb : 0u;
+    const uint32_t rb_z = U > 0 ? rb : 0u;
+    const uint32_t rb_tr = has_traj ? rb : 0u;  // no trajectory: stores dropped by the range check
     auto load_in = [&](int t, StepIn<D, T>& in) {
         const int tc = t < T_ ? t : T_ - 1;
         if (tc > ld_upd_step) {
             ld_upd_step += k_upd;
             ++ld_s;
         }
-        if (has_u) {
 #pragma unroll
-            for (int i = 0; i < D; ++i) in.u[i] = ldb<T>(a.u, int64_t(tc) * D + i, rb, off);
-        } else {
+        for (int i = 0; i < D; ++i) in.u[i] = ldb<T>(a.u, int64_t(tc) * D + i, rb_u, off);
+        int s = ld_s < U ? ld_s : U - 1;
+        s = s > 0 ? s : 0;
 #pragma unroll
-            for (int i = 0; i < D; ++i) in.u[i] = T(0);
-        }
-        const int s = ld_s < U ? ld_s : U - 1;
-        if (U > 0) {
-#pragma unroll
-            for (int i = 0; i < M; ++i) in.z[i] = ldb<T>(a.z, int64_t(s) * M + i, rb, off);
-        } else {
-#pragma unroll
-            for (int i = 0; i < M; ++i) in.z[i] = T(0);
-        }
+        for (int i = 0; i < M; ++i) in.z[i] = ldb<T>(a.z, int64_t(s) * M + i, rb_z, off);
         in.use = (has_mask && U > 0) ? a.mask[int64_t(s) * B + f] : uint8_t(1);
     };
 
@@ -412,10 +440,8 @@ __global__ __launch_bounds__(kBlock, (RunOcc<D, T>::value)) void cv_run_kernel(c
                 st = ok ? st : kNotSpd;
             }
         }
-        if (has_traj) {
 #pragma unroll
-            for (int i = 0; i < N; ++i) stb(a.traj, int64_t(t) * N + i, rb, off, x[i]);
-        }
+        for (int i = 0; i < N; ++i) stb(a.traj, int64_t(t) * N + i, rb_tr, off, x[i]);
         if (has_ld) {
             const T ld = logdet_ldl<N, T>(P);
             st = (ld == ld) ? st : kNotSpd;
@@ -612,8 +638,22 @@ __global__ __launch_bounds__(kBlock) void cv_synth_kernel(const SynthArgs a) {
     }
 }
 
+// Optional cap on resident workgroups per CU for the run kernel (experiments / tail tuning):
+// KFMI_BLOCKS_PER_CU=k reserves 160 KiB / (k + 0.5) of (unused) LDS per workgroup so at most
+// k workgroups (k waves per SIMD) fit on a CU.  Unset = no cap.
+size_t lds_cap_bytes() {
+    static const size_t bytes = [] {
+        const char* e = getenv("KFMI_BLOCKS_PER_CU");
+        const int k = e ? atoi(e) : 0;
+        if (k < 2 || k > 8) return size_t(0);
+        return (size_t(160 * 1024) * 2 / (2 * k + 1) + 15) / 16 * 16;
+    }();
+    return bytes;
+}
+
 template <int D, typename T>
 hipError_t launch_run(const CvArgs& a, dim3 grid, hipStream_t st) {
+    const size_t lds = lds_cap_bytes();
     const bool fast = a.dt_steps == nullptr && a.u != nullptr && a.mask == nullptr &&
                       a.traj != nullptr && a.logdet != nullptr;
     bool diag = true;
@@ -624,13 +664,13 @@ hipError_t launch_run(const CvArgs& a, dim3 grid, hipStream_t st) {
                 if (i != j && a.r[k] != 0.0) diag = false;
     }
     if (fast && diag)
-        cv_run_kernel<D, T, false, true><<<grid, kBlock, 0, st>>>(a);
+        cv_run_kernel<D, T, false, true><<<grid, kBlock, lds, st>>>(a);
     else if (fast)
-        cv_run_kernel<D, T, false, false><<<grid, kBlock, 0, st>>>(a);
+        cv_run_kernel<D, T, false, false><<<grid, kBlock, lds, st>>>(a);
     else if (diag)
-        cv_run_kernel<D, T, true, true><<<grid, kBlock, 0, st>>>(a);
+        cv_run_kernel<D, T, true, true><<<grid, kBlock, lds, st>>>(a);
     else
-        cv_run_kernel<D, T, true, false><<<grid, kBlock, 0, st>>>(a);
+        cv_run_kernel<D, T, true, false><<<grid, kBlock, lds, st>>>(a);
     return hipGetLastError();
 }
 

@@ -275,3 +275,34 @@ def test_full_size_config_sampled(dtype):
     # depend on the data in a linear KF): a checksum across the whole batch
     spread = (ld.max(dim=1).values - ld.min(dim=1).values).abs().max().item()
     assert spread <= (1e-9 if dtype == 'f64' else 1e-3)
+
+
+@pytest.mark.parametrize('dtype', ['f64', 'f32'])
+@pytest.mark.parametrize('name', ['cv2', 'cv3'])
+@pytest.mark.parametrize('wide', [False, True])
+def test_logdet_kernel_on_random_spd(dtype, name, wide):
+    """logdet from the in-lane LDL^T (+ reduced-range log) vs numpy slogdet on random SPD
+    covariances (predict with dt = 0 leaves P as is).  spread = log10 of the eigenvalue range:
+    0.3 isolates the log (strict bound); the wide case checks the factorisation at condition
+    number ~1e8 (fp64) / ~1e4 (fp32), where any two backward-stable methods may differ by
+    ~kappa * eps."""
+    spread = (8.0 if dtype == 'f64' else 4.0) if wide else 0.3
+    n = 4 if name == 'cv2' else 6
+    B = 4096
+    rng = np.random.default_rng(21)
+    Qm, _ = np.linalg.qr(rng.normal(size=(B, n, n)))
+    ev = 10.0 ** rng.uniform(-spread / 2, spread / 2, (B, n)) * 10.0 ** rng.uniform(-2, 3, (B, 1))
+    P = np.einsum('bij,bj,bkj->bik', Qm, ev, Qm)
+    P = 0.5 * (P + P.transpose(0, 2, 1))
+    Pt = ref_kf.tri_pack(P).astype(NP[dtype])
+    kf = kfmi.BatchedKF(name, B, dtype)
+    kf.set_state(torch.zeros(n, B, dtype=TD[dtype], device='cuda'), torch.from_numpy(Pt).cuda())
+    ld = kf.predict(0.0, logdet=True).double().cpu().numpy()
+    Pd = ref_kf.tri_unpack(Pt.astype(np.float64), n)
+    ref = np.linalg.slogdet(Pd)[1]
+    kappa = np.linalg.cond(Pd)
+    eps = np.finfo(NP[dtype]).eps
+    err = np.abs(ld - ref) / np.maximum(np.abs(ref), 1.0)
+    bound = np.maximum(50 * kappa * eps, 1e-13 if dtype == 'f64' else 2e-6)
+    assert (err <= bound).all(), float((err / bound).max())
+    assert (kf.status().cpu().numpy() == 0).all()

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Build libkfmi from git revision REV into sensorfusion-kalmanfilter_amd/kfmi/libkfmi_NAME.so
+# (for in-session A/B on the GPU box:  KFMI_LIB=sensorfusion-kalmanfilter_amd/kfmi/libkfmi_NAME.so).
+set -eu
+REV=$1; NAME=$2
+ROOT=$(git rev-parse --show-toplevel)
+TMP=$(mktemp -d)
+git -C "$ROOT" archive "$REV" sensorfusion-kalmanfilter_amd include | tar -x -C "$TMP"
+make -C "$TMP/sensorfusion-kalmanfilter_amd" -j8 OUT="$ROOT/sensorfusion-kalmanfilter_amd/kfmi/libkfmi_$NAME.so" >/dev/null
+rm -rf "$TMP"
+echo "built libkfmi_$NAME.so from $REV"

@@ -9,7 +9,7 @@ cd "$ROOT"
 for r in $(seq 1 "$ROUNDS"); do
   for lib in $LIBS; do
     for c in $CFGS; do
-      KFMI_LIB=$lib timeout -k 10 300 python bench.py --config "$c" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/tmp.json" 2> "$OUT/err_${c}.log"
+      KFMI_LIB=$lib timeout -k 10 300 python bench.py --config "$c" --steps 20 --warmup 10 --no-cpu-baseline > "$OUT/tmp.json" 2> "$OUT/err_${c}.log"
       rc=$?
       if [ $rc -ne 0 ]; then echo "lib=$lib cfg=$c rc=$rc"; tail -5 "$OUT/err_${c}.log"; exit $rc; fi
       python3 -c "import json,sys; d=json.load(open('$OUT/tmp.json')); print('round=$r lib=$lib cfg=$c', f\"value={d['value']:.4e} kern_ms={d['roofline']['kernel_ms']:.3f} GB/s={d['roofline']['achieved']:.0f} frac={d['roofline']['frac']:.3f} bad={d['failed_filters']}\")" | tee -a "$OUT/ab.txt"

@@ -1,0 +1,73 @@
+"""Reduce rocprofv3 PMC CSVs (tools/pmc_traffic.sh) to HBM bytes per cv_run_kernel launch.
+
+usage: python tools/pmc_traffic.py OUTDIR CFG [CFG ...]   -> writes OUTDIR/pmc_traffic.json
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE is only
+calibrated for 16 B/lane streams (reads half the bytes there); other widths must be calibrated
+on a known byte count in the same access pattern.  The probe's soa_read (T*6*B*8 bytes read,
+8 B per lane) and soa_write (T*7*B*8 bytes written) provide that calibration here.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def per_kernel(d, counter):
+    """kernel name substring -> list of per-dispatch counter values (KiB)."""
+    rows = {}
+    for f in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r.get('Counter_Name') != counter:
+                    continue
+                key = (r['Kernel_Name'], r.get('Dispatch_Id') or r.get('Correlation_Id'))
+                rows[key] = rows.get(key, 0.0) + float(r['Counter_Value'])
+    out = {}
+    for (name, _), v in rows.items():
+        out.setdefault(name, []).append(v)
+    return out
+
+
+def pick(d, sub):
+    vals = [v for k, v in d.items() if sub in k]
+    if not vals:
+        raise SystemExit(f'no kernel matching {sub!r} in {list(d)[:5]}')
+    return vals[0]
+
+
+def main():
+    out_dir, cfgs = sys.argv[1], [int(c) for c in sys.argv[2:]]
+    from bench import CONFIGS, algorithmic_bytes
+    B, T = 1048576, 64
+    known_read, known_write = T * 6 * B * 8, T * 7 * B * 8
+    pf = per_kernel(os.path.join(out_dir, 'probe_FETCH_SIZE'), 'FETCH_SIZE')
+    pw = per_kernel(os.path.join(out_dir, 'probe_WRITE_SIZE'), 'WRITE_SIZE')
+    rd = pick(pf, 'soa_read')
+    wr = pick(pw, 'soa_write')
+    read_scale = known_read / (1024 * sum(rd) / len(rd))
+    write_scale = known_write / (1024 * sum(wr) / len(wr))
+    res = {'calibration': {'fetch_size_scale': read_scale, 'write_size_scale': write_scale,
+                           'probe': 'tools/probes/bw_probe soa_read/soa_write, 8 B per lane, B=2^20, T=64'}}
+    for c in cfgs:
+        f = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE'), 'cv_run_kernel')
+        w = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE'), 'cv_run_kernel')
+        fetch = 1024 * sum(f) / len(f)
+        write = 1024 * sum(w) / len(w)
+        alg, _ = algorithmic_bytes(CONFIGS[c])
+        res[f'config{c}'] = {
+            'fetch_bytes_raw': fetch, 'write_bytes_raw': write,
+            'bytes_per_launch': fetch * read_scale + write * write_scale,
+            'algorithmic_bytes_per_launch': alg,
+            'traffic_over_algorithmic': (fetch * read_scale + write * write_scale) / alg,
+            'launches_profiled': len(f)}
+    with open(os.path.join(out_dir, 'pmc_traffic.json'), 'w') as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == '__main__':
+    main()
