@@ -52,6 +52,22 @@ extern "C" {
 #define KF_MODEL_CV2 2
 #define KF_MODEL_CV3 3
 
+/* The reference's own 15-state GPS+IMU model (kf_workers.py:493-614): state
+ * [pos(3), att(3), vel(3), rate(3), acc(3)], GPS fix m=3, IMU pseudo-measurement m=15, all
+ * constants as in the reference (kf_params must be NULL).  Every covariance reachable from the
+ * reference's diagonal P0 is exactly block-diagonal over the axis chains (pos,vel,acc) and
+ * (att,rate), so the handle stores P as 27 block-packed rows ([27][B]):
+ *   rows 6i..6i+5   axis i (pos_i, vel_i, acc_i) upper triangle (pp pv pa vv va aa)
+ *   rows 18+3i..+2  axis i (att_i, rate_i) upper triangle (tt tw ww)
+ * Driven by per-filter event streams (kf_run_events) or the combination search (kf_eval_combos). */
+#define KF_MODEL_REF15 15
+
+/* Event codes for kf_run_events / kf_eval_combos. */
+#define KF_EVENT_GPS     0    /* payload = (easting, northing, altitude, ...)              */
+#define KF_EVENT_IMU     1    /* payload = (roll, pitch, yaw, wx, wy, wz, ax, ay, az)     */
+#define KF_EVENT_PREDICT 2    /* predict only (the worker's final propagation)            */
+#define KF_EVENT_NONE    255  /* no event: state unchanged (padding of ragged streams)    */
+
 /* Model constants; kf_default_params() fills the reference's values. */
 typedef struct kf_params {
     double q_pos;   /* Q = diag(q_pos*dt I, q_vel*dt I): 5, 1   (kf_workers.py:521,523)        */
@@ -87,7 +103,8 @@ int kf_init(int device);
 int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_params* params);
 int kf_free(kf_batch* handle);
 
-/* Dimensions of a handle (any pointer may be NULL). */
+/* Dimensions of a handle (any pointer may be NULL).  For KF_MODEL_REF15: n = 15, m = 3 (GPS),
+ * c = 0, and the covariance has 27 block-packed rows instead of n(n+1)/2. */
 int kf_dims(const kf_batch* handle, int* n, int* m, int* c, int64_t* batch, int* dtype);
 
 /* Re-initialise every filter: x = x0 (device [n][B]; NULL = zeros), P = P0, status = OK.
@@ -141,6 +158,32 @@ int kf_run(kf_batch* handle, int T, double dt, const double* dt_steps, const voi
  * missing imu_data.csv (.MISSING_LARGE_BLOBS) with a synthetic stream of the same shape. */
 int kf_synth(kf_batch* handle, uint64_t seed, int64_t filter_offset, int T, double dt,
              int update_every, void* x0_out, void* u_out, void* z_out, void* stream);
+
+/* KF_MODEL_REF15: T events per filter in one launch.  etype device [T][B] uint8 (KF_EVENT_*),
+ * dt device [T][B] double (time since the filter's previous event), payload device [T][9][B]
+ * (handle dtype).  Per event: predict over dt, then the GPS update (kf_workers.py:694-697) or
+ * the IMU pseudo-measurement update built from the predicted state (:698-706); with gate != 0
+ * the update is applied only when logdet(P_pred) > threshold (:1023-1025).  traj device
+ * [T][6][B] receives x[0:6] after each event (:714), logdet [T][B] the log-determinant
+ * (:716-717), updated [T][B] uint8 whether the update was applied; each may be NULL.
+ * Replaces the loops of run_kalman_filter_full (:681-721) and
+ * run_adaptive_threshold_kalman_filter (:1010-1053), batched over filters. */
+int kf_run_events(kf_batch* handle, int T, const uint8_t* etype, const double* dt, const void* payload,
+                  void* traj, void* logdet, uint8_t* updated, int gate, double threshold, void* stream);
+
+/* KF_MODEL_REF15 brute-force search: filter f of the handle evaluates combination number
+ * combo_offset + f (itertools.combinations order) of k out of n_events candidate events, from the
+ * common initial state init (host [15 + 27] doubles: x, block-packed P), exactly as
+ * evaluate_combo_chunk_worker does (kf_workers.py:22-97): events in combination order, an event
+ * with negative dt skipped, then a predict to target_end.  events: host [n_events][11] doubles
+ * (t, KF_EVENT_GPS|KF_EVENT_IMU, payload[9]), n_events <= 64.  Outputs per filter: the final
+ * state in the handle, logdets device [k+2][B] (records, NaN-padded) and max_logdet device [B]
+ * (the brute-force acceptance test max(log_det) < R_threshold, :1353), n_records device [B];
+ * status 1 marks lanes past the last combination.  Replaces the Pool(30) fan-out of
+ * run_brute_force_kalman_filter_no_sampling_min_usage (:1320-1346). */
+int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const double* init,
+                   double prev_time, double target_end, int k, uint64_t combo_offset, void* logdets,
+                   void* max_logdet, int32_t* n_records, void* stream);
 
 #ifdef __cplusplus
 }

@@ -518,3 +518,25 @@ def parity_errors(traj, logdet, traj_ref, logdet_ref):
     nx = np.maximum(np.linalg.norm(traj_ref, axis=1), 1.0)
     dl = np.abs(logdet - logdet_ref) / np.maximum(np.abs(logdet_ref), 1.0)
     return float(np.max(dx / nx)) if dx.size else 0.0, float(np.max(dl)) if dl.size else 0.0
+
+
+def run_brute_force(events, start_idx, end_idx, R_threshold, initial_pt, initial_state):
+    """run_brute_force_kalman_filter_no_sampling_min_usage (kf_workers.py:1218-1392), warm-start
+    branch, serially: the first k-subset (smallest k, itertools.combinations order) whose
+    max(log_det) < R_threshold (:1349-1371)."""
+    from itertools import combinations
+    xt = np.zeros(15)
+    Pt = np.asarray(initial_pt, dtype=np.float64)
+    xt[0:6] = initial_state[1:7]
+    prev_time = initial_state[0]
+    cand = list(events[start_idx:end_idx])
+    target_end = events[end_idx - 1][2]
+    for k in range(1, len(cand) + 1):
+        for combo in combinations(cand, k):
+            res = evaluate_combo_chunk([combo], xt, Pt, prev_time, target_end)
+            if res and max(res[0][5]) < R_threshold:
+                metric, traj, combo, x_bf, P_bf, log_det, used = res[0]
+                return {'selected_sensors': combo, 'final_state': x_bf, 'final_covariance': P_bf,
+                        'trajectory': traj, 'accuracy_metric': metric, 'log_determinants': log_det,
+                        'num_measurements_used': used}
+    return None

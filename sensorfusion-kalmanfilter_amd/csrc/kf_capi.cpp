@@ -15,6 +15,7 @@ struct kf_batch {
     int model;
     int axes;   // d: state n = 2d, measurement m = d, control c = d
     int n, m, c;
+    int np;     // covariance rows: n(n+1)/2, or 27 block-packed rows for KF_MODEL_REF15
     int dtype;
     int64_t B;
     int device;
@@ -22,6 +23,7 @@ struct kf_batch {
     void* x;          // [n][B]
     void* P;          // [n(n+1)/2][B]
     int32_t* status;  // [B]
+    void* ws;         // KF_MODEL_REF15: device workspace for kf_eval_combos (events, binomials, init)
 };
 
 namespace {
@@ -43,7 +45,19 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 size_t elem(const kf_batch* h) { return h->dtype == KF_F64 ? 8 : 4; }
-int64_t ntri(const kf_batch* h) { return int64_t(h->n) * (h->n + 1) / 2; }
+int64_t ntri(const kf_batch* h) { return h->np; }
+
+constexpr int kMaxComboEvents = 64;
+constexpr size_t kWsEvents = sizeof(double) * kMaxComboEvents * 11;
+constexpr size_t kWsBinom = sizeof(uint64_t) * (kMaxComboEvents + 1) * (kMaxComboEvents + 1);
+constexpr size_t kWsInit = sizeof(double) * 42;
+
+bool is_ref15(const kf_batch* h) { return h->model == KF_MODEL_REF15; }
+
+int need_cv(const kf_batch* h, const char* what) {
+    if (is_ref15(h)) return fail(KF_EINVAL, "%s: not available for KF_MODEL_REF15 (use kf_run_events)", what);
+    return KF_OK;
+}
 
 kfmi::CvArgs base_args(const kf_batch* h) {
     kfmi::CvArgs a{};
@@ -79,8 +93,18 @@ int model_axes(int model) {
     switch (model) {
         case KF_MODEL_CV2: return 2;
         case KF_MODEL_CV3: return 3;
+        case KF_MODEL_REF15: return 3;
         default: return 0;
     }
+}
+
+kfmi::Ref15Args ref15_args(const kf_batch* h) {
+    kfmi::Ref15Args a{};
+    a.B = h->B;
+    a.x = h->x;
+    a.P = h->P;
+    a.status = h->status;
+    return a;
 }
 
 }  // namespace
@@ -94,6 +118,7 @@ const char* kf_last_error(void) { return g_err.c_str(); }
 int kf_default_params(int model, kf_params* out) {
     const int d = model_axes(model);
     if (!d) return fail(KF_EINVAL, "unknown model %d", model);
+    if (model == KF_MODEL_REF15) return fail(KF_EINVAL, "KF_MODEL_REF15 uses the reference constants; no kf_params");
     if (!out) return fail(KF_EINVAL, "null params");
     std::memset(out, 0, sizeof *out);
     out->q_pos = 5.0;  // position_noise = 5 * dt   (kf_workers.py:521)
@@ -138,22 +163,25 @@ int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_pa
     if (!d) return fail(KF_EINVAL, "unknown model %d", model);
     if (dtype != KF_F32 && dtype != KF_F64) return fail(KF_EINVAL, "unknown dtype %d", dtype);
     if (batch < 0) return fail(KF_EINVAL, "negative batch %lld", static_cast<long long>(batch));
-    if (batch > (int64_t(1) << 40)) return fail(KF_EINVAL, "batch %lld too large", static_cast<long long>(batch));
+    if (batch * 8 >= (int64_t(1) << 31))
+        return fail(KF_EINVAL, "batch %lld too large (one [B] row must stay below 2 GiB)", static_cast<long long>(batch));
+    if (model == KF_MODEL_REF15 && params) return fail(KF_EINVAL, "KF_MODEL_REF15 takes no kf_params (reference constants)");
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return fail(KF_ENODEV, "no current HIP device: %s", hipGetErrorString(e));
     kf_batch* h = new kf_batch{};
     h->model = model;
     h->axes = d;
-    h->n = 2 * d;
+    h->n = model == KF_MODEL_REF15 ? 15 : 2 * d;
     h->m = d;
-    h->c = d;
+    h->c = model == KF_MODEL_REF15 ? 0 : d;
+    h->np = model == KF_MODEL_REF15 ? 27 : h->n * (h->n + 1) / 2;
     h->dtype = dtype;
     h->B = batch;
     h->device = dev;
     if (params) {
         h->params = *params;
-    } else {
+    } else if (model != KF_MODEL_REF15) {
         kf_default_params(model, &h->params);
     }
     const size_t w = elem(h);
@@ -166,6 +194,11 @@ int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_pa
             kf_free(h);
             return fail(KF_ENOMEM, "hipMalloc of %zu filters failed", nb);
         }
+    }
+    if (model == KF_MODEL_REF15 && hipMalloc(&h->ws, kWsEvents + kWsBinom + kWsInit) != hipSuccess) {
+        (void)hipGetLastError();
+        kf_free(h);
+        return fail(KF_ENOMEM, "hipMalloc of the combination workspace failed");
     }
     int rc = kf_reset(h, nullptr, nullptr);
     if (rc == KF_OK && nb) {
@@ -185,6 +218,7 @@ int kf_free(kf_batch* h) {
     if (h->x) (void)hipFree(h->x);
     if (h->P) (void)hipFree(h->P);
     if (h->status) (void)hipFree(h->status);
+    if (h->ws) (void)hipFree(h->ws);
     delete h;
     return KF_OK;
 }
@@ -201,6 +235,13 @@ int kf_dims(const kf_batch* h, int* n, int* m, int* c, int64_t* batch, int* dtyp
 
 int kf_reset(kf_batch* h, const void* x0, void* stream) {
     if (int rc = check_handle(h)) return rc;
+    if (is_ref15(h)) {
+        if (h->B == 0) return KF_OK;
+        kfmi::Ref15Args a = ref15_args(h);
+        a.x0 = x0;
+        hipError_t e = kfmi::launch_ref15_reset(h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
+        return e == hipSuccess ? KF_OK : hip_fail(e, "kf_reset");
+    }
     kfmi::CvArgs a = base_args(h);
     a.x0 = x0;
     return launch(h, kfmi::Op::Reset, a, stream, "kf_reset");
@@ -251,6 +292,7 @@ int kf_get_status(const kf_batch* h, int32_t* status, int on_device, void* strea
 int kf_predict(kf_batch* h, double dt, const double* dt_per_filter, const void* u, void* logdet_out,
                void* stream) {
     if (int rc = check_handle(h)) return rc;
+    if (int rc = need_cv(h, "kf_predict")) return rc;
     if (!dt_per_filter && !(dt >= 0.0)) return fail(KF_EINVAL, "kf_predict: dt must be >= 0 (got %g)", dt);
     kfmi::CvArgs a = base_args(h);
     a.dt = dt;
@@ -262,6 +304,7 @@ int kf_predict(kf_batch* h, double dt, const double* dt_per_filter, const void* 
 
 int kf_update(kf_batch* h, const void* z, const uint8_t* mask, void* logdet_out, void* stream) {
     if (int rc = check_handle(h)) return rc;
+    if (int rc = need_cv(h, "kf_update")) return rc;
     if (!z && h->B) return fail(KF_EINVAL, "kf_update: null measurement stream z");
     kfmi::CvArgs a = base_args(h);
     a.z = z;
@@ -273,6 +316,7 @@ int kf_update(kf_batch* h, const void* z, const uint8_t* mask, void* logdet_out,
 int kf_run(kf_batch* h, int T, double dt, const double* dt_steps, const void* u, const void* z,
            const uint8_t* mask, int update_every, void* traj, void* logdet, void* stream) {
     if (int rc = check_handle(h)) return rc;
+    if (int rc = need_cv(h, "kf_run")) return rc;
     if (T < 0) return fail(KF_EINVAL, "kf_run: T = %d < 0", T);
     if (update_every < 1) return fail(KF_EINVAL, "kf_run: update_every = %d < 1", update_every);
     if (!dt_steps && !(dt >= 0.0)) return fail(KF_EINVAL, "kf_run: dt must be >= 0 (got %g)", dt);
@@ -295,6 +339,7 @@ int kf_run(kf_batch* h, int T, double dt, const double* dt_steps, const void* u,
 int kf_synth(kf_batch* h, uint64_t seed, int64_t filter_offset, int T, double dt, int update_every,
              void* x0_out, void* u_out, void* z_out, void* stream) {
     if (int rc = check_handle(h)) return rc;
+    if (int rc = need_cv(h, "kf_synth")) return rc;
     if (T < 0 || update_every < 1 || filter_offset < 0)
         return fail(KF_EINVAL, "kf_synth: bad T/update_every/filter_offset");
     if (h->B && (!x0_out || (T > 0 && !u_out) || (T / update_every > 0 && !z_out)))
@@ -313,6 +358,82 @@ int kf_synth(kf_batch* h, uint64_t seed, int64_t filter_offset, int T, double dt
     hipError_t e = kfmi::launch_synth(h->axes, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "kf_synth");
     return KF_OK;
+}
+
+int kf_run_events(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload,
+                  void* traj, void* logdet, uint8_t* updated, int gate, double threshold, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (!is_ref15(h)) return fail(KF_EINVAL, "kf_run_events: needs a KF_MODEL_REF15 handle");
+    if (T < 0) return fail(KF_EINVAL, "kf_run_events: T = %d < 0", T);
+    if (T == 0 || h->B == 0) return KF_OK;
+    if (!etype || !dt || !payload) return fail(KF_EINVAL, "kf_run_events: null etype/dt/payload stream");
+    kfmi::Ref15Args a = ref15_args(h);
+    a.T = T;
+    a.etype = etype;
+    a.dt = dt;
+    a.payload = payload;
+    a.traj = traj;
+    a.logdet = logdet;
+    a.updated = updated;
+    a.gate = gate;
+    a.threshold = threshold;
+    hipError_t e = kfmi::launch_ref15_events(h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? KF_OK : hip_fail(e, "kf_run_events");
+}
+
+int kf_eval_combos(kf_batch* h, int n_events, const double* events, const double* init, double prev_time,
+                   double target_end, int k, uint64_t combo_offset, void* logdets, void* max_logdet,
+                   int32_t* n_records, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (!is_ref15(h)) return fail(KF_EINVAL, "kf_eval_combos: needs a KF_MODEL_REF15 handle");
+    if (n_events < 1 || n_events > kMaxComboEvents)
+        return fail(KF_EINVAL, "kf_eval_combos: n_events = %d outside [1, %d]", n_events, kMaxComboEvents);
+    if (k < 1 || k > n_events) return fail(KF_EINVAL, "kf_eval_combos: k = %d outside [1, %d]", k, n_events);
+    if (!events || !init) return fail(KF_EINVAL, "kf_eval_combos: null events/init");
+    for (int i = 0; i < n_events; ++i) {
+        const double ty = events[i * 11 + 1];
+        if (ty != KF_EVENT_GPS && ty != KF_EVENT_IMU)
+            return fail(KF_EINVAL, "kf_eval_combos: event %d has type %g (GPS=0 or IMU=1)", i, ty);
+    }
+    if (h->B == 0) return KF_OK;
+    // binomial table C(a, b), a, b <= 64 (exact in uint64)
+    static uint64_t binom[(kMaxComboEvents + 1) * (kMaxComboEvents + 1)];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (int a = 0; a <= kMaxComboEvents; ++a)
+            for (int b = 0; b <= kMaxComboEvents; ++b) {
+                uint64_t v = 0;
+                if (b == 0) v = 1;
+                else if (a > 0 && b <= a) v = binom[(a - 1) * (kMaxComboEvents + 1) + b - 1] + binom[(a - 1) * (kMaxComboEvents + 1) + b];
+                binom[a * (kMaxComboEvents + 1) + b] = v;
+            }
+    });
+    const uint64_t n_combos = binom[n_events * (kMaxComboEvents + 1) + k];
+    char* ws = static_cast<char*>(h->ws);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipError_t e = hipMemcpyAsync(ws, events, sizeof(double) * 11 * n_events, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(ws + kWsEvents, binom, kWsBinom, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(ws + kWsEvents + kWsBinom, init, kWsInit, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail(e, "kf_eval_combos: upload");
+    kfmi::Ref15ComboArgs a{};
+    a.B = h->B;
+    a.n_events = n_events;
+    a.k = k;
+    a.combo_offset = combo_offset;
+    a.n_combos = n_combos;
+    a.ev = reinterpret_cast<const double*>(ws);
+    a.binom = reinterpret_cast<const uint64_t*>(ws + kWsEvents);
+    a.init = reinterpret_cast<const double*>(ws + kWsEvents + kWsBinom);
+    a.prev_time = prev_time;
+    a.target_end = target_end;
+    a.x = h->x;
+    a.P = h->P;
+    a.status = h->status;
+    a.logdets = logdets;
+    a.max_logdet = max_logdet;
+    a.n_records = n_records;
+    e = kfmi::launch_ref15_combos(h->dtype == KF_F64, a, st);
+    return e == hipSuccess ? KF_OK : hip_fail(e, "kf_eval_combos");
 }
 
 }  // extern "C"

@@ -24,121 +24,15 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "kf_common.h"
 #include "kf_internal.h"
 
 namespace kfmi {
 namespace {
 
-constexpr int32_t kNotSpd = -3;  // KF_ENOTSPD
+using namespace dev;
 
-// Upper-triangle packed row-major index of (i, j) in an N x N symmetric matrix.
-template <int N>
-__host__ __device__ constexpr int tri(int i, int j) {
-    return i <= j ? i * N - i * (i - 1) / 2 + (j - i) : j * N - j * (j - 1) / 2 + (i - j);
-}
 
-__device__ __forceinline__ double fmaT(double a, double b, double c) { return __builtin_fma(a, b, c); }
-__device__ __forceinline__ float fmaT(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-
-template <typename T>
-__device__ __forceinline__ T quiet_nan();
-template <>
-__device__ __forceinline__ double quiet_nan<double>() { return __builtin_nan(""); }
-template <>
-__device__ __forceinline__ float quiet_nan<float>() { return __builtin_nanf(""); }
-
-// 1/d: the hardware approximation (v_rcp_f64 / v_rcp_f32) refined by NEWTON Newton steps.
-template <int NEWTON>
-__device__ __forceinline__ double rcp_nr(double d) {
-    double r = __builtin_amdgcn_rcp(d);
-#pragma unroll
-    for (int i = 0; i < NEWTON; ++i) r = fmaT(r, fmaT(-d, r, 1.0), r);
-    return r;
-}
-template <int NEWTON>
-__device__ __forceinline__ float rcp_nr(float d) {
-    float r = __builtin_amdgcn_rcpf(d);
-#pragma unroll
-    for (int i = 0; i < NEWTON; ++i) r = fmaT(r, fmaT(-d, r, 1.0f), r);
-    return r;
-}
-// Same, but NaN unless d > 0: a non-positive pivot of S poisons everything derived from it.
-template <int NEWTON, typename T>
-__device__ __forceinline__ T rcp_pos(T d) {
-    const T r = rcp_nr<NEWTON>(d);
-    return d > T(0) ? r : quiet_nan<T>();
-}
-
-// log(m) + e ln 2 for a mantissa m in [0.5, 1) (the frexp-normalised pivot product).
-// fp64: reduce to m' in [sqrt(1/2), sqrt(2)), then log m' = 2 atanh(s), s = (m'-1)/(m'+1),
-// |s| < 0.1716, summed to s^21 (truncation < 1e-17) — ~25 VALU ops instead of the ~100 of
-// the general double-double log().  fp32: the hardware log (v_log_f32).
-__device__ __forceinline__ double log_mant(double m, int e) {
-    const bool lo = m < 0.70710678118654752440;
-    m = lo ? m + m : m;
-    e = lo ? e - 1 : e;
-    const double f = m - 1.0;
-    const double s = f * rcp_nr<2>(2.0 + f);
-    const double s2 = s * s;
-    double p = 1.0 / 21;
-    p = fmaT(p, s2, 1.0 / 19);
-    p = fmaT(p, s2, 1.0 / 17);
-    p = fmaT(p, s2, 1.0 / 15);
-    p = fmaT(p, s2, 1.0 / 13);
-    p = fmaT(p, s2, 1.0 / 11);
-    p = fmaT(p, s2, 1.0 / 9);
-    p = fmaT(p, s2, 1.0 / 7);
-    p = fmaT(p, s2, 1.0 / 5);
-    p = fmaT(p, s2, 1.0 / 3);
-    const double two_s = s + s;
-    const double lm = fmaT(two_s * s2, p, two_s);
-    return fmaT(double(e), 0.69314718055994530942, lm);
-}
-__device__ __forceinline__ float log_mant(float m, int e) {
-    return fmaT(float(e), 0.69314718055994530942f, __logf(m));
-}
-
-// log det of an SPD N x N matrix (packed upper) via LDL^T: log of the pivot product, with
-// the product renormalised by its binary exponent every 3 pivots so fp32 cannot overflow.
-// NaN if a pivot is not > 0 (covariance lost positive definiteness).
-template <int N, typename T>
-__device__ __forceinline__ T logdet_ldl(const T (&P)[N * (N + 1) / 2]) {
-    T L[N][N];
-    T d[N];
-    T prod = T(1);
-    int ex = 0;
-    bool ok = true;
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        T v[N];
-        T dj = P[tri<N>(j, j)];
-#pragma unroll
-        for (int k = 0; k < j; ++k) {
-            v[k] = L[j][k] * d[k];
-            dj = fmaT(-L[j][k], v[k], dj);
-        }
-        ok = ok && (dj > T(0));
-        d[j] = dj;
-        prod *= dj;
-        if (j % 3 == 2 || j == N - 1) {
-            int e;
-            prod = frexp(prod, &e);
-            ex += e;
-        }
-        if (j + 1 < N) {
-            const T dinv = rcp_nr<1>(dj);  // a bad pivot already makes `ok` false
-#pragma unroll
-            for (int i = j + 1; i < N; ++i) {
-                T s = P[tri<N>(i, j)];
-#pragma unroll
-                for (int k = 0; k < j; ++k) s = fmaT(-L[i][k], v[k], s);
-                L[i][j] = s * dinv;
-            }
-        }
-    }
-    const T ld = log_mant(prod, ex);  // prod was frexp-normalised at the last pivot
-    return ok ? ld : quiet_nan<T>();
-}
 
 template <int D, typename T>
 struct Cv {
@@ -180,139 +74,13 @@ struct Cv {
     }
 
     // GPS update with H = [I 0] (kf_workers.py:551-558, 616-621, 708-711; Joseph form).
-    // R is packed upper (m x m); DIAG_R skips its zero off-diagonal terms.
-    // Returns false when S is not positive definite (x and P are then NaN).
     template <bool DIAG_R>
     __device__ static __forceinline__ bool update(T (&x)[N], T (&P)[NT], const T (&z)[M],
                                                   const T (&R)[MT]) {
-        // S = H P H^T + R, then its LDL^T
-        T S[MT];
-#pragma unroll
-        for (int i = 0; i < M; ++i)
-#pragma unroll
-            for (int j = i; j < M; ++j)
-                S[tri<M>(i, j)] = (i == j || !DIAG_R) ? P[tri<N>(i, j)] + R[tri<M>(i, j)] : P[tri<N>(i, j)];
-        T L[M][M];
-        T d[M];
-        T dinv[M];
-        bool ok = true;
-#pragma unroll
-        for (int j = 0; j < M; ++j) {
-            T v[M];
-            T dj = S[tri<M>(j, j)];
-#pragma unroll
-            for (int k = 0; k < j; ++k) {
-                v[k] = L[j][k] * d[k];
-                dj = fmaT(-L[j][k], v[k], dj);
-            }
-            ok = ok && (dj > T(0));
-            d[j] = dj;
-            dinv[j] = rcp_pos<2>(dj);
-#pragma unroll
-            for (int i = j + 1; i < M; ++i) {
-                T s = S[tri<M>(i, j)];
-#pragma unroll
-                for (int k = 0; k < j; ++k) s = fmaT(-L[i][k], v[k], s);
-                L[i][j] = s * dinv[j];
-            }
-        }
-        // K row i solves S k = (P H^T)_i = P[i, 0:m]
-        T K[N][M];
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            T w[M];
-#pragma unroll
-            for (int a = 0; a < M; ++a) {
-                T s = P[tri<N>(i, a)];
-#pragma unroll
-                for (int b = 0; b < a; ++b) s = fmaT(-L[a][b], w[b], s);
-                w[a] = s;
-            }
-#pragma unroll
-            for (int a = M - 1; a >= 0; --a) {
-                T s = w[a] * dinv[a];
-#pragma unroll
-                for (int b = a + 1; b < M; ++b) s = fmaT(-L[b][a], K[i][b], s);
-                K[i][a] = s;
-            }
-        }
-        // x += K (z - H x)
-        T y[M];
-#pragma unroll
-        for (int a = 0; a < M; ++a) y[a] = z[a] - x[a];
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            T s = x[i];
-#pragma unroll
-            for (int a = 0; a < M; ++a) s = fmaT(K[i][a], y[a], s);
-            x[i] = s;
-        }
-        // Joseph: P+ = (I-KH) P (I-KH)^T + K R K^T = (P - K G^T) + E K^T with G = P H^T and
-        // E = K S - G, an identity for ANY K (E is the residual of the gain equation K S = G,
-        // so an error dK in the gain enters P+ only as dK S dK^T).  Upper triangle only, row
-        // by row; row i's E is formed just before it is used so only m values of E are live.
-        // Rows >= m are written in place (their old values are read only by themselves); rows
-        // < m hold G and feed every row, so their new values are staged until the end.
-        T top[M][N];
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            T E[M];
-#pragma unroll
-            for (int a = 0; a < M; ++a) {
-                T e = -P[tri<N>(i, a)];
-#pragma unroll
-                for (int b = 0; b < M; ++b) e = fmaT(K[i][b], S[tri<M>(b, a)], e);
-                E[a] = e;
-            }
-#pragma unroll
-            for (int j = i; j < N; ++j) {
-                T s = P[tri<N>(i, j)];
-#pragma unroll
-                for (int b = 0; b < M; ++b) s = fmaT(-K[i][b], P[tri<N>(b, j)], s);
-#pragma unroll
-                for (int a = 0; a < M; ++a) s = fmaT(E[a], K[j][a], s);
-                if (i < M)
-                    top[i][j] = s;
-                else
-                    P[tri<N>(i, j)] = s;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < M; ++i)
-#pragma unroll
-            for (int j = i; j < N; ++j) P[tri<N>(i, j)] = top[i][j];
-        return ok;
+        return sel_update<N, M, DIAG_R, T>(x, P, z, R);
     }
 };
 
-// Addressing: every access goes through a raw buffer descriptor built from wave-uniform
-// scalars — the base of one [B]-long row (component i of step t) and the row's byte length —
-// plus the lane's 32-bit byte offset (buffer_load ... offen).  No 64-bit address lives in
-// VGPRs, and the hardware range check turns an out-of-row access into a dropped store /
-// zero load instead of a fault.  B * sizeof(T) < 2^31 is enforced by kf_alloc.
-typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, int64_t r, uint32_t row_bytes) {
-    const char* p = reinterpret_cast<const char*>(base) + r * int64_t(row_bytes);
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(p), 0, row_bytes, 0x00020000);
-}
-
-template <typename T>
-__device__ __forceinline__ T ldb(const void* base, int64_t r, uint32_t row_bytes, uint32_t off);
-template <>
-__device__ __forceinline__ double ldb<double>(const void* base, int64_t r, uint32_t row_bytes, uint32_t off) {
-    return __builtin_bit_cast(double, (v2u)__builtin_amdgcn_raw_buffer_load_b64(row_rsrc(base, r, row_bytes), off, 0, 0));
-}
-template <>
-__device__ __forceinline__ float ldb<float>(const void* base, int64_t r, uint32_t row_bytes, uint32_t off) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base, r, row_bytes), off, 0, 0));
-}
-__device__ __forceinline__ void stb(void* base, int64_t r, uint32_t row_bytes, uint32_t off, double v) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), row_rsrc(base, r, row_bytes), off, 0, 0);
-}
-__device__ __forceinline__ void stb(void* base, int64_t r, uint32_t row_bytes, uint32_t off, float v) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), row_rsrc(base, r, row_bytes), off, 0, 0);
-}
 
 template <int D, typename T>
 __device__ __forceinline__ void load_state(const CvArgs& a, uint32_t rb, uint32_t off, T (&x)[2 * D],
@@ -540,47 +308,6 @@ __global__ __launch_bounds__(kBlock) void cv_reset_kernel(const CvArgs a) {
     a.status[f] = 0;
 }
 
-// ------------------------------------------------------------------------------------
-// Synthetic GPS+IMU streams: Philox4x32-10 (Salmon et al., SC'11), counter = (t, draw,
-// filter lo, filter hi), key = seed.  Generated in fp64, rounded once to T.
-// ------------------------------------------------------------------------------------
-struct U4 {
-    uint32_t v[4];
-};
-
-__device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                            uint32_t k0, uint32_t k1) {
-    constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint64_t p0 = uint64_t(M0) * c0;
-        const uint64_t p1 = uint64_t(M1) * c2;
-        const uint32_t n0 = uint32_t(p1 >> 32) ^ c1 ^ k0;
-        const uint32_t n1 = uint32_t(p1);
-        const uint32_t n2 = uint32_t(p0 >> 32) ^ c3 ^ k1;
-        const uint32_t n3 = uint32_t(p0);
-        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
-        k0 += W0;
-        k1 += W1;
-    }
-    return U4{{c0, c1, c2, c3}};
-}
-
-__device__ __forceinline__ double u53(uint32_t hi, uint32_t lo) {
-    const uint64_t a = (uint64_t(hi) << 21) ^ (lo >> 11);
-    return (double(a & ((1ull << 53) - 1)) + 0.5) * 0x1.0p-53;  // (0, 1)
-}
-
-// Two independent N(0,1) from one Philox block (53-bit uniforms, Box-Muller).
-__device__ __forceinline__ void normal2(const U4& r, double& n0, double& n1) {
-    const double u1 = u53(r.v[0], r.v[1]);
-    const double u2 = u53(r.v[2], r.v[3]);
-    const double rad = sqrt(-2.0 * log(u1));
-    double sn, cs;
-    sincos(6.283185307179586476925 * u2, &sn, &cs);
-    n0 = rad * cs;
-    n1 = rad * sn;
-}
 
 template <int D, typename T>
 __global__ __launch_bounds__(kBlock) void cv_synth_kernel(const SynthArgs a) {

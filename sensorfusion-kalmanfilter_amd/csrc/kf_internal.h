@@ -41,11 +41,55 @@ struct SynthArgs {
     void* z;                 // [U][m][B]
 };
 
+// Reference 15-state model (kf_workers.py:493-614) on per-filter event streams.
+// Event codes in etype: 0 GPS fix, 1 IMU sample, 2 predict only, 255 no event (padding).
+struct Ref15Args {
+    int64_t B;
+    int T;
+    const uint8_t* etype;    // [T][B]
+    const double* dt;        // [T][B] time since the filter's previous event
+    const void* payload;     // [T][9][B]: GPS (easting, northing, altitude, -), IMU (roll, pitch,
+                             // yaw, wx, wy, wz, ax, ay, az) as in kf_workers.py:367
+    void* x;                 // [15][B]
+    void* P;                 // [27][B] block-packed covariance (see kf_ref15.hip)
+    int32_t* status;         // [B]
+    const void* x0;          // reset: [15][B] or nullptr
+    void* traj;              // [T][6][B] x[0:6] after each event, or nullptr
+    void* logdet;            // [T][B] or nullptr
+    uint8_t* updated;        // [T][B] 1 if the event's update was applied, or nullptr
+    int gate;                // adaptive threshold (kf_workers.py:1023-1025): update only if
+    double threshold;        //   logdet(P_pred) > threshold
+};
+
+// Brute-force search over k-subsets of n candidate events (kf_workers.py:22-97, 1218-1392):
+// lane f evaluates combination number combo_offset + f in itertools.combinations order.
+struct Ref15ComboArgs {
+    int64_t B;
+    int n_events;
+    int k;
+    uint64_t combo_offset;
+    uint64_t n_combos;       // C(n, k)
+    const double* ev;        // device [n][11]: t, type, payload[9]
+    const uint64_t* binom;   // device [65][65] binomial coefficients
+    double prev_time;
+    double target_end;
+    const double* init;      // device [15 + 27]: x0, P0 blocks
+    void* x;                 // [15][B] final state per combination
+    void* P;                 // [27][B]
+    int32_t* status;         // [B]: 0, KF_ENOTSPD, or 1 = padding lane (no combination)
+    void* logdets;           // [k+2][B] record list (NaN-padded) or nullptr
+    void* max_logdet;        // [B] or nullptr
+    int32_t* n_records;      // [B] or nullptr
+};
+
 enum class Op { Run, Predict, Update, Reset };
 
 // Launchers (kf_cv.hip).  Return hipSuccess or the launch error.
 hipError_t launch_cv(int axes, bool f64, Op op, const CvArgs& a, hipStream_t stream);
 hipError_t launch_synth(int axes, bool f64, const SynthArgs& a, hipStream_t stream);
+hipError_t launch_ref15_events(bool f64, const Ref15Args& a, hipStream_t stream);
+hipError_t launch_ref15_reset(bool f64, const Ref15Args& a, hipStream_t stream);
+hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream);
 
 constexpr int kBlock = 256;  // 4 wave64 per workgroup
 

@@ -1,0 +1,401 @@
+// gfx950 kernels for the reference's 15-state GPS+IMU model (KF_MODEL_REF15,
+// kf_workers.py:493-614) on per-filter event streams, and the brute-force combination search
+// built on it (kf_workers.py:22-97, 1218-1392).
+//
+// Structure exploited (exact, not an approximation): F(dt) (kf_workers.py:500-516) couples a
+// state only within its axis chain (pos_i, vel_i, acc_i) or (att_i, rate_i); Q, R_gps, R_imu and
+// the reference's P0 are diagonal; H_gps selects pos_i and H_imu = I.  So every covariance
+// reachable from a diagonal P0 is block-diagonal — three 3x3 (pos, vel, acc) blocks and three 2x2
+// (att, rate) blocks — and the reference's own 15x15 arithmetic keeps the off-block entries at
+// exactly 0.0 (checked on its outputs, tests/golden/ref15_*.npz).  A lane therefore runs six
+// small chain filters: 27 covariance entries instead of 120, the same numbers.
+//
+// Block-packed covariance rows ([27][B] in HBM):
+//   rows 6i .. 6i+5 : axis i (pos_i, vel_i, acc_i) upper triangle (pp pv pa vv va aa), i = 0..2
+//   rows 18+3i .. 18+3i+2 : axis i (att_i, rate_i) upper triangle (tt tw ww)
+// State x [15][B] in the reference order (pos, att, vel, rate, acc).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kf_common.h"
+#include "kf_internal.h"
+
+namespace kfmi {
+namespace {
+
+using namespace dev;
+
+constexpr int kGps = 0, kImu = 1;  // KF_EVENT_GPS / KF_EVENT_IMU; 2 = predict only, 255 = none
+
+// Reference constants (kf_workers.py:519-544, 581-614, 651).
+constexpr double kQPos = 5.0, kQAtt = 0.05, kQVel = 1.0, kQRate = 0.1, kQAcc = 2.0;
+constexpr double kRGps = 3.0;
+constexpr double kRPos = 50.0, kRAtt = 0.05, kRVel = 10.0, kRRate = 0.1, kRAcc = 100.0;
+constexpr double kP0Pos = 10000.0, kP0Att = 1000.0, kP0Vel = 1000.0, kP0Rate = 1000.0, kP0Acc = 10000.0;
+
+template <typename T>
+struct Ref15 {
+    T x[15];
+    T pva[3][6];  // per axis: (pos, vel, acc) packed upper 3x3
+    T aw[3][3];   // per axis: (att, rate) packed upper 2x2
+
+    // Chain predict x = F x, P = F P F^T + Q for a block whose F row i is
+    // e_i + dt e_{i+1} + dt^2/2 e_{i+2} (kf_workers.py:500-516).
+    template <int NB>
+    __device__ static __forceinline__ void chain_predict(T (&xb)[NB], T (&Pb)[NB * (NB + 1) / 2], T dt,
+                                                         const T (&q)[NB]) {
+        const T c[3] = {T(1), dt, T(0.5) * dt * dt};
+        T xn[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            T s = xb[i];
+#pragma unroll
+            for (int d = 1; d < NB - i && d < 3; ++d) s = fmaT(c[d], xb[i + d], s);
+            xn[i] = s;
+        }
+        T FP[NB][NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                T s = Pb[tri<NB>(i, j)];
+#pragma unroll
+                for (int d = 1; d < NB - i && d < 3; ++d) s = fmaT(c[d], Pb[tri<NB>(i + d, j)], s);
+                FP[i][j] = s;
+            }
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+#pragma unroll
+            for (int j = i; j < NB; ++j) {
+                T s = FP[i][j];
+#pragma unroll
+                for (int e = 1; e < NB - j && e < 3; ++e) s = fmaT(FP[i][j + e], c[e], s);
+                Pb[tri<NB>(i, j)] = (i == j) ? s + q[i] * dt : s;
+            }
+#pragma unroll
+        for (int i = 0; i < NB; ++i) xb[i] = xn[i];
+    }
+
+    __device__ __forceinline__ void predict(T dt) {
+        const T qpva[3] = {T(kQPos), T(kQVel), T(kQAcc)};
+        const T qaw[2] = {T(kQAtt), T(kQRate)};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            T xb[3] = {x[i], x[6 + i], x[12 + i]};
+            chain_predict<3>(xb, pva[i], dt, qpva);
+            x[i] = xb[0];
+            x[6 + i] = xb[1];
+            x[12 + i] = xb[2];
+            T xa[2] = {x[3 + i], x[9 + i]};
+            chain_predict<2>(xa, aw[i], dt, qaw);
+            x[3 + i] = xa[0];
+            x[9 + i] = xa[1];
+        }
+    }
+
+    // GPS fix (kf_workers.py:694-697): H selects pos_i in each (pos, vel, acc) block, R = 3.
+    __device__ __forceinline__ bool update_gps(const T (&z)[3]) {
+        bool ok = true;
+        const T R[1] = {T(kRGps)};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            T xb[3] = {x[i], x[6 + i], x[12 + i]};
+            const T zb[1] = {z[i]};
+            ok = sel_update<3, 1, true, T>(xb, pva[i], zb, R) && ok;
+            x[i] = xb[0];
+            x[6 + i] = xb[1];
+            x[12 + i] = xb[2];
+        }
+        return ok;
+    }
+
+    // IMU pseudo-measurement (kf_workers.py:698-706): Z from the PREDICTED state and the raw
+    // sample, H = I, R = diag(50, 0.05, 10, 0.1, 100 per group).  imu = (roll, pitch, yaw, wx, wy,
+    // wz, ax, ay, az).
+    __device__ __forceinline__ bool update_imu(const T (&imu)[9], T dt) {
+        bool ok = true;
+        const T Rp[6] = {T(kRPos), T(0), T(0), T(kRVel), T(0), T(kRAcc)};
+        const T Ra[3] = {T(kRAtt), T(0), T(kRRate)};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const T a = imu[6 + i];
+            const T V = fmaT(a, dt, x[6 + i]);   // V = x_v + a dt
+            const T X = fmaT(V, dt, x[i]);       // X = x_p + V dt
+            T xb[3] = {x[i], x[6 + i], x[12 + i]};
+            const T zb[3] = {X, V, a};
+            ok = sel_update<3, 3, true, T>(xb, pva[i], zb, Rp) && ok;
+            x[i] = xb[0];
+            x[6 + i] = xb[1];
+            x[12 + i] = xb[2];
+            T xa[2] = {x[3 + i], x[9 + i]};
+            const T za[2] = {imu[i], imu[3 + i]};
+            ok = sel_update<2, 2, true, T>(xa, aw[i], za, Ra) && ok;
+            x[3 + i] = xa[0];
+            x[9 + i] = xa[1];
+        }
+        return ok;
+    }
+
+    // slogdet of the full 15x15 P = sum over the six blocks (kf_workers.py:716-717).
+    __device__ __forceinline__ T logdet() const {
+        T prod = T(1);
+        int ex = 0;
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) ldl_pivot_product<3, T>(pva[i], prod, ex, ok);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) ldl_pivot_product<2, T>(aw[i], prod, ex, ok);
+        int e;
+        prod = frexp(prod, &e);
+        const T ld = log_mant(prod, ex + e);
+        return ok ? ld : quiet_nan<T>();
+    }
+
+    __device__ __forceinline__ void reset_cov() {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const T p[6] = {T(kP0Pos), T(0), T(0), T(kP0Vel), T(0), T(kP0Acc)};
+            const T w[3] = {T(kP0Att), T(0), T(kP0Rate)};
+#pragma unroll
+            for (int k = 0; k < 6; ++k) pva[i][k] = p[k];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) aw[i][k] = w[k];
+        }
+    }
+
+    __device__ __forceinline__ void load(const void* xbase, const void* Pbase, uint32_t rb, uint32_t off) {
+#pragma unroll
+        for (int i = 0; i < 15; ++i) x[i] = ldb<T>(xbase, i, rb, off);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) pva[i][k] = ldb<T>(Pbase, 6 * i + k, rb, off);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) aw[i][k] = ldb<T>(Pbase, 18 + 3 * i + k, rb, off);
+    }
+
+    __device__ __forceinline__ void store(void* xbase, void* Pbase, uint32_t rb, uint32_t off) const {
+#pragma unroll
+        for (int i = 0; i < 15; ++i) stb(xbase, i, rb, off, x[i]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) stb(Pbase, 6 * i + k, rb, off, pva[i][k]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) stb(Pbase, 18 + 3 * i + k, rb, off, aw[i][k]);
+    }
+
+    __device__ __forceinline__ void fill_nan() {
+#pragma unroll
+        for (int i = 0; i < 15; ++i) x[i] = quiet_nan<T>();
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) pva[i][k] = quiet_nan<T>();
+#pragma unroll
+            for (int k = 0; k < 3; ++k) aw[i][k] = quiet_nan<T>();
+        }
+    }
+
+    // One event of the reference loop (kf_workers.py:682-717): predict over dt, then the GPS or
+    // IMU update; with `gate`, the update only when logdet(P_pred) > threshold
+    // (run_adaptive_threshold_kalman_filter, kf_workers.py:1023-1025).  Returns whether the
+    // update was applied; `ok` turns false on a non-positive-definite S.
+    __device__ __forceinline__ bool event(int type, T dt, const T (&pay)[9], bool gate, T threshold, bool& ok) {
+        predict(dt);
+        bool apply = (type == kGps || type == kImu);
+        if (gate && apply) apply = logdet() > threshold;
+        if (apply) {
+            if (type == kGps) {
+                const T z[3] = {pay[0], pay[1], pay[2]};
+                ok = update_gps(z) && ok;
+            } else {
+                ok = update_imu(pay, dt) && ok;
+            }
+        }
+        return apply;
+    }
+};
+
+// ------------------------------------------------------------------------------------
+// Per-filter event streams (kf_run_events).
+// ------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock) void ref15_events_kernel(const Ref15Args a) {
+    const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (f >= a.B) return;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
+    const uint32_t rb8 = uint32_t(a.B) * 8u;
+    const uint32_t off8 = uint32_t(f) * 8u;
+    Ref15<T> s;
+    s.load(a.x, a.P, rb, off);
+    int32_t st = a.status[f];
+    const uint32_t rb_tr = a.traj ? rb : 0u, rb_ld = a.logdet ? rb : 0u;
+    for (int t = 0; t < a.T; ++t) {
+        const int type = a.etype[int64_t(t) * a.B + f];
+        const T dt = T(ldb<double>(a.dt, t, rb8, off8));
+        T pay[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) pay[i] = ldb<T>(a.payload, int64_t(t) * 9 + i, rb, off);
+        bool applied = false;
+        if (type != 255) {
+            bool ok = true;
+            applied = s.event(type, dt, pay, a.gate != 0, T(a.threshold), ok);
+            if (!ok) {
+                st = kNotSpd;
+                s.fill_nan();
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) stb(a.traj, int64_t(t) * 6 + i, rb_tr, off, s.x[i]);
+        if (a.logdet) {
+            const T ld = s.logdet();
+            st = (ld == ld) ? st : kNotSpd;
+            stb(a.logdet, t, rb_ld, off, ld);
+        }
+        if (a.updated) a.updated[int64_t(t) * a.B + f] = applied ? 1 : 0;
+    }
+    s.store(a.x, a.P, rb, off);
+    a.status[f] = st;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void ref15_reset_kernel(const Ref15Args a) {
+    const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (f >= a.B) return;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
+    Ref15<T> s;
+#pragma unroll
+    for (int i = 0; i < 15; ++i) s.x[i] = a.x0 ? ldb<T>(a.x0, i, rb, off) : T(0);
+    s.reset_cov();
+    s.store(a.x, a.P, rb, off);
+    a.status[f] = 0;
+}
+
+// ------------------------------------------------------------------------------------
+// Brute-force combination search (kf_eval_combos).  The n candidate events and the binomial
+// table sit in LDS; lane f unranks combination combo_offset + f (lexicographic =
+// itertools.combinations order) one index at a time while it runs the filter, so no per-lane
+// index list is stored.
+// ------------------------------------------------------------------------------------
+constexpr int kMaxEvents = 64;
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void ref15_combo_kernel(const Ref15ComboArgs a) {
+    __shared__ double s_ev[kMaxEvents * 11];
+    __shared__ uint64_t s_binom[(kMaxEvents + 1) * (kMaxEvents + 1)];
+    const int n = a.n_events;
+    for (int i = threadIdx.x; i < n * 11; i += kBlock) s_ev[i] = a.ev[i];
+    for (int i = threadIdx.x; i < (n + 1) * (kMaxEvents + 1); i += kBlock) s_binom[i] = a.binom[i];
+    __syncthreads();
+
+    const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (f >= a.B) return;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
+    const uint64_t rank0 = a.combo_offset + uint64_t(f);
+    const bool live = rank0 < a.n_combos;
+    const uint32_t rb_ld = a.logdets ? rb : 0u;
+
+    Ref15<T> s;
+#pragma unroll
+    for (int i = 0; i < 15; ++i) s.x[i] = T(a.init[i]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) s.pva[i][k] = T(a.init[15 + 6 * i + k]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) s.aw[i][k] = T(a.init[33 + 3 * i + k]);
+
+    // record 0: logdet of the initial covariance (kf_workers.py:32)
+    T ld = s.logdet();
+    T ld_max = ld;
+    int rec = 0;
+    stb(a.logdets, rec, rb_ld, off, ld);
+    ++rec;
+    bool ok = true;
+    double cur = a.prev_time;
+    uint64_t r = live ? rank0 : 0;
+    int cand = 0;
+    const T no_gate = T(0);
+    for (int j = 0; j < a.k; ++j) {
+        // unrank the j-th element: skip candidates whose sub-tree is entirely below r
+        const int left = a.k - j - 1;
+        while (cand < n) {
+            const uint64_t cnt = s_binom[(n - cand - 1) * (kMaxEvents + 1) + left];
+            if (r < cnt) break;
+            r -= cnt;
+            ++cand;
+        }
+        const int e = cand < n ? cand : n - 1;
+        ++cand;
+        const double te = s_ev[e * 11];
+        const double dtd = te - cur;
+        if (dtd < 0.0) continue;  // kf_workers.py:38-40: skip, prev time unchanged
+        T pay[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) pay[i] = T(s_ev[e * 11 + 2 + i]);
+        s.event(int(s_ev[e * 11 + 1]), T(dtd), pay, false, no_gate, ok);
+        cur = te;
+        ld = s.logdet();
+        ld_max = ld > ld_max ? ld : ld_max;
+        stb(a.logdets, rec, rb_ld, off, ld);
+        ++rec;
+    }
+    // always propagate to the common end time (kf_workers.py:74-82)
+    if (cur < a.target_end - 1e-8) {
+        s.predict(T(a.target_end - cur));
+        ld = s.logdet();
+        ld_max = ld > ld_max ? ld : ld_max;
+        stb(a.logdets, rec, rb_ld, off, ld);
+        ++rec;
+    }
+    for (int q = rec; q < a.k + 2; ++q) stb(a.logdets, q, rb_ld, off, quiet_nan<T>());
+    int32_t st = ok ? 0 : kNotSpd;
+    if (!live) {
+        st = 1;
+        ld_max = quiet_nan<T>();
+    } else if (!ok || !(ld_max == ld_max)) {
+        st = kNotSpd;
+        s.fill_nan();
+        ld_max = quiet_nan<T>();
+    }
+    if (a.max_logdet) stb(a.max_logdet, 0, rb, off, ld_max);
+    if (a.n_records) a.n_records[f] = rec;
+    s.store(a.x, a.P, rb, off);
+    a.status[f] = st;
+}
+
+}  // namespace
+
+hipError_t launch_ref15_events(bool f64, const Ref15Args& a, hipStream_t stream) {
+    const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
+    if (f64) ref15_events_kernel<double><<<grid, kBlock, 0, stream>>>(a);
+    else ref15_events_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_ref15_reset(bool f64, const Ref15Args& a, hipStream_t stream) {
+    const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
+    if (f64) ref15_reset_kernel<double><<<grid, kBlock, 0, stream>>>(a);
+    else ref15_reset_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream) {
+    if (a.n_events > kMaxEvents) return hipErrorInvalidValue;
+    const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
+    if (f64) ref15_combo_kernel<double><<<grid, kBlock, 0, stream>>>(a);
+    else ref15_combo_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    return hipGetLastError();
+}
+
+}  // namespace kfmi

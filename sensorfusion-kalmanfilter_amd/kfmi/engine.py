@@ -16,9 +16,10 @@ from . import _lib
 from ._lib import KFError, check
 
 MODELS = {
-    # name: (model id, axes d); n = 2d, m = d, c = d
-    'cv2': (_lib.KF_MODEL_CV2, 2),   # 4-state/2-meas, hw5_2.py:219-304 restricted to [x,y,vx,vy]
-    'cv3': (_lib.KF_MODEL_CV3, 3),   # 6-state/3-meas, kf_workers.py:493-614 restricted to pos/vel
+    # name: (model id, n, m, c, covariance rows)
+    'cv2': (_lib.KF_MODEL_CV2, 4, 2, 2, 10),    # 4-state/2-meas, hw5_2.py:219-304 restricted to [x,y,vx,vy]
+    'cv3': (_lib.KF_MODEL_CV3, 6, 3, 3, 21),    # 6-state/3-meas, kf_workers.py:493-614 restricted to pos/vel
+    'ref15': (_lib.KF_MODEL_REF15, 15, 3, 0, 27),  # the reference's 15-state model; P block-packed
 }
 DTYPES = {'f32': (_lib.KF_F32, torch.float32, np.float32), 'f64': (_lib.KF_F64, torch.float64, np.float64)}
 
@@ -57,17 +58,20 @@ class BatchedKF:
         if self.batch < 0:
             raise ValueError('batch must be >= 0')
         self.device = torch.device('cuda', device)
-        self.axes = MODELS[model][1]
-        self.n, self.m, self.c = 2 * self.axes, self.axes, self.axes
-        self.ntri = self.n * (self.n + 1) // 2
+        _, self.n, self.m, self.c, self.ntri = MODELS[model]
         self.torch_dtype = DTYPES[dtype][1]
         L = _lib.lib()
         check(L.kf_init(device))
         torch.cuda.set_device(self.device)
-        self.params = params if params is not None else default_params(model)
+        if model == 'ref15':
+            if params is not None:
+                raise ValueError('ref15 uses the reference constants; params must be None')
+            self.params = None
+        else:
+            self.params = params if params is not None else default_params(model)
         h = ctypes.c_void_p()
         check(L.kf_alloc(ctypes.byref(h), MODELS[model][0], self.batch, DTYPES[dtype][0],
-                         ctypes.byref(self.params)))
+                         ctypes.byref(self.params) if self.params is not None else None))
         self._h = h
 
     # -- lifecycle ---------------------------------------------------------------------
@@ -186,6 +190,48 @@ class BatchedKF:
         check(_lib.lib().kf_run(self.handle, T, float(dt or 0.0), _ptr(dts), _ptr(ud), _ptr(zd),
                                 _ptr(md), int(update_every), _ptr(tr), _ptr(ld), self._stream()))
         return tr, ld
+
+    # -- reference 15-state model: per-filter event streams -------------------------------
+    def run_events(self, etype, dt, payload, traj=True, logdet=True, updated=False, threshold=None):
+        """KF_MODEL_REF15: T events per filter in one launch (kf_run_events).
+
+        etype [T, B] uint8 (KF_EVENT_*), dt [T, B] float64, payload [T, 9, B] (GPS: e, n, alt;
+        IMU: roll, pitch, yaw, wx, wy, wz, ax, ay, az).  threshold: adaptive-threshold gating
+        (update only if logdet(P_pred) > threshold).  Returns (traj [T, 6, B], logdet [T, B],
+        updated [T, B]) with None for outputs not asked for."""
+        if self.model != 'ref15':
+            raise ValueError('run_events needs a ref15 handle')
+        T = int(etype.shape[0])
+        et = self._dev(etype, (T, self.batch), 'etype', torch.uint8)
+        dtd = self._dev(dt, (T, self.batch), 'dt', torch.float64)
+        pay = self._dev(payload, (T, 9, self.batch), 'payload')
+        tr = self.empty(T, 6, self.batch) if traj else None
+        ld = self.empty(T, self.batch) if logdet else None
+        up = torch.empty(T, self.batch, dtype=torch.uint8, device=self.device) if updated else None
+        gate = threshold is not None
+        check(_lib.lib().kf_run_events(self.handle, T, _ptr(et), _ptr(dtd), _ptr(pay), _ptr(tr), _ptr(ld),
+                                       _ptr(up), int(gate), float(threshold) if gate else 0.0, self._stream()))
+        return tr, ld, up
+
+    def eval_combos(self, events, init, prev_time, target_end, k, combo_offset=0, logdets=True):
+        """KF_MODEL_REF15 brute force (kf_eval_combos): filter f evaluates combination
+        combo_offset + f of k out of the n candidate events.  events: host [n, 11] float64
+        (t, type, payload[9]); init: host [42] float64 (x[15], block-packed P[27]).
+        Returns (max_logdet [B], logdets [k+2, B] or None, n_records [B] int32)."""
+        if self.model != 'ref15':
+            raise ValueError('eval_combos needs a ref15 handle')
+        ev = np.ascontiguousarray(events, dtype=np.float64)
+        ini = np.ascontiguousarray(init, dtype=np.float64)
+        if ev.ndim != 2 or ev.shape[1] != 11 or ini.shape != (42,):
+            raise ValueError('events must be [n, 11] and init [42]')
+        mx = self.empty(self.batch)
+        ld = self.empty(k + 2, self.batch) if logdets else None
+        nr = torch.empty(self.batch, dtype=torch.int32, device=self.device)
+        check(_lib.lib().kf_eval_combos(self.handle, ev.shape[0], ev.ctypes.data_as(ctypes.c_void_p),
+                                        ini.ctypes.data_as(ctypes.c_void_p), float(prev_time), float(target_end),
+                                        int(k), int(combo_offset), _ptr(ld), _ptr(mx), _ptr(nr), self._stream()))
+        torch.cuda.current_stream(self.device).synchronize()  # host arrays were staged; keep them alive
+        return mx, ld, nr
 
     # -- synthetic streams (SURVEY.md §8d) -----------------------------------------------
     def synth(self, T, dt, update_every=1, seed=20251015, filter_offset=0):

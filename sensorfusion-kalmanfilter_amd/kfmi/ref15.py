@@ -1,0 +1,318 @@
+"""The reference's 15-state GPS+IMU drivers on the engine (KF_MODEL_REF15).
+
+Same names, arguments and return layouts as the reference's methods on KF_SensorFusion, with
+the event list (``indexed_sensor_data``, built by combine_sensor_data, kf_workers.py:375-385:
+``[(idx, 'GPS'|'IMU', t, payload), ...]``) passed explicitly:
+
+    run_kalman_filter_full                               kf_workers.py:623-728
+    run_adaptive_threshold_kalman_filter                 kf_workers.py:959-1058
+    evaluate_combo_chunk (evaluate_combo_chunk_worker)   kf_workers.py:22-97
+    run_brute_force_kalman_filter_no_sampling_min_usage  kf_workers.py:1218-1392
+
+Host code here only selects events and differences their time stamps in fp64 with the
+reference's rules (first-GPS start, negative-dt skips); every predict/update/logdet runs in the
+HIP kernels (kf_run_events, kf_eval_combos).  Covariances cross the boundary as 15x15 NumPy
+arrays (the reference's format) and are stored block-packed on the GPU: they must be
+block-diagonal over the axis chains (pos,vel,acc) and (att,rate), which every covariance the
+reference itself produces is, exactly (see csrc/kf_ref15.hip).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from .engine import BatchedKF
+
+GPS, IMU, PREDICT, NONE = _lib.KF_EVENT_GPS, _lib.KF_EVENT_IMU, _lib.KF_EVENT_PREDICT, _lib.KF_EVENT_NONE
+
+# block-packed row r -> (i, j) in the 15x15 covariance
+_PVA = [(0, 6, 12), (1, 7, 13), (2, 8, 14)]   # (pos, vel, acc) per axis
+_AW = [(3, 9), (4, 10), (5, 11)]              # (att, rate) per axis
+_ROWS = []
+for _blk in _PVA:
+    for _a in range(3):
+        for _b in range(_a, 3):
+            _ROWS.append((_blk[_a], _blk[_b]))
+for _blk in _AW:
+    for _a in range(2):
+        for _b in range(_a, 2):
+            _ROWS.append((_blk[_a], _blk[_b]))
+_BLOCK_MASK = np.zeros((15, 15), bool)
+for _i, _j in _ROWS:
+    _BLOCK_MASK[_i, _j] = _BLOCK_MASK[_j, _i] = True
+
+# reference P0 (kf_workers.py:651)
+P0 = np.diag([10000.0] * 3 + [1000.0] * 3 + [1000.0] * 3 + [1000.0] * 3 + [10000.0] * 3)
+
+
+def to_blocks(P):
+    """15x15 (or [..., 15, 15]) covariance -> block-packed [..., 27]; raises ValueError if it
+    couples different axis chains (the engine stores only the chain blocks)."""
+    P = np.asarray(P, dtype=np.float64)
+    off = np.abs(P[..., ~_BLOCK_MASK])
+    if off.size and off.max() > 0.0:
+        raise ValueError(f'covariance couples different axis chains (max |off-block| = {off.max():g}); '
+                         'KF_MODEL_REF15 stores the (pos,vel,acc)/(att,rate) blocks only')
+    return np.stack([P[..., i, j] for i, j in _ROWS], axis=-1)
+
+
+def from_blocks(b):
+    """block-packed [..., 27] -> 15x15 symmetric."""
+    b = np.asarray(b, dtype=np.float64)
+    P = np.zeros(b.shape[:-1] + (15, 15))
+    for r, (i, j) in enumerate(_ROWS):
+        P[..., i, j] = b[..., r]
+        P[..., j, i] = b[..., r]
+    return P
+
+
+def event_payload(stype, sdata):
+    """The 9 payload values of one reference event (kf_workers.py:331, 367)."""
+    if stype == 'GPS':
+        return [sdata['easting'], sdata['northing'], sdata['altitude'], 0, 0, 0, 0, 0, 0]
+    return [float(v) for v in sdata[1:10]]
+
+
+def _run_streams(streams, x0, P0b, dtype='f64', device=0, threshold=None):
+    """Run one event list per filter in ONE kf_run_events launch.
+
+    streams: list (per filter) of [(type, dt, payload9)]; each stream is preceded by a NONE
+    event so row 0 of the outputs holds the initial state and logdet.  x0 [B, 15] and P0b
+    [B, 27] are the initial states.  Returns traj [T, 6, B], logdet [T, B], updated [T, B],
+    x [15, B], P blocks [27, B], status [B] as NumPy arrays."""
+    B = len(streams)
+    T = 1 + max((len(s) for s in streams), default=0)
+    etype = np.full((T, B), NONE, np.uint8)
+    dt = np.zeros((T, B))
+    pay = np.zeros((T, 9, B))
+    for f, s in enumerate(streams):
+        for t, (ty, d, p) in enumerate(s, start=1):
+            etype[t, f] = ty
+            dt[t, f] = d
+            pay[t, :, f] = p
+    kf = BatchedKF('ref15', B, dtype, device=device)
+    npd = np.float64 if dtype == 'f64' else np.float32
+    kf.set_state(np.ascontiguousarray(np.asarray(x0, np.float64).T.astype(npd)),
+                 np.ascontiguousarray(np.asarray(P0b, np.float64).T.astype(npd)))
+    tr, ld, up = kf.run_events(etype, dt, pay.astype(npd), updated=True, threshold=threshold)
+    x, Pb = kf.state()
+    st = kf.status()
+    torch.cuda.synchronize(kf.device)
+    out = (tr.double().cpu().numpy(), ld.double().cpu().numpy(), up.cpu().numpy(), x.double().cpu().numpy(),
+           Pb.double().cpu().numpy(), st.cpu().numpy())
+    kf.close()
+    return out
+
+
+def _window(events, start_idx, end_idx):
+    if start_idx is None or start_idx < 0:
+        start_idx = 0
+    if end_idx is None or end_idx > len(events):
+        end_idx = len(events)
+    return start_idx, end_idx
+
+
+def _cold_start(events, start_idx, stop):
+    """First GPS fix in events[start_idx:stop]: (x0, t0, absolute index) or None
+    (kf_workers.py:655-666)."""
+    for i, (_, stype, t, sdata) in enumerate(events[start_idx:stop]):
+        if stype == 'GPS':
+            x = np.zeros(15)
+            x[0], x[1], x[2] = sdata['easting'], sdata['northing'], sdata['altitude']
+            return x, t, start_idx + i
+    return None
+
+
+def run_kalman_filter_full(events, start_idx=None, end_idx=None, initial_pt=None, initial_state=None,
+                           print_output=False, dtype='f64', device=0):
+    """kf_workers.py:623-728 on the GPU: returns (states, logdets, P, prev_time) in the
+    reference's layout (states = [(t, x, y, z, roll, pitch, yaw), ...])."""
+    if not events:
+        return [], [], []
+    start_idx, end_idx = _window(events, start_idx, end_idx)
+    x0 = np.zeros(15)
+    if initial_pt is not None and initial_state is not None:
+        P = np.asarray(initial_pt, np.float64)
+        x0[0:6] = initial_state[1:7]
+        prev = initial_state[0]
+        start_off = start_idx
+    else:
+        P = P0
+        cs = _cold_start(events, start_idx, end_idx + 1)
+        if cs is None:
+            return [], [], []
+        x0, prev, start_off = cs
+    stream, times = [], []
+    for (_, stype, t, sdata) in events[start_off:end_idx]:
+        dt = t - prev
+        if dt < 0:  # kf_workers.py:683-685
+            prev = t
+            continue
+        stream.append((GPS if stype == 'GPS' else IMU, dt, event_payload(stype, sdata)))
+        times.append(t)
+        prev = t
+    tr, ld, _, x, Pb, st = _run_streams([stream], x0[None], to_blocks(P)[None], dtype, device)
+    states = [(initial_state[0] if (initial_pt is not None and initial_state is not None) else
+               events[start_off][2], *tr[0, :, 0])]
+    states += [(t, *tr[i + 1, :, 0]) for i, t in enumerate(times)]
+    logdets = [float(v) for v in ld[:len(times) + 1, 0]]
+    if print_output:
+        print(f'Full Kalman Filter (GPU): processed {len(times)} measurements from index {start_off} to {end_idx}')
+    return states, logdets, from_blocks(Pb[:, 0]), prev
+
+
+def run_adaptive_threshold_kalman_filter(events, start_idx=None, end_idx=None, R_threshold=None,
+                                         initial_pt=None, initial_state=None, print_output=False,
+                                         dtype='f64', device=0):
+    """kf_workers.py:959-1058 on the GPU: the update is applied only when logdet(P_pred) >
+    R_threshold.  Returns (states, logdets, P, previous_time, measurement_times)."""
+    start_idx, end_idx = _window(events, start_idx, end_idx)
+    if R_threshold is None:
+        R_threshold = -float('inf')
+    x0 = np.zeros(15)
+    mtimes = []
+    if initial_pt is not None and initial_state is not None:
+        P = np.asarray(initial_pt, np.float64)
+        x0[0:6] = initial_state[1:7]
+        prev = initial_state[0]
+        start_off = start_idx
+    else:
+        P = P0
+        cs = _cold_start(events, start_idx, end_idx)
+        if cs is None:
+            return None
+        x0, prev, start_off = cs
+        mtimes.append(prev)
+    t_first = prev
+    stream, times = [], []
+    for (_, stype, t, sdata) in events[start_off:end_idx]:
+        dt = t - prev
+        if dt < 0:
+            # kf_workers.py:1013-1015 assigns an unused name, so previous_time is NOT advanced
+            continue
+        stream.append((GPS if stype == 'GPS' else IMU, dt, event_payload(stype, sdata)))
+        times.append(t)
+        prev = t
+    tr, ld, up, x, Pb, st = _run_streams([stream], x0[None], to_blocks(P)[None], dtype, device,
+                                         threshold=float(R_threshold))
+    states = [(t_first, *tr[0, :, 0])] + [(t, *tr[i + 1, :, 0]) for i, t in enumerate(times)]
+    logdets = [float(v) for v in ld[:len(times) + 1, 0]]
+    mtimes += [t for i, t in enumerate(times) if up[i + 1, 0]]
+    if print_output:
+        print(f'Adaptive Kalman Filter (GPU): processed {len(times)} events from index {start_off} to {end_idx}')
+    return states, logdets, from_blocks(Pb[:, 0]), prev, mtimes
+
+
+def _combo_stream(combo, prev_time, target_end):
+    """Event stream of one combination with the worker's rules (kf_workers.py:36-82)."""
+    s, times = [], []
+    cur = prev_time
+    for (_, stype, t, sdata) in combo:
+        dt = t - cur
+        if dt < 0:
+            continue
+        s.append((GPS if stype == 'GPS' else IMU, dt, event_payload(stype, sdata)))
+        times.append(t)
+        cur = t
+    if cur < target_end - 1e-8:
+        s.append((PREDICT, target_end - cur, [0.0] * 9))
+        times.append(target_end)
+    return s, times
+
+
+def evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time, dtype='f64', device=0):
+    """evaluate_combo_chunk_worker (kf_workers.py:22-97) for a whole chunk in ONE launch, one
+    filter per combination.  Returns [(0, traj, combo, x_final, None, log_det, k), ...]."""
+    if not chunk:
+        return []
+    built = [_combo_stream(c, prev_time, target_end_time) for c in chunk]
+    B = len(chunk)
+    tr, ld, _, x, Pb, st = _run_streams([b[0] for b in built], np.broadcast_to(np.asarray(xt, np.float64), (B, 15)),
+                                        np.broadcast_to(to_blocks(Pt), (B, 27)), dtype, device)
+    results = []
+    for f, (combo, (s, times)) in enumerate(zip(chunk, built)):
+        if st[f] != 0:  # the worker skips a combination that raised (kf_workers.py:88-91)
+            continue
+        n = len(times)
+        traj = [(prev_time, *tr[0, :, f])] + [(t, *tr[i + 1, :, f]) for i, t in enumerate(times)]
+        results.append((0, traj, combo, x[:, f].copy(), None, [float(v) for v in ld[:n + 1, f]], len(combo)))
+    return results
+
+
+def unrank_combination(n, k, r):
+    """The r-th k-subset of range(n) in itertools.combinations order."""
+    out, a = [], 0
+    for j in range(k):
+        while True:
+            c = math.comb(n - a - 1, k - j - 1)
+            if r < c:
+                break
+            r -= c
+            a += 1
+        out.append(a)
+        a += 1
+    return out
+
+
+def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end_idx=None, R_threshold=None,
+                                                       initial_pt=None, initial_state=None,
+                                                       max_combos_in_memory=1 << 22, dtype='f64', device=0):
+    """kf_workers.py:1218-1392 on the GPU: for k = 1..n, evaluate every k-subset of the candidate
+    events (kf_eval_combos, one filter per subset, up to ``max_combos_in_memory`` per launch) and
+    return the first subset, in itertools.combinations order, whose max log-determinant is below
+    R_threshold — the reference's result dict — or None."""
+    if R_threshold is None:
+        raise ValueError('R_threshold must be specified for brute force KF.')
+    if start_idx is None or start_idx < 0:
+        start_idx = 0
+    if end_idx is None or end_idx > len(events):
+        end_idx = len(events)
+    xt = np.zeros(15)
+    if initial_pt is not None and initial_state is not None:
+        Pt = np.asarray(initial_pt, np.float64)
+        xt[0:6] = initial_state[1:7]
+        prev_time = initial_state[0]
+        cand = list(events[start_idx:end_idx])
+    else:
+        Pt = P0
+        cand, prev_time, started = [], None, False
+        for (idx, stype, t, sdata) in events[start_idx:end_idx + 1]:  # the reference's +1 slice
+            if not started and stype == 'GPS':
+                xt[0], xt[1], xt[2] = sdata['easting'], sdata['northing'], sdata['altitude']
+                started, prev_time = True, t
+            if started:
+                cand.append((idx, stype, t, sdata))
+        if not cand:
+            return None
+    target_end = events[end_idx - 1][2]
+    n = len(cand)
+    if n > 64:
+        raise ValueError(f'{n} candidate events: the GPU search supports at most 64 (2^64 subsets)')
+    ev = np.zeros((n, 11))
+    for i, (_, stype, t, sdata) in enumerate(cand):
+        ev[i, 0] = t
+        ev[i, 1] = GPS if stype == 'GPS' else IMU
+        ev[i, 2:] = event_payload(stype, sdata)
+    init = np.concatenate([xt, to_blocks(Pt)])
+    width = int(min(max_combos_in_memory, max(math.comb(n, k) for k in range(1, n + 1))))
+    kf = BatchedKF('ref15', width, dtype, device=device)
+    try:
+        for k in range(1, n + 1):
+            total = math.comb(n, k)
+            for off in range(0, total, width):
+                mx, _, _ = kf.eval_combos(ev, init, prev_time, target_end, k, combo_offset=off, logdets=False)
+                ok = mx < R_threshold
+                if bool(ok.any()):
+                    r = off + int(torch.argmax(ok.to(torch.int8)).item())
+                    combo = tuple(cand[i] for i in unrank_combination(n, k, r))
+                    res = evaluate_combo_chunk([combo], xt, Pt, prev_time, target_end, dtype, device)[0]
+                    metric, traj, combo, x_bf, P_bf, log_det, used = res
+                    return {'selected_sensors': combo, 'final_state': x_bf, 'final_covariance': P_bf,
+                            'trajectory': traj, 'accuracy_metric': metric, 'log_determinants': log_det,
+                            'num_measurements_used': used}
+    finally:
+        kf.close()
+    return None

@@ -14,6 +14,7 @@ Fixtures written (inputs and the reference's outputs, nothing else):
   ref15_full.npz    run_kalman_filter_full (kf_workers.py:623-728), cold start + warm
                     start window, plus run_adaptive_threshold_kalman_filter (959-1058)
   ref15_combos.npz  evaluate_combo_chunk_worker (kf_workers.py:22-97) on k=1..3 subsets
+  ref15_bruteforce.npz  run_brute_force_kalman_filter_no_sampling_min_usage (1218-1392)
   ref8_full.npz     hw5_2.run_kalman_filter (hw5_2.py:313-380)
   cv_batch.npz      4/2 and 6/3 constant-velocity filters stepped with the reference's
                     own predict_covariance (kf_workers.py:546-549) and
@@ -24,7 +25,12 @@ import sys
 import types
 from itertools import combinations
 
-import numpy as np
+# the reference's brute force forks a multiprocessing.Pool(30): keep BLAS single-threaded so
+# forked children cannot inherit a locked BLAS thread pool
+for _v in ('OPENBLAS_NUM_THREADS', 'OMP_NUM_THREADS', 'MKL_NUM_THREADS'):
+    os.environ[_v] = '1'
+
+import numpy as np  # noqa: E402
 
 REF = '/root/reference'
 OUT = os.path.dirname(os.path.abspath(__file__))
@@ -173,6 +179,41 @@ def ref15_combos(kfw):
     print('ref15_combos:', len(chunk), 'combos')
 
 
+def ref15_bruteforce(kfw):
+    """run_brute_force_kalman_filter_no_sampling_min_usage (kf_workers.py:1218-1392) on a small
+    warm-started window; R_threshold placed between the best k=1 and best k=2 subsets so the
+    answer needs two measurements."""
+    from itertools import combinations as comb
+    events = synth_events(seed=15, seconds=0.4, out_of_order=False)
+    sf = kfw.KF_SensorFusion('gps.csv', 'imu.csv')
+    sf.indexed_sensor_data = events
+    st, ld, P, prev = sf.run_kalman_filter_full(start_idx=0, end_idx=30)
+    start, end = 30, 38
+    cand = events[start:end]
+    xt = np.zeros(15)
+    xt[0:6] = st[-1][1:7]
+    class_args = {name: getattr(sf, name) for name in (
+        'get_state_transition_matrix', 'get_process_noise_covariance_matrix', 'predict_covariance',
+        'get_gps_observation_matrix', 'get_gps_measurement_noise_covariance_matrix',
+        'get_imu_observation_matrix', 'get_imu_measurement_noise_covariance_matrix', 'calculate_kalman_gain')}
+    best = {}
+    for k in (1, 2):
+        res = kfw.evaluate_combo_chunk_worker(list(comb(cand, k)), xt, P, class_args, st[-1][0], events[end - 1][2])
+        best[k] = min(max(r[5]) for r in res)
+    assert best[2] < best[1], best
+    thr = 0.5 * (best[1] + best[2])
+    out = sf.run_brute_force_kalman_filter_no_sampling_min_usage(
+        start_idx=start, end_idx=end, R_threshold=thr, initial_pt=P, initial_state=st[-1])
+    assert out is not None and out['num_measurements_used'] == 2
+    sel = [cand.index(e) for e in out['selected_sensors']]
+    o = pack_events(events)
+    o.update(start=np.array(start), end=np.array(end), init_P=np.array(P), init_state=np.array(st[-1]),
+             threshold=np.array(thr), selected=np.array(sel), final_state=np.array(out['final_state']),
+             log_determinants=np.array(out['log_determinants']), trajectory=np.array(out['trajectory']))
+    np.savez_compressed(os.path.join(OUT, 'ref15_bruteforce.npz'), **o)
+    print('ref15_bruteforce: selected', sel, 'threshold', thr)
+
+
 def ref8_full(h5):
     events = synth_events(seed=13, seconds=1.5, out_of_order=False)
     sf = h5.KF_SensorFusion('gps.csv', 'imu.csv')
@@ -244,6 +285,7 @@ if __name__ == '__main__':
     kfw, h5 = import_reference()
     ref15_full(kfw)
     ref15_combos(kfw)
+    ref15_bruteforce(kfw)
     ref8_full(h5)
     cv_batch(kfw)
     # analytic known answer: slogdet(P0) of kf_workers.py:651 = 6 ln 1e4 + 9 ln 1e3

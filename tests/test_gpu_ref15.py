@@ -1,0 +1,179 @@
+"""The reference's 15-state model on the GPU (KF_MODEL_REF15) vs the reference's own outputs
+(tests/golden/ref15_*.npz) and the CPU oracle — needs an MI355X.
+
+Tolerance (north_star): 1e-6 relative for fp64 (states normalised by max(|x|, 1), logdets by
+max(|logdet|, 1)); the engine uses the Joseph form and LDL^T solves where the reference uses
+(I-KH)P and np.linalg.inv, so agreement is ~1e-10, not bitwise.
+"""
+import math
+import os
+from itertools import combinations
+
+import numpy as np
+import pytest
+import torch
+
+import kfmi
+from golden_events import unpack_events
+from kfmi import ref15
+from oracle import ref_kf
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+
+
+def _rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1.0))) if a.size else 0.0
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def test_run_kalman_filter_full_cold(golden_dir):
+    g = _load(golden_dir, 'ref15_full.npz')
+    events = unpack_events(g)
+    st, ld, P, prev = ref15.run_kalman_filter_full(events, 0, len(events))
+    assert np.array(st).shape == g['cold_states'].shape
+    assert _rel(st, g['cold_states']) <= TOL
+    assert _rel(ld, g['cold_logdets']) <= TOL
+    assert _rel(P, g['cold_P']) <= TOL
+    assert prev == float(g['cold_prev_time'])
+
+
+def test_run_kalman_filter_full_warm(golden_dir):
+    g = _load(golden_dir, 'ref15_full.npz')
+    events = unpack_events(g)
+    s0 = int(g['warm_start'])
+    st, ld, P, _ = ref15.run_kalman_filter_full(events, s0, s0 + 60, initial_pt=g['warm_init_P'],
+                                                initial_state=tuple(g['warm_init_state']))
+    assert _rel(st, g['warm_states']) <= TOL
+    assert _rel(ld, g['warm_logdets']) <= TOL
+    assert _rel(P, g['warm_P']) <= TOL
+
+
+def test_adaptive_threshold(golden_dir):
+    g = _load(golden_dir, 'ref15_full.npz')
+    events = unpack_events(g)
+    st, ld, P, prev, times = ref15.run_adaptive_threshold_kalman_filter(
+        events, 0, len(events), R_threshold=float(g['adapt_threshold']))
+    np.testing.assert_array_equal(np.array(times), g['adapt_times'])
+    assert _rel(st, g['adapt_states']) <= TOL
+    assert _rel(ld, g['adapt_logdets']) <= TOL
+    assert _rel(P, g['adapt_P']) <= TOL
+
+
+def test_combo_chunk_worker(golden_dir):
+    g = _load(golden_dir, 'ref15_combos.npz')
+    cand = unpack_events(g)
+    chunk = [tuple(cand[i] for i in row if i >= 0) for row in g['combo_idx']]
+    res = ref15.evaluate_combo_chunk(chunk, g['x0'], g['P0'], float(g['prev_time']), float(g['target_end']))
+    assert len(res) == len(chunk)
+    assert [len(r[5]) for r in res] == list(np.diff(g['offsets']))
+    assert _rel([v for r in res for v in r[5]], g['logdet_flat']) <= TOL
+    assert _rel([v for r in res for v in r[1]], g['traj_flat']) <= TOL
+    assert _rel([r[3] for r in res], g['x_final']) <= TOL
+    assert all(r[0] == 0 and r[4] is None and r[6] == len(r[2]) for r in res)
+
+
+def test_brute_force_search(golden_dir):
+    g = _load(golden_dir, 'ref15_bruteforce.npz')
+    events = unpack_events(g)
+    s, e = int(g['start']), int(g['end'])
+    out = ref15.run_brute_force_kalman_filter_no_sampling_min_usage(
+        events, s, e, R_threshold=float(g['threshold']), initial_pt=g['init_P'],
+        initial_state=tuple(g['init_state']))
+    cand = events[s:e]
+    assert [cand.index(ev) for ev in out['selected_sensors']] == list(g['selected'])
+    assert out['num_measurements_used'] == len(g['selected'])
+    assert _rel(out['log_determinants'], g['log_determinants']) <= TOL
+    assert _rel(out['final_state'], g['final_state']) <= TOL
+    assert _rel(out['trajectory'], g['trajectory']) <= TOL
+    # a threshold no subset meets -> None (kf_workers.py:1391-1392)
+    assert ref15.run_brute_force_kalman_filter_no_sampling_min_usage(
+        events, s, e, R_threshold=-1e9, initial_pt=g['init_P'], initial_state=tuple(g['init_state'])) is None
+
+
+@pytest.mark.parametrize('n,k', [(10, 1), (10, 4), (12, 6)])
+def test_eval_combos_kernel_vs_oracle(golden_dir, n, k):
+    """Every k-subset of n candidates, unranked in-kernel, against the oracle's worker: record
+    lists, max logdet and final state per subset (itertools.combinations order)."""
+    g = _load(golden_dir, 'ref15_full.npz')
+    events = unpack_events(g)
+    s0 = 100
+    st, ld, P, prev = ref_kf.run_kalman_filter_full(events, 0, s0)
+    cand = events[s0:s0 + n]
+    xt = np.zeros(15)
+    xt[0:6] = st[-1][1:7]
+    target = events[s0 + n - 1][2]
+    ev = np.array([[t, 0 if s == 'GPS' else 1, *ref15.event_payload(s, d)] for (_, s, t, d) in cand])
+    init = np.concatenate([xt, ref15.to_blocks(P)])
+    total = math.comb(n, k)
+    kf = kfmi.BatchedKF('ref15', total + 37, 'f64')  # a ragged tail of padding lanes
+    mx, lds, nrec = kf.eval_combos(ev, init, st[-1][0], target, k)
+    x, _ = kf.state()
+    mx, lds, nrec, x = mx.cpu().numpy(), lds.cpu().numpy(), nrec.cpu().numpy(), x.cpu().numpy()
+    st_lane = kf.status().cpu().numpy()
+    assert (st_lane[:total] == 0).all() and (st_lane[total:] == 1).all()
+    assert np.isnan(mx[total:]).all()
+    ref = ref_kf.evaluate_combo_chunk(list(combinations(cand, k)), xt, P, st[-1][0], target)
+    for f, r in enumerate(ref):
+        assert nrec[f] == len(r[5])
+        assert _rel(lds[:nrec[f], f], r[5]) <= TOL
+        assert np.isnan(lds[nrec[f]:, f]).all()
+        assert abs(mx[f] - max(r[5])) <= TOL * max(abs(max(r[5])), 1.0)
+        assert _rel(x[:, f], r[3]) <= TOL
+
+
+def test_run_events_random_batch_vs_oracle():
+    """B independent filters on their own random GPS/IMU/predict-only/padding streams (ragged,
+    irregular dt) against the oracle's dense 15x15 reference-order step."""
+    rng = np.random.default_rng(7)
+    B, T = 300, 40
+    etype = rng.choice([0, 1, 1, 1, 2], size=(T, B)).astype(np.uint8)
+    etype[30:, ::3] = 255                          # ragged ends
+    dt = rng.uniform(0.0, 0.12, (T, B))
+    pay = np.zeros((T, 9, B))
+    pay[:, 0:3] = rng.normal(0, 20, (T, 3, B))    # GPS e, n, alt (and IMU angles for IMU)
+    pay[:, 3:6] = rng.normal(0, 0.05, (T, 3, B))
+    pay[:, 6:9] = rng.normal(0, 0.5, (T, 3, B))
+    x0 = np.zeros((B, 15))
+    x0[:, :3] = rng.normal(0, 20, (B, 3))
+    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    kf.reset(torch.from_numpy(np.ascontiguousarray(x0.T)).cuda())
+    tr, ld, up = kf.run_events(etype, dt, pay, updated=True)
+    tr, ld, up = tr.cpu().numpy(), ld.cpu().numpy(), up.cpu().numpy()
+    x, Pb = kf.state()
+    x, Pb = x.cpu().numpy(), Pb.cpu().numpy()
+    assert (kf.status().cpu().numpy() == 0).all()
+    for f in range(0, B, 7):
+        xf, Pf = x0[f].copy(), ref_kf.P0_REF15.copy()
+        for t in range(T):
+            ty = etype[t, f]
+            if ty == 255:
+                pass
+            elif ty == 2:
+                F = ref_kf.F_ref15(dt[t, f])
+                xf = F @ xf
+                Pf = ref_kf.predict_covariance(Pf, F, ref_kf.Q_ref15(dt[t, f]))
+            else:
+                if ty == 0:
+                    sdata = {'easting': pay[t, 0, f], 'northing': pay[t, 1, f], 'altitude': pay[t, 2, f]}
+                else:
+                    sdata = ['t', *pay[t, :, f]]
+                xf, Pf = ref_kf.step15(xf, Pf, 'GPS' if ty == 0 else 'IMU', sdata, dt[t, f])
+            assert _rel(tr[t, :, f], xf[:6]) <= TOL, (f, t)
+            assert abs(ld[t, f] - np.linalg.slogdet(Pf)[1]) <= TOL * max(1.0, abs(np.linalg.slogdet(Pf)[1]))
+            assert up[t, f] == (1 if ty in (0, 1) else 0)
+        assert _rel(x[:, f], xf) <= TOL
+        assert _rel(ref15.from_blocks(Pb[:, f]), Pf) <= TOL
+
+
+def test_ref15_handle_rejects_cv_entry_points():
+    kf = kfmi.BatchedKF('ref15', 4, 'f64')
+    with pytest.raises(kfmi.KFError):
+        kf.predict(0.1)
+    with pytest.raises(ValueError):
+        kfmi.BatchedKF('cv3', 4, 'f64').run_events(np.zeros((1, 4), np.uint8), np.zeros((1, 4)), np.zeros((1, 9, 4)))

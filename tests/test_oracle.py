@@ -128,3 +128,15 @@ def test_batch_mask_skips_update():
                                               update_every=T + 1)
     np.testing.assert_allclose(tr[:, :, 2], tr_pred[:, :, 0], rtol=1e-14)
     np.testing.assert_allclose(ld[:, 2], ld_pred[:, 0], rtol=1e-14)
+
+
+def test_ref15_bruteforce_search(golden_dir):
+    g = _load(golden_dir, 'ref15_bruteforce.npz')
+    events = unpack_events(g)
+    s, e = int(g['start']), int(g['end'])
+    out = ref_kf.run_brute_force(events, s, e, float(g['threshold']), g['init_P'], tuple(g['init_state']))
+    cand = events[s:e]
+    assert [cand.index(ev) for ev in out['selected_sensors']] == list(g['selected'])
+    assert _rel(out['log_determinants'], g['log_determinants']) < RTOL
+    assert _rel(out['final_state'], g['final_state']) < RTOL
+    assert _rel(out['trajectory'], g['trajectory']) < RTOL

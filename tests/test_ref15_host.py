@@ -1,0 +1,53 @@
+"""Host-side logic of kfmi.ref15 (no GPU): block packing of the 15x15 covariance and the
+combination unranking used by the brute-force search."""
+import math
+from itertools import combinations
+
+import numpy as np
+import pytest
+
+from golden_events import unpack_events
+from kfmi import ref15
+
+
+def test_blocks_roundtrip_on_reference_covariances(golden_dir):
+    g = np.load(f'{golden_dir}/ref15_full.npz')
+    for key in ('cold_P', 'warm_P', 'adapt_P', 'warm_init_P'):
+        P = g[key]
+        # the reference's simple-form update leaves P asymmetric by ~1 ulp; packing keeps i <= j
+        Psym = np.triu(P) + np.triu(P, 1).T
+        np.testing.assert_array_equal(ref15.from_blocks(ref15.to_blocks(P)), Psym)
+        np.testing.assert_allclose(Psym, P, rtol=1e-14, atol=1e-17)
+    np.testing.assert_array_equal(ref15.from_blocks(ref15.to_blocks(ref15.P0)), ref15.P0)
+
+
+def test_blocks_reject_cross_chain_coupling():
+    P = ref15.P0.copy()
+    P[0, 1] = P[1, 0] = 1e-3   # pos_x <-> pos_y couples two chains
+    with pytest.raises(ValueError):
+        ref15.to_blocks(P)
+    P = ref15.P0.copy()
+    P[0, 6] = P[6, 0] = 5.0    # pos_x <-> vel_x is inside a chain: fine
+    assert ref15.to_blocks(P)[1] == 5.0
+
+
+@pytest.mark.parametrize('n,k', [(5, 1), (8, 3), (12, 6), (25, 12)])
+def test_unrank_matches_itertools(n, k):
+    total = math.comb(n, k)
+    ranks = list(range(min(total, 300))) + [total // 2, total - 1]
+    allc = None
+    if total <= 5000:
+        allc = list(combinations(range(n), k))
+    for r in ranks:
+        got = ref15.unrank_combination(n, k, r)
+        if allc is not None:
+            assert tuple(got) == allc[r]
+        assert sorted(got) == got and len(set(got)) == k and got[-1] < n
+
+
+def test_event_payload_layout(golden_dir):
+    events = unpack_events(np.load(f'{golden_dir}/ref15_full.npz'))
+    gps = next(e for e in events if e[1] == 'GPS')
+    imu = next(e for e in events if e[1] == 'IMU')
+    assert ref15.event_payload('GPS', gps[3])[:3] == [gps[3]['easting'], gps[3]['northing'], gps[3]['altitude']]
+    assert ref15.event_payload('IMU', imu[3]) == [float(v) for v in imu[3][1:10]]
