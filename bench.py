@@ -1,26 +1,29 @@
-"""Benchmark of the batched KF hot path (kf_run) on 1..N MI355X, one process per GPU.
+"""Benchmark of the batched KF hot path on 1..N MI355X, one process per GPU.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
     torchrun --nproc-per-node N bench.py --gpus N ...        (multi-GPU, RCCL)
 
-One bench *step* = one kf_run launch: every filter of this rank's shard advances T time
-steps (fused predict + GPS update, trajectory and logdet written to HBM) — one pass of the
-hot path over one batch of synthetic streams.  The streams are generated on the GPU by the
-counter-based Philox generator (kf_synth) and are resident in HBM before timing starts;
-consecutive bench steps continue the same filters (warm start, like the reference's
-windowed runs, kf_workers.py:2316-2323) over the same stream chunk.
+One bench *step* = one launch of the hot path over one batch of synthetic input that is
+resident in HBM before timing starts.  Consecutive steps continue the same filters (warm
+start, like the reference's windowed runs, kf_workers.py:2316-2323) over the same inputs.
 
 Configs (BASELINE.json / SURVEY.md §8d); per GPU (weak scaling: each rank owns B filters):
     2  cv2 (4-state/2-meas)  fp32  B=65,536     T=1024 dt=0.1  update every step
     3  cv3 (6-state/3-meas)  fp64  B=1,048,576  T=256  dt=0.1  update every step   [default]
     4  cv3 (6-state/3-meas)  fp32  B=1,048,576  T=256  dt=0.1  update every step   (x8 GPUs)
     5  cv3 (6-state/3-meas)  fp64  B=1,048,576  T=500  dt=0.01 GPS update every 10th step
+SURVEY.md §8f rows on the same engine (not BASELINE lines):
+    ref15  the reference's 15-state model, fp64, B=1,048,576 filters, T=256 events of a 200 Hz
+           IMU + 10 Hz GPS stream (kf_run_events)
+    bf     the reference's brute-force search: every k-subset (k = 1..25) of n = 25 candidate
+           events (kf_workers.py:2311), 2^25 - 1 filters (kf_eval_combos)
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import platform
 import sys
@@ -35,10 +38,12 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 CONFIGS = {
-    2: dict(model='cv2', dtype='f32', B=65536, T=1024, dt=0.1, k=1),
-    3: dict(model='cv3', dtype='f64', B=1048576, T=256, dt=0.1, k=1),
-    4: dict(model='cv3', dtype='f32', B=1048576, T=256, dt=0.1, k=1),
-    5: dict(model='cv3', dtype='f64', B=1048576, T=500, dt=0.01, k=10),
+    '2': dict(model='cv2', dtype='f32', B=65536, T=1024, dt=0.1, k=1),
+    '3': dict(model='cv3', dtype='f64', B=1048576, T=256, dt=0.1, k=1),
+    '4': dict(model='cv3', dtype='f32', B=1048576, T=256, dt=0.1, k=1),
+    '5': dict(model='cv3', dtype='f64', B=1048576, T=500, dt=0.01, k=10),
+    'ref15': dict(model='ref15', dtype='f64', B=1048576, T=256, dt=0.005, k=20),
+    'bf': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 SEED = 20251015
@@ -57,45 +62,206 @@ def algorithmic_bytes(cfg):
     return per_filter * B, per_filter / T
 
 
-def cpu_baseline(cfg, x0, u, z, budget_s=12.0):
-    """The reference CPU loop (oracle/ref_kf.run_filter_loop: one filter at a time, NumPy in
-    the reference's op order, kf_workers.py:688-717) on this host, 1 core, over as many of
-    this workload's filters as fit in ``budget_s``."""
-    from oracle import ref_kf
-    model = ref_kf.CV2 if cfg['model'] == 'cv2' else ref_kf.CV3
-    T, k = cfg['T'], cfg['k']
-    dt = np.full(T, cfg['dt'])
-    nf = min(4096, cfg['B'])
-    idx = torch.linspace(0, cfg['B'] - 1, nf).long().to(u.device)
-    xs = x0[:, idx].double().cpu().numpy().T
-    us = u[:, :, idx].double().cpu().numpy()
-    zs = z[:, :, idx].double().cpu().numpy()
-    steps = 0
-    done = 0
-    t0 = time.perf_counter()
-    while done < nf and time.perf_counter() - t0 < budget_s:
-        ref_kf.run_filter_loop(model, xs[done], model.P0(), dt, us[:, :, done], zs[:, :, done], k)
-        steps += T
-        done += 1
-    el = time.perf_counter() - t0
-    return {'value': steps / el, 'unit': 'KF steps/s', 'cores': 1, 'kind': 'port',
-            'sample': f'{done} filters x {T} steps of this workload (same synthetic streams), '
-                      f'oracle/ref_kf.run_filter_loop, NumPy {np.__version__}, 1 thread, '
-                      f'{platform.processor() or platform.machine()}',
-            'seconds': round(el, 2)}
-
-
-def load_traffic(cfg_id, n_gpus):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py),
-    if one exists for this config."""
-    path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+def host_cpu():
     try:
-        with open(path) as f:
-            data = json.load(f)
-        rec = data.get(f'config{cfg_id}')
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def load_traffic(cfg_id):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
+    try:
+        with open(os.path.join(ROOT, 'profiles', 'pmc_traffic.json')) as f:
+            rec = json.load(f).get(f'config{cfg_id}')
         return rec['bytes_per_launch'] if rec else None
     except (OSError, ValueError, KeyError):
         return None
+
+
+# --------------------------------------------------------------------------------------------
+# Workloads: each returns dict(step, units, bytes, kernel, cpu, gather, desc, extra, ...)
+# --------------------------------------------------------------------------------------------
+
+def cv_workload(cfg_id, cfg, args, rank, world, dev):
+    import kfmi
+    from kfmi import dist as kdist
+    B, T, k, dt = cfg['B'], cfg['T'], cfg['k'], cfg['dt']
+    kf = kfmi.BatchedKF(cfg['model'], B, cfg['dtype'], device=dev.index)
+    # weak scaling: world*B filters in total; shard r owns a contiguous slice and regenerates
+    # its own streams from the counter-based generator (keyed by the global filter index)
+    offset, count = kdist.shard_range(world * B, rank, world)
+    assert count == B
+    x0, u, z = kf.synth(T=T, dt=dt, update_every=k, seed=SEED, filter_offset=offset)
+    kf.reset(x0)
+    traj = kf.empty(T, kf.n, B)
+    logdet = kf.empty(T, B)
+    out = (None if 'no-traj' in args.ablate else traj, None if 'no-logdet' in args.ablate else logdet)
+
+    def step():
+        kf.run(u, z, dt=dt, update_every=k, out=out)
+
+    def gather_payload():
+        xf, _ = kf.state()
+        return torch.cat([xf, logdet[-1:]], dim=0).contiguous()
+
+    def cpu():
+        """The reference CPU loop (oracle/ref_kf.run_filter_loop: one filter at a time, NumPy in
+        the reference's op order, kf_workers.py:688-717), 1 core, ~12 s of this workload."""
+        from oracle import ref_kf
+        model = ref_kf.CV2 if cfg['model'] == 'cv2' else ref_kf.CV3
+        nf = min(4096, B)
+        idx = torch.linspace(0, B - 1, nf).long().to(u.device)
+        xs = x0[:, idx].double().cpu().numpy().T
+        us = u[:, :, idx].double().cpu().numpy()
+        zs = z[:, :, idx].double().cpu().numpy()
+        steps, done, t0 = 0, 0, time.perf_counter()
+        while done < nf and time.perf_counter() - t0 < 12.0:
+            ref_kf.run_filter_loop(model, xs[done], model.P0(), np.full(T, dt), us[:, :, done], zs[:, :, done], k)
+            steps += T
+            done += 1
+        el = time.perf_counter() - t0
+        return {'value': steps / el, 'unit': 'KF steps/s', 'cores': 1, 'kind': 'port',
+                'sample': f'{done} filters x {T} steps of this workload (same synthetic streams), '
+                          f'oracle/ref_kf.run_filter_loop, NumPy {np.__version__}, 1 thread, {host_cpu()}',
+                'seconds': round(el, 2)}
+
+    d = 2 if cfg['model'] == 'cv2' else 3
+    bytes_launch, bytes_step = algorithmic_bytes(cfg)
+    return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_step, kernel='cv_run_kernel',
+                traffic=load_traffic(cfg_id), cpu=cpu, gather=gather_payload, kf=kf,
+                desc=f"BASELINE config {cfg_id}: {cfg['model']} ({2 * d}-state/{d}-meas), {cfg['dtype']}, "
+                     f"B={B} filters/GPU, T={T}, dt={dt}, GPS update every {k} step(s)",
+                extra={'filters_per_gpu': B, 'time_steps_per_launch': T, 'update_every': k})
+
+
+def ref15_workload(cfg, args, rank, world, dev):
+    """The reference's 15-state model on 200 Hz IMU + 10 Hz GPS event streams (every k-th event a
+    GPS fix), one stream per filter, synthetic (torch RNG on the device; the reference's
+    imu_data.csv is absent)."""
+    import kfmi
+    from kfmi import _lib
+    from kfmi.engine import _ptr
+    B, T, dt, k = cfg['B'], cfg['T'], cfg['dt'], cfg['k']
+    kf = kfmi.BatchedKF('ref15', B, 'f64', device=dev.index)
+    g = torch.Generator(device=dev).manual_seed(SEED + rank)
+    etype = torch.ones(T, B, dtype=torch.uint8, device=dev)
+    etype[k - 1::k] = 0
+    dts = torch.full((T, B), dt, dtype=torch.float64, device=dev)
+    pay = torch.randn(T, 9, B, dtype=torch.float64, device=dev, generator=g)
+    pay[:, 0:3] *= 0.05   # roll/pitch/yaw
+    pay[:, 3:6] *= 0.01   # angular rates
+    pay[:, 6:9] *= 0.3    # accelerations
+    gps = (etype == 0)[:, None, :]
+    pay[:, 0:3] = torch.where(gps, pay[:, 0:3] * 60.0, pay[:, 0:3])  # GPS fixes within ~3 m
+    traj = kf.empty(T, 6, B)
+    logdet = kf.empty(T, B)
+
+    def step():
+        _lib.check(_lib.lib().kf_run_events(kf.handle, T, _ptr(etype), _ptr(dts), _ptr(pay), _ptr(traj),
+                                            _ptr(logdet), None, 0, 0.0, kf._stream()))
+
+    def gather_payload():
+        xf, _ = kf.state()
+        return torch.cat([xf, logdet[-1:]], dim=0).contiguous()
+
+    def cpu():
+        """oracle/ref_kf.step15 + slogdet (the reference's dense 15x15 per-event NumPy step,
+        kf_workers.py:688-717), 1 core, ~12 s over these streams."""
+        from oracle import ref_kf
+        nf = min(B, 2048)
+        et = etype[:, :nf].cpu().numpy()
+        pa = pay[:, :, :nf].cpu().numpy()
+        steps, t0 = 0, time.perf_counter()
+        for f in range(nf):
+            x, P = np.zeros(15), ref_kf.P0_REF15.copy()
+            for t in range(T):
+                if et[t, f] == 0:
+                    sd = {'easting': pa[t, 0, f], 'northing': pa[t, 1, f], 'altitude': pa[t, 2, f]}
+                    x, P = ref_kf.step15(x, P, 'GPS', sd, dt)
+                else:
+                    x, P = ref_kf.step15(x, P, 'IMU', ['t', *pa[t, :, f]], dt)
+                np.linalg.slogdet(P)
+                steps += 1
+            if time.perf_counter() - t0 > 12.0:
+                break
+        el = time.perf_counter() - t0
+        return {'value': steps / el, 'unit': 'KF events/s', 'cores': 1, 'kind': 'port',
+                'sample': f'{steps} events of these streams through oracle/ref_kf.step15 + slogdet '
+                          f'(reference op order, dense 15x15), NumPy {np.__version__}, 1 thread, {host_cpu()}',
+                'seconds': round(el, 2)}
+
+    # per event: etype 1 + dt 8 + payload 72 read, traj 48 + logdet 8 written; state per launch
+    per_filter = T * (1 + 8 + 72 + 48 + 8) + 2 * (15 + 27) * 8 + 8
+    return dict(step=step, units=B * T, bytes=per_filter * B, bytes_per_unit=per_filter / T,
+                kernel='ref15_events_kernel', traffic=None, cpu=cpu, gather=gather_payload, kf=kf,
+                desc=f'SURVEY 8f row 2: reference 15-state model (kf_workers.py:493-614), f64, B={B} filters/GPU, '
+                     f'T={T} events (IMU 200 Hz, GPS fix every {k}th event), dt={dt}',
+                extra={'filters_per_gpu': B, 'events_per_launch': T})
+
+
+def bf_workload(cfg, args, rank, world, dev):
+    """Exhaustive brute-force search (kf_workers.py:1218-1392 without the early exit): every
+    k-subset, k = 1..n, of n candidate events after a warm start, through kf_eval_combos.  Each
+    rank runs the whole search (weak scaling: the same search per GPU)."""
+    import kfmi
+    from kfmi import ref15 as r15
+    n, chunk = cfg['n'], cfg['chunk']
+    rng = np.random.default_rng(SEED)
+    t0 = 1697739552.3362827
+    ev = np.zeros((n, 11))
+    ev[:, 0] = t0 + 0.005 * np.arange(1, n + 1)
+    ev[:, 1] = 1
+    ev[::20, 1] = 0          # GPS fixes among the IMU samples (10 Hz vs 200 Hz)
+    ev[:, 2:5] = rng.normal(0, 0.05, (n, 3))
+    ev[:, 5:8] = rng.normal(0, 0.01, (n, 3))
+    ev[:, 8:11] = rng.normal(0, 0.3, (n, 3))
+    gps = ev[:, 1] == 0
+    ev[gps, 2:5] = rng.normal(0, 3, (int(gps.sum()), 3))
+    # a warm-start covariance of the shape the reference's own runs produce (block-diagonal)
+    Pw = np.diag([0.9, 0.9, 0.9, 0.02, 0.02, 0.02, 0.5, 0.5, 0.5, 0.05, 0.05, 0.05, 20.0, 20.0, 20.0])
+    init = np.concatenate([np.zeros(15), r15.to_blocks(Pw)])
+    width = min(chunk, max(math.comb(n, k) for k in range(1, n + 1)))
+    kf = kfmi.BatchedKF('ref15', width, 'f64', device=dev.index)
+    total_combos = 2 ** n - 1
+    total_steps = sum(math.comb(n, k) * (k + 1) for k in range(1, n + 1))
+    launches = [(k, off) for k in range(1, n + 1) for off in range(0, math.comb(n, k), width)]
+    t_end = t0 + 0.005 * (n + 1)
+
+    def step():
+        for k, off in launches:
+            kf.eval_combos(ev, init, t0, t_end, k, combo_offset=off, logdets=False)
+
+    def cpu():
+        """oracle/ref_kf.evaluate_combo_chunk (the reference worker's NumPy loop) on the 12-subsets,
+        1 core, ~12 s."""
+        from itertools import combinations, islice
+        from oracle import ref_kf
+        cand = [(i, 'GPS' if ev[i, 1] == 0 else 'IMU', ev[i, 0],
+                 ({'easting': ev[i, 2], 'northing': ev[i, 3], 'altitude': ev[i, 4]} if ev[i, 1] == 0
+                  else ['t', *ev[i, 2:]])) for i in range(n)]
+        done, steps, ts = 0, 0, time.perf_counter()
+        for combo in islice(combinations(cand, 12), 100000):
+            ref_kf.evaluate_combo_chunk([combo], np.zeros(15), Pw, t0, t_end)
+            done += 1
+            steps += 13
+            if time.perf_counter() - ts > 12.0:
+                break
+        el = time.perf_counter() - ts
+        return {'value': steps / el, 'unit': 'KF steps/s', 'combinations_per_s': done / el, 'cores': 1,
+                'kind': 'port', 'sample': f'{done} 12-subsets of the {n} candidates through '
+                                          f'oracle/ref_kf.evaluate_combo_chunk, NumPy {np.__version__}, 1 thread, '
+                                          f'{host_cpu()}', 'seconds': round(el, 2)}
+
+    return dict(step=step, units=total_steps, bytes=None, bytes_per_unit=None, kernel='ref15_combo_kernel',
+                traffic=None, cpu=cpu, gather=None, kf=kf, combos=total_combos,
+                desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '
+                     f'all 2^{n}-1 subsets, reference 15-state model, f64, {len(launches)} kf_eval_combos launches',
+                extra={'candidate_events': n, 'combinations': total_combos, 'launch_width': width})
 
 
 def main():
@@ -103,7 +269,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=10)
-    ap.add_argument('--config', type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument('--config', default='3', choices=sorted(CONFIGS))
     ap.add_argument('--batch', type=int, default=None, help='override filters per GPU')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--ablate', choices=['none', 'no-traj', 'no-logdet', 'no-traj-no-logdet'], default='none',
@@ -120,30 +286,19 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
 
-    import kfmi
     cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg['B'] = args.batch
-    B, T, k, dt = cfg['B'], cfg['T'], cfg['k'], cfg['dt']
-    dev = torch.device('cuda', local)
-
-    from kfmi import dist as kdist
-    kf = kfmi.BatchedKF(cfg['model'], B, cfg['dtype'], device=local)
-    # weak scaling: world*B filters in total; shard r owns a contiguous slice and regenerates
-    # its own streams from the counter-based generator (keyed by the global filter index)
-    offset, count = kdist.shard_range(world * B, rank, world)
-    assert count == B
-    x0, u, z = kf.synth(T=T, dt=dt, update_every=k, seed=SEED, filter_offset=offset)
-    kf.reset(x0)
-    traj = kf.empty(T, kf.n, B)
-    logdet = kf.empty(T, B)
+    if args.config == 'ref15':
+        w = ref15_workload(cfg, args, rank, world, dev)
+    elif args.config == 'bf':
+        w = bf_workload(cfg, args, rank, world, dev)
+    else:
+        w = cv_workload(args.config, cfg, args, rank, world, dev)
+    step = w['step']
     stream = torch.cuda.current_stream(dev)
-
-    out = (None if 'no-traj' in args.ablate else traj, None if 'no-logdet' in args.ablate else logdet)
-
-    def step():
-        kf.run(u, z, dt=dt, update_every=k, out=out)
 
     for _ in range(args.warmup):
         step()
@@ -164,32 +319,29 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev])) if ev else float('nan')
 
-    bad = int((kf.status() != 0).sum().item())
+    kf = w['kf']
+    bad = int((kf.status() != 0).sum().item()) if args.config != 'bf' else 0
     gather_ms = None
     if dist:
+        from kfmi import dist as kdist
         elapsed, kern_ms, bad = kdist.max_over_ranks([elapsed, kern_ms, bad], dev)
         bad = int(bad)
-        # reassemble the final states + logdets of every shard on every rank (RCCL over xGMI);
-        # timed separately from the steps: it is a once-per-job reassembly, not the hot path
-        xf, _ = kf.state()
-        local_out = torch.cat([xf, logdet[-1:]], dim=0).contiguous()
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        g0 = time.perf_counter()
-        gathered = kdist.gather_shards(local_out, world * B)
-        torch.cuda.synchronize(dev)
-        assert gathered.shape == (kf.n + 1, world * B)
-        gather_ms = (time.perf_counter() - g0) * 1e3
+        if w['gather'] is not None:
+            # reassemble the final states + logdets of every shard on every rank (RCCL over
+            # xGMI); timed separately: a once-per-job reassembly, not the hot path
+            local_out = w['gather']()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            g0 = time.perf_counter()
+            gathered = kdist.gather_shards(local_out, world * kf.batch)
+            torch.cuda.synchronize(dev)
+            assert gathered.shape[-1] == world * kf.batch
+            gather_ms = (time.perf_counter() - g0) * 1e3
 
     if rank == 0:
-        total_steps = world * B * T * args.steps
-        value = total_steps / elapsed
-        bytes_launch, bytes_step = algorithmic_bytes(cfg)
-        achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(args.config, world)
         rec = {
             'metric': 'KF predict+update steps/sec (batched filters)',
-            'value': value,
+            'value': world * w['units'] * args.steps / elapsed,
             'unit': 'KF steps/s',
             'n_gpus': world,
             'steps': args.steps,
@@ -199,30 +351,29 @@ def main():
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': cfg['dtype'],
-            'data': 'synthetic (Philox4x32-10 GPS+IMU streams per SURVEY.md §8d, resident in HBM)',
-            'config': {'workload': f"BASELINE config {args.config}: {cfg['model']} "
-                                   f"({2 * (2 if cfg['model'] == 'cv2' else 3)}-state), "
-                                   f"{cfg['dtype']}, B={B} filters/GPU, T={T}, dt={dt}, "
-                                   f"GPS update every {k} step(s)",
-                       'filters_per_gpu': B, 'time_steps_per_launch': T, 'update_every': k,
-                       'parallelism': f'filter shards x{world} (no data-path collective)'},
-            'hbm_gbs': achieved,
-            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': achieved / HBM_PEAK_GBS,
-                         'traffic': traffic,
-                         'kernel': 'cv_run_kernel', 'kernel_ms': kern_ms,
-                         'algorithmic_bytes_per_launch': bytes_launch,
-                         'algorithmic_bytes_per_step': bytes_step},
-            'failed_filters': bad,
+            'data': 'synthetic (GPS+IMU streams per SURVEY.md §8d, generated on the GPU, resident in HBM)',
+            'config': dict({'workload': w['desc'], 'parallelism': f'filter shards x{world} (no data-path collective)'},
+                           **w['extra']),
         }
+        if w['bytes'] is not None:
+            achieved = w['bytes'] / (kern_ms * 1e-3) / 1e9
+            rec['hbm_gbs'] = achieved
+            rec['roofline'] = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                               'frac': achieved / HBM_PEAK_GBS, 'traffic': w['traffic'], 'kernel': w['kernel'],
+                               'kernel_ms': kern_ms, 'algorithmic_bytes_per_launch': w['bytes'],
+                               'algorithmic_bytes_per_step': w['bytes_per_unit']}
+        else:
+            rec['roofline'] = {'bound': 'hbm', 'achieved': None, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': None,
+                               'traffic': None, 'kernel': w['kernel'], 'kernel_ms': kern_ms,
+                               'note': 'compute-bound search: events in LDS, ~350 B of HBM traffic per subset'}
+        if 'combos' in w:
+            rec['combinations_per_s'] = world * w['combos'] * args.steps / elapsed
+        rec['failed_filters'] = bad
         if args.ablate != 'none':
             rec['ablation'] = args.ablate + ' (diagnostic run: NOT the benchmark workload)'
         if gather_ms is not None:
             rec['allgather_ms'] = gather_ms
-        if world == 1 and not args.no_cpu_baseline:
-            rec['cpu_baseline'] = cpu_baseline(cfg, x0, u, z)
-        else:
-            rec['cpu_baseline'] = None
+        rec['cpu_baseline'] = w['cpu']() if (world == 1 and not args.no_cpu_baseline) else None
         print(json.dumps(rec), flush=True)
     kf.close()
     if dist:

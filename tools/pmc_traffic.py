@@ -57,7 +57,7 @@ def main():
         w = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE'), 'cv_run_kernel')
         fetch = 1024 * sum(f) / len(f)
         write = 1024 * sum(w) / len(w)
-        alg, _ = algorithmic_bytes(CONFIGS[c])
+        alg, _ = algorithmic_bytes(CONFIGS[str(c)])
         res[f'config{c}'] = {
             'fetch_bytes_raw': fetch, 'write_bytes_raw': write,
             'bytes_per_launch': fetch * read_scale + write * write_scale,
