@@ -185,6 +185,28 @@ int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const d
                    double prev_time, double target_end, int k, uint64_t combo_offset, void* logdets,
                    void* max_logdet, int32_t* n_records, void* stream);
 
+/* KF_MODEL_REF15 scheduler scoring: gain device [n_types][B] = trace of the posterior
+ * covariance each candidate sensor type (types: host [n_types] KF_EVENT_GPS|KF_EVENT_IMU,
+ * n_types <= 16) would give every filter's current covariance.  full = 0: the reference's
+ * Scheduler.gain, an update with the first measurement row only (cov_matrix(S=[1]),
+ * kf_workers.py:112-147, 174-185); full = 1: every measurement row of the sensor. */
+int kf_score_candidates(kf_batch* handle, int n_types, const int32_t* types, int full, void* gain,
+                        void* stream);
+
+/* KF_MODEL_REF15 rate-decimated greedy filter (run_kalman_filter_scheduled with
+ * selection_method='greedy', kf_workers.py:826-957), per filter in one launch.  Streams:
+ * t device [T][B] absolute event times (double), etype device [T][B] (KF_EVENT_GPS|IMU, NONE =
+ * padding at the end), payload device [T][9][B].  prev_time device [B]: time of the state in the
+ * handle.  Events within 1/f of the last processed one are queued; the first event past the
+ * window triggers the greedy pick from the queue (first candidate with the largest Scheduler.gain
+ * on the current covariance; the trigger itself is dropped unless the queue was empty, as in the
+ * reference), then one predict over the accumulated dt and one update.  f per filter: freq
+ * device [B] (a sampling sweep in one launch), or freq_all when freq is NULL.  Outputs per
+ * selection s (compacted): traj [s][6][B], logdet [s][B], sel_time [s][B]; n_sel [B]. */
+int kf_run_scheduled(kf_batch* handle, int T, const double* t, const uint8_t* etype, const void* payload,
+                     const double* prev_time, const double* freq, double freq_all, void* traj, void* logdet,
+                     double* sel_time, int32_t* n_sel, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -540,3 +540,94 @@ def run_brute_force(events, start_idx, end_idx, R_threshold, initial_pt, initial
                         'trajectory': traj, 'accuracy_metric': metric, 'log_determinants': log_det,
                         'num_measurements_used': used}
     return None
+
+
+# --------------------------------------------------------------------------------------
+# Sensor scheduling (kf_workers.py:99-213, 826-957)
+# --------------------------------------------------------------------------------------
+
+def scheduler_cov_matrix(S, Sigma_prev, R, H):
+    """Scheduler.cov_matrix, device='cpu' branch (kf_workers.py:112-147): posterior covariance
+    after updating with the 1-based measurement rows S of (H, R) (all rows if len(S) == m)."""
+    k = len(S)
+    if k == R.shape[0]:
+        R_hat, H_hat = R, H
+    else:
+        idx = np.array(sorted(S)) - 1
+        R_hat, H_hat = R[np.ix_(idx, idx)], H[idx, :]
+    Sm = R_hat + np.dot(H_hat, np.dot(Sigma_prev, H_hat.T))
+    K = np.dot(np.dot(Sigma_prev, H_hat.T), np.linalg.inv(Sm))
+    return Sigma_prev - np.dot(np.dot(K, H_hat), Sigma_prev)
+
+
+def scheduler_gain(stype, Sigma):
+    """Scheduler.gain (kf_workers.py:174-185): trace of cov_matrix(S=[1]) for the sensor."""
+    if stype == 'GPS':
+        return np.trace(scheduler_cov_matrix([1], Sigma, R_gps15(), H_gps15()))
+    return np.trace(scheduler_cov_matrix([1], Sigma, R_imu15(), H_imu15()))
+
+
+def greedy_schedule(queue, Sigma):
+    """Scheduler.greedy_schedule (kf_workers.py:195-213): first candidate with the largest gain."""
+    best, best_i = -np.inf, None
+    for i, (_, stype, _, _) in enumerate(queue):
+        g = scheduler_gain(stype, Sigma)
+        if g > best:
+            best, best_i = g, i
+    return best_i
+
+
+def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt=None, initial_state=None,
+                                selection_method=None, processing_frequency=None, rng_choice=None):
+    """kf_workers.py:826-957: events whose time is within 1/f of the last processed one are
+    queued; the next event past the window triggers a selection from the queue (random or
+    greedy), then one predict over the accumulated dt and one update on the selection.  The
+    triggering event itself is dropped unless the queue was empty (as in the reference).
+    rng_choice(n) supplies the random pick (default np.random.choice)."""
+    if start_idx is None or start_idx < 0:
+        start_idx = 0
+    if end_idx is None or end_idx > len(events):
+        end_idx = len(events)
+    if selection_method not in ('random', 'greedy'):
+        return None
+    choice = rng_choice or np.random.choice
+    xt = np.zeros(15)
+    if initial_state is not None:
+        Pt = initial_pt
+        xt[0:6] = initial_state[1:7]
+        start_off = start_idx
+        prev = initial_state[0]
+    else:
+        Pt = P0_REF15.copy()
+        prev, start_off = None, 0
+        for i, (_, stype, t, sdata) in enumerate(events[start_idx:end_idx]):
+            if stype == 'GPS':
+                xt[0], xt[1], xt[2] = sdata['easting'], sdata['northing'], sdata['altitude']
+                prev, start_off = t, start_idx + i
+                break
+        if prev is None:
+            return None, None
+    states = [(prev, *xt[:6])]
+    logdets = [np.linalg.slogdet(Pt)[1]]
+    queue = []
+    if end_idx == -1:
+        end_idx = len(events)
+    for ev in events[start_off + 1:end_idx]:
+        (_, stype, t, sdata) = ev
+        if t - prev < 1 / processing_frequency:
+            queue.append(ev)
+            continue
+        if not queue:
+            queue.append(ev)
+        if selection_method == 'random':
+            sel = choice(len(queue))
+        else:
+            sel = greedy_schedule(queue, Pt)
+        (_, s_type, s_t, s_data) = queue[sel]
+        queue = []
+        dt = s_t - prev
+        xt, Pt = step15(xt, Pt, s_type, s_data, dt)
+        states.append((s_t, *xt[:6]))
+        logdets.append(np.linalg.slogdet(Pt)[1])
+        prev = s_t
+    return states, logdets, Pt

@@ -436,4 +436,55 @@ int kf_eval_combos(kf_batch* h, int n_events, const double* events, const double
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_eval_combos");
 }
 
+int kf_score_candidates(kf_batch* h, int n_types, const int32_t* types, int full, void* gain, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (!is_ref15(h)) return fail(KF_EINVAL, "kf_score_candidates: needs a KF_MODEL_REF15 handle");
+    if (n_types < 1 || n_types > 16) return fail(KF_EINVAL, "kf_score_candidates: n_types = %d outside [1, 16]", n_types);
+    if (!types || !gain) return fail(KF_EINVAL, "kf_score_candidates: null types/gain");
+    if (h->B == 0) return KF_OK;
+    kfmi::Ref15ScoreArgs a{};
+    a.B = h->B;
+    a.n_types = n_types;
+    a.full = full;
+    for (int i = 0; i < n_types; ++i) {
+        if (types[i] != KF_EVENT_GPS && types[i] != KF_EVENT_IMU)
+            return fail(KF_EINVAL, "kf_score_candidates: candidate %d has type %d (GPS=0 or IMU=1)", i, types[i]);
+        a.types[i] = static_cast<int8_t>(types[i]);
+    }
+    a.x = h->x;
+    a.P = h->P;
+    a.gain = gain;
+    hipError_t e = kfmi::launch_ref15_score(h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? KF_OK : hip_fail(e, "kf_score_candidates");
+}
+
+int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, const void* payload,
+                     const double* prev_time, const double* freq, double freq_all, void* traj, void* logdet,
+                     double* sel_time, int32_t* n_sel, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (!is_ref15(h)) return fail(KF_EINVAL, "kf_run_scheduled: needs a KF_MODEL_REF15 handle");
+    if (T < 0) return fail(KF_EINVAL, "kf_run_scheduled: T = %d < 0", T);
+    if (!freq && !(freq_all > 0.0)) return fail(KF_EINVAL, "kf_run_scheduled: processing frequency must be > 0");
+    if (h->B == 0) return KF_OK;
+    if (!t || !etype || !payload || !prev_time) return fail(KF_EINVAL, "kf_run_scheduled: null input stream");
+    kfmi::Ref15SchedArgs a{};
+    a.B = h->B;
+    a.T = T;
+    a.t = t;
+    a.etype = etype;
+    a.payload = payload;
+    a.prev_time = prev_time;
+    a.freq = freq;
+    a.freq_all = freq_all;
+    a.x = h->x;
+    a.P = h->P;
+    a.status = h->status;
+    a.traj = traj;
+    a.logdet = logdet;
+    a.sel_time = sel_time;
+    a.n_sel = n_sel;
+    hipError_t e = kfmi::launch_ref15_scheduled(h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? KF_OK : hip_fail(e, "kf_run_scheduled");
+}
+
 }  // extern "C"

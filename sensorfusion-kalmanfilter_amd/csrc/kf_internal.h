@@ -82,6 +82,38 @@ struct Ref15ComboArgs {
     int32_t* n_records;      // [B] or nullptr
 };
 
+// Scheduler scoring (kf_workers.py:112-185): trace of the posterior covariance each candidate
+// sensor would give, per filter.  full = 0: the reference's S = [1] (first measurement row
+// only); full = 1: every row of the sensor.
+struct Ref15ScoreArgs {
+    int64_t B;
+    int n_types;
+    int full;
+    int8_t types[16];        // KF_EVENT_GPS / KF_EVENT_IMU per candidate
+    const void* x;
+    const void* P;
+    void* gain;              // [n_types][B]
+};
+
+// Rate-decimated greedy driver (run_kalman_filter_scheduled, kf_workers.py:826-957), per filter.
+struct Ref15SchedArgs {
+    int64_t B;
+    int T;
+    const double* t;         // [T][B] absolute event times (fp64)
+    const uint8_t* etype;    // [T][B]
+    const void* payload;     // [T][9][B]
+    const double* prev_time; // [B] time of the state in the handle
+    const double* freq;      // [B] processing frequency per filter, or nullptr
+    double freq_all;         // used when freq == nullptr
+    void* x;
+    void* P;
+    int32_t* status;
+    void* traj;              // [T][6][B] per selection (compacted)
+    void* logdet;            // [T][B]
+    double* sel_time;        // [T][B]
+    int32_t* n_sel;          // [B]
+};
+
 enum class Op { Run, Predict, Update, Reset };
 
 // Launchers (kf_cv.hip).  Return hipSuccess or the launch error.
@@ -90,6 +122,8 @@ hipError_t launch_synth(int axes, bool f64, const SynthArgs& a, hipStream_t stre
 hipError_t launch_ref15_events(bool f64, const Ref15Args& a, hipStream_t stream);
 hipError_t launch_ref15_reset(bool f64, const Ref15Args& a, hipStream_t stream);
 hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream);
+hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream);
+hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream);
 
 constexpr int kBlock = 256;  // 4 wave64 per workgroup
 

@@ -374,7 +374,135 @@ __global__ __launch_bounds__(kBlock) void ref15_combo_kernel(const Ref15ComboArg
     a.status[f] = st;
 }
 
+// ------------------------------------------------------------------------------------
+// Scheduler scoring and the rate-decimated greedy driver (kf_workers.py:99-213, 826-957).
+// ------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T cov_trace(const Ref15<T>& s) {
+    T tr = T(0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) tr += s.pva[i][0] + s.pva[i][3] + s.pva[i][5];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) tr += s.aw[i][0] + s.aw[i][2];
+    return tr;
+}
+
+// trace of Scheduler.cov_matrix (kf_workers.py:112-147) for one candidate sensor.  The first
+// row of both H_gps and H_imu is e_0 (pos_x), with R[0,0] = 3 (GPS) or 50 (IMU); a full update
+// uses every row.  The state vector is not needed, so a zero one is carried through.
+template <typename T>
+__device__ __forceinline__ T posterior_trace(const Ref15<T>& s0, int type, bool full) {
+    Ref15<T> c = s0;
+#pragma unroll
+    for (int i = 0; i < 15; ++i) c.x[i] = T(0);
+    if (!full) {
+        T xb[3] = {T(0), T(0), T(0)};
+        const T z[1] = {T(0)};
+        const T R[1] = {T(type == kGps ? kRGps : kRPos)};
+        sel_update<3, 1, true, T>(xb, c.pva[0], z, R);
+    } else if (type == kGps) {
+        const T z[3] = {T(0), T(0), T(0)};
+        c.update_gps(z);
+    } else {
+        T imu[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) imu[i] = T(0);
+        c.update_imu(imu, T(0));
+    }
+    return cov_trace(c);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void ref15_score_kernel(const Ref15ScoreArgs a) {
+    const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (f >= a.B) return;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
+    Ref15<T> s;
+    s.load(a.x, a.P, rb, off);
+    for (int c = 0; c < a.n_types; ++c) stb(a.gain, c, rb, off, posterior_trace(s, int(a.types[c]), a.full != 0));
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void ref15_sched_kernel(const Ref15SchedArgs a) {
+    const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (f >= a.B) return;
+    const int64_t B = a.B;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(B) * uint32_t(sizeof(T));
+    const uint32_t rb_tr = a.traj ? rb : 0u, rb_ld = a.logdet ? rb : 0u;
+    Ref15<T> s;
+    s.load(a.x, a.P, rb, off);
+    int32_t st = a.status[f];
+    double prev = a.prev_time[f];
+    const double period = 1.0 / (a.freq ? a.freq[f] : a.freq_all);  // kf_workers.py:880
+    int q_start = 0, q_len = 0, nsel = 0;
+    for (int i = 0; i < a.T; ++i) {
+        const int ty = a.etype[int64_t(i) * B + f];
+        if (ty == 255) continue;  // padding of a ragged stream
+        const double ti = a.t[int64_t(i) * B + f];
+        if (ti - prev < period) {  // still inside the window: queue it
+            if (q_len == 0) q_start = i;
+            ++q_len;
+            continue;
+        }
+        if (q_len == 0) {  // gap larger than the window: the current event alone
+            q_start = i;
+            q_len = 1;
+        }
+        // greedy_schedule (kf_workers.py:195-213): first queued candidate with the largest
+        // gain = trace of the S=[1] posterior on the current covariance
+        const T g_gps = posterior_trace(s, kGps, false);
+        const T g_imu = posterior_trace(s, kImu, false);
+        T best = -__builtin_inf();
+        int sel = q_start;
+        for (int j = q_start; j < q_start + q_len; ++j) {
+            const int tj = a.etype[int64_t(j) * B + f];
+            if (tj == 255) continue;
+            const T g = tj == kGps ? g_gps : g_imu;
+            if (g > best) {
+                best = g;
+                sel = j;
+            }
+        }
+        q_len = 0;
+        const double tsel = a.t[int64_t(sel) * B + f];
+        T pay[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) pay[k] = ldb<T>(a.payload, int64_t(sel) * 9 + k, rb, off);
+        bool ok = true;
+        s.event(a.etype[int64_t(sel) * B + f], T(tsel - prev), pay, false, T(0), ok);
+        if (!ok) {
+            st = kNotSpd;
+            s.fill_nan();
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) stb(a.traj, int64_t(nsel) * 6 + k, rb_tr, off, s.x[k]);
+        if (a.logdet) stb(a.logdet, nsel, rb_ld, off, s.logdet());
+        if (a.sel_time) a.sel_time[int64_t(nsel) * B + f] = tsel;
+        ++nsel;
+        prev = tsel;
+    }
+    if (a.n_sel) a.n_sel[f] = nsel;
+    s.store(a.x, a.P, rb, off);
+    a.status[f] = st;
+}
+
 }  // namespace
+
+hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream) {
+    const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
+    if (f64) ref15_score_kernel<double><<<grid, kBlock, 0, stream>>>(a);
+    else ref15_score_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream) {
+    const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
+    if (f64) ref15_sched_kernel<double><<<grid, kBlock, 0, stream>>>(a);
+    else ref15_sched_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    return hipGetLastError();
+}
 
 hipError_t launch_ref15_events(bool f64, const Ref15Args& a, hipStream_t stream) {
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));

@@ -233,6 +233,42 @@ class BatchedKF:
         torch.cuda.current_stream(self.device).synchronize()  # host arrays were staged; keep them alive
         return mx, ld, nr
 
+    def score_candidates(self, types, full=False):
+        """KF_MODEL_REF15 scheduler scoring (kf_score_candidates): [len(types), B] traces of the
+        posterior covariance each candidate sensor would give (full=False: the reference's
+        Scheduler.gain, first measurement row only)."""
+        if self.model != 'ref15':
+            raise ValueError('score_candidates needs a ref15 handle')
+        ty = np.ascontiguousarray(types, dtype=np.int32)
+        out = self.empty(len(ty), self.batch)
+        check(_lib.lib().kf_score_candidates(self.handle, len(ty), ty.ctypes.data_as(ctypes.c_void_p), int(full),
+                                             _ptr(out), self._stream()))
+        return out
+
+    def run_scheduled(self, t, etype, payload, prev_time, freq):
+        """KF_MODEL_REF15 rate-decimated greedy filter (kf_run_scheduled).  t [T, B] float64
+        absolute times, etype [T, B] uint8, payload [T, 9, B], prev_time [B] float64, freq scalar
+        or [B] float64 (a sampling sweep in one launch).  Returns (traj [T, 6, B], logdet [T, B],
+        sel_time [T, B], n_sel [B]) with the first n_sel[f] rows of filter f valid."""
+        if self.model != 'ref15':
+            raise ValueError('run_scheduled needs a ref15 handle')
+        T = int(t.shape[0])
+        td = self._dev(t, (T, self.batch), 't', torch.float64)
+        et = self._dev(etype, (T, self.batch), 'etype', torch.uint8)
+        pay = self._dev(payload, (T, 9, self.batch), 'payload')
+        pv = self._dev(prev_time, (self.batch,), 'prev_time', torch.float64)
+        fr = None
+        if np.ndim(freq) != 0:
+            fr = self._dev(freq, (self.batch,), 'freq', torch.float64)
+        tr = self.empty(max(T, 1), 6, self.batch)
+        ld = self.empty(max(T, 1), self.batch)
+        stt = torch.empty(max(T, 1), self.batch, dtype=torch.float64, device=self.device)
+        ns = torch.empty(self.batch, dtype=torch.int32, device=self.device)
+        check(_lib.lib().kf_run_scheduled(self.handle, T, _ptr(td), _ptr(et), _ptr(pay), _ptr(pv), _ptr(fr),
+                                          float(freq) if fr is None else 0.0, _ptr(tr), _ptr(ld), _ptr(stt),
+                                          _ptr(ns), self._stream()))
+        return tr, ld, stt, ns
+
     # -- synthetic streams (SURVEY.md §8d) -----------------------------------------------
     def synth(self, T, dt, update_every=1, seed=20251015, filter_offset=0):
         """Deterministic synthetic (x0 [n,B], u [T,c,B], z [U,m,B]) generated on the GPU."""

@@ -8,6 +8,9 @@ the event list (``indexed_sensor_data``, built by combine_sensor_data, kf_worker
     run_adaptive_threshold_kalman_filter                 kf_workers.py:959-1058
     evaluate_combo_chunk (evaluate_combo_chunk_worker)   kf_workers.py:22-97
     run_brute_force_kalman_filter_no_sampling_min_usage  kf_workers.py:1218-1392
+    run_kalman_filter_scheduled                          kf_workers.py:826-957
+    scheduler_gain / scheduler_cov_trace (Scheduler)     kf_workers.py:112-185
+    sampling_sweep (the driver behind sampling_sweep/kf_plot_{10..120}.png)
 
 Host code here only selects events and differences their time stamps in fp64 with the
 reference's rules (first-GPS start, negative-dt skips); every predict/update/logdet runs in the
@@ -316,3 +319,142 @@ def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end
     finally:
         kf.close()
     return None
+
+
+# --------------------------------------------------------------------------------------------
+# Sensor scheduling (kf_workers.py:99-213, 826-957)
+# --------------------------------------------------------------------------------------------
+
+def scheduler_gain(covariances, types=('GPS', 'IMU'), full=False, dtype='f64', device=0):
+    """Scheduler.gain (kf_workers.py:174-185) for a batch: covariances [B, 15, 15] (block-diagonal)
+    -> [B, len(types)] traces of the posterior covariance after a candidate of each type
+    (full=False: the reference's cov_matrix(S=[1]); full=True: every row of the sensor),
+    computed in one kf_score_candidates launch."""
+    Ps = np.asarray(covariances, np.float64)
+    if Ps.ndim == 2:
+        Ps = Ps[None]
+    B = Ps.shape[0]
+    kf = BatchedKF('ref15', B, dtype, device=device)
+    npd = np.float64 if dtype == 'f64' else np.float32
+    kf.set_state(np.zeros((15, B), npd), np.ascontiguousarray(to_blocks(Ps).T.astype(npd)))
+    g = kf.score_candidates([GPS if s == 'GPS' else IMU for s in types], full=full)
+    out = g.double().cpu().numpy().T
+    kf.close()
+    return out
+
+
+def _scheduled_window_events(events, start_idx, end_idx, initial_pt, initial_state):
+    """Start state and candidate list exactly as run_kalman_filter_scheduled sets them up
+    (kf_workers.py:828-877).  Returns (x0, P, prev_time, candidates) or None."""
+    if start_idx is None or start_idx < 0:
+        start_idx = 0
+    if end_idx is None or end_idx > len(events):
+        end_idx = len(events)
+    x0 = np.zeros(15)
+    if initial_state is not None:
+        P = np.asarray(initial_pt, np.float64)
+        x0[0:6] = initial_state[1:7]
+        start_off, prev = start_idx, initial_state[0]
+    else:
+        P = P0
+        cs = _cold_start(events, start_idx, end_idx)
+        if cs is None:
+            return None
+        x0, prev, start_off = cs
+    if end_idx == -1:
+        end_idx = len(events)
+    return x0, P, prev, list(events[start_off + 1:end_idx])
+
+
+def _stream_arrays(cands, B=1):
+    T = len(cands)
+    t = np.zeros((max(T, 1), B))
+    et = np.full((max(T, 1), B), NONE, np.uint8)
+    pay = np.zeros((max(T, 1), 9, B))
+    for i, (_, stype, ti, sdata) in enumerate(cands):
+        t[i, :] = ti
+        et[i, :] = GPS if stype == 'GPS' else IMU
+        pay[i, :, :] = np.asarray(event_payload(stype, sdata))[:, None]
+    return t, et, pay
+
+
+def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt=None, initial_state=None,
+                                selection_method=None, processing_frequency=None, print_output=False,
+                                dtype='f64', device=0):
+    """kf_workers.py:826-957 on the GPU.  'greedy': windowing, Scheduler scoring and the filter
+    all run in kf_run_scheduled; 'random': the pick is np.random.choice over the queue, drawn
+    from the global NumPy RNG in the same order as the reference (the windows do not depend on
+    the filter state), and the selected events run in kf_run_events.  Returns (states,
+    logdets, P)."""
+    if selection_method not in ('random', 'greedy'):
+        print("Invalid selection_method. Choose either 'random' or 'greedy'.")
+        return None
+    w = _scheduled_window_events(events, start_idx, end_idx, initial_pt, initial_state)
+    if w is None:
+        return None, None
+    x0, P, prev0, cands = w
+    f = float(processing_frequency)
+    if selection_method == 'greedy':
+        kf = BatchedKF('ref15', 1, dtype, device=device)
+        npd = np.float64 if dtype == 'f64' else np.float32
+        kf.set_state(x0[:, None].astype(npd), to_blocks(P)[:, None].astype(npd))
+        t, et, pay = _stream_arrays(cands)
+        tr, ld, stt, ns = kf.run_scheduled(t[:len(cands) or 1], et[:len(cands) or 1], pay.astype(npd)[:len(cands) or 1],
+                                           np.array([prev0]), f)
+        # the handle's initial logdet comes from a zero-event pass of the same kernels
+        ld0 = _run_streams([[]], x0[None], to_blocks(P)[None], dtype, device)[1][0, 0]
+        n = int(ns[0])
+        tr, ld, stt = tr.double().cpu().numpy(), ld.double().cpu().numpy(), stt.cpu().numpy()
+        xf, Pb = kf.state()
+        Pf = from_blocks(Pb[:, 0].double().cpu().numpy())
+        kf.close()
+        states = [(prev0, *x0[:6])] + [(stt[i, 0], *tr[i, :, 0]) for i in range(n)]
+        logdets = [float(ld0)] + [float(v) for v in ld[:n, 0]]
+    else:
+        selected, queue, prev = [], [], prev0
+        for ev in cands:
+            if ev[2] - prev < 1 / f:
+                queue.append(ev)
+                continue
+            if not queue:
+                queue.append(ev)
+            sel = queue[np.random.choice(len(queue))]
+            queue = []
+            selected.append((GPS if sel[1] == 'GPS' else IMU, sel[2] - prev, event_payload(sel[1], sel[3]), sel[2]))
+            prev = sel[2]
+        tr, ld, _, x, Pb, st = _run_streams([[s[:3] for s in selected]], x0[None], to_blocks(P)[None], dtype, device)
+        states = [(prev0, *tr[0, :, 0])] + [(s[3], *tr[i + 1, :, 0]) for i, s in enumerate(selected)]
+        logdets = [float(v) for v in ld[:len(selected) + 1, 0]]
+        Pf = from_blocks(Pb[:, 0])
+    if print_output:
+        print(f'{selection_method.capitalize()} Scheduled Kalman Filter (GPU): processed {len(states) - 1} measurements')
+    return states, logdets, Pf
+
+
+def sampling_sweep(events, frequencies, start_idx=None, end_idx=None, initial_pt=None, initial_state=None,
+                   dtype='f64', device=0):
+    """The greedy scheduled filter at every processing frequency in ONE kf_run_scheduled launch
+    (one filter per frequency) — the experiment behind the reference's
+    sampling_sweep/kf_plot_{10..120}.png.  Returns {f: (states, logdets, P)}."""
+    w = _scheduled_window_events(events, start_idx, end_idx, initial_pt, initial_state)
+    if w is None:
+        return {}
+    x0, P, prev0, cands = w
+    freqs = np.asarray(frequencies, np.float64)
+    B = len(freqs)
+    npd = np.float64 if dtype == 'f64' else np.float32
+    kf = BatchedKF('ref15', B, dtype, device=device)
+    kf.set_state(np.repeat(x0[:, None], B, 1).astype(npd), np.repeat(to_blocks(P)[:, None], B, 1).astype(npd))
+    t, et, pay = _stream_arrays(cands, B)
+    tr, ld, stt, ns = kf.run_scheduled(t, et, pay.astype(npd), np.full(B, prev0), freqs)
+    ld0 = _run_streams([[]], x0[None], to_blocks(P)[None], dtype, device)[1][0, 0]
+    tr, ld, stt, ns = tr.double().cpu().numpy(), ld.double().cpu().numpy(), stt.cpu().numpy(), ns.cpu().numpy()
+    _, Pb = kf.state()
+    Pb = Pb.double().cpu().numpy()
+    kf.close()
+    out = {}
+    for b, f in enumerate(frequencies):
+        n = int(ns[b])
+        states = [(prev0, *x0[:6])] + [(stt[i, b], *tr[i, :, b]) for i in range(n)]
+        out[f] = (states, [float(ld0)] + [float(v) for v in ld[:n, b]], from_blocks(Pb[:, b]))
+    return out

@@ -15,6 +15,7 @@ Fixtures written (inputs and the reference's outputs, nothing else):
                     start window, plus run_adaptive_threshold_kalman_filter (959-1058)
   ref15_combos.npz  evaluate_combo_chunk_worker (kf_workers.py:22-97) on k=1..3 subsets
   ref15_bruteforce.npz  run_brute_force_kalman_filter_no_sampling_min_usage (1218-1392)
+  ref15_scheduled.npz   run_kalman_filter_scheduled (826-957), Scheduler.gain/cov_matrix (112-185)
   ref8_full.npz     hw5_2.run_kalman_filter (hw5_2.py:313-380)
   cv_batch.npz      4/2 and 6/3 constant-velocity filters stepped with the reference's
                     own predict_covariance (kf_workers.py:546-549) and
@@ -214,6 +215,45 @@ def ref15_bruteforce(kfw):
     print('ref15_bruteforce: selected', sel, 'threshold', thr)
 
 
+def ref15_scheduled(kfw):
+    """run_kalman_filter_scheduled (kf_workers.py:826-957): greedy selection at several
+    processing rates, random selection with the global numpy RNG seeded, and the Scheduler's
+    gain / cov_matrix (kf_workers.py:112-185) on a few covariances."""
+    events = synth_events(seed=16, seconds=1.2, out_of_order=False)
+    sf = kfw.KF_SensorFusion('gps.csv', 'imu.csv')
+    sf.indexed_sensor_data = events
+    o = pack_events(events)
+    for f in (20, 50, 120):
+        sf.set_processing_frequency(f)
+        st, ld, P = sf.run_kalman_filter_scheduled(start_idx=0, end_idx=len(events), selection_method='greedy')
+        o.update({f'greedy{f}_states': np.array(st), f'greedy{f}_logdets': np.array(ld), f'greedy{f}_P': np.array(P)})
+    sf.set_processing_frequency(50)
+    np.random.seed(1234)
+    st, ld, P = sf.run_kalman_filter_scheduled(start_idx=0, end_idx=len(events), selection_method='random')
+    o.update(random50_seed=np.array(1234), random50_states=np.array(st), random50_logdets=np.array(ld),
+             random50_P=np.array(P))
+    # warm-start scheduled window
+    st0, _, P0w, _ = sf.run_kalman_filter_full(start_idx=0, end_idx=60)
+    sf.set_processing_frequency(100)
+    st, ld, P = sf.run_kalman_filter_scheduled(start_idx=60, end_idx=180, initial_pt=P0w, initial_state=st0[-1],
+                                               selection_method='greedy')
+    o.update(warm_init_P=np.array(P0w), warm_init_state=np.array(st0[-1]), warm_states=np.array(st),
+             warm_logdets=np.array(ld), warm_P=np.array(P))
+    # Scheduler.gain / cov_matrix on covariances met along the run
+    sch = kfw.Scheduler()
+    Rm = {'GPS': sf.get_gps_measurement_noise_covariance_matrix(), 'IMU': sf.get_imu_measurement_noise_covariance_matrix()}
+    Hm = {'GPS': sf.get_gps_observation_matrix(), 'IMU': sf.get_imu_observation_matrix()}
+    sig = [P0w, P, np.diag([10000.0] * 3 + [1000.0] * 9 + [10000.0] * 3)]
+    gains = [[sch.gain(('x', s), S, Rm, Hm, device='cpu') for s in ('GPS', 'IMU')] for S in sig]
+    covs = [[sch.cov_matrix([1], S, Rm[s], Hm[s], device='cpu') for s in ('GPS', 'IMU')] for S in sig]
+    full = [[sch.cov_matrix(list(range(1, Rm[s].shape[0] + 1)), S, Rm[s], Hm[s], device='cpu')
+             for s in ('GPS', 'IMU')] for S in sig]
+    o.update(sched_sigma=np.array(sig), sched_gain=np.array(gains), sched_cov_first=np.array(covs),
+             sched_cov_full=np.array(full))
+    np.savez_compressed(os.path.join(OUT, 'ref15_scheduled.npz'), **o)
+    print('ref15_scheduled:', len(events), 'events; greedy120', len(o['greedy120_states']), 'selections')
+
+
 def ref8_full(h5):
     events = synth_events(seed=13, seconds=1.5, out_of_order=False)
     sf = h5.KF_SensorFusion('gps.csv', 'imu.csv')
@@ -282,11 +322,12 @@ def cv_batch(kfw):
 
 
 if __name__ == '__main__':
+    # python tests/golden/make_golden.py [generator ...]   (default: all)
     kfw, h5 = import_reference()
-    ref15_full(kfw)
-    ref15_combos(kfw)
-    ref15_bruteforce(kfw)
-    ref8_full(h5)
-    cv_batch(kfw)
+    gens = {'ref15_full': lambda: ref15_full(kfw), 'ref15_combos': lambda: ref15_combos(kfw),
+            'ref15_bruteforce': lambda: ref15_bruteforce(kfw), 'ref15_scheduled': lambda: ref15_scheduled(kfw),
+            'ref8_full': lambda: ref8_full(h5), 'cv_batch': lambda: cv_batch(kfw)}
+    for name in (sys.argv[1:] or list(gens)):
+        gens[name]()
     # analytic known answer: slogdet(P0) of kf_workers.py:651 = 6 ln 1e4 + 9 ln 1e3
     print('KAT logdet(P0) =', np.linalg.slogdet(np.diag([1e4] * 3 + [1e3] * 9 + [1e4] * 3))[1])

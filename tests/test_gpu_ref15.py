@@ -177,3 +177,92 @@ def test_ref15_handle_rejects_cv_entry_points():
         kf.predict(0.1)
     with pytest.raises(ValueError):
         kfmi.BatchedKF('cv3', 4, 'f64').run_events(np.zeros((1, 4), np.uint8), np.zeros((1, 4)), np.zeros((1, 9, 4)))
+
+
+# -- sensor scheduling (kf_workers.py:99-213, 826-957) ----------------------------------------
+
+@pytest.mark.parametrize('f', [20, 50, 120])
+def test_scheduled_greedy(golden_dir, f):
+    g = _load(golden_dir, 'ref15_scheduled.npz')
+    events = unpack_events(g)
+    st, ld, P = ref15.run_kalman_filter_scheduled(events, 0, len(events), selection_method='greedy',
+                                                  processing_frequency=f)
+    assert np.array(st).shape == g[f'greedy{f}_states'].shape
+    assert _rel(st, g[f'greedy{f}_states']) <= TOL
+    assert _rel(ld, g[f'greedy{f}_logdets']) <= TOL
+    assert _rel(P, g[f'greedy{f}_P']) <= TOL
+
+
+def test_scheduled_random_and_warm(golden_dir):
+    g = _load(golden_dir, 'ref15_scheduled.npz')
+    events = unpack_events(g)
+    np.random.seed(int(g['random50_seed']))
+    st, ld, P = ref15.run_kalman_filter_scheduled(events, 0, len(events), selection_method='random',
+                                                  processing_frequency=50)
+    assert np.array(st).shape == g['random50_states'].shape
+    assert _rel(st, g['random50_states']) <= TOL
+    assert _rel(ld, g['random50_logdets']) <= TOL
+    assert _rel(P, g['random50_P']) <= TOL
+    st, ld, P = ref15.run_kalman_filter_scheduled(events, 60, 180, initial_pt=g['warm_init_P'],
+                                                  initial_state=tuple(g['warm_init_state']),
+                                                  selection_method='greedy', processing_frequency=100)
+    assert np.array(st).shape == g['warm_states'].shape
+    assert _rel(st, g['warm_states']) <= TOL
+    assert _rel(ld, g['warm_logdets']) <= TOL
+    assert _rel(P, g['warm_P']) <= TOL
+    assert ref15.run_kalman_filter_scheduled(events, 0, 10, selection_method='bogus',
+                                             processing_frequency=50) is None
+
+
+def test_scheduler_gain(golden_dir):
+    g = _load(golden_dir, 'ref15_scheduled.npz')
+    S = g['sched_sigma']
+    gain = ref15.scheduler_gain(S)
+    assert _rel(gain, g['sched_gain']) <= TOL
+    assert _rel(gain, np.trace(g['sched_cov_first'], axis1=2, axis2=3)) <= TOL
+    full = ref15.scheduler_gain(S, full=True)
+    assert _rel(full, np.trace(g['sched_cov_full'], axis1=2, axis2=3)) <= TOL
+
+
+def test_sampling_sweep_one_launch(golden_dir):
+    """Every processing frequency as its own filter in ONE kf_run_scheduled launch, against the
+    reference's outputs (20/50/120 Hz) and the oracle (the rest)."""
+    g = _load(golden_dir, 'ref15_scheduled.npz')
+    events = unpack_events(g)
+    freqs = [10, 20, 30, 40, 50, 60, 70, 80, 90, 100, 110, 120, 1000]
+    out = ref15.sampling_sweep(events, freqs)
+    for f in freqs:
+        st, ld, P = out[f]
+        if f in (20, 50, 120):
+            rs, rl, rP = g[f'greedy{f}_states'], g[f'greedy{f}_logdets'], g[f'greedy{f}_P']
+        else:
+            rs, rl, rP = ref_kf.run_kalman_filter_scheduled(events, 0, len(events), selection_method='greedy',
+                                                            processing_frequency=f)
+        assert np.array(st).shape == np.array(rs).shape, f
+        assert _rel(st, rs) <= TOL, f
+        assert _rel(ld, rl) <= TOL, f
+        assert _rel(P, rP) <= TOL, f
+
+
+def test_score_candidates_random_batch():
+    """kf_score_candidates over a batch of random block-diagonal covariances vs the oracle's
+    Scheduler.cov_matrix trace (first row and full)."""
+    rng = np.random.default_rng(3)
+    B = 130
+    Ps = []
+    for _ in range(B):
+        P = np.zeros((15, 15))
+        for idx in ref15._PVA + ref15._AW:
+            A = rng.normal(size=(len(idx), len(idx)))
+            P[np.ix_(idx, idx)] = A @ A.T + np.eye(len(idx)) * rng.uniform(0.1, 100)
+        Ps.append(P)
+    Ps = np.array(Ps)
+    for full in (False, True):
+        gain = ref15.scheduler_gain(Ps, full=full)
+        for b in range(0, B, 5):
+            for ti, s in enumerate(('GPS', 'IMU')):
+                R = ref_kf.R_gps15() if s == 'GPS' else ref_kf.R_imu15()
+                H = ref_kf.H_gps15() if s == 'GPS' else ref_kf.H_imu15()
+                rows = list(range(1, R.shape[0] + 1)) if full else [1]
+                want = np.trace(ref_kf.scheduler_cov_matrix(rows, Ps[b], R, H))
+                assert abs(gain[b, ti] - want) <= TOL * max(1.0, abs(want)), (full, b, s)

@@ -140,3 +140,43 @@ def test_ref15_bruteforce_search(golden_dir):
     assert _rel(out['log_determinants'], g['log_determinants']) < RTOL
     assert _rel(out['final_state'], g['final_state']) < RTOL
     assert _rel(out['trajectory'], g['trajectory']) < RTOL
+
+
+@pytest.mark.parametrize('f', [20, 50, 120])
+def test_ref15_scheduled_greedy(golden_dir, f):
+    g = _load(golden_dir, 'ref15_scheduled.npz')
+    events = unpack_events(g)
+    st, ld, P = ref_kf.run_kalman_filter_scheduled(events, 0, len(events), selection_method='greedy',
+                                                   processing_frequency=f)
+    assert np.array(st).shape == g[f'greedy{f}_states'].shape
+    assert _rel(st, g[f'greedy{f}_states']) < RTOL
+    assert _rel(ld, g[f'greedy{f}_logdets']) < RTOL
+    assert _rel(P, g[f'greedy{f}_P']) < RTOL
+
+
+def test_ref15_scheduled_random_and_warm(golden_dir):
+    g = _load(golden_dir, 'ref15_scheduled.npz')
+    events = unpack_events(g)
+    np.random.seed(int(g['random50_seed']))
+    st, ld, P = ref_kf.run_kalman_filter_scheduled(events, 0, len(events), selection_method='random',
+                                                   processing_frequency=50)
+    assert _rel(st, g['random50_states']) < RTOL
+    assert _rel(ld, g['random50_logdets']) < RTOL
+    st, ld, P = ref_kf.run_kalman_filter_scheduled(events, 60, 180, initial_pt=g['warm_init_P'],
+                                                   initial_state=tuple(g['warm_init_state']),
+                                                   selection_method='greedy', processing_frequency=100)
+    assert _rel(st, g['warm_states']) < RTOL
+    assert _rel(ld, g['warm_logdets']) < RTOL
+    assert _rel(P, g['warm_P']) < RTOL
+
+
+def test_scheduler_gain_and_cov_matrix(golden_dir):
+    g = _load(golden_dir, 'ref15_scheduled.npz')
+    for si, S in enumerate(g['sched_sigma']):
+        for ti, s in enumerate(('GPS', 'IMU')):
+            R = ref_kf.R_gps15() if s == 'GPS' else ref_kf.R_imu15()
+            H = ref_kf.H_gps15() if s == 'GPS' else ref_kf.H_imu15()
+            assert _rel(ref_kf.scheduler_gain(s, S), g['sched_gain'][si, ti]) < RTOL
+            assert _rel(ref_kf.scheduler_cov_matrix([1], S, R, H), g['sched_cov_first'][si, ti]) < RTOL
+            full = list(range(1, R.shape[0] + 1))
+            assert _rel(ref_kf.scheduler_cov_matrix(full, S, R, H), g['sched_cov_full'][si, ti]) < RTOL
