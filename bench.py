@@ -163,7 +163,7 @@ def ref15_workload(cfg, args, rank, world, dev):
 
     def step():
         _lib.check(_lib.lib().kf_run_events(kf.handle, T, _ptr(etype), _ptr(dts), _ptr(pay), _ptr(traj),
-                                            _ptr(logdet), None, 0, 0.0, kf._stream()))
+                                            None, _ptr(logdet), None, 0, 0.0, kf._stream()))
 
     def gather_payload():
         xf, _ = kf.state()

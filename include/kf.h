@@ -62,6 +62,15 @@ extern "C" {
  * Driven by per-filter event streams (kf_run_events) or the combination search (kf_eval_combos). */
 #define KF_MODEL_REF15 15
 
+/* The reference's 8-state planar model (hw5_2.py:219-311): state [x, y, theta, vx, vy,
+ * theta_dot, ax, ay], GPS fix m=2 (easting, northing), IMU pseudo-measurement m=8 with theta =
+ * yaw and theta_dot = wz (hw5_2.py:352-366), P0 = diag(1000, 1000, 100, 100, 100, 100, 1000,
+ * 1000).  Same chain structure, 15 block-packed rows ([15][B]):
+ *   rows 6i..6i+5   axis i in {x, y}: (pos_i, vel_i, acc_i) upper triangle
+ *   rows 12..14     (theta, theta_dot) upper triangle
+ * kf_run_events only; its trajectory records (x, y, theta) as hw5_2.py:369 does. */
+#define KF_MODEL_REF8 8
+
 /* Event codes for kf_run_events / kf_eval_combos. */
 #define KF_EVENT_GPS     0    /* payload = (easting, northing, altitude, ...)              */
 #define KF_EVENT_IMU     1    /* payload = (roll, pitch, yaw, wx, wy, wz, ax, ay, az)     */
@@ -104,7 +113,8 @@ int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_pa
 int kf_free(kf_batch* handle);
 
 /* Dimensions of a handle (any pointer may be NULL).  For KF_MODEL_REF15: n = 15, m = 3 (GPS),
- * c = 0, and the covariance has 27 block-packed rows instead of n(n+1)/2. */
+ * c = 0, and the covariance has 27 block-packed rows instead of n(n+1)/2 (KF_MODEL_REF8: n = 8,
+ * m = 2, c = 0, 15 rows). */
 int kf_dims(const kf_batch* handle, int* n, int* m, int* c, int64_t* batch, int* dtype);
 
 /* Re-initialise every filter: x = x0 (device [n][B]; NULL = zeros), P = P0, status = OK.
@@ -159,17 +169,22 @@ int kf_run(kf_batch* handle, int T, double dt, const double* dt_steps, const voi
 int kf_synth(kf_batch* handle, uint64_t seed, int64_t filter_offset, int T, double dt,
              int update_every, void* x0_out, void* u_out, void* z_out, void* stream);
 
-/* KF_MODEL_REF15: T events per filter in one launch.  etype device [T][B] uint8 (KF_EVENT_*),
- * dt device [T][B] double (time since the filter's previous event), payload device [T][9][B]
- * (handle dtype).  Per event: predict over dt, then the GPS update (kf_workers.py:694-697) or
- * the IMU pseudo-measurement update built from the predicted state (:698-706); with gate != 0
- * the update is applied only when logdet(P_pred) > threshold (:1023-1025).  traj device
- * [T][6][B] receives x[0:6] after each event (:714), logdet [T][B] the log-determinant
- * (:716-717), updated [T][B] uint8 whether the update was applied; each may be NULL.
- * Replaces the loops of run_kalman_filter_full (:681-721) and
- * run_adaptive_threshold_kalman_filter (:1010-1053), batched over filters. */
+/* KF_MODEL_REF15 / KF_MODEL_REF8: T events per filter in one launch.  etype device [T][B]
+ * uint8 (KF_EVENT_*), dt device [T][B] double (time since the filter's previous event), payload
+ * device [T][9][B] (handle dtype).  Per event: predict over dt, then the GPS update
+ * (kf_workers.py:694-697) or the IMU pseudo-measurement update built from the predicted state
+ * (:698-706); with gate != 0 the update is applied only when logdet(P_pred) > threshold
+ * (:1023-1025).  Per-event records, each of which may be NULL: traj device [T][6][B] (REF8:
+ * [T][3][B]) receives x[0:6] after each event (:714; hw5_2.py:369), cov device [T][27][B]
+ * (REF8: [T][15][B]) the block-packed covariance (the sf_KF_covariance list of :739-824),
+ * logdet [T][B] the log-determinant (:716-717), updated [T][B] uint8 whether the update was
+ * applied.  Replaces the loops of run_kalman_filter_full (:681-721), run_kalman_filter
+ * (:763-824), run_adaptive_threshold_kalman_filter (:1010-1053), run_no_update_kalman_filter
+ * (:1110-1155, as KF_EVENT_PREDICT streams) and hw5_2.run_kalman_filter (hw5_2.py:328-380),
+ * batched over filters. */
 int kf_run_events(kf_batch* handle, int T, const uint8_t* etype, const double* dt, const void* payload,
-                  void* traj, void* logdet, uint8_t* updated, int gate, double threshold, void* stream);
+                  void* traj, void* cov, void* logdet, uint8_t* updated, int gate, double threshold,
+                  void* stream);
 
 /* KF_MODEL_REF15 brute-force search: filter f of the handle evaluates combination number
  * combo_offset + f (itertools.combinations order) of k out of n_events candidate events, from the

@@ -292,6 +292,73 @@ def run_kalman_filter_full(events, start_idx=0, end_idx=None, initial_pt=None, i
     return states, logdets, Pt, prev_time
 
 
+def run_kalman_filter_simple(events, start_idx, end_idx):
+    """kf_workers.py:738-824: x0 = 0 and the reference's integer P0 (:744-760), skip events
+    until the window's first GPS (whose dt is 0), no dt < 0 guard.  Returns (states,
+    covariances) with states[0] = (0, 0, ...) and one covariance per record."""
+    xt = np.zeros(15, dtype=np.int64)
+    Pt = P0_REF15.astype(np.int64)
+    states = [(0, *xt[:6])]
+    covs = [Pt.copy()]
+    started = False
+    prev = None
+    for (_, stype, t, sdata) in events[start_idx:end_idx]:
+        if stype == 'GPS' and not started:
+            started = True
+            prev = t
+        if not started:
+            continue
+        dt = t - prev if prev is not None else 0
+        xt, Pt = step15(xt, Pt, stype, sdata, dt)
+        states.append((t, *xt[:6]))
+        covs.append(Pt.copy())
+        prev = t
+    return states, covs
+
+
+def run_no_update(events, start_idx=None, end_idx=None, initial_pt=None, initial_state=None):
+    """kf_workers.py:1060-1160: the adaptive driver's loop with every update commented out —
+    predictions only, logdet after each.  A dt < 0 event is skipped WITHOUT advancing the
+    previous time (:1113-1116 assigns an unused name).  Returns (states, logdets, P,
+    previous_time, measurement_times) or None when no GPS starts the window."""
+    if start_idx is None or start_idx < 0:
+        start_idx = 0
+    if end_idx is None or end_idx > len(events):
+        end_idx = len(events)
+    xt = np.zeros(15)
+    mtimes = []
+    if initial_pt is not None and initial_state is not None:
+        Pt = initial_pt
+        xt[0:6] = initial_state[1:7]
+        prev = initial_state[0]
+        start_off = start_idx
+    else:
+        Pt = P0_REF15.copy()
+        start_off = -1
+        for i, (_, stype, t, sdata) in enumerate(events[start_idx:end_idx]):
+            if stype == 'GPS':
+                xt[0], xt[1], xt[2] = sdata['easting'], sdata['northing'], sdata['altitude']
+                prev = t
+                start_off = start_idx + i
+                mtimes.append(t)
+                break
+        if start_off == -1:
+            return None
+    states = [(prev, *xt[:6])]
+    logdets = [np.linalg.slogdet(Pt)[1]]
+    for (_, stype, t, sdata) in events[start_off:end_idx]:
+        dt = t - prev
+        if dt < 0:
+            continue
+        F = F_ref15(dt)
+        xt = np.dot(F, xt)
+        Pt = predict_covariance(Pt, F, Q_ref15(dt))
+        states.append((t, *xt[:6]))
+        logdets.append(np.linalg.slogdet(Pt)[1])
+        prev = t
+    return states, logdets, Pt, prev, mtimes
+
+
 def evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time):
     """kf_workers.py:22-97 with the 15-state class_args bound in.
 
@@ -379,11 +446,33 @@ def run_adaptive_threshold(events, start_idx=0, end_idx=None, R_threshold=-np.in
     return states, logdets, Pt, prev, times
 
 
+def step8(x, P, stype, sdata, dt):
+    """One event of hw5_2.run_kalman_filter (hw5_2.py:336-366)."""
+    I = np.eye(8)
+    F = F_ref8(dt)
+    x = np.dot(F, x)
+    P = predict_covariance(P, F, Q_ref8(dt))
+    if stype == 'GPS':
+        H, R = H_gps8(), R_gps8()
+        Z = [sdata['easting'], sdata['northing']]
+        K = calculate_kalman_gain(P, H, R)
+        y = Z - np.dot(H, x)
+        x = x + np.dot(K, y)
+        P = np.dot(I - np.dot(K, H), P)
+    elif stype == 'IMU':
+        Z = imu_pseudo_measurement8(x, sdata, dt)
+        H, R = H_imu8(), R_imu8()
+        K = calculate_kalman_gain(P, H, R)
+        y = np.array(Z) - np.dot(H, x)
+        x = x + np.dot(K, y)
+        P = np.dot(I - np.dot(K, H), P)
+    return x, P
+
+
 def run_kalman_filter_8state(events):
     """hw5_2.py:313-380 (8-state, x0 = 0, starts at the first GPS event)."""
     xt = np.array([0, 0, 0, 0, 0, 0, 0, 0])
     Pt = P0_REF8.astype(np.int64)  # integer literal array as in hw5_2.py:317-326
-    I = np.eye(8)
     states = [(xt[0], xt[1], xt[2])]
     started = False
     prev = None
@@ -394,23 +483,7 @@ def run_kalman_filter_8state(events):
         if not started:
             continue
         dt = t - prev if prev is not None else 0
-        F = F_ref8(dt)
-        xt = np.dot(F, xt)
-        Pt = predict_covariance(Pt, F, Q_ref8(dt))
-        if stype == 'GPS':
-            H, R = H_gps8(), R_gps8()
-            Z = [sdata['easting'], sdata['northing']]
-            K = calculate_kalman_gain(Pt, H, R)
-            y = Z - np.dot(H, xt)
-            xt = xt + np.dot(K, y)
-            Pt = np.dot(I - np.dot(K, H), Pt)
-        elif stype == 'IMU':
-            Z = imu_pseudo_measurement8(xt, sdata, dt)
-            H, R = H_imu8(), R_imu8()
-            K = calculate_kalman_gain(Pt, H, R)
-            y = np.array(Z) - np.dot(H, xt)
-            xt = xt + np.dot(K, y)
-            Pt = np.dot(I - np.dot(K, H), Pt)
+        xt, Pt = step8(xt, Pt, stype, sdata, dt)
         states.append((xt[0], xt[1], xt[2]))
         prev = t
     return states, Pt

@@ -15,7 +15,7 @@ struct kf_batch {
     int model;
     int axes;   // d: state n = 2d, measurement m = d, control c = d
     int n, m, c;
-    int np;     // covariance rows: n(n+1)/2, or 27 block-packed rows for KF_MODEL_REF15
+    int np;     // covariance rows: n(n+1)/2, or the block-packed rows of KF_MODEL_REF15 (27) / REF8 (15)
     int dtype;
     int64_t B;
     int device;
@@ -53,9 +53,11 @@ constexpr size_t kWsBinom = sizeof(uint64_t) * (kMaxComboEvents + 1) * (kMaxComb
 constexpr size_t kWsInit = sizeof(double) * 42;
 
 bool is_ref15(const kf_batch* h) { return h->model == KF_MODEL_REF15; }
+bool is_ref(int model) { return model == KF_MODEL_REF15 || model == KF_MODEL_REF8; }
+bool is_ref(const kf_batch* h) { return is_ref(h->model); }
 
 int need_cv(const kf_batch* h, const char* what) {
-    if (is_ref15(h)) return fail(KF_EINVAL, "%s: not available for KF_MODEL_REF15 (use kf_run_events)", what);
+    if (is_ref(h)) return fail(KF_EINVAL, "%s: not available for the reference models (use kf_run_events)", what);
     return KF_OK;
 }
 
@@ -94,12 +96,13 @@ int model_axes(int model) {
         case KF_MODEL_CV2: return 2;
         case KF_MODEL_CV3: return 3;
         case KF_MODEL_REF15: return 3;
+        case KF_MODEL_REF8: return 2;
         default: return 0;
     }
 }
 
-kfmi::Ref15Args ref15_args(const kf_batch* h) {
-    kfmi::Ref15Args a{};
+kfmi::RefArgs ref_args(const kf_batch* h) {
+    kfmi::RefArgs a{};
     a.B = h->B;
     a.x = h->x;
     a.P = h->P;
@@ -118,7 +121,7 @@ const char* kf_last_error(void) { return g_err.c_str(); }
 int kf_default_params(int model, kf_params* out) {
     const int d = model_axes(model);
     if (!d) return fail(KF_EINVAL, "unknown model %d", model);
-    if (model == KF_MODEL_REF15) return fail(KF_EINVAL, "KF_MODEL_REF15 uses the reference constants; no kf_params");
+    if (is_ref(model)) return fail(KF_EINVAL, "the reference models use the reference constants; no kf_params");
     if (!out) return fail(KF_EINVAL, "null params");
     std::memset(out, 0, sizeof *out);
     out->q_pos = 5.0;  // position_noise = 5 * dt   (kf_workers.py:521)
@@ -165,23 +168,23 @@ int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_pa
     if (batch < 0) return fail(KF_EINVAL, "negative batch %lld", static_cast<long long>(batch));
     if (batch * 8 >= (int64_t(1) << 31))
         return fail(KF_EINVAL, "batch %lld too large (one [B] row must stay below 2 GiB)", static_cast<long long>(batch));
-    if (model == KF_MODEL_REF15 && params) return fail(KF_EINVAL, "KF_MODEL_REF15 takes no kf_params (reference constants)");
+    if (is_ref(model) && params) return fail(KF_EINVAL, "model %d takes no kf_params (reference constants)", model);
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return fail(KF_ENODEV, "no current HIP device: %s", hipGetErrorString(e));
     kf_batch* h = new kf_batch{};
     h->model = model;
     h->axes = d;
-    h->n = model == KF_MODEL_REF15 ? 15 : 2 * d;
+    h->n = model == KF_MODEL_REF15 ? 15 : model == KF_MODEL_REF8 ? 8 : 2 * d;
     h->m = d;
-    h->c = model == KF_MODEL_REF15 ? 0 : d;
-    h->np = model == KF_MODEL_REF15 ? 27 : h->n * (h->n + 1) / 2;
+    h->c = is_ref(model) ? 0 : d;
+    h->np = model == KF_MODEL_REF15 ? 27 : model == KF_MODEL_REF8 ? 15 : h->n * (h->n + 1) / 2;
     h->dtype = dtype;
     h->B = batch;
     h->device = dev;
     if (params) {
         h->params = *params;
-    } else if (model != KF_MODEL_REF15) {
+    } else if (!is_ref(model)) {
         kf_default_params(model, &h->params);
     }
     const size_t w = elem(h);
@@ -235,11 +238,11 @@ int kf_dims(const kf_batch* h, int* n, int* m, int* c, int64_t* batch, int* dtyp
 
 int kf_reset(kf_batch* h, const void* x0, void* stream) {
     if (int rc = check_handle(h)) return rc;
-    if (is_ref15(h)) {
+    if (is_ref(h)) {
         if (h->B == 0) return KF_OK;
-        kfmi::Ref15Args a = ref15_args(h);
+        kfmi::RefArgs a = ref_args(h);
         a.x0 = x0;
-        hipError_t e = kfmi::launch_ref15_reset(h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
+        hipError_t e = kfmi::launch_ref_reset(h->model, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
         return e == hipSuccess ? KF_OK : hip_fail(e, "kf_reset");
     }
     kfmi::CvArgs a = base_args(h);
@@ -361,23 +364,25 @@ int kf_synth(kf_batch* h, uint64_t seed, int64_t filter_offset, int T, double dt
 }
 
 int kf_run_events(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload,
-                  void* traj, void* logdet, uint8_t* updated, int gate, double threshold, void* stream) {
+                  void* traj, void* cov, void* logdet, uint8_t* updated, int gate, double threshold,
+                  void* stream) {
     if (int rc = check_handle(h)) return rc;
-    if (!is_ref15(h)) return fail(KF_EINVAL, "kf_run_events: needs a KF_MODEL_REF15 handle");
+    if (!is_ref(h)) return fail(KF_EINVAL, "kf_run_events: needs a KF_MODEL_REF15 or KF_MODEL_REF8 handle");
     if (T < 0) return fail(KF_EINVAL, "kf_run_events: T = %d < 0", T);
     if (T == 0 || h->B == 0) return KF_OK;
     if (!etype || !dt || !payload) return fail(KF_EINVAL, "kf_run_events: null etype/dt/payload stream");
-    kfmi::Ref15Args a = ref15_args(h);
+    kfmi::RefArgs a = ref_args(h);
     a.T = T;
     a.etype = etype;
     a.dt = dt;
     a.payload = payload;
     a.traj = traj;
+    a.cov = cov;
     a.logdet = logdet;
     a.updated = updated;
     a.gate = gate;
     a.threshold = threshold;
-    hipError_t e = kfmi::launch_ref15_events(h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
+    hipError_t e = kfmi::launch_ref_events(h->model, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_run_events");
 }
 

@@ -41,20 +41,22 @@ struct SynthArgs {
     void* z;                 // [U][m][B]
 };
 
-// Reference 15-state model (kf_workers.py:493-614) on per-filter event streams.
+// Reference chain models on per-filter event streams: KF_MODEL_REF15 (kf_workers.py:493-614,
+// N = 15, NBLK = 27, NTRAJ = 6) and KF_MODEL_REF8 (hw5_2.py:219-311, N = 8, NBLK = 15, NTRAJ = 3).
 // Event codes in etype: 0 GPS fix, 1 IMU sample, 2 predict only, 255 no event (padding).
-struct Ref15Args {
+struct RefArgs {
     int64_t B;
     int T;
     const uint8_t* etype;    // [T][B]
     const double* dt;        // [T][B] time since the filter's previous event
     const void* payload;     // [T][9][B]: GPS (easting, northing, altitude, -), IMU (roll, pitch,
                              // yaw, wx, wy, wz, ax, ay, az) as in kf_workers.py:367
-    void* x;                 // [15][B]
-    void* P;                 // [27][B] block-packed covariance (see kf_ref15.hip)
+    void* x;                 // [N][B]
+    void* P;                 // [NBLK][B] block-packed covariance (see kf_ref.hip)
     int32_t* status;         // [B]
-    const void* x0;          // reset: [15][B] or nullptr
-    void* traj;              // [T][6][B] x[0:6] after each event, or nullptr
+    const void* x0;          // reset: [N][B] or nullptr
+    void* traj;              // [T][NTRAJ][B] x[0:NTRAJ] after each event, or nullptr
+    void* cov;               // [T][NBLK][B] covariance after each event, or nullptr
     void* logdet;            // [T][B] or nullptr
     uint8_t* updated;        // [T][B] 1 if the event's update was applied, or nullptr
     int gate;                // adaptive threshold (kf_workers.py:1023-1025): update only if
@@ -116,11 +118,11 @@ struct Ref15SchedArgs {
 
 enum class Op { Run, Predict, Update, Reset };
 
-// Launchers (kf_cv.hip).  Return hipSuccess or the launch error.
+// Launchers (kf_cv.hip, kf_ref.hip).  Return hipSuccess or the launch error.
 hipError_t launch_cv(int axes, bool f64, Op op, const CvArgs& a, hipStream_t stream);
 hipError_t launch_synth(int axes, bool f64, const SynthArgs& a, hipStream_t stream);
-hipError_t launch_ref15_events(bool f64, const Ref15Args& a, hipStream_t stream);
-hipError_t launch_ref15_reset(bool f64, const Ref15Args& a, hipStream_t stream);
+hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream);
+hipError_t launch_ref_reset(int model, bool f64, const RefArgs& a, hipStream_t stream);
 hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream);
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream);
 hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream);

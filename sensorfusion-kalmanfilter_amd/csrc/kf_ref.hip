@@ -1,19 +1,21 @@
-// gfx950 kernels for the reference's 15-state GPS+IMU model (KF_MODEL_REF15,
-// kf_workers.py:493-614) on per-filter event streams, and the brute-force combination search
-// built on it (kf_workers.py:22-97, 1218-1392).
+// gfx950 kernels for the reference's chain-structured GPS+IMU models on per-filter event
+// streams — KF_MODEL_REF15 (kf_workers.py:493-614) and KF_MODEL_REF8 (hw5_2.py:219-311) — and
+// the brute-force combination search and sensor scheduling built on the 15-state one
+// (kf_workers.py:22-213, 826-957, 1218-1392).
 //
-// Structure exploited (exact, not an approximation): F(dt) (kf_workers.py:500-516) couples a
-// state only within its axis chain (pos_i, vel_i, acc_i) or (att_i, rate_i); Q, R_gps, R_imu and
-// the reference's P0 are diagonal; H_gps selects pos_i and H_imu = I.  So every covariance
-// reachable from a diagonal P0 is block-diagonal — three 3x3 (pos, vel, acc) blocks and three 2x2
-// (att, rate) blocks — and the reference's own 15x15 arithmetic keeps the off-block entries at
-// exactly 0.0 (checked on its outputs, tests/golden/ref15_*.npz).  A lane therefore runs six
-// small chain filters: 27 covariance entries instead of 120, the same numbers.
+// Structure exploited (exact, not an approximation): F(dt) (kf_workers.py:500-516,
+// hw5_2.py:221-230) couples a state only within its axis chain (pos_i, vel_i, acc_i) or
+// (att_i, rate_i); Q, R_gps, R_imu and the reference's P0 are diagonal; H_gps selects pos_i and
+// H_imu = I.  So every covariance reachable from a diagonal P0 is block-diagonal — 3x3
+// (pos, vel, acc) blocks and 2x2 (att, rate) blocks — and the reference's own dense arithmetic
+// keeps the off-block entries at exactly 0.0 (checked on its outputs, tests/golden/ref15_*.npz).
+// A lane therefore runs small chain filters: REF15 = 3 pva + 3 aw chains (27 covariance entries
+// instead of 120), REF8 = 2 pva (x, y) + 1 aw (theta) chain (15 instead of 36); same numbers.
 //
-// Block-packed covariance rows ([27][B] in HBM):
-//   rows 6i .. 6i+5 : axis i (pos_i, vel_i, acc_i) upper triangle (pp pv pa vv va aa), i = 0..2
-//   rows 18+3i .. 18+3i+2 : axis i (att_i, rate_i) upper triangle (tt tw ww)
-// State x [15][B] in the reference order (pos, att, vel, rate, acc).
+// Block-packed covariance rows ([NBLK][B] in HBM):
+//   rows 6c .. 6c+5 : pva chain c upper triangle (pp pv pa vv va aa), c = 0..NP-1
+//   rows 6NP+3c .. 6NP+3c+2 : aw chain c upper triangle (tt tw ww), c = 0..NA-1
+// State x [N][B] in the reference's order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,18 +29,42 @@ using namespace dev;
 
 constexpr int kGps = 0, kImu = 1;  // KF_EVENT_GPS / KF_EVENT_IMU; 2 = predict only, 255 = none
 
-// Reference constants (kf_workers.py:519-544, 581-614, 651).
+// Noise constants shared by both reference models (kf_workers.py:519-544, 581-614;
+// hw5_2.py:233-251, 280-304).
 constexpr double kQPos = 5.0, kQAtt = 0.05, kQVel = 1.0, kQRate = 0.1, kQAcc = 2.0;
 constexpr double kRGps = 3.0;
 constexpr double kRPos = 50.0, kRAtt = 0.05, kRVel = 10.0, kRRate = 0.1, kRAcc = 100.0;
-constexpr double kP0Pos = 10000.0, kP0Att = 1000.0, kP0Vel = 1000.0, kP0Rate = 1000.0, kP0Acc = 10000.0;
 
-template <typename T>
-struct Ref15 {
-    T x[15];
-    T pva[3][6];  // per axis: (pos, vel, acc) packed upper 3x3
-    T aw[3][3];   // per axis: (att, rate) packed upper 2x2
+// KF_MODEL_REF15: x = (pos xyz, att rpy, vel xyz, rate xyz, acc xyz) (kf_workers.py:493-517).
+struct M15 {
+    static constexpr int N = 15, NP = 3, NA = 3, NTRAJ = 6, NBLK = 27;
+    __device__ static constexpr int pva(int c, int k) { return c + 6 * k; }          // (i, 6+i, 12+i)
+    __device__ static constexpr int aw(int c, int k) { return 3 + c + 6 * k; }       // (3+i, 9+i)
+    __device__ static constexpr int imu_acc(int c) { return 6 + c; }                 // ax, ay, az
+    __device__ static constexpr int imu_att(int c) { return c; }                     // roll, pitch, yaw
+    __device__ static constexpr int imu_rate(int c) { return 3 + c; }                // wx, wy, wz
+    static constexpr double P0Pos = 10000.0, P0Att = 1000.0, P0Vel = 1000.0, P0Rate = 1000.0,
+                            P0Acc = 10000.0;  // kf_workers.py:651
+};
 
+// KF_MODEL_REF8: x = (x, y, theta, vx, vy, theta_dot, ax, ay) (hw5_2.py:219-231); the IMU
+// pseudo-measurement takes yaw as theta and wz as theta_dot (hw5_2.py:355-362).
+struct M8 {
+    static constexpr int N = 8, NP = 2, NA = 1, NTRAJ = 3, NBLK = 15;
+    __device__ static constexpr int pva(int c, int k) { return c + 3 * k; }          // (i, 3+i, 6+i)
+    __device__ static constexpr int aw(int, int k) { return 2 + 3 * k; }             // (2, 5)
+    __device__ static constexpr int imu_acc(int c) { return 6 + c; }                 // ax, ay
+    __device__ static constexpr int imu_att(int) { return 2; }                       // yaw
+    __device__ static constexpr int imu_rate(int) { return 5; }                      // wz
+    static constexpr double P0Pos = 1000.0, P0Att = 100.0, P0Vel = 100.0, P0Rate = 100.0,
+                            P0Acc = 1000.0;  // hw5_2.py:317-326
+};
+
+template <typename T, class M>
+struct Chains {
+    T x[M::N];
+    T pva[M::NP][6];  // per chain: (pos, vel, acc) packed upper 3x3
+    T aw[M::NA][3];   // per chain: (att, rate) packed upper 2x2
     // Chain predict x = F x, P = F P F^T + Q for a block whose F row i is
     // e_i + dt e_{i+1} + dt^2/2 e_{i+2} (kf_workers.py:500-516).
     template <int NB>
@@ -80,71 +106,92 @@ struct Ref15 {
         const T qpva[3] = {T(kQPos), T(kQVel), T(kQAcc)};
         const T qaw[2] = {T(kQAtt), T(kQRate)};
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            T xb[3] = {x[i], x[6 + i], x[12 + i]};
-            chain_predict<3>(xb, pva[i], dt, qpva);
-            x[i] = xb[0];
-            x[6 + i] = xb[1];
-            x[12 + i] = xb[2];
-            T xa[2] = {x[3 + i], x[9 + i]};
-            chain_predict<2>(xa, aw[i], dt, qaw);
-            x[3 + i] = xa[0];
-            x[9 + i] = xa[1];
+        for (int c = 0; c < M::NP; ++c) {
+            T xb[3];
+            get_pva(c, xb);
+            chain_predict<3>(xb, pva[c], dt, qpva);
+            put_pva(c, xb);
+        }
+#pragma unroll
+        for (int c = 0; c < M::NA; ++c) {
+            T xa[2];
+            get_aw(c, xa);
+            chain_predict<2>(xa, aw[c], dt, qaw);
+            put_aw(c, xa);
         }
     }
 
-    // GPS fix (kf_workers.py:694-697): H selects pos_i in each (pos, vel, acc) block, R = 3.
+    __device__ __forceinline__ void get_pva(int c, T (&xb)[3]) const {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) xb[k] = x[M::pva(c, k)];
+    }
+    __device__ __forceinline__ void put_pva(int c, const T (&xb)[3]) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) x[M::pva(c, k)] = xb[k];
+    }
+    __device__ __forceinline__ void get_aw(int c, T (&xa)[2]) const {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) xa[k] = x[M::aw(c, k)];
+    }
+    __device__ __forceinline__ void put_aw(int c, const T (&xa)[2]) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) x[M::aw(c, k)] = xa[k];
+    }
+
+    // GPS fix (kf_workers.py:694-697, hw5_2.py:341-349): H selects pos_c in each (pos, vel,
+    // acc) chain, R = 3; z = (easting, northing[, altitude]).
     __device__ __forceinline__ bool update_gps(const T (&z)[3]) {
         bool ok = true;
         const T R[1] = {T(kRGps)};
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            T xb[3] = {x[i], x[6 + i], x[12 + i]};
-            const T zb[1] = {z[i]};
-            ok = sel_update<3, 1, true, T>(xb, pva[i], zb, R) && ok;
-            x[i] = xb[0];
-            x[6 + i] = xb[1];
-            x[12 + i] = xb[2];
+        for (int c = 0; c < M::NP; ++c) {
+            T xb[3];
+            get_pva(c, xb);
+            const T zb[1] = {z[c]};
+            ok = sel_update<3, 1, true, T>(xb, pva[c], zb, R) && ok;
+            put_pva(c, xb);
         }
         return ok;
     }
 
-    // IMU pseudo-measurement (kf_workers.py:698-706): Z from the PREDICTED state and the raw
-    // sample, H = I, R = diag(50, 0.05, 10, 0.1, 100 per group).  imu = (roll, pitch, yaw, wx, wy,
-    // wz, ax, ay, az).
+    // IMU pseudo-measurement (kf_workers.py:698-706, hw5_2.py:352-366): Z from the PREDICTED
+    // state and the raw sample, H = I, R = diag(50, 0.05, 10, 0.1, 100 per group).  imu = (roll,
+    // pitch, yaw, wx, wy, wz, ax, ay, az).
     __device__ __forceinline__ bool update_imu(const T (&imu)[9], T dt) {
         bool ok = true;
         const T Rp[6] = {T(kRPos), T(0), T(0), T(kRVel), T(0), T(kRAcc)};
         const T Ra[3] = {T(kRAtt), T(0), T(kRRate)};
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const T a = imu[6 + i];
-            const T V = fmaT(a, dt, x[6 + i]);   // V = x_v + a dt
-            const T X = fmaT(V, dt, x[i]);       // X = x_p + V dt
-            T xb[3] = {x[i], x[6 + i], x[12 + i]};
+        for (int c = 0; c < M::NP; ++c) {
+            T xb[3];
+            get_pva(c, xb);
+            const T a = imu[M::imu_acc(c)];
+            const T V = fmaT(a, dt, xb[1]);   // V = x_v + a dt
+            const T X = fmaT(V, dt, xb[0]);   // X = x_p + V dt
             const T zb[3] = {X, V, a};
-            ok = sel_update<3, 3, true, T>(xb, pva[i], zb, Rp) && ok;
-            x[i] = xb[0];
-            x[6 + i] = xb[1];
-            x[12 + i] = xb[2];
-            T xa[2] = {x[3 + i], x[9 + i]};
-            const T za[2] = {imu[i], imu[3 + i]};
-            ok = sel_update<2, 2, true, T>(xa, aw[i], za, Ra) && ok;
-            x[3 + i] = xa[0];
-            x[9 + i] = xa[1];
+            ok = sel_update<3, 3, true, T>(xb, pva[c], zb, Rp) && ok;
+            put_pva(c, xb);
+        }
+#pragma unroll
+        for (int c = 0; c < M::NA; ++c) {
+            T xa[2];
+            get_aw(c, xa);
+            const T za[2] = {imu[M::imu_att(c)], imu[M::imu_rate(c)]};
+            ok = sel_update<2, 2, true, T>(xa, aw[c], za, Ra) && ok;
+            put_aw(c, xa);
         }
         return ok;
     }
 
-    // slogdet of the full 15x15 P = sum over the six blocks (kf_workers.py:716-717).
+    // slogdet of the full P = sum over the chain blocks (kf_workers.py:716-717).
     __device__ __forceinline__ T logdet() const {
         T prod = T(1);
         int ex = 0;
         bool ok = true;
 #pragma unroll
-        for (int i = 0; i < 3; ++i) ldl_pivot_product<3, T>(pva[i], prod, ex, ok);
+        for (int c = 0; c < M::NP; ++c) ldl_pivot_product<3, T>(pva[c], prod, ex, ok);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) ldl_pivot_product<2, T>(aw[i], prod, ex, ok);
+        for (int c = 0; c < M::NA; ++c) ldl_pivot_product<2, T>(aw[c], prod, ex, ok);
         int e;
         prod = frexp(prod, &e);
         const T ld = log_mant(prod, ex + e);
@@ -152,53 +199,46 @@ struct Ref15 {
     }
 
     __device__ __forceinline__ void reset_cov() {
+        const T p[6] = {T(M::P0Pos), T(0), T(0), T(M::P0Vel), T(0), T(M::P0Acc)};
+        const T w[3] = {T(M::P0Att), T(0), T(M::P0Rate)};
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const T p[6] = {T(kP0Pos), T(0), T(0), T(kP0Vel), T(0), T(kP0Acc)};
-            const T w[3] = {T(kP0Att), T(0), T(kP0Rate)};
+        for (int c = 0; c < M::NP; ++c)
 #pragma unroll
-            for (int k = 0; k < 6; ++k) pva[i][k] = p[k];
+            for (int k = 0; k < 6; ++k) pva[c][k] = p[k];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) aw[i][k] = w[k];
-        }
+        for (int c = 0; c < M::NA; ++c)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) aw[c][k] = w[k];
     }
+
+    // block-packed covariance row r (see the file comment)
+    __device__ __forceinline__ T& blk(int r) { return r < 6 * M::NP ? pva[r / 6][r % 6] : aw[(r - 6 * M::NP) / 3][(r - 6 * M::NP) % 3]; }
+    __device__ __forceinline__ T blk(int r) const { return r < 6 * M::NP ? pva[r / 6][r % 6] : aw[(r - 6 * M::NP) / 3][(r - 6 * M::NP) % 3]; }
 
     __device__ __forceinline__ void load(const void* xbase, const void* Pbase, uint32_t rb, uint32_t off) {
 #pragma unroll
-        for (int i = 0; i < 15; ++i) x[i] = ldb<T>(xbase, i, rb, off);
+        for (int i = 0; i < M::N; ++i) x[i] = ldb<T>(xbase, i, rb, off);
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int k = 0; k < 6; ++k) pva[i][k] = ldb<T>(Pbase, 6 * i + k, rb, off);
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int k = 0; k < 3; ++k) aw[i][k] = ldb<T>(Pbase, 18 + 3 * i + k, rb, off);
+        for (int r = 0; r < M::NBLK; ++r) blk(r) = ldb<T>(Pbase, r, rb, off);
     }
 
     __device__ __forceinline__ void store(void* xbase, void* Pbase, uint32_t rb, uint32_t off) const {
 #pragma unroll
-        for (int i = 0; i < 15; ++i) stb(xbase, i, rb, off, x[i]);
+        for (int i = 0; i < M::N; ++i) stb(xbase, i, rb, off, x[i]);
+        store_cov(Pbase, 0, rb, off);
+    }
+
+    // covariance rows at row offset r0 of a [.][B] array (r0 = t * NBLK for a per-step record)
+    __device__ __forceinline__ void store_cov(void* Pbase, int64_t r0, uint32_t rb, uint32_t off) const {
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int k = 0; k < 6; ++k) stb(Pbase, 6 * i + k, rb, off, pva[i][k]);
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int k = 0; k < 3; ++k) stb(Pbase, 18 + 3 * i + k, rb, off, aw[i][k]);
+        for (int r = 0; r < M::NBLK; ++r) stb(Pbase, r0 + r, rb, off, blk(r));
     }
 
     __device__ __forceinline__ void fill_nan() {
 #pragma unroll
-        for (int i = 0; i < 15; ++i) x[i] = quiet_nan<T>();
+        for (int i = 0; i < M::N; ++i) x[i] = quiet_nan<T>();
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-#pragma unroll
-            for (int k = 0; k < 6; ++k) pva[i][k] = quiet_nan<T>();
-#pragma unroll
-            for (int k = 0; k < 3; ++k) aw[i][k] = quiet_nan<T>();
-        }
+        for (int r = 0; r < M::NBLK; ++r) blk(r) = quiet_nan<T>();
     }
 
     // One event of the reference loop (kf_workers.py:682-717): predict over dt, then the GPS or
@@ -211,7 +251,7 @@ struct Ref15 {
         if (gate && apply) apply = logdet() > threshold;
         if (apply) {
             if (type == kGps) {
-                const T z[3] = {pay[0], pay[1], pay[2]};
+                const T z[3] = {pay[0], pay[1], pay[2]};  // (easting, northing, altitude)
                 ok = update_gps(z) && ok;
             } else {
                 ok = update_imu(pay, dt) && ok;
@@ -224,18 +264,18 @@ struct Ref15 {
 // ------------------------------------------------------------------------------------
 // Per-filter event streams (kf_run_events).
 // ------------------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(kBlock) void ref15_events_kernel(const Ref15Args a) {
+template <typename T, class M>
+__global__ __launch_bounds__(kBlock) void ref_events_kernel(const RefArgs a) {
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
     const uint32_t rb8 = uint32_t(a.B) * 8u;
     const uint32_t off8 = uint32_t(f) * 8u;
-    Ref15<T> s;
+    Chains<T, M> s;
     s.load(a.x, a.P, rb, off);
     int32_t st = a.status[f];
-    const uint32_t rb_tr = a.traj ? rb : 0u, rb_ld = a.logdet ? rb : 0u;
+    const uint32_t rb_tr = a.traj ? rb : 0u, rb_ld = a.logdet ? rb : 0u, rb_cv = a.cov ? rb : 0u;
     for (int t = 0; t < a.T; ++t) {
         const int type = a.etype[int64_t(t) * a.B + f];
         const T dt = T(ldb<double>(a.dt, t, rb8, off8));
@@ -252,7 +292,8 @@ __global__ __launch_bounds__(kBlock) void ref15_events_kernel(const Ref15Args a)
             }
         }
 #pragma unroll
-        for (int i = 0; i < 6; ++i) stb(a.traj, int64_t(t) * 6 + i, rb_tr, off, s.x[i]);
+        for (int i = 0; i < M::NTRAJ; ++i) stb(a.traj, int64_t(t) * M::NTRAJ + i, rb_tr, off, s.x[i]);
+        if (a.cov) s.store_cov(a.cov, int64_t(t) * M::NBLK, rb_cv, off);
         if (a.logdet) {
             const T ld = s.logdet();
             st = (ld == ld) ? st : kNotSpd;
@@ -264,15 +305,15 @@ __global__ __launch_bounds__(kBlock) void ref15_events_kernel(const Ref15Args a)
     a.status[f] = st;
 }
 
-template <typename T>
-__global__ __launch_bounds__(kBlock) void ref15_reset_kernel(const Ref15Args a) {
+template <typename T, class M>
+__global__ __launch_bounds__(kBlock) void ref_reset_kernel(const RefArgs a) {
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
-    Ref15<T> s;
+    Chains<T, M> s;
 #pragma unroll
-    for (int i = 0; i < 15; ++i) s.x[i] = a.x0 ? ldb<T>(a.x0, i, rb, off) : T(0);
+    for (int i = 0; i < M::N; ++i) s.x[i] = a.x0 ? ldb<T>(a.x0, i, rb, off) : T(0);
     s.reset_cov();
     s.store(a.x, a.P, rb, off);
     a.status[f] = 0;
@@ -285,6 +326,9 @@ __global__ __launch_bounds__(kBlock) void ref15_reset_kernel(const Ref15Args a) 
 // index list is stored.
 // ------------------------------------------------------------------------------------
 constexpr int kMaxEvents = 64;
+
+template <typename T>
+using Ref15 = Chains<T, M15>;
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void ref15_combo_kernel(const Ref15ComboArgs a) {
@@ -307,13 +351,7 @@ __global__ __launch_bounds__(kBlock) void ref15_combo_kernel(const Ref15ComboArg
 #pragma unroll
     for (int i = 0; i < 15; ++i) s.x[i] = T(a.init[i]);
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int k = 0; k < 6; ++k) s.pva[i][k] = T(a.init[15 + 6 * i + k]);
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) s.aw[i][k] = T(a.init[33 + 3 * i + k]);
+    for (int r = 0; r < 27; ++r) s.blk(r) = T(a.init[15 + r]);
 
     // record 0: logdet of the initial covariance (kf_workers.py:32)
     T ld = s.logdet();
@@ -504,17 +542,31 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
     return hipGetLastError();
 }
 
-hipError_t launch_ref15_events(bool f64, const Ref15Args& a, hipStream_t stream) {
+hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream) {
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-    if (f64) ref15_events_kernel<double><<<grid, kBlock, 0, stream>>>(a);
-    else ref15_events_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    if (model == 15) {
+        if (f64) ref_events_kernel<double, M15><<<grid, kBlock, 0, stream>>>(a);
+        else ref_events_kernel<float, M15><<<grid, kBlock, 0, stream>>>(a);
+    } else if (model == 8) {
+        if (f64) ref_events_kernel<double, M8><<<grid, kBlock, 0, stream>>>(a);
+        else ref_events_kernel<float, M8><<<grid, kBlock, 0, stream>>>(a);
+    } else {
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_ref15_reset(bool f64, const Ref15Args& a, hipStream_t stream) {
+hipError_t launch_ref_reset(int model, bool f64, const RefArgs& a, hipStream_t stream) {
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-    if (f64) ref15_reset_kernel<double><<<grid, kBlock, 0, stream>>>(a);
-    else ref15_reset_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    if (model == 15) {
+        if (f64) ref_reset_kernel<double, M15><<<grid, kBlock, 0, stream>>>(a);
+        else ref_reset_kernel<float, M15><<<grid, kBlock, 0, stream>>>(a);
+    } else if (model == 8) {
+        if (f64) ref_reset_kernel<double, M8><<<grid, kBlock, 0, stream>>>(a);
+        else ref_reset_kernel<float, M8><<<grid, kBlock, 0, stream>>>(a);
+    } else {
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -25,6 +25,7 @@ KF_F64 = 1
 KF_MODEL_CV2 = 2
 KF_MODEL_CV3 = 3
 KF_MODEL_REF15 = 15
+KF_MODEL_REF8 = 8
 KF_EVENT_GPS = 0
 KF_EVENT_IMU = 1
 KF_EVENT_PREDICT = 2
@@ -71,7 +72,7 @@ SIGNATURES = {
     'kf_update': (_i, [_vp, _vp, _vp, _vp, _vp]),
     'kf_run': (_i, [_vp, _i, _d, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     'kf_synth': (_i, [_vp, ctypes.c_uint64, _i64, _i, _d, _i, _vp, _vp, _vp, _vp]),
-    'kf_run_events': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _d, _vp]),
+    'kf_run_events': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _d, _vp]),
     'kf_eval_combos': (_i, [_vp, _i, _vp, _vp, _d, _d, _i, ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     'kf_score_candidates': (_i, [_vp, _i, _vp, _i, _vp, _vp]),
     'kf_run_scheduled': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _d, _vp, _vp, _vp, _vp, _vp]),

@@ -20,7 +20,10 @@ MODELS = {
     'cv2': (_lib.KF_MODEL_CV2, 4, 2, 2, 10),    # 4-state/2-meas, hw5_2.py:219-304 restricted to [x,y,vx,vy]
     'cv3': (_lib.KF_MODEL_CV3, 6, 3, 3, 21),    # 6-state/3-meas, kf_workers.py:493-614 restricted to pos/vel
     'ref15': (_lib.KF_MODEL_REF15, 15, 3, 0, 27),  # the reference's 15-state model; P block-packed
+    'ref8': (_lib.KF_MODEL_REF8, 8, 2, 0, 15),     # hw5_2.py's 8-state model; P block-packed
 }
+REF_MODELS = ('ref15', 'ref8')
+TRAJ_WIDTH = {'ref15': 6, 'ref8': 3}  # kf_workers.py:714 (x, y, z, roll, pitch, yaw); hw5_2.py:369 (x, y, theta)
 DTYPES = {'f32': (_lib.KF_F32, torch.float32, np.float32), 'f64': (_lib.KF_F64, torch.float64, np.float64)}
 
 
@@ -63,9 +66,9 @@ class BatchedKF:
         L = _lib.lib()
         check(L.kf_init(device))
         torch.cuda.set_device(self.device)
-        if model == 'ref15':
+        if model in REF_MODELS:
             if params is not None:
-                raise ValueError('ref15 uses the reference constants; params must be None')
+                raise ValueError(f'{model} uses the reference constants; params must be None')
             self.params = None
         else:
             self.params = params if params is not None else default_params(model)
@@ -191,27 +194,30 @@ class BatchedKF:
                                 _ptr(md), int(update_every), _ptr(tr), _ptr(ld), self._stream()))
         return tr, ld
 
-    # -- reference 15-state model: per-filter event streams -------------------------------
-    def run_events(self, etype, dt, payload, traj=True, logdet=True, updated=False, threshold=None):
-        """KF_MODEL_REF15: T events per filter in one launch (kf_run_events).
+    # -- reference models: per-filter event streams ----------------------------------------
+    def run_events(self, etype, dt, payload, traj=True, logdet=True, updated=False, threshold=None, cov=False):
+        """KF_MODEL_REF15 / KF_MODEL_REF8: T events per filter in one launch (kf_run_events).
 
         etype [T, B] uint8 (KF_EVENT_*), dt [T, B] float64, payload [T, 9, B] (GPS: e, n, alt;
         IMU: roll, pitch, yaw, wx, wy, wz, ax, ay, az).  threshold: adaptive-threshold gating
-        (update only if logdet(P_pred) > threshold).  Returns (traj [T, 6, B], logdet [T, B],
-        updated [T, B]) with None for outputs not asked for."""
-        if self.model != 'ref15':
-            raise ValueError('run_events needs a ref15 handle')
+        (update only if logdet(P_pred) > threshold).  Returns (traj [T, W, B], logdet [T, B],
+        updated [T, B], cov [T, rows, B]) with None for outputs not asked for (W = 6 for ref15,
+        3 for ref8; cov is block-packed)."""
+        if self.model not in REF_MODELS:
+            raise ValueError('run_events needs a ref15 or ref8 handle')
         T = int(etype.shape[0])
         et = self._dev(etype, (T, self.batch), 'etype', torch.uint8)
         dtd = self._dev(dt, (T, self.batch), 'dt', torch.float64)
         pay = self._dev(payload, (T, 9, self.batch), 'payload')
-        tr = self.empty(T, 6, self.batch) if traj else None
+        tr = self.empty(T, TRAJ_WIDTH[self.model], self.batch) if traj else None
         ld = self.empty(T, self.batch) if logdet else None
         up = torch.empty(T, self.batch, dtype=torch.uint8, device=self.device) if updated else None
+        cv = self.empty(T, self.ntri, self.batch) if cov else None
         gate = threshold is not None
-        check(_lib.lib().kf_run_events(self.handle, T, _ptr(et), _ptr(dtd), _ptr(pay), _ptr(tr), _ptr(ld),
-                                       _ptr(up), int(gate), float(threshold) if gate else 0.0, self._stream()))
-        return tr, ld, up
+        check(_lib.lib().kf_run_events(self.handle, T, _ptr(et), _ptr(dtd), _ptr(pay), _ptr(tr), _ptr(cv),
+                                       _ptr(ld), _ptr(up), int(gate), float(threshold) if gate else 0.0,
+                                       self._stream()))
+        return tr, ld, up, cv
 
     def eval_combos(self, events, init, prev_time, target_end, k, combo_offset=0, logdets=True):
         """KF_MODEL_REF15 brute force (kf_eval_combos): filter f evaluates combination

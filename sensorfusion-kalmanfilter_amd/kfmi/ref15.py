@@ -9,6 +9,8 @@ the event list (``indexed_sensor_data``, built by combine_sensor_data, kf_worker
     evaluate_combo_chunk (evaluate_combo_chunk_worker)   kf_workers.py:22-97
     run_brute_force_kalman_filter_no_sampling_min_usage  kf_workers.py:1218-1392
     run_kalman_filter_scheduled                          kf_workers.py:826-957
+    run_kalman_filter (states + per-step covariances)    kf_workers.py:738-824
+    run_no_update_kalman_filter                          kf_workers.py:1060-1160
     scheduler_gain / scheduler_cov_trace (Scheduler)     kf_workers.py:112-185
     sampling_sweep (the driver behind sampling_sweep/kf_plot_{10..120}.png)
 
@@ -31,42 +33,55 @@ from .engine import BatchedKF
 
 GPS, IMU, PREDICT, NONE = _lib.KF_EVENT_GPS, _lib.KF_EVENT_IMU, _lib.KF_EVENT_PREDICT, _lib.KF_EVENT_NONE
 
-# block-packed row r -> (i, j) in the 15x15 covariance
-_PVA = [(0, 6, 12), (1, 7, 13), (2, 8, 14)]   # (pos, vel, acc) per axis
-_AW = [(3, 9), (4, 10), (5, 11)]              # (att, rate) per axis
-_ROWS = []
-for _blk in _PVA:
-    for _a in range(3):
-        for _b in range(_a, 3):
-            _ROWS.append((_blk[_a], _blk[_b]))
-for _blk in _AW:
-    for _a in range(2):
-        for _b in range(_a, 2):
-            _ROWS.append((_blk[_a], _blk[_b]))
-_BLOCK_MASK = np.zeros((15, 15), bool)
-for _i, _j in _ROWS:
-    _BLOCK_MASK[_i, _j] = _BLOCK_MASK[_j, _i] = True
+def _block_rows(pva, aw):
+    rows = []
+    for blk in pva:
+        rows += [(blk[a], blk[b]) for a in range(3) for b in range(a, 3)]
+    for blk in aw:
+        rows += [(blk[a], blk[b]) for a in range(2) for b in range(a, 2)]
+    return rows
+
+
+# block-packed row r -> (i, j) of the dense covariance, per model (csrc/kf_ref.hip, include/kf.h)
+_LAYOUT = {
+    # n: (rows, model name) — REF15 chains (pos, vel, acc)_i = (i, 6+i, 12+i), (att, rate)_i = (3+i, 9+i)
+    15: (_block_rows([(0, 6, 12), (1, 7, 13), (2, 8, 14)], [(3, 9), (4, 10), (5, 11)]), 'ref15'),
+    # REF8 (hw5_2.py:219-231): (x, vx, ax), (y, vy, ay), (theta, theta_dot)
+    8: (_block_rows([(0, 3, 6), (1, 4, 7)], [(2, 5)]), 'ref8'),
+}
+_BY_ROWS = {len(r): n for n, (r, _) in _LAYOUT.items()}
+_MASK = {}
+for _n, (_rows, _) in _LAYOUT.items():
+    _MASK[_n] = np.zeros((_n, _n), bool)
+    for _i, _j in _rows:
+        _MASK[_n][_i, _j] = _MASK[_n][_j, _i] = True
+_ROWS = _LAYOUT[15][0]
 
 # reference P0 (kf_workers.py:651)
 P0 = np.diag([10000.0] * 3 + [1000.0] * 3 + [1000.0] * 3 + [1000.0] * 3 + [10000.0] * 3)
 
 
 def to_blocks(P):
-    """15x15 (or [..., 15, 15]) covariance -> block-packed [..., 27]; raises ValueError if it
-    couples different axis chains (the engine stores only the chain blocks)."""
+    """n x n (or [..., n, n]) covariance of REF15 (n = 15) or REF8 (n = 8) -> block-packed
+    [..., 27 | 15]; raises ValueError if it couples different axis chains (the engine stores only
+    the chain blocks)."""
     P = np.asarray(P, dtype=np.float64)
-    off = np.abs(P[..., ~_BLOCK_MASK])
+    n = P.shape[-1]
+    if n not in _LAYOUT or P.shape[-2] != n:
+        raise ValueError(f'expected a [..., 15, 15] or [..., 8, 8] covariance, got {P.shape}')
+    off = np.abs(P[..., ~_MASK[n]])
     if off.size and off.max() > 0.0:
         raise ValueError(f'covariance couples different axis chains (max |off-block| = {off.max():g}); '
-                         'KF_MODEL_REF15 stores the (pos,vel,acc)/(att,rate) blocks only')
-    return np.stack([P[..., i, j] for i, j in _ROWS], axis=-1)
+                         f'KF_MODEL_{_LAYOUT[n][1].upper()} stores the (pos,vel,acc)/(att,rate) blocks only')
+    return np.stack([P[..., i, j] for i, j in _LAYOUT[n][0]], axis=-1)
 
 
 def from_blocks(b):
-    """block-packed [..., 27] -> 15x15 symmetric."""
+    """block-packed [..., 27 | 15] -> 15x15 | 8x8 symmetric."""
     b = np.asarray(b, dtype=np.float64)
-    P = np.zeros(b.shape[:-1] + (15, 15))
-    for r, (i, j) in enumerate(_ROWS):
+    n = _BY_ROWS[b.shape[-1]]
+    P = np.zeros(b.shape[:-1] + (n, n))
+    for r, (i, j) in enumerate(_LAYOUT[n][0]):
         P[..., i, j] = b[..., r]
         P[..., j, i] = b[..., r]
     return P
@@ -79,13 +94,14 @@ def event_payload(stype, sdata):
     return [float(v) for v in sdata[1:10]]
 
 
-def _run_streams(streams, x0, P0b, dtype='f64', device=0, threshold=None):
+def _run_streams(streams, x0, P0b, dtype='f64', device=0, threshold=None, model='ref15', cov=False):
     """Run one event list per filter in ONE kf_run_events launch.
 
     streams: list (per filter) of [(type, dt, payload9)]; each stream is preceded by a NONE
-    event so row 0 of the outputs holds the initial state and logdet.  x0 [B, 15] and P0b
-    [B, 27] are the initial states.  Returns traj [T, 6, B], logdet [T, B], updated [T, B],
-    x [15, B], P blocks [27, B], status [B] as NumPy arrays."""
+    event so row 0 of the outputs holds the initial state and logdet.  x0 [B, n] and P0b
+    [B, rows] are the initial states.  Returns traj [T, W, B], logdet [T, B], updated [T, B],
+    x [n, B], P blocks [rows, B], status [B] (and cov [T, rows, B] with cov=True) as NumPy
+    arrays."""
     B = len(streams)
     T = 1 + max((len(s) for s in streams), default=0)
     etype = np.full((T, B), NONE, np.uint8)
@@ -96,16 +112,18 @@ def _run_streams(streams, x0, P0b, dtype='f64', device=0, threshold=None):
             etype[t, f] = ty
             dt[t, f] = d
             pay[t, :, f] = p
-    kf = BatchedKF('ref15', B, dtype, device=device)
+    kf = BatchedKF(model, B, dtype, device=device)
     npd = np.float64 if dtype == 'f64' else np.float32
     kf.set_state(np.ascontiguousarray(np.asarray(x0, np.float64).T.astype(npd)),
                  np.ascontiguousarray(np.asarray(P0b, np.float64).T.astype(npd)))
-    tr, ld, up = kf.run_events(etype, dt, pay.astype(npd), updated=True, threshold=threshold)
+    tr, ld, up, cv = kf.run_events(etype, dt, pay.astype(npd), updated=True, threshold=threshold, cov=cov)
     x, Pb = kf.state()
     st = kf.status()
     torch.cuda.synchronize(kf.device)
     out = (tr.double().cpu().numpy(), ld.double().cpu().numpy(), up.cpu().numpy(), x.double().cpu().numpy(),
            Pb.double().cpu().numpy(), st.cpu().numpy())
+    if cov:
+        out += (cv.double().cpu().numpy(),)
     kf.close()
     return out
 
@@ -206,6 +224,65 @@ def run_adaptive_threshold_kalman_filter(events, start_idx=None, end_idx=None, R
     mtimes += [t for i, t in enumerate(times) if up[i + 1, 0]]
     if print_output:
         print(f'Adaptive Kalman Filter (GPU): processed {len(times)} events from index {start_off} to {end_idx}')
+    return states, logdets, from_blocks(Pb[:, 0]), prev, mtimes
+
+
+def run_kalman_filter(events, start_idx, end_idx, dtype='f64', device=0):
+    """kf_workers.py:738-824 on the GPU: x0 = 0, the reference's P0, the window's events from
+    its first GPS fix on (that fix at dt = 0), no dt < 0 guard.  Returns (states,
+    covariances) — states[0] = (0, 0, 0, 0, 0, 0, 0) and one 15x15 covariance per record, the
+    per-step covariances coming from kf_run_events' cov stream."""
+    stream, times = [], []
+    prev = None
+    for (_, stype, t, sdata) in events[start_idx:end_idx]:
+        if stype == 'GPS' and prev is None:
+            prev = t
+        if prev is None:
+            continue
+        stream.append((GPS if stype == 'GPS' else IMU, t - prev, event_payload(stype, sdata)))
+        times.append(t)
+        prev = t
+    tr, _, _, _, _, _, cv = _run_streams([stream], np.zeros((1, 15)), to_blocks(P0)[None], dtype, device, cov=True)
+    states = [(0, *tr[0, :, 0])] + [(t, *tr[i + 1, :, 0]) for i, t in enumerate(times)]
+    covs = list(from_blocks(cv[:len(times) + 1, :, 0]))
+    return states, covs
+
+
+def run_no_update_kalman_filter(events, start_idx=None, end_idx=None, R_threshold=None, initial_pt=None,
+                                initial_state=None, print_output=False, dtype='f64', device=0):
+    """kf_workers.py:1060-1160 on the GPU: the window as KF_EVENT_PREDICT events (every update
+    of the reference's loop is commented out), logdet after each.  A dt < 0 event is skipped
+    without advancing the previous time (:1113-1116).  Returns (states, logdets, P,
+    previous_time, measurement_times), or None when no GPS fix starts a cold window."""
+    start_idx, end_idx = _window(events, start_idx, end_idx)
+    x0 = np.zeros(15)
+    mtimes = []
+    if initial_pt is not None and initial_state is not None:
+        P = np.asarray(initial_pt, np.float64)
+        x0[0:6] = initial_state[1:7]
+        prev = initial_state[0]
+        start_off = start_idx
+    else:
+        P = P0
+        cs = _cold_start(events, start_idx, end_idx)
+        if cs is None:
+            return None
+        x0, prev, start_off = cs
+        mtimes.append(prev)
+    t_first = prev
+    stream, times = [], []
+    for (_, stype, t, sdata) in events[start_off:end_idx]:
+        dt = t - prev
+        if dt < 0:
+            continue
+        stream.append((PREDICT, dt, [0.0] * 9))
+        times.append(t)
+        prev = t
+    tr, ld, _, _, Pb, _ = _run_streams([stream], x0[None], to_blocks(P)[None], dtype, device)
+    states = [(t_first, *tr[0, :, 0])] + [(t, *tr[i + 1, :, 0]) for i, t in enumerate(times)]
+    logdets = [float(v) for v in ld[:len(times) + 1, 0]]
+    if print_output:
+        print(f'No-update Kalman Filter (GPU): {len(times)} predictions from index {start_off} to {end_idx}')
     return states, logdets, from_blocks(Pb[:, 0]), prev, mtimes
 
 

@@ -16,7 +16,9 @@ Fixtures written (inputs and the reference's outputs, nothing else):
   ref15_combos.npz  evaluate_combo_chunk_worker (kf_workers.py:22-97) on k=1..3 subsets
   ref15_bruteforce.npz  run_brute_force_kalman_filter_no_sampling_min_usage (1218-1392)
   ref15_scheduled.npz   run_kalman_filter_scheduled (826-957), Scheduler.gain/cov_matrix (112-185)
-  ref8_full.npz     hw5_2.run_kalman_filter (hw5_2.py:313-380)
+  ref15_drivers.npz run_kalman_filter (kf_workers.py:738-824, states + per-step covariances)
+                    and run_no_update_kalman_filter (1060-1160), cold and warm
+  ref8_full.npz     hw5_2.run_kalman_filter (hw5_2.py:313-380), in-order and out-of-order streams
   cv_batch.npz      4/2 and 6/3 constant-velocity filters stepped with the reference's
                     own predict_covariance (kf_workers.py:546-549) and
                     calculate_kalman_gain (616-621), in the op order of 688-717
@@ -254,6 +256,31 @@ def ref15_scheduled(kfw):
     print('ref15_scheduled:', len(events), 'events; greedy120', len(o['greedy120_states']), 'selections')
 
 
+def ref15_drivers(kfw):
+    events = synth_events(seed=17, seconds=1.0)
+    sf = kfw.KF_SensorFusion('gps.csv', 'imu.csv')
+    sf.indexed_sensor_data = events
+    out = pack_events(events)
+    # run_kalman_filter: zero initial state, starts at the window's first GPS (kf_workers.py:738-824)
+    st, covs = sf.run_kalman_filter(0, len(events))
+    out.update(simple_states=np.array(st, dtype=np.float64), simple_covs=np.array(covs, dtype=np.float64))
+    s0, e0 = 37, 140   # a window that starts between GPS fixes
+    st, covs = sf.run_kalman_filter(s0, e0)
+    out.update(simple_win=np.array([s0, e0]), simple_win_states=np.array(st, dtype=np.float64),
+               simple_win_covs=np.array(covs, dtype=np.float64))
+    # run_no_update_kalman_filter: predictions only (kf_workers.py:1060-1160), cold and warm
+    st, ld, P, prev, mt = sf.run_no_update_kalman_filter(start_idx=0, end_idx=len(events))
+    out.update(noupd_states=np.array(st), noupd_logdets=np.array(ld), noupd_P=np.array(P),
+               noupd_prev=np.array(prev), noupd_mtimes=np.array(mt))
+    st_a, _, P_a, _ = sf.run_kalman_filter_full(start_idx=0, end_idx=60)
+    st, ld, P, prev, mt = sf.run_no_update_kalman_filter(start_idx=60, end_idx=100, initial_pt=P_a,
+                                                         initial_state=st_a[-1])
+    out.update(noupd_warm_P0=np.array(P_a), noupd_warm_state0=np.array(st_a[-1]), noupd_warm_states=np.array(st),
+               noupd_warm_logdets=np.array(ld), noupd_warm_P=np.array(P), noupd_warm_prev=np.array(prev))
+    np.savez_compressed(os.path.join(OUT, 'ref15_drivers.npz'), **out)
+    print('ref15_drivers:', len(events), 'events')
+
+
 def ref8_full(h5):
     events = synth_events(seed=13, seconds=1.5, out_of_order=False)
     sf = h5.KF_SensorFusion('gps.csv', 'imu.csv')
@@ -261,6 +288,12 @@ def ref8_full(h5):
     st = sf.run_kalman_filter()
     out = pack_events(events)
     out.update(states=np.array(st, dtype=np.float64))
+    # an out-of-order stream: hw5_2 has no dt < 0 guard, it predicts over the negative dt
+    ev2 = synth_events(seed=18, seconds=0.8, out_of_order=True)
+    sf.indexed_sensor_data = ev2
+    st2 = sf.run_kalman_filter()
+    out.update({'ooo_' + k: v for k, v in pack_events(ev2).items()})
+    out.update(ooo_states=np.array(st2, dtype=np.float64))
     np.savez_compressed(os.path.join(OUT, 'ref8_full.npz'), **out)
     print('ref8_full:', len(events), 'events')
 
@@ -326,7 +359,7 @@ if __name__ == '__main__':
     kfw, h5 = import_reference()
     gens = {'ref15_full': lambda: ref15_full(kfw), 'ref15_combos': lambda: ref15_combos(kfw),
             'ref15_bruteforce': lambda: ref15_bruteforce(kfw), 'ref15_scheduled': lambda: ref15_scheduled(kfw),
-            'ref8_full': lambda: ref8_full(h5), 'cv_batch': lambda: cv_batch(kfw)}
+            'ref15_drivers': lambda: ref15_drivers(kfw), 'ref8_full': lambda: ref8_full(h5), 'cv_batch': lambda: cv_batch(kfw)}
     for name in (sys.argv[1:] or list(gens)):
         gens[name]()
     # analytic known answer: slogdet(P0) of kf_workers.py:651 = 6 ln 1e4 + 9 ln 1e3

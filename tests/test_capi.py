@@ -28,10 +28,23 @@ def test_every_header_function_is_exported_and_bound():
     assert sorted(_lib.SIGNATURES) == names
 
 
+def test_binding_arity_matches_header_prototypes():
+    """Each ctypes argtypes list has as many entries as the C prototype has parameters."""
+    import re
+    text = re.sub(r'/\*.*?\*/', '', open(_lib.HEADER).read(), flags=re.S)
+    protos = dict(re.findall(r'\b(kf_\w+)\s*\(([^;{]*?)\)\s*;', text))
+    assert sorted(protos) == sorted(_lib.SIGNATURES)
+    for name, params in protos.items():
+        params = ' '.join(params.split())
+        n = 0 if params in ('', 'void') else params.count(',') + 1
+        assert len(_lib.SIGNATURES[name][1]) == n, (name, params)
+
+
 def test_header_constants_match_binding():
     text = open(_lib.HEADER).read()
     for name in ('KF_OK', 'KF_EINVAL', 'KF_EHIP', 'KF_ENOTSPD', 'KF_ENODEV', 'KF_ENOMEM',
-                 'KF_F32', 'KF_F64', 'KF_MODEL_CV2', 'KF_MODEL_CV3'):
+                 'KF_F32', 'KF_F64', 'KF_MODEL_CV2', 'KF_MODEL_CV3', 'KF_MODEL_REF15', 'KF_MODEL_REF8',
+                 'KF_EVENT_GPS', 'KF_EVENT_IMU', 'KF_EVENT_PREDICT', 'KF_EVENT_NONE'):
         import re
         m = re.search(rf'#define {name}\s+\(?(-?\d+)\)?', text)
         assert m, name

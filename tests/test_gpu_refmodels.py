@@ -1,0 +1,125 @@
+"""The reference's remaining drivers on the engine vs the reference's own outputs — needs an
+MI355X: run_kalman_filter (kf_workers.py:738-824, per-step covariances),
+run_no_update_kalman_filter (1060-1160) and hw5_2's 8-state filter (KF_MODEL_REF8,
+hw5_2.py:313-380), plus a random batched REF8 stream against the oracle's dense step.
+
+Tolerance (north_star): 1e-6 relative for fp64, normalised by max(|ref|, 1).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import kfmi
+from golden_events import unpack_events
+from kfmi import ref8, ref15
+from oracle import ref_kf
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+
+
+def _rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1.0))) if a.size else 0.0
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def test_run_kalman_filter_states_and_covariances(golden_dir):
+    g = _load(golden_dir, 'ref15_drivers.npz')
+    events = unpack_events(g)
+    st, covs = ref15.run_kalman_filter(events, 0, len(events))
+    assert np.array(st).shape == g['simple_states'].shape
+    assert _rel(st, g['simple_states']) <= TOL
+    assert np.array(covs).shape == g['simple_covs'].shape
+    assert _rel(covs, g['simple_covs']) <= TOL
+    s0, e0 = (int(v) for v in g['simple_win'])
+    st, covs = ref15.run_kalman_filter(events, s0, e0)
+    assert _rel(st, g['simple_win_states']) <= TOL
+    assert _rel(covs, g['simple_win_covs']) <= TOL
+
+
+def test_run_no_update_kalman_filter(golden_dir):
+    g = _load(golden_dir, 'ref15_drivers.npz')
+    events = unpack_events(g)
+    st, ld, P, prev, mt = ref15.run_no_update_kalman_filter(events, 0, len(events))
+    assert np.array(st).shape == g['noupd_states'].shape
+    assert _rel(st, g['noupd_states']) <= TOL
+    assert _rel(ld, g['noupd_logdets']) <= TOL
+    assert _rel(P, g['noupd_P']) <= TOL
+    assert prev == float(g['noupd_prev'])
+    np.testing.assert_array_equal(mt, g['noupd_mtimes'])
+    st, ld, P, prev, mt = ref15.run_no_update_kalman_filter(events, 60, 100, initial_pt=g['noupd_warm_P0'],
+                                                            initial_state=tuple(g['noupd_warm_state0']))
+    assert _rel(st, g['noupd_warm_states']) <= TOL
+    assert _rel(ld, g['noupd_warm_logdets']) <= TOL
+    assert _rel(P, g['noupd_warm_P']) <= TOL
+    assert prev == float(g['noupd_warm_prev']) and mt == []
+    # no GPS fix in a cold window -> None (kf_workers.py:1103-1105)
+    first_gps = next(i for i, e in enumerate(events) if e[1] == 'GPS')
+    if first_gps > 1:
+        assert ref15.run_no_update_kalman_filter(events, 0, first_gps) is None
+
+
+@pytest.mark.parametrize('prefix', ['', 'ooo_'])
+def test_ref8_run_kalman_filter(golden_dir, prefix):
+    g = _load(golden_dir, 'ref8_full.npz')
+    events = unpack_events(g, prefix)
+    st = ref8.run_kalman_filter(events)
+    assert np.array(st).shape == g[prefix + 'states'].shape
+    assert _rel(st, g[prefix + 'states']) <= TOL
+
+
+def test_ref8_random_batch_vs_oracle():
+    """B independent REF8 filters on random GPS/IMU/predict/padding streams with irregular dt,
+    against the oracle's dense 8x8 reference-order step (hw5_2.py:336-366)."""
+    rng = np.random.default_rng(8)
+    B, T = 257, 36
+    etype = rng.choice([0, 1, 1, 2], size=(T, B)).astype(np.uint8)
+    etype[28:, ::4] = 255
+    dt = rng.uniform(0.0, 0.1, (T, B))
+    pay = np.zeros((T, 9, B))
+    pay[:, 0:3] = rng.normal(0, 20, (T, 3, B))
+    pay[:, 3:6] = rng.normal(0, 0.05, (T, 3, B))
+    pay[:, 6:9] = rng.normal(0, 0.5, (T, 3, B))
+    x0 = rng.normal(0, 5, (B, 8))
+    kf = kfmi.BatchedKF('ref8', B, 'f64')
+    kf.reset(torch.from_numpy(np.ascontiguousarray(x0.T)).cuda())
+    tr, ld, up, cv = kf.run_events(etype, dt, pay, updated=True, cov=True)
+    tr, ld, cv = tr.cpu().numpy(), ld.cpu().numpy(), cv.cpu().numpy()
+    x, Pb = kf.state()
+    x, Pb = x.cpu().numpy(), Pb.cpu().numpy()
+    assert tr.shape == (T, 3, B) and cv.shape == (T, 15, B)
+    assert (kf.status().cpu().numpy() == 0).all()
+    for f in range(0, B, 5):
+        xf, Pf = x0[f].copy(), ref8.P0.copy()
+        for t in range(T):
+            ty = etype[t, f]
+            if ty == 2:
+                F = ref_kf.F_ref8(dt[t, f])
+                xf = F @ xf
+                Pf = ref_kf.predict_covariance(Pf, F, ref_kf.Q_ref8(dt[t, f]))
+            elif ty in (0, 1):
+                sdata = ({'easting': pay[t, 0, f], 'northing': pay[t, 1, f]} if ty == 0
+                         else ['t', *pay[t, :, f]])
+                xf, Pf = ref_kf.step8(xf, Pf, 'GPS' if ty == 0 else 'IMU', sdata, dt[t, f])
+            assert _rel(tr[t, :, f], xf[:3]) <= TOL, (f, t)
+            assert _rel(ref15.from_blocks(cv[t, :, f]), Pf) <= TOL, (f, t)
+            ref_ld = np.linalg.slogdet(Pf)[1]
+            assert abs(ld[t, f] - ref_ld) <= TOL * max(1.0, abs(ref_ld))
+        assert _rel(x[:, f], xf) <= TOL
+        assert _rel(ref15.from_blocks(Pb[:, f]), Pf) <= TOL
+
+
+def test_ref8_handle_rejects_ref15_only_entry_points():
+    kf = kfmi.BatchedKF('ref8', 4, 'f64')
+    with pytest.raises(kfmi.KFError):
+        kf.predict(0.1)
+    for call in (lambda: kf.score_candidates([0]), lambda: kf.eval_combos(np.zeros((2, 11)), np.zeros(42), 0, 1, 1)):
+        with pytest.raises(ValueError):
+            call()

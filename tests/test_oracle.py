@@ -83,6 +83,37 @@ def test_ref8_full(golden_dir):
     events = unpack_events(g)
     st, _ = ref_kf.run_kalman_filter_8state(events)
     assert _rel(st, g['states']) < RTOL
+    st, _ = ref_kf.run_kalman_filter_8state(unpack_events(g, 'ooo_'))
+    assert _rel(st, g['ooo_states']) < RTOL
+
+
+def test_ref15_run_kalman_filter_simple(golden_dir):
+    g = _load(golden_dir, 'ref15_drivers.npz')
+    events = unpack_events(g)
+    st, covs = ref_kf.run_kalman_filter_simple(events, 0, len(events))
+    assert _rel(st, g['simple_states']) < RTOL
+    assert _rel(covs, g['simple_covs']) < RTOL
+    s0, e0 = (int(v) for v in g['simple_win'])
+    st, covs = ref_kf.run_kalman_filter_simple(events, s0, e0)
+    assert _rel(st, g['simple_win_states']) < RTOL
+    assert _rel(covs, g['simple_win_covs']) < RTOL
+
+
+def test_ref15_no_update(golden_dir):
+    g = _load(golden_dir, 'ref15_drivers.npz')
+    events = unpack_events(g)
+    st, ld, P, prev, mt = ref_kf.run_no_update(events, 0, len(events))
+    assert _rel(st, g['noupd_states']) < RTOL
+    assert _rel(ld, g['noupd_logdets']) < RTOL
+    assert _rel(P, g['noupd_P']) < RTOL
+    assert prev == float(g['noupd_prev'])
+    np.testing.assert_array_equal(mt, g['noupd_mtimes'])
+    st, ld, P, prev, mt = ref_kf.run_no_update(events, 60, 100, initial_pt=g['noupd_warm_P0'],
+                                               initial_state=tuple(g['noupd_warm_state0']))
+    assert _rel(st, g['noupd_warm_states']) < RTOL
+    assert _rel(ld, g['noupd_warm_logdets']) < RTOL
+    assert _rel(P, g['noupd_warm_P']) < RTOL
+    assert mt == []
 
 
 @pytest.mark.parametrize('d', [2, 3])
