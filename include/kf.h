@@ -222,6 +222,65 @@ int kf_run_scheduled(kf_batch* handle, int T, const double* t, const uint8_t* et
                      const double* prev_time, const double* freq, double freq_all, void* traj, void* logdet,
                      double* sel_time, int32_t* n_sel, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Ingest: CSV logs -> one merged event stream in HBM (the reference's load_data,
+ * gps_to_modified_utm, compute_imu_biases, unbias_imu_data, combine_sensor_data;
+ * kf_workers.py:290-385, hw5_2.py:15-119).
+ * --------------------------------------------------------------------------------------- */
+
+/* Data rows and the field count of the first data row of a CSV file (header skipped when
+ * has_header; trailing blank lines are not rows).  Host-only, no GPU needed. */
+int kf_csv_shape(const char* path, int has_header, int64_t* rows, int* cols);
+
+/* Parse the first ncols fields of each of `rows` data rows into host out[col * ld + row]
+ * (column-major doubles).  A field containing "nan" in any case becomes NaN (the reference's
+ * 'nan' in s.lower() test, kf_workers.py:310, 336); any other field must parse as Python's
+ * float() would, else KF_EINVAL naming the row and column.  Multithreaded, host-only.
+ * Replaces load_data_from_csv (kf_workers.py:290-298) + the float() calls at each use. */
+int kf_csv_read(const char* path, int has_header, int ncols, double* out, int64_t ld, int64_t rows);
+
+#define KF_INGEST_GPS_ALTITUDE 1  /* kf_workers.py:310: drop a fix whose altitude is 'nan' too;
+                                     0 = hw5_2.py:35 (latitude/longitude only)              */
+
+typedef struct kf_ingest_info {
+    int64_t n_events;           /* fixes kept + IMU rows                                    */
+    int64_t n_fixes;            /* len(utm_data)                                            */
+    int64_t n_imu;
+    int64_t first_valid_index;  /* compute_imu_biases: first GPS row with a latitude        */
+    int64_t origin_row;         /* GPS row of the first kept fix (UTM origin), -1 if none   */
+    double gyro_bias[3];        /* angular_velocity_bias                                    */
+    double accel_bias[3];       /* linear_acceleration_bias                                 */
+    double utm_origin[2];       /* easting/northing subtracted from every fix               */
+} kf_ingest_info;
+
+/* Build the merged event stream.  gps device [4][ld_gps] (time, latitude, longitude,
+ * altitude), imu device [11][ld_imu] (time, orientation x y z w, angular velocity x y z,
+ * linear acceleration x y z) — the column layouts hw5_1.py:14-38 writes.  Outputs (device,
+ * capacity >= n_gps + n_imu; info->n_events rows written): etype [N] (KF_EVENT_GPS/IMU),
+ * t [N], payload [N][9] — fix: (easting - e0, northing - n0, altitude, 0...), the UTM
+ * projection of the `utm` package; IMU: (roll, pitch, yaw, w - bias_w, a - bias_a) —
+ * src [N] (position in utm_data for a fix, IMU row index), zone_number [N], zone_letter [N]
+ * (0 for IMU rows); src/zone_* may be NULL.  Events are ordered by time, fixes first on ties
+ * (Python's stable sort, kf_workers.py:384).  Synchronous (the event count is returned).
+ * KF_EINVAL when no GPS row has a latitude (the reference's biases are undefined then). */
+int kf_ingest(const double* gps, int64_t n_gps, int64_t ld_gps, const double* imu, int64_t n_imu, int64_t ld_imu,
+              int flags, uint8_t* etype, double* t, double* payload, int32_t* src, int8_t* zone_number,
+              char* zone_letter, kf_ingest_info* info, void* stream);
+
+/* Time since the previous event for a driver over a merged stream, computed on the device.
+ *   KF_DT_FULL      run_kalman_filter_full (kf_workers.py:682-686): previous = the previous
+ *                   event's time; a negative dt marks the event KF_EVENT_NONE (skipped)
+ *   KF_DT_MONOTONE  adaptive / no-update drivers and the combination worker (:1012-1016,
+ *                   :1113-1116, :38-40): a skipped event does not move the previous time
+ *   KF_DT_RAW       run_kalman_filter / hw5_2 (:763-767, hw5_2.py:331-336): no guard
+ * t/etype_in/dt/etype_out device [n]; prev0 = the time of the state the run starts from;
+ * etype_in NULL = all KF_EVENT_IMU; etype_out may be NULL. */
+#define KF_DT_FULL     0
+#define KF_DT_MONOTONE 1
+#define KF_DT_RAW      2
+int kf_events_dt(int64_t n, const double* t, const uint8_t* etype_in, double prev0, int rule, double* dt,
+                 uint8_t* etype_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

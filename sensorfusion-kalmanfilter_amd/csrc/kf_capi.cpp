@@ -30,6 +30,7 @@ namespace {
 
 thread_local std::string g_err;
 
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
@@ -111,6 +112,18 @@ kfmi::RefArgs ref_args(const kf_batch* h) {
 }
 
 }  // namespace
+
+namespace kfmi {
+int set_error(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+}  // namespace kfmi
 
 extern "C" {
 

@@ -1,0 +1,438 @@
+// gfx950 ingest: parsed GPS/IMU columns -> one merged, time-sorted event stream in HBM
+// (kf_ingest), and the per-event dt of the reference drivers (kf_events_dt).
+//
+// Replaces the per-row Python of KF_SensorFusion (kf_workers.py:304-385):
+//   gps_to_modified_utm (304-331)  -> fix_kernel: keep/drop test, UTM projection per fix
+//   compute_imu_biases (333-347)   -> bias_kernel: mean of the first first_valid_index IMU rows
+//   unbias_imu_data (349-373) with quaternion_to_euler (399-425)
+//                                  -> fused into gather_kernel, computed once per IMU event
+//   combine_sensor_data (375-385)  -> stable radix sort on time of [fixes..., IMU rows...]
+//                                     (hipCUB), so ties keep GPS first as Python's stable sort
+//                                     does, then gather_kernel writes the SoA stream
+// Everything is fp64, as in the reference.  Expressions are evaluated in the reference's order
+// with FMA contraction off, so the only differences left are the last-ulp behaviour of the
+// transcendental functions (sin/cos/atan2/asin vs the host libm).
+//
+// Output stream layout (one row per event, the [T][9] payload layout kf_run_events reads for a
+// single filter): etype [N] uint8, t [N] f64, payload [N][9] f64, src [N] int32 (position in
+// the reference's utm_data list for a fix, IMU row index for an IMU sample).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include "../../include/kf.h"
+#include "kf_internal.h"
+
+namespace kfmi {
+namespace {
+
+constexpr int kIngBlock = 256;
+
+// --- utm.from_latlon (published algorithm of the `utm` package; oracle/ref_ingest.py) --------
+constexpr double kK0 = 0.9996;
+constexpr double kE = 0.00669438;
+constexpr double kE2 = kE * kE;
+constexpr double kE3 = kE2 * kE;
+constexpr double kEP2 = kE / (1 - kE);
+constexpr double kM1 = (1 - kE / 4 - 3 * kE2 / 64 - 5 * kE3 / 256);
+constexpr double kM2 = (3 * kE / 8 + 3 * kE2 / 32 + 45 * kE3 / 1024);
+constexpr double kM3 = (15 * kE2 / 256 + 45 * kE3 / 1024);
+constexpr double kM4 = (35 * kE3 / 3072);
+constexpr double kR = 6378137.0;
+constexpr double kPi = 3.141592653589793;
+
+__device__ __forceinline__ double radians(double d) {
+#pragma clang fp contract(off)
+    return d * (kPi / 180.0);  // math.radians: x * (pi / 180)
+}
+
+__device__ __forceinline__ int zone_number(double lat, double lon) {
+    if (56 <= lat && lat < 64 && 3 <= lon && lon < 12) return 32;
+    if (72 <= lat && lat <= 84 && lon >= 0) {
+        if (lon < 9) return 31;
+        if (lon < 21) return 33;
+        if (lon < 33) return 35;
+        if (lon < 42) return 37;
+    }
+    return static_cast<int>((lon + 180) / 6) + 1;  // int() truncates toward zero
+}
+
+__device__ __forceinline__ char zone_letter(double lat) {
+    const char letters[] = "CDEFGHJKLMNPQRSTUVWXX";
+    if (!(-80 <= lat && lat <= 84)) return 0;
+    return letters[static_cast<int>(lat + 80) >> 3];
+}
+
+__device__ void utm_from_latlon(double lat, double lon, double& easting, double& northing, int& zn, char& zl) {
+#pragma clang fp contract(off)
+    const double lat_rad = radians(lat);
+    const double lat_sin = sin(lat_rad);
+    const double lat_cos = cos(lat_rad);
+    const double lat_tan = lat_sin / lat_cos;
+    const double lat_tan2 = lat_tan * lat_tan;
+    const double lat_tan4 = lat_tan2 * lat_tan2;
+    zn = zone_number(lat, lon);
+    zl = zone_letter(lat);
+    const double lon_rad = radians(lon);
+    const double central_lon_rad = radians(static_cast<double>((zn - 1) * 6 - 180 + 3));
+    const double n = kR / sqrt(1 - kE * (lat_sin * lat_sin));
+    const double c = kEP2 * (lat_cos * lat_cos);
+    const double a = lat_cos * (lon_rad - central_lon_rad);
+    const double a2 = a * a, a3 = pow(a, 3.0), a4 = pow(a, 4.0), a5 = pow(a, 5.0), a6 = pow(a, 6.0);
+    const double m = kR * (kM1 * lat_rad - kM2 * sin(2 * lat_rad) + kM3 * sin(4 * lat_rad) - kM4 * sin(6 * lat_rad));
+    easting = kK0 * n * (a + a3 / 6 * (1 - lat_tan2 + c) + a5 / 120 * (5 - 18 * lat_tan2 + lat_tan4 + 72 * c - 58 * kEP2)) +
+              500000;
+    northing = kK0 * (m + n * lat_tan * (a2 / 2 + a4 / 24 * (5 - lat_tan2 + 9 * c + 4 * (c * c)) +
+                                         a6 / 720 * (61 - 58 * lat_tan2 + lat_tan4 + 600 * c - 330 * kEP2)));
+    if (lat < 0) northing += 10000000;
+}
+
+// quaternion_to_euler (kf_workers.py:399-425)
+__device__ void quat_to_euler(double x, double y, double z, double w, double& roll, double& pitch, double& yaw) {
+#pragma clang fp contract(off)
+    const double sinr_cosp = 2 * (w * x + y * z);
+    const double cosr_cosp = 1 - 2 * (x * x + y * y);
+    roll = atan2(sinr_cosp, cosr_cosp);
+    const double sinp = 2 * (w * y - z * x);
+    if (fabs(sinp) >= 1)
+        pitch = kPi / 2 * (sinp > 0 ? 1.0 : -1.0);  // np.pi / 2 * np.sign(sinp)
+    else
+        pitch = asin(sinp);
+    const double siny_cosp = 2 * (w * z + x * y);
+    const double cosy_cosp = 1 - 2 * (y * y + z * z);
+    yaw = atan2(siny_cosp, cosy_cosp);
+}
+
+struct IngestArgs {
+    int64_t n_gps, n_imu;
+    int64_t ld_gps, ld_imu;
+    const double* gps;          // [4][ld_gps]: time, latitude, longitude, altitude
+    const double* imu;          // [11][ld_imu]: time, qx, qy, qz, qw, wx, wy, wz, ax, ay, az
+    int check_alt;
+    double* east;               // [n_gps] workspace
+    double* north;
+    int8_t* zone;               // [n_gps] zone number (0: not kept)
+    char* letter;
+    int32_t* keep;              // [n_gps] 0/1
+    unsigned long long* first;  // [2]: first row with a latitude, first kept row
+    double* bias;               // [6]: angular velocity, linear acceleration
+    double* keys;               // [n_gps + n_imu]
+    int32_t* vals;
+};
+
+__global__ __launch_bounds__(kIngBlock) void fix_kernel(const IngestArgs a) {
+    const int64_t i = int64_t(blockIdx.x) * kIngBlock + threadIdx.x;
+    if (i >= a.n_gps) return;
+    const double t = a.gps[i];
+    const double lat = a.gps[a.ld_gps + i];
+    const double lon = a.gps[2 * a.ld_gps + i];
+    const double alt = a.gps[3 * a.ld_gps + i];
+    const bool lat_ok = !isnan(lat);
+    const bool kept = lat_ok && !isnan(lon) && !(a.check_alt && isnan(alt));  // kf_workers.py:310 / hw5_2.py:35
+    if (lat_ok) atomicMin(&a.first[0], static_cast<unsigned long long>(i));
+    double e = 0, n = 0;
+    int zn = 0;
+    char zl = 0;
+    if (kept) {
+        atomicMin(&a.first[1], static_cast<unsigned long long>(i));
+        utm_from_latlon(lat, lon, e, n, zn, zl);
+    }
+    a.east[i] = e;
+    a.north[i] = n;
+    a.zone[i] = static_cast<int8_t>(zn);
+    a.letter[i] = zl;
+    a.keep[i] = kept ? 1 : 0;
+    a.keys[i] = kept ? t : __builtin_inf();  // dropped fixes sort past every event
+    a.vals[i] = static_cast<int32_t>(i);
+}
+
+__global__ __launch_bounds__(kIngBlock) void imu_keys_kernel(const IngestArgs a) {
+    const int64_t j = int64_t(blockIdx.x) * kIngBlock + threadIdx.x;
+    if (j >= a.n_imu) return;
+    a.keys[a.n_gps + j] = a.imu[j];
+    a.vals[a.n_gps + j] = static_cast<int32_t>(a.n_gps + j);
+}
+
+// compute_imu_biases: np.mean over axis 0 of the first first_valid_index rows, i.e. a sequential
+// row-by-row sum per component divided by the count (NaN for an empty slice, as NumPy gives).
+__global__ void bias_kernel(const IngestArgs a) {
+    const int k = threadIdx.x;
+    if (k >= 6) return;
+    const unsigned long long f = a.first[0];
+    const int64_t cnt = static_cast<int64_t>(f < static_cast<unsigned long long>(a.n_imu) ? f : a.n_imu);
+    const double* col = a.imu + (5 + k) * a.ld_imu;
+    double s = 0.0;
+    for (int64_t r = 0; r < cnt; ++r) s += col[r];
+    a.bias[k] = s / static_cast<double>(cnt);
+}
+
+struct GatherArgs {
+    int64_t n_events, n_gps, ld_gps, ld_imu;
+    const double* gps;
+    const double* imu;
+    const int32_t* vals;   // sorted source ids
+    const int32_t* pos;    // exclusive scan of keep: fix id -> utm_data position
+    const double* east;
+    const double* north;
+    const int8_t* zone;
+    const char* letter;
+    const unsigned long long* first;
+    const double* bias;
+    uint8_t* etype;
+    double* t;
+    double* payload;       // [N][9]
+    int32_t* src;
+    int8_t* zone_out;
+    char* letter_out;
+};
+
+__global__ __launch_bounds__(kIngBlock) void gather_kernel(const GatherArgs a) {
+#pragma clang fp contract(off)
+    const int64_t p = int64_t(blockIdx.x) * kIngBlock + threadIdx.x;
+    if (p >= a.n_events) return;
+    const int64_t v = a.vals[p];
+    double pay[9];
+    if (v < a.n_gps) {
+        const int64_t o = static_cast<int64_t>(a.first[1]);
+        a.etype[p] = KF_EVENT_GPS;
+        a.t[p] = a.gps[v];
+        pay[0] = a.east[v] - a.east[o];    // kf_workers.py:325-328
+        pay[1] = a.north[v] - a.north[o];
+        pay[2] = a.gps[3 * a.ld_gps + v];  // altitude
+#pragma unroll
+        for (int k = 3; k < 9; ++k) pay[k] = 0.0;
+        if (a.src) a.src[p] = a.pos[v];
+        if (a.zone_out) a.zone_out[p] = a.zone[v];
+        if (a.letter_out) a.letter_out[p] = a.letter[v];
+    } else {
+        const int64_t j = v - a.n_gps;
+        const double* q = a.imu + j;
+        a.etype[p] = KF_EVENT_IMU;
+        a.t[p] = q[0];
+        quat_to_euler(q[1 * a.ld_imu], q[2 * a.ld_imu], q[3 * a.ld_imu], q[4 * a.ld_imu], pay[0], pay[1], pay[2]);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) pay[3 + k] = q[(5 + k) * a.ld_imu] - a.bias[k];  // kf_workers.py:358-359
+        if (a.src) a.src[p] = static_cast<int32_t>(j);
+        if (a.zone_out) a.zone_out[p] = 0;
+        if (a.letter_out) a.letter_out[p] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a.payload[p * 9 + k] = pay[k];
+}
+
+// kf_events_dt.  rule 0 (run_kalman_filter_full, kf_workers.py:682-686): the previous time is
+// the previous event's time whether or not that event was skipped; rule 1 (adaptive / no-update
+// drivers and the combination worker, :1012-1016, :38-40): a skipped event leaves the previous
+// time alone, so it is the running maximum of the times before; rule 2 (run_kalman_filter,
+// :763-767, hw5_2.py:331-336): no guard, negative dt is predicted over.
+__global__ __launch_bounds__(kIngBlock) void dt_kernel(int64_t n, const double* t, const double* prev,
+                                                        const uint8_t* et_in, double prev0, int rule, double* dt,
+                                                        uint8_t* et_out) {
+    const int64_t i = int64_t(blockIdx.x) * kIngBlock + threadIdx.x;
+    if (i >= n) return;
+    double p;
+    if (rule == 1)
+        p = prev[i];
+    else
+        p = i == 0 ? prev0 : t[i - 1];
+    const double d = t[i] - p;
+    const uint8_t e = et_in ? et_in[i] : uint8_t(KF_EVENT_IMU);
+    dt[i] = d;
+    if (et_out) et_out[i] = (rule != 2 && d < 0) ? uint8_t(KF_EVENT_NONE) : e;
+}
+
+struct MaxOp {
+    __device__ __forceinline__ double operator()(double a, double b) const { return b > a ? b : a; }
+};
+
+unsigned grid(int64_t n) { return static_cast<unsigned>((n + kIngBlock - 1) / kIngBlock); }
+
+}  // namespace
+}  // namespace kfmi
+
+using namespace kfmi;
+
+namespace {
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+int hip_err(hipError_t e, const char* what) {
+    return set_error(KF_EHIP, "%s: %s (%d)", what, hipGetErrorString(e), static_cast<int>(e));
+}
+}  // namespace
+
+#define KF_TRY(expr, what)                          \
+    do {                                            \
+        hipError_t e_ = (expr);                     \
+        if (e_ != hipSuccess) return hip_err(e_, what); \
+    } while (0)
+
+extern "C" {
+
+int kf_ingest(const double* gps, int64_t n_gps, int64_t ld_gps, const double* imu, int64_t n_imu, int64_t ld_imu,
+              int flags, uint8_t* etype, double* t, double* payload, int32_t* src, int8_t* zone_number,
+              char* zone_letter, kf_ingest_info* info, void* stream) {
+    if (n_gps < 0 || n_imu < 0) return set_error(KF_EINVAL, "kf_ingest: negative row count");
+    if ((n_gps && (!gps || ld_gps < n_gps)) || (n_imu && (!imu || ld_imu < n_imu)))
+        return set_error(KF_EINVAL, "kf_ingest: null column array or leading dimension below the row count");
+    if (n_gps + n_imu >= (int64_t(1) << 31)) return set_error(KF_EINVAL, "kf_ingest: more than 2^31 rows");
+    if (!etype || !t || !payload || !info) return set_error(KF_EINVAL, "kf_ingest: null output");
+    if (flags & ~KF_INGEST_GPS_ALTITUDE) return set_error(KF_EINVAL, "kf_ingest: unknown flags 0x%x", flags);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int64_t nk = n_gps + n_imu;
+
+    // one workspace: east, north, keys, keys_sorted (8 B); keep, pos, vals, vals_sorted (4 B);
+    // zone, letter (1 B); first[2], bias[6]; then hipCUB temporaries
+    size_t sort_tmp = 0, scan_tmp = 0;
+    KF_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (double*)nullptr, (double*)nullptr, (int32_t*)nullptr,
+                                              (int32_t*)nullptr, static_cast<int>(nk), 0, 64, st),
+           "kf_ingest sort sizing");
+    KF_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (int32_t*)nullptr, (int32_t*)nullptr,
+                                            static_cast<int>(n_gps), st),
+           "kf_ingest scan sizing");
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t g8 = al(8 * std::max<int64_t>(n_gps, 1)), k8 = al(8 * std::max<int64_t>(nk, 1));
+    const size_t g4 = al(4 * std::max<int64_t>(n_gps, 1)), k4 = al(4 * std::max<int64_t>(nk, 1));
+    const size_t g1 = al(std::max<int64_t>(n_gps, 1));
+    const size_t bytes = 2 * g8 + 2 * k8 + 2 * g4 + 2 * k4 + 2 * g1 + al(8 * 8) + al(std::max(sort_tmp, scan_tmp));
+    DevBuf ws;
+    KF_TRY(hipMalloc(&ws.p, bytes), "kf_ingest workspace");
+    char* w = static_cast<char*>(ws.p);
+    IngestArgs a{};
+    a.n_gps = n_gps;
+    a.n_imu = n_imu;
+    a.ld_gps = ld_gps;
+    a.ld_imu = ld_imu;
+    a.gps = gps;
+    a.imu = imu;
+    a.check_alt = (flags & KF_INGEST_GPS_ALTITUDE) ? 1 : 0;
+    a.east = reinterpret_cast<double*>(w); w += g8;
+    a.north = reinterpret_cast<double*>(w); w += g8;
+    a.keys = reinterpret_cast<double*>(w); w += k8;
+    double* keys_sorted = reinterpret_cast<double*>(w); w += k8;
+    a.keep = reinterpret_cast<int32_t*>(w); w += g4;
+    int32_t* pos = reinterpret_cast<int32_t*>(w); w += g4;
+    a.vals = reinterpret_cast<int32_t*>(w); w += k4;
+    int32_t* vals_sorted = reinterpret_cast<int32_t*>(w); w += k4;
+    a.zone = reinterpret_cast<int8_t*>(w); w += g1;
+    a.letter = w; w += g1;
+    a.first = reinterpret_cast<unsigned long long*>(w);
+    a.bias = reinterpret_cast<double*>(w + 16);
+    w += al(8 * 8);
+    void* tmp = w;
+
+    const unsigned long long none[2] = {~0ull, ~0ull};
+    KF_TRY(hipMemcpyAsync(a.first, none, sizeof none, hipMemcpyHostToDevice, st), "kf_ingest init");
+    if (n_gps) {
+        fix_kernel<<<grid(n_gps), kIngBlock, 0, st>>>(a);
+        KF_TRY(hipGetLastError(), "kf_ingest fix_kernel");
+    }
+    if (n_imu) {
+        imu_keys_kernel<<<grid(n_imu), kIngBlock, 0, st>>>(a);
+        KF_TRY(hipGetLastError(), "kf_ingest imu_keys_kernel");
+    }
+    bias_kernel<<<1, 64, 0, st>>>(a);
+    KF_TRY(hipGetLastError(), "kf_ingest bias_kernel");
+    if (n_gps) {
+        size_t tb = scan_tmp;
+        KF_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, a.keep, pos, static_cast<int>(n_gps), st), "kf_ingest scan");
+    }
+    if (nk) {
+        size_t tb = sort_tmp;
+        KF_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, a.keys, keys_sorted, a.vals, vals_sorted,
+                                                  static_cast<int>(nk), 0, 64, st),
+               "kf_ingest sort");
+    }
+    unsigned long long first[2];
+    double bias[6];
+    int32_t last_pos = 0, last_keep = 0;
+    KF_TRY(hipMemcpyAsync(first, a.first, sizeof first, hipMemcpyDeviceToHost, st), "kf_ingest readback");
+    KF_TRY(hipMemcpyAsync(bias, a.bias, sizeof bias, hipMemcpyDeviceToHost, st), "kf_ingest readback");
+    if (n_gps) {
+        KF_TRY(hipMemcpyAsync(&last_pos, pos + n_gps - 1, 4, hipMemcpyDeviceToHost, st), "kf_ingest readback");
+        KF_TRY(hipMemcpyAsync(&last_keep, a.keep + n_gps - 1, 4, hipMemcpyDeviceToHost, st), "kf_ingest readback");
+    }
+    KF_TRY(hipStreamSynchronize(st), "kf_ingest sync");
+    if (first[0] == ~0ull)
+        return set_error(KF_EINVAL, "kf_ingest: no GPS row has a latitude (compute_imu_biases finds no "
+                                    "first valid index, kf_workers.py:336-338)");
+    const int64_t n_fix = last_pos + last_keep;
+    GatherArgs g{};
+    g.n_events = n_fix + n_imu;
+    g.n_gps = n_gps;
+    g.ld_gps = ld_gps;
+    g.ld_imu = ld_imu;
+    g.gps = gps;
+    g.imu = imu;
+    g.vals = vals_sorted;
+    g.pos = pos;
+    g.east = a.east;
+    g.north = a.north;
+    g.zone = a.zone;
+    g.letter = a.letter;
+    g.first = a.first;
+    g.bias = a.bias;
+    g.etype = etype;
+    g.t = t;
+    g.payload = payload;
+    g.src = src;
+    g.zone_out = zone_number;
+    g.letter_out = zone_letter;
+    if (g.n_events) {
+        gather_kernel<<<grid(g.n_events), kIngBlock, 0, st>>>(g);
+        KF_TRY(hipGetLastError(), "kf_ingest gather_kernel");
+    }
+    double origin[2] = {0.0, 0.0};
+    if (n_fix) {
+        KF_TRY(hipMemcpyAsync(&origin[0], a.east + first[1], 8, hipMemcpyDeviceToHost, st), "kf_ingest readback");
+        KF_TRY(hipMemcpyAsync(&origin[1], a.north + first[1], 8, hipMemcpyDeviceToHost, st), "kf_ingest readback");
+    }
+    KF_TRY(hipStreamSynchronize(st), "kf_ingest sync");
+    info->n_events = g.n_events;
+    info->n_fixes = n_fix;
+    info->n_imu = n_imu;
+    info->first_valid_index = static_cast<int64_t>(first[0]);
+    info->origin_row = n_fix ? static_cast<int64_t>(first[1]) : -1;
+    for (int k = 0; k < 3; ++k) {
+        info->gyro_bias[k] = bias[k];
+        info->accel_bias[k] = bias[3 + k];
+    }
+    info->utm_origin[0] = origin[0];
+    info->utm_origin[1] = origin[1];
+    return KF_OK;
+}
+
+int kf_events_dt(int64_t n, const double* t, const uint8_t* etype_in, double prev0, int rule, double* dt,
+                 uint8_t* etype_out, void* stream) {
+    if (n < 0) return set_error(KF_EINVAL, "kf_events_dt: n = %lld", (long long)n);
+    if (rule < KF_DT_FULL || rule > KF_DT_RAW) return set_error(KF_EINVAL, "kf_events_dt: unknown rule %d", rule);
+    if (n == 0) return KF_OK;
+    if (!t || !dt) return set_error(KF_EINVAL, "kf_events_dt: null t/dt");
+    if (n >= (int64_t(1) << 31)) return set_error(KF_EINVAL, "kf_events_dt: more than 2^31 events");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    DevBuf ws;
+    const double* prev = nullptr;
+    if (rule == KF_DT_MONOTONE) {
+        size_t tmp = 0;
+        KF_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, tmp, t, (double*)nullptr, MaxOp{}, prev0, static_cast<int>(n), st),
+               "kf_events_dt scan sizing");
+        const size_t pb = (8 * size_t(n) + 255) & ~size_t(255);
+        KF_TRY(hipMalloc(&ws.p, pb + tmp), "kf_events_dt workspace");
+        double* pm = static_cast<double*>(ws.p);
+        KF_TRY(hipcub::DeviceScan::ExclusiveScan(static_cast<char*>(ws.p) + pb, tmp, t, pm, MaxOp{}, prev0,
+                                                 static_cast<int>(n), st),
+               "kf_events_dt scan");
+        prev = pm;
+    }
+    dt_kernel<<<grid(n), kIngBlock, 0, st>>>(n, t, prev, etype_in, prev0, rule, dt, etype_out);
+    KF_TRY(hipGetLastError(), "kf_events_dt");
+    if (ws.p) KF_TRY(hipStreamSynchronize(st), "kf_events_dt sync");  // before the workspace goes
+    return KF_OK;
+}
+
+}  // extern "C"

@@ -129,4 +129,7 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
 
 constexpr int kBlock = 256;  // 4 wave64 per workgroup
 
+// Record the thread-local message kf_last_error returns; returns `code` (kf_capi.cpp).
+int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
 }  // namespace kfmi

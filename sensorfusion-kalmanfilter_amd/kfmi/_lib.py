@@ -30,6 +30,10 @@ KF_EVENT_GPS = 0
 KF_EVENT_IMU = 1
 KF_EVENT_PREDICT = 2
 KF_EVENT_NONE = 255
+KF_INGEST_GPS_ALTITUDE = 1
+KF_DT_FULL = 0
+KF_DT_MONOTONE = 1
+KF_DT_RAW = 2
 
 _ERRNAMES = {KF_EINVAL: 'KF_EINVAL', KF_EHIP: 'KF_EHIP', KF_ENOTSPD: 'KF_ENOTSPD',
              KF_ENODEV: 'KF_ENODEV', KF_ENOMEM: 'KF_ENOMEM'}
@@ -46,6 +50,13 @@ class KFError(RuntimeError):
 class kf_params(ctypes.Structure):
     _fields_ = [('q_pos', ctypes.c_double), ('q_vel', ctypes.c_double),
                 ('r', ctypes.c_double * 9), ('p0_pos', ctypes.c_double), ('p0_vel', ctypes.c_double)]
+
+
+class kf_ingest_info(ctypes.Structure):
+    _fields_ = [('n_events', ctypes.c_int64), ('n_fixes', ctypes.c_int64), ('n_imu', ctypes.c_int64),
+                ('first_valid_index', ctypes.c_int64), ('origin_row', ctypes.c_int64),
+                ('gyro_bias', ctypes.c_double * 3), ('accel_bias', ctypes.c_double * 3),
+                ('utm_origin', ctypes.c_double * 2)]
 
 
 _vp = ctypes.c_void_p
@@ -76,6 +87,11 @@ SIGNATURES = {
     'kf_eval_combos': (_i, [_vp, _i, _vp, _vp, _d, _d, _i, ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     'kf_score_candidates': (_i, [_vp, _i, _vp, _i, _vp, _vp]),
     'kf_run_scheduled': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _d, _vp, _vp, _vp, _vp, _vp]),
+    'kf_csv_shape': (_i, [ctypes.c_char_p, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i)]),
+    'kf_csv_read': (_i, [ctypes.c_char_p, _i, _i, _vp, _i64, _i64]),
+    'kf_ingest': (_i, [_vp, _i64, _i64, _vp, _i64, _i64, _i, _vp, _vp, _vp, _vp, _vp, _vp,
+                       ctypes.POINTER(kf_ingest_info), _vp]),
+    'kf_events_dt': (_i, [_i64, _vp, _vp, _d, _i, _vp, _vp, _vp]),
 }
 
 _lib = None

@@ -150,7 +150,19 @@ def _cold_start(events, start_idx, stop):
 def run_kalman_filter_full(events, start_idx=None, end_idx=None, initial_pt=None, initial_state=None,
                            print_output=False, dtype='f64', device=0):
     """kf_workers.py:623-728 on the GPU: returns (states, logdets, P, prev_time) in the
-    reference's layout (states = [(t, x, y, z, roll, pitch, yaw), ...])."""
+    reference's layout (states = [(t, x, y, z, roll, pitch, yaw), ...]).  ``events`` is the
+    reference's event list or a kfmi.ingest.EventStream (then the whole window runs from HBM:
+    run_full_stream, with the lists built from its arrays)."""
+    from .ingest import EventStream
+    if isinstance(events, EventStream):
+        r = run_full_stream(events, start_idx, end_idx, initial_pt, initial_state, dtype)
+        if r is None:
+            return [], [], []
+        t, traj, ld, P, prev = r
+        states = [(float(t[i]), *traj[i]) for i in range(len(t))]
+        if print_output:
+            print(f'Full Kalman Filter (GPU): processed {len(t) - 1} measurements')
+        return states, [float(v) for v in ld], P, prev
     if not events:
         return [], [], []
     start_idx, end_idx = _window(events, start_idx, end_idx)
@@ -183,6 +195,60 @@ def run_kalman_filter_full(events, start_idx=None, end_idx=None, initial_pt=None
     if print_output:
         print(f'Full Kalman Filter (GPU): processed {len(times)} measurements from index {start_off} to {end_idx}')
     return states, logdets, from_blocks(Pb[:, 0]), prev
+
+
+def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initial_state=None, dtype='f64'):
+    """run_kalman_filter_full (kf_workers.py:623-728) over an EventStream window, entirely on
+    the device: cold-start fix search, per-event dt with the driver's dt < 0 rule
+    (kf_events_dt, KF_DT_FULL) and one single-filter kf_run_events launch.  Returns NumPy
+    (t [R], traj [R, 6], logdet [R], P 15x15, prev_time) with R = 1 + processed events, or None
+    when a cold window holds no fix."""
+    from .ingest import events_dt
+    n = len(stream)
+    start_idx = 0 if start_idx is None or start_idx < 0 else int(start_idx)
+    end_idx = n if end_idx is None or end_idx > n else int(end_idx)
+    dev = stream.t.device
+    x0 = np.zeros(15)
+    if initial_pt is not None and initial_state is not None:
+        P = np.asarray(initial_pt, np.float64)
+        x0[0:6] = initial_state[1:7]
+        prev0 = float(initial_state[0])
+        start_off = start_idx
+        t_first = prev0
+    else:
+        P = P0
+        win = stream.etype[start_idx:min(end_idx + 1, n)]  # the reference searches [start, end] (:655)
+        hit = torch.nonzero(win == GPS)
+        if hit.numel() == 0:
+            return None
+        start_off = start_idx + int(hit[0, 0])
+        p = stream.payload[start_off].cpu().numpy()
+        x0[0:3] = p[0:3]
+        prev0 = float(stream.t[start_off])
+        t_first = prev0
+    T = max(end_idx - start_off, 0)
+    kf = BatchedKF('ref15', 1, dtype, device=dev.index or 0)
+    npd = np.float64 if dtype == 'f64' else np.float32
+    kf.set_state(x0[:, None].astype(npd), to_blocks(P)[:, None].astype(npd))
+    t = stream.t[start_off:start_off + T]
+    dt, et = events_dt(t, prev0, _lib.KF_DT_FULL, stream.etype[start_off:start_off + T])
+    pay = stream.payload[start_off:start_off + T]
+    if dtype != 'f64':
+        pay = pay.float()
+    # a NONE event first records the initial state and logdet (states[0], logdets[0])
+    et = torch.cat([torch.full((1,), NONE, dtype=torch.uint8, device=dev), et])
+    dt = torch.cat([torch.zeros(1, dtype=torch.float64, device=dev), dt])
+    pay = torch.cat([torch.zeros(1, 9, dtype=pay.dtype, device=dev), pay])
+    tr, ld, _, _ = kf.run_events(et[:, None], dt[:, None], pay[:, :, None])
+    keep = et != NONE
+    keep[0] = True
+    t_all = torch.cat([torch.full((1,), t_first, dtype=torch.float64, device=dev), t])
+    x, Pb = kf.state()
+    prev = float(t[-1]) if T else prev0
+    out = (t_all[keep].cpu().numpy(), tr[keep, :, 0].double().cpu().numpy(), ld[keep, 0].double().cpu().numpy(),
+           from_blocks(Pb[:, 0].double().cpu().numpy()), prev)
+    kf.close()
+    return out
 
 
 def run_adaptive_threshold_kalman_filter(events, start_idx=None, end_idx=None, R_threshold=None,

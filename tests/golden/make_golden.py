@@ -19,6 +19,13 @@ Fixtures written (inputs and the reference's outputs, nothing else):
   ref15_drivers.npz run_kalman_filter (kf_workers.py:738-824, states + per-step covariances)
                     and run_no_update_kalman_filter (1060-1160), cold and warm
   ref8_full.npz     hw5_2.run_kalman_filter (hw5_2.py:313-380), in-order and out-of-order streams
+  ingest.npz        load_data_from_csv / gps_to_modified_utm / compute_imu_biases /
+                    unbias_imu_data / combine_sensor_data (kf_workers.py:290-385) and
+                    hw5_2.gps_to_utm (hw5_2.py:29-54) on synthetic GPS and IMU CSVs in the
+                    reference's column layout (gps_synth.csv.gz, imu_synth.csv.gz; the
+                    reference's own gps_data.csv is location data and is not copied, its
+                    imu_data.csv is absent), with oracle.ref_ingest's restated projection
+                    injected as utm.from_latlon
   cv_batch.npz      4/2 and 6/3 constant-velocity filters stepped with the reference's
                     own predict_covariance (kf_workers.py:546-549) and
                     calculate_kalman_gain (616-621), in the op order of 688-717
@@ -298,6 +305,124 @@ def ref8_full(h5):
     print('ref8_full:', len(events), 'events')
 
 
+def synth_gps_csv(path, n=1500, n_lead_nan=300, t0=1697739278.761565, seed=22):
+    """A synthetic GPS CSV in the layout of hw5_1.py's exporter (time, latitude, longitude,
+    altitude; 'nan' strings while there is no fix).  A ~10 Hz drive around an arbitrary point
+    (lat 40.0, lon -75.0), shaped like a real log: a block of leading no-fix rows, interior
+    dropouts, and rows where only the altitude is 'nan' (kf_workers.py:310 drops them,
+    hw5_2.py:35 keeps them) or the longitude is 'NaN'."""
+    import gzip
+    rng = np.random.RandomState(seed)
+    t = t0
+    lat, lon, alt = 40.0, -75.0, 12.5
+    rows = []
+    for i in range(n):
+        if i < n_lead_nan or (i % 211 == 3):
+            rows.append([repr(t), 'nan', 'nan', 'nan'])
+        elif i % 173 == 7:
+            rows.append([repr(t), repr(lat), repr(lon), 'nan'])
+        elif i % 389 == 11:
+            rows.append([repr(t), repr(lat), 'NaN', repr(alt)])
+        else:
+            rows.append([repr(t), repr(lat), repr(lon), repr(alt)])
+        if i >= n_lead_nan:
+            lat += 1e-6 * (3.0 + rng.normal(0, 0.3))
+            lon += 1e-6 * (2.0 + rng.normal(0, 0.3))
+            alt += rng.normal(0, 0.05)
+        t += 0.1 + rng.uniform(-0.005, 0.005)
+    with gzip.open(path, 'wt', newline='') as f:
+        f.write('time,latitude,longitude,altitude\n')
+        for r in rows:
+            f.write(','.join(r) + '\n')
+
+
+def synth_imu_csv(path, t0=1697739278.7381794, n=2500, hz=20.0, seed=21, gps_times=()):
+    """A synthetic IMU CSV with the column layout of hw5_1.py's exporter (time, orientation
+    x y z w, angular_velocity x y z, linear_acceleration x y z).  Exercises: yaw across +-pi,
+    exact gimbal-lock rows (|sinp| >= 1), time stamps equal to GPS stamps (ties go GPS first),
+    and biases of the size the notebook prints (KF_SensorFusion.ipynb:1331)."""
+    import gzip
+    rng = np.random.RandomState(seed)
+    rows = []
+    t = t0
+    gps_times = list(gps_times)
+    for i in range(n):
+        r, p, y = rng.normal(0, 0.05), rng.normal(-0.05, 0.02), -np.pi + 2 * np.pi * i / n
+        cr, sr, cp, sp, cy, sy = np.cos(r / 2), np.sin(r / 2), np.cos(p / 2), np.sin(p / 2), np.cos(y / 2), np.sin(y / 2)
+        q = [sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy, cr * cp * sy - sr * sp * cy,
+             cr * cp * cy + sr * sp * sy]
+        if i == 17:
+            q = [0.0, float(np.sqrt(0.5)), 0.0, float(np.sqrt(0.5))]   # pitch = +90 deg
+        if i == 18:
+            q = [0.0, -0.7071067811865476, 0.0, 0.7071067811865476]  # pitch = -90 deg
+        w = rng.normal([-0.0017, -0.0075, -0.036], 0.002)
+        a = rng.normal([-0.52, 0.0086, -9.53], 0.05)
+        stamp = t
+        if gps_times and i % 53 == 5:
+            stamp = gps_times[(i * 7) % len(gps_times)]  # exact tie with a GPS stamp
+        rows.append([repr(float(stamp)), *(repr(float(v)) for v in q), *(repr(float(v)) for v in w),
+                     *(repr(float(v)) for v in a)])
+        t += 1.0 / hz + rng.uniform(-1e-4, 1e-4)
+    with gzip.open(path, 'wt', newline='') as f:
+        f.write('time,orientation_x,orientation_y,orientation_z,orientation_w,angular_velocity_x,'
+                'angular_velocity_y,angular_velocity_z,linear_acceleration_x,linear_acceleration_y,'
+                'linear_acceleration_z\n')
+        for r in rows:
+            f.write(','.join(r) + '\n')
+
+
+def ingest(kfw, h5):
+    import gzip
+    import shutil
+    import tempfile
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from oracle import ref_ingest
+    sys.modules['utm'].from_latlon = ref_ingest.utm_from_latlon   # restated projection
+    tmp = tempfile.mkdtemp()
+    gps_gz = os.path.join(OUT, 'gps_synth.csv.gz')
+    synth_gps_csv(gps_gz)
+    gps_csv = os.path.join(tmp, 'gps.csv')
+    with gzip.open(gps_gz, 'rt') as fi, open(gps_csv, 'w') as fo:
+        fo.write(fi.read())
+    with open(gps_csv) as f:
+        gps_times = [float(l.split(',')[0]) for l in f.readlines()[301:]]
+    imu_gz = os.path.join(OUT, 'imu_synth.csv.gz')
+    synth_imu_csv(imu_gz, gps_times=gps_times)
+    imu_csv = os.path.join(tmp, 'imu.csv')
+    with gzip.open(imu_gz, 'rt') as fi, open(imu_csv, 'w') as fo:
+        fo.write(fi.read())
+    sf = kfw.KF_SensorFusion(gps_csv, imu_csv)
+    sf.load_data()
+    sf.gps_to_modified_utm()
+    bw, ba, fvi = sf.compute_imu_biases(sf.gps_data, sf.imu_data)
+    sf.unbias_imu_data(bw, ba)
+    sf.combine_sensor_data()
+    u = sf.utm_data
+    unb = sf.unbias_imu_data
+    ev = sf.indexed_sensor_data
+    gps_pos = {id(g): k for k, g in enumerate(u)}
+    imu_pos = {id(e): k for k, e in enumerate(unb)}
+    out = dict(
+        utm_time=np.array([g['time'] for g in u]),
+        utm_easting=np.array([g['easting'] for g in u]), utm_northing=np.array([g['northing'] for g in u]),
+        utm_altitude=np.array([g['altitude'] for g in u]), utm_zone_number=np.array([g['zone_number'] for g in u]),
+        utm_zone_letter=np.array([ord(g['zone_letter']) for g in u]),
+        gyro_bias=np.asarray(bw), accel_bias=np.asarray(ba), first_valid_index=np.array(fvi),
+        imu_values=np.array([[float(v) for v in e[1:10]] for e in unb]),
+        ev_is_imu=np.array([e[1] == 'IMU' for e in ev]), ev_time=np.array([e[2] for e in ev]),
+        ev_src=np.array([gps_pos[id(e[3])] if e[1] == 'GPS' else imu_pos[id(e[3])] for e in ev]))
+    h = h5.KF_SensorFusion(gps_csv, imu_csv)
+    h.load_data()
+    h.gps_to_utm()
+    out.update(hw5_utm_time=np.array([g['time'] for g in h.utm_data]),
+               hw5_utm_easting=np.array([g['easting'] for g in h.utm_data]),
+               hw5_utm_northing=np.array([g['northing'] for g in h.utm_data]),
+               hw5_has_altitude=np.array(any('altitude' in g for g in h.utm_data)))
+    np.savez_compressed(os.path.join(OUT, 'ingest.npz'), **out)
+    shutil.rmtree(tmp)
+    print('ingest:', len(u), 'fixes,', len(unb), 'imu rows,', len(ev), 'events; first_valid_index', fvi)
+
+
 def cv_batch(kfw):
     """4/2 and 6/3 constant-velocity filters stepped with the reference's own
     predict_covariance / calculate_kalman_gain, in the op order of kf_workers.py:688-717.
@@ -359,7 +484,8 @@ if __name__ == '__main__':
     kfw, h5 = import_reference()
     gens = {'ref15_full': lambda: ref15_full(kfw), 'ref15_combos': lambda: ref15_combos(kfw),
             'ref15_bruteforce': lambda: ref15_bruteforce(kfw), 'ref15_scheduled': lambda: ref15_scheduled(kfw),
-            'ref15_drivers': lambda: ref15_drivers(kfw), 'ref8_full': lambda: ref8_full(h5), 'cv_batch': lambda: cv_batch(kfw)}
+            'ref15_drivers': lambda: ref15_drivers(kfw), 'ref8_full': lambda: ref8_full(h5),
+            'ingest': lambda: ingest(kfw, h5), 'cv_batch': lambda: cv_batch(kfw)}
     for name in (sys.argv[1:] or list(gens)):
         gens[name]()
     # analytic known answer: slogdet(P0) of kf_workers.py:651 = 6 ln 1e4 + 9 ln 1e3
