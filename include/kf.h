@@ -204,9 +204,10 @@ int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const d
  * covariance each candidate sensor type (types: host [n_types] KF_EVENT_GPS|KF_EVENT_IMU,
  * n_types <= 16) would give every filter's current covariance.  full = 0: the reference's
  * Scheduler.gain, an update with the first measurement row only (cov_matrix(S=[1]),
- * kf_workers.py:112-147, 174-185); full = 1: every measurement row of the sensor. */
+ * kf_workers.py:112-147, 174-185); full = 1: every measurement row of the sensor.  post:
+ * device [n_types][27][B] block-packed posterior covariances (Scheduler.cov_matrix), or NULL. */
 int kf_score_candidates(kf_batch* handle, int n_types, const int32_t* types, int full, void* gain,
-                        void* stream);
+                        void* post, void* stream);
 
 /* KF_MODEL_REF15 rate-decimated greedy filter (run_kalman_filter_scheduled with
  * selection_method='greedy', kf_workers.py:826-957), per filter in one launch.  Streams:
@@ -255,7 +256,9 @@ typedef struct kf_ingest_info {
 
 /* Build the merged event stream.  gps device [4][ld_gps] (time, latitude, longitude,
  * altitude), imu device [11][ld_imu] (time, orientation x y z w, angular velocity x y z,
- * linear acceleration x y z) — the column layouts hw5_1.py:14-38 writes.  Outputs (device,
+ * linear acceleration x y z) — the column layouts hw5_1.py:14-38 writes.  bias: host [6]
+ * (angular velocity, linear acceleration) to subtract instead of the compute_imu_biases means,
+ * or NULL.  Outputs (device,
  * capacity >= n_gps + n_imu; info->n_events rows written): etype [N] (KF_EVENT_GPS/IMU),
  * t [N], payload [N][9] — fix: (easting - e0, northing - n0, altitude, 0...), the UTM
  * projection of the `utm` package; IMU: (roll, pitch, yaw, w - bias_w, a - bias_a) —
@@ -264,8 +267,12 @@ typedef struct kf_ingest_info {
  * (Python's stable sort, kf_workers.py:384).  Synchronous (the event count is returned).
  * KF_EINVAL when no GPS row has a latitude (the reference's biases are undefined then). */
 int kf_ingest(const double* gps, int64_t n_gps, int64_t ld_gps, const double* imu, int64_t n_imu, int64_t ld_imu,
-              int flags, uint8_t* etype, double* t, double* payload, int32_t* src, int8_t* zone_number,
-              char* zone_letter, kf_ingest_info* info, void* stream);
+              int flags, const double* bias, uint8_t* etype, double* t, double* payload, int32_t* src,
+              int8_t* zone_number, char* zone_letter, kf_ingest_info* info, void* stream);
+
+/* quaternion_to_euler (kf_workers.py:399-425) for n quaternions: q device [4][ld] (x, y, z, w),
+ * out device [3][n] (roll, pitch, yaw). */
+int kf_quat_to_euler(int64_t n, const double* q, int64_t ld, double* out, void* stream);
 
 /* Time since the previous event for a driver over a merged stream, computed on the device.
  *   KF_DT_FULL      run_kalman_filter_full (kf_workers.py:682-686): previous = the previous

@@ -454,7 +454,8 @@ int kf_eval_combos(kf_batch* h, int n_events, const double* events, const double
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_eval_combos");
 }
 
-int kf_score_candidates(kf_batch* h, int n_types, const int32_t* types, int full, void* gain, void* stream) {
+int kf_score_candidates(kf_batch* h, int n_types, const int32_t* types, int full, void* gain, void* post,
+                        void* stream) {
     if (int rc = check_handle(h)) return rc;
     if (!is_ref15(h)) return fail(KF_EINVAL, "kf_score_candidates: needs a KF_MODEL_REF15 handle");
     if (n_types < 1 || n_types > 16) return fail(KF_EINVAL, "kf_score_candidates: n_types = %d outside [1, 16]", n_types);
@@ -472,6 +473,7 @@ int kf_score_candidates(kf_batch* h, int n_types, const int32_t* types, int full
     a.x = h->x;
     a.P = h->P;
     a.gain = gain;
+    a.post = post;
     hipError_t e = kfmi::launch_ref15_score(h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_score_candidates");
 }

@@ -242,6 +242,12 @@ __global__ __launch_bounds__(kIngBlock) void dt_kernel(int64_t n, const double* 
     if (et_out) et_out[i] = (rule != 2 && d < 0) ? uint8_t(KF_EVENT_NONE) : e;
 }
 
+__global__ __launch_bounds__(kIngBlock) void euler_kernel(int64_t n, const double* q, int64_t ld, double* out) {
+    const int64_t i = int64_t(blockIdx.x) * kIngBlock + threadIdx.x;
+    if (i >= n) return;
+    quat_to_euler(q[i], q[ld + i], q[2 * ld + i], q[3 * ld + i], out[i], out[n + i], out[2 * n + i]);
+}
+
 struct MaxOp {
     __device__ __forceinline__ double operator()(double a, double b) const { return b > a ? b : a; }
 };
@@ -275,8 +281,8 @@ int hip_err(hipError_t e, const char* what) {
 extern "C" {
 
 int kf_ingest(const double* gps, int64_t n_gps, int64_t ld_gps, const double* imu, int64_t n_imu, int64_t ld_imu,
-              int flags, uint8_t* etype, double* t, double* payload, int32_t* src, int8_t* zone_number,
-              char* zone_letter, kf_ingest_info* info, void* stream) {
+              int flags, const double* bias, uint8_t* etype, double* t, double* payload, int32_t* src,
+              int8_t* zone_number, char* zone_letter, kf_ingest_info* info, void* stream) {
     if (n_gps < 0 || n_imu < 0) return set_error(KF_EINVAL, "kf_ingest: negative row count");
     if ((n_gps && (!gps || ld_gps < n_gps)) || (n_imu && (!imu || ld_imu < n_imu)))
         return set_error(KF_EINVAL, "kf_ingest: null column array or leading dimension below the row count");
@@ -336,8 +342,12 @@ int kf_ingest(const double* gps, int64_t n_gps, int64_t ld_gps, const double* im
         imu_keys_kernel<<<grid(n_imu), kIngBlock, 0, st>>>(a);
         KF_TRY(hipGetLastError(), "kf_ingest imu_keys_kernel");
     }
-    bias_kernel<<<1, 64, 0, st>>>(a);
-    KF_TRY(hipGetLastError(), "kf_ingest bias_kernel");
+    if (bias) {  // caller's biases (unbias_imu_data takes them as arguments, kf_workers.py:349)
+        KF_TRY(hipMemcpyAsync(a.bias, bias, 6 * sizeof(double), hipMemcpyHostToDevice, st), "kf_ingest bias");
+    } else {
+        bias_kernel<<<1, 64, 0, st>>>(a);
+        KF_TRY(hipGetLastError(), "kf_ingest bias_kernel");
+    }
     if (n_gps) {
         size_t tb = scan_tmp;
         KF_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, a.keep, pos, static_cast<int>(n_gps), st), "kf_ingest scan");
@@ -349,10 +359,10 @@ int kf_ingest(const double* gps, int64_t n_gps, int64_t ld_gps, const double* im
                "kf_ingest sort");
     }
     unsigned long long first[2];
-    double bias[6];
+    double bias_out[6];
     int32_t last_pos = 0, last_keep = 0;
     KF_TRY(hipMemcpyAsync(first, a.first, sizeof first, hipMemcpyDeviceToHost, st), "kf_ingest readback");
-    KF_TRY(hipMemcpyAsync(bias, a.bias, sizeof bias, hipMemcpyDeviceToHost, st), "kf_ingest readback");
+    KF_TRY(hipMemcpyAsync(bias_out, a.bias, sizeof bias_out, hipMemcpyDeviceToHost, st), "kf_ingest readback");
     if (n_gps) {
         KF_TRY(hipMemcpyAsync(&last_pos, pos + n_gps - 1, 4, hipMemcpyDeviceToHost, st), "kf_ingest readback");
         KF_TRY(hipMemcpyAsync(&last_keep, a.keep + n_gps - 1, 4, hipMemcpyDeviceToHost, st), "kf_ingest readback");
@@ -399,11 +409,19 @@ int kf_ingest(const double* gps, int64_t n_gps, int64_t ld_gps, const double* im
     info->first_valid_index = static_cast<int64_t>(first[0]);
     info->origin_row = n_fix ? static_cast<int64_t>(first[1]) : -1;
     for (int k = 0; k < 3; ++k) {
-        info->gyro_bias[k] = bias[k];
-        info->accel_bias[k] = bias[3 + k];
+        info->gyro_bias[k] = bias_out[k];
+        info->accel_bias[k] = bias_out[3 + k];
     }
     info->utm_origin[0] = origin[0];
     info->utm_origin[1] = origin[1];
+    return KF_OK;
+}
+
+int kf_quat_to_euler(int64_t n, const double* q, int64_t ld, double* out, void* stream) {
+    if (n < 0 || (n && (!q || !out || ld < n))) return set_error(KF_EINVAL, "kf_quat_to_euler: bad arguments");
+    if (n == 0) return KF_OK;
+    euler_kernel<<<grid(n), kIngBlock, 0, static_cast<hipStream_t>(stream)>>>(n, q, ld, out);
+    KF_TRY(hipGetLastError(), "kf_quat_to_euler");
     return KF_OK;
 }
 

@@ -95,6 +95,7 @@ struct Ref15ScoreArgs {
     const void* x;
     const void* P;
     void* gain;              // [n_types][B]
+    void* post;              // [n_types][27][B] posterior covariance blocks, or nullptr
 };
 
 // Rate-decimated greedy driver (run_kalman_filter_scheduled, kf_workers.py:826-957), per filter.

@@ -429,7 +429,7 @@ __device__ __forceinline__ T cov_trace(const Ref15<T>& s) {
 // row of both H_gps and H_imu is e_0 (pos_x), with R[0,0] = 3 (GPS) or 50 (IMU); a full update
 // uses every row.  The state vector is not needed, so a zero one is carried through.
 template <typename T>
-__device__ __forceinline__ T posterior_trace(const Ref15<T>& s0, int type, bool full) {
+__device__ __forceinline__ Ref15<T> posterior(const Ref15<T>& s0, int type, bool full) {
     Ref15<T> c = s0;
 #pragma unroll
     for (int i = 0; i < 15; ++i) c.x[i] = T(0);
@@ -447,7 +447,12 @@ __device__ __forceinline__ T posterior_trace(const Ref15<T>& s0, int type, bool 
         for (int i = 0; i < 9; ++i) imu[i] = T(0);
         c.update_imu(imu, T(0));
     }
-    return cov_trace(c);
+    return c;
+}
+
+template <typename T>
+__device__ __forceinline__ T posterior_trace(const Ref15<T>& s0, int type, bool full) {
+    return cov_trace(posterior(s0, type, full));
 }
 
 template <typename T>
@@ -456,9 +461,14 @@ __global__ __launch_bounds__(kBlock) void ref15_score_kernel(const Ref15ScoreArg
     if (f >= a.B) return;
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
+    const uint32_t rb_post = a.post ? rb : 0u;
     Ref15<T> s;
     s.load(a.x, a.P, rb, off);
-    for (int c = 0; c < a.n_types; ++c) stb(a.gain, c, rb, off, posterior_trace(s, int(a.types[c]), a.full != 0));
+    for (int c = 0; c < a.n_types; ++c) {
+        const Ref15<T> p = posterior(s, int(a.types[c]), a.full != 0);
+        stb(a.gain, c, rb, off, cov_trace(p));
+        p.store_cov(a.post, int64_t(c) * 27, rb_post, off);
+    }
 }
 
 template <typename T>

@@ -85,12 +85,13 @@ SIGNATURES = {
     'kf_synth': (_i, [_vp, ctypes.c_uint64, _i64, _i, _d, _i, _vp, _vp, _vp, _vp]),
     'kf_run_events': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _d, _vp]),
     'kf_eval_combos': (_i, [_vp, _i, _vp, _vp, _d, _d, _i, ctypes.c_uint64, _vp, _vp, _vp, _vp]),
-    'kf_score_candidates': (_i, [_vp, _i, _vp, _i, _vp, _vp]),
+    'kf_score_candidates': (_i, [_vp, _i, _vp, _i, _vp, _vp, _vp]),
     'kf_run_scheduled': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _d, _vp, _vp, _vp, _vp, _vp]),
     'kf_csv_shape': (_i, [ctypes.c_char_p, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i)]),
     'kf_csv_read': (_i, [ctypes.c_char_p, _i, _i, _vp, _i64, _i64]),
-    'kf_ingest': (_i, [_vp, _i64, _i64, _vp, _i64, _i64, _i, _vp, _vp, _vp, _vp, _vp, _vp,
+    'kf_ingest': (_i, [_vp, _i64, _i64, _vp, _i64, _i64, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                        ctypes.POINTER(kf_ingest_info), _vp]),
+    'kf_quat_to_euler': (_i, [_i64, _vp, _i64, _vp, _vp]),
     'kf_events_dt': (_i, [_i64, _vp, _vp, _d, _i, _vp, _vp, _vp]),
 }
 

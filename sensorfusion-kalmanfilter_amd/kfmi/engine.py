@@ -239,17 +239,19 @@ class BatchedKF:
         torch.cuda.current_stream(self.device).synchronize()  # host arrays were staged; keep them alive
         return mx, ld, nr
 
-    def score_candidates(self, types, full=False):
+    def score_candidates(self, types, full=False, posterior=False):
         """KF_MODEL_REF15 scheduler scoring (kf_score_candidates): [len(types), B] traces of the
         posterior covariance each candidate sensor would give (full=False: the reference's
-        Scheduler.gain, first measurement row only)."""
+        Scheduler.gain, first measurement row only).  posterior=True also returns the
+        block-packed posterior covariances [len(types), 27, B] (Scheduler.cov_matrix)."""
         if self.model != 'ref15':
             raise ValueError('score_candidates needs a ref15 handle')
         ty = np.ascontiguousarray(types, dtype=np.int32)
         out = self.empty(len(ty), self.batch)
+        post = self.empty(len(ty), 27, self.batch) if posterior else None
         check(_lib.lib().kf_score_candidates(self.handle, len(ty), ty.ctypes.data_as(ctypes.c_void_p), int(full),
-                                             _ptr(out), self._stream()))
-        return out
+                                             _ptr(out), _ptr(post), self._stream()))
+        return (out, post) if posterior else out
 
     def run_scheduled(self, t, etype, payload, prev_time, freq):
         """KF_MODEL_REF15 rate-decimated greedy filter (kf_run_scheduled).  t [T, B] float64

@@ -120,9 +120,11 @@ class EventStream:
         return out
 
 
-def ingest_arrays(gps, imu, with_altitude=True, device=0):
+def ingest_arrays(gps, imu, with_altitude=True, device=0, bias=None):
     """Merged event stream from parsed columns: gps [4, n] (time, latitude, longitude,
-    altitude), imu [11, m] (GPS_COLUMNS / IMU_COLUMNS order), NumPy or torch."""
+    altitude), imu [11, m] (GPS_COLUMNS / IMU_COLUMNS order), NumPy or torch.  bias: optional
+    (angular_velocity_bias[3], linear_acceleration_bias[3]) to use instead of the
+    compute_imu_biases means."""
     dev = torch.device('cuda', device) if isinstance(device, int) else torch.device(device)
     g = torch.as_tensor(np.ascontiguousarray(gps, dtype=np.float64) if not torch.is_tensor(gps) else gps,
                         dtype=torch.float64).to(dev).contiguous()
@@ -140,9 +142,15 @@ def ingest_arrays(gps, imu, with_altitude=True, device=0):
     zl = torch.empty(cap, dtype=torch.uint8, device=dev)
     info = _lib.kf_ingest_info()
     flags = _lib.KF_INGEST_GPS_ALTITUDE if with_altitude else 0
+    b = None
+    if bias is not None:
+        b = np.ascontiguousarray(np.concatenate([np.ravel(bias[0]), np.ravel(bias[1])]), dtype=np.float64)
+        if b.shape != (6,):
+            raise ValueError('bias must be (angular_velocity_bias[3], linear_acceleration_bias[3])')
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     with torch.cuda.device(dev):
         check(_lib.lib().kf_ingest(_ptr(g) if ng else None, ng, ng, _ptr(m) if ni else None, ni, ni, flags,
+                                   None if b is None else b.ctypes.data_as(ctypes.c_void_p),
                                    _ptr(etype), _ptr(t), _ptr(payload), _ptr(src), _ptr(zn), _ptr(zl),
                                    ctypes.byref(info), stream))
     n = int(info.n_events)
@@ -155,6 +163,20 @@ def ingest_csv(gps_csv, imu_csv, with_altitude=True, device=0):
     """The reference's ingest sequence (kf_workers.py:2256-2274: load_data, gps_to_modified_utm,
     compute_imu_biases, unbias_imu_data, combine_sensor_data) as parse + one kf_ingest."""
     return ingest_arrays(read_csv(gps_csv, 4), read_csv(imu_csv, 11), with_altitude, device)
+
+
+def quaternion_to_euler(q, device=0):
+    """quaternion_to_euler (kf_workers.py:399-425) on the device for q [4, n] (x, y, z, w);
+    returns [3, n] (roll, pitch, yaw)."""
+    dev = torch.device('cuda', device) if isinstance(device, int) else torch.device(device)
+    qd = torch.as_tensor(np.asarray(q, dtype=np.float64) if not torch.is_tensor(q) else q,
+                         dtype=torch.float64).to(dev).reshape(4, -1).contiguous()
+    n = int(qd.shape[1])
+    out = torch.empty(3, n, dtype=torch.float64, device=dev)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    with torch.cuda.device(dev):
+        check(_lib.lib().kf_quat_to_euler(n, _ptr(qd), n, _ptr(out), stream))
+    return out
 
 
 def events_dt(t, prev0, rule, etype=None):

@@ -88,9 +88,10 @@ def from_blocks(b):
 
 
 def event_payload(stype, sdata):
-    """The 9 payload values of one reference event (kf_workers.py:331, 367)."""
+    """The 9 payload values of one reference event (kf_workers.py:331, 367; hw5_2.py:54 stores
+    no altitude, which its 8-state model never reads)."""
     if stype == 'GPS':
-        return [sdata['easting'], sdata['northing'], sdata['altitude'], 0, 0, 0, 0, 0, 0]
+        return [sdata['easting'], sdata['northing'], sdata.get('altitude', 0.0), 0, 0, 0, 0, 0, 0]
     return [float(v) for v in sdata[1:10]]
 
 
@@ -197,12 +198,14 @@ def run_kalman_filter_full(events, start_idx=None, end_idx=None, initial_pt=None
     return states, logdets, from_blocks(Pb[:, 0]), prev
 
 
-def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initial_state=None, dtype='f64'):
+def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initial_state=None, dtype='f64',
+                    cov=False):
     """run_kalman_filter_full (kf_workers.py:623-728) over an EventStream window, entirely on
     the device: cold-start fix search, per-event dt with the driver's dt < 0 rule
     (kf_events_dt, KF_DT_FULL) and one single-filter kf_run_events launch.  Returns NumPy
-    (t [R], traj [R, 6], logdet [R], P 15x15, prev_time) with R = 1 + processed events, or None
-    when a cold window holds no fix."""
+    (t [R], traj [R, 6], logdet [R], P 15x15, prev_time) with R = 1 + processed events (plus
+    the block-packed per-record covariances [R, 27] with cov=True), or None when a cold window
+    holds no fix."""
     from .ingest import events_dt
     n = len(stream)
     start_idx = 0 if start_idx is None or start_idx < 0 else int(start_idx)
@@ -239,7 +242,7 @@ def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initi
     et = torch.cat([torch.full((1,), NONE, dtype=torch.uint8, device=dev), et])
     dt = torch.cat([torch.zeros(1, dtype=torch.float64, device=dev), dt])
     pay = torch.cat([torch.zeros(1, 9, dtype=pay.dtype, device=dev), pay])
-    tr, ld, _, _ = kf.run_events(et[:, None], dt[:, None], pay[:, :, None])
+    tr, ld, _, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None], cov=cov)
     keep = et != NONE
     keep[0] = True
     t_all = torch.cat([torch.full((1,), t_first, dtype=torch.float64, device=dev), t])
@@ -247,6 +250,8 @@ def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initi
     prev = float(t[-1]) if T else prev0
     out = (t_all[keep].cpu().numpy(), tr[keep, :, 0].double().cpu().numpy(), ld[keep, 0].double().cpu().numpy(),
            from_blocks(Pb[:, 0].double().cpu().numpy()), prev)
+    if cov:
+        out += (cv[keep, :, 0].double().cpu().numpy(),)
     kf.close()
     return out
 

@@ -151,3 +151,19 @@ def test_real_gps_log_first_fix_kat():
         (0.0, 0.0, 19, 'T', -32.6)
     assert u[0]['time'] == 1697739552.3362827
     assert len(u) == 21871
+
+
+def test_compat_model_matrices_are_the_reference_model():
+    """kfmi.kf_workers keeps the reference's model definitions for class_args callers."""
+    from kfmi import kf_workers as kfw
+    from oracle import ref_kf
+    sf = kfw.KF_SensorFusion('g.csv', 'i.csv')
+    for dt in (0.0, 0.005, 0.1, 1.3):
+        np.testing.assert_array_equal(sf.get_state_transition_matrix(dt), ref_kf.F_ref15(dt))
+        np.testing.assert_array_equal(sf.get_process_noise_covariance_matrix(dt), ref_kf.Q_ref15(dt))
+    np.testing.assert_array_equal(sf.get_gps_observation_matrix(), ref_kf.H_gps15())
+    np.testing.assert_array_equal(sf.get_imu_observation_matrix(), ref_kf.H_imu15())
+    np.testing.assert_array_equal(sf.get_gps_measurement_noise_covariance_matrix(), ref_kf.R_gps15())
+    np.testing.assert_array_equal(sf.get_imu_measurement_noise_covariance_matrix(), ref_kf.R_imu15())
+    t = kfw.CsvTable(np.array([[1.5, 2.0], [np.nan, 3.25]]))
+    assert t[0] == ['1.5', 'nan'] and t[-1] == ['2.0', '3.25'] and len(t) == 2 and t[:1] == [t[0]]
