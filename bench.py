@@ -8,6 +8,9 @@ resident in HBM before timing starts.  Consecutive steps continue the same filte
 start, like the reference's windowed runs, kf_workers.py:2316-2323) over the same inputs.
 
 Configs (BASELINE.json / SURVEY.md §8d); per GPU (weak scaling: each rank owns B filters):
+    1  the reference's own case: ONE filter over a whole drive log — 15-state model,
+       run_kalman_filter_full over ~638k merged GPS+IMU events (synthetic log with the shape of
+       gps_data.csv + the 200 Hz IMU log: CSV -> kf_ingest -> kf_events_dt + kf_run_events)
     2  cv2 (4-state/2-meas)  fp32  B=65,536     T=1024 dt=0.1  update every step
     3  cv3 (6-state/3-meas)  fp64  B=1,048,576  T=256  dt=0.1  update every step   [default]
     4  cv3 (6-state/3-meas)  fp32  B=1,048,576  T=256  dt=0.1  update every step   (x8 GPUs)
@@ -38,6 +41,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 CONFIGS = {
+    '1': dict(model='ref15', dtype='f64', B=1, n_gps=30758, n_gps_nan_lead=2735, n_gps_nan=8887, n_imu=616322),
     '2': dict(model='cv2', dtype='f32', B=65536, T=1024, dt=0.1, k=1),
     '3': dict(model='cv3', dtype='f64', B=1048576, T=256, dt=0.1, k=1),
     '4': dict(model='cv3', dtype='f32', B=1048576, T=256, dt=0.1, k=1),
@@ -204,6 +208,113 @@ def ref15_workload(cfg, args, rank, world, dev):
                 extra={'filters_per_gpu': B, 'events_per_launch': T})
 
 
+def synth_log(cfg, root, seed=SEED):
+    """CSV logs with the reference drive's shape (gps_data.csv: 30 758 rows at ~10 Hz, 2 735
+    leading and 8 887 total no-fix rows; the IMU log at 200 Hz, 616 322 rows = the 638 193
+    merged events of KF_SensorFusion.ipynb:1960 minus the 21 871 fixes).  Columns as hw5_1.py
+    writes them.  Synthetic: the reference's own log is location data and its IMU log is absent."""
+    rng = np.random.default_rng(seed)
+    ng, ni = cfg['n_gps'], cfg['n_imu']
+    t0g, t0i = 1697739278.761565, 1697739278.7381794
+    tg = t0g + np.cumsum(np.r_[0.0, rng.uniform(0.095, 0.105, ng - 1)])
+    ti = t0i + np.cumsum(np.r_[0.0, rng.uniform(0.00499, 0.00501, ni - 1)])
+    lat = 40.0 + np.cumsum(rng.normal(3e-6, 3e-7, ng))
+    lon = -75.0 + np.cumsum(rng.normal(2e-6, 3e-7, ng))
+    alt = 12.5 + np.cumsum(rng.normal(0, 0.05, ng))
+    gps = np.stack([tg, lat, lon, alt], 1)
+    nan_rows = np.r_[np.arange(cfg['n_gps_nan_lead']),
+                     rng.choice(np.arange(cfg['n_gps_nan_lead'], ng), cfg['n_gps_nan'] - cfg['n_gps_nan_lead'],
+                                replace=False)]
+    gps[nan_rows, 1:] = np.nan
+    yaw = np.cumsum(rng.normal(0, 2e-4, ni))
+    r, p = rng.normal(0, 0.02, ni), rng.normal(-0.05, 0.01, ni)
+    cr, sr, cp, sp, cy, sy = np.cos(r / 2), np.sin(r / 2), np.cos(p / 2), np.sin(p / 2), np.cos(yaw / 2), np.sin(yaw / 2)
+    q = np.stack([sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy, cr * cp * sy - sr * sp * cy,
+                  cr * cp * cy + sr * sp * sy], 1)
+    w = rng.normal([-0.0017, -0.0075, -0.036], 0.01, (ni, 3))
+    a = rng.normal([-0.52, 0.0086, -9.53], 0.3, (ni, 3))
+    imu = np.concatenate([ti[:, None], q, w, a], 1)
+    gp, ip = os.path.join(root, 'gps_log.csv'), os.path.join(root, 'imu_log.csv')
+    np.savetxt(gp, gps, fmt='%.17g', delimiter=',', header='time,latitude,longitude,altitude', comments='')
+    np.savetxt(ip, imu, fmt='%.17g', delimiter=',', comments='',
+               header='time,orientation_x,orientation_y,orientation_z,orientation_w,angular_velocity_x,'
+                      'angular_velocity_y,angular_velocity_z,linear_acceleration_x,linear_acceleration_y,'
+                      'linear_acceleration_z')
+    return gp, ip
+
+
+def log_workload(cfg, args, rank, world, dev):
+    """BASELINE config 1: run_kalman_filter_full (kf_workers.py:623-728) over a whole drive log
+    with ONE filter — the reference's own use.  Ingest runs once, outside the timed region
+    (reported separately); a step is the device dt pass + one kf_run_events over every event."""
+    import tempfile
+    import kfmi
+    from kfmi import _lib, ingest
+    from kfmi.engine import _ptr
+    root = tempfile.mkdtemp(prefix='kfmi_log_')
+    gp, ip = synth_log(cfg, root)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    gcols, icols = ingest.read_csv(gp, 4), ingest.read_csv(ip, 11)
+    t1 = time.perf_counter()
+    stream = ingest.ingest_arrays(gcols, icols, device=dev.index)
+    torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
+    N = len(stream)
+    first = int(torch.nonzero(stream.etype == _lib.KF_EVENT_GPS)[0, 0])
+    T = N - first
+    t_ev = stream.t[first:].contiguous()
+    e_ev = stream.etype[first:].contiguous()
+    pay = stream.payload[first:].contiguous()
+    x0 = torch.zeros(15, 1, dtype=torch.float64, device=dev)
+    x0[0:3, 0] = pay[0, 0:3]
+    kf = kfmi.BatchedKF('ref15', 1, 'f64', device=dev.index)
+    dt = torch.empty(T, dtype=torch.float64, device=dev)
+    et = torch.empty(T, dtype=torch.uint8, device=dev)
+    traj = kf.empty(T, 6, 1)
+    logdet = kf.empty(T, 1)
+    prev0 = float(t_ev[0])
+    L = _lib.lib()
+
+    def step():
+        kf.reset(x0)
+        _lib.check(L.kf_events_dt(T, _ptr(t_ev), _ptr(e_ev), prev0, _lib.KF_DT_FULL, _ptr(dt), _ptr(et),
+                                  kf._stream()))
+        _lib.check(L.kf_run_events(kf.handle, T, _ptr(et), _ptr(dt), _ptr(pay), _ptr(traj), None, _ptr(logdet),
+                                   None, 0, 0.0, kf._stream()))
+
+    def cpu():
+        """oracle/ref_kf.run_kalman_filter_full (the reference's per-event NumPy loop) over the
+        first events of the same log, 1 core, ~12 s."""
+        from oracle import ref_kf
+        from kfmi.kf_workers import EventList
+        n = 1
+        el = 0.0
+        ev = EventList(stream)
+        while True:
+            n = min(T, max(n * 4, 4000))
+            lst = ev[first:first + n]   # from the first fix, where the reference's loop starts
+            ts = time.perf_counter()
+            st, _, _, _ = ref_kf.run_kalman_filter_full(lst, 0, n)
+            el = time.perf_counter() - ts
+            if el > 3.0 or n == T:
+                break
+        return {'value': (len(st) - 1) / el, 'unit': 'KF events/s', 'cores': 1, 'kind': 'port',
+                'sample': f'run_kalman_filter_full over the first {n} events from the first fix of this log '
+                          f'({len(st) - 1} processed) with oracle/ref_kf (the reference loop: dense 15x15 NumPy, '
+                          f'slogdet per event), NumPy {np.__version__}, 1 thread, {host_cpu()}',
+                'seconds': round(el, 2)}
+
+    per_event = 1 + 8 + 8 + 72 + 1 + 8 + 48 + 8   # dt pass (t, etype in; dt, etype out) + filter (in/out)
+    return dict(step=step, units=T, bytes=per_event * T, bytes_per_unit=per_event, kernel='ref_events_kernel',
+                traffic=None, cpu=cpu, gather=None, kf=kf,
+                desc=f'BASELINE config 1: ONE 15-state filter (run_kalman_filter_full, kf_workers.py:623-728) over a '
+                     f'whole drive log, {N} merged events ({stream.n_fixes} fixes + {stream.n_imu} IMU at 200 Hz), '
+                     f'f64; synthetic log with the reference log\'s shape',
+                extra={'events': N, 'events_filtered': T, 'csv_parse_ms': (t1 - t0) * 1e3,
+                       'kf_ingest_ms': (t2 - t1) * 1e3, 'filters': 1})
+
+
 def bf_workload(cfg, args, rank, world, dev):
     """Exhaustive brute-force search (kf_workers.py:1218-1392 without the early exit): every
     k-subset, k = 1..n, of n candidate events after a warm start, through kf_eval_combos.  Each
@@ -291,7 +402,9 @@ def main():
     cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg['B'] = args.batch
-    if args.config == 'ref15':
+    if args.config == '1':
+        w = log_workload(cfg, args, rank, world, dev)
+    elif args.config == 'ref15':
         w = ref15_workload(cfg, args, rank, world, dev)
     elif args.config == 'bf':
         w = bf_workload(cfg, args, rank, world, dev)
