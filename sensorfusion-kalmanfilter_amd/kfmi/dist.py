@@ -7,6 +7,10 @@ kf_workers.py:29-30), so rank r owns the contiguous global filter range
 counter-based generator (kf_synth keyed by the GLOBAL filter index) — no scatter and no
 collective in the time loop.  The only collective is the final reassembly of per-shard
 results (``gather_shards``), plus scalar reductions for timing.
+
+The brute-force search (kf_workers.py:1218-1392) shards by combination rank instead: for each
+subset size k every rank scans its slice of the C(n, k) ranks and one MIN all-reduce picks the
+globally first acceptable combination (``brute_force_search``).
 """
 from __future__ import annotations
 
@@ -58,3 +62,58 @@ def max_over_ranks(values, device, group=None):
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return [float(v) for v in t.tolist()]
+
+
+_NONE = (1 << 63) - 1
+
+
+def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, initial_pt=None, initial_state=None,
+                       max_combos_in_memory=1 << 22, dtype='f64', device=0, group=None, first_valid=None,
+                       finish=None):
+    """run_brute_force_kalman_filter_no_sampling_min_usage sharded over the ranks of ``group``:
+    for k = 1..n, rank r scans combination ranks shard_range(C(n, k), r, world) on its GPU
+    (kf_eval_combos), then an all-reduce MIN of the first acceptable rank (or "none") decides
+    — the same winner as the single-GPU search (the first acceptable subset of the smallest size,
+    in itertools.combinations order).  Every rank returns the reference's result dict (or None).
+
+    ``first_valid(k, lo, hi)`` / ``finish(k, rank)`` replace the GPU evaluation (tests drive the
+    reduction logic with the CPU oracle on gloo)."""
+    import math
+
+    import torch.distributed as dist
+
+    from . import ref15
+    if R_threshold is None:
+        raise ValueError('R_threshold must be specified for brute force KF.')
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    st = ref15.brute_force_setup(events, start_idx, end_idx, initial_pt, initial_state)
+    if st is None:
+        return None
+    cand, xt, Pt, prev_time, target_end, ev, init = st
+    n = len(cand)
+    kf = None
+    if first_valid is None:
+        width = max(1, min(max_combos_in_memory, max(shard_range(math.comb(n, k), rank, world)[1]
+                                                     for k in range(1, n + 1))))
+        kf = ref15.BatchedKF('ref15', width, dtype, device=device)
+
+        def first_valid(k, lo, hi):
+            return ref15.first_valid_rank(kf, ev, init, prev_time, target_end, k, lo, hi, R_threshold)
+    if finish is None:
+        def finish(k, r):
+            return ref15.brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype, device)
+    backend = dist.get_backend(group)
+    tdev = torch.device('cuda', torch.cuda.current_device()) if backend == 'nccl' else torch.device('cpu')
+    try:
+        for k in range(1, n + 1):
+            lo, cnt = shard_range(math.comb(n, k), rank, world)
+            r = first_valid(k, lo, lo + cnt) if cnt else None
+            t = torch.tensor([_NONE if r is None else int(r)], dtype=torch.int64, device=tdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+            best = int(t.item())
+            if best != _NONE:
+                return finish(k, best)
+    finally:
+        if kf is not None:
+            kf.close()
+    return None

@@ -408,15 +408,9 @@ def unrank_combination(n, k, r):
     return out
 
 
-def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end_idx=None, R_threshold=None,
-                                                       initial_pt=None, initial_state=None,
-                                                       max_combos_in_memory=1 << 22, dtype='f64', device=0):
-    """kf_workers.py:1218-1392 on the GPU: for k = 1..n, evaluate every k-subset of the candidate
-    events (kf_eval_combos, one filter per subset, up to ``max_combos_in_memory`` per launch) and
-    return the first subset, in itertools.combinations order, whose max log-determinant is below
-    R_threshold — the reference's result dict — or None."""
-    if R_threshold is None:
-        raise ValueError('R_threshold must be specified for brute force KF.')
+def brute_force_setup(events, start_idx=0, end_idx=None, initial_pt=None, initial_state=None):
+    """The search's inputs as kf_workers.py:1262-1310 sets them up: (candidates, x0, P0,
+    prev_time, target_end, events [n, 11], init [42]), or None without a starting fix."""
     if start_idx is None or start_idx < 0:
         start_idx = 0
     if end_idx is None or end_idx > len(events):
@@ -447,23 +441,53 @@ def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end
         ev[i, 0] = t
         ev[i, 1] = GPS if stype == 'GPS' else IMU
         ev[i, 2:] = event_payload(stype, sdata)
-    init = np.concatenate([xt, to_blocks(Pt)])
+    return cand, xt, Pt, prev_time, target_end, ev, np.concatenate([xt, to_blocks(Pt)])
+
+
+def first_valid_rank(kf, ev, init, prev_time, target_end, k, lo, hi, threshold):
+    """Smallest combination rank r in [lo, hi) of the k-subsets whose max log-determinant is
+    below threshold (the reference's acceptance test, kf_workers.py:1353), or None; kf_eval_combos
+    launches of kf.batch lanes."""
+    width = kf.batch
+    for off in range(lo, hi, width):
+        cnt = min(width, hi - off)
+        mx, _, _ = kf.eval_combos(ev, init, prev_time, target_end, k, combo_offset=off, logdets=False)
+        ok = mx[:cnt] < threshold
+        if bool(ok.any()):
+            return off + int(torch.argmax(ok.to(torch.int8)).item())
+    return None
+
+
+def brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype='f64', device=0):
+    """The reference's result dict (kf_workers.py:1358-1367) for combination rank r of size k."""
+    combo = tuple(cand[i] for i in unrank_combination(len(cand), k, r))
+    metric, traj, combo, x_bf, P_bf, log_det, used = evaluate_combo_chunk([combo], xt, Pt, prev_time, target_end,
+                                                                          dtype, device)[0]
+    return {'selected_sensors': combo, 'final_state': x_bf, 'final_covariance': P_bf, 'trajectory': traj,
+            'accuracy_metric': metric, 'log_determinants': log_det, 'num_measurements_used': used}
+
+
+def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end_idx=None, R_threshold=None,
+                                                       initial_pt=None, initial_state=None,
+                                                       max_combos_in_memory=1 << 22, dtype='f64', device=0):
+    """kf_workers.py:1218-1392 on the GPU: for k = 1..n, evaluate every k-subset of the candidate
+    events (kf_eval_combos, one filter per subset, up to ``max_combos_in_memory`` per launch) and
+    return the first subset, in itertools.combinations order, whose max log-determinant is below
+    R_threshold — the reference's result dict — or None.  Multi-GPU: kfmi.dist.brute_force_search."""
+    if R_threshold is None:
+        raise ValueError('R_threshold must be specified for brute force KF.')
+    st = brute_force_setup(events, start_idx, end_idx, initial_pt, initial_state)
+    if st is None:
+        return None
+    cand, xt, Pt, prev_time, target_end, ev, init = st
+    n = len(cand)
     width = int(min(max_combos_in_memory, max(math.comb(n, k) for k in range(1, n + 1))))
     kf = BatchedKF('ref15', width, dtype, device=device)
     try:
         for k in range(1, n + 1):
-            total = math.comb(n, k)
-            for off in range(0, total, width):
-                mx, _, _ = kf.eval_combos(ev, init, prev_time, target_end, k, combo_offset=off, logdets=False)
-                ok = mx < R_threshold
-                if bool(ok.any()):
-                    r = off + int(torch.argmax(ok.to(torch.int8)).item())
-                    combo = tuple(cand[i] for i in unrank_combination(n, k, r))
-                    res = evaluate_combo_chunk([combo], xt, Pt, prev_time, target_end, dtype, device)[0]
-                    metric, traj, combo, x_bf, P_bf, log_det, used = res
-                    return {'selected_sensors': combo, 'final_state': x_bf, 'final_covariance': P_bf,
-                            'trajectory': traj, 'accuracy_metric': metric, 'log_determinants': log_det,
-                            'num_measurements_used': used}
+            r = first_valid_rank(kf, ev, init, prev_time, target_end, k, 0, math.comb(n, k), R_threshold)
+            if r is not None:
+                return brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype, device)
     finally:
         kf.close()
     return None

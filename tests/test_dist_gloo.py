@@ -74,3 +74,63 @@ def test_gloo_world2_shard_and_gather(total):
     err, slow = q.get(timeout=10)
     assert err < 1e-12
     assert slow == [1.5, 0.0]
+
+
+def _bf_worker(rank, world, port, golden, thr, out_q):
+    """kfmi.dist.brute_force_search on gloo with the oracle as the per-rank evaluator."""
+    import sys
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    sys.path.insert(0, os.path.dirname(__file__))
+    from golden_events import unpack_events
+    from kfmi import ref15
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        g = np.load(golden)
+        events = unpack_events(g)
+        s, e = int(g['start']), int(g['end'])
+        thr = float(g['threshold']) if thr is None else thr
+        cand, xt, Pt, prev, end, _, _ = ref15.brute_force_setup(events, s, e, g['init_P'], tuple(g['init_state']))
+        n = len(cand)
+        scanned = []
+
+        def first_valid(k, lo, hi):
+            scanned.append((k, lo, hi))
+            for r in range(lo, hi):
+                combo = tuple(cand[i] for i in ref15.unrank_combination(n, k, r))
+                res = ref_kf.evaluate_combo_chunk([combo], xt, Pt, prev, end)[0]
+                if max(res[5]) < thr:
+                    return r
+            return None
+
+        def finish(k, r):
+            return ref15.unrank_combination(n, k, r)
+
+        out = kdist.brute_force_search(events, s, e, R_threshold=thr, initial_pt=g['init_P'],
+                                       initial_state=tuple(g['init_state']), first_valid=first_valid, finish=finish)
+        out_q.put((rank, out, scanned, n))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('thr', [None, -1e9])  # the reference's threshold and winner; nothing acceptable
+def test_gloo_world2_brute_force_search(golden_dir, thr):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    golden = os.path.join(golden_dir, 'ref15_bruteforce.npz')
+    procs = [ctx.Process(target=_bf_worker, args=(r, 2, port, golden, thr, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert [p.exitcode for p in procs] == [0, 0]
+    res = dict((r, (out, sc, n)) for r, out, sc, n in (q.get(timeout=10), q.get(timeout=10)))
+    g = np.load(golden)
+    want = list(g['selected']) if thr is None else None
+    assert res[0][0] == want and res[1][0] == want          # every rank returns the same winner
+    n = res[0][2]
+    from math import comb
+    for k in range(1, (len(want) if want else n) + 1):      # the two ranks split each size exactly
+        spans = sorted((lo, hi) for r in (0, 1) for (kk, lo, hi) in res[r][1] if kk == k)
+        assert spans[0][0] == 0 and spans[-1][1] == comb(n, k)      # (a rank with no ranks skips)
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))

@@ -266,3 +266,27 @@ def test_score_candidates_random_batch():
                 rows = list(range(1, R.shape[0] + 1)) if full else [1]
                 want = np.trace(ref_kf.scheduler_cov_matrix(rows, Ps[b], R, H))
                 assert abs(gain[b, ti] - want) <= TOL * max(1.0, abs(want)), (full, b, s)
+
+
+def test_sharded_brute_force_single_rank(golden_dir):
+    """kfmi.dist.brute_force_search with the GPU evaluator on a world-1 group gives the
+    reference's winner (the gloo world-2 logic is covered in tests/test_dist_gloo.py)."""
+    import socket
+    import torch.distributed as dist
+    from kfmi import dist as kdist
+    g = _load(golden_dir, 'ref15_bruteforce.npz')
+    events = unpack_events(g)
+    s, e = int(g['start']), int(g['end'])
+    sk = socket.socket()
+    sk.bind(('127.0.0.1', 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1)
+    try:
+        out = kdist.brute_force_search(events, s, e, R_threshold=float(g['threshold']), initial_pt=g['init_P'],
+                                       initial_state=tuple(g['init_state']))
+    finally:
+        dist.destroy_process_group()
+    cand = events[s:e]
+    assert [cand.index(ev) for ev in out['selected_sensors']] == list(g['selected'])
+    assert _rel(out['log_determinants'], g['log_determinants']) <= TOL
