@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -49,6 +50,9 @@ size_t elem(const kf_batch* h) { return h->dtype == KF_F64 ? 8 : 4; }
 int64_t ntri(const kf_batch* h) { return h->np; }
 
 constexpr int kMaxComboEvents = 64;
+// below this many filters kf_run_events runs the chain-parallel kernel (B * 8 lanes): at 16384
+// filters one lane each is 256 waves, a quarter of the chip's SIMDs
+constexpr int64_t kChainMaxFilters = 16384;
 constexpr size_t kWsEvents = sizeof(double) * kMaxComboEvents * 11;
 constexpr size_t kWsBinom = sizeof(uint64_t) * (kMaxComboEvents + 1) * (kMaxComboEvents + 1);
 constexpr size_t kWsInit = sizeof(double) * 42;
@@ -395,7 +399,14 @@ int kf_run_events(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     a.updated = updated;
     a.gate = gate;
     a.threshold = threshold;
-    hipError_t e = kfmi::launch_ref_events(h->model, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
+    // Few filters cannot fill the chip one lane each: give every axis chain its own lane
+    // (8 lanes per filter).  KFMI_EVENTS_KERNEL=lane|chain forces a variant (tests, A/B).
+    bool chain = h->B < kChainMaxFilters;
+    if (const char* v = std::getenv("KFMI_EVENTS_KERNEL")) {
+        if (!std::strcmp(v, "chain")) chain = true;
+        else if (!std::strcmp(v, "lane")) chain = false;
+    }
+    hipError_t e = kfmi::launch_ref_events(h->model, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream), chain);
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_run_events");
 }
 

@@ -122,7 +122,8 @@ enum class Op { Run, Predict, Update, Reset };
 // Launchers (kf_cv.hip, kf_ref.hip).  Return hipSuccess or the launch error.
 hipError_t launch_cv(int axes, bool f64, Op op, const CvArgs& a, hipStream_t stream);
 hipError_t launch_synth(int axes, bool f64, const SynthArgs& a, hipStream_t stream);
-hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream);
+// chain = true: the chain-parallel kernel (kGroup lanes per filter), for few filters.
+hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, bool chain);
 hipError_t launch_ref_reset(int model, bool f64, const RefArgs& a, hipStream_t stream);
 hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream);
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream);

@@ -320,6 +320,165 @@ __global__ __launch_bounds__(kBlock) void ref_reset_kernel(const RefArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// Chain-parallel variant of ref_events_kernel for few filters (a single drive log): one lane
+// per axis chain, kGroup lanes per filter.  Without the adaptive gate the chains are
+// independent filters sharing an event stream, so a filter's per-event instruction stream
+// shrinks to one chain's; the log-determinant (and the gate) is the sum of the chains' logs
+// over the lane group (xor shuffles).  Every lane runs a 3-state chain: an (att, rate) chain
+// carries an inert third state (F couples nothing to it, Q = 0; its IMU row measures z = 0
+// with R = 1 and is reset after each update), so pva and aw lanes execute the same code.
+// The arithmetic per chain is the lane kernel's, operation for operation (the extra terms are
+// exact zeros); only the logdet is summed per chain instead of multiplied then logged.
+// ------------------------------------------------------------------------------------
+constexpr int kGroup = 8;
+
+template <typename T>
+__device__ __forceinline__ T group_sum(T v) {
+    v += __shfl_xor(v, 1, kGroup);
+    v += __shfl_xor(v, 2, kGroup);
+    v += __shfl_xor(v, 4, kGroup);
+    return v;
+}
+
+__device__ __forceinline__ bool group_any(bool b) {
+    int v = b ? 1 : 0;
+    v |= __shfl_xor(v, 1, kGroup);
+    v |= __shfl_xor(v, 2, kGroup);
+    v |= __shfl_xor(v, 4, kGroup);
+    return v != 0;
+}
+
+template <typename T>
+__device__ __forceinline__ T chain_log_det(const T (&P)[6]) {
+    T prod = T(1);
+    int ex = 0;
+    bool ok = true;
+    ldl_pivot_product<3, T>(P, prod, ex, ok);
+    const T ld = log_mant(prod, ex);
+    return ok ? ld : quiet_nan<T>();
+}
+
+template <typename T, class M>
+__global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
+    const int64_t g = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const int64_t f = g / kGroup;
+    if (f >= a.B) return;  // whole groups leave together (kGroup divides the wave)
+    const int c = static_cast<int>(g % kGroup);
+    const bool pva = c < M::NP;
+    const bool live = c < M::NP + M::NA;
+    const int ca = pva ? c : (live ? c - M::NP : 0);
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
+    const uint32_t rb8 = uint32_t(a.B) * 8u;
+    const uint32_t off8 = uint32_t(f) * 8u;
+    // this lane's state indices, block rows and constants
+    int xi[3], pr[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) xi[k] = pva ? M::pva(ca, k) : (k < 2 ? M::aw(ca, k) : -1);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int aw_row = k == 0 ? 0 : k == 1 ? 1 : k == 3 ? 2 : -1;  // (tt tw ww) of the 3x3 packing
+        pr[k] = !live ? -1 : pva ? 6 * ca + k : (aw_row < 0 ? -1 : 6 * M::NP + 3 * ca + aw_row);
+    }
+    const T q[3] = {T(pva ? kQPos : kQAtt), T(pva ? kQVel : kQRate), T(pva ? kQAcc : 0.0)};
+    const T Rimu[6] = {T(pva ? kRPos : kRAtt), T(0), T(0), T(pva ? kRVel : kRRate), T(0), T(pva ? kRAcc : 1.0)};
+    const int ia = pva ? ca : M::imu_att(ca);              // GPS position / IMU attitude column
+    const int ib = pva ? M::imu_acc(ca) : M::imu_rate(ca);  // IMU acceleration / rate column
+    T x[3], P[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) x[k] = (live && xi[k] >= 0) ? ldb<T>(a.x, xi[k], rb, off) : T(0);
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        P[k] = pr[k] >= 0 ? ldb<T>(a.P, pr[k], rb, off) : T(k == 0 || k == 3 || k == 5 ? 1 : 0);
+    int32_t st = a.status[f];
+    const uint32_t rb_tr = (a.traj && live && xi[0] < M::NTRAJ) ? rb : 0u;
+    const uint32_t rb_ld = (a.logdet && c == 0) ? rb : 0u;
+    const uint32_t rb_cv = (a.cov && live) ? rb : 0u;
+    const bool need_ld = a.logdet != nullptr;
+    for (int t = 0; t < a.T; ++t) {
+        const int type = a.etype[int64_t(t) * a.B + f];
+        const T dt = T(ldb<double>(a.dt, t, rb8, off8));
+        const T va = ldb<T>(a.payload, int64_t(t) * 9 + ia, rb, off);
+        const T vb = ldb<T>(a.payload, int64_t(t) * 9 + ib, rb, off);
+        bool applied = false;
+        if (type != 255) {
+            // predict: F = [[1, dt, c02], [0, 1, c12], [0, 0, 1]] (c02 = c12 = 0 on an aw lane)
+            const T c02 = pva ? T(0.5) * dt * dt : T(0);
+            const T c12 = pva ? dt : T(0);
+            const T xn0 = fmaT(c02, x[2], fmaT(dt, x[1], x[0]));
+            const T xn1 = fmaT(c12, x[2], x[1]);
+            T FP[3][3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                FP[0][j] = fmaT(c02, P[tri<3>(2, j)], fmaT(dt, P[tri<3>(1, j)], P[tri<3>(0, j)]));
+                FP[1][j] = fmaT(c12, P[tri<3>(2, j)], P[tri<3>(1, j)]);
+                FP[2][j] = P[tri<3>(2, j)];
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = i; j < 3; ++j) {
+                    T s = FP[i][j];
+                    if (j == 0) s = fmaT(FP[i][2], c02, fmaT(FP[i][1], dt, s));
+                    if (j == 1) s = fmaT(FP[i][2], c12, s);
+                    P[tri<3>(i, j)] = (i == j) ? s + q[i] * dt : s;
+                }
+            x[0] = xn0;
+            x[1] = xn1;
+            applied = (type == kGps || type == kImu);
+            if (a.gate && applied) applied = group_sum(live ? chain_log_det(P) : T(0)) > T(a.threshold);
+            bool ok = true;
+            if (applied) {
+                if (type == kGps) {
+                    if (pva) {
+                        const T zb[1] = {va};
+                        const T R[1] = {T(kRGps)};
+                        ok = sel_update<3, 1, true, T>(x, P, zb, R);
+                    }
+                } else {
+                    const T V = fmaT(vb, dt, x[1]);
+                    const T X = fmaT(V, dt, x[0]);
+                    const T zb[3] = {pva ? X : va, pva ? V : vb, pva ? vb : T(0)};
+                    ok = sel_update<3, 3, true, T>(x, P, zb, Rimu);
+                    if (!pva) {  // reset the inert state
+                        x[2] = T(0);
+                        P[5] = T(1);
+                    }
+                }
+            }
+            if (group_any(!ok)) {
+                st = kNotSpd;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) x[k] = quiet_nan<T>();
+#pragma unroll
+                for (int k = 0; k < 6; ++k) P[k] = quiet_nan<T>();
+            }
+        }
+        stb(a.traj, int64_t(t) * M::NTRAJ + (xi[0] < M::NTRAJ ? xi[0] : 0), rb_tr, off, x[0]);
+        if (rb_cv) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                if (pr[k] >= 0) stb(a.cov, int64_t(t) * M::NBLK + pr[k], rb_cv, off, P[k]);
+        }
+        if (need_ld) {
+            const T ld = group_sum(live ? chain_log_det(P) : T(0));
+            st = (ld == ld) ? st : kNotSpd;
+            stb(a.logdet, t, rb_ld, off, ld);
+        }
+        if (a.updated && c == 0) a.updated[int64_t(t) * a.B + f] = applied ? 1 : 0;
+    }
+    if (live) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            if (xi[k] >= 0) stb(a.x, xi[k], rb, off, x[k]);
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            if (pr[k] >= 0) stb(a.P, pr[k], rb, off, P[k]);
+    }
+    if (c == 0) a.status[f] = st;
+}
+
+// ------------------------------------------------------------------------------------
 // Brute-force combination search (kf_eval_combos).  The n candidate events and the binomial
 // table sit in LDS; lane f unranks combination combo_offset + f (lexicographic =
 // itertools.combinations order) one index at a time while it runs the filter, so no per-lane
@@ -552,7 +711,20 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
     return hipGetLastError();
 }
 
-hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream) {
+hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, bool chain) {
+    if (chain) {
+        const dim3 cgrid(static_cast<unsigned>((a.B * kGroup + kBlock - 1) / kBlock));
+        if (model == 15) {
+            if (f64) ref_chain_kernel<double, M15><<<cgrid, kBlock, 0, stream>>>(a);
+            else ref_chain_kernel<float, M15><<<cgrid, kBlock, 0, stream>>>(a);
+        } else if (model == 8) {
+            if (f64) ref_chain_kernel<double, M8><<<cgrid, kBlock, 0, stream>>>(a);
+            else ref_chain_kernel<float, M8><<<cgrid, kBlock, 0, stream>>>(a);
+        } else {
+            return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
     if (model == 15) {
         if (f64) ref_events_kernel<double, M15><<<grid, kBlock, 0, stream>>>(a);

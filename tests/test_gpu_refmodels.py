@@ -123,3 +123,61 @@ def test_ref8_handle_rejects_ref15_only_entry_points():
     for call in (lambda: kf.score_candidates([0]), lambda: kf.eval_combos(np.zeros((2, 11)), np.zeros(42), 0, 1, 1)):
         with pytest.raises(ValueError):
             call()
+
+
+def _events_run(model, kernel, etype, dt, pay, x0, P0b, threshold=None):
+    import os as _os
+    old = _os.environ.get('KFMI_EVENTS_KERNEL')
+    _os.environ['KFMI_EVENTS_KERNEL'] = kernel
+    try:
+        B = etype.shape[1]
+        kf = kfmi.BatchedKF(model, B, 'f64')
+        kf.set_state(np.ascontiguousarray(x0.T), np.ascontiguousarray(P0b.T))
+        tr, ld, up, cv = kf.run_events(etype, dt, pay, updated=True, cov=True, threshold=threshold)
+        x, Pb = kf.state()
+        out = [v.cpu().numpy() for v in (tr, ld, up, cv, x, Pb, kf.status())]
+        kf.close()
+        return out
+    finally:
+        if old is None:
+            del _os.environ['KFMI_EVENTS_KERNEL']
+        else:
+            _os.environ['KFMI_EVENTS_KERNEL'] = old
+
+
+@pytest.mark.parametrize('model', ['ref15', 'ref8'])
+@pytest.mark.parametrize('gated', [False, True])
+def test_chain_kernel_matches_lane_kernel(model, gated):
+    """The chain-parallel kernel (one lane per axis chain, used below 16384 filters) against the
+    lane-per-filter kernel on the same random streams: states, covariance records and update
+    decisions agree to rounding, logdets to the summation-order difference."""
+    rng = np.random.default_rng(21 if model == 'ref15' else 22)
+    n = 15 if model == 'ref15' else 8
+    B, T = 133, 48
+    etype = rng.choice([0, 1, 1, 1, 2], size=(T, B)).astype(np.uint8)
+    etype[40:, ::5] = 255
+    dt = rng.uniform(0.0, 0.05, (T, B))
+    pay = np.zeros((T, 9, B))
+    pay[:, 0:3] = rng.normal(0, 20, (T, 3, B))
+    pay[:, 3:6] = rng.normal(0, 0.05, (T, 3, B))
+    pay[:, 6:9] = rng.normal(0, 0.5, (T, 3, B))
+    x0 = rng.normal(0, 5, (B, n))
+    P0 = ref15.P0 if model == 'ref15' else ref8.P0
+    P0b = np.repeat(ref15.to_blocks(P0)[None], B, 0)
+    P0b[7] = -P0b[7]                                   # one non-positive-definite filter
+    thr = None
+    if gated:  # a threshold inside the run's own logdet range, so the gate both applies and skips
+        ld = _events_run(model, 'lane', etype, dt, pay, x0, P0b)[1]
+        thr = float(np.median(ld[np.isfinite(ld)]))
+    lane = _events_run(model, 'lane', etype, dt, pay, x0, P0b, thr)
+    chain = _events_run(model, 'chain', etype, dt, pay, x0, P0b, thr)
+    for name, a, b in zip(('traj', 'logdet', 'updated', 'cov', 'x', 'P', 'status'), lane, chain):
+        ok = np.isfinite(a)
+        np.testing.assert_array_equal(ok, np.isfinite(b), err_msg=name)
+        if name in ('updated', 'status'):
+            np.testing.assert_array_equal(a, b, err_msg=name)
+        else:
+            assert _rel(b[ok], a[ok]) <= 1e-12, name
+    assert lane[6][7] == kfmi.KF_ENOTSPD and (lane[6][np.arange(B) != 7] == 0).all()
+    if gated:
+        assert 0 < lane[2].mean() < 1                   # the gate both applied and skipped updates
