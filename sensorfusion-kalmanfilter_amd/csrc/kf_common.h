@@ -247,6 +247,30 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, int
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(p), 0, row_bytes, 0x00020000);
 }
 
+// A descriptor over rows [r0, r0 + nrows) of a [.][B] array, for lanes that address different
+// rows: the lane's row goes into voffset (row * row_bytes + off) so the descriptor stays
+// wave-uniform (a per-lane descriptor costs a waterfall loop per access).  A masked lane uses
+// kDropOffset: beyond every span, so its store is dropped and its load returns 0.
+constexpr uint32_t kDropOffset = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t span_rsrc(const void* base, int64_t r0, uint32_t row_bytes,
+                                                            uint32_t nrows) {
+    const char* p = reinterpret_cast<const char*>(base) + r0 * int64_t(row_bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(p), 0, base ? row_bytes * nrows : 0u, 0x00020000);
+}
+__device__ __forceinline__ double ldv(__amdgpu_buffer_rsrc_t r, uint32_t voff, double) {
+    return __builtin_bit_cast(double, (v2u)__builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0));
+}
+__device__ __forceinline__ float ldv(__amdgpu_buffer_rsrc_t r, uint32_t voff, float) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
+}
+__device__ __forceinline__ void stv(__amdgpu_buffer_rsrc_t r, uint32_t voff, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), r, voff, 0, 0);
+}
+__device__ __forceinline__ void stv(__amdgpu_buffer_rsrc_t r, uint32_t voff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, voff, 0, 0);
+}
+
 template <typename T>
 __device__ __forceinline__ T ldb(const void* base, int64_t r, uint32_t row_bytes, uint32_t off);
 template <>
@@ -256,6 +280,10 @@ __device__ __forceinline__ double ldb<double>(const void* base, int64_t r, uint3
 template <>
 __device__ __forceinline__ float ldb<float>(const void* base, int64_t r, uint32_t row_bytes, uint32_t off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base, r, row_bytes), off, 0, 0));
+}
+template <>
+__device__ __forceinline__ uint8_t ldb<uint8_t>(const void* base, int64_t r, uint32_t row_bytes, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b8(row_rsrc(base, r, row_bytes), off, 0, 0);
 }
 __device__ __forceinline__ void stb(void* base, int64_t r, uint32_t row_bytes, uint32_t off, double v) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), row_rsrc(base, r, row_bytes), off, 0, 0);

@@ -332,19 +332,37 @@ __global__ __launch_bounds__(kBlock) void ref_reset_kernel(const RefArgs a) {
 // ------------------------------------------------------------------------------------
 constexpr int kGroup = 8;
 
+// Sums / ORs over the 8-lane group with DPP (a VALU-latency lane exchange, no LDS round trip):
+// quad_perm [1,0,3,2] (xor 1), quad_perm [2,3,0,1] (xor 2), then row_half_mirror (lane i <-> 7-i
+// within each 8 lanes), which pairs the two quads.  Every lane of the group ends with the total.
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141;
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const v2u u = __builtin_bit_cast(v2u, v);
+    v2u r;
+    r.x = __builtin_amdgcn_mov_dpp(int(u.x), CTRL, 0xF, 0xF, false);
+    r.y = __builtin_amdgcn_mov_dpp(int(u.y), CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, r);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_d(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
 template <typename T>
 __device__ __forceinline__ T group_sum(T v) {
-    v += __shfl_xor(v, 1, kGroup);
-    v += __shfl_xor(v, 2, kGroup);
-    v += __shfl_xor(v, 4, kGroup);
+    v += dpp_d<kDppXor1>(v);
+    v += dpp_d<kDppXor2>(v);
+    v += dpp_d<kDppHalfMirror>(v);
     return v;
 }
 
 __device__ __forceinline__ bool group_any(bool b) {
     int v = b ? 1 : 0;
-    v |= __shfl_xor(v, 1, kGroup);
-    v |= __shfl_xor(v, 2, kGroup);
-    v |= __shfl_xor(v, 4, kGroup);
+    v |= __builtin_amdgcn_mov_dpp(v, kDppXor1, 0xF, 0xF, false);
+    v |= __builtin_amdgcn_mov_dpp(v, kDppXor2, 0xF, 0xF, false);
+    v |= __builtin_amdgcn_mov_dpp(v, kDppHalfMirror, 0xF, 0xF, false);
     return v != 0;
 }
 
@@ -357,6 +375,14 @@ __device__ __forceinline__ T chain_log_det(const T (&P)[6]) {
     const T ld = log_mant(prod, ex);
     return ok ? ld : quiet_nan<T>();
 }
+
+// Inputs of one event for one lane.
+template <typename T>
+struct ChainIn {
+    int type;
+    double dt;
+    T va, vb;
+};
 
 template <typename T, class M>
 __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
@@ -371,35 +397,50 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
     const uint32_t rb8 = uint32_t(a.B) * 8u;
     const uint32_t off8 = uint32_t(f) * 8u;
-    // this lane's state indices, block rows and constants
+    // this lane's state indices and block rows (-1: none), as voffsets into row spans
     int xi[3], pr[6];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) xi[k] = pva ? M::pva(ca, k) : (k < 2 ? M::aw(ca, k) : -1);
+    for (int k = 0; k < 3; ++k) xi[k] = !live ? -1 : pva ? M::pva(ca, k) : (k < 2 ? M::aw(ca, k) : -1);
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         const int aw_row = k == 0 ? 0 : k == 1 ? 1 : k == 3 ? 2 : -1;  // (tt tw ww) of the 3x3 packing
         pr[k] = !live ? -1 : pva ? 6 * ca + k : (aw_row < 0 ? -1 : 6 * M::NP + 3 * ca + aw_row);
     }
-    const T q[3] = {T(pva ? kQPos : kQAtt), T(pva ? kQVel : kQRate), T(pva ? kQAcc : 0.0)};
-    const T Rimu[6] = {T(pva ? kRPos : kRAtt), T(0), T(0), T(pva ? kRVel : kRRate), T(0), T(pva ? kRAcc : 1.0)};
+    uint32_t vx[3], vp[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) vx[k] = xi[k] >= 0 ? uint32_t(xi[k]) * rb + off : kDropOffset;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) vp[k] = pr[k] >= 0 ? uint32_t(pr[k]) * rb + off : kDropOffset;
+    const uint32_t v_tr = (xi[0] >= 0 && xi[0] < M::NTRAJ) ? uint32_t(xi[0]) * rb + off : kDropOffset;
+    const uint32_t v_ld = c == 0 ? off : kDropOffset;
     const int ia = pva ? ca : M::imu_att(ca);              // GPS position / IMU attitude column
     const int ib = pva ? M::imu_acc(ca) : M::imu_rate(ca);  // IMU acceleration / rate column
+    const uint32_t v_a = uint32_t(ia) * rb + off, v_b = uint32_t(ib) * rb + off;
+    const T q[3] = {T(pva ? kQPos : kQAtt), T(pva ? kQVel : kQRate), T(pva ? kQAcc : 0.0)};
+    const T Rimu[6] = {T(pva ? kRPos : kRAtt), T(0), T(0), T(pva ? kRVel : kRRate), T(0), T(pva ? kRAcc : 1.0)};
+
     T x[3], P[6];
+    {
+        const auto rx = span_rsrc(a.x, 0, rb, M::N), rp = span_rsrc(a.P, 0, rb, M::NBLK);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) x[k] = (live && xi[k] >= 0) ? ldb<T>(a.x, xi[k], rb, off) : T(0);
+        for (int k = 0; k < 3; ++k) x[k] = ldv(rx, vx[k], T(0));
 #pragma unroll
-    for (int k = 0; k < 6; ++k)
-        P[k] = pr[k] >= 0 ? ldb<T>(a.P, pr[k], rb, off) : T(k == 0 || k == 3 || k == 5 ? 1 : 0);
+        for (int k = 0; k < 6; ++k) P[k] = pr[k] >= 0 ? ldv(rp, vp[k], T(0)) : T(k == 0 || k == 3 || k == 5 ? 1 : 0);
+    }
     int32_t st = a.status[f];
-    const uint32_t rb_tr = (a.traj && live && xi[0] < M::NTRAJ) ? rb : 0u;
-    const uint32_t rb_ld = (a.logdet && c == 0) ? rb : 0u;
-    const uint32_t rb_cv = (a.cov && live) ? rb : 0u;
     const bool need_ld = a.logdet != nullptr;
-    for (int t = 0; t < a.T; ++t) {
-        const int type = a.etype[int64_t(t) * a.B + f];
-        const T dt = T(ldb<double>(a.dt, t, rb8, off8));
-        const T va = ldb<T>(a.payload, int64_t(t) * 9 + ia, rb, off);
-        const T vb = ldb<T>(a.payload, int64_t(t) * 9 + ib, rb, off);
+
+    auto load = [&](int t, ChainIn<T>& in) {
+        in.type = int(ldb<uint8_t>(a.etype, t, uint32_t(a.B), uint32_t(f)));
+        in.dt = ldb<double>(a.dt, t, rb8, off8);
+        const auto rpay = span_rsrc(a.payload, int64_t(t) * 9, rb, 9);
+        in.va = ldv(rpay, v_a, T(0));
+        in.vb = ldv(rpay, v_b, T(0));
+    };
+    auto step = [&](int t, const ChainIn<T>& in) {
+        const int type = in.type;
+        const T dt = T(in.dt);
+        const T va = in.va, vb = in.vb;
         bool applied = false;
         if (type != 255) {
             // predict: F = [[1, dt, c02], [0, 1, c12], [0, 0, 1]] (c02 = c12 = 0 on an aw lane)
@@ -454,26 +495,38 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
                 for (int k = 0; k < 6; ++k) P[k] = quiet_nan<T>();
             }
         }
-        stb(a.traj, int64_t(t) * M::NTRAJ + (xi[0] < M::NTRAJ ? xi[0] : 0), rb_tr, off, x[0]);
-        if (rb_cv) {
+        stv(span_rsrc(a.traj, int64_t(t) * M::NTRAJ, rb, M::NTRAJ), v_tr, x[0]);
+        {
+            const auto rc = span_rsrc(a.cov, int64_t(t) * M::NBLK, rb, M::NBLK);
 #pragma unroll
-            for (int k = 0; k < 6; ++k)
-                if (pr[k] >= 0) stb(a.cov, int64_t(t) * M::NBLK + pr[k], rb_cv, off, P[k]);
+            for (int k = 0; k < 6; ++k) stv(rc, vp[k], P[k]);
         }
         if (need_ld) {
             const T ld = group_sum(live ? chain_log_det(P) : T(0));
             st = (ld == ld) ? st : kNotSpd;
-            stb(a.logdet, t, rb_ld, off, ld);
+            stv(span_rsrc(a.logdet, t, rb, 1), v_ld, ld);
         }
         if (a.updated && c == 0) a.updated[int64_t(t) * a.B + f] = applied ? 1 : 0;
+    };
+
+    // unrolled x2 over two named input buffers: event t+1 loads while event t computes, with no
+    // loop-carried register copy (a copy would wait on the loads at the back edge)
+    ChainIn<T> A, Bn;
+    if (a.T > 0) load(0, A);
+    for (int t = 0; t < a.T; t += 2) {
+        const bool two = t + 1 < a.T;
+        load(two ? t + 1 : t, Bn);
+        step(t, A);
+        if (!two) break;
+        load(t + 2 < a.T ? t + 2 : t + 1, A);
+        step(t + 1, Bn);
     }
-    if (live) {
+    {
+        const auto rx = span_rsrc(a.x, 0, rb, M::N), rp = span_rsrc(a.P, 0, rb, M::NBLK);
 #pragma unroll
-        for (int k = 0; k < 3; ++k)
-            if (xi[k] >= 0) stb(a.x, xi[k], rb, off, x[k]);
+        for (int k = 0; k < 3; ++k) stv(rx, vx[k], x[k]);
 #pragma unroll
-        for (int k = 0; k < 6; ++k)
-            if (pr[k] >= 0) stb(a.P, pr[k], rb, off, P[k]);
+        for (int k = 0; k < 6; ++k) stv(rp, vp[k], P[k]);
     }
     if (c == 0) a.status[f] = st;
 }
