@@ -557,7 +557,8 @@ __global__ __launch_bounds__(kBlock) void ref15_combo_kernel(const Ref15ComboArg
     const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
     const uint64_t rank0 = a.combo_offset + uint64_t(f);
     const bool live = rank0 < a.n_combos;
-    const uint32_t rb_ld = a.logdets ? rb : 0u;
+    // records land at a per-lane row (a skipped event shifts them): one span over the k+2 rows
+    const auto r_ld = span_rsrc(a.logdets, 0, rb, uint32_t(a.k + 2));
 
     Ref15<T> s;
 #pragma unroll
@@ -569,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void ref15_combo_kernel(const Ref15ComboArg
     T ld = s.logdet();
     T ld_max = ld;
     int rec = 0;
-    stb(a.logdets, rec, rb_ld, off, ld);
+    stv(r_ld, uint32_t(rec) * rb + off, ld);
     ++rec;
     bool ok = true;
     double cur = a.prev_time;
@@ -597,7 +598,7 @@ __global__ __launch_bounds__(kBlock) void ref15_combo_kernel(const Ref15ComboArg
         cur = te;
         ld = s.logdet();
         ld_max = ld > ld_max ? ld : ld_max;
-        stb(a.logdets, rec, rb_ld, off, ld);
+        stv(r_ld, uint32_t(rec) * rb + off, ld);
         ++rec;
     }
     // always propagate to the common end time (kf_workers.py:74-82)
@@ -605,10 +606,10 @@ __global__ __launch_bounds__(kBlock) void ref15_combo_kernel(const Ref15ComboArg
         s.predict(T(a.target_end - cur));
         ld = s.logdet();
         ld_max = ld > ld_max ? ld : ld_max;
-        stb(a.logdets, rec, rb_ld, off, ld);
+        stv(r_ld, uint32_t(rec) * rb + off, ld);
         ++rec;
     }
-    for (int q = rec; q < a.k + 2; ++q) stb(a.logdets, q, rb_ld, off, quiet_nan<T>());
+    for (int q = rec; q < a.k + 2; ++q) stv(r_ld, uint32_t(q) * rb + off, quiet_nan<T>());
     int32_t st = ok ? 0 : kNotSpd;
     if (!live) {
         st = 1;
@@ -667,6 +668,25 @@ __device__ __forceinline__ T posterior_trace(const Ref15<T>& s0, int type, bool 
     return cov_trace(posterior(s0, type, full));
 }
 
+// The greedy scheduler's gain (S = [1]): only the x-axis (pos, vel, acc) block changes, so the
+// trace is the current one with that block's diagonal replaced — no copy of the whole state.
+template <typename T>
+__device__ __forceinline__ T first_row_gain(const Ref15<T>& s, int type) {
+    T p[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) p[k] = s.pva[0][k];
+    T xb[3] = {T(0), T(0), T(0)};
+    const T z[1] = {T(0)};
+    const T R[1] = {T(type == kGps ? kRGps : kRPos)};
+    sel_update<3, 1, true, T>(xb, p, z, R);
+    T tr = p[0] + p[3] + p[5];
+#pragma unroll
+    for (int i = 1; i < 3; ++i) tr += s.pva[i][0] + s.pva[i][3] + s.pva[i][5];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) tr += s.aw[i][0] + s.aw[i][2];
+    return tr;
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void ref15_score_kernel(const Ref15ScoreArgs a) {
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -690,7 +710,7 @@ __global__ __launch_bounds__(kBlock) void ref15_sched_kernel(const Ref15SchedArg
     const int64_t B = a.B;
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(B) * uint32_t(sizeof(T));
-    const uint32_t rb_tr = a.traj ? rb : 0u, rb_ld = a.logdet ? rb : 0u;
+    // compacted per-selection records are addressed per lane below
     Ref15<T> s;
     s.load(a.x, a.P, rb, off);
     int32_t st = a.status[f];
@@ -712,8 +732,8 @@ __global__ __launch_bounds__(kBlock) void ref15_sched_kernel(const Ref15SchedArg
         }
         // greedy_schedule (kf_workers.py:195-213): first queued candidate with the largest
         // gain = trace of the S=[1] posterior on the current covariance
-        const T g_gps = posterior_trace(s, kGps, false);
-        const T g_imu = posterior_trace(s, kImu, false);
+        const T g_gps = first_row_gain(s, kGps);
+        const T g_imu = first_row_gain(s, kImu);
         T best = -__builtin_inf();
         int sel = q_start;
         for (int j = q_start; j < q_start + q_len; ++j) {
@@ -728,17 +748,23 @@ __global__ __launch_bounds__(kBlock) void ref15_sched_kernel(const Ref15SchedArg
         q_len = 0;
         const double tsel = a.t[int64_t(sel) * B + f];
         T pay[9];
+        // the selected event differs per lane: plain 64-bit addressing (a buffer descriptor per
+        // lane would be a waterfall loop)
+        const T* ps = static_cast<const T*>(a.payload) + int64_t(sel) * 9 * B + f;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) pay[k] = ldb<T>(a.payload, int64_t(sel) * 9 + k, rb, off);
+        for (int k = 0; k < 9; ++k) pay[k] = ps[int64_t(k) * B];
         bool ok = true;
         s.event(a.etype[int64_t(sel) * B + f], T(tsel - prev), pay, false, T(0), ok);
         if (!ok) {
             st = kNotSpd;
             s.fill_nan();
         }
+        if (a.traj) {
+            T* tr = static_cast<T*>(a.traj) + int64_t(nsel) * 6 * B + f;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) stb(a.traj, int64_t(nsel) * 6 + k, rb_tr, off, s.x[k]);
-        if (a.logdet) stb(a.logdet, nsel, rb_ld, off, s.logdet());
+            for (int k = 0; k < 6; ++k) tr[int64_t(k) * B] = s.x[k];
+        }
+        if (a.logdet) static_cast<T*>(a.logdet)[int64_t(nsel) * B + f] = s.logdet();
         if (a.sel_time) a.sel_time[int64_t(nsel) * B + f] = tsel;
         ++nsel;
         prev = tsel;
