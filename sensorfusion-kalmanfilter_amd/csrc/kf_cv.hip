@@ -122,8 +122,9 @@ struct StepIn {
 // The time loop is unrolled by two with statically named input buffers A and B: step t+1's
 // inputs are loaded before step t computes, and no loop-carried register copy forces the
 // wave to wait for its own trajectory stores (s_waitcnt counts loads and stores together).
-// Every step loads the z of the next update (clamped), so between GPS updates the same
-// line is re-read from L2 instead of a branch being taken around the load.
+// z is read only for the steps that update: on the others its row descriptor has length 0 (the
+// step index is wave-uniform), so the load instruction issues but the range check returns 0
+// without touching memory — no branch, and no re-reads of the same fix between updates.
 // ------------------------------------------------------------------------------------
 // Minimum waves per SIMD requested from the register allocator for the run kernel (1 = let
 // the compiler choose).  Overridable at build time for occupancy experiments.
@@ -189,9 +190,11 @@ __global__ __launch_bounds__(kBlock, (RunOcc<D, T>::value)) void cv_run_kernel(c
         for (int i = 0; i < D; ++i) in.u[i] = ldb<T>(a.u, int64_t(tc) * D + i, rb_u, off);
         int s = ld_s < U ? ld_s : U - 1;
         s = s > 0 ? s : 0;
+        const bool upd = tc == ld_upd_step;  // wave-uniform
+        const uint32_t rbz = upd ? rb_z : 0u;
 #pragma unroll
-        for (int i = 0; i < M; ++i) in.z[i] = ldb<T>(a.z, int64_t(s) * M + i, rb_z, off);
-        in.use = (has_mask && U > 0) ? a.mask[int64_t(s) * B + f] : uint8_t(1);
+        for (int i = 0; i < M; ++i) in.z[i] = ldb<T>(a.z, int64_t(s) * M + i, rbz, off);
+        in.use = (has_mask && U > 0 && upd) ? a.mask[int64_t(s) * B + f] : uint8_t(1);
     };
 
     int until_upd = k_upd;
