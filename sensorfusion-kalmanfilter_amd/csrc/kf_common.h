@@ -271,6 +271,29 @@ __device__ __forceinline__ void stv(__amdgpu_buffer_rsrc_t r, uint32_t voff, flo
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, voff, 0, 0);
 }
 
+// Cache policy of the once-touched streams (inputs read once, records written once).  Default
+// policy: nt (aux = 2) was A/B-measured mixed (config 2 +3 %, config 4 -2 %, configs 3/5 within
+// box noise; profiles/r01_ab/nt_streams_ab.txt).  -DKF_STREAM_CPOL=2 builds the nt variant.
+#ifndef KF_STREAM_CPOL
+#define KF_STREAM_CPOL 0
+#endif
+__device__ __forceinline__ double ldb_stream(const void* base, int64_t r, uint32_t row_bytes, uint32_t off, double) {
+    return __builtin_bit_cast(double, (v2u)__builtin_amdgcn_raw_buffer_load_b64(row_rsrc(base, r, row_bytes), off, 0,
+                                                                                KF_STREAM_CPOL));
+}
+__device__ __forceinline__ float ldb_stream(const void* base, int64_t r, uint32_t row_bytes, uint32_t off, float) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base, r, row_bytes), off, 0,
+                                                                          KF_STREAM_CPOL));
+}
+__device__ __forceinline__ void stb_stream(void* base, int64_t r, uint32_t row_bytes, uint32_t off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), row_rsrc(base, r, row_bytes), off, 0,
+                                          KF_STREAM_CPOL);
+}
+__device__ __forceinline__ void stb_stream(void* base, int64_t r, uint32_t row_bytes, uint32_t off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), row_rsrc(base, r, row_bytes), off, 0,
+                                          KF_STREAM_CPOL);
+}
+
 template <typename T>
 __device__ __forceinline__ T ldb(const void* base, int64_t r, uint32_t row_bytes, uint32_t off);
 template <>

@@ -187,13 +187,13 @@ __global__ __launch_bounds__(kBlock, (RunOcc<D, T>::value)) void cv_run_kernel(c
             ++ld_s;
         }
 #pragma unroll
-        for (int i = 0; i < D; ++i) in.u[i] = ldb<T>(a.u, int64_t(tc) * D + i, rb_u, off);
+        for (int i = 0; i < D; ++i) in.u[i] = ldb_stream(a.u, int64_t(tc) * D + i, rb_u, off, T(0));
         int s = ld_s < U ? ld_s : U - 1;
         s = s > 0 ? s : 0;
         const bool upd = tc == ld_upd_step;  // wave-uniform
         const uint32_t rbz = upd ? rb_z : 0u;
 #pragma unroll
-        for (int i = 0; i < M; ++i) in.z[i] = ldb<T>(a.z, int64_t(s) * M + i, rbz, off);
+        for (int i = 0; i < M; ++i) in.z[i] = ldb_stream(a.z, int64_t(s) * M + i, rbz, off, T(0));
         in.use = (has_mask && U > 0 && upd) ? a.mask[int64_t(s) * B + f] : uint8_t(1);
     };
 
@@ -212,11 +212,11 @@ __global__ __launch_bounds__(kBlock, (RunOcc<D, T>::value)) void cv_run_kernel(c
             }
         }
 #pragma unroll
-        for (int i = 0; i < N; ++i) stb(a.traj, int64_t(t) * N + i, rb_tr, off, x[i]);
+        for (int i = 0; i < N; ++i) stb_stream(a.traj, int64_t(t) * N + i, rb_tr, off, x[i]);
         if (has_ld) {
             const T ld = logdet_ldl<N, T>(P);
             st = (ld == ld) ? st : kNotSpd;
-            stb(a.logdet, t, rb, off, ld);
+            stb_stream(a.logdet, t, rb, off, ld);
         }
     };
 

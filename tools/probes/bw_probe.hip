@@ -42,6 +42,71 @@ __global__ __launch_bounds__(256) void tiled_stream(const double* __restrict__ i
         for (int i = 0; i < 7; ++i) out[((long(t) * W + w) * 7 + i) * 64 + l] = acc + i;
     }
 }
+// SoA rows moved 16 B per lane: lane pairs (2j, 2j+1) swap one value with DPP (quad_perm
+// [1,0,3,2]) so the even lane moves row r of filters (2j, 2j+1) and the odd lane row r+1.
+__device__ __forceinline__ double swap_pair(double v) {
+    int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0xB1, 0xF, 0xF, false);
+    int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+template <bool PAIR_LOADS>
+__global__ __launch_bounds__(256) void soa_stream_pair(const double* __restrict__ in, double* __restrict__ out,
+                                                       long B, int T) {
+    long f = long(blockIdx.x) * 256 + threadIdx.x;
+    if (f >= B) return;
+    const bool odd = f & 1;
+    const long fe = f & ~1L;  // the pair's even filter
+    double acc = 0;
+    for (int t = 0; t < T; ++t) {
+        double v[6];
+        if (PAIR_LOADS) {
+#pragma unroll
+            for (int i = 0; i < 6; i += 2) {
+                // even lane loads row i of (fe, fe+1), odd lane row i+1
+                const double2 w = *reinterpret_cast<const double2*>(&in[(long(t) * 6 + i + (odd ? 1 : 0)) * B + fe]);
+                const double mine = odd ? w.y : w.x;     // this lane's filter in the row it loaded
+                const double other = odd ? w.x : w.y;    // the partner's filter
+                const double got = swap_pair(other);     // partner sends me my filter of its row
+                v[i] = odd ? got : mine;
+                v[i + 1] = odd ? mine : got;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) v[i] = in[(long(t) * 6 + i) * B + f];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) acc += v[i];
+        double o[7];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) o[i] = acc + i;
+#pragma unroll
+        for (int i = 0; i < 6; i += 2) {
+            const double send = odd ? o[i] : o[i + 1];   // what the partner stores for me
+            const double recv = swap_pair(send);
+            double2 w;
+            w.x = odd ? recv : o[i];        // even: (row i: fe, fe+1); odd: (row i+1: fe, fe+1)
+            w.y = odd ? o[i + 1] : recv;
+            *reinterpret_cast<double2*>(&out[(long(t) * 7 + i + (odd ? 1 : 0)) * B + fe]) = w;
+        }
+        out[(long(t) * 7 + 6) * B + f] = o[6];
+    }
+}
+// Non-temporal stores of the SoA pattern.
+__global__ __launch_bounds__(256) void soa_stream_nt(const double* __restrict__ in, double* __restrict__ out,
+                                                     long B, int T) {
+    long f = long(blockIdx.x) * 256 + threadIdx.x;
+    if (f >= B) return;
+    double acc = 0;
+    for (int t = 0; t < T; ++t) {
+        double v[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v[i] = __builtin_nontemporal_load(&in[(long(t) * 6 + i) * B + f]);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) acc += v[i];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) __builtin_nontemporal_store(acc + i, &out[(long(t) * 7 + i) * B + f]);
+    }
+}
 // Read-only and write-only SoA variants.
 __global__ __launch_bounds__(256) void soa_read(const double* __restrict__ in, double* __restrict__ out, long B, int T) {
     long f = long(blockIdx.x) * 256 + threadIdx.x;
@@ -91,6 +156,10 @@ int main(int argc, char** argv) {
         ms /= reps;
         printf("%-14s %8.3f ms  %7.0f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
     };
+    timeit("soa_stream", [&] { soa_stream<<<grid, 256>>>(in, out, B, T); }, double(in_bytes + out_bytes));
+    timeit("soa_pair_ldst", [&] { soa_stream_pair<true><<<grid, 256>>>(in, out, B, T); }, double(in_bytes + out_bytes));
+    timeit("soa_pair_st", [&] { soa_stream_pair<false><<<grid, 256>>>(in, out, B, T); }, double(in_bytes + out_bytes));
+    timeit("soa_stream_nt", [&] { soa_stream_nt<<<grid, 256>>>(in, out, B, T); }, double(in_bytes + out_bytes));
     timeit("soa_stream", [&] { soa_stream<<<grid, 256>>>(in, out, B, T); }, double(in_bytes + out_bytes));
     timeit("tiled_stream", [&] { tiled_stream<<<grid, 256>>>(in, out, B, T); }, double(in_bytes + out_bytes));
     timeit("soa_read", [&] { soa_read<<<grid, 256>>>(in, out, B, T); }, double(in_bytes));
