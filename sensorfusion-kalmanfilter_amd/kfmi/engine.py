@@ -148,7 +148,14 @@ class BatchedKF:
 
     # -- per-step call shape (kf_workers.py:688-717) ----------------------------------------
     def predict(self, dt, u=None, dt_per_filter=None, logdet=False):
-        """x = F(dt) x + G(dt) u, P = F P F^T + Q(dt).  Returns logdet(P_pred) [B] if asked."""
+        """x = F(dt) x + G(dt) u, P = F P F^T + Q(dt).  Returns logdet(P_pred) [B] if asked.
+        Reference models: one KF_EVENT_PREDICT event per filter (kf_run_events, T = 1)."""
+        if self.model in REF_MODELS:
+            if u is not None:
+                raise ValueError(f'{self.model}: no control input (the IMU enters as a measurement)')
+            dts = (dt_per_filter if dt_per_filter is not None else
+                   np.full(self.batch, float(dt if dt is not None else 0.0)))
+            return self._event(_lib.KF_EVENT_PREDICT, dts, None, None, logdet)
         ud = self._dev(u, (self.c, self.batch), 'u') if u is not None else None
         dtf = (self._dev(dt_per_filter, (self.batch,), 'dt_per_filter', torch.float64)
                if dt_per_filter is not None else None)
@@ -157,13 +164,61 @@ class BatchedKF:
                                     _ptr(ud), _ptr(ld), self._stream()))
         return ld
 
-    def update(self, z, mask=None, logdet=True):
-        """GPS update with z [m, B]; mask [B] (0 = skip).  Returns logdet(P) [B] if asked."""
+    def update(self, z, mask=None, logdet=True, sensor='gps'):
+        """GPS update with z [m, B]; mask [B] (0 = skip).  Returns logdet(P) [B] if asked.
+        Reference models: a GPS fix event at dt = 0 (the predict is then exactly the identity);
+        the IMU pseudo-measurement is built from the predicted state and the event's dt
+        (kf_workers.py:698-706), so it is an event: ``step('imu', dt, payload)``."""
+        if self.model in REF_MODELS:
+            if sensor != 'gps':
+                raise ValueError("the IMU update needs the event's dt: use step('imu', dt, payload)")
+            zz = z.cpu().numpy() if torch.is_tensor(z) else np.asarray(z)
+            if zz.shape != (self.m, self.batch):
+                raise ValueError(f'z: shape {zz.shape} != expected {(self.m, self.batch)}')
+            pay = np.zeros((9, self.batch))
+            pay[:self.m] = zz
+            return self._event(_lib.KF_EVENT_GPS, np.zeros(self.batch), pay, mask, logdet)
         zd = self._dev(z, (self.m, self.batch), 'z')
         md = self._dev(mask, (self.batch,), 'mask', torch.uint8) if mask is not None else None
         ld = self.empty(self.batch) if logdet else None
         check(_lib.lib().kf_update(self.handle, _ptr(zd), _ptr(md), _ptr(ld), self._stream()))
         return ld
+
+    def step(self, sensor, dt, payload, mask=None, logdet=True):
+        """Reference models: one event of the reference loop for every filter (kf_workers.py:
+        688-717): predict over dt (scalar or [B]), then the GPS fix (payload [3, B]: easting,
+        northing, altitude) or the IMU pseudo-measurement (payload [9, B]: roll, pitch, yaw,
+        wx, wy, wz, ax, ay, az).  mask [B]: 0 = no event for that filter.  Returns logdet [B]."""
+        if self.model not in REF_MODELS:
+            raise ValueError('step() is the event call of the reference models (ref15 / ref8)')
+        et = {'gps': _lib.KF_EVENT_GPS, 'imu': _lib.KF_EVENT_IMU}.get(sensor)
+        if et is None:
+            raise ValueError(f"sensor must be 'gps' or 'imu', not {sensor!r}")
+        pp = payload.cpu().numpy() if torch.is_tensor(payload) else np.asarray(payload)
+        rows = 3 if sensor == 'gps' else 9
+        if pp.shape != (rows, self.batch):
+            raise ValueError(f'payload: shape {pp.shape} != expected {(rows, self.batch)}')
+        pay = np.zeros((9, self.batch))
+        pay[:rows] = pp
+        dts = np.array(np.broadcast_to(np.asarray(dt, dtype=np.float64), (self.batch,)))
+        return self._event(et, dts, pay, mask, logdet)
+
+    def logdet(self):
+        """log det P of every filter's current covariance [B] (no state change)."""
+        if self.model in REF_MODELS:
+            return self._event(_lib.KF_EVENT_NONE, np.zeros(self.batch), None, None, True)
+        return self.predict(0.0, logdet=True)  # F(0) = I, Q(0) = 0: P is left exactly as it is
+
+    def _event(self, etype, dts, payload, mask, logdet):
+        et = np.full((1, self.batch), etype, np.uint8)
+        if mask is not None:
+            m = mask.cpu().numpy() if torch.is_tensor(mask) else np.asarray(mask)
+            et[0, m.reshape(-1) == 0] = _lib.KF_EVENT_NONE
+        npd = DTYPES[self.dtype][2]
+        pay = np.zeros((1, 9, self.batch), npd) if payload is None else np.asarray(payload, npd)[None]
+        _, ld, _, _ = self.run_events(et, np.asarray(dts, np.float64).reshape(1, self.batch), pay, traj=False,
+                                      logdet=logdet)
+        return ld[0] if logdet else None
 
     # -- fused hot path -----------------------------------------------------------------
     def run(self, u, z, dt=None, dt_steps=None, update_every=1, mask=None, traj=True, logdet=True,

@@ -172,9 +172,11 @@ def test_run_events_random_batch_vs_oracle():
 
 
 def test_ref15_handle_rejects_cv_entry_points():
+    from kfmi import _lib
     kf = kfmi.BatchedKF('ref15', 4, 'f64')
-    with pytest.raises(kfmi.KFError):
-        kf.predict(0.1)
+    assert _lib.lib().kf_predict(kf.handle, 0.1, None, None, None, None) == _lib.KF_EINVAL  # C ABI: cv only
+    with pytest.raises(ValueError):
+        kf.predict(0.1, u=np.zeros((3, 4)))
     with pytest.raises(ValueError):
         kfmi.BatchedKF('cv3', 4, 'f64').run_events(np.zeros((1, 4), np.uint8), np.zeros((1, 4)), np.zeros((1, 9, 4)))
 

@@ -117,9 +117,9 @@ def test_ref8_random_batch_vs_oracle():
 
 
 def test_ref8_handle_rejects_ref15_only_entry_points():
+    from kfmi import _lib
     kf = kfmi.BatchedKF('ref8', 4, 'f64')
-    with pytest.raises(kfmi.KFError):
-        kf.predict(0.1)
+    assert _lib.lib().kf_update(kf.handle, None, None, None, None) == _lib.KF_EINVAL
     for call in (lambda: kf.score_candidates([0]), lambda: kf.eval_combos(np.zeros((2, 11)), np.zeros(42), 0, 1, 1)):
         with pytest.raises(ValueError):
             call()
@@ -181,3 +181,48 @@ def test_chain_kernel_matches_lane_kernel(model, gated):
     assert lane[6][7] == kfmi.KF_ENOTSPD and (lane[6][np.arange(B) != 7] == 0).all()
     if gated:
         assert 0 < lane[2].mean() < 1                   # the gate both applied and skipped updates
+
+
+def test_per_step_calls_on_reference_models():
+    """predict / update(sensor='gps') / step('imu') / logdet on a ref15 handle reproduce the
+    oracle's dense per-event steps (the reference's per-call shape, kf_workers.py:688-717)."""
+    rng = np.random.default_rng(31)
+    B = 70
+    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    x0 = rng.normal(0, 5, (B, 15))
+    kf.reset(torch.from_numpy(np.ascontiguousarray(x0.T)).cuda())
+    xs = [x0[f].copy() for f in range(B)]
+    Ps = [ref_kf.P0_REF15.copy() for _ in range(B)]
+    ld0 = kf.logdet().cpu().numpy()
+    assert np.allclose(ld0, np.linalg.slogdet(ref_kf.P0_REF15)[1], rtol=1e-12)
+    for k in range(12):
+        dt = rng.uniform(0.001, 0.05, B)
+        if k % 3 == 0:
+            ld = kf.predict(None, dt_per_filter=dt, logdet=True).cpu().numpy()
+            for f in range(B):
+                F = ref_kf.F_ref15(dt[f])
+                xs[f] = F @ xs[f]
+                Ps[f] = ref_kf.predict_covariance(Ps[f], F, ref_kf.Q_ref15(dt[f]))
+        elif k % 3 == 1:
+            z = rng.normal(0, 20, (3, B))
+            mask = (rng.random(B) > 0.2).astype(np.uint8)
+            ld = kf.update(z, mask=mask, sensor='gps').cpu().numpy()
+            for f in range(B):
+                if mask[f]:
+                    xs[f], Ps[f] = ref_kf.step15(xs[f], Ps[f], 'GPS', {'easting': z[0, f], 'northing': z[1, f],
+                                                                        'altitude': z[2, f]}, 0.0)
+        else:
+            imu = np.concatenate([rng.normal(0, 0.05, (6, B)), rng.normal(0, 0.5, (3, B))])
+            ld = kf.step('imu', dt, imu).cpu().numpy()
+            for f in range(B):
+                xs[f], Ps[f] = ref_kf.step15(xs[f], Ps[f], 'IMU', ['t', *imu[:, f]], dt[f])
+        for f in range(0, B, 3):
+            ref = np.linalg.slogdet(Ps[f])[1]
+            assert abs(ld[f] - ref) <= TOL * max(1.0, abs(ref)), (k, f)
+    x, Pb = kf.state()
+    x, Pb = x.cpu().numpy(), Pb.cpu().numpy()
+    for f in range(B):
+        assert _rel(x[:, f], xs[f]) <= TOL
+        assert _rel(ref15.from_blocks(Pb[:, f]), Ps[f]) <= TOL
+    with pytest.raises(ValueError):
+        kf.update(np.zeros((3, B)), sensor='imu')
