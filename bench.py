@@ -66,6 +66,15 @@ def algorithmic_bytes(cfg):
     return per_filter * B, per_filter / T
 
 
+def ref15_algorithmic_bytes(cfg):
+    """Bytes one kf_run_events launch must move for the 15-state model: per filter per event
+    etype 1 + dt 8 + payload 72 read, traj 48 + logdet 8 written; per filter per launch the
+    state (15 + 27 block rows) loaded and stored and status read + written."""
+    T, B = cfg['T'], cfg['B']
+    per_filter = T * (1 + 8 + 72 + 48 + 8) + 2 * (15 + 27) * 8 + 8
+    return per_filter * B, per_filter / T
+
+
 def host_cpu():
     try:
         with open('/proc/cpuinfo') as f:
@@ -199,10 +208,9 @@ def ref15_workload(cfg, args, rank, world, dev):
                           f'(reference op order, dense 15x15), NumPy {np.__version__}, 1 thread, {host_cpu()}',
                 'seconds': round(el, 2)}
 
-    # per event: etype 1 + dt 8 + payload 72 read, traj 48 + logdet 8 written; state per launch
-    per_filter = T * (1 + 8 + 72 + 48 + 8) + 2 * (15 + 27) * 8 + 8
-    return dict(step=step, units=B * T, bytes=per_filter * B, bytes_per_unit=per_filter / T,
-                kernel='ref15_events_kernel', traffic=None, cpu=cpu, gather=gather_payload, kf=kf,
+    bytes_launch, bytes_event = ref15_algorithmic_bytes(cfg)
+    return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_event,
+                kernel='ref_events_kernel', traffic=load_traffic('ref15'), cpu=cpu, gather=gather_payload, kf=kf,
                 desc=f'SURVEY 8f row 2: reference 15-state model (kf_workers.py:493-614), f64, B={B} filters/GPU, '
                      f'T={T} events (IMU 200 Hz, GPS fix every {k}th event), dt={dt}',
                 extra={'filters_per_gpu': B, 'events_per_launch': T})

@@ -40,8 +40,8 @@ def pick(d, sub):
 
 
 def main():
-    out_dir, cfgs = sys.argv[1], [int(c) for c in sys.argv[2:]]
-    from bench import CONFIGS, algorithmic_bytes
+    out_dir, cfgs = sys.argv[1], sys.argv[2:]
+    from bench import CONFIGS, algorithmic_bytes, ref15_algorithmic_bytes
     B, T = 1048576, 64
     known_read, known_write = T * 6 * B * 8, T * 7 * B * 8
     pf = per_kernel(os.path.join(out_dir, 'probe_FETCH_SIZE'), 'FETCH_SIZE')
@@ -53,11 +53,12 @@ def main():
     res = {'calibration': {'fetch_size_scale': read_scale, 'write_size_scale': write_scale,
                            'probe': 'tools/probes/bw_probe soa_read/soa_write, 8 B per lane, B=2^20, T=64'}}
     for c in cfgs:
-        f = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE'), 'cv_run_kernel')
-        w = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE'), 'cv_run_kernel')
+        kern = 'ref_events_kernel' if c == 'ref15' else 'cv_run_kernel'
+        f = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE'), kern)
+        w = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE'), kern)
         fetch = 1024 * sum(f) / len(f)
         write = 1024 * sum(w) / len(w)
-        alg, _ = algorithmic_bytes(CONFIGS[str(c)])
+        alg, _ = (ref15_algorithmic_bytes if c == 'ref15' else algorithmic_bytes)(CONFIGS[str(c)])
         res[f'config{c}'] = {
             'fetch_bytes_raw': fetch, 'write_bytes_raw': write,
             'bytes_per_launch': fetch * read_scale + write * write_scale,
