@@ -226,3 +226,46 @@ def test_per_step_calls_on_reference_models():
         assert _rel(ref15.from_blocks(Pb[:, f]), Ps[f]) <= TOL
     with pytest.raises(ValueError):
         kf.update(np.zeros((3, B)), sensor='imu')
+
+
+@pytest.mark.parametrize('kernel', ['lane', 'chain'])
+def test_ref15_fp32_events_vs_fp64_oracle(kernel):
+    """fp32 handle (north_star: 1e-3 relative in fp32) against the fp64 oracle fed the same
+    fp32-rounded inputs, on realistic 200 Hz IMU + 10 Hz GPS streams."""
+    import os as _os
+    rng = np.random.default_rng(41)
+    B, T = 96, 200
+    etype = np.ones((T, B), np.uint8)
+    etype[::20] = 0
+    dt = np.full((T, B), 0.005)
+    pay = np.zeros((T, 9, B))
+    pay[:, 0:3] = rng.normal(0, 0.05, (T, 3, B))
+    pay[:, 3:6] = rng.normal(0, 0.01, (T, 3, B))
+    pay[:, 6:9] = rng.normal(0, 0.3, (T, 3, B))
+    gps = etype == 0
+    pay[:, 0:3] = np.where(gps[:, None, :], rng.normal(0, 3, (T, 3, B)), pay[:, 0:3])
+    pay32 = pay.astype(np.float32)
+    old = _os.environ.get('KFMI_EVENTS_KERNEL')
+    _os.environ['KFMI_EVENTS_KERNEL'] = kernel
+    try:
+        kf = kfmi.BatchedKF('ref15', B, 'f32')
+        tr, ld, _, _ = kf.run_events(etype, dt, pay32)
+        tr, ld = tr.double().cpu().numpy(), ld.double().cpu().numpy()
+    finally:
+        if old is None:
+            del _os.environ['KFMI_EVENTS_KERNEL']
+        else:
+            _os.environ['KFMI_EVENTS_KERNEL'] = old
+    worst_x = worst_l = 0.0
+    for f in range(0, B, 11):
+        x, P = np.zeros(15), ref_kf.P0_REF15.copy()
+        for t in range(T):
+            p = pay32[t, :, f].astype(np.float64)
+            if etype[t, f] == 0:
+                x, P = ref_kf.step15(x, P, 'GPS', {'easting': p[0], 'northing': p[1], 'altitude': p[2]}, dt[t, f])
+            else:
+                x, P = ref_kf.step15(x, P, 'IMU', ['t', *p], dt[t, f])
+            ref_ld = np.linalg.slogdet(P)[1]
+            worst_x = max(worst_x, np.linalg.norm(tr[t, :, f] - x[:6]) / max(np.linalg.norm(x[:6]), 1.0))
+            worst_l = max(worst_l, abs(ld[t, f] - ref_ld) / max(abs(ref_ld), 1.0))
+    assert worst_x <= 1e-3 and worst_l <= 1e-3, (worst_x, worst_l)
