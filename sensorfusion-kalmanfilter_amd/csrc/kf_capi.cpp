@@ -406,6 +406,8 @@ int kf_run_events(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
         if (!std::strcmp(v, "chain")) chain = true;
         else if (!std::strcmp(v, "lane")) chain = false;
     }
+    // the chain kernel addresses up to 27 [B] rows through one descriptor (32-bit byte count)
+    if (chain && static_cast<uint64_t>(h->B) * elem(h) * 27u >= (uint64_t(1) << 32)) chain = false;
     hipError_t e = kfmi::launch_ref_events(h->model, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream), chain);
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_run_events");
 }
