@@ -123,25 +123,38 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
         return torch.cat([xf, logdet[-1:]], dim=0).contiguous()
 
     def cpu():
-        """The reference CPU loop (oracle/ref_kf.run_filter_loop: one filter at a time, NumPy in
-        the reference's op order, kf_workers.py:688-717), 1 core, ~12 s of this workload."""
-        from oracle import ref_kf
+        """The reference's per-filter step restated in C (oracle/cpu_kf.c: dense matrices in the
+        reference's op order, OpenMP over filters) on this host's allotted cores for ~10 s of
+        this workload; plus the NumPy reference loop (oracle/ref_kf.run_filter_loop) on 1 core."""
+        from oracle import cpu_kf, ref_kf
         model = ref_kf.CV2 if cfg['model'] == 'cv2' else ref_kf.CV3
-        nf = min(4096, B)
+        d = 2 if cfg['model'] == 'cv2' else 3
+        nth = cpu_kf.threads()
+        nf = min(B, 1 << 16)
         idx = torch.linspace(0, B - 1, nf).long().to(u.device)
-        xs = x0[:, idx].double().cpu().numpy().T
+        xs = x0[:, idx].double().cpu().numpy()
         us = u[:, :, idx].double().cpu().numpy()
         zs = z[:, :, idx].double().cpu().numpy()
-        steps, done, t0 = 0, 0, time.perf_counter()
-        while done < nf and time.perf_counter() - t0 < 12.0:
-            ref_kf.run_filter_loop(model, xs[done], model.P0(), np.full(T, dt), us[:, :, done], zs[:, :, done], k)
-            steps += T
-            done += 1
+        done, t0 = 0, time.perf_counter()
+        chunk = max(nth * 64, 256)
+        while done < nf and time.perf_counter() - t0 < 10.0:
+            hi = min(nf, done + chunk)
+            cpu_kf.cv_run(d, xs, model.P0(), dt, us, zs, k, filters=(done, hi), nthreads=nth)
+            done = hi
         el = time.perf_counter() - t0
-        return {'value': steps / el, 'unit': 'KF steps/s', 'cores': 1, 'kind': 'port',
-                'sample': f'{done} filters x {T} steps of this workload (same synthetic streams), '
-                          f'oracle/ref_kf.run_filter_loop, NumPy {np.__version__}, 1 thread, {host_cpu()}',
-                'seconds': round(el, 2)}
+        # the NumPy reference loop, 1 core, ~3 s
+        n_np, t1 = 0, time.perf_counter()
+        while n_np < nf and time.perf_counter() - t1 < 3.0:
+            ref_kf.run_filter_loop(model, xs[:, n_np], model.P0(), np.full(T, dt), us[:, :, n_np], zs[:, :, n_np], k)
+            n_np += 1
+        el_np = time.perf_counter() - t1
+        return {'value': done * T / el, 'unit': 'KF steps/s', 'cores': nth, 'kind': 'port',
+                'sample': f'{done} filters x {T} steps of this workload (same synthetic streams) through '
+                          f'oracle/cpu_kf.c (the reference step, dense, C -O3 OpenMP) on {nth} threads, {host_cpu()}',
+                'seconds': round(el, 2),
+                'numpy_reference_loop': {'value': n_np * T / el_np, 'cores': 1,
+                                         'sample': f'{n_np} filters, oracle/ref_kf.run_filter_loop, '
+                                                   f'NumPy {np.__version__}'}}
 
     d = 2 if cfg['model'] == 'cv2' else 3
     bytes_launch, bytes_step = algorithmic_bytes(cfg)
@@ -183,13 +196,24 @@ def ref15_workload(cfg, args, rank, world, dev):
         return torch.cat([xf, logdet[-1:]], dim=0).contiguous()
 
     def cpu():
-        """oracle/ref_kf.step15 + slogdet (the reference's dense 15x15 per-event NumPy step,
-        kf_workers.py:688-717), 1 core, ~12 s over these streams."""
-        from oracle import ref_kf
-        nf = min(B, 2048)
+        """The reference's dense 15x15 event step restated in C (oracle/cpu_kf.c) on this host's
+        allotted cores for ~10 s of these streams; plus the NumPy step (oracle/ref_kf.step15 +
+        slogdet, kf_workers.py:688-717) on 1 core."""
+        from oracle import cpu_kf, ref_kf
+        nth = cpu_kf.threads()
+        nf = min(B, 1 << 15)
         et = etype[:, :nf].cpu().numpy()
+        dd = dts[:, :nf].cpu().numpy()
         pa = pay[:, :, :nf].cpu().numpy()
-        steps, t0 = 0, time.perf_counter()
+        x0 = np.zeros((15, nf))
+        done, t0 = 0, time.perf_counter()
+        chunk = max(nth * 16, 64)
+        while done < nf and time.perf_counter() - t0 < 10.0:
+            hi = min(nf, done + chunk)
+            cpu_kf.ref15_events(et, dd, pa, x0, ref_kf.P0_REF15, filters=(done, hi), nthreads=nth)
+            done = hi
+        el = time.perf_counter() - t0
+        steps, t1 = 0, time.perf_counter()
         for f in range(nf):
             x, P = np.zeros(15), ref_kf.P0_REF15.copy()
             for t in range(T):
@@ -200,13 +224,16 @@ def ref15_workload(cfg, args, rank, world, dev):
                     x, P = ref_kf.step15(x, P, 'IMU', ['t', *pa[t, :, f]], dt)
                 np.linalg.slogdet(P)
                 steps += 1
-            if time.perf_counter() - t0 > 12.0:
+            if time.perf_counter() - t1 > 3.0:
                 break
-        el = time.perf_counter() - t0
-        return {'value': steps / el, 'unit': 'KF events/s', 'cores': 1, 'kind': 'port',
-                'sample': f'{steps} events of these streams through oracle/ref_kf.step15 + slogdet '
-                          f'(reference op order, dense 15x15), NumPy {np.__version__}, 1 thread, {host_cpu()}',
-                'seconds': round(el, 2)}
+        el_np = time.perf_counter() - t1
+        return {'value': done * T / el, 'unit': 'KF events/s', 'cores': nth, 'kind': 'port',
+                'sample': f'{done} filters x {T} events of these streams through oracle/cpu_kf.c (the reference '
+                          f'step, dense 15x15, C -O3 OpenMP) on {nth} threads, {host_cpu()}',
+                'seconds': round(el, 2),
+                'numpy_reference_loop': {'value': steps / el_np, 'cores': 1,
+                                         'sample': f'{steps} events, oracle/ref_kf.step15 + slogdet, '
+                                                   f'NumPy {np.__version__}'}}
 
     bytes_launch, bytes_event = ref15_algorithmic_bytes(cfg)
     return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_event,
@@ -292,30 +319,47 @@ def log_workload(cfg, args, rank, world, dev):
                                    None, 0, 0.0, kf._stream()))
 
     def cpu():
-        """oracle/ref_kf.run_kalman_filter_full (the reference's per-event NumPy loop) over the
-        first events of the same log, 1 core, ~12 s."""
-        from oracle import ref_kf
+        """One filter cannot use more than one core: the reference's dense event step restated in
+        C (oracle/cpu_kf.c) over the whole log from the first fix (run_kalman_filter_full's dt
+        rule applied on the host), 1 thread; plus the NumPy reference loop
+        (oracle/ref_kf.run_kalman_filter_full) over the first events, 1 core, ~3 s."""
+        from oracle import cpu_kf, ref_kf
         from kfmi.kf_workers import EventList
-        n = 1
-        el = 0.0
+        h = stream.host()
+        t_h, e_h, p_h = h['t'][first:], h['etype'][first:].copy(), h['payload'][first:]
+        prev = np.r_[t_h[0], t_h[:-1]]
+        d_h = t_h - prev
+        e_h[d_h < 0] = 255                                    # kf_workers.py:683-685
+        x0h = np.zeros((15, 1))
+        x0h[0:3, 0] = p_h[0, 0:3]
+        n_c = min(T, 1 << 20)
+        ts = time.perf_counter()
+        cpu_kf.ref15_events(e_h[:n_c, None], d_h[:n_c, None], p_h[:n_c, :, None], x0h, ref_kf.P0_REF15,
+                            nthreads=1)
+        el = time.perf_counter() - ts
         ev = EventList(stream)
+        n = 2000
         while True:
-            n = min(T, max(n * 4, 4000))
-            lst = ev[first:first + n]   # from the first fix, where the reference's loop starts
-            ts = time.perf_counter()
+            lst = ev[first:first + n]
+            t1 = time.perf_counter()
             st, _, _, _ = ref_kf.run_kalman_filter_full(lst, 0, n)
-            el = time.perf_counter() - ts
-            if el > 3.0 or n == T:
+            el_np = time.perf_counter() - t1
+            if el_np > 3.0 or n >= T:
                 break
-        return {'value': (len(st) - 1) / el, 'unit': 'KF events/s', 'cores': 1, 'kind': 'port',
-                'sample': f'run_kalman_filter_full over the first {n} events from the first fix of this log '
-                          f'({len(st) - 1} processed) with oracle/ref_kf (the reference loop: dense 15x15 NumPy, '
-                          f'slogdet per event), NumPy {np.__version__}, 1 thread, {host_cpu()}',
-                'seconds': round(el, 2)}
+            n = min(T, n * 4)
+        return {'value': n_c / el, 'unit': 'KF events/s', 'cores': 1, 'kind': 'port',
+                'sample': f'run_kalman_filter_full over {n_c} events of this log (from the first fix) through '
+                          f'oracle/cpu_kf.c (the reference step, dense 15x15, C -O3), 1 thread (one filter), '
+                          f'{host_cpu()}', 'seconds': round(el, 2),
+                'numpy_reference_loop': {'value': (len(st) - 1) / el_np, 'cores': 1,
+                                         'sample': f'{len(st) - 1} events, oracle/ref_kf.run_kalman_filter_full, '
+                                                   f'NumPy {np.__version__}'}}
 
     per_event = 1 + 8 + 8 + 72 + 1 + 8 + 48 + 8   # dt pass (t, etype in; dt, etype out) + filter (in/out)
-    return dict(step=step, units=T, bytes=per_event * T, bytes_per_unit=per_event, kernel='ref_events_kernel',
+    return dict(step=step, units=T, bytes=per_event * T, bytes_per_unit=per_event, kernel='ref_chain_kernel',
                 traffic=None, cpu=cpu, gather=None, kf=kf,
+                roofline_note='one filter: one wave whose per-event dependency chain bounds the rate (8 lanes, '
+                              'one per axis chain); HBM is idle, so the fraction is not the figure of merit',
                 desc=f'BASELINE config 1: ONE 15-state filter (run_kalman_filter_full, kf_workers.py:623-728) over a '
                      f'whole drive log, {N} merged events ({stream.n_fixes} fixes + {stream.n_imu} IMU at 200 Hz), '
                      f'f64; synthetic log with the reference log\'s shape',
@@ -356,25 +400,50 @@ def bf_workload(cfg, args, rank, world, dev):
             kf.eval_combos(ev, init, t0, t_end, k, combo_offset=off, logdets=False)
 
     def cpu():
-        """oracle/ref_kf.evaluate_combo_chunk (the reference worker's NumPy loop) on the 12-subsets,
-        1 core, ~12 s."""
+        """The reference worker's per-subset filter (kf_workers.py:22-97) restated in C
+        (oracle/cpu_kf.c, dense 15x15): the 12-subsets of the candidates as event streams (k
+        events + the final predict), OpenMP over subsets on this host's allotted cores, ~10 s;
+        plus the worker's NumPy loop (oracle/ref_kf.evaluate_combo_chunk) on 1 core, ~3 s."""
         from itertools import combinations, islice
-        from oracle import ref_kf
+        from oracle import cpu_kf, ref_kf
+        nth = cpu_kf.threads()
+        kk = 12
+        done, ts = 0, time.perf_counter()
+        it = combinations(range(n), kk)
+        while time.perf_counter() - ts < 10.0:
+            combos = np.array(list(islice(it, 4096)))
+            if not len(combos):
+                break
+            nc = len(combos)
+            et = np.full((kk + 1, nc), 2, np.uint8)
+            et[:kk] = ev[combos.T, 1].astype(np.uint8)
+            tt = ev[combos.T, 0]
+            dd = np.empty((kk + 1, nc))
+            dd[0] = tt[0] - t0
+            dd[1:kk] = np.diff(tt, axis=0)
+            dd[kk] = t_end - tt[-1]                            # the worker's final predict (:74-82)
+            pp = np.zeros((kk + 1, 9, nc))
+            pp[:kk] = np.transpose(ev[combos.T, 2:], (0, 2, 1))
+            cpu_kf.ref15_events(et, dd, pp, np.zeros((15, nc)), Pw, nthreads=nth, records=True)
+            done += nc
+        el = time.perf_counter() - ts
         cand = [(i, 'GPS' if ev[i, 1] == 0 else 'IMU', ev[i, 0],
                  ({'easting': ev[i, 2], 'northing': ev[i, 3], 'altitude': ev[i, 4]} if ev[i, 1] == 0
                   else ['t', *ev[i, 2:]])) for i in range(n)]
-        done, steps, ts = 0, 0, time.perf_counter()
-        for combo in islice(combinations(cand, 12), 100000):
+        n_np, t1 = 0, time.perf_counter()
+        for combo in islice(combinations(cand, kk), 100000):
             ref_kf.evaluate_combo_chunk([combo], np.zeros(15), Pw, t0, t_end)
-            done += 1
-            steps += 13
-            if time.perf_counter() - ts > 12.0:
+            n_np += 1
+            if time.perf_counter() - t1 > 3.0:
                 break
-        el = time.perf_counter() - ts
-        return {'value': steps / el, 'unit': 'KF steps/s', 'combinations_per_s': done / el, 'cores': 1,
-                'kind': 'port', 'sample': f'{done} 12-subsets of the {n} candidates through '
-                                          f'oracle/ref_kf.evaluate_combo_chunk, NumPy {np.__version__}, 1 thread, '
-                                          f'{host_cpu()}', 'seconds': round(el, 2)}
+        el_np = time.perf_counter() - t1
+        return {'value': done * (kk + 1) / el, 'unit': 'KF steps/s', 'combinations_per_s': done / el, 'cores': nth,
+                'kind': 'port', 'sample': f'{done} {kk}-subsets of the {n} candidates as event streams through '
+                                          f'oracle/cpu_kf.c (the reference step, dense 15x15, C -O3 OpenMP) on '
+                                          f'{nth} threads, {host_cpu()}', 'seconds': round(el, 2),
+                'numpy_reference_loop': {'value': n_np * (kk + 1) / el_np, 'combinations_per_s': n_np / el_np,
+                                         'cores': 1, 'sample': f'{n_np} subsets, oracle/ref_kf.evaluate_combo_chunk, '
+                                                               f'NumPy {np.__version__}'}}
 
     return dict(step=step, units=total_steps, bytes=None, bytes_per_unit=None, kernel='ref15_combo_kernel',
                 traffic=None, cpu=cpu, gather=None, kf=kf, combos=total_combos,
@@ -483,6 +552,8 @@ def main():
                                'frac': achieved / HBM_PEAK_GBS, 'traffic': w['traffic'], 'kernel': w['kernel'],
                                'kernel_ms': kern_ms, 'algorithmic_bytes_per_launch': w['bytes'],
                                'algorithmic_bytes_per_step': w['bytes_per_unit']}
+            if w.get('roofline_note'):
+                rec['roofline']['note'] = w['roofline_note']
         else:
             rec['roofline'] = {'bound': 'hbm', 'achieved': None, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': None,
                                'traffic': None, 'kernel': w['kernel'], 'kernel_ms': kern_ms,

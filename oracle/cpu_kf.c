@@ -1,0 +1,296 @@
+/* CPU restatement of the reference's filter step in C — TEST INFRASTRUCTURE ONLY.
+ *
+ * The checker / CPU baseline, never the product: only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg load it (via ctypes).  It restates, in the reference's operation
+ * order and with dense matrices, what oracle/ref_kf.py restates in NumPy:
+ *
+ *   x = F x (+ G u)                 kf_workers.py:690
+ *   P = (F P) F^T + Q               predict_covariance, kf_workers.py:546-549
+ *   K = (P H^T) inv((H P) H^T + R)  calculate_kalman_gain, kf_workers.py:616-621
+ *   y = Z - H x ; x = x + K y        kf_workers.py:709-710
+ *   P = (I - K H) P                  kf_workers.py:711
+ *   slogdet(P)                       kf_workers.py:716-717
+ *
+ * for the BASELINE 4/2 and 6/3 constant-velocity restrictions and for the
+ * 15-state model's GPS / IMU-pseudo-measurement events (kf_workers.py:493-614, 698-706).
+ * inv() and slogdet() are LU with partial pivoting, as LAPACK's dgesv/dgetrf do.  OpenMP over
+ * filters (the reference itself is one filter per Python process).
+ * Pinned against oracle/ref_kf.py in tests/test_oracle.py (<= 1e-10 relative).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#define NMAX 15
+
+/* C = A B, A m x k, B k x n, row-major, straightforward dot products */
+static void matmul(int m, int k, int n, const double* A, const double* B, double* C) {
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < n; ++j) {
+            double s = 0.0;
+            for (int l = 0; l < k; ++l) s += A[i * k + l] * B[l * n + j];
+            C[i * n + j] = s;
+        }
+}
+
+/* C = A B^T */
+static void matmul_bt(int m, int k, int n, const double* A, const double* B, double* C) {
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < n; ++j) {
+            double s = 0.0;
+            for (int l = 0; l < k; ++l) s += A[i * k + l] * B[j * k + l];
+            C[i * n + j] = s;
+        }
+}
+
+/* LU with partial pivoting in place (n x n); returns 0 if singular.  piv[i] = row swapped in. */
+static int lu(int n, double* A, int* piv, int* nswap) {
+    *nswap = 0;
+    for (int k = 0; k < n; ++k) {
+        int p = k;
+        double best = fabs(A[k * n + k]);
+        for (int i = k + 1; i < n; ++i)
+            if (fabs(A[i * n + k]) > best) {
+                best = fabs(A[i * n + k]);
+                p = i;
+            }
+        piv[k] = p;
+        if (best == 0.0) return 0;
+        if (p != k) {
+            ++*nswap;
+            for (int j = 0; j < n; ++j) {
+                double t = A[k * n + j];
+                A[k * n + j] = A[p * n + j];
+                A[p * n + j] = t;
+            }
+        }
+        for (int i = k + 1; i < n; ++i) {
+            A[i * n + k] /= A[k * n + k];
+            const double l = A[i * n + k];
+            for (int j = k + 1; j < n; ++j) A[i * n + j] -= l * A[k * n + j];
+        }
+    }
+    return 1;
+}
+
+/* inverse via LU (columns of the identity solved one by one) */
+static int inv(int n, const double* A, double* Ai) {
+    double LU[NMAX * NMAX];
+    int piv[NMAX], ns;
+    memcpy(LU, A, sizeof(double) * n * n);
+    if (!lu(n, LU, piv, &ns)) return 0;
+    for (int c = 0; c < n; ++c) {
+        double b[NMAX];
+        for (int i = 0; i < n; ++i) b[i] = (i == c) ? 1.0 : 0.0;
+        for (int k = 0; k < n; ++k) {
+            const int p = piv[k];
+            if (p != k) {
+                double t = b[k];
+                b[k] = b[p];
+                b[p] = t;
+            }
+        }
+        for (int i = 0; i < n; ++i)
+            for (int k = 0; k < i; ++k) b[i] -= LU[i * n + k] * b[k];
+        for (int i = n - 1; i >= 0; --i) {
+            for (int k = i + 1; k < n; ++k) b[i] -= LU[i * n + k] * b[k];
+            b[i] /= LU[i * n + i];
+        }
+        for (int i = 0; i < n; ++i) Ai[i * n + c] = b[i];
+    }
+    return 1;
+}
+
+/* log |det A| (NaN if singular or the sign is negative, i.e. not a covariance) */
+static double logdet(int n, const double* A) {
+    double LU[NMAX * NMAX];
+    int piv[NMAX], ns;
+    memcpy(LU, A, sizeof(double) * n * n);
+    if (!lu(n, LU, piv, &ns)) return NAN;
+    double s = 0.0;
+    int neg = ns & 1;
+    for (int i = 0; i < n; ++i) {
+        const double d = LU[i * n + i];
+        if (d < 0) neg ^= 1;
+        s += log(fabs(d));
+    }
+    return neg ? NAN : s;
+}
+
+/* predict x = F x + G u, P = (F P) F^T + Q */
+static void predict(int n, const double* F, const double* Q, const double* Gu, double* x, double* P) {
+    double xn[NMAX], FP[NMAX * NMAX];
+    for (int i = 0; i < n; ++i) {
+        double s = 0.0;
+        for (int j = 0; j < n; ++j) s += F[i * n + j] * x[j];
+        xn[i] = s + (Gu ? Gu[i] : 0.0);
+    }
+    memcpy(x, xn, sizeof(double) * n);
+    matmul(n, n, n, F, P, FP);
+    matmul_bt(n, n, n, FP, F, P);
+    for (int i = 0; i < n * n; ++i) P[i] += Q[i];
+}
+
+/* update with H (m x n), R (m x m), Z (m): K = (P H^T) inv((H P) H^T + R); x += K (Z - H x);
+ * P = (I - K H) P.  Returns 0 if S is singular. */
+static int update(int n, int m, const double* H, const double* R, const double* Z, double* x, double* P) {
+    double PHt[NMAX * NMAX], HP[NMAX * NMAX], S[NMAX * NMAX], Si[NMAX * NMAX], K[NMAX * NMAX];
+    matmul_bt(n, n, m, P, H, PHt);
+    matmul(m, n, n, H, P, HP);
+    matmul_bt(m, n, m, HP, H, S);
+    for (int i = 0; i < m * m; ++i) S[i] += R[i];
+    if (!inv(m, S, Si)) return 0;
+    matmul(n, m, m, PHt, Si, K);
+    double y[NMAX];
+    for (int i = 0; i < m; ++i) {
+        double s = 0.0;
+        for (int j = 0; j < n; ++j) s += H[i * n + j] * x[j];
+        y[i] = Z[i] - s;
+    }
+    for (int i = 0; i < n; ++i) {
+        double s = 0.0;
+        for (int j = 0; j < m; ++j) s += K[i * m + j] * y[j];
+        x[i] += s;
+    }
+    double IKH[NMAX * NMAX], Pn[NMAX * NMAX];
+    matmul(n, m, n, K, H, IKH);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) IKH[i * n + j] = (i == j ? 1.0 : 0.0) - IKH[i * n + j];
+    matmul(n, n, n, IKH, P, Pn);
+    memcpy(P, Pn, sizeof(double) * n * n);
+    return 1;
+}
+
+/* BASELINE constant-velocity filters (d = 2: 4/2, d = 3: 6/3), one per column of the SoA
+ * streams: u [T][d][B], z [T/k][d][B], x0 [n][B]; traj [T][n][B] and logdet [T][B] optional.
+ * Step t updates when (t+1) % k == 0 (oracle/ref_kf.is_update_step).  Filters [f0, f1). */
+static void cv_model(int d, double dt, double q_pos, double q_vel, double* F, double* Q) {
+    const int n = 2 * d;
+    memset(F, 0, sizeof(double) * n * n);
+    memset(Q, 0, sizeof(double) * n * n);
+    for (int i = 0; i < n; ++i) F[i * n + i] = 1.0;
+    for (int i = 0; i < d; ++i) {
+        F[i * n + d + i] = dt;
+        Q[i * n + i] = q_pos * dt;
+        Q[(d + i) * n + d + i] = q_vel * dt;
+    }
+}
+
+void cpu_cv_run(int d, int64_t B, int T, double dt0, const double* dt_steps, int k, const double* u, const double* z,
+                const double* x0, const double* P0, double q_pos, double q_vel, double r_gps, double* traj,
+                double* logdet_out, double* x_out, double* P_out, int64_t f0, int64_t f1, int nthreads) {
+    const int n = 2 * d;
+    double F0[NMAX * NMAX], Q0[NMAX * NMAX], H[NMAX * NMAX] = {0}, R[NMAX * NMAX] = {0};
+    cv_model(d, dt0, q_pos, q_vel, F0, Q0);
+    for (int i = 0; i < d; ++i) {
+        H[i * n + i] = 1.0;
+        R[i * d + i] = r_gps;
+    }
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+    for (int64_t f = f0; f < f1; ++f) {
+        double x[NMAX], P[NMAX * NMAX], Fs[NMAX * NMAX], Qs[NMAX * NMAX];
+        for (int i = 0; i < n; ++i) x[i] = x0[i * B + f];
+        memcpy(P, P0, sizeof(double) * n * n);
+        for (int t = 0; t < T; ++t) {
+            const double dt = dt_steps ? dt_steps[t] : dt0;
+            const double* F = F0;
+            const double* Q = Q0;
+            if (dt_steps) {
+                cv_model(d, dt, q_pos, q_vel, Fs, Qs);
+                F = Fs;
+                Q = Qs;
+            }
+            double Gu[NMAX];
+            for (int i = 0; i < d; ++i) {
+                const double a = u[((int64_t)t * d + i) * B + f];
+                Gu[i] = 0.5 * dt * dt * a;
+                Gu[d + i] = dt * a;
+            }
+            predict(n, F, Q, Gu, x, P);
+            if ((t + 1) % k == 0) {
+                double Z[NMAX];
+                const int s = (t + 1) / k - 1;
+                for (int i = 0; i < d; ++i) Z[i] = z[((int64_t)s * d + i) * B + f];
+                update(n, d, H, R, Z, x, P);
+            }
+            if (traj)
+                for (int i = 0; i < n; ++i) traj[((int64_t)t * n + i) * B + f] = x[i];
+            if (logdet_out) logdet_out[(int64_t)t * B + f] = logdet(n, P);
+        }
+        if (x_out)
+            for (int i = 0; i < n; ++i) x_out[i * B + f] = x[i];
+        if (P_out) memcpy(P_out + f * n * n, P, sizeof(double) * n * n);
+    }
+}
+
+/* The reference's 15-state model (kf_workers.py:493-614): F(dt), Q(dt), the GPS fix update and
+ * the IMU pseudo-measurement update built from the predicted state (kf_workers.py:698-706). */
+static void F15(double dt, double* F) {
+    memset(F, 0, sizeof(double) * 225);
+    for (int i = 0; i < 15; ++i) F[i * 15 + i] = 1.0;
+    for (int i = 0; i < 3; ++i) {
+        F[i * 15 + 6 + i] = dt;
+        F[i * 15 + 12 + i] = 0.5 * dt * dt;
+        F[(3 + i) * 15 + 9 + i] = dt;
+        F[(6 + i) * 15 + 12 + i] = dt;
+    }
+}
+
+static void Q15(double dt, double* Q) {
+    static const double q[5] = {5.0, 0.05, 1.0, 0.1, 2.0};
+    memset(Q, 0, sizeof(double) * 225);
+    for (int g = 0; g < 5; ++g)
+        for (int i = 0; i < 3; ++i) Q[(3 * g + i) * 15 + 3 * g + i] = q[g] * dt;
+}
+
+/* events: etype [T][B] (0 GPS, 1 IMU, 2 predict only, 255 none), dt [T][B], payload [T][9][B];
+ * x0 [15][B]; P0 15x15 (shared); traj [T][6][B], logdet [T][B] optional.  Filters [f0, f1). */
+void cpu_ref15_events(int64_t B, int T, const uint8_t* etype, const double* dt, const double* payload,
+                      const double* x0, const double* P0, double* traj, double* logdet_out, int64_t f0, int64_t f1,
+                      int nthreads) {
+    static const double rimu[5] = {50.0, 0.05, 10.0, 0.1, 100.0};
+    double Hg[3 * 15] = {0}, Rg[9] = {0}, Hi[225] = {0}, Ri[225] = {0};
+    for (int i = 0; i < 3; ++i) {
+        Hg[i * 15 + i] = 1.0;
+        Rg[i * 3 + i] = 3.0;
+    }
+    for (int i = 0; i < 15; ++i) {
+        Hi[i * 15 + i] = 1.0;
+        Ri[i * 15 + i] = rimu[i / 3];
+    }
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+    for (int64_t f = f0; f < f1; ++f) {
+        double x[15], P[225], F[225], Q[225];
+        for (int i = 0; i < 15; ++i) x[i] = x0[i * B + f];
+        memcpy(P, P0, sizeof(P));
+        for (int t = 0; t < T; ++t) {
+            const int ty = etype[(int64_t)t * B + f];
+            const double h = dt[(int64_t)t * B + f];
+            const double* p = payload + (int64_t)t * 9 * B + f;
+            if (ty != 255) {
+                F15(h, F);
+                Q15(h, Q);
+                predict(15, F, Q, NULL, x, P);
+                if (ty == 0) {
+                    const double Z[3] = {p[0], p[B], p[2 * B]};
+                    update(15, 3, Hg, Rg, Z, x, P);
+                } else if (ty == 1) {
+                    double Z[15];
+                    for (int i = 0; i < 3; ++i) {
+                        const double a = p[(6 + i) * B];
+                        const double V = x[6 + i] + a * h;
+                        Z[i] = x[i] + V * h;
+                        Z[3 + i] = p[i * B];
+                        Z[6 + i] = V;
+                        Z[9 + i] = p[(3 + i) * B];
+                        Z[12 + i] = a;
+                    }
+                    update(15, 15, Hi, Ri, Z, x, P);
+                }
+            }
+            if (traj)
+                for (int i = 0; i < 6; ++i) traj[((int64_t)t * 6 + i) * B + f] = x[i];
+            if (logdet_out) logdet_out[(int64_t)t * B + f] = logdet(15, P);
+        }
+    }
+}

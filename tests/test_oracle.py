@@ -211,3 +211,63 @@ def test_scheduler_gain_and_cov_matrix(golden_dir):
             assert _rel(ref_kf.scheduler_cov_matrix([1], S, R, H), g['sched_cov_first'][si, ti]) < RTOL
             full = list(range(1, R.shape[0] + 1))
             assert _rel(ref_kf.scheduler_cov_matrix(full, S, R, H), g['sched_cov_full'][si, ti]) < RTOL
+
+
+# ---- the C restatement (oracle/cpu_kf.c): the CPU baseline's engine, pinned here ---------
+
+@pytest.fixture(scope='module')
+def cpu_kf():
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(['make', '-C', os.path.join(root, 'oracle')], check=True, capture_output=True)
+    from oracle import cpu_kf as ck
+    return ck
+
+
+@pytest.mark.parametrize('d', [2, 3])
+@pytest.mark.parametrize('k', [1, 5])
+def test_c_restatement_vs_goldens(golden_dir, cpu_kf, d, k):
+    """The C port reproduces the reference-generated BASELINE goldens (cv_batch.npz)."""
+    g = _load(golden_dir, 'cv_batch.npz')
+    key = f'cv{d}_k{k}'
+    dt, u, z, x0, P0 = (g[f'{key}_{s}'] for s in ('dt', 'u', 'z', 'x0', 'P0'))
+    tr, ld, x, P = cpu_kf.cv_run(d, x0.T, P0, dt, u, z, k)   # irregular dt: a zero and a 1.7x step
+    assert _rel(tr, g[f'{key}_traj']) < 1e-10
+    assert _rel(ld, g[f'{key}_logdet']) < 1e-10
+    assert _rel(P, g[f'{key}_Pfinal']) < 1e-10
+
+
+def test_c_restatement_vs_numpy_oracle(cpu_kf):
+    rng = np.random.default_rng(3)
+    for d, k in ((2, 1), (3, 1), (3, 10)):
+        model = ref_kf.CV2 if d == 2 else ref_kf.CV3
+        B, T = 9, 40
+        x0 = rng.normal(0, 100, (B, 2 * d))
+        u = rng.normal(0, 0.3, (T, d, B))
+        z = rng.normal(0, 30, (T // k, d, B))
+        tr, ld, x, P = cpu_kf.cv_run(d, x0.T, model.P0(), 0.1, u, z, k)
+        rt, rl, rx, rP = ref_kf.run_batch(model, x0, model.P0(), np.full(T, 0.1), u, z, k)
+        assert _rel(tr, rt) < 1e-10 and _rel(ld, rl) < 1e-10 and _rel(P, rP) < 1e-10
+
+
+def test_c_ref15_events_vs_numpy_oracle(cpu_kf):
+    rng = np.random.default_rng(4)
+    B, T = 7, 50
+    etype = rng.choice([0, 1, 1, 2, 255], size=(T, B)).astype(np.uint8)
+    dt = rng.uniform(0, 0.05, (T, B))
+    pay = rng.normal(0, 1, (T, 9, B)) * np.array([20, 20, 20, .05, .05, .05, .5, .5, .5])[None, :, None]
+    x0 = rng.normal(0, 5, (15, B))
+    tr, ld = cpu_kf.ref15_events(etype, dt, pay, x0, ref_kf.P0_REF15)
+    for f in range(B):
+        x, P = x0[:, f].copy(), ref_kf.P0_REF15.copy()
+        for t in range(T):
+            ty = etype[t, f]
+            if ty == 2:
+                F = ref_kf.F_ref15(dt[t, f])
+                x, P = F @ x, ref_kf.predict_covariance(P, F, ref_kf.Q_ref15(dt[t, f]))
+            elif ty in (0, 1):
+                sd = ({'easting': pay[t, 0, f], 'northing': pay[t, 1, f], 'altitude': pay[t, 2, f]} if ty == 0
+                      else ['t', *pay[t, :, f]])
+                x, P = ref_kf.step15(x, P, 'GPS' if ty == 0 else 'IMU', sd, dt[t, f])
+            assert _rel(tr[t, :, f], x[:6]) < 1e-10
+            assert abs(ld[t, f] - np.linalg.slogdet(P)[1]) < 1e-10 * max(1, abs(np.linalg.slogdet(P)[1]))
