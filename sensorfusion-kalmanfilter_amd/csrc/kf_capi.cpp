@@ -25,6 +25,9 @@ struct kf_batch {
     void* P;          // [n(n+1)/2][B]
     int32_t* status;  // [B]
     void* ws;         // KF_MODEL_REF15: device workspace for kf_eval_combos (events, binomials, init)
+    bool r_diag;      // BASELINE models: R has no off-diagonal entry
+    bool block_p;     // BASELINE models: every filter's P is block-diagonal over the axes
+    int* flag;        // device int for the kf_set_state block check (allocated on first use)
 };
 
 namespace {
@@ -81,6 +84,10 @@ kfmi::CvArgs base_args(const kf_batch* h) {
         for (int j = i; j < h->m; ++j) a.r[k++] = h->params.r[i * h->m + j];
     a.p0_pos = h->params.p0_pos;
     a.p0_vel = h->params.p0_vel;
+    // the block kernel needs a block-diagonal P (kept so by a diagonal R);
+    // KFMI_CV_KERNEL=general forces the general kernel (tests, A/B)
+    const char* v = std::getenv("KFMI_CV_KERNEL");
+    a.block_p = (h->block_p && h->r_diag && !(v && !std::strcmp(v, "general"))) ? 1 : 0;
     return a;
 }
 
@@ -204,6 +211,10 @@ int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_pa
     } else if (!is_ref(model)) {
         kf_default_params(model, &h->params);
     }
+    h->r_diag = true;
+    for (int i = 0; i < h->m; ++i)
+        for (int j = 0; j < h->m; ++j)
+            if (i != j && h->params.r[i * h->m + j] != 0.0) h->r_diag = false;
     const size_t w = elem(h);
     const size_t nb = static_cast<size_t>(batch);
     if (nb) {
@@ -239,6 +250,7 @@ int kf_free(kf_batch* h) {
     if (h->P) (void)hipFree(h->P);
     if (h->status) (void)hipFree(h->status);
     if (h->ws) (void)hipFree(h->ws);
+    if (h->flag) (void)hipFree(h->flag);
     delete h;
     return KF_OK;
 }
@@ -264,6 +276,7 @@ int kf_reset(kf_batch* h, const void* x0, void* stream) {
     }
     kfmi::CvArgs a = base_args(h);
     a.x0 = x0;
+    h->block_p = true;  // P = P0 is diagonal
     return launch(h, kfmi::Op::Reset, a, stream, "kf_reset");
 }
 
@@ -280,6 +293,23 @@ int kf_set_state(kf_batch* h, const void* x, const void* P, int on_device, void*
         e = hipMemsetAsync(h->status, 0, sizeof(int32_t) * nb, static_cast<hipStream_t>(stream));
     if (e == hipSuccess && !on_device) e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "kf_set_state");
+    if (P && nb && !is_ref(h)) {
+        // does the new P keep every filter block-diagonal over the axes (cv_block_kernel)?
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        if (!h->flag && hipMalloc(reinterpret_cast<void**>(&h->flag), sizeof(int)) != hipSuccess) {
+            (void)hipGetLastError();
+            h->flag = nullptr;
+            h->block_p = false;
+            return KF_OK;
+        }
+        int any = 1;
+        e = hipMemsetAsync(h->flag, 0, sizeof(int), st);
+        if (e == hipSuccess) e = kfmi::launch_cv_offblock(h->axes, h->dtype == KF_F64, base_args(h), h->flag, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(&any, h->flag, sizeof(int), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return hip_fail(e, "kf_set_state block check");
+        h->block_p = any == 0;
+    }
     return KF_OK;
 }
 

@@ -238,6 +238,176 @@ __global__ __launch_bounds__(kBlock, (RunOcc<D, T>::value)) void cv_run_kernel(c
     a.status[f] = st;
 }
 
+// ------------------------------------------------------------------------------------
+// Block variant of the fused run for a block-diagonal P and diagonal R (the reference's
+// constants: Q, R, P0 diagonal; F and H couple only pos_i with vel_i).  P then stays exactly
+// block-diagonal — D independent 2-state (pos_i, vel_i) chains — and the general kernel spends
+// most of its VALU on entries that are exact zeros.  This kernel keeps, per axis, x = (p, v)
+// and P_i = (pp, pv, vv) and evaluates the general kernel's expressions for those entries in
+// the same order (the dropped terms are exact zeros), so its results equal the general
+// kernel's; the logdet multiplies the LDL pivots in the general kernel's order (positions,
+// renormalise, velocities, renormalise).  The host selects it only when the handle's P is
+// known to be block-diagonal (kf_alloc / kf_reset, or checked on the device in kf_set_state).
+// ------------------------------------------------------------------------------------
+template <int D, typename T>
+__global__ __launch_bounds__(kBlock) void cv_block_kernel(const CvArgs a) {
+    constexpr int N = 2 * D;
+    const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (f >= a.B) return;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
+    T xp[D], xv[D], pp[D], pv[D], vv[D], r[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        xp[i] = ldb<T>(a.x, i, rb, off);
+        xv[i] = ldb<T>(a.x, D + i, rb, off);
+        pp[i] = ldb<T>(a.P, tri<N>(i, i), rb, off);
+        pv[i] = ldb<T>(a.P, tri<N>(i, D + i), rb, off);
+        vv[i] = ldb<T>(a.P, tri<N>(D + i, D + i), rb, off);
+        r[i] = T(a.r[tri<D>(i, i)]);
+    }
+    int32_t st = a.status[f];
+    const int T_ = a.T;
+    const int k_upd = a.update_every;
+    const int U = T_ / k_upd;
+    int ld_upd_step = k_upd - 1;
+    int ld_s = 0;
+    const uint32_t rb_z = U > 0 ? rb : 0u;
+    const T dt = T(a.dt);
+    const T hdt2 = T(0.5) * dt * dt;
+    const T qp = T(a.q_pos * a.dt), qv = T(a.q_vel * a.dt);
+    auto load_in = [&](int t, StepIn<D, T>& in) {
+        const int tc = t < T_ ? t : T_ - 1;
+        if (tc > ld_upd_step) {
+            ld_upd_step += k_upd;
+            ++ld_s;
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) in.u[i] = ldb_stream(a.u, int64_t(tc) * D + i, rb, off, T(0));
+        int s = ld_s < U ? ld_s : U - 1;
+        s = s > 0 ? s : 0;
+        const uint32_t rbz = tc == ld_upd_step ? rb_z : 0u;  // z only on update steps
+#pragma unroll
+        for (int i = 0; i < D; ++i) in.z[i] = ldb_stream(a.z, int64_t(s) * D + i, rbz, off, T(0));
+    };
+    int until_upd = k_upd;
+    auto step = [&](int t, const StepIn<D, T>& in) {
+        // predict (Cv::predict per axis): Bm' = Bm + dt C, A' = A + dt (Bm' + Bm^T), + Q
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            xp[i] = fmaT(hdt2, in.u[i], fmaT(dt, xv[i], xp[i]));
+            xv[i] = fmaT(dt, in.u[i], xv[i]);
+            const T bn = fmaT(dt, vv[i], pv[i]);
+            pp[i] = fmaT(dt, bn + pv[i], pp[i]);
+            pv[i] = bn;
+            pp[i] += qp;
+            vv[i] += qv;
+        }
+        if (--until_upd == 0) {  // wave-uniform
+            until_upd = k_upd;
+            bool ok = true;
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                // sel_update with a diagonal S: one scalar pivot per axis, Joseph form
+                const T S = pp[i] + r[i];
+                ok = ok && (S > T(0));
+                const T dinv = rcp_pos<2>(S);
+                const T k0 = pp[i] * dinv, k1 = pv[i] * dinv;
+                const T y = in.z[i] - xp[i];
+                xp[i] = fmaT(k0, y, xp[i]);
+                xv[i] = fmaT(k1, y, xv[i]);
+                const T e0 = fmaT(k0, S, -pp[i]);
+                const T e1 = fmaT(k1, S, -pv[i]);
+                const T npp = fmaT(e0, k0, fmaT(-k0, pp[i], pp[i]));
+                const T npv = fmaT(e0, k1, fmaT(-k0, pv[i], pv[i]));
+                const T nvv = fmaT(e1, k1, fmaT(-k1, pv[i], vv[i]));
+                pp[i] = npp;
+                pv[i] = npv;
+                vv[i] = nvv;
+            }
+            // a bad pivot poisons the whole filter, as in the general kernel (where its NaN
+            // reaches every row through the LDL factors)
+            const T poison = ok ? T(0) : quiet_nan<T>();
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                xp[i] += poison;
+                xv[i] += poison;
+                pp[i] += poison;
+                pv[i] += poison;
+                vv[i] += poison;
+            }
+            st = ok ? st : kNotSpd;
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            stb(a.traj, int64_t(t) * N + i, rb, off, xp[i]);
+            stb(a.traj, int64_t(t) * N + D + i, rb, off, xv[i]);
+        }
+        // logdet: LDL pivots in the general 6x6 order (positions, then velocities)
+        T prod = T(1);
+        int ex = 0, e;
+        bool pd = true;
+        T dv[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            pd = pd && (pp[i] > T(0));
+            prod *= pp[i];
+            const T l = pv[i] * rcp_nr<1>(pp[i]);
+            const T v = l * pp[i];
+            dv[i] = fmaT(-l, v, vv[i]);
+        }
+        prod = frexp(prod, &e);
+        ex += e;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            pd = pd && (dv[i] > T(0));
+            prod *= dv[i];
+        }
+        prod = frexp(prod, &e);
+        ex += e;
+        const T ld = pd ? log_mant(prod, ex) : quiet_nan<T>();
+        st = (ld == ld) ? st : kNotSpd;
+        stb(a.logdet, t, rb, off, ld);
+    };
+    StepIn<D, T> A, Bf;
+    load_in(0, A);
+    __builtin_amdgcn_s_waitcnt(0);
+    int t = 0;
+    for (; t + 1 < T_; t += 2) {
+        load_in(t + 1, Bf);
+        step(t, A);
+        load_in(t + 2, A);
+        step(t + 1, Bf);
+    }
+    if (t < T_) step(t, A);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        stb(a.x, i, rb, off, xp[i]);
+        stb(a.x, D + i, rb, off, xv[i]);
+        stb(a.P, tri<N>(i, i), rb, off, pp[i]);
+        stb(a.P, tri<N>(i, D + i), rb, off, pv[i]);
+        stb(a.P, tri<N>(D + i, D + i), rb, off, vv[i]);
+    }
+    a.status[f] = st;
+}
+
+// 1 in *flag if any filter's packed P has a non-zero entry coupling different axes.
+template <int D, typename T>
+__global__ __launch_bounds__(kBlock) void cv_offblock_kernel(const CvArgs a, int* flag) {
+    constexpr int N = 2 * D;
+    const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (f >= a.B) return;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = i; j < N; ++j)
+            if ((i % D) != (j % D)) any = any || (ldb<T>(a.P, tri<N>(i, j), rb, off) != T(0));
+    if (any) atomicOr(flag, 1);
+}
+
 // Single predict step (kf_predict): optional per-filter dt and logdet of the prediction.
 template <int D, typename T>
 __global__ __launch_bounds__(kBlock) void cv_predict_kernel(const CvArgs a) {
@@ -393,7 +563,9 @@ hipError_t launch_run(const CvArgs& a, dim3 grid, hipStream_t st) {
             for (int j = i; j < D; ++j, ++k)
                 if (i != j && a.r[k] != 0.0) diag = false;
     }
-    if (fast && diag)
+    if (fast && diag && a.block_p)
+        cv_block_kernel<D, T><<<grid, kBlock, 0, st>>>(a);
+    else if (fast && diag)
         cv_run_kernel<D, T, false, true><<<grid, kBlock, lds, st>>>(a);
     else if (fast)
         cv_run_kernel<D, T, false, false><<<grid, kBlock, lds, st>>>(a);
@@ -421,6 +593,18 @@ hipError_t launch_cv_t(Op op, const CvArgs& a, hipStream_t st) {
 hipError_t launch_cv(int axes, bool f64, Op op, const CvArgs& a, hipStream_t stream) {
     if (axes == 2) return f64 ? launch_cv_t<2, double>(op, a, stream) : launch_cv_t<2, float>(op, a, stream);
     return f64 ? launch_cv_t<3, double>(op, a, stream) : launch_cv_t<3, float>(op, a, stream);
+}
+
+hipError_t launch_cv_offblock(int axes, bool f64, const CvArgs& a, int* flag, hipStream_t stream) {
+    const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
+    if (axes == 2) {
+        if (f64) cv_offblock_kernel<2, double><<<grid, kBlock, 0, stream>>>(a, flag);
+        else cv_offblock_kernel<2, float><<<grid, kBlock, 0, stream>>>(a, flag);
+    } else {
+        if (f64) cv_offblock_kernel<3, double><<<grid, kBlock, 0, stream>>>(a, flag);
+        else cv_offblock_kernel<3, float><<<grid, kBlock, 0, stream>>>(a, flag);
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_synth(int axes, bool f64, const SynthArgs& a, hipStream_t stream) {

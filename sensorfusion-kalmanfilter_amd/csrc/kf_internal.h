@@ -27,6 +27,7 @@ struct CvArgs {
     double q_pos, q_vel;     // Q = diag(q_pos dt, q_vel dt)
     double r[6];             // R upper triangle, packed row-major (m <= 3)
     double p0_pos, p0_vel;   // reset covariance
+    int block_p;             // P is block-diagonal over the axes (kf_run may use cv_block_kernel)
 };
 
 struct SynthArgs {
@@ -121,6 +122,8 @@ enum class Op { Run, Predict, Update, Reset };
 
 // Launchers (kf_cv.hip, kf_ref.hip).  Return hipSuccess or the launch error.
 hipError_t launch_cv(int axes, bool f64, Op op, const CvArgs& a, hipStream_t stream);
+// *flag |= 1 if any filter's P couples different axes (flag: device int, zeroed by the caller).
+hipError_t launch_cv_offblock(int axes, bool f64, const CvArgs& a, int* flag, hipStream_t stream);
 hipError_t launch_synth(int axes, bool f64, const SynthArgs& a, hipStream_t stream);
 // chain = true: the chain-parallel kernel (kGroup lanes per filter), for few filters.
 hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, bool chain);

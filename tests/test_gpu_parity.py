@@ -306,3 +306,62 @@ def test_logdet_kernel_on_random_spd(dtype, name, wide):
     bound = np.maximum(50 * kappa * eps, 1e-13 if dtype == 'f64' else 2e-6)
     assert (err <= bound).all(), float((err / bound).max())
     assert (kf.status().cpu().numpy() == 0).all()
+
+
+def _run_with_kernel(kernel, name, dtype, x0, u, z, k, dt, P=None):
+    old = os.environ.get('KFMI_CV_KERNEL')
+    os.environ['KFMI_CV_KERNEL'] = kernel
+    try:
+        B = x0.shape[0]
+        kf = kfmi.BatchedKF(name, B, dtype)
+        kf.reset(torch.from_numpy(np.ascontiguousarray(x0.T.astype(NP[dtype]))).cuda())
+        if P is not None:
+            kf.set_state(np.ascontiguousarray(x0.T.astype(NP[dtype])), np.ascontiguousarray(P.astype(NP[dtype])))
+        tr, ld = kf.run(torch.from_numpy(u.astype(NP[dtype])).cuda(), torch.from_numpy(z.astype(NP[dtype])).cuda(),
+                        dt=dt, update_every=k)
+        x, Pp = kf.state()
+        return [v.cpu().numpy() for v in (tr, ld, x, Pp, kf.status())]
+    finally:
+        if old is None:
+            del os.environ['KFMI_CV_KERNEL']
+        else:
+            os.environ['KFMI_CV_KERNEL'] = old
+
+
+@pytest.mark.parametrize('dtype', ['f64', 'f32'])
+@pytest.mark.parametrize('name', ['cv2', 'cv3'])
+@pytest.mark.parametrize('k', [1, 10])
+def test_block_kernel_equals_general_kernel(dtype, name, k):
+    """With the reference's diagonal R and P0, P stays block-diagonal over the axes and
+    kf_run uses cv_block_kernel; it evaluates the general kernel's expressions for the non-zero
+    entries in the same order, so both produce the same numbers."""
+    model = MODEL[name]
+    x0, u, z = random_inputs(model, 777, 60, k, seed=11 + k)
+    blk = _run_with_kernel('auto', name, dtype, x0, u, z, k, 0.1 if k == 1 else 0.01)
+    gen = _run_with_kernel('general', name, dtype, x0, u, z, k, 0.1 if k == 1 else 0.01)
+    for a, b in zip(blk, gen):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_block_check_falls_back_for_coupled_covariance():
+    """set_state with a P that couples the axes must take the general kernel (the block check
+    on the device); a block-diagonal P keeps the block kernel; both match the oracle."""
+    model = MODEL['cv3']
+    B, T = 64, 30
+    x0, u, z = random_inputs(model, B, T, 1, seed=5)
+    rng = np.random.default_rng(6)
+    A = rng.normal(size=(B, 6, 6))
+    Pfull = np.einsum('bij,bkj->bik', A, A) + 50 * np.eye(6)
+    Pblock = Pfull.copy()
+    for i in range(6):
+        for j in range(6):
+            if i % 3 != j % 3:
+                Pblock[:, i, j] = 0.0
+    for P in (Pfull, Pblock):
+        packed = ref_kf.tri_pack(P)                        # [21, B]
+        tr, ld, _, _, st = _run_with_kernel('auto', 'cv3', 'f64', x0, u, z, 1, 0.1, P=packed)
+        gen = _run_with_kernel('general', 'cv3', 'f64', x0, u, z, 1, 0.1, P=packed)
+        np.testing.assert_array_equal(tr, gen[0])
+        rt, rl, _, _ = ref_kf.run_batch(model, x0, P, np.full(T, 0.1), u, z, 1)
+        ex, el = ref_kf.parity_errors(tr, ld, rt, rl)
+        assert ex <= 1e-6 and el <= 1e-6 and (st == 0).all()
