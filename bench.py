@@ -53,16 +53,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 SEED = 20251015
 
 
-def algorithmic_bytes(cfg):
+def block_kernel_in_use():
+    """kf_run takes cv_block_kernel for the bench's handles (diagonal R, P = P0) unless forced."""
+    return os.environ.get('KFMI_CV_KERNEL', 'auto') != 'general'
+
+
+def algorithmic_bytes(cfg, block=None):
     """Bytes one kf_run launch must move: per filter per step c control values
     read, m measurement values read on update steps, n state values + 1 logdet written; per
-    filter per launch (x, P) loaded and stored once and status read + written."""
+    filter per launch (x, P) loaded and stored once and status read + written.  The block
+    kernel keeps P's 3 d per-axis entries (the rest are exact zeros it never touches)."""
     d = 2 if cfg['model'] == 'cv2' else 3
     n, m, c = 2 * d, d, d
     w = 8 if cfg['dtype'] == 'f64' else 4
     T, k, B = cfg['T'], cfg['k'], cfg['B']
     U = T // k
-    per_filter = T * (c + n + 1) * w + U * m * w + 2 * (n + n * (n + 1) // 2) * w + 2 * 4
+    block = block_kernel_in_use() if block is None else block
+    p_entries = 3 * d if block else n * (n + 1) // 2
+    per_filter = T * (c + n + 1) * w + U * m * w + 2 * (n + p_entries) * w + 2 * 4
     return per_filter * B, per_filter / T
 
 
@@ -158,8 +166,10 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
 
     d = 2 if cfg['model'] == 'cv2' else 3
     bytes_launch, bytes_step = algorithmic_bytes(cfg)
-    return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_step, kernel='cv_run_kernel',
-                traffic=load_traffic(cfg_id), cpu=cpu, gather=gather_payload, kf=kf,
+    kernel = 'cv_block_kernel' if block_kernel_in_use() else 'cv_run_kernel'
+    return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_step, kernel=kernel,
+                traffic=load_traffic(cfg_id) if kernel == 'cv_block_kernel' else None, cpu=cpu,
+                gather=gather_payload, kf=kf,
                 desc=f"BASELINE config {cfg_id}: {cfg['model']} ({2 * d}-state/{d}-meas), {cfg['dtype']}, "
                      f"B={B} filters/GPU, T={T}, dt={dt}, GPS update every {k} step(s)",
                 extra={'filters_per_gpu': B, 'time_steps_per_launch': T, 'update_every': k})

@@ -1,4 +1,5 @@
-"""Reduce rocprofv3 PMC CSVs (tools/pmc_traffic.sh) to HBM bytes per cv_run_kernel launch.
+"""Reduce rocprofv3 PMC CSVs (tools/pmc_traffic.sh) to HBM bytes per launch of each config's
+dominant kernel (cv_block_kernel for the BASELINE configs, ref_events_kernel for ref15).
 
 usage: python tools/pmc_traffic.py OUTDIR CFG [CFG ...]   -> writes OUTDIR/pmc_traffic.json
 
@@ -53,7 +54,7 @@ def main():
     res = {'calibration': {'fetch_size_scale': read_scale, 'write_size_scale': write_scale,
                            'probe': 'tools/probes/bw_probe soa_read/soa_write, 8 B per lane, B=2^20, T=64'}}
     for c in cfgs:
-        kern = 'ref_events_kernel' if c == 'ref15' else 'cv_run_kernel'
+        kern = 'ref_events_kernel' if c == 'ref15' else 'cv_block_kernel'
         f = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE'), kern)
         w = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE'), kern)
         fetch = 1024 * sum(f) / len(f)
