@@ -88,6 +88,13 @@ kfmi::CvArgs base_args(const kf_batch* h) {
     // KFMI_CV_KERNEL=general forces the general kernel (tests, A/B)
     const char* v = std::getenv("KFMI_CV_KERNEL");
     a.block_p = (h->block_p && h->r_diag && !(v && !std::strcmp(v, "general"))) ? 1 : 0;
+    // the block kernel keeps 7 steps of inputs in flight per lane: with one filter per lane a
+    // small batch is one or two waves per SIMD, too few to cover HBM latency with 1-step
+    // prefetch, and at 2^20 filters depth 8 still measured ~1.5% ahead of depth 2
+    // (profiles/r01_ab/prefetch_depth_ab.txt); KFMI_CV_KERNEL=block2|block4 forces the depth
+    a.prefetch_depth = 8;
+    if (v && !std::strcmp(v, "block2")) a.prefetch_depth = 2;
+    if (v && !std::strcmp(v, "block4")) a.prefetch_depth = 4;
     return a;
 }
 

@@ -249,7 +249,7 @@ __global__ __launch_bounds__(kBlock, (RunOcc<D, T>::value)) void cv_run_kernel(c
 // renormalise, velocities, renormalise).  The host selects it only when the handle's P is
 // known to be block-diagonal (kf_alloc / kf_reset, or checked on the device in kf_set_state).
 // ------------------------------------------------------------------------------------
-template <int D, typename T>
+template <int D, typename T, int DEPTH>
 __global__ __launch_bounds__(kBlock) void cv_block_kernel(const CvArgs a) {
     constexpr int N = 2 * D;
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -369,17 +369,25 @@ __global__ __launch_bounds__(kBlock) void cv_block_kernel(const CvArgs a) {
         st = (ld == ld) ? st : kNotSpd;
         stb(a.logdet, t, rb, off, ld);
     };
-    StepIn<D, T> A, Bf;
-    load_in(0, A);
+    // Inputs are prefetched DEPTH - 1 steps ahead through a ring of DEPTH named buffers (the
+    // ring is fully unrolled, so every buffer index is static and nothing is copied): with few
+    // filters a SIMD has one or two waves, and the bytes in flight — not the arithmetic — bound
+    // the step rate.
+    StepIn<D, T> buf[DEPTH];
+#pragma unroll
+    for (int j = 0; j < DEPTH - 1; ++j) load_in(j, buf[j]);
     __builtin_amdgcn_s_waitcnt(0);
     int t = 0;
-    for (; t + 1 < T_; t += 2) {
-        load_in(t + 1, Bf);
-        step(t, A);
-        load_in(t + 2, A);
-        step(t + 1, Bf);
+    for (; t + DEPTH <= T_; t += DEPTH) {
+#pragma unroll
+        for (int j = 0; j < DEPTH; ++j) {
+            load_in(t + j + DEPTH - 1, buf[(j + DEPTH - 1) % DEPTH]);
+            step(t + j, buf[j]);
+        }
     }
-    if (t < T_) step(t, A);
+#pragma unroll
+    for (int j = 0; j < DEPTH - 1; ++j)
+        if (t + j < T_) step(t + j, buf[j]);
 #pragma unroll
     for (int i = 0; i < D; ++i) {
         stb(a.x, i, rb, off, xp[i]);
@@ -563,8 +571,12 @@ hipError_t launch_run(const CvArgs& a, dim3 grid, hipStream_t st) {
             for (int j = i; j < D; ++j, ++k)
                 if (i != j && a.r[k] != 0.0) diag = false;
     }
-    if (fast && diag && a.block_p)
-        cv_block_kernel<D, T><<<grid, kBlock, 0, st>>>(a);
+    if (fast && diag && a.block_p && a.prefetch_depth == 8)
+        cv_block_kernel<D, T, 8><<<grid, kBlock, 0, st>>>(a);
+    else if (fast && diag && a.block_p && a.prefetch_depth == 4)
+        cv_block_kernel<D, T, 4><<<grid, kBlock, 0, st>>>(a);
+    else if (fast && diag && a.block_p)
+        cv_block_kernel<D, T, 2><<<grid, kBlock, 0, st>>>(a);
     else if (fast && diag)
         cv_run_kernel<D, T, false, true><<<grid, kBlock, lds, st>>>(a);
     else if (fast)

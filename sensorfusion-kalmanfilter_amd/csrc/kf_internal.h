@@ -28,6 +28,7 @@ struct CvArgs {
     double r[6];             // R upper triangle, packed row-major (m <= 3)
     double p0_pos, p0_vel;   // reset covariance
     int block_p;             // P is block-diagonal over the axes (kf_run may use cv_block_kernel)
+    int prefetch_depth;      // cv_block_kernel's input ring: 2, 4 or 8 steps
 };
 
 struct SynthArgs {

@@ -331,13 +331,15 @@ def _run_with_kernel(kernel, name, dtype, x0, u, z, k, dt, P=None):
 @pytest.mark.parametrize('dtype', ['f64', 'f32'])
 @pytest.mark.parametrize('name', ['cv2', 'cv3'])
 @pytest.mark.parametrize('k', [1, 10])
-def test_block_kernel_equals_general_kernel(dtype, name, k):
+@pytest.mark.parametrize('variant', ['block2', 'block4', 'block8'])
+def test_block_kernel_equals_general_kernel(dtype, name, k, variant):
     """With the reference's diagonal R and P0, P stays block-diagonal over the axes and
-    kf_run uses cv_block_kernel; it evaluates the general kernel's expressions for the non-zero
-    entries in the same order, so both produce the same numbers."""
+    kf_run uses cv_block_kernel (prefetch depth 2, or 4 for few filters); it evaluates the general
+    kernel's expressions for the non-zero entries in the same order, so all produce the same
+    numbers."""
     model = MODEL[name]
     x0, u, z = random_inputs(model, 777, 60, k, seed=11 + k)
-    blk = _run_with_kernel('auto', name, dtype, x0, u, z, k, 0.1 if k == 1 else 0.01)
+    blk = _run_with_kernel(variant, name, dtype, x0, u, z, k, 0.1 if k == 1 else 0.01)
     gen = _run_with_kernel('general', name, dtype, x0, u, z, k, 0.1 if k == 1 else 0.01)
     for a, b in zip(blk, gen):
         np.testing.assert_array_equal(a, b)
