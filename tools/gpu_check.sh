@@ -26,6 +26,9 @@ step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py "$@"
 cd /tmp
-step rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o kt -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline "$@"
+# the bench command itself under rocprof: its JSON line (bench_profiled.json) and the kernel
+# stats come from one process, so they see the same HBM placement
+step rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o kt -- python3 "$ROOT/bench.py" --no-cpu-baseline "$@"
 cd "$ROOT"
+grep '^{"metric"' "$OUT/rocprof_stats.log" | tail -1 > "$OUT/bench_profiled.json" || true
 tail -3 "$OUT/pytest_gpu.log"; cat "$OUT/bench.log" | tail -2

@@ -42,6 +42,25 @@ __global__ __launch_bounds__(256) void tiled_stream(const double* __restrict__ i
         for (int i = 0; i < 7; ++i) out[((long(t) * W + w) * 7 + i) * 64 + l] = acc + i;
     }
 }
+// Filter-block major: in [B/256][T][6][256], out [B/256][T][7][256]: a workgroup's whole
+// launch is one contiguous span, so the pages it touches are few and consecutive.
+__global__ __launch_bounds__(256) void blocked_stream(const double* __restrict__ in, double* __restrict__ out,
+                                                      long B, int T) {
+    long f = long(blockIdx.x) * 256 + threadIdx.x;
+    if (f >= B) return;
+    const double* ib = in + long(blockIdx.x) * T * 6 * 256 + threadIdx.x;
+    double* ob = out + long(blockIdx.x) * T * 7 * 256 + threadIdx.x;
+    double acc = 0;
+    for (int t = 0; t < T; ++t) {
+        double v[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v[i] = ib[(long(t) * 6 + i) * 256];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) acc += v[i];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) ob[(long(t) * 7 + i) * 256] = acc + i;
+    }
+}
 // SoA rows moved 16 B per lane: lane pairs (2j, 2j+1) swap one value with DPP (quad_perm
 // [1,0,3,2]) so the even lane moves row r of filters (2j, 2j+1) and the odd lane row r+1.
 __device__ __forceinline__ double swap_pair(double v) {
@@ -162,6 +181,7 @@ int main(int argc, char** argv) {
     timeit("soa_stream_nt", [&] { soa_stream_nt<<<grid, 256>>>(in, out, B, T); }, double(in_bytes + out_bytes));
     timeit("soa_stream", [&] { soa_stream<<<grid, 256>>>(in, out, B, T); }, double(in_bytes + out_bytes));
     timeit("tiled_stream", [&] { tiled_stream<<<grid, 256>>>(in, out, B, T); }, double(in_bytes + out_bytes));
+    timeit("blocked_stream", [&] { blocked_stream<<<grid, 256>>>(in, out, B, T); }, double(in_bytes + out_bytes));
     timeit("soa_read", [&] { soa_read<<<grid, 256>>>(in, out, B, T); }, double(in_bytes));
     timeit("soa_write", [&] { soa_write<<<grid, 256>>>(in, out, B, T); }, double(out_bytes));
     const long n4 = long(in_bytes / 16);
