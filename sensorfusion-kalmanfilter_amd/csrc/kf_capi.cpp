@@ -437,15 +437,23 @@ int kf_run_events(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     a.gate = gate;
     a.threshold = threshold;
     // Few filters cannot fill the chip one lane each: give every axis chain its own lane
-    // (8 lanes per filter).  KFMI_EVENTS_KERNEL=lane|chain forces a variant (tests, A/B).
-    bool chain = h->B < kChainMaxFilters;
+    // (8 lanes per filter).  Otherwise one lane per filter, with the inputs staged through LDS
+    // by DMA where its layout conditions hold.  KFMI_EVENTS_KERNEL=lane|chain|lds forces a
+    // variant (tests, A/B) where it is legal.
+    const uint64_t span = static_cast<uint64_t>(h->B) * elem(h);
+    // the chain kernel addresses up to 27 [B] rows through one descriptor (32-bit byte count);
+    // the LDS kernel moves 16-B chunks (B % 16 == 0: none straddles B) of a 9-row payload span
+    const bool chain_ok = span * 27u < (uint64_t(1) << 32);
+    const bool lds_ok = h->B % 16 == 0 && span * 9u < (uint64_t(1) << 32);
+    int variant = h->B < kChainMaxFilters && chain_ok ? kfmi::kEventsChain
+                  : lds_ok                            ? kfmi::kEventsLds
+                                                      : kfmi::kEventsLane;
     if (const char* v = std::getenv("KFMI_EVENTS_KERNEL")) {
-        if (!std::strcmp(v, "chain")) chain = true;
-        else if (!std::strcmp(v, "lane")) chain = false;
+        if (!std::strcmp(v, "chain") && chain_ok) variant = kfmi::kEventsChain;
+        else if (!std::strcmp(v, "lane")) variant = kfmi::kEventsLane;
+        else if (!std::strcmp(v, "lds") && lds_ok) variant = kfmi::kEventsLds;
     }
-    // the chain kernel addresses up to 27 [B] rows through one descriptor (32-bit byte count)
-    if (chain && static_cast<uint64_t>(h->B) * elem(h) * 27u >= (uint64_t(1) << 32)) chain = false;
-    hipError_t e = kfmi::launch_ref_events(h->model, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream), chain);
+    hipError_t e = kfmi::launch_ref_events(h->model, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream), variant);
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_run_events");
 }
 

@@ -294,6 +294,21 @@ __device__ __forceinline__ void stb_stream(void* base, int64_t r, uint32_t row_b
                                           KF_STREAM_CPOL);
 }
 
+// LDS-DMA: 64 lanes x 16 B from a row-span descriptor (the lane's chunk at voff + soff) to the
+// wave-uniform LDS address `lds` + lane * 16 (buffer_load_dwordx4 ... lds).
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, unsigned char* lds, uint32_t voff, int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bytes_rsrc(const void* p, uint32_t nbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, p ? nbytes : 0u, 0x00020000);
+}
+__device__ __forceinline__ void stb_u8(void* base, int64_t r, uint32_t row_bytes, uint32_t off, uint8_t v) {
+    __builtin_amdgcn_raw_buffer_store_b8(v, row_rsrc(base, r, row_bytes), off, 0, 0);
+}
+__device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+template <int IMM>
+__device__ __forceinline__ void waitcnt() { __builtin_amdgcn_s_waitcnt(IMM); }
+
 template <typename T>
 __device__ __forceinline__ T ldb(const void* base, int64_t r, uint32_t row_bytes, uint32_t off);
 template <>

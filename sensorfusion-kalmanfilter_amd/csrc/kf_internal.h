@@ -127,7 +127,10 @@ hipError_t launch_cv(int axes, bool f64, Op op, const CvArgs& a, hipStream_t str
 hipError_t launch_cv_offblock(int axes, bool f64, const CvArgs& a, int* flag, hipStream_t stream);
 hipError_t launch_synth(int axes, bool f64, const SynthArgs& a, hipStream_t stream);
 // chain = true: the chain-parallel kernel (kGroup lanes per filter), for few filters.
-hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, bool chain);
+// kf_run_events kernel variants: one lane per filter (inputs loaded to registers), one lane
+// per axis chain (few filters), one lane per filter with inputs staged through LDS by DMA
+constexpr int kEventsLane = 0, kEventsChain = 1, kEventsLds = 2;
+hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, int variant);
 hipError_t launch_ref_reset(int model, bool f64, const RefArgs& a, hipStream_t stream);
 hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream);
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream);

@@ -72,12 +72,15 @@ struct Chains {
     __device__ static __forceinline__ void chain_predict(T (&xb)[NB], T (&Pb)[NB * (NB + 1) / 2], T dt,
                                                          const T (&q)[NB]) {
         const T c[3] = {T(1), dt, T(0.5) * dt * dt};
+        // the d / e loops run a constant 2 trips with a compile-time guard: a trip count of
+        // min(NB - i, 3) - 1 was left as a runtime loop with indexed register reads (s_set_gpr_idx)
         T xn[NB];
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
             T s = xb[i];
 #pragma unroll
-            for (int d = 1; d < NB - i && d < 3; ++d) s = fmaT(c[d], xb[i + d], s);
+            for (int d = 1; d < 3; ++d)
+                if (i + d < NB) s = fmaT(c[d], xb[i + d], s);
             xn[i] = s;
         }
         T FP[NB][NB];
@@ -87,7 +90,8 @@ struct Chains {
             for (int j = 0; j < NB; ++j) {
                 T s = Pb[tri<NB>(i, j)];
 #pragma unroll
-                for (int d = 1; d < NB - i && d < 3; ++d) s = fmaT(c[d], Pb[tri<NB>(i + d, j)], s);
+                for (int d = 1; d < 3; ++d)
+                    if (i + d < NB) s = fmaT(c[d], Pb[tri<NB>(i + d, j)], s);
                 FP[i][j] = s;
             }
 #pragma unroll
@@ -96,7 +100,8 @@ struct Chains {
             for (int j = i; j < NB; ++j) {
                 T s = FP[i][j];
 #pragma unroll
-                for (int e = 1; e < NB - j && e < 3; ++e) s = fmaT(FP[i][j + e], c[e], s);
+                for (int e = 1; e < 3; ++e)
+                    if (j + e < NB) s = fmaT(FP[i][j + e], c[e], s);
                 Pb[tri<NB>(i, j)] = (i == j) ? s + q[i] * dt : s;
             }
 #pragma unroll
@@ -158,7 +163,9 @@ struct Chains {
     // IMU pseudo-measurement (kf_workers.py:698-706, hw5_2.py:352-366): Z from the PREDICTED
     // state and the raw sample, H = I, R = diag(50, 0.05, 10, 0.1, 100 per group).  imu = (roll,
     // pitch, yaw, wx, wy, wz, ax, ay, az).
-    __device__ __forceinline__ bool update_imu(const T (&imu)[9], T dt) {
+    // `imu` is any indexable payload: a register array, or an LDS image (ref_events_lds_kernel)
+    template <class Pay>
+    __device__ __forceinline__ bool update_imu(const Pay& imu, T dt) {
         bool ok = true;
         const T Rp[6] = {T(kRPos), T(0), T(0), T(kRVel), T(0), T(kRAcc)};
         const T Ra[3] = {T(kRAtt), T(0), T(kRRate)};
@@ -246,7 +253,8 @@ struct Chains {
     // IMU update; with `gate`, the update only when logdet(P_pred) > threshold
     // (run_adaptive_threshold_kalman_filter, kf_workers.py:1023-1025).  Returns whether the
     // update was applied; `ok` turns false on a non-positive-definite S.
-    __device__ __forceinline__ bool event(int type, T dt, const T (&pay)[9], bool gate, T threshold, bool& ok) {
+    template <class Pay>
+    __device__ __forceinline__ bool event(int type, T dt, const Pay& pay, bool gate, T threshold, bool& ok) {
         predict(dt);
         bool apply = (type == kGps || type == kImu);
         if (gate && apply) apply = logdet() > threshold;
@@ -266,7 +274,7 @@ struct Chains {
 // Per-filter event streams (kf_run_events).
 // ------------------------------------------------------------------------------------
 template <typename T, class M>
-__global__ __launch_bounds__(kBlock) void ref_events_kernel(const RefArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void ref_events_kernel(const RefArgs a) {
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
@@ -317,6 +325,112 @@ __global__ __launch_bounds__(kBlock) void ref_events_kernel(const RefArgs a) {
     }
     s.store(a.x, a.P, rb, off);
     a.status[f] = st;
+}
+
+// ------------------------------------------------------------------------------------
+// ref_events_kernel with its inputs staged through LDS by the DMA engine (buffer_load ... lds):
+// event t+1's payload, dt and type travel HBM -> LDS while event t computes, without VGPRs
+// (a register prefetch of the same inputs costs this fp64 kernel its third wave per SIMD).
+// Each wave owns one LDS image of an event's inputs:
+//   [0, 9*64*W)              payload rows 0..8, 64 filters each (row-major, lane-linear)
+//   [DT_OFF, DT_OFF + 512)   dt, 64 doubles
+//   [ET_OFF, ET_OFF + 64)    event type, 64 bytes
+// Every DMA instruction moves 64 lanes x 16 B of ONE input (a wave-uniform row-span descriptor,
+// the lane's chunk in voffset; the range check drops what lies beyond the span).  Order per
+// event: wait for the image (counted vmcnt: only the previous event's NST stores are younger),
+// read it into registers, drain those reads (lgkmcnt), issue the next event's DMA into the same
+// image, compute, store.  The per-event store count NST is fixed (absent records go to
+// zero-length descriptors) so the wait can be counted.  Requires B % 16 == 0 (no 16-B chunk
+// straddles B) and 9 * B * W < 2^32; the host falls back to ref_events_kernel otherwise.
+// ------------------------------------------------------------------------------------
+constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
+
+// payload element i of this lane, read from the wave's LDS image where the update uses it
+template <typename T>
+struct LdsPayload {
+    const T* img;  // image base + lane
+    __device__ __forceinline__ T operator[](int i) const { return img[i * 64]; }
+};
+
+template <typename T, class M, bool COV>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void ref_events_lds_kernel(
+    const RefArgs a) {
+    constexpr int W = int(sizeof(T));
+    constexpr int PAY = 9 * 64 * W;
+    constexpr int NIP = (PAY + 1023) / 1024;    // payload DMA instructions
+    constexpr int LPR = 4 * W;                  // lanes per 64-filter row (16 B each)
+    constexpr int DT_OFF = NIP * 1024, ET_OFF = DT_OFF + 1024, IMG = ET_OFF + 64;
+    constexpr int NDMA = NIP + 2;
+    constexpr int NST = M::NTRAJ + 2 + (COV ? M::NBLK : 0);  // traj, logdet, updated (+ cov)
+    static_assert(NST + NDMA <= 63, "vmcnt range");
+    __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * 2 * IMG];
+    const int lane = int(threadIdx.x & 63);
+    const int wave = wave_uniform(int(threadIdx.x >> 6));
+    const int64_t f0 = int64_t(blockIdx.x) * kBlock + int64_t(wave) * 64;
+    if (f0 >= a.B) return;  // whole wave; partial waves keep their dead lanes for the DMA
+    const int64_t f = f0 + lane;
+    unsigned char* const img0 = lds + wave * 2 * IMG;
+    const uint32_t off = uint32_t(f) * uint32_t(W);  // dead lanes: beyond every row
+    const uint32_t rb = uint32_t(a.B) * uint32_t(W);
+    Chains<T, M> s;
+    s.load(a.x, a.P, rb, off);
+    int32_t st = f < a.B ? a.status[f] : 0;
+    const uint32_t rb_tr = a.traj ? rb : 0u, rb_ld = a.logdet ? rb : 0u, rb_cv = a.cov ? rb : 0u;
+    const uint32_t rb_up = a.updated ? uint32_t(a.B) : 0u;
+    // drain the state loads once: left pending into the loop, the waitcnt pass puts a wait for
+    // them at each first use in every iteration, and those waits would drain the DMA prefetch
+    waitcnt<vmcnt_imm(0)>();
+    // payload DMA instruction k moves rows 16/W*k + lane / LPR, 16-B chunk lane % LPR of each;
+    // the row step k * (16/W) * rb goes into soffset
+    const uint32_t voff_pay = uint32_t(lane / LPR) * rb + uint32_t(lane % LPR) * 16u;
+    auto issue = [&](int t, unsigned char* img) {
+        const char* pb = reinterpret_cast<const char*>(a.payload) + int64_t(t) * 9 * int64_t(rb) + f0 * W;
+        const __amdgpu_buffer_rsrc_t rp = bytes_rsrc(pb, 9u * rb - uint32_t(f0) * W);
+#pragma unroll
+        for (int k = 0; k < NIP; ++k)
+            if (k + 1 < NIP || k * 1024 + lane * 16 < PAY)
+                lds_dma16(rp, img + k * 1024, voff_pay, k * (16 / W) * int(rb));
+        const char* db = reinterpret_cast<const char*>(a.dt) + int64_t(t) * int64_t(a.B) * 8 + f0 * 8;
+        if (lane < 32) lds_dma16(bytes_rsrc(db, uint32_t(a.B - f0) * 8u), img + DT_OFF, uint32_t(lane) * 16u, 0);
+        const char* eb = reinterpret_cast<const char*>(a.etype) + int64_t(t) * int64_t(a.B) + f0;
+        if (lane < 4) lds_dma16(bytes_rsrc(eb, uint32_t(a.B - f0)), img + ET_OFF, uint32_t(lane) * 16u, 0);
+    };
+    issue(0, img0);
+    // the in-loop count assumes a previous event's NST stores are younger than this image's
+    // DMA; event 0 has none, so its image is waited for here
+    waitcnt<vmcnt_imm(0)>();
+    for (int t = 0; t < a.T; ++t) {
+        unsigned char* const img = img0 + (t & 1) * IMG;
+        // the other image was last read by event t - 1, whose reads have completed
+        if (t + 1 < a.T) {
+            issue(t + 1, img0 + ((t + 1) & 1) * IMG);
+            // event t's image: its DMA is older than event t-1's NST stores and this NDMA
+            waitcnt<vmcnt_imm(NST + NDMA)>();
+        } else {
+            waitcnt<vmcnt_imm(NST)>();
+        }
+        const int type = img[ET_OFF + lane];
+        const T dt = T(reinterpret_cast<const double*>(img + DT_OFF)[lane]);
+        const LdsPayload<T> pay{reinterpret_cast<const T*>(img) + lane};
+        bool applied = false;
+        if (type != 255) {
+            bool ok = true;
+            applied = s.event(type, dt, pay, a.gate != 0, T(a.threshold), ok);
+            if (!ok) {
+                st = kNotSpd;
+                s.fill_nan();
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < M::NTRAJ; ++i) stb(a.traj, int64_t(t) * M::NTRAJ + i, rb_tr, off, s.x[i]);
+        if constexpr (COV) s.store_cov(a.cov, int64_t(t) * M::NBLK, rb_cv, off);
+        const T ld = a.logdet ? s.logdet() : T(0);
+        st = (ld == ld) ? st : kNotSpd;
+        stb(a.logdet, t, rb_ld, off, ld);
+        stb_u8(a.updated, t, rb_up, uint32_t(f), applied ? uint8_t(1) : uint8_t(0));
+    }
+    s.store(a.x, a.P, rb, off);
+    if (f < a.B) a.status[f] = st;
 }
 
 template <typename T, class M>
@@ -804,8 +918,32 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
     return hipGetLastError();
 }
 
-hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, bool chain) {
-    if (chain) {
+hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, int variant) {
+    if (variant == kEventsLds) {
+        const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
+        const bool cov = a.cov != nullptr;
+        if (model == 15) {
+            if (f64) {
+                if (cov) ref_events_lds_kernel<double, M15, true><<<grid, kBlock, 0, stream>>>(a);
+                else ref_events_lds_kernel<double, M15, false><<<grid, kBlock, 0, stream>>>(a);
+            } else {
+                if (cov) ref_events_lds_kernel<float, M15, true><<<grid, kBlock, 0, stream>>>(a);
+                else ref_events_lds_kernel<float, M15, false><<<grid, kBlock, 0, stream>>>(a);
+            }
+        } else if (model == 8) {
+            if (f64) {
+                if (cov) ref_events_lds_kernel<double, M8, true><<<grid, kBlock, 0, stream>>>(a);
+                else ref_events_lds_kernel<double, M8, false><<<grid, kBlock, 0, stream>>>(a);
+            } else {
+                if (cov) ref_events_lds_kernel<float, M8, true><<<grid, kBlock, 0, stream>>>(a);
+                else ref_events_lds_kernel<float, M8, false><<<grid, kBlock, 0, stream>>>(a);
+            }
+        } else {
+            return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    if (variant == kEventsChain) {
         const dim3 cgrid(static_cast<unsigned>((a.B * kGroup + kBlock - 1) / kBlock));
         if (model == 15) {
             if (f64) ref_chain_kernel<double, M15><<<cgrid, kBlock, 0, stream>>>(a);

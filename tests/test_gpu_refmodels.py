@@ -125,17 +125,20 @@ def test_ref8_handle_rejects_ref15_only_entry_points():
             call()
 
 
-def _events_run(model, kernel, etype, dt, pay, x0, P0b, threshold=None):
+def _events_run(model, kernel, etype, dt, pay, x0, P0b, threshold=None, dtype='f64', records=True):
     import os as _os
     old = _os.environ.get('KFMI_EVENTS_KERNEL')
     _os.environ['KFMI_EVENTS_KERNEL'] = kernel
     try:
         B = etype.shape[1]
-        kf = kfmi.BatchedKF(model, B, 'f64')
-        kf.set_state(np.ascontiguousarray(x0.T), np.ascontiguousarray(P0b.T))
-        tr, ld, up, cv = kf.run_events(etype, dt, pay, updated=True, cov=True, threshold=threshold)
+        kf = kfmi.BatchedKF(model, B, dtype)
+        npd = np.float64 if dtype == 'f64' else np.float32
+        kf.set_state(np.ascontiguousarray(x0.T, npd), np.ascontiguousarray(P0b.T, npd))
+        tr, ld, up, cv = kf.run_events(etype, dt, np.ascontiguousarray(pay, npd), updated=records, cov=records,
+                                       threshold=threshold)
         x, Pb = kf.state()
-        out = [v.cpu().numpy() for v in (tr, ld, up, cv, x, Pb, kf.status())]
+        out = [None if v is None else v.double().cpu().numpy() if v.is_floating_point() else v.cpu().numpy()
+               for v in (tr, ld, up, cv, x, Pb, kf.status())]
         kf.close()
         return out
     finally:
@@ -269,3 +272,48 @@ def test_ref15_fp32_events_vs_fp64_oracle(kernel):
             worst_x = max(worst_x, np.linalg.norm(tr[t, :, f] - x[:6]) / max(np.linalg.norm(x[:6]), 1.0))
             worst_l = max(worst_l, abs(ld[t, f] - ref_ld) / max(abs(ref_ld), 1.0))
     assert worst_x <= 1e-3 and worst_l <= 1e-3, (worst_x, worst_l)
+
+
+@pytest.mark.parametrize('model', ['ref15', 'ref8'])
+@pytest.mark.parametrize('dtype', ['f64', 'f32'])
+@pytest.mark.parametrize('records,gated', [(True, False), (False, False), (True, True)])
+@pytest.mark.parametrize('B', [1040, 4096])
+def test_lds_kernel_matches_lane_kernel(model, dtype, records, gated, B):
+    """ref_events_lds_kernel (inputs staged through LDS by DMA; the default when B % 16 == 0)
+    against the register-input kernel on the same streams: the same per-event arithmetic, so
+    states, records, gate decisions and statuses agree to rounding.  B = 1040 leaves the last
+    wave with 16 live lanes (its dead lanes still move their share of every DMA)."""
+    rng = np.random.default_rng(41 + B + (dtype == 'f32'))
+    n = 15 if model == 'ref15' else 8
+    T = 37
+    etype = rng.choice([0, 1, 1, 1, 2], size=(T, B)).astype(np.uint8)
+    etype[30:, ::7] = 255
+    dt = rng.uniform(0.0, 0.05, (T, B))
+    pay = np.zeros((T, 9, B))
+    pay[:, 0:3] = rng.normal(0, 20, (T, 3, B))
+    pay[:, 3:6] = rng.normal(0, 0.05, (T, 3, B))
+    pay[:, 6:9] = rng.normal(0, 0.5, (T, 3, B))
+    x0 = rng.normal(0, 5, (B, n))
+    P0 = ref15.P0 if model == 'ref15' else ref8.P0
+    P0b = np.repeat(ref15.to_blocks(P0)[None], B, 0)
+    P0b[B - 3] = -P0b[B - 3]                            # a non-positive-definite filter in the last wave
+    thr = None
+    if gated:
+        ld = _events_run(model, 'lane', etype, dt, pay, x0, P0b, dtype=dtype)[1]
+        thr = float(np.median(ld[np.isfinite(ld)]))
+    lane = _events_run(model, 'lane', etype, dt, pay, x0, P0b, thr, dtype, records)
+    lds = _events_run(model, 'lds', etype, dt, pay, x0, P0b, thr, dtype, records)
+    tol = 1e-12 if dtype == 'f64' else 1e-5
+    for name, a, b in zip(('traj', 'logdet', 'updated', 'cov', 'x', 'P', 'status'), lane, lds):
+        if a is None:
+            assert b is None, name
+            continue
+        ok = np.isfinite(a)
+        np.testing.assert_array_equal(ok, np.isfinite(b), err_msg=name)
+        if name in ('updated', 'status'):
+            np.testing.assert_array_equal(a, b, err_msg=name)
+        else:
+            assert _rel(b[ok], a[ok]) <= tol, name
+    assert lds[6][B - 3] == kfmi.KF_ENOTSPD and (lds[6][np.arange(B) != B - 3] == 0).all()
+    if gated:
+        assert 0 < lds[2].mean() < 1
