@@ -115,6 +115,37 @@ __device__ __forceinline__ void ldl_pivot_product(const T (&P)[N * (N + 1) / 2],
     }
 }
 
+// Division-free determinants of small SPD blocks for the log-det, with the LDL pivots' test of
+// positive definiteness (every leading minor > 0, Sylvester).  3 x 3 by one fraction-free
+// elimination step with pivot a (the LDL order): a * det = (ad - b^2)(af - c^2) - (ae - bc)^2,
+// so num accumulates a * det and den accumulates a; the caller divides once.  The pivot
+// product d0 d1 d2 of LDL^T is the same quantity (d0 = a, d1 = (ad - b^2)/a,
+// d2 = num/(a (ad - b^2))) without its two reciprocals per block.
+template <typename T>
+__device__ __forceinline__ void det3_scaled(const T (&P)[6], T& num, T& den, bool& ok) {
+    const T a = P[0], b = P[1], c = P[2], d = P[3], e = P[4], f = P[5];
+    const T m2 = fmaT(-b, b, a * d);
+    const T g = fmaT(-c, c, a * f);
+    const T h = fmaT(-b, c, a * e);
+    const T n = fmaT(-h, h, m2 * g);
+    ok = ok && (a > T(0)) && (m2 > T(0)) && (n > T(0));
+    num *= n;
+    den *= a;
+}
+template <typename T>
+__device__ __forceinline__ void det2(const T (&P)[3], T& num, bool& ok) {
+    const T m2 = fmaT(-P[1], P[1], P[0] * P[2]);
+    ok = ok && (P[0] > T(0)) && (m2 > T(0));
+    num *= m2;
+}
+// renormalise a running product: prod = mantissa in [0.5, 1), exponent into ex
+template <typename T>
+__device__ __forceinline__ void renorm(T& prod, int& ex) {
+    int e;
+    prod = frexp(prod, &e);
+    ex += e;
+}
+
 // log det of an SPD N x N matrix (packed upper) via LDL^T; NaN unless positive definite.
 template <int N, typename T>
 __device__ __forceinline__ T logdet_ldl(const T (&P)[N * (N + 1) / 2]) {

@@ -191,18 +191,27 @@ struct Chains {
         return ok;
     }
 
-    // slogdet of the full P = sum over the chain blocks (kf_workers.py:716-717).
+    // slogdet of the full P = sum over the chain blocks (kf_workers.py:716-717): the product of
+    // the blocks' determinants, division-free per block (det3_scaled / det2) and one reciprocal
+    // for the pva pivots; fp32 renormalises after every block (three pva blocks reach 1e48).
     __device__ __forceinline__ T logdet() const {
-        T prod = T(1);
+        constexpr bool kNarrow = sizeof(T) == 4;
+        T num = T(1), den = T(1);
         int ex = 0;
         bool ok = true;
 #pragma unroll
-        for (int c = 0; c < M::NP; ++c) ldl_pivot_product<3, T>(pva[c], prod, ex, ok);
+        for (int c = 0; c < M::NP; ++c) {
+            det3_scaled<T>(pva[c], num, den, ok);
+            if (kNarrow || c == M::NP - 1) renorm(num, ex);
+        }
 #pragma unroll
-        for (int c = 0; c < M::NA; ++c) ldl_pivot_product<2, T>(aw[c], prod, ex, ok);
-        int e;
-        prod = frexp(prod, &e);
-        const T ld = log_mant(prod, ex + e);
+        for (int c = 0; c < M::NA; ++c) {
+            det2<T>(aw[c], num, ok);
+            if (kNarrow) renorm(num, ex);
+        }
+        T prod = num * rcp_nr<2>(den);
+        renorm(prod, ex);
+        const T ld = log_mant(prod, ex);
         return ok ? ld : quiet_nan<T>();
     }
 
@@ -496,10 +505,13 @@ __device__ __forceinline__ bool group_any(bool b) {
 
 template <typename T>
 __device__ __forceinline__ T chain_log_det(const T (&P)[6]) {
-    T prod = T(1);
+    // one 3-state chain's log det (an aw chain's inert third state has variance 1, no coupling)
+    T num = T(1), den = T(1);
     int ex = 0;
     bool ok = true;
-    ldl_pivot_product<3, T>(P, prod, ex, ok);
+    det3_scaled<T>(P, num, den, ok);
+    T prod = num * rcp_nr<2>(den);
+    renorm(prod, ex);
     const T ld = log_mant(prod, ex);
     return ok ? ld : quiet_nan<T>();
 }
