@@ -162,8 +162,11 @@ __device__ __forceinline__ T logdet_ldl(const T (&P)[N * (N + 1) / 2]) {
 //   S = P[0:M,0:M] + R, LDL^T(S) in-lane, K = P H^T S^-1 by substitution per row,
 //   x += K (z - x[0:M]),
 //   Joseph: P+ = (I-KH) P (I-KH)^T + K R K^T = (P - K G^T) + E K^T, G = P H^T, E = K S - G.
-// Returns false when S is not positive definite (x and P are then NaN).
-template <int N, int M, bool DIAG_R, typename T>
+// Returns false when S is not positive definite (x and P are then NaN).  NEWTON: Newton steps
+// on each pivot reciprocal (1 leaves a ~2^-46 relative gain error, which Joseph's form turns
+// into a second-order term of P+ and x carries at ~1e-14; the BASELINE kernels keep 2 so the
+// block and general constant-velocity kernels stay bit-identical).
+template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2>
 __device__ __forceinline__ bool sel_update(T (&x)[N], T (&P)[N * (N + 1) / 2], const T (&z)[M],
                                            const T (&R)[M * (M + 1) / 2]) {
     constexpr int MT = M * (M + 1) / 2;
@@ -189,7 +192,7 @@ __device__ __forceinline__ bool sel_update(T (&x)[N], T (&P)[N * (N + 1) / 2], c
         }
         ok = ok && (dj > T(0));
         d[j] = dj;
-        dinv[j] = rcp_pos<2>(dj);
+        dinv[j] = rcp_pos<NEWTON>(dj);
 #pragma unroll
         for (int i = j + 1; i < M; ++i) {
             T s = S[tri<M>(i, j)];

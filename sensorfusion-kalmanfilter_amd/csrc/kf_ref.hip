@@ -28,6 +28,8 @@ namespace {
 using namespace dev;
 
 constexpr int kGps = 0, kImu = 1;  // KF_EVENT_GPS / KF_EVENT_IMU; 2 = predict only, 255 = none
+// Newton steps on the update's pivot reciprocals (see sel_update)
+constexpr int kRefNewton = 1;
 
 
 // Noise constants shared by both reference models (kf_workers.py:519-544, 581-614;
@@ -154,7 +156,7 @@ struct Chains {
             T xb[3];
             get_pva(c, xb);
             const T zb[1] = {z[c]};
-            ok = sel_update<3, 1, true, T>(xb, pva[c], zb, R) && ok;
+            ok = sel_update<3, 1, true, T, kRefNewton>(xb, pva[c], zb, R) && ok;
             put_pva(c, xb);
         }
         return ok;
@@ -177,7 +179,7 @@ struct Chains {
             const T V = fmaT(a, dt, xb[1]);   // V = x_v + a dt
             const T X = fmaT(V, dt, xb[0]);   // X = x_p + V dt
             const T zb[3] = {X, V, a};
-            ok = sel_update<3, 3, true, T>(xb, pva[c], zb, Rp) && ok;
+            ok = sel_update<3, 3, true, T, kRefNewton>(xb, pva[c], zb, Rp) && ok;
             put_pva(c, xb);
         }
 #pragma unroll
@@ -185,7 +187,7 @@ struct Chains {
             T xa[2];
             get_aw(c, xa);
             const T za[2] = {imu[M::imu_att(c)], imu[M::imu_rate(c)]};
-            ok = sel_update<2, 2, true, T>(xa, aw[c], za, Ra) && ok;
+            ok = sel_update<2, 2, true, T, kRefNewton>(xa, aw[c], za, Ra) && ok;
             put_aw(c, xa);
         }
         return ok;
@@ -209,7 +211,7 @@ struct Chains {
             det2<T>(aw[c], num, ok);
             if (kNarrow) renorm(num, ex);
         }
-        T prod = num * rcp_nr<2>(den);
+        T prod = num * rcp_nr<kRefNewton>(den);
         renorm(prod, ex);
         const T ld = log_mant(prod, ex);
         return ok ? ld : quiet_nan<T>();
@@ -510,7 +512,7 @@ __device__ __forceinline__ T chain_log_det(const T (&P)[6]) {
     int ex = 0;
     bool ok = true;
     det3_scaled<T>(P, num, den, ok);
-    T prod = num * rcp_nr<2>(den);
+    T prod = num * rcp_nr<kRefNewton>(den);
     renorm(prod, ex);
     const T ld = log_mant(prod, ex);
     return ok ? ld : quiet_nan<T>();
@@ -614,13 +616,13 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
                     if (pva) {
                         const T zb[1] = {va};
                         const T R[1] = {T(kRGps)};
-                        ok = sel_update<3, 1, true, T>(x, P, zb, R);
+                        ok = sel_update<3, 1, true, T, kRefNewton>(x, P, zb, R);
                     }
                 } else {
                     const T V = fmaT(vb, dt, x[1]);
                     const T X = fmaT(V, dt, x[0]);
                     const T zb[3] = {pva ? X : va, pva ? V : vb, pva ? vb : T(0)};
-                    ok = sel_update<3, 3, true, T>(x, P, zb, Rimu);
+                    ok = sel_update<3, 3, true, T, kRefNewton>(x, P, zb, Rimu);
                     if (!pva) {  // reset the inert state
                         x[2] = T(0);
                         P[5] = T(1);
@@ -790,7 +792,7 @@ __device__ __forceinline__ Ref15<T> posterior(const Ref15<T>& s0, int type, bool
         T xb[3] = {T(0), T(0), T(0)};
         const T z[1] = {T(0)};
         const T R[1] = {T(type == kGps ? kRGps : kRPos)};
-        sel_update<3, 1, true, T>(xb, c.pva[0], z, R);
+        sel_update<3, 1, true, T, kRefNewton>(xb, c.pva[0], z, R);
     } else if (type == kGps) {
         const T z[3] = {T(0), T(0), T(0)};
         c.update_gps(z);
@@ -818,7 +820,7 @@ __device__ __forceinline__ T first_row_gain(const Ref15<T>& s, int type) {
     T xb[3] = {T(0), T(0), T(0)};
     const T z[1] = {T(0)};
     const T R[1] = {T(type == kGps ? kRGps : kRPos)};
-    sel_update<3, 1, true, T>(xb, p, z, R);
+    sel_update<3, 1, true, T, kRefNewton>(xb, p, z, R);
     T tr = p[0] + p[3] + p[5];
 #pragma unroll
     for (int i = 1; i < 3; ++i) tr += s.pva[i][0] + s.pva[i][3] + s.pva[i][5];
