@@ -166,7 +166,9 @@ __device__ __forceinline__ T logdet_ldl(const T (&P)[N * (N + 1) / 2]) {
 // on each pivot reciprocal (1 leaves a ~2^-46 relative gain error, which Joseph's form turns
 // into a second-order term of P+ and x carries at ~1e-14; the BASELINE kernels keep 2 so the
 // block and general constant-velocity kernels stay bit-identical).
-template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2>
+// POISON = false: a non-positive pivot is only reported (return value), for callers that
+// replace the whole filter with NaN themselves (saves a select per reciprocal).
+template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2, bool POISON = true>
 __device__ __forceinline__ bool sel_update(T (&x)[N], T (&P)[N * (N + 1) / 2], const T (&z)[M],
                                            const T (&R)[M * (M + 1) / 2]) {
     constexpr int MT = M * (M + 1) / 2;
@@ -192,7 +194,7 @@ __device__ __forceinline__ bool sel_update(T (&x)[N], T (&P)[N * (N + 1) / 2], c
         }
         ok = ok && (dj > T(0));
         d[j] = dj;
-        dinv[j] = rcp_pos<NEWTON>(dj);
+        dinv[j] = POISON ? rcp_pos<NEWTON>(dj) : rcp_nr<NEWTON>(dj);
 #pragma unroll
         for (int i = j + 1; i < M; ++i) {
             T s = S[tri<M>(i, j)];

@@ -148,6 +148,7 @@ struct Chains {
 
     // GPS fix (kf_workers.py:694-697, hw5_2.py:341-349): H selects pos_c in each (pos, vel,
     // acc) chain, R = 3; z = (easting, northing[, altitude]).
+    template <bool POISON = true>
     __device__ __forceinline__ bool update_gps(const T (&z)[3]) {
         bool ok = true;
         const T R[1] = {T(kRGps)};
@@ -156,7 +157,7 @@ struct Chains {
             T xb[3];
             get_pva(c, xb);
             const T zb[1] = {z[c]};
-            ok = sel_update<3, 1, true, T, kRefNewton>(xb, pva[c], zb, R) && ok;
+            ok = sel_update<3, 1, true, T, kRefNewton, POISON>(xb, pva[c], zb, R) && ok;
             put_pva(c, xb);
         }
         return ok;
@@ -166,7 +167,7 @@ struct Chains {
     // state and the raw sample, H = I, R = diag(50, 0.05, 10, 0.1, 100 per group).  imu = (roll,
     // pitch, yaw, wx, wy, wz, ax, ay, az).
     // `imu` is any indexable payload: a register array, or an LDS image (ref_events_lds_kernel)
-    template <class Pay>
+    template <bool POISON = true, class Pay>
     __device__ __forceinline__ bool update_imu(const Pay& imu, T dt) {
         bool ok = true;
         const T Rp[6] = {T(kRPos), T(0), T(0), T(kRVel), T(0), T(kRAcc)};
@@ -179,7 +180,7 @@ struct Chains {
             const T V = fmaT(a, dt, xb[1]);   // V = x_v + a dt
             const T X = fmaT(V, dt, xb[0]);   // X = x_p + V dt
             const T zb[3] = {X, V, a};
-            ok = sel_update<3, 3, true, T, kRefNewton>(xb, pva[c], zb, Rp) && ok;
+            ok = sel_update<3, 3, true, T, kRefNewton, POISON>(xb, pva[c], zb, Rp) && ok;
             put_pva(c, xb);
         }
 #pragma unroll
@@ -187,7 +188,7 @@ struct Chains {
             T xa[2];
             get_aw(c, xa);
             const T za[2] = {imu[M::imu_att(c)], imu[M::imu_rate(c)]};
-            ok = sel_update<2, 2, true, T, kRefNewton>(xa, aw[c], za, Ra) && ok;
+            ok = sel_update<2, 2, true, T, kRefNewton, POISON>(xa, aw[c], za, Ra) && ok;
             put_aw(c, xa);
         }
         return ok;
@@ -264,7 +265,8 @@ struct Chains {
     // IMU update; with `gate`, the update only when logdet(P_pred) > threshold
     // (run_adaptive_threshold_kalman_filter, kf_workers.py:1023-1025).  Returns whether the
     // update was applied; `ok` turns false on a non-positive-definite S.
-    template <class Pay>
+    // POISON = false for callers that fill the filter with NaN when `ok` turns false
+    template <bool POISON = true, class Pay>
     __device__ __forceinline__ bool event(int type, T dt, const Pay& pay, bool gate, T threshold, bool& ok) {
         predict(dt);
         bool apply = (type == kGps || type == kImu);
@@ -272,9 +274,9 @@ struct Chains {
         if (apply) {
             if (type == kGps) {
                 const T z[3] = {pay[0], pay[1], pay[2]};  // (easting, northing, altitude)
-                ok = update_gps(z) && ok;
+                ok = update_gps<POISON>(z) && ok;
             } else {
-                ok = update_imu(pay, dt) && ok;
+                ok = update_imu<POISON>(pay, dt) && ok;
             }
         }
         return apply;
@@ -311,7 +313,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
         bool applied = false;
         if (in.type != 255) {
             bool ok = true;
-            applied = s.event(in.type, T(in.dt), in.pay, a.gate != 0, T(a.threshold), ok);
+            applied = s.template event<false>(in.type, T(in.dt), in.pay, a.gate != 0, T(a.threshold), ok);
             if (!ok) {
                 st = kNotSpd;
                 s.fill_nan();
@@ -426,7 +428,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
         bool applied = false;
         if (type != 255) {
             bool ok = true;
-            applied = s.event(type, dt, pay, a.gate != 0, T(a.threshold), ok);
+            applied = s.template event<false>(type, dt, pay, a.gate != 0, T(a.threshold), ok);
             if (!ok) {
                 st = kNotSpd;
                 s.fill_nan();
@@ -896,7 +898,7 @@ __global__ __launch_bounds__(kBlock) void ref15_sched_kernel(const Ref15SchedArg
 #pragma unroll
         for (int k = 0; k < 9; ++k) pay[k] = ps[int64_t(k) * B];
         bool ok = true;
-        s.event(a.etype[int64_t(sel) * B + f], T(tsel - prev), pay, false, T(0), ok);
+        s.template event<false>(a.etype[int64_t(sel) * B + f], T(tsel - prev), pay, false, T(0), ok);
         if (!ok) {
             st = kNotSpd;
             s.fill_nan();
