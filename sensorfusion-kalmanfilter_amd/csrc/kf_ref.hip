@@ -472,6 +472,10 @@ __global__ __launch_bounds__(kBlock) void ref_reset_kernel(const RefArgs a) {
 // exact zeros); only the logdet is summed per chain instead of multiplied then logged.
 // ------------------------------------------------------------------------------------
 constexpr int kGroup = 8;
+#ifndef KF_CHAIN_DEPTH
+#define KF_CHAIN_DEPTH 2
+#endif
+constexpr int kChainDepth = KF_CHAIN_DEPTH;  // input ring of ref_chain_kernel
 
 // Sums / ORs over the 8-lane group with DPP (a VALU-latency lane exchange, no LDS round trip):
 // quad_perm [1,0,3,2] (xor 1), quad_perm [2,3,0,1] (xor 2), then row_half_mirror (lane i <-> 7-i
@@ -653,17 +657,32 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
         if (a.updated && c == 0) a.updated[int64_t(t) * a.B + f] = applied ? 1 : 0;
     };
 
-    // unrolled x2 over two named input buffers: event t+1 loads while event t computes, with no
-    // loop-carried register copy (a copy would wait on the loads at the back edge)
-    ChainIn<T> A, Bn;
-    if (a.T > 0) load(0, A);
-    for (int t = 0; t < a.T; t += 2) {
-        const bool two = t + 1 < a.T;
-        load(two ? t + 1 : t, Bn);
-        step(t, A);
-        if (!two) break;
-        load(t + 2 < a.T ? t + 2 : t + 1, A);
-        step(t + 1, Bn);
+    // Inputs are prefetched kChainDepth - 1 events ahead through a fully unrolled ring of named
+    // buffers (static indices, no loop-carried copies); loads past the end re-read the last
+    // event, and the prologue's loads are drained once so no in-loop wait targets them.  Depths
+    // 2, 3, 4 and 8 were A/B-measured on config 1 (one filter) without a resolvable difference:
+    // a single wave's launch time varies +-10% from launch to launch
+    // (profiles/r01_ab/chain_depth_inproc.json), and each depth adds a copy of the event body
+    // (48 KB of code at 8), so the default stays at 2.
+    constexpr int D = kChainDepth;
+    const int T_ = a.T;
+    auto load_c = [&](int t, ChainIn<T>& in) { load(t < T_ ? t : T_ - 1, in); };
+    if (T_ > 0) {
+        ChainIn<T> buf[D];
+#pragma unroll
+        for (int j = 0; j < D - 1; ++j) load_c(j, buf[j]);
+        __builtin_amdgcn_s_waitcnt(0);
+        int t = 0;
+        for (; t + D <= T_; t += D) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                load_c(t + j + D - 1, buf[(j + D - 1) % D]);
+                step(t + j, buf[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < D - 1; ++j)
+            if (t + j < T_) step(t + j, buf[j]);
     }
     {
         const auto rx = span_rsrc(a.x, 0, rb, M::N), rp = span_rsrc(a.P, 0, rb, M::NBLK);
