@@ -47,7 +47,8 @@ CONFIGS = {
     '4': dict(model='cv3', dtype='f32', B=1048576, T=256, dt=0.1, k=1),
     '5': dict(model='cv3', dtype='f64', B=1048576, T=500, dt=0.01, k=10),
     'ref15': dict(model='ref15', dtype='f64', B=1048576, T=256, dt=0.005, k=20),
-    'bf': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22),
+    'bf': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=True),
+    'bf_subsets': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=False),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 SEED = 20251015
@@ -404,8 +405,17 @@ def bf_workload(cfg, args, rank, world, dev):
     total_steps = sum(math.comb(n, k) * (k + 1) for k in range(1, n + 1))
     launches = [(k, off) for k in range(1, n + 1) for off in range(0, math.comb(n, k), width)]
     t_end = t0 + 0.005 * (n + 1)
+    search = cfg['search']
+    if search:
+        kf.close()
+        kf = kfmi.BatchedKF('ref15', 1, 'f64', device=dev.index)
 
     def step():
+        if search:
+            # R_threshold below every subset's score: the reference's longest search (every
+            # size, kf_workers.py:1391-1392); one kf_search_combos call, levels 1..n
+            kf.search_combos(ev, init, t0, t_end, -1e30, exhaustive=True)
+            return
         for k, off in launches:
             kf.eval_combos(ev, init, t0, t_end, k, combo_offset=off, logdets=False)
 
@@ -455,10 +465,25 @@ def bf_workload(cfg, args, rank, world, dev):
                                          'cores': 1, 'sample': f'{n_np} subsets, oracle/ref_kf.evaluate_combo_chunk, '
                                                                f'NumPy {np.__version__}'}}
 
+    if search:
+        from kfmi.ref15 import search_level_bytes
+        # every stored node (the C(n-1, k) subsets of size k < n without the last candidate) is
+        # written once and read once as a parent
+        lvl = sum(search_level_bytes(math.comb(n - 1, k), 'f64') for k in range(1, n))
+        return dict(step=step, units=total_steps, bytes=2 * lvl, bytes_per_unit=2 * lvl / total_combos,
+                    kernel='ref15_search_kernel', traffic=None, cpu=cpu, gather=None, kf=kf, combos=total_combos,
+                    roofline_note='level-buffer bytes only (each stored prefix filter written and read once); the '
+                                  'kernel is co-limited by fp64 issue (one event step + final predict per subset)',
+                    desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '
+                         f'all 2^{n}-1 subsets, reference 15-state model, f64, shared-prefix search '
+                         f'(kf_search_combos: one event step + final predict per subset, {n} level launches); '
+                         f'value counts the reference-equivalent steps (k events + final predict per k-subset)',
+                    extra={'candidate_events': n, 'combinations': total_combos, 'levels': n})
     return dict(step=step, units=total_steps, bytes=None, bytes_per_unit=None, kernel='ref15_combo_kernel',
                 traffic=None, cpu=cpu, gather=None, kf=kf, combos=total_combos,
                 desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '
-                     f'all 2^{n}-1 subsets, reference 15-state model, f64, {len(launches)} kf_eval_combos launches',
+                     f'all 2^{n}-1 subsets, reference 15-state model, f64, {len(launches)} kf_eval_combos launches '
+                     f'(one filter per subset)',
                 extra={'candidate_events': n, 'combinations': total_combos, 'launch_width': width})
 
 
@@ -493,7 +518,7 @@ def main():
         w = log_workload(cfg, args, rank, world, dev)
     elif args.config == 'ref15':
         w = ref15_workload(cfg, args, rank, world, dev)
-    elif args.config == 'bf':
+    elif args.config in ('bf', 'bf_subsets'):
         w = bf_workload(cfg, args, rank, world, dev)
     else:
         w = cv_workload(args.config, cfg, args, rank, world, dev)
@@ -520,7 +545,7 @@ def main():
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev])) if ev else float('nan')
 
     kf = w['kf']
-    bad = int((kf.status() != 0).sum().item()) if args.config != 'bf' else 0
+    bad = int((kf.status() != 0).sum().item()) if not args.config.startswith('bf') else 0
     gather_ms = None
     if dist:
         from kfmi import dist as kdist

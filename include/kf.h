@@ -200,6 +200,26 @@ int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const d
                    double prev_time, double target_end, int k, uint64_t combo_offset, void* logdets,
                    void* max_logdet, int32_t* n_records, void* stream);
 
+/* KF_MODEL_REF15 brute-force search with shared prefixes: the search of
+ * run_brute_force_kalman_filter_no_sampling_min_usage (kf_workers.py:1218-1392) over the
+ * subsets of the n_events candidates, for subset sizes k = 1 .. k_max.  The filter of a subset
+ * is its prefix's filter (stored in device level buffers owned by the handle) advanced by one
+ * event, so each subset costs one event step plus the worker's final predict instead of a
+ * whole filter run; the arithmetic per subset is kf_eval_combos's.  A subset is accepted when
+ * its max log-determinant (records as kf_eval_combos) is < threshold (:1353).  The search
+ * stops after the first size with an accepted subset unless `exhaustive`.  Host outputs:
+ * *k_found = that size (0 = none), *winner = bit mask (bit i = candidate i) of its first
+ * accepted subset in itertools.combinations order (the reference's pick, :1349-1356),
+ * n_accepted host [k_max + 1] (nullable) accepted subsets per size.  subset_max: device [2^n]
+ * of the handle's dtype (n_events <= 30, nullable) receives every evaluated subset's max
+ * log-determinant (NaN for a failed filter), indexed by mask.  Level k stores the C(n - 1, k)
+ * subsets without the last candidate (the others have no extensions); C(n - 1, k) must stay
+ * below 2^28, and the handle's level buffers take 2 * C(n - 1, k) * (43 w + 16) bytes at the
+ * widest stored level (w = 8 for f64, 4 for f32).  The call synchronises `stream`. */
+int kf_search_combos(kf_batch* handle, int n_events, const double* events, const double* init,
+                     double prev_time, double target_end, double threshold, int k_max, int exhaustive,
+                     uint64_t* winner, int* k_found, uint64_t* n_accepted, void* subset_max, void* stream);
+
 /* KF_MODEL_REF15 scheduler scoring: gain device [n_types][B] = trace of the posterior
  * covariance each candidate sensor type (types: host [n_types] KF_EVENT_GPS|KF_EVENT_IMU,
  * n_types <= 16) would give every filter's current covariance.  full = 0: the reference's

@@ -25,6 +25,8 @@ struct kf_batch {
     void* P;          // [n(n+1)/2][B]
     int32_t* status;  // [B]
     void* ws;         // KF_MODEL_REF15: device workspace for kf_eval_combos (events, binomials, init)
+    void* search_ws;  // KF_MODEL_REF15: kf_search_combos level buffers (grown on demand)
+    size_t search_ws_bytes;
     bool r_diag;      // BASELINE models: R has no off-diagonal entry
     bool block_p;     // BASELINE models: every filter's P is block-diagonal over the axes
     int* flag;        // device int for the kf_set_state block check (allocated on first use)
@@ -61,6 +63,45 @@ constexpr size_t kWsBinom = sizeof(uint64_t) * (kMaxComboEvents + 1) * (kMaxComb
 constexpr size_t kWsInit = sizeof(double) * 42;
 
 bool is_ref15(const kf_batch* h) { return h->model == KF_MODEL_REF15; }
+
+// binomial table C(a, b), a, b <= 64 (exact in uint64; C(64, 32) < 2^63)
+const uint64_t* binom_table() {
+    static uint64_t binom[(kMaxComboEvents + 1) * (kMaxComboEvents + 1)];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (int a = 0; a <= kMaxComboEvents; ++a)
+            for (int b = 0; b <= kMaxComboEvents; ++b) {
+                uint64_t v = 0;
+                if (b == 0) v = 1;
+                else if (a > 0 && b <= a) v = binom[(a - 1) * (kMaxComboEvents + 1) + b - 1] + binom[(a - 1) * (kMaxComboEvents + 1) + b];
+                binom[a * (kMaxComboEvents + 1) + b] = v;
+            }
+    });
+    return binom;
+}
+
+// Upload the combination search's inputs (events, binomials, root state) to the handle's workspace.
+int upload_combo_inputs(kf_batch* h, int n_events, const double* events, const double* init, hipStream_t st,
+                        const char* what) {
+    char* ws = static_cast<char*>(h->ws);
+    hipError_t e = hipMemcpyAsync(ws, events, sizeof(double) * 11 * n_events, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(ws + kWsEvents, binom_table(), kWsBinom, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(ws + kWsEvents + kWsBinom, init, kWsInit, hipMemcpyHostToDevice, st);
+    return e == hipSuccess ? KF_OK : hip_fail(e, what);
+}
+
+int check_combo_inputs(const kf_batch* h, int n_events, const double* events, const double* init, const char* what) {
+    if (!is_ref15(h)) return fail(KF_EINVAL, "%s: needs a KF_MODEL_REF15 handle", what);
+    if (n_events < 1 || n_events > kMaxComboEvents)
+        return fail(KF_EINVAL, "%s: n_events = %d outside [1, %d]", what, n_events, kMaxComboEvents);
+    if (!events || !init) return fail(KF_EINVAL, "%s: null events/init", what);
+    for (int i = 0; i < n_events; ++i) {
+        const double ty = events[i * 11 + 1];
+        if (ty != KF_EVENT_GPS && ty != KF_EVENT_IMU)
+            return fail(KF_EINVAL, "%s: event %d has type %g (GPS=0 or IMU=1)", what, i, ty);
+    }
+    return KF_OK;
+}
 bool is_ref(int model) { return model == KF_MODEL_REF15 || model == KF_MODEL_REF8; }
 bool is_ref(const kf_batch* h) { return is_ref(h->model); }
 
@@ -257,6 +298,7 @@ int kf_free(kf_batch* h) {
     if (h->P) (void)hipFree(h->P);
     if (h->status) (void)hipFree(h->status);
     if (h->ws) (void)hipFree(h->ws);
+    if (h->search_ws) (void)hipFree(h->search_ws);
     if (h->flag) (void)hipFree(h->flag);
     delete h;
     return KF_OK;
@@ -461,36 +503,13 @@ int kf_eval_combos(kf_batch* h, int n_events, const double* events, const double
                    double target_end, int k, uint64_t combo_offset, void* logdets, void* max_logdet,
                    int32_t* n_records, void* stream) {
     if (int rc = check_handle(h)) return rc;
-    if (!is_ref15(h)) return fail(KF_EINVAL, "kf_eval_combos: needs a KF_MODEL_REF15 handle");
-    if (n_events < 1 || n_events > kMaxComboEvents)
-        return fail(KF_EINVAL, "kf_eval_combos: n_events = %d outside [1, %d]", n_events, kMaxComboEvents);
+    if (int rc = check_combo_inputs(h, n_events, events, init, "kf_eval_combos")) return rc;
     if (k < 1 || k > n_events) return fail(KF_EINVAL, "kf_eval_combos: k = %d outside [1, %d]", k, n_events);
-    if (!events || !init) return fail(KF_EINVAL, "kf_eval_combos: null events/init");
-    for (int i = 0; i < n_events; ++i) {
-        const double ty = events[i * 11 + 1];
-        if (ty != KF_EVENT_GPS && ty != KF_EVENT_IMU)
-            return fail(KF_EINVAL, "kf_eval_combos: event %d has type %g (GPS=0 or IMU=1)", i, ty);
-    }
     if (h->B == 0) return KF_OK;
-    // binomial table C(a, b), a, b <= 64 (exact in uint64)
-    static uint64_t binom[(kMaxComboEvents + 1) * (kMaxComboEvents + 1)];
-    static std::once_flag once;
-    std::call_once(once, [] {
-        for (int a = 0; a <= kMaxComboEvents; ++a)
-            for (int b = 0; b <= kMaxComboEvents; ++b) {
-                uint64_t v = 0;
-                if (b == 0) v = 1;
-                else if (a > 0 && b <= a) v = binom[(a - 1) * (kMaxComboEvents + 1) + b - 1] + binom[(a - 1) * (kMaxComboEvents + 1) + b];
-                binom[a * (kMaxComboEvents + 1) + b] = v;
-            }
-    });
-    const uint64_t n_combos = binom[n_events * (kMaxComboEvents + 1) + k];
-    char* ws = static_cast<char*>(h->ws);
+    const uint64_t n_combos = binom_table()[n_events * (kMaxComboEvents + 1) + k];
     hipStream_t st = static_cast<hipStream_t>(stream);
-    hipError_t e = hipMemcpyAsync(ws, events, sizeof(double) * 11 * n_events, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(ws + kWsEvents, binom, kWsBinom, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(ws + kWsEvents + kWsBinom, init, kWsInit, hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return hip_fail(e, "kf_eval_combos: upload");
+    if (int rc = upload_combo_inputs(h, n_events, events, init, st, "kf_eval_combos: upload")) return rc;
+    char* ws = static_cast<char*>(h->ws);
     kfmi::Ref15ComboArgs a{};
     a.B = h->B;
     a.n_events = n_events;
@@ -508,8 +527,92 @@ int kf_eval_combos(kf_batch* h, int n_events, const double* events, const double
     a.logdets = logdets;
     a.max_logdet = max_logdet;
     a.n_records = n_records;
-    e = kfmi::launch_ref15_combos(h->dtype == KF_F64, a, st);
+    hipError_t e = kfmi::launch_ref15_combos(h->dtype == KF_F64, a, st);
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_eval_combos");
+}
+
+int kf_search_combos(kf_batch* h, int n_events, const double* events, const double* init, double prev_time,
+                     double target_end, double threshold, int k_max, int exhaustive, uint64_t* winner,
+                     int* k_found, uint64_t* n_accepted, void* subset_max, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (int rc = check_combo_inputs(h, n_events, events, init, "kf_search_combos")) return rc;
+    const int n = n_events;
+    if (k_max < 1 || k_max > n) return fail(KF_EINVAL, "kf_search_combos: k_max = %d outside [1, %d]", k_max, n);
+    if (!winner || !k_found) return fail(KF_EINVAL, "kf_search_combos: null winner/k_found");
+    if (subset_max && n > 30) return fail(KF_EINVAL, "kf_search_combos: subset_max needs n_events <= 30 (2^n entries)");
+    const uint64_t* binom = binom_table();
+    auto C = [&](int a, int b) { return binom[a * (kMaxComboEvents + 1) + b]; };
+    // Levels 1 .. k_max - 1 are stored, and of each only the subsets without event n - 1 (the
+    // others have no children): the colex ranks below C(n - 1, k).
+    uint64_t widest = 0;
+    for (int k = 1; k < k_max; ++k) widest = C(n - 1, k) > widest ? C(n - 1, k) : widest;
+    for (int k = 1; k <= k_max; ++k)
+        if (C(n - 1, k - 1) >= (1ull << 28))
+            return fail(KF_EINVAL, "kf_search_combos: level %d has C(%d, %d) = %llu parents (limit 2^28); lower k_max",
+                        k, n - 1, k - 1, static_cast<unsigned long long>(C(n - 1, k - 1)));
+    const int esz = static_cast<int>(elem(h));
+    const size_t head = 4096;  // best[65], n_acc[65]
+    const size_t level = widest ? static_cast<size_t>(kfmi::search_level_bytes(widest, esz)) : 0;
+    const size_t need = head + 2 * level;
+    if (h->search_ws_bytes < need) {
+        if (h->search_ws) (void)hipFree(h->search_ws);
+        h->search_ws = nullptr;
+        h->search_ws_bytes = 0;
+        if (hipMalloc(&h->search_ws, need) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(KF_ENOMEM, "kf_search_combos: hipMalloc of %zu bytes of level buffers failed", need);
+        }
+        h->search_ws_bytes = need;
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (int rc = upload_combo_inputs(h, n, events, init, st, "kf_search_combos: upload")) return rc;
+    char* ws = static_cast<char*>(h->ws);
+    char* sw = static_cast<char*>(h->search_ws);
+    uint64_t* d_best = reinterpret_cast<uint64_t*>(sw);
+    uint64_t* d_acc = d_best + (kMaxComboEvents + 1);
+    hipError_t e = hipMemsetAsync(sw, 0, head, st);
+    if (e != hipSuccess) return hip_fail(e, "kf_search_combos: clear");
+    char* lv[2] = {sw + head, sw + head + level};
+    uint64_t best[kMaxComboEvents + 1] = {}, acc[kMaxComboEvents + 1] = {};
+    int found = 0, last = 0;
+    for (int k = 1; k <= k_max; ++k) {
+        kfmi::Ref15SearchArgs a{};
+        a.n_events = n;
+        a.k = k;
+        a.n_par = k == 1 ? 1 : C(n - 1, k - 1);  // the parents with children
+        a.n_child = C(n, k);
+        a.ev = reinterpret_cast<const double*>(ws);
+        a.binom = reinterpret_cast<const uint64_t*>(ws + kWsEvents);
+        a.init = reinterpret_cast<const double*>(ws + kWsEvents + kWsBinom);
+        a.prev_time = prev_time;
+        a.target_end = target_end;
+        a.threshold = threshold;
+        a.par = k > 1 ? lv[(k - 1) & 1] : nullptr;
+        a.child = k < k_max ? lv[k & 1] : nullptr;
+        a.best = d_best;
+        a.n_acc = d_acc;
+        a.subset_max = subset_max;
+        e = kfmi::launch_ref15_search(h->dtype == KF_F64, a, st);
+        if (e != hipSuccess) return hip_fail(e, "kf_search_combos: level launch");
+        last = k;
+        if (!exhaustive) {  // the reference stops at the first size with an acceptable subset
+            e = hipMemcpyAsync(&best[k], &d_best[k], sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return hip_fail(e, "kf_search_combos: level result");
+            if (best[k]) break;
+        }
+    }
+    e = hipMemcpyAsync(best, d_best, sizeof best, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(acc, d_acc, sizeof acc, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(e, "kf_search_combos: results");
+    for (int k = 1; k <= last && !found; ++k)
+        if (best[k]) found = k;
+    *k_found = found;
+    *winner = found ? __builtin_bitreverse64(best[found]) : 0;
+    if (n_accepted)
+        for (int k = 0; k <= k_max; ++k) n_accepted[k] = k <= last ? acc[k] : 0;
+    return KF_OK;
 }
 
 int kf_score_candidates(kf_batch* h, int n_types, const int32_t* types, int full, void* gain, void* post,

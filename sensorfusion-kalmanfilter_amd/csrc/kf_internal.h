@@ -86,6 +86,37 @@ struct Ref15ComboArgs {
     int32_t* n_records;      // [B] or nullptr
 };
 
+// Brute-force search with shared prefixes (kf_search_combos): the filter of a k-subset S is its
+// parent's (S minus its largest event) advanced by one event, so level k is built from level
+// k - 1's stored states.  Levels are in colex order: the subsets whose largest event is j hold
+// ranks [C(j, k), C(j + 1, k)) and child rank = parent rank + C(j, k).  One lane per parent
+// evaluates all of its children.  Level buffer: node blocks of 64 nodes, block b =
+//   [43][64] T       x (15), block-packed P (27), running max log-det (NaN = failed filter)
+//   [64] double      time of the last applied event
+//   [64] uint64      subset bit mask
+struct Ref15SearchArgs {
+    int n_events;
+    int k;                   // child level (k >= 1; k = 1 reads the root from init)
+    uint64_t n_par;          // C(n, k - 1) parents, one lane each
+    uint64_t n_child;        // C(n, k)
+    const double* ev;        // device [n][11]: t, type, payload[9]
+    const uint64_t* binom;   // device [65][65]
+    const double* init;      // device [15 + 27]: root state (level 0)
+    double prev_time;        // root time
+    double target_end;
+    double threshold;        // acceptance: max log-det < threshold (kf_workers.py:1353)
+    const void* par;         // level k - 1 buffer (unused for k = 1)
+    void* child;             // level k buffer, or nullptr when level k is not stored
+    uint64_t* best;          // device [65]: per level, max over accepted subsets of bitrev(mask)
+    uint64_t* n_acc;         // device [65]: per level, number of accepted subsets
+    void* subset_max;        // device [2^n] T: every subset's max log-det by mask, or nullptr
+};
+
+__host__ __device__ constexpr uint64_t search_block_bytes(uint64_t elem) { return 64 * (43 * elem + 16); }
+__host__ __device__ inline uint64_t search_level_bytes(uint64_t nodes, uint64_t elem) {
+    return (nodes + 63) / 64 * search_block_bytes(elem);
+}
+
 // Scheduler scoring (kf_workers.py:112-185): trace of the posterior covariance each candidate
 // sensor would give, per filter.  full = 0: the reference's S = [1] (first measurement row
 // only); full = 1: every row of the sensor.
@@ -133,6 +164,7 @@ constexpr int kEventsLane = 0, kEventsChain = 1, kEventsLds = 2;
 hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, int variant);
 hipError_t launch_ref_reset(int model, bool f64, const RefArgs& a, hipStream_t stream);
 hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream);
+hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, hipStream_t stream);
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream);
 hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream);
 

@@ -789,6 +789,220 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
 }
 
 // ------------------------------------------------------------------------------------
+// Brute-force search with shared prefixes (kf_search_combos).  The worker runs every subset's
+// filter from the common start (kf_workers.py:29-71), so a k-subset repeats all of the work of
+// its (k-1)-prefix: over all subsets of n events that is ~n/2 + 1 event steps per subset.  Here
+// the filter of subset S = P + {j} (j > max P) is P's stored filter advanced by event j — the
+// same operations in the same order as the per-combination kernel, so the same numbers — and
+// each subset costs one event step plus the worker's final predict (:74-82).
+//
+// One lane per parent P (level k - 1, colex order).  Its children j = max P + 1 .. n - 1 are
+// visited in a wave-uniform loop: parents of a wave share max P except at run boundaries, so
+// event j is the same for every active lane (scalar loads, uniform GPS/IMU branch), and for a
+// fixed j the children of consecutive parents are consecutive ranks (coalesced stores).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const uint64_t o = __shfl_xor(v, s, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s, 64);
+    return v;
+}
+
+// Level buffers in node blocks of 64 (kf_internal.h): a wave's parents are one contiguous block.
+template <typename T>
+__device__ __forceinline__ char* level_block(const void* base, uint64_t c) {
+    return static_cast<char*>(const_cast<void*>(base)) + (c >> 6) * search_block_bytes(sizeof(T));
+}
+template <typename T>
+__device__ __forceinline__ T* level_row(char* blk, uint32_t lane, int r) {
+    return reinterpret_cast<T*>(blk + r * 64 * int(sizeof(T))) + lane;
+}
+template <typename T>
+__device__ __forceinline__ double* level_tail(char* blk, uint32_t lane, int q) {
+    return reinterpret_cast<double*>(blk + 43 * 64 * int(sizeof(T)) + q * 512) + lane;
+}
+
+// Chains<T, M15>::logdet() accumulated one block at a time, in its order (pva chains, then aw
+// chains) with its renormalisations, so the value is the same.
+template <typename T>
+struct LogdetAcc {
+    T num = T(1), den = T(1);
+    int ex = 0;
+    bool ok = true;
+    __device__ __forceinline__ void add_pva(const T (&P)[6], int c) {
+        det3_scaled<T>(P, num, den, ok);
+        if (sizeof(T) == 4 || c == M15::NP - 1) renorm(num, ex);
+    }
+    __device__ __forceinline__ void add_aw(const T (&P)[3]) {
+        det2<T>(P, num, ok);
+        if (sizeof(T) == 4) renorm(num, ex);
+    }
+    __device__ __forceinline__ T finish() {
+        T prod = num * rcp_nr<kRefNewton>(den);
+        renorm(prod, ex);
+        const T ld = log_mant(prod, ex);
+        return ok ? ld : quiet_nan<T>();
+    }
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void ref15_search_kernel(const Ref15SearchArgs a) {
+    const int64_t p = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (uint64_t(p) >= a.n_par) return;
+    using C15 = Chains<T, M15>;
+    const int n = a.n_events, k = a.k;
+    // the parent (the root for k = 1, else node p of level k - 1) stays in registers
+    T px[15], pP[27];
+    T run;
+    double prev;
+    uint64_t mask;
+    if (k == 1) {
+        Ref15<T> r;
+#pragma unroll
+        for (int i = 0; i < 15; ++i) r.x[i] = T(a.init[i]);
+#pragma unroll
+        for (int i = 0; i < 27; ++i) r.blk(i) = T(a.init[15 + i]);
+        run = r.logdet();  // record 0: logdet of the initial covariance (kf_workers.py:32)
+#pragma unroll
+        for (int i = 0; i < 15; ++i) px[i] = r.x[i];
+#pragma unroll
+        for (int i = 0; i < 27; ++i) pP[i] = r.blk(i);
+        prev = a.prev_time;
+        mask = 0;
+    } else {
+        char* blk = level_block<T>(a.par, uint64_t(p));
+        const uint32_t lane = uint32_t(p) & 63u;
+#pragma unroll
+        for (int i = 0; i < 15; ++i) px[i] = *level_row<T>(blk, lane, i);
+#pragma unroll
+        for (int i = 0; i < 27; ++i) pP[i] = *level_row<T>(blk, lane, 15 + i);
+        run = *level_row<T>(blk, lane, 42);
+        prev = *level_tail<T>(blk, lane, 0);
+        mask = __builtin_bit_cast(uint64_t, *level_tail<T>(blk, lane, 1));
+    }
+    const int m = mask ? 63 - __builtin_clzll(mask) : -1;
+    // colex order: max P is non-decreasing over the wave, so the first lane holds the smallest
+    const int j0 = wave_uniform(m) + 1;
+    const T qpva[3] = {T(kQPos), T(kQVel), T(kQAcc)};
+    const T qaw[2] = {T(kQAtt), T(kQRate)};
+    const T Rg[1] = {T(kRGps)};
+    const T Rp[6] = {T(kRPos), T(0), T(0), T(kRVel), T(0), T(kRAcc)};
+    const T Ra[3] = {T(kRAtt), T(0), T(kRRate)};
+    const T thr = T(a.threshold);
+    uint64_t best = 0, cnt = 0;
+    for (int j = j0; j < n; ++j) {
+        if (j <= m) continue;
+        const double* e = a.ev + j * 11;  // wave-uniform: scalar loads, uniform GPS/IMU branch
+        const int type = int(e[1]);
+        const uint64_t c = uint64_t(p) + a.binom[j * (kMaxEvents + 1) + k];  // child colex rank
+        const uint64_t cmask = mask | (uint64_t(1) << j);
+        const double dtd = e[0] - prev;
+        const bool step = dtd >= 0.0;  // kf_workers.py:38-40: a negative dt is skipped, time unchanged
+        const T dt = T(dtd);
+        const double cprev = step ? e[0] : prev;
+        const bool final_predict = cprev < a.target_end - 1e-8;  // kf_workers.py:74-82
+        const T dte = T(a.target_end - cprev);
+        char* cb = (a.child && j < n - 1) ? level_block<T>(a.child, c) : nullptr;  // a subset holding event n-1 has no children
+        const uint32_t cl = uint32_t(c) & 63u;
+        // Chains::event chain by chain (every chain's predict and update touch only that chain),
+        // then the chain's share of the record's log-det and of the final predict's
+        LogdetAcc<T> rec, fin;
+        bool ok = true;
+#pragma unroll
+        for (int ch = 0; ch < M15::NP; ++ch) {
+            T xb[3], Pb[6];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) xb[i] = px[M15::pva(ch, i)];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) Pb[i] = pP[6 * ch + i];
+            if (step) {
+                C15::template chain_predict<3>(xb, Pb, dt, qpva);
+                if (type == kGps) {
+                    const T zb[1] = {T(e[2 + ch])};
+                    ok = sel_update<3, 1, true, T, kRefNewton, true>(xb, Pb, zb, Rg) && ok;
+                } else {
+                    const T acc = T(e[2 + M15::imu_acc(ch)]);
+                    const T V = fmaT(acc, dt, xb[1]);
+                    const T X = fmaT(V, dt, xb[0]);
+                    const T zb[3] = {X, V, acc};
+                    ok = sel_update<3, 3, true, T, kRefNewton, true>(xb, Pb, zb, Rp) && ok;
+                }
+            }
+            if (cb) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, M15::pva(ch, i)) = xb[i];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) *level_row<T>(cb, cl, 15 + 6 * ch + i) = Pb[i];
+            }
+            rec.add_pva(Pb, ch);
+            if (final_predict) C15::template chain_predict<3>(xb, Pb, dte, qpva);
+            fin.add_pva(Pb, ch);
+        }
+#pragma unroll
+        for (int ch = 0; ch < M15::NA; ++ch) {
+            T xa[2], Pa[3];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) xa[i] = px[M15::aw(ch, i)];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) Pa[i] = pP[6 * M15::NP + 3 * ch + i];
+            if (step) {
+                C15::template chain_predict<2>(xa, Pa, dt, qaw);
+                if (type != kGps) {  // a GPS fix updates the pva chains only
+                    const T za[2] = {T(e[2 + M15::imu_att(ch)]), T(e[2 + M15::imu_rate(ch)])};
+                    ok = sel_update<2, 2, true, T, kRefNewton, true>(xa, Pa, za, Ra) && ok;
+                }
+            }
+            if (cb) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) *level_row<T>(cb, cl, M15::aw(ch, i)) = xa[i];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, 15 + 6 * M15::NP + 3 * ch + i) = Pa[i];
+            }
+            rec.add_aw(Pa);
+            if (final_predict) C15::template chain_predict<2>(xa, Pa, dte, qaw);
+            fin.add_aw(Pa);
+        }
+        T crun = run;
+        if (step) {
+            const T ld = rec.finish();
+            crun = ld > run ? ld : run;
+            crun = ok ? crun : quiet_nan<T>();  // a failed filter (kf_eval_combos: KF_ENOTSPD)
+        }
+        T fmax = crun;
+        if (final_predict) {
+            const T ld = fin.finish();
+            fmax = ld > crun ? ld : crun;
+        }
+        if (cb) {
+            *level_row<T>(cb, cl, 42) = crun;
+            *level_tail<T>(cb, cl, 0) = cprev;
+            *level_tail<T>(cb, cl, 1) = __builtin_bit_cast(double, cmask);
+        }
+        if (a.subset_max) static_cast<T*>(a.subset_max)[cmask] = fmax;
+        if (fmax < thr) {  // max(log_det) < R_threshold (kf_workers.py:1353); NaN never passes
+            const uint64_t key = __builtin_bitreverse64(cmask);  // larger key = earlier in itertools order
+            best = key > best ? key : best;
+            ++cnt;
+        }
+    }
+    if (__builtin_amdgcn_ballot_w64(cnt != 0) != 0) {  // wave-uniform
+        best = wave_max_u64(best);
+        cnt = wave_sum_u64(cnt);
+        if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0) {
+            atomicMax(reinterpret_cast<unsigned long long*>(&a.best[k]), static_cast<unsigned long long>(best));
+            atomicAdd(reinterpret_cast<unsigned long long*>(&a.n_acc[k]), static_cast<unsigned long long>(cnt));
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Scheduler scoring and the rate-decimated greedy driver (kf_workers.py:99-213, 826-957).
 // ------------------------------------------------------------------------------------
 template <typename T>
@@ -1023,6 +1237,17 @@ hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t st
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
     if (f64) ref15_combo_kernel<double><<<grid, kBlock, 0, stream>>>(a);
     else ref15_combo_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, hipStream_t stream) {
+    // node offsets are 32-bit byte offsets (buffer voffset)
+    if (a.n_events > kMaxEvents || a.k < 1 || a.k > a.n_events || a.n_par == 0 || a.n_par >= (1ull << 28) ||
+        a.n_child >= (1ull << 28))
+        return hipErrorInvalidValue;
+    const dim3 grid(static_cast<unsigned>((a.n_par + kBlock - 1) / kBlock));
+    if (f64) ref15_search_kernel<double><<<grid, kBlock, 0, stream>>>(a);
+    else ref15_search_kernel<float><<<grid, kBlock, 0, stream>>>(a);
     return hipGetLastError();
 }
 

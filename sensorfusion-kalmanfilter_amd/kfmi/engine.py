@@ -294,6 +294,35 @@ class BatchedKF:
         torch.cuda.current_stream(self.device).synchronize()  # host arrays were staged; keep them alive
         return mx, ld, nr
 
+    def search_combos(self, events, init, prev_time, target_end, threshold, k_max=None, exhaustive=False,
+                      subset_max=False):
+        """KF_MODEL_REF15 brute-force search with shared prefixes (kf_search_combos): sizes
+        k = 1 .. k_max of the n candidate events, each subset's filter advanced from its prefix's
+        by one event.  Stops after the first size with a subset whose max log-det is below
+        threshold unless ``exhaustive``.  Returns (k_found, winner indices tuple or None,
+        accepted count per size [k_max + 1], subset_max [2^n] or None)."""
+        if self.model != 'ref15':
+            raise ValueError('search_combos needs a ref15 handle')
+        ev = np.ascontiguousarray(events, dtype=np.float64)
+        ini = np.ascontiguousarray(init, dtype=np.float64)
+        if ev.ndim != 2 or ev.shape[1] != 11 or ini.shape != (42,):
+            raise ValueError('events must be [n, 11] and init [42]')
+        n = ev.shape[0]
+        k_max = n if k_max is None else int(k_max)
+        win = ctypes.c_uint64(0)
+        kf = ctypes.c_int(0)
+        acc = np.zeros(max(k_max, 0) + 1, dtype=np.uint64)
+        sm = self.empty(1 << n) if subset_max else None
+        if sm is not None:
+            sm.fill_(float('nan'))
+        check(_lib.lib().kf_search_combos(self.handle, n, ev.ctypes.data_as(ctypes.c_void_p),
+                                          ini.ctypes.data_as(ctypes.c_void_p), float(prev_time), float(target_end),
+                                          float(threshold), k_max, int(bool(exhaustive)), ctypes.byref(win),
+                                          ctypes.byref(kf), acc.ctypes.data_as(ctypes.c_void_p), _ptr(sm),
+                                          self._stream()))
+        combo = tuple(i for i in range(n) if (win.value >> i) & 1) if kf.value else None
+        return kf.value, combo, acc, sm
+
     def score_candidates(self, types, full=False, posterior=False):
         """KF_MODEL_REF15 scheduler scoring (kf_score_candidates): [len(types), B] traces of the
         posterior covariance each candidate sensor would give (full=False: the reference's

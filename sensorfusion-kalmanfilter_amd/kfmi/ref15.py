@@ -458,22 +458,50 @@ def first_valid_rank(kf, ev, init, prev_time, target_end, k, lo, hi, threshold):
     return None
 
 
-def brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype='f64', device=0):
-    """The reference's result dict (kf_workers.py:1358-1367) for combination rank r of size k."""
-    combo = tuple(cand[i] for i in unrank_combination(len(cand), k, r))
+def brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype='f64', device=0, indices=None):
+    """The reference's result dict (kf_workers.py:1358-1367) for combination rank r of size k
+    (or the candidate ``indices`` of the subset)."""
+    idx = unrank_combination(len(cand), k, r) if indices is None else indices
+    combo = tuple(cand[i] for i in idx)
     metric, traj, combo, x_bf, P_bf, log_det, used = evaluate_combo_chunk([combo], xt, Pt, prev_time, target_end,
                                                                           dtype, device)[0]
     return {'selected_sensors': combo, 'final_state': x_bf, 'final_covariance': P_bf, 'trajectory': traj,
             'accuracy_metric': metric, 'log_determinants': log_det, 'num_measurements_used': used}
 
 
+def search_level_bytes(nodes, dtype):
+    """Device bytes of one kf_search_combos level buffer (node blocks of 64, kf_internal.h)."""
+    w = 8 if dtype == 'f64' else 4
+    return (nodes + 63) // 64 * 64 * (43 * w + 16)
+
+
+def search_levels(n, dtype='f64', mem_bytes=32 << 30):
+    """Largest k_max for which kf_search_combos' level buffers (two of the widest stored level:
+    the C(n - 1, k) subsets of size k < k_max without the last candidate) fit in ``mem_bytes``
+    and every level stays below 2^28 parents."""
+    k_max, widest = 0, 0
+    for k in range(1, n + 1):
+        if math.comb(n - 1, k - 1) >= 1 << 28:
+            break
+        if k > 1:
+            widest = max(widest, math.comb(n - 1, k - 1))
+        if 2 * search_level_bytes(widest, dtype) + 4096 > mem_bytes:
+            break
+        k_max = k
+    return k_max
+
+
 def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end_idx=None, R_threshold=None,
                                                        initial_pt=None, initial_state=None,
-                                                       max_combos_in_memory=1 << 22, dtype='f64', device=0):
+                                                       max_combos_in_memory=1 << 22, dtype='f64', device=0,
+                                                       search_mem_bytes=32 << 30):
     """kf_workers.py:1218-1392 on the GPU: for k = 1..n, evaluate every k-subset of the candidate
-    events (kf_eval_combos, one filter per subset, up to ``max_combos_in_memory`` per launch) and
-    return the first subset, in itertools.combinations order, whose max log-determinant is below
-    R_threshold — the reference's result dict — or None.  Multi-GPU: kfmi.dist.brute_force_search."""
+    events and return the first subset, in itertools.combinations order, whose max
+    log-determinant is below R_threshold — the reference's result dict — or None.  Sizes whose
+    prefix levels fit in ``search_mem_bytes`` run as one shared-prefix search
+    (kf_search_combos: one event step per subset); larger sizes evaluate one filter per subset
+    (kf_eval_combos, up to ``max_combos_in_memory`` per launch).  Multi-GPU:
+    kfmi.dist.brute_force_search."""
     if R_threshold is None:
         raise ValueError('R_threshold must be specified for brute force KF.')
     st = brute_force_setup(events, start_idx, end_idx, initial_pt, initial_state)
@@ -481,10 +509,23 @@ def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end
         return None
     cand, xt, Pt, prev_time, target_end, ev, init = st
     n = len(cand)
-    width = int(min(max_combos_in_memory, max(math.comb(n, k) for k in range(1, n + 1))))
+    # sizes 1 .. k_search by the shared-prefix search (kf_search_combos), the rest (if its level
+    # buffers would not fit) one filter per subset (kf_eval_combos)
+    k_search = search_levels(n, dtype, search_mem_bytes)
+    if k_search:
+        kf = BatchedKF('ref15', 1, dtype, device=device)
+        try:
+            k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=k_search)
+        finally:
+            kf.close()
+        if k:
+            return brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device, indices=idx)
+        if k_search == n:
+            return None
+    width = int(min(max_combos_in_memory, max(math.comb(n, k) for k in range(k_search + 1, n + 1))))
     kf = BatchedKF('ref15', width, dtype, device=device)
     try:
-        for k in range(1, n + 1):
+        for k in range(k_search + 1, n + 1):
             r = first_valid_rank(kf, ev, init, prev_time, target_end, k, 0, math.comb(n, k), R_threshold)
             if r is not None:
                 return brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype, device)

@@ -78,13 +78,16 @@ def test_combo_chunk_worker(golden_dir):
     assert all(r[0] == 0 and r[4] is None and r[6] == len(r[2]) for r in res)
 
 
-def test_brute_force_search(golden_dir):
+@pytest.mark.parametrize('mem', [32 << 30, 0, 200_000])
+def test_brute_force_search(golden_dir, mem):
+    """The reference's search result; mem = level-buffer budget of the shared-prefix search (0:
+    every size one filter per subset; 200 kB: the first sizes by the search, the rest per subset)."""
     g = _load(golden_dir, 'ref15_bruteforce.npz')
     events = unpack_events(g)
     s, e = int(g['start']), int(g['end'])
     out = ref15.run_brute_force_kalman_filter_no_sampling_min_usage(
         events, s, e, R_threshold=float(g['threshold']), initial_pt=g['init_P'],
-        initial_state=tuple(g['init_state']))
+        initial_state=tuple(g['init_state']), search_mem_bytes=mem)
     cand = events[s:e]
     assert [cand.index(ev) for ev in out['selected_sensors']] == list(g['selected'])
     assert out['num_measurements_used'] == len(g['selected'])
@@ -93,7 +96,107 @@ def test_brute_force_search(golden_dir):
     assert _rel(out['trajectory'], g['trajectory']) <= TOL
     # a threshold no subset meets -> None (kf_workers.py:1391-1392)
     assert ref15.run_brute_force_kalman_filter_no_sampling_min_usage(
-        events, s, e, R_threshold=-1e9, initial_pt=g['init_P'], initial_state=tuple(g['init_state'])) is None
+        events, s, e, R_threshold=-1e9, initial_pt=g['init_P'], initial_state=tuple(g['init_state']),
+        search_mem_bytes=mem) is None
+
+
+def _search_case(golden_dir, n, swap=True):
+    """n candidates after a warm start on the golden log; with ``swap`` two candidates are
+    out of time order, so some subsets meet a negative dt (skipped, kf_workers.py:38-40)."""
+    g = _load(golden_dir, 'ref15_full.npz')
+    events = unpack_events(g)
+    s0 = 100
+    st, ld, P, prev = ref_kf.run_kalman_filter_full(events, 0, s0)
+    cand = list(events[s0:s0 + n])
+    if swap:
+        cand[3], cand[6] = cand[6], cand[3]
+    xt = np.zeros(15)
+    xt[0:6] = st[-1][1:7]
+    target = max(c[2] for c in cand)
+    ev = np.array([[t, 0 if s == 'GPS' else 1, *ref15.event_payload(s, d)] for (_, s, t, d) in cand])
+    init = np.concatenate([xt, ref15.to_blocks(P)])
+    return cand, ev, init, st[-1][0], target
+
+
+@pytest.mark.parametrize('dtype', ['f64', 'f32'])
+def test_search_subset_max_equals_eval_combos(golden_dir, dtype):
+    """kf_search_combos (one event step per subset, from the stored prefix) gives every subset the
+    max log-det the per-subset kernel gives (same operations in the same order)."""
+    n = 12
+    cand, ev, init, t0, target = _search_case(golden_dir, n)
+    kf = kfmi.BatchedKF('ref15', 1, dtype)
+    kfound, win, acc, sm = kf.search_combos(ev, init, t0, target, threshold=-1e30, exhaustive=True, subset_max=True)
+    kf.close()
+    assert kfound == 0 and win is None and int(acc.sum()) == 0
+    sm = sm.double().cpu().numpy()
+    assert np.isnan(sm[0])  # the empty subset is not evaluated
+    worst, exact, total = 0.0, 0, 0
+    for k in range(1, n + 1):
+        combos = list(combinations(range(n), k))
+        kc = kfmi.BatchedKF('ref15', len(combos), dtype)
+        mx, _, _ = kc.eval_combos(ev, init, t0, target, k, logdets=False)
+        mx = mx.double().cpu().numpy()
+        kc.close()
+        masks = np.array([sum(1 << i for i in c) for c in combos])
+        got = sm[masks]
+        assert np.isfinite(got).all() and np.isfinite(mx).all()
+        worst = max(worst, float(np.max(np.abs(got - mx) / np.maximum(np.abs(mx), 1.0))))
+        exact += int((got == mx).sum())
+        total += len(combos)
+    assert total == 2 ** n - 1
+    assert worst <= (1e-12 if dtype == 'f64' else 1e-6), (worst, exact, total)
+
+
+@pytest.mark.parametrize('q', [0.0, 0.01, 0.3, 0.9])
+def test_search_winner_matches_per_subset_search(golden_dir, q):
+    """The search's winner and per-size accepted counts at thresholds across the distribution of
+    subset scores equal the per-subset kernel's (first acceptable subset in itertools order of
+    the smallest size)."""
+    n = 11
+    cand, ev, init, t0, target = _search_case(golden_dir, n)
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    _, _, _, sm = kf.search_combos(ev, init, t0, target, threshold=-1e30, exhaustive=True, subset_max=True)
+    vals = np.sort(sm.cpu().numpy()[1:])
+    thr = float(vals[int(q * (len(vals) - 1))]) + (1e-9 if q > 0 else -1.0)
+    kfound, win, acc, _ = kf.search_combos(ev, init, t0, target, thr, exhaustive=True)
+    k1, win1, _, _ = kf.search_combos(ev, init, t0, target, thr, exhaustive=False)
+    kf.close()
+    assert (k1, win1) == (kfound, win)
+    want_k, want_combo = 0, None
+    for k in range(1, n + 1):
+        combos = list(combinations(range(n), k))
+        kc = kfmi.BatchedKF('ref15', len(combos), 'f64')
+        mx, _, _ = kc.eval_combos(ev, init, t0, target, k, logdets=False)
+        ok = (mx < thr).cpu().numpy()
+        kc.close()
+        assert int(acc[k]) == int(ok.sum()), k
+        if want_k == 0 and ok.any():
+            want_k, want_combo = k, combos[int(np.argmax(ok))]
+    assert (kfound, win) == (want_k, want_combo)
+    if q == 0.0:
+        assert kfound == 0
+
+
+def test_search_combos_rejects_bad_arguments():
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    ev = np.zeros((4, 11))
+    ev[:, 0] = np.arange(4)
+    init = np.zeros(42)
+    with pytest.raises(kfmi.KFError):
+        kf.search_combos(ev, init, 0.0, 4.0, 0.0, k_max=5)
+    bad = ev.copy()
+    bad[1, 1] = 7
+    with pytest.raises(kfmi.KFError):
+        kf.search_combos(bad, init, 0.0, 4.0, 0.0)
+    big = np.tile(ev, (17, 1))  # 68 candidates: more than the 64-bit subset masks hold
+    big[:, 0] = np.arange(len(big))
+    with pytest.raises(kfmi.KFError):
+        kf.search_combos(big, init, 0.0, 68.0, 0.0, k_max=1)
+    kf.close()
+    cv = kfmi.BatchedKF('cv3', 4, 'f64')
+    with pytest.raises(ValueError):
+        cv.search_combos(ev, init, 0.0, 4.0, 0.0)
+    cv.close()
 
 
 @pytest.mark.parametrize('n,k', [(10, 1), (10, 4), (12, 6)])
