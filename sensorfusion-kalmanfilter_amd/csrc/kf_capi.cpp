@@ -61,6 +61,8 @@ constexpr int64_t kChainMaxFilters = 16384;
 constexpr size_t kWsEvents = sizeof(double) * kMaxComboEvents * 11;
 constexpr size_t kWsBinom = sizeof(uint64_t) * (kMaxComboEvents + 1) * (kMaxComboEvents + 1);
 constexpr size_t kWsInit = sizeof(double) * 42;
+// levels with at most this many parents run child-major (see search_child_major)
+constexpr uint64_t kSearchChildMajorParents = 200000;
 
 bool is_ref15(const kf_batch* h) { return h->model == KF_MODEL_REF15; }
 
@@ -88,6 +90,18 @@ int upload_combo_inputs(kf_batch* h, int n_events, const double* events, const d
     if (e == hipSuccess) e = hipMemcpyAsync(ws + kWsEvents, binom_table(), kWsBinom, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(ws + kWsEvents + kWsBinom, init, kWsInit, hipMemcpyHostToDevice, st);
     return e == hipSuccess ? KF_OK : hip_fail(e, what);
+}
+
+// kf_search_combos kernel per level: child-major (one wave per parent block and child event)
+// for the narrow levels, where one lane per parent would walk up to n - 1 children in sequence;
+// parent-major (one lane per parent, its children in a wave-uniform loop) for the wide ones,
+// where it reads each parent once and keeps it in registers (interleaved A/B:
+// profiles/r01_ab/search_kernels_ab.txt).  KFMI_SEARCH_KERNEL=cm|pm forces one.
+bool search_child_major(uint64_t n_par) {
+    const char* v = std::getenv("KFMI_SEARCH_KERNEL");
+    if (v && !std::strcmp(v, "cm")) return true;
+    if (v && !std::strcmp(v, "pm")) return false;
+    return n_par <= kSearchChildMajorParents;
 }
 
 int check_combo_inputs(const kf_batch* h, int n_events, const double* events, const double* init, const char* what) {
@@ -583,6 +597,7 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.n_child = C(n, k);
         a.ev = reinterpret_cast<const double*>(ws);
         a.binom = reinterpret_cast<const uint64_t*>(ws + kWsEvents);
+        a.binom_host = binom;
         a.init = reinterpret_cast<const double*>(ws + kWsEvents + kWsBinom);
         a.prev_time = prev_time;
         a.target_end = target_end;
@@ -592,7 +607,7 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.best = d_best;
         a.n_acc = d_acc;
         a.subset_max = subset_max;
-        e = kfmi::launch_ref15_search(h->dtype == KF_F64, a, st);
+        e = kfmi::launch_ref15_search(h->dtype == KF_F64, a, search_child_major(a.n_par), st);
         if (e != hipSuccess) return hip_fail(e, "kf_search_combos: level launch");
         last = k;
         if (!exhaustive) {  // the reference stops at the first size with an acceptable subset

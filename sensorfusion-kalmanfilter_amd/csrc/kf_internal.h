@@ -101,6 +101,7 @@ struct Ref15SearchArgs {
     uint64_t n_child;        // C(n, k)
     const double* ev;        // device [n][11]: t, type, payload[9]
     const uint64_t* binom;   // device [65][65]
+    const uint64_t* binom_host;  // host copy (launch geometry)
     const double* init;      // device [15 + 27]: root state (level 0)
     double prev_time;        // root time
     double target_end;
@@ -164,7 +165,8 @@ constexpr int kEventsLane = 0, kEventsChain = 1, kEventsLds = 2;
 hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, int variant);
 hipError_t launch_ref_reset(int model, bool f64, const RefArgs& a, hipStream_t stream);
 hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream);
-hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, hipStream_t stream);
+// child_major: one wave per (parent block, child event) instead of one lane per parent
+hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream);
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream);
 hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream);
 

@@ -852,146 +852,153 @@ struct LogdetAcc {
     }
 };
 
+// A stored node of the search: the filter after a subset's events, its running max log-det,
+// the time of its last applied event and its subset mask.
 template <typename T>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void ref15_search_kernel(const Ref15SearchArgs a) {
-    const int64_t p = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (uint64_t(p) >= a.n_par) return;
-    using C15 = Chains<T, M15>;
-    const int n = a.n_events, k = a.k;
-    // the parent (the root for k = 1, else node p of level k - 1) stays in registers
-    T px[15], pP[27];
+struct SearchNode {
+    T x[15], P[27];
     T run;
     double prev;
     uint64_t mask;
-    if (k == 1) {
+
+    // the root (the empty subset): record 0 is the logdet of the initial covariance (kf_workers.py:32)
+    __device__ __forceinline__ void root(const Ref15SearchArgs& a) {
         Ref15<T> r;
 #pragma unroll
         for (int i = 0; i < 15; ++i) r.x[i] = T(a.init[i]);
 #pragma unroll
         for (int i = 0; i < 27; ++i) r.blk(i) = T(a.init[15 + i]);
-        run = r.logdet();  // record 0: logdet of the initial covariance (kf_workers.py:32)
+        run = r.logdet();
 #pragma unroll
-        for (int i = 0; i < 15; ++i) px[i] = r.x[i];
+        for (int i = 0; i < 15; ++i) x[i] = r.x[i];
 #pragma unroll
-        for (int i = 0; i < 27; ++i) pP[i] = r.blk(i);
+        for (int i = 0; i < 27; ++i) P[i] = r.blk(i);
         prev = a.prev_time;
         mask = 0;
-    } else {
-        char* blk = level_block<T>(a.par, uint64_t(p));
+    }
+    __device__ __forceinline__ void load(const void* level, uint64_t p) {
+        char* blk = level_block<T>(level, p);
         const uint32_t lane = uint32_t(p) & 63u;
 #pragma unroll
-        for (int i = 0; i < 15; ++i) px[i] = *level_row<T>(blk, lane, i);
+        for (int i = 0; i < 15; ++i) x[i] = *level_row<T>(blk, lane, i);
 #pragma unroll
-        for (int i = 0; i < 27; ++i) pP[i] = *level_row<T>(blk, lane, 15 + i);
+        for (int i = 0; i < 27; ++i) P[i] = *level_row<T>(blk, lane, 15 + i);
         run = *level_row<T>(blk, lane, 42);
         prev = *level_tail<T>(blk, lane, 0);
         mask = __builtin_bit_cast(uint64_t, *level_tail<T>(blk, lane, 1));
     }
-    const int m = mask ? 63 - __builtin_clzll(mask) : -1;
-    // colex order: max P is non-decreasing over the wave, so the first lane holds the smallest
-    const int j0 = wave_uniform(m) + 1;
+    __device__ __forceinline__ int max_event() const { return mask ? 63 - __builtin_clzll(mask) : -1; }
+};
+
+// Child j (> the parent's largest event) of node `par`, colex rank c at level a.k: its filter
+// (stored when a.child is set and the child has children), its max log-det with the worker's
+// final predict, and the acceptance test folded into (best, cnt).  Chains::event runs chain by
+// chain (each chain's predict and update touch only that chain); the record's log-det and the
+// final predict's are accumulated in Chains::logdet's block order, so the numbers are
+// kf_eval_combos's.
+template <typename T>
+__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const SearchNode<T>& par, int j, uint64_t c,
+                                             uint64_t& best, uint64_t& cnt) {
+    using C15 = Chains<T, M15>;
     const T qpva[3] = {T(kQPos), T(kQVel), T(kQAcc)};
     const T qaw[2] = {T(kQAtt), T(kQRate)};
     const T Rg[1] = {T(kRGps)};
     const T Rp[6] = {T(kRPos), T(0), T(0), T(kRVel), T(0), T(kRAcc)};
     const T Ra[3] = {T(kRAtt), T(0), T(kRRate)};
-    const T thr = T(a.threshold);
-    uint64_t best = 0, cnt = 0;
-    for (int j = j0; j < n; ++j) {
-        if (j <= m) continue;
-        const double* e = a.ev + j * 11;  // wave-uniform: scalar loads, uniform GPS/IMU branch
-        const int type = int(e[1]);
-        const uint64_t c = uint64_t(p) + a.binom[j * (kMaxEvents + 1) + k];  // child colex rank
-        const uint64_t cmask = mask | (uint64_t(1) << j);
-        const double dtd = e[0] - prev;
-        const bool step = dtd >= 0.0;  // kf_workers.py:38-40: a negative dt is skipped, time unchanged
-        const T dt = T(dtd);
-        const double cprev = step ? e[0] : prev;
-        const bool final_predict = cprev < a.target_end - 1e-8;  // kf_workers.py:74-82
-        const T dte = T(a.target_end - cprev);
-        char* cb = (a.child && j < n - 1) ? level_block<T>(a.child, c) : nullptr;  // a subset holding event n-1 has no children
-        const uint32_t cl = uint32_t(c) & 63u;
-        // Chains::event chain by chain (every chain's predict and update touch only that chain),
-        // then the chain's share of the record's log-det and of the final predict's
-        LogdetAcc<T> rec, fin;
-        bool ok = true;
+    const double* e = a.ev + j * 11;
+    const int type = int(e[1]);
+    const uint64_t cmask = par.mask | (uint64_t(1) << j);
+    const double dtd = e[0] - par.prev;
+    const bool step = dtd >= 0.0;  // kf_workers.py:38-40: a negative dt is skipped, time unchanged
+    const T dt = T(dtd);
+    const double cprev = step ? e[0] : par.prev;
+    const bool final_predict = cprev < a.target_end - 1e-8;  // kf_workers.py:74-82
+    const T dte = T(a.target_end - cprev);
+    // a subset holding event n - 1 has no children and is not stored
+    char* cb = (a.child && j < a.n_events - 1) ? level_block<T>(a.child, c) : nullptr;
+    const uint32_t cl = uint32_t(c) & 63u;
+    LogdetAcc<T> rec, fin;
+    bool ok = true;
 #pragma unroll
-        for (int ch = 0; ch < M15::NP; ++ch) {
-            T xb[3], Pb[6];
+    for (int ch = 0; ch < M15::NP; ++ch) {
+        T xb[3], Pb[6];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) xb[i] = px[M15::pva(ch, i)];
+        for (int i = 0; i < 3; ++i) xb[i] = par.x[M15::pva(ch, i)];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) Pb[i] = pP[6 * ch + i];
-            if (step) {
-                C15::template chain_predict<3>(xb, Pb, dt, qpva);
-                if (type == kGps) {
-                    const T zb[1] = {T(e[2 + ch])};
-                    ok = sel_update<3, 1, true, T, kRefNewton, true>(xb, Pb, zb, Rg) && ok;
-                } else {
-                    const T acc = T(e[2 + M15::imu_acc(ch)]);
-                    const T V = fmaT(acc, dt, xb[1]);
-                    const T X = fmaT(V, dt, xb[0]);
-                    const T zb[3] = {X, V, acc};
-                    ok = sel_update<3, 3, true, T, kRefNewton, true>(xb, Pb, zb, Rp) && ok;
-                }
-            }
-            if (cb) {
-#pragma unroll
-                for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, M15::pva(ch, i)) = xb[i];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) *level_row<T>(cb, cl, 15 + 6 * ch + i) = Pb[i];
-            }
-            rec.add_pva(Pb, ch);
-            if (final_predict) C15::template chain_predict<3>(xb, Pb, dte, qpva);
-            fin.add_pva(Pb, ch);
-        }
-#pragma unroll
-        for (int ch = 0; ch < M15::NA; ++ch) {
-            T xa[2], Pa[3];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) xa[i] = px[M15::aw(ch, i)];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) Pa[i] = pP[6 * M15::NP + 3 * ch + i];
-            if (step) {
-                C15::template chain_predict<2>(xa, Pa, dt, qaw);
-                if (type != kGps) {  // a GPS fix updates the pva chains only
-                    const T za[2] = {T(e[2 + M15::imu_att(ch)]), T(e[2 + M15::imu_rate(ch)])};
-                    ok = sel_update<2, 2, true, T, kRefNewton, true>(xa, Pa, za, Ra) && ok;
-                }
-            }
-            if (cb) {
-#pragma unroll
-                for (int i = 0; i < 2; ++i) *level_row<T>(cb, cl, M15::aw(ch, i)) = xa[i];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, 15 + 6 * M15::NP + 3 * ch + i) = Pa[i];
-            }
-            rec.add_aw(Pa);
-            if (final_predict) C15::template chain_predict<2>(xa, Pa, dte, qaw);
-            fin.add_aw(Pa);
-        }
-        T crun = run;
+        for (int i = 0; i < 6; ++i) Pb[i] = par.P[6 * ch + i];
         if (step) {
-            const T ld = rec.finish();
-            crun = ld > run ? ld : run;
-            crun = ok ? crun : quiet_nan<T>();  // a failed filter (kf_eval_combos: KF_ENOTSPD)
-        }
-        T fmax = crun;
-        if (final_predict) {
-            const T ld = fin.finish();
-            fmax = ld > crun ? ld : crun;
+            C15::template chain_predict<3>(xb, Pb, dt, qpva);
+            if (type == kGps) {
+                const T zb[1] = {T(e[2 + ch])};
+                ok = sel_update<3, 1, true, T, kRefNewton, true>(xb, Pb, zb, Rg) && ok;
+            } else {
+                const T acc = T(e[2 + M15::imu_acc(ch)]);
+                const T V = fmaT(acc, dt, xb[1]);
+                const T X = fmaT(V, dt, xb[0]);
+                const T zb[3] = {X, V, acc};
+                ok = sel_update<3, 3, true, T, kRefNewton, true>(xb, Pb, zb, Rp) && ok;
+            }
         }
         if (cb) {
-            *level_row<T>(cb, cl, 42) = crun;
-            *level_tail<T>(cb, cl, 0) = cprev;
-            *level_tail<T>(cb, cl, 1) = __builtin_bit_cast(double, cmask);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, M15::pva(ch, i)) = xb[i];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) *level_row<T>(cb, cl, 15 + 6 * ch + i) = Pb[i];
         }
-        if (a.subset_max) static_cast<T*>(a.subset_max)[cmask] = fmax;
-        if (fmax < thr) {  // max(log_det) < R_threshold (kf_workers.py:1353); NaN never passes
-            const uint64_t key = __builtin_bitreverse64(cmask);  // larger key = earlier in itertools order
-            best = key > best ? key : best;
-            ++cnt;
-        }
+        rec.add_pva(Pb, ch);
+        if (final_predict) C15::template chain_predict<3>(xb, Pb, dte, qpva);
+        fin.add_pva(Pb, ch);
     }
+#pragma unroll
+    for (int ch = 0; ch < M15::NA; ++ch) {
+        T xa[2], Pa[3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) xa[i] = par.x[M15::aw(ch, i)];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Pa[i] = par.P[6 * M15::NP + 3 * ch + i];
+        if (step) {
+            C15::template chain_predict<2>(xa, Pa, dt, qaw);
+            if (type != kGps) {  // a GPS fix updates the pva chains only
+                const T za[2] = {T(e[2 + M15::imu_att(ch)]), T(e[2 + M15::imu_rate(ch)])};
+                ok = sel_update<2, 2, true, T, kRefNewton, true>(xa, Pa, za, Ra) && ok;
+            }
+        }
+        if (cb) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) *level_row<T>(cb, cl, M15::aw(ch, i)) = xa[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, 15 + 6 * M15::NP + 3 * ch + i) = Pa[i];
+        }
+        rec.add_aw(Pa);
+        if (final_predict) C15::template chain_predict<2>(xa, Pa, dte, qaw);
+        fin.add_aw(Pa);
+    }
+    T crun = par.run;
+    if (step) {
+        const T ld = rec.finish();
+        crun = ld > par.run ? ld : par.run;
+        crun = ok ? crun : quiet_nan<T>();  // a failed filter (kf_eval_combos: KF_ENOTSPD)
+    }
+    T fmax = crun;
+    if (final_predict) {
+        const T ld = fin.finish();
+        fmax = ld > crun ? ld : crun;
+    }
+    if (cb) {
+        *level_row<T>(cb, cl, 42) = crun;
+        *level_tail<T>(cb, cl, 0) = cprev;
+        *level_tail<T>(cb, cl, 1) = __builtin_bit_cast(double, cmask);
+    }
+    if (a.subset_max) static_cast<T*>(a.subset_max)[cmask] = fmax;
+    if (fmax < T(a.threshold)) {  // max(log_det) < R_threshold (kf_workers.py:1353); NaN never passes
+        const uint64_t key = __builtin_bitreverse64(cmask);  // larger key = earlier in itertools order
+        best = key > best ? key : best;
+        ++cnt;
+    }
+}
+
+// one atomic pair per wave, and only from waves with an accepted subset
+__device__ __forceinline__ void search_publish(const Ref15SearchArgs& a, int k, uint64_t best, uint64_t cnt) {
     if (__builtin_amdgcn_ballot_w64(cnt != 0) != 0) {  // wave-uniform
         best = wave_max_u64(best);
         cnt = wave_sum_u64(cnt);
@@ -1000,6 +1007,66 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
             atomicAdd(reinterpret_cast<unsigned long long*>(&a.n_acc[k]), static_cast<unsigned long long>(cnt));
         }
     }
+}
+
+// Parent-major: one lane per parent, its children in a wave-uniform loop over j (parents of a
+// wave share their largest event except at run boundaries, so event j is the same for every
+// active lane: scalar loads, a uniform GPS/IMU branch).  For the wide levels.
+template <typename T>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void ref15_search_pm_kernel(const Ref15SearchArgs a) {
+    const int64_t p = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (uint64_t(p) >= a.n_par) return;
+    SearchNode<T> par;
+    if (a.k == 1) par.root(a);
+    else par.load(a.par, uint64_t(p));
+    const int m = par.max_event();
+    const int j0 = wave_uniform(m) + 1;  // colex order: the first lane holds the smallest max
+    uint64_t best = 0, cnt = 0;
+    for (int j = j0; j < a.n_events; ++j) {
+        if (j <= m) continue;
+        search_child<T>(a, par, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt);
+    }
+    search_publish(a, a.k, best, cnt);
+}
+
+// Child-major: one wave per (parent block of 64, child event) work item, one child per lane,
+// so no lane walks a long list of children (the narrow levels, where few parents have many
+// children each).  Items are ordered by parent block, then j, and dealt to the XCDs in
+// contiguous ranges, so the items that read one parent block run back to back on one XCD and
+// re-read it from that XCD's L2.  Blocks are grouped by their first parent's largest event v
+// (non-decreasing in colex order); a block of group v has items j = v + 1 .. n - 1.
+template <typename T>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void ref15_search_cm_kernel(const Ref15SearchArgs a,
+                                                                                                     uint64_t n_items) {
+    const uint64_t per_xcd = (n_items + 7) / 8;
+    const uint64_t item = uint64_t(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+    if (item >= n_items) return;
+    const int n = a.n_events, k = a.k;
+    const uint64_t* C = a.binom;
+    auto binom = [&](int x, int y) -> uint64_t { return x < 0 ? (y == 0 ? 1 : 0) : C[x * (kMaxEvents + 1) + y]; };
+    // find the item's group v (scalar loop): group v holds blocks [ceil(C(v, k-1)/64), ceil(C(v+1, k-1)/64))
+    int v = k == 1 ? -1 : k - 2;
+    uint64_t start = 0;
+    uint64_t b0 = 0, nb = 1;
+    for (;; ++v) {
+        b0 = k == 1 ? 0 : (binom(v, k - 1) + 63) / 64;
+        const uint64_t b1 = k == 1 ? 1 : (binom(v + 1, k - 1) + 63) / 64;
+        nb = b1 - b0;
+        const uint64_t span = nb * uint64_t(n - 1 - v);
+        if (item < start + span || v >= n - 2) break;
+        start += span;
+    }
+    const uint64_t r = item - start;
+    const uint64_t blk = b0 + r / uint64_t(n - 1 - v);
+    const int j = v + 1 + int(r % uint64_t(n - 1 - v));
+    const uint64_t p = blk * 64 + threadIdx.x;
+    if (p >= a.n_par) return;
+    SearchNode<T> par;
+    if (k == 1) par.root(a);
+    else par.load(a.par, p);
+    uint64_t best = 0, cnt = 0;
+    if (par.max_event() < j) search_child<T>(a, par, j, p + binom(j, k), best, cnt);
+    search_publish(a, a.k, best, cnt);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1240,14 +1307,34 @@ hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t st
     return hipGetLastError();
 }
 
-hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, hipStream_t stream) {
+hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream) {
     // node offsets are 32-bit byte offsets (buffer voffset)
     if (a.n_events > kMaxEvents || a.k < 1 || a.k > a.n_events || a.n_par == 0 || a.n_par >= (1ull << 28) ||
         a.n_child >= (1ull << 28))
         return hipErrorInvalidValue;
+    if (child_major) {
+        // work items: per group v of parent blocks, blocks x (n - 1 - v) child events
+        const uint64_t* C = a.binom_host;
+        const int n = a.n_events, k = a.k;
+        uint64_t items = 0;
+        if (k == 1) {
+            items = uint64_t(n);
+        } else {
+            for (int v = k - 2; v <= n - 2; ++v) {
+                const uint64_t b0 = (C[v * (kMaxEvents + 1) + k - 1] + 63) / 64;
+                const uint64_t b1 = (C[(v + 1) * (kMaxEvents + 1) + k - 1] + 63) / 64;
+                items += (b1 - b0) * uint64_t(n - 1 - v);
+            }
+        }
+        const uint64_t waves = (items + 7) / 8 * 8;
+        if (waves >= (1ull << 31)) return hipErrorInvalidValue;
+        if (f64) ref15_search_cm_kernel<double><<<dim3(unsigned(waves)), 64, 0, stream>>>(a, items);
+        else ref15_search_cm_kernel<float><<<dim3(unsigned(waves)), 64, 0, stream>>>(a, items);
+        return hipGetLastError();
+    }
     const dim3 grid(static_cast<unsigned>((a.n_par + kBlock - 1) / kBlock));
-    if (f64) ref15_search_kernel<double><<<grid, kBlock, 0, stream>>>(a);
-    else ref15_search_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    if (f64) ref15_search_pm_kernel<double><<<grid, kBlock, 0, stream>>>(a);
+    else ref15_search_pm_kernel<float><<<grid, kBlock, 0, stream>>>(a);
     return hipGetLastError();
 }
 

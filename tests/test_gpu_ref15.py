@@ -118,10 +118,13 @@ def _search_case(golden_dir, n, swap=True):
     return cand, ev, init, st[-1][0], target
 
 
+@pytest.mark.parametrize('kernel', ['cm', 'pm'])
 @pytest.mark.parametrize('dtype', ['f64', 'f32'])
-def test_search_subset_max_equals_eval_combos(golden_dir, dtype):
+def test_search_subset_max_equals_eval_combos(golden_dir, dtype, kernel, monkeypatch):
     """kf_search_combos (one event step per subset, from the stored prefix) gives every subset the
-    max log-det the per-subset kernel gives (same operations in the same order)."""
+    max log-det the per-subset kernel gives (same operations in the same order), with either
+    search kernel (child-major / parent-major levels)."""
+    monkeypatch.setenv('KFMI_SEARCH_KERNEL', kernel)
     n = 12
     cand, ev, init, t0, target = _search_case(golden_dir, n)
     kf = kfmi.BatchedKF('ref15', 1, dtype)
@@ -147,11 +150,13 @@ def test_search_subset_max_equals_eval_combos(golden_dir, dtype):
     assert worst <= (1e-12 if dtype == 'f64' else 1e-6), (worst, exact, total)
 
 
+@pytest.mark.parametrize('kernel', ['cm', 'pm'])
 @pytest.mark.parametrize('q', [0.0, 0.01, 0.3, 0.9])
-def test_search_winner_matches_per_subset_search(golden_dir, q):
+def test_search_winner_matches_per_subset_search(golden_dir, q, kernel, monkeypatch):
     """The search's winner and per-size accepted counts at thresholds across the distribution of
     subset scores equal the per-subset kernel's (first acceptable subset in itertools order of
     the smallest size)."""
+    monkeypatch.setenv('KFMI_SEARCH_KERNEL', kernel)
     n = 11
     cand, ev, init, t0, target = _search_case(golden_dir, n)
     kf = kfmi.BatchedKF('ref15', 1, 'f64')
