@@ -210,6 +210,9 @@ int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const d
  * stops after the first size with an accepted subset unless `exhaustive`.  Host outputs:
  * *k_found = that size (0 = none), *winner = bit mask (bit i = candidate i) of its first
  * accepted subset in itertools.combinations order (the reference's pick, :1349-1356),
+ * n_fixed / fixed_mask: search only the subsets whose intersection with candidates
+ * 0 .. n_fixed - 1 is fixed_mask (0 / 0 = every subset; one class per GPU shards the search
+ * evenly, kfmi.dist), k_max counting the fixed candidates,
  * n_accepted host [k_max + 1] (nullable) accepted subsets per size.  subset_max: device [2^n]
  * of the handle's dtype (n_events <= 30, nullable) receives every evaluated subset's max
  * log-determinant (NaN for a failed filter), indexed by mask.  Level k stores the C(n - 1, k)
@@ -218,7 +221,8 @@ int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const d
  * widest stored level (w = 8 for f64, 4 for f32).  The call synchronises `stream`. */
 int kf_search_combos(kf_batch* handle, int n_events, const double* events, const double* init,
                      double prev_time, double target_end, double threshold, int k_max, int exhaustive,
-                     uint64_t* winner, int* k_found, uint64_t* n_accepted, void* subset_max, void* stream);
+                     int n_fixed, uint64_t fixed_mask, uint64_t* winner, int* k_found,
+                     uint64_t* n_accepted, void* subset_max, void* stream);
 
 /* KF_MODEL_REF15 scheduler scoring: gain device [n_types][B] = trace of the posterior
  * covariance each candidate sensor type (types: host [n_types] KF_EVENT_GPS|KF_EVENT_IMU,

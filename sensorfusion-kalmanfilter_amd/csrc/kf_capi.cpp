@@ -546,21 +546,30 @@ int kf_eval_combos(kf_batch* h, int n_events, const double* events, const double
 }
 
 int kf_search_combos(kf_batch* h, int n_events, const double* events, const double* init, double prev_time,
-                     double target_end, double threshold, int k_max, int exhaustive, uint64_t* winner,
-                     int* k_found, uint64_t* n_accepted, void* subset_max, void* stream) {
+                     double target_end, double threshold, int k_max, int exhaustive, int n_fixed,
+                     uint64_t fixed_mask, uint64_t* winner, int* k_found, uint64_t* n_accepted, void* subset_max,
+                     void* stream) {
     if (int rc = check_handle(h)) return rc;
     if (int rc = check_combo_inputs(h, n_events, events, init, "kf_search_combos")) return rc;
-    const int n = n_events;
-    if (k_max < 1 || k_max > n) return fail(KF_EINVAL, "kf_search_combos: k_max = %d outside [1, %d]", k_max, n);
+    if (n_fixed < 0 || n_fixed >= n_events)
+        return fail(KF_EINVAL, "kf_search_combos: n_fixed = %d outside [0, %d)", n_fixed, n_events);
+    if (n_fixed < 64 && (fixed_mask >> n_fixed) != 0)
+        return fail(KF_EINVAL, "kf_search_combos: fixed_mask has bits at or above n_fixed = %d", n_fixed);
+    const int k_base = __builtin_popcountll(fixed_mask);
+    const int n = n_events - n_fixed;  // free candidates
+    if (k_max <= k_base || k_max > n_events)
+        return fail(KF_EINVAL, "kf_search_combos: k_max = %d outside [%d, %d]", k_max, k_base + 1, n_events);
     if (!winner || !k_found) return fail(KF_EINVAL, "kf_search_combos: null winner/k_found");
-    if (subset_max && n > 30) return fail(KF_EINVAL, "kf_search_combos: subset_max needs n_events <= 30 (2^n entries)");
+    if (subset_max && n_events > 30)
+        return fail(KF_EINVAL, "kf_search_combos: subset_max needs n_events <= 30 (2^n entries)");
+    const int kf_max = k_max - k_base < n ? k_max - k_base : n;  // free levels searched
     const uint64_t* binom = binom_table();
     auto C = [&](int a, int b) { return binom[a * (kMaxComboEvents + 1) + b]; };
-    // Levels 1 .. k_max - 1 are stored, and of each only the subsets without event n - 1 (the
-    // others have no children): the colex ranks below C(n - 1, k).
+    // Free levels 1 .. kf_max - 1 are stored, and of each only the subsets without the last
+    // candidate (the others have no children): the colex ranks below C(n - 1, k).
     uint64_t widest = 0;
-    for (int k = 1; k < k_max; ++k) widest = C(n - 1, k) > widest ? C(n - 1, k) : widest;
-    for (int k = 1; k <= k_max; ++k)
+    for (int k = 1; k < kf_max; ++k) widest = C(n - 1, k) > widest ? C(n - 1, k) : widest;
+    for (int k = 1; k <= kf_max; ++k)
         if (C(n - 1, k - 1) >= (1ull << 28))
             return fail(KF_EINVAL, "kf_search_combos: level %d has C(%d, %d) = %llu parents (limit 2^28); lower k_max",
                         k, n - 1, k - 1, static_cast<unsigned long long>(C(n - 1, k - 1)));
@@ -579,7 +588,7 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         h->search_ws_bytes = need;
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (int rc = upload_combo_inputs(h, n, events, init, st, "kf_search_combos: upload")) return rc;
+    if (int rc = upload_combo_inputs(h, n_events, events, init, st, "kf_search_combos: upload")) return rc;
     char* ws = static_cast<char*>(h->ws);
     char* sw = static_cast<char*>(h->search_ws);
     uint64_t* d_best = reinterpret_cast<uint64_t*>(sw);
@@ -589,13 +598,17 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
     char* lv[2] = {sw + head, sw + head + level};
     uint64_t best[kMaxComboEvents + 1] = {}, acc[kMaxComboEvents + 1] = {};
     int found = 0, last = 0;
-    for (int k = 1; k <= k_max; ++k) {
+    for (int k = 1; k <= kf_max; ++k) {
         kfmi::Ref15SearchArgs a{};
         a.n_events = n;
         a.k = k;
+        a.shift = n_fixed;
+        a.k_base = k_base;
+        a.root_mask = fixed_mask;
+        a.ev_all = reinterpret_cast<const double*>(ws);
         a.n_par = k == 1 ? 1 : C(n - 1, k - 1);  // the parents with children
         a.n_child = C(n, k);
-        a.ev = reinterpret_cast<const double*>(ws);
+        a.ev = reinterpret_cast<const double*>(ws) + 11 * n_fixed;
         a.binom = reinterpret_cast<const uint64_t*>(ws + kWsEvents);
         a.binom_host = binom;
         a.init = reinterpret_cast<const double*>(ws + kWsEvents + kWsBinom);
@@ -603,25 +616,27 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.target_end = target_end;
         a.threshold = threshold;
         a.par = k > 1 ? lv[(k - 1) & 1] : nullptr;
-        a.child = k < k_max ? lv[k & 1] : nullptr;
+        a.child = k < kf_max ? lv[k & 1] : nullptr;
         a.best = d_best;
         a.n_acc = d_acc;
         a.subset_max = subset_max;
         e = kfmi::launch_ref15_search(h->dtype == KF_F64, a, search_child_major(a.n_par), st);
         if (e != hipSuccess) return hip_fail(e, "kf_search_combos: level launch");
-        last = k;
+        last = k_base + k;
         if (!exhaustive) {  // the reference stops at the first size with an acceptable subset
-            e = hipMemcpyAsync(&best[k], &d_best[k], sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+            // (the first launch also scores the fixed root itself, size k_base)
+            const int lo = k == 1 ? k_base : last;
+            e = hipMemcpyAsync(&best[lo], &d_best[lo], sizeof(uint64_t) * (last - lo + 1), hipMemcpyDeviceToHost, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);
             if (e != hipSuccess) return hip_fail(e, "kf_search_combos: level result");
-            if (best[k]) break;
+            if (best[lo] || best[last]) break;
         }
     }
     e = hipMemcpyAsync(best, d_best, sizeof best, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(acc, d_acc, sizeof acc, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(e, "kf_search_combos: results");
-    for (int k = 1; k <= last && !found; ++k)
+    for (int k = k_base > 0 ? k_base : 1; k <= last && !found; ++k)
         if (best[k]) found = k;
     *k_found = found;
     *winner = found ? __builtin_bitreverse64(best[found]) : 0;

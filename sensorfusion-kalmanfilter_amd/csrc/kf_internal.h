@@ -95,11 +95,15 @@ struct Ref15ComboArgs {
 //   [64] double      time of the last applied event
 //   [64] uint64      subset bit mask
 struct Ref15SearchArgs {
-    int n_events;
-    int k;                   // child level (k >= 1; k = 1 reads the root from init)
+    int n_events;            // free candidates (events shift .. shift + n_events - 1 of ev_all)
+    int k;                   // child level: k free events (k >= 1; k = 1 builds the root)
+    int shift;               // fixed candidates below the free ones
+    int k_base;              // popcount(root_mask): level k holds subsets of size k_base + k
+    uint64_t root_mask;      // the fixed candidates every subset of this search contains
+    const double* ev_all;    // device [shift + n_events][11]
     uint64_t n_par;          // C(n, k - 1) parents, one lane each
     uint64_t n_child;        // C(n, k)
-    const double* ev;        // device [n][11]: t, type, payload[9]
+    const double* ev;        // device [n_events][11]: the free candidates (t, type, payload[9])
     const uint64_t* binom;   // device [65][65]
     const uint64_t* binom_host;  // host copy (launch geometry)
     const double* init;      // device [15 + 27]: root state (level 0)
@@ -108,8 +112,8 @@ struct Ref15SearchArgs {
     double threshold;        // acceptance: max log-det < threshold (kf_workers.py:1353)
     const void* par;         // level k - 1 buffer (unused for k = 1)
     void* child;             // level k buffer, or nullptr when level k is not stored
-    uint64_t* best;          // device [65]: per level, max over accepted subsets of bitrev(mask)
-    uint64_t* n_acc;         // device [65]: per level, number of accepted subsets
+    uint64_t* best;          // device [65]: per subset size, max over accepted subsets of bitrev(mask)
+    uint64_t* n_acc;         // device [65]: per subset size, number of accepted subsets
     void* subset_max;        // device [2^n] T: every subset's max log-det by mask, or nullptr
 };
 

@@ -861,20 +861,45 @@ struct SearchNode {
     double prev;
     uint64_t mask;
 
-    // the root (the empty subset): record 0 is the logdet of the initial covariance (kf_workers.py:32)
-    __device__ __forceinline__ void root(const Ref15SearchArgs& a) {
+    // The root: the search's fixed events (a.root_mask, none for a whole search) applied to the
+    // initial filter in index order as the worker applies a combination's events
+    // (kf_workers.py:36-71); record 0 is the logdet of the initial covariance (:32).  With
+    // `eval`, the root subset itself is also scored (its max log-det with the final predict).
+    __device__ __forceinline__ T root(const Ref15SearchArgs& a, bool eval) {
         Ref15<T> r;
 #pragma unroll
         for (int i = 0; i < 15; ++i) r.x[i] = T(a.init[i]);
 #pragma unroll
         for (int i = 0; i < 27; ++i) r.blk(i) = T(a.init[15 + i]);
         run = r.logdet();
+        prev = a.prev_time;
+        mask = a.root_mask;
+        const T no_gate = T(0);
+        for (uint64_t rest = a.root_mask; rest; rest &= rest - 1) {
+            const double* e = a.ev_all + __builtin_ctzll(rest) * 11;
+            const double dtd = e[0] - prev;
+            if (dtd < 0.0) continue;  // kf_workers.py:38-40
+            T pay[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) pay[i] = T(e[2 + i]);
+            bool ok = true;
+            r.event(int(e[1]), T(dtd), pay, false, no_gate, ok);
+            const T ld = r.logdet();
+            run = ld > run ? ld : run;
+            run = ok ? run : quiet_nan<T>();
+            prev = e[0];
+        }
 #pragma unroll
         for (int i = 0; i < 15; ++i) x[i] = r.x[i];
 #pragma unroll
         for (int i = 0; i < 27; ++i) P[i] = r.blk(i);
-        prev = a.prev_time;
-        mask = 0;
+        T fmax = run;
+        if (eval && prev < a.target_end - 1e-8) {  // kf_workers.py:74-82
+            r.predict(T(a.target_end - prev));
+            const T ld = r.logdet();
+            fmax = ld > run ? ld : run;
+        }
+        return fmax;
     }
     __device__ __forceinline__ void load(const void* level, uint64_t p) {
         char* blk = level_block<T>(level, p);
@@ -887,8 +912,24 @@ struct SearchNode {
         prev = *level_tail<T>(blk, lane, 0);
         mask = __builtin_bit_cast(uint64_t, *level_tail<T>(blk, lane, 1));
     }
-    __device__ __forceinline__ int max_event() const { return mask ? 63 - __builtin_clzll(mask) : -1; }
+    // largest free candidate in the subset (local index), -1 for the root
+    __device__ __forceinline__ int max_event(int shift) const {
+        const uint64_t loc = mask >> shift;
+        return loc ? 63 - __builtin_clzll(loc) : -1;
+    }
 };
+
+// a scored subset: every max log-det to subset_max, the acceptance test into (best, cnt)
+template <typename T>
+__device__ __forceinline__ void search_score(const Ref15SearchArgs& a, uint64_t mask, T fmax, uint64_t& best,
+                                             uint64_t& cnt) {
+    if (a.subset_max) static_cast<T*>(a.subset_max)[mask] = fmax;
+    if (fmax < T(a.threshold)) {  // max(log_det) < R_threshold (kf_workers.py:1353); NaN never passes
+        const uint64_t key = __builtin_bitreverse64(mask);  // larger key = earlier in itertools order
+        best = key > best ? key : best;
+        ++cnt;
+    }
+}
 
 // Child j (> the parent's largest event) of node `par`, colex rank c at level a.k: its filter
 // (stored when a.child is set and the child has children), its max log-det with the worker's
@@ -907,7 +948,7 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
     const T Ra[3] = {T(kRAtt), T(0), T(kRRate)};
     const double* e = a.ev + j * 11;
     const int type = int(e[1]);
-    const uint64_t cmask = par.mask | (uint64_t(1) << j);
+    const uint64_t cmask = par.mask | (uint64_t(1) << (j + a.shift));
     const double dtd = e[0] - par.prev;
     const bool step = dtd >= 0.0;  // kf_workers.py:38-40: a negative dt is skipped, time unchanged
     const T dt = T(dtd);
@@ -989,22 +1030,17 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
         *level_tail<T>(cb, cl, 0) = cprev;
         *level_tail<T>(cb, cl, 1) = __builtin_bit_cast(double, cmask);
     }
-    if (a.subset_max) static_cast<T*>(a.subset_max)[cmask] = fmax;
-    if (fmax < T(a.threshold)) {  // max(log_det) < R_threshold (kf_workers.py:1353); NaN never passes
-        const uint64_t key = __builtin_bitreverse64(cmask);  // larger key = earlier in itertools order
-        best = key > best ? key : best;
-        ++cnt;
-    }
+    search_score(a, cmask, fmax, best, cnt);
 }
 
-// one atomic pair per wave, and only from waves with an accepted subset
+// one atomic pair per wave, and only from waves with an accepted subset; k = local level
 __device__ __forceinline__ void search_publish(const Ref15SearchArgs& a, int k, uint64_t best, uint64_t cnt) {
     if (__builtin_amdgcn_ballot_w64(cnt != 0) != 0) {  // wave-uniform
         best = wave_max_u64(best);
         cnt = wave_sum_u64(cnt);
         if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0) {
-            atomicMax(reinterpret_cast<unsigned long long*>(&a.best[k]), static_cast<unsigned long long>(best));
-            atomicAdd(reinterpret_cast<unsigned long long*>(&a.n_acc[k]), static_cast<unsigned long long>(cnt));
+            atomicMax(reinterpret_cast<unsigned long long*>(&a.best[a.k_base + k]), static_cast<unsigned long long>(best));
+            atomicAdd(reinterpret_cast<unsigned long long*>(&a.n_acc[a.k_base + k]), static_cast<unsigned long long>(cnt));
         }
     }
 }
@@ -1017,9 +1053,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     const int64_t p = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (uint64_t(p) >= a.n_par) return;
     SearchNode<T> par;
-    if (a.k == 1) par.root(a);
-    else par.load(a.par, uint64_t(p));
-    const int m = par.max_event();
+    if (a.k == 1) {
+        uint64_t rb = 0, rc = 0;  // a fixed root is itself one of the subsets searched
+        const T f = par.root(a, a.root_mask != 0);
+        if (a.root_mask) search_score(a, a.root_mask, f, rb, rc);
+        search_publish(a, 0, rb, rc);
+    } else {
+        par.load(a.par, uint64_t(p));
+    }
+    const int m = par.max_event(a.shift);
     const int j0 = wave_uniform(m) + 1;  // colex order: the first lane holds the smallest max
     uint64_t best = 0, cnt = 0;
     for (int j = j0; j < a.n_events; ++j) {
@@ -1062,10 +1104,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
     const uint64_t p = blk * 64 + threadIdx.x;
     if (p >= a.n_par) return;
     SearchNode<T> par;
-    if (k == 1) par.root(a);
-    else par.load(a.par, p);
+    if (k == 1) {
+        uint64_t rb = 0, rc = 0;  // a fixed root is itself one of the subsets searched (item 0 scores it)
+        const bool eval = a.root_mask != 0 && item == 0;
+        const T f = par.root(a, eval);
+        if (eval) search_score(a, a.root_mask, f, rb, rc);
+        search_publish(a, 0, rb, rc);
+    } else {
+        par.load(a.par, p);
+    }
     uint64_t best = 0, cnt = 0;
-    if (par.max_event() < j) search_child<T>(a, par, j, p + binom(j, k), best, cnt);
+    if (par.max_event(a.shift) < j) search_child<T>(a, par, j, p + binom(j, k), best, cnt);
     search_publish(a, a.k, best, cnt);
 }
 

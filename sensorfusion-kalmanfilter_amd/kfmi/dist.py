@@ -8,9 +8,11 @@ counter-based generator (kf_synth keyed by the GLOBAL filter index) — no scatt
 collective in the time loop.  The only collective is the final reassembly of per-shard
 results (``gather_shards``), plus scalar reductions for timing.
 
-The brute-force search (kf_workers.py:1218-1392) shards by combination rank instead: for each
-subset size k every rank scans its slice of the C(n, k) ranks and one MIN all-reduce picks the
-globally first acceptable combination (``brute_force_search``).
+The brute-force search (kf_workers.py:1218-1392) shards by subset class instead: the subsets
+are split by their intersection with the first few candidates, each rank runs the
+shared-prefix search over its classes, and two all-reduces pick the globally first acceptable
+combination (``brute_force_search``).  ``brute_force_search_ranks`` shards one filter per
+subset by combination rank, for searches whose prefix levels do not fit on the GPU.
 """
 from __future__ import annotations
 
@@ -67,14 +69,98 @@ def max_over_ranks(values, device, group=None):
 _NONE = (1 << 63) - 1
 
 
+def search_classes(n, world):
+    """Shard plan of the shared-prefix search over ``world`` ranks: the subsets are split by their
+    intersection with the first w candidates (2^w classes of 2^(n-w) subsets each), w the
+    smallest with 2^w >= 4 world (at most n - 1); class c goes to rank c % world.  Returns w."""
+    w = 0
+    while (1 << w) < 4 * world and w < n - 1:
+        w += 1
+    return w if world > 1 else 0
+
+
 def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, initial_pt=None, initial_state=None,
-                       max_combos_in_memory=1 << 22, dtype='f64', device=0, group=None, first_valid=None,
-                       finish=None):
-    """run_brute_force_kalman_filter_no_sampling_min_usage sharded over the ranks of ``group``:
-    for k = 1..n, rank r scans combination ranks shard_range(C(n, k), r, world) on its GPU
-    (kf_eval_combos), then an all-reduce MIN of the first acceptable rank (or "none") decides
-    — the same winner as the single-GPU search (the first acceptable subset of the smallest size,
-    in itertools.combinations order).  Every rank returns the reference's result dict (or None).
+                       max_combos_in_memory=1 << 22, dtype='f64', device=0, group=None, search_class=None,
+                       finish=None, search_mem_bytes=32 << 30):
+    """run_brute_force_kalman_filter_no_sampling_min_usage sharded over the ranks of ``group``
+    with the shared-prefix search (kf_search_combos): the subsets are split into 2^w classes by
+    their intersection with the first w candidates (``search_classes``); each rank searches its
+    classes, keeping per class the first size with an acceptable subset and its first such
+    subset in itertools order, and two all-reduces (MIN of the size, then MAX of the
+    bit-reversed subset mask at that size) pick the same winner as the single-GPU search.
+    Every rank returns the reference's result dict (or None).  Falls back to
+    ``brute_force_search_ranks`` when a class's levels would not fit in ``search_mem_bytes``.
+
+    ``search_class(n_fixed, fixed_mask) -> (k, indices or None)`` / ``finish(k, indices)``
+    replace the GPU evaluation (tests drive the reduction logic with the CPU oracle on gloo)."""
+    import torch.distributed as dist
+
+    from . import ref15
+    if R_threshold is None:
+        raise ValueError('R_threshold must be specified for brute force KF.')
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    st = ref15.brute_force_setup(events, start_idx, end_idx, initial_pt, initial_state)
+    if st is None:
+        return None
+    cand, xt, Pt, prev_time, target_end, ev, init = st
+    n = len(cand)
+    w = search_classes(n, world)
+    if search_class is None and ref15.search_levels(n - w, dtype, search_mem_bytes) < n - w:
+        return brute_force_search_ranks(events, start_idx, end_idx, R_threshold, initial_pt, initial_state,
+                                        max_combos_in_memory, dtype, device, group)
+    kf = None
+    if search_class is None:
+        kf = ref15.BatchedKF('ref15', 1, dtype, device=device)
+
+        def search_class(n_fixed, fixed_mask):
+            k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=n,
+                                            n_fixed=n_fixed, fixed_mask=fixed_mask)
+            return k, idx
+    if finish is None:
+        def finish(k, idx):
+            return ref15.brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device,
+                                            indices=idx)
+    backend = dist.get_backend(group)
+    tdev = torch.device('cuda', torch.cuda.current_device()) if backend == 'nccl' else torch.device('cpu')
+    try:
+        k_r, key_r = _NONE, 0  # this rank: smallest accepted size, and its max bit-reversed mask
+        for c in range(rank, 1 << w, world):
+            k, idx = search_class(w, c)
+            if k and idx is not None:
+                key = _bitrev64(sum(1 << i for i in idx))
+                if k < k_r or (k == k_r and key > key_r):
+                    k_r, key_r = k, key
+    finally:
+        if kf is not None:
+            kf.close()
+    t = torch.tensor([k_r], dtype=torch.int64, device=tdev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    k_min = int(t.item())
+    if k_min == _NONE:
+        return None
+    # keys are unsigned 64-bit: all-reduce them as two non-negative halves (high, then low)
+    hi = torch.tensor([key_r >> 32 if k_r == k_min else -1], dtype=torch.int64, device=tdev)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    lo = torch.tensor([key_r & 0xFFFFFFFF if (k_r == k_min and key_r >> 32 == int(hi.item())) else -1],
+                      dtype=torch.int64, device=tdev)
+    dist.all_reduce(lo, op=dist.ReduceOp.MAX, group=group)
+    mask = _bitrev64((int(hi.item()) << 32) | int(lo.item()))
+    return finish(k_min, tuple(i for i in range(n) if (mask >> i) & 1))
+
+
+def _bitrev64(v):
+    return int(f'{v & ((1 << 64) - 1):064b}'[::-1], 2)
+
+
+def brute_force_search_ranks(events, start_idx=0, end_idx=None, R_threshold=None, initial_pt=None,
+                             initial_state=None, max_combos_in_memory=1 << 22, dtype='f64', device=0, group=None,
+                             first_valid=None, finish=None):
+    """run_brute_force_kalman_filter_no_sampling_min_usage sharded over the ranks of ``group``,
+    one filter per subset: for k = 1..n, rank r scans combination ranks
+    shard_range(C(n, k), r, world) on its GPU (kf_eval_combos), then an all-reduce MIN of the
+    first acceptable rank (or "none") decides — the same winner as the single-GPU search (the
+    first acceptable subset of the smallest size, in itertools.combinations order).  Every rank
+    returns the reference's result dict (or None).  For searches whose prefix levels do not fit.
 
     ``first_valid(k, lo, hi)`` / ``finish(k, rank)`` replace the GPU evaluation (tests drive the
     reduction logic with the CPU oracle on gloo)."""

@@ -295,12 +295,14 @@ class BatchedKF:
         return mx, ld, nr
 
     def search_combos(self, events, init, prev_time, target_end, threshold, k_max=None, exhaustive=False,
-                      subset_max=False):
+                      subset_max=False, n_fixed=0, fixed_mask=0):
         """KF_MODEL_REF15 brute-force search with shared prefixes (kf_search_combos): sizes
         k = 1 .. k_max of the n candidate events, each subset's filter advanced from its prefix's
         by one event.  Stops after the first size with a subset whose max log-det is below
-        threshold unless ``exhaustive``.  Returns (k_found, winner indices tuple or None,
-        accepted count per size [k_max + 1], subset_max [2^n] or None)."""
+        threshold unless ``exhaustive``.  ``n_fixed`` / ``fixed_mask`` restrict it to the subsets
+        whose intersection with candidates 0 .. n_fixed - 1 is fixed_mask (one shard of the
+        search).  Returns (k_found, winner indices tuple or None, accepted count per size
+        [k_max + 1], subset_max [2^n] or None)."""
         if self.model != 'ref15':
             raise ValueError('search_combos needs a ref15 handle')
         ev = np.ascontiguousarray(events, dtype=np.float64)
@@ -317,7 +319,8 @@ class BatchedKF:
             sm.fill_(float('nan'))
         check(_lib.lib().kf_search_combos(self.handle, n, ev.ctypes.data_as(ctypes.c_void_p),
                                           ini.ctypes.data_as(ctypes.c_void_p), float(prev_time), float(target_end),
-                                          float(threshold), k_max, int(bool(exhaustive)), ctypes.byref(win),
+                                          float(threshold), k_max, int(bool(exhaustive)), int(n_fixed),
+                                          int(fixed_mask), ctypes.byref(win),
                                           ctypes.byref(kf), acc.ctypes.data_as(ctypes.c_void_p), _ptr(sm),
                                           self._stream()))
         combo = tuple(i for i in range(n) if (win.value >> i) & 1) if kf.value else None

@@ -105,11 +105,96 @@ def _bf_worker(rank, world, port, golden, thr, out_q):
         def finish(k, r):
             return ref15.unrank_combination(n, k, r)
 
-        out = kdist.brute_force_search(events, s, e, R_threshold=thr, initial_pt=g['init_P'],
-                                       initial_state=tuple(g['init_state']), first_valid=first_valid, finish=finish)
+        out = kdist.brute_force_search_ranks(events, s, e, R_threshold=thr, initial_pt=g['init_P'],
+                                             initial_state=tuple(g['init_state']), first_valid=first_valid,
+                                             finish=finish)
         out_q.put((rank, out, scanned, n))
     finally:
         dist.destroy_process_group()
+
+
+def _bf_class_worker(rank, world, port, golden, thr, out_q):
+    """kfmi.dist.brute_force_search (shared-prefix classes) on gloo with the oracle as the
+    per-class search."""
+    import sys
+    from itertools import combinations
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    sys.path.insert(0, os.path.dirname(__file__))
+    from golden_events import unpack_events
+    from kfmi import ref15
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        g = np.load(golden)
+        events = unpack_events(g)
+        s, e = int(g['start']), int(g['end'])
+        thr = float(g['threshold']) if thr is None else thr
+        cand, xt, Pt, prev, end, _, _ = ref15.brute_force_setup(events, s, e, g['init_P'], tuple(g['init_state']))
+        n = len(cand)
+        searched = []
+
+        def search_class(w, c):
+            """first acceptable subset (smallest size, then itertools order) among those whose
+            intersection with candidates 0..w-1 is the bit pattern c"""
+            searched.append(c)
+            fixed = [i for i in range(w) if (c >> i) & 1]
+            subsets = [tuple(fixed) + t for kk in range(n - w + 1) for t in combinations(range(w, n), kk)]
+            subsets = sorted((x for x in subsets if x), key=lambda x: (len(x), x))
+            for x in subsets:
+                res = ref_kf.evaluate_combo_chunk([tuple(cand[i] for i in x)], xt, Pt, prev, end)[0]
+                if max(res[5]) < thr:
+                    return len(x), x
+            return 0, None
+
+        def finish(k, idx):
+            return list(idx)
+
+        out = kdist.brute_force_search(events, s, e, R_threshold=thr, initial_pt=g['init_P'],
+                                       initial_state=tuple(g['init_state']), search_class=search_class,
+                                       finish=finish)
+        out_q.put((rank, out, searched, n))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+@pytest.mark.parametrize('thr', [None, -27.0, -1e9])  # the reference's threshold; a looser one; nothing
+def test_gloo_class_sharded_brute_force_search(golden_dir, thr, world):
+    """Every rank returns the winner of the unsharded search (the first acceptable subset of the
+    smallest size in itertools order), and the ranks' classes partition the 2^w classes."""
+    from itertools import combinations
+    from kfmi import ref15
+    from golden_events import unpack_events
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    golden = os.path.join(golden_dir, 'ref15_bruteforce.npz')
+    procs = [ctx.Process(target=_bf_class_worker, args=(r, world, port, golden, thr, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert [p.exitcode for p in procs] == [0] * world
+    res = dict((r, (out, sc, n)) for r, out, sc, n in (q.get(timeout=10) for _ in range(world)))
+    g = np.load(golden)
+    n = res[0][2]
+    w = kdist.search_classes(n, world)
+    assert sorted(c for r in res for c in res[r][1]) == list(range(1 << w))
+    if thr is None:
+        want = list(g['selected'])
+    else:  # the unsharded search with the oracle
+        events = unpack_events(g)
+        cand, xt, Pt, prev, end, _, _ = ref15.brute_force_setup(events, int(g['start']), int(g['end']), g['init_P'],
+                                                                tuple(g['init_state']))
+        want = None
+        for k in range(1, n + 1):
+            for x in combinations(range(n), k):
+                res_x = ref_kf.evaluate_combo_chunk([tuple(cand[i] for i in x)], xt, Pt, prev, end)[0]
+                if max(res_x[5]) < thr:
+                    want = list(x)
+                    break
+            if want:
+                break
+    assert all(res[r][0] == want for r in res)
 
 
 @pytest.mark.parametrize('thr', [None, -1e9])  # the reference's threshold and winner; nothing acceptable

@@ -182,6 +182,40 @@ def test_search_winner_matches_per_subset_search(golden_dir, q, kernel, monkeypa
         assert kfound == 0
 
 
+@pytest.mark.parametrize('w', [1, 3])
+def test_search_classes_partition_the_search(golden_dir, w):
+    """The per-GPU shards of kfmi.dist.brute_force_search: searches restricted to the subsets
+    with a fixed intersection with the first w candidates score each of their subsets as the
+    whole search does, cover every subset exactly once, and their per-class winners combine
+    (smallest size, then itertools order) into the whole search's winner."""
+    n = 11
+    cand, ev, init, t0, target = _search_case(golden_dir, n)
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    _, _, _, full = kf.search_combos(ev, init, t0, target, threshold=-1e30, exhaustive=True, subset_max=True)
+    full = full.cpu().numpy()
+    seen = np.zeros(1 << n, dtype=int)
+    for c in range(1 << w):
+        _, _, _, sm = kf.search_combos(ev, init, t0, target, -1e30, exhaustive=True, subset_max=True,
+                                       n_fixed=w, fixed_mask=c)
+        sm = sm.cpu().numpy()
+        idx = np.flatnonzero(~np.isnan(sm))
+        assert ((idx & ((1 << w) - 1)) == c).all()
+        seen[idx] += 1
+        assert np.max(np.abs(sm[idx] - full[idx]) / np.maximum(np.abs(full[idx]), 1.0)) <= 1e-12
+    assert (seen[1:] == 1).all() and seen[0] == 0
+    vals = np.sort(full[1:])
+    for q in (0.0, 0.02, 0.5):
+        thr = float(vals[int(q * (len(vals) - 1))]) + (1e-9 if q > 0 else -1.0)
+        want = kf.search_combos(ev, init, t0, target, thr)[:2]
+        got = (0, None)
+        for c in range(1 << w):
+            k, idx, _, _ = kf.search_combos(ev, init, t0, target, thr, n_fixed=w, fixed_mask=c)
+            if k and (got[0] == 0 or (k, idx) < got):
+                got = (k, idx)
+        assert got == want, (q, got, want)
+    kf.close()
+
+
 def test_search_combos_rejects_bad_arguments():
     kf = kfmi.BatchedKF('ref15', 1, 'f64')
     ev = np.zeros((4, 11))
@@ -197,6 +231,12 @@ def test_search_combos_rejects_bad_arguments():
     big[:, 0] = np.arange(len(big))
     with pytest.raises(kfmi.KFError):
         kf.search_combos(big, init, 0.0, 68.0, 0.0, k_max=1)
+    with pytest.raises(kfmi.KFError):  # a fixed bit at or above n_fixed
+        kf.search_combos(ev, init, 0.0, 4.0, 0.0, n_fixed=1, fixed_mask=2)
+    with pytest.raises(kfmi.KFError):  # every candidate fixed
+        kf.search_combos(ev, init, 0.0, 4.0, 0.0, n_fixed=4, fixed_mask=0)
+    with pytest.raises(kfmi.KFError):  # k_max not above the fixed subset's size
+        kf.search_combos(ev, init, 0.0, 4.0, 0.0, k_max=2, n_fixed=2, fixed_mask=3)
     kf.close()
     cv = kfmi.BatchedKF('cv3', 4, 'f64')
     with pytest.raises(ValueError):
