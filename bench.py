@@ -248,7 +248,7 @@ def ref15_workload(cfg, args, rank, world, dev):
 
     bytes_launch, bytes_event = ref15_algorithmic_bytes(cfg)
     return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_event,
-                kernel='ref_events_kernel', traffic=load_traffic('ref15'), cpu=cpu, gather=gather_payload, kf=kf,
+                kernel='ref_events_lds_kernel', traffic=load_traffic('ref15'), cpu=cpu, gather=gather_payload, kf=kf,
                 desc=f'SURVEY 8f row 2: reference 15-state model (kf_workers.py:493-614), f64, B={B} filters/GPU, '
                      f'T={T} events (IMU 200 Hz, GPS fix every {k}th event), dt={dt}',
                 extra={'filters_per_gpu': B, 'events_per_launch': T})
@@ -471,7 +471,7 @@ def bf_workload(cfg, args, rank, world, dev):
         # written once and read once as a parent
         lvl = sum(search_level_bytes(math.comb(n - 1, k), 'f64') for k in range(1, n))
         return dict(step=step, units=total_steps, bytes=2 * lvl, bytes_per_unit=2 * lvl / total_combos,
-                    kernel='ref15_search_kernel', traffic=None, cpu=cpu, gather=None, kf=kf, combos=total_combos,
+                    kernel='ref15_search_pm_kernel+ref15_search_cm_kernel (the 25 level launches of one search)', traffic=None, cpu=cpu, gather=None, kf=kf, combos=total_combos,
                     roofline_note='level-buffer bytes only (each stored prefix filter written and read once); the '
                                   'kernel is co-limited by fp64 issue (one event step + final predict per subset)',
                     desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '
