@@ -325,19 +325,21 @@ def log_workload(cfg, args, rank, world, dev):
     prev0 = float(t_ev[0])
     L = _lib.lib()
 
-    from kfmi import ref15
-    P0b = torch.as_tensor(ref15.to_blocks(ref15.P0), device=dev)
-    fallbacks = [0]
+    if not cfg['parallel']:
+        os.environ['KFMI_STREAM'] = 'off'   # kf_run_events would route a one-filter log through kf_run_stream
+    stream_check = {}
 
     def step():
         kf.reset(x0)
         _lib.check(L.kf_events_dt(T, _ptr(t_ev), _ptr(e_ev), prev0, _lib.KF_DT_FULL, _ptr(dt), _ptr(et),
                                   kf._stream()))
         if cfg['parallel']:
-            # time-parallel: chunks of the log as filters of one launch (ref15.run_stream_parallel)
-            if ref15.run_stream_parallel(et, dt, pay, x0[:, 0], P0b) is not None:
-                return
-            fallbacks[0] += 1
+            # time-parallel (kf_run_stream): chunks of the log as filters, checked on the device
+            _lib.check(L.kf_run_stream(kf.handle, T, _ptr(et), _ptr(dt), _ptr(pay), _ptr(traj), None, _ptr(logdet),
+                                       None, 0, -1, kf._stream()))
+            if not stream_check:  # first (warm-up) step: record the device checks (synchronises)
+                stream_check.update(kf.stream_check())
+            return
         _lib.check(L.kf_run_events(kf.handle, T, _ptr(et), _ptr(dt), _ptr(pay), _ptr(traj), None, _ptr(logdet),
                                    None, 0, 0.0, kf._stream()))
 
@@ -381,17 +383,17 @@ def log_workload(cfg, args, rank, world, dev):
     per_event = 1 + 8 + 8 + 72 + 1 + 8 + 48 + 8   # dt pass (t, etype in; dt, etype out) + filter (in/out)
     if cfg['parallel']:
         return dict(step=step, units=T, bytes=per_event * T, bytes_per_unit=per_event,
-                    kernel='ref_chain_kernel (3 launches: warm-up, chunk maps, records) + host composition',
+                    kernel='ref_chain_kernel<f64,M15,stream> (warm-up, map and record passes) + stream_* kernels',
                     traffic=None, cpu=cpu, gather=None, kf=kf,
                     roofline_note='latency-bound: the warm-up + 2 chunk lengths of events in sequence; '
                                   'the fraction is not the figure of merit',
                     desc=f'BASELINE config 1: ONE 15-state filter (run_kalman_filter_full, kf_workers.py:623-728) '
                          f'over a whole drive log, {N} merged events ({stream.n_fixes} fixes + {stream.n_imu} IMU '
-                         f'at 200 Hz), f64; time-parallel (ref15.run_stream_parallel: chunks of the log as filters, '
-                         f'covariance warm-up + affine state maps, checked); synthetic log with the reference '
-                         f"log's shape",
+                         f'at 200 Hz), f64; time-parallel (kf_run_stream: chunks of the log as filters, '
+                         f'covariance warm-up + affine state maps composed on the device, checked, sequential '
+                         f"fallback); synthetic log with the reference log's shape",
                     extra={'events': N, 'events_filtered': T, 'csv_parse_ms': (t1 - t0) * 1e3,
-                           'kf_ingest_ms': (t2 - t1) * 1e3, 'filters': 1, 'fallbacks': fallbacks})
+                           'kf_ingest_ms': (t2 - t1) * 1e3, 'filters': 1, 'stream_check': stream_check})
     return dict(step=step, units=T, bytes=per_event * T, bytes_per_unit=per_event, kernel='ref_chain_kernel',
                 traffic=None, cpu=cpu, gather=None, kf=kf,
                 roofline_note='one filter: one wave whose per-event dependency chain bounds the rate (8 lanes, '

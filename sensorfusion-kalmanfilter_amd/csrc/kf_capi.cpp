@@ -2,6 +2,8 @@
 // and dispatch to the gfx950 kernels in kf_cv.hip.  No compute happens here.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <climits>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -30,6 +32,9 @@ struct kf_batch {
     bool r_diag;      // BASELINE models: R has no off-diagonal entry
     bool block_p;     // BASELINE models: every filter's P is block-diagonal over the axes
     int* flag;        // device int for the kf_set_state block check (allocated on first use)
+    void* stream_ws;  // kf_run_stream: chunk banks, maps, check (grown on demand)
+    size_t stream_ws_bytes;
+    int64_t s_chunks, s_len, s_warm;  // the last kf_run_stream's split (s_chunks = 1: sequential)
 };
 
 namespace {
@@ -314,6 +319,7 @@ int kf_free(kf_batch* h) {
     if (h->ws) (void)hipFree(h->ws);
     if (h->search_ws) (void)hipFree(h->search_ws);
     if (h->flag) (void)hipFree(h->flag);
+    if (h->stream_ws) (void)hipFree(h->stream_ws);
     delete h;
     return KF_OK;
 }
@@ -473,14 +479,12 @@ int kf_synth(kf_batch* h, uint64_t seed, int64_t filter_offset, int T, double dt
     return KF_OK;
 }
 
-int kf_run_events(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload,
-                  void* traj, void* cov, void* logdet, uint8_t* updated, int gate, double threshold,
-                  void* stream) {
-    if (int rc = check_handle(h)) return rc;
-    if (!is_ref(h)) return fail(KF_EINVAL, "kf_run_events: needs a KF_MODEL_REF15 or KF_MODEL_REF8 handle");
-    if (T < 0) return fail(KF_EINVAL, "kf_run_events: T = %d < 0", T);
-    if (T == 0 || h->B == 0) return KF_OK;
-    if (!etype || !dt || !payload) return fail(KF_EINVAL, "kf_run_events: null etype/dt/payload stream");
+namespace {
+
+// kf_run_events' kernel choice and launch (skip: device flag, see RefArgs::skip)
+int run_events_launch(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload, void* traj,
+                      void* cov, void* logdet, uint8_t* updated, int gate, double threshold, const int32_t* skip,
+                      void* stream) {
     kfmi::RefArgs a = ref_args(h);
     a.T = T;
     a.etype = etype;
@@ -492,6 +496,7 @@ int kf_run_events(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     a.updated = updated;
     a.gate = gate;
     a.threshold = threshold;
+    a.skip = skip;
     // Few filters cannot fill the chip one lane each: give every axis chain its own lane
     // (8 lanes per filter).  Otherwise one lane per filter, with the inputs staged through LDS
     // by DMA where its layout conditions hold.  KFMI_EVENTS_KERNEL=lane|chain|lds forces a
@@ -509,8 +514,157 @@ int kf_run_events(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
         else if (!std::strcmp(v, "lane")) variant = kfmi::kEventsLane;
         else if (!std::strcmp(v, "lds") && lds_ok) variant = kfmi::kEventsLds;
     }
+    if (skip && variant != kfmi::kEventsChain) return fail(KF_EINVAL, "kf_run_stream: fallback needs the chain kernel");
     hipError_t e = kfmi::launch_ref_events(h->model, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream), variant);
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_run_events");
+}
+
+// kf_run_events routes one-filter runs of at least this many events through kf_run_stream
+constexpr int kStreamMinEvents = 65536;
+constexpr int kStreamDefaultWarmup = 2048;
+constexpr int64_t kStreamTargetChunks = 2048;
+
+size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
+
+}  // namespace
+
+int kf_run_events(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload,
+                  void* traj, void* cov, void* logdet, uint8_t* updated, int gate, double threshold,
+                  void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (!is_ref(h)) return fail(KF_EINVAL, "kf_run_events: needs a KF_MODEL_REF15 or KF_MODEL_REF8 handle");
+    if (T < 0) return fail(KF_EINVAL, "kf_run_events: T = %d < 0", T);
+    if (T == 0 || h->B == 0) return KF_OK;
+    if (!etype || !dt || !payload) return fail(KF_EINVAL, "kf_run_events: null etype/dt/payload stream");
+    // one filter over a long stream: parallel over time (checked, with a sequential fallback)
+    const char* sv = std::getenv("KFMI_STREAM");
+    if (h->B == 1 && !gate && T >= kStreamMinEvents && !(sv && !std::strcmp(sv, "off")))
+        return kf_run_stream(h, T, etype, dt, payload, traj, cov, logdet, updated, 0, -1, stream);
+    return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, gate, threshold, nullptr, stream);
+}
+
+int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload, void* traj,
+                  void* cov, void* logdet, uint8_t* updated, int chunk, int warmup, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (!is_ref(h)) return fail(KF_EINVAL, "kf_run_stream: needs a KF_MODEL_REF15 or KF_MODEL_REF8 handle");
+    if (h->B != 1) return fail(KF_EINVAL, "kf_run_stream: needs a handle of one filter (B = %lld)", (long long)h->B);
+    if (T < 0) return fail(KF_EINVAL, "kf_run_stream: T = %d < 0", T);
+    if (T == 0) return KF_OK;
+    if (!etype || !dt || !payload) return fail(KF_EINVAL, "kf_run_stream: null etype/dt/payload stream");
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const int64_t L = chunk > 0 ? chunk : std::max<int64_t>(128, (int64_t(T) + kStreamTargetChunks - 1) / kStreamTargetChunks);
+    const int64_t C = (int64_t(T) + L - 1) / L;
+    const int64_t W = warmup >= 0 ? warmup : kStreamDefaultWarmup;
+    const size_t w = elem(h);
+    const int nblk = h->np, n = h->n;
+    const int nch = h->model == KF_MODEL_REF15 ? 6 : 3;
+    // stream offsets are 32-bit products (events before the start wrap past every length, and
+    // bit 31 marks dropped records): (T + W) rows of the widest record below 2^31 bytes
+    const bool fits = uint64_t(T + std::max<int64_t>(W, 0)) * uint64_t(std::max(nblk, 9)) * 8u < (uint64_t(1) << 31);
+    h->s_len = L;
+    h->s_warm = W;
+    if (C < 2 || !fits || L > INT32_MAX || W > INT32_MAX) {
+        h->s_chunks = 1;
+        return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, 0, 0.0, nullptr, stream);
+    }
+    h->s_chunks = C;
+    // workspace: check | banks W (C), M (4C), F (C) | maps | starts
+    const size_t bank1 = align256(size_t(n + nblk) * C * w) + align256(sizeof(int32_t) * C);
+    const size_t bank4 = align256(size_t(n + nblk) * 4 * C * w) + align256(sizeof(int32_t) * 4 * C);
+    const int64_t nseg = (C + kfmi::kStreamSegChunks - 1) / kfmi::kStreamSegChunks;
+    const size_t need = 256 + 2 * bank1 + bank4 + align256(sizeof(double) * 12 * nch * C) +
+                        align256(sizeof(double) * 15 * nch * nseg) + align256(sizeof(double) * n * C);
+    if (h->stream_ws_bytes < need) {
+        if (h->stream_ws) (void)hipFree(h->stream_ws);
+        h->stream_ws = nullptr;
+        h->stream_ws_bytes = 0;
+        if (hipMalloc(&h->stream_ws, need) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(KF_EHIP, "kf_run_stream: cannot allocate %zu bytes of chunk banks", need);
+        }
+        h->stream_ws_bytes = need;
+    }
+    char* p = static_cast<char*>(h->stream_ws);
+    kfmi::StreamArgs sa{};
+    sa.C = C;
+    sa.delta = 1024.0;  // the maps are affine: a large step only shrinks the roundoff of the differences
+    sa.tol_state = h->dtype == KF_F64 ? 1e-9 : 1e-4;
+    sa.tol_cov = h->dtype == KF_F64 ? 1e-12 : 1e-5;
+    sa.hx = h->x;
+    sa.hP = h->P;
+    sa.hstatus = h->status;
+    sa.check = reinterpret_cast<kfmi::StreamCheck*>(p);
+    p += 256;
+    auto bank = [&](int64_t B, void*& x, void*& P, int32_t*& status) {
+        x = p;
+        P = p + size_t(n) * B * w;
+        p += align256(size_t(n + nblk) * B * w);
+        status = reinterpret_cast<int32_t*>(p);
+        p += align256(sizeof(int32_t) * B);
+    };
+    bank(C, sa.wx, sa.wP, sa.wst);
+    bank(4 * C, sa.mx, sa.mP, sa.mst);
+    bank(C, sa.fx, sa.fP, sa.fst);
+    sa.maps = reinterpret_cast<double*>(p);
+    p += align256(sizeof(double) * 12 * nch * C);
+    sa.segmaps = reinterpret_cast<double*>(p);
+    sa.segstart = sa.segmaps + 12 * nch * nseg;
+    p += align256(sizeof(double) * 15 * nch * nseg);
+    sa.starts = reinterpret_cast<double*>(p);
+
+    const bool f64 = h->dtype == KF_F64;
+    auto chain = [&](int64_t B, void* x, void* P, int32_t* status, int64_t Tc, int64_t shift, bool records) {
+        kfmi::RefArgs a{};
+        a.B = B;
+        a.T = int(Tc);
+        a.etype = etype;
+        a.dt = dt;
+        a.payload = payload;
+        a.x = x;
+        a.P = P;
+        a.status = status;
+        if (records) {
+            a.traj = traj;
+            a.cov = cov;
+            a.logdet = logdet;
+            a.updated = updated;
+        }
+        a.s_len = T;
+        a.s_chunk = L;
+        a.s_shift = shift;
+        a.s_nchunks = C;
+        return kfmi::launch_ref_stream(h->model, f64, a, st);
+    };
+    hipError_t e = kfmi::launch_stream_phase(h->model, f64, 0, sa, st);
+    if (e == hipSuccess && W > 0) e = chain(C, sa.wx, sa.wP, sa.wst, W, -W, false);
+    if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, 1, sa, st);
+    if (e == hipSuccess) e = chain(4 * C, sa.mx, sa.mP, sa.mst, L, 0, false);
+    for (int ph = 2; ph <= 4 && e == hipSuccess; ++ph) e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
+    if (e == hipSuccess) e = chain(C, sa.fx, sa.fP, sa.fst, L, 0, true);
+    if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, 5, sa, st);
+    if (e != hipSuccess) return hip_fail(e, "kf_run_stream");
+    // the sequential run, which does nothing unless a check failed
+    return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, 0, 0.0, &sa.check->ok, stream);
+}
+
+int kf_stream_check(kf_batch* h, double* out, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (!out) return fail(KF_EINVAL, "kf_stream_check: null output");
+    if (!h->stream_ws && h->s_chunks != 1) return fail(KF_EINVAL, "kf_stream_check: no kf_run_stream on this handle");
+    kfmi::StreamCheck k{};
+    if (h->s_chunks > 1) {
+        hipError_t e = hipMemcpyAsync(&k, h->stream_ws, sizeof k, hipMemcpyDeviceToHost, static_cast<hipStream_t>(stream));
+        if (e == hipSuccess) e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+        if (e != hipSuccess) return hip_fail(e, "kf_stream_check");
+    }
+    out[0] = k.ok;
+    out[1] = k.bad ? 1.0 : 0.0;
+    out[2] = k.cov_gap;
+    out[3] = k.state_gap;
+    out[4] = double(h->s_chunks);
+    out[5] = double(h->s_len);
+    out[6] = double(h->s_warm);
+    return KF_OK;
 }
 
 int kf_eval_combos(kf_batch* h, int n_events, const double* events, const double* init, double prev_time,

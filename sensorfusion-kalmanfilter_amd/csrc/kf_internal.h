@@ -63,7 +63,52 @@ struct RefArgs {
     uint8_t* updated;        // [T][B] 1 if the event's update was applied, or nullptr
     int gate;                // adaptive threshold (kf_workers.py:1023-1025): update only if
     double threshold;        //   logdet(P_pred) > threshold
+    // Stream mode (kf_run_stream, chain kernel only): ONE event stream of s_len events, laid
+    // out as a single filter's [S] / [S][9] / records [S][W] ...; filter f runs the events
+    // (f % s_nchunks) * s_chunk + s_shift + t, t < T; events outside [0, S) are skipped and
+    // record nothing.  s_len = 0: the per-filter [T][B] layout above.
+    int64_t s_len;
+    int64_t s_chunk;
+    int64_t s_shift;
+    int64_t s_nchunks;
+    const int32_t* skip;     // if non-null and *skip != 0, the launch does nothing
 };
+
+// Time-parallel run of one filter over a long event stream (kf_run_stream): the state banks of
+// the three chunk passes and the check.  Bank layouts are the handle's ([N][B], [NBLK][B]).
+struct StreamCheck {
+    int32_t ok;              // 1: the chunked run passed every check, its records stand
+    int32_t bad;             // a chunk filter failed (non-SPD)
+    double cov_gap;          // max over chunk seams of the warm-up covariance's relative gap
+    double state_gap;        // max over chunk seams of |end state - next start| / max(|start|, 1)
+};
+struct StreamArgs {
+    int64_t C;               // chunks
+    double delta;            // state perturbation of the map pass
+    double tol_state, tol_cov;
+    void* hx;                // handle state (one filter): [N], [NBLK], status
+    void* hP;
+    int32_t* hstatus;
+    void* wx;                // warm-up bank [.][C]: each chunk's start covariance and a state guess
+    void* wP;
+    int32_t* wst;
+    void* mx;                // map bank [.][4C]: guess + 0 / delta e_q (q = chain component)
+    void* mP;
+    int32_t* mst;
+    void* fx;                // final bank [.][C]: the true chunk starts, run with the records
+    void* fP;
+    int32_t* fst;
+    double* maps;            // [C][chains][12]: per chunk and chain, A (3x3) and b of x_end = A x_start + b
+    double* segmaps;         // [C / kStreamSeg][chains][12]: the product of a segment's chunk maps
+    double* segstart;        // [C / kStreamSeg][chains][3]: each segment's start
+    double* starts;          // [N][C] the chunk starts (fp64)
+    StreamCheck* check;
+};
+// phase 0: warm-up bank from the handle, check zeroed; 1: map bank from the warm-up bank;
+// 2: chunk maps, segment products, covariance seam check; 3: segment starts; 4: chunk starts
+// into the final bank; 5: state seam check, verdict, and (if it passed) the handle's final state
+constexpr int kStreamSegChunks = 64;  // chunks per segment (kStreamSeg in kf_ref.hip)
+hipError_t launch_stream_phase(int model, bool f64, int phase, const StreamArgs& a, hipStream_t stream);
 
 // Brute-force search over k-subsets of n candidate events (kf_workers.py:22-97, 1218-1392):
 // lane f evaluates combination number combo_offset + f in itertools.combinations order.
@@ -167,6 +212,8 @@ hipError_t launch_synth(int axes, bool f64, const SynthArgs& a, hipStream_t stre
 // per axis chain (few filters), one lane per filter with inputs staged through LDS by DMA
 constexpr int kEventsLane = 0, kEventsChain = 1, kEventsLds = 2;
 hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, int variant);
+// the chain kernel in stream mode (a.s_len > 0)
+hipError_t launch_ref_stream(int model, bool f64, const RefArgs& a, hipStream_t stream);
 hipError_t launch_ref_reset(int model, bool f64, const RefArgs& a, hipStream_t stream);
 hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream);
 // child_major: one wave per (parent block, child event) instead of one lane per parent

@@ -476,6 +476,10 @@ constexpr int kGroup = 8;
 #define KF_CHAIN_DEPTH 2
 #endif
 constexpr int kChainDepth = KF_CHAIN_DEPTH;  // input ring of ref_chain_kernel
+#ifndef KF_STREAM_DEPTH
+#define KF_STREAM_DEPTH 8
+#endif
+constexpr int kStreamDepth = KF_STREAM_DEPTH;  // its input ring in stream mode (kf_run_stream)
 
 // Sums / ORs over the 8-lane group with DPP (a VALU-latency lane exchange, no LDS round trip):
 // quad_perm [1,0,3,2] (xor 1), quad_perm [2,3,0,1] (xor 2), then row_half_mirror (lane i <-> 7-i
@@ -532,8 +536,9 @@ struct ChainIn {
     T va, vb;
 };
 
-template <typename T, class M>
+template <typename T, class M, bool STREAM>
 __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
+    if (a.skip && *a.skip) return;  // the sequential fallback of a stream run that passed its checks
     const int64_t g = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     const int64_t f = g / kGroup;
     if (f >= a.B) return;  // whole groups leave together (kGroup divides the wave)
@@ -578,12 +583,42 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     int32_t st = a.status[f];
     const bool need_ld = a.logdet != nullptr;
 
+    // stream mode: this filter's event t is stream event e0 + t; one descriptor per stream
+    // (events outside [0, S) are skipped: dropped loads, NONE type, dropped records)
+    const int64_t e0 = STREAM ? (f % a.s_nchunks) * a.s_chunk + a.s_shift : 0;
+    const uint32_t S = STREAM ? uint32_t(a.s_len) : 0u;
+    const auto r_et = bytes_rsrc(a.etype, S), r_dt = bytes_rsrc(a.dt, S * 8u);
+    const auto r_pay = bytes_rsrc(a.payload, S * 9u * uint32_t(sizeof(T)));
+    const auto r_str = bytes_rsrc(a.traj, S * uint32_t(M::NTRAJ * sizeof(T)));
+    const auto r_scv = bytes_rsrc(a.cov, S * uint32_t(M::NBLK * sizeof(T)));
+    const auto r_sld = bytes_rsrc(a.logdet, S * uint32_t(sizeof(T)));
+    const auto r_sup = bytes_rsrc(a.updated, S);
+    // Stream offsets are plain 32-bit products of ue = uint32(e): an event before the stream
+    // start wraps far past every descriptor's length and one past its end lands beyond it, so
+    // loads return 0 and stores drop without a select on the address (a select there was turned
+    // into branches around the loads, whose joins drained the prefetch ring with vmcnt(0)).
+    // Lanes without a record OR in bit 31 (kf_run_stream keeps (S + W) * rows * w < 2^31).
+    const uint32_t m_tr = v_tr != kDropOffset ? 0u : kDropOffset;
+    const uint32_t col_tr = v_tr != kDropOffset ? uint32_t(xi[0]) * uint32_t(sizeof(T)) : 0u;
+    const uint32_t m_ld = c == 0 ? 0u : kDropOffset;
+    uint32_t col_cv[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) col_cv[k] = pr[k] >= 0 ? uint32_t(pr[k]) * uint32_t(sizeof(T)) : kDropOffset;
     auto load = [&](int t, ChainIn<T>& in) {
-        in.type = int(ldb<uint8_t>(a.etype, t, uint32_t(a.B), uint32_t(f)));
-        in.dt = ldb<double>(a.dt, t, rb8, off8);
-        const auto rpay = span_rsrc(a.payload, int64_t(t) * 9, rb, 9);
-        in.va = ldv(rpay, v_a, T(0));
-        in.vb = ldv(rpay, v_b, T(0));
+        if constexpr (STREAM) {
+            const uint32_t ue = uint32_t(e0 + t);
+            const int ty = int(__builtin_amdgcn_raw_buffer_load_b8(r_et, ue, 0, 0));
+            in.type = ue < S ? ty : 255;
+            in.dt = ldv(r_dt, ue * 8u, 0.0);
+            in.va = ldv(r_pay, (ue * 9u + uint32_t(ia)) * uint32_t(sizeof(T)), T(0));
+            in.vb = ldv(r_pay, (ue * 9u + uint32_t(ib)) * uint32_t(sizeof(T)), T(0));
+        } else {
+            in.type = int(ldb<uint8_t>(a.etype, t, uint32_t(a.B), uint32_t(f)));
+            in.dt = ldb<double>(a.dt, t, rb8, off8);
+            const auto rpay = span_rsrc(a.payload, int64_t(t) * 9, rb, 9);
+            in.va = ldv(rpay, v_a, T(0));
+            in.vb = ldv(rpay, v_b, T(0));
+        }
     };
     auto step = [&](int t, const ChainIn<T>& in) {
         const int type = in.type;
@@ -643,18 +678,31 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
                 for (int k = 0; k < 6; ++k) P[k] = quiet_nan<T>();
             }
         }
-        stv(span_rsrc(a.traj, int64_t(t) * M::NTRAJ, rb, M::NTRAJ), v_tr, x[0]);
-        {
-            const auto rc = span_rsrc(a.cov, int64_t(t) * M::NBLK, rb, M::NBLK);
+        if constexpr (STREAM) {
+            const uint32_t ue = uint32_t(e0 + t);
+            stv(r_str, (ue * uint32_t(M::NTRAJ * sizeof(T)) + col_tr) | m_tr, x[0]);
 #pragma unroll
-            for (int k = 0; k < 6; ++k) stv(rc, vp[k], P[k]);
+            for (int k = 0; k < 6; ++k) stv(r_scv, (ue * uint32_t(M::NBLK * sizeof(T)) + col_cv[k]) | (col_cv[k] & kDropOffset), P[k]);
+            if (need_ld) {
+                const T ld = group_sum(live ? chain_log_det(P) : T(0));
+                st = (ld == ld) ? st : kNotSpd;
+                stv(r_sld, (ue * uint32_t(sizeof(T))) | m_ld, ld);
+            }
+            __builtin_amdgcn_raw_buffer_store_b8(applied ? uint8_t(1) : uint8_t(0), r_sup, ue | m_ld, 0, 0);
+        } else {
+            stv(span_rsrc(a.traj, int64_t(t) * M::NTRAJ, rb, M::NTRAJ), v_tr, x[0]);
+            {
+                const auto rc = span_rsrc(a.cov, int64_t(t) * M::NBLK, rb, M::NBLK);
+#pragma unroll
+                for (int k = 0; k < 6; ++k) stv(rc, vp[k], P[k]);
+            }
+            if (need_ld) {
+                const T ld = group_sum(live ? chain_log_det(P) : T(0));
+                st = (ld == ld) ? st : kNotSpd;
+                stv(span_rsrc(a.logdet, t, rb, 1), v_ld, ld);
+            }
+            if (a.updated && c == 0) a.updated[int64_t(t) * a.B + f] = applied ? 1 : 0;
         }
-        if (need_ld) {
-            const T ld = group_sum(live ? chain_log_det(P) : T(0));
-            st = (ld == ld) ? st : kNotSpd;
-            stv(span_rsrc(a.logdet, t, rb, 1), v_ld, ld);
-        }
-        if (a.updated && c == 0) a.updated[int64_t(t) * a.B + f] = applied ? 1 : 0;
     };
 
     // Inputs are prefetched kChainDepth - 1 events ahead through a fully unrolled ring of named
@@ -664,7 +712,9 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     // a single wave's launch time varies +-10% from launch to launch
     // (profiles/r01_ab/chain_depth_inproc.json), and each depth adds a copy of the event body
     // (48 KB of code at 8), so the default stays at 2.
-    constexpr int D = kChainDepth;
+    // stream mode gathers each filter's events from its own part of the stream (a cache line
+    // per 1.8 events, lines differ per filter), so its loads see HBM latency: a deeper ring
+    constexpr int D = STREAM ? kStreamDepth : kChainDepth;
     const int T_ = a.T;
     auto load_c = [&](int t, ChainIn<T>& in) { load(t < T_ ? t : T_ - 1, in); };
     if (T_ > 0) {
@@ -692,6 +742,329 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
         for (int k = 0; k < 6; ++k) stv(rp, vp[k], P[k]);
     }
     if (c == 0) a.status[f] = st;
+}
+
+// ------------------------------------------------------------------------------------
+// Time-parallel run of ONE filter over a long event stream (kf_run_stream; the reference's own
+// use of run_kalman_filter_full, kf_workers.py:623-728, is one filter over a whole drive log).
+// The stream is cut into C chunks of L events that run as filters of the chain kernel:
+//  * the covariance recursion does not depend on the measurements and forgets its start, so
+//    chunk c's start covariance is the warm-up bank's: chunk c run over the W events before it
+//    from the handle's state (chunks within W of the stream start begin at event 0: exact);
+//  * given the gains, the state recursion is affine (the IMU pseudo-measurement is built from
+//    the predicted state, kf_workers.py:698-706, which keeps it affine), and block-diagonal
+//    over the axis chains: the map bank runs each chunk from a guess and from three perturbed
+//    guesses (one per chain component), giving x_end = A x_start + b per chunk and chain;
+//  * the maps are composed from the handle's state (segment products, then the segments in
+//    order) into every chunk's true start, and the final bank runs the chunks from them with
+//    the records;
+//  * checks: each warm-up covariance equals the previous chunk's end covariance, each chunk's
+//    final end state its successor's start, no chunk filter failed.  Only then does the
+//    handle take the last chunk's end state; otherwise the sequential chain kernel, launched
+//    after these with skip = &check.ok, runs the stream as one filter and rewrites every record.
+// ------------------------------------------------------------------------------------
+constexpr int kStreamSeg = kStreamSegChunks;  // chunks per segment of the map composition
+
+template <class M>
+__device__ __forceinline__ int chain_state(int a, int q) {  // chain a (pva chains first), component q; -1: none
+    return a < M::NP ? M::pva(a, q) : (q < 2 ? M::aw(a - M::NP, q) : -1);
+}
+template <class M>
+__device__ __forceinline__ int chain_row0(int a) {  // first block-packed covariance row of chain a
+    return a < M::NP ? 6 * a : 6 * M::NP + 3 * (a - M::NP);
+}
+template <class M>
+__device__ __forceinline__ int state_component(int i) {  // component of state i within its chain
+    int comp = 0;
+#pragma unroll
+    for (int a = 0; a < M::NP + M::NA; ++a)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            if (chain_state<M>(a, q) == i) comp = q;
+    return comp;
+}
+// non-negative doubles (and +NaN) order as their bit patterns: atomic max via uint64
+__device__ __forceinline__ void atomic_max_pos(double* p, double v) {
+    if (!(v >= 0.0)) v = __builtin_nan("");
+    atomicMax(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v));
+}
+
+// phase 0: every chunk of the warm-up bank starts from the handle's state; check zeroed
+template <typename T, class M>
+__global__ __launch_bounds__(kBlock) void stream_init_kernel(const StreamArgs a) {
+    const int64_t c = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (c == 0) {
+        a.check->ok = 0;
+        a.check->bad = 0;
+        a.check->cov_gap = 0.0;
+        a.check->state_gap = 0.0;
+    }
+    if (c >= a.C) return;
+    const T* hx = static_cast<const T*>(a.hx);
+    const T* hP = static_cast<const T*>(a.hP);
+#pragma unroll
+    for (int i = 0; i < M::N; ++i) static_cast<T*>(a.wx)[i * a.C + c] = hx[i];
+#pragma unroll
+    for (int r = 0; r < M::NBLK; ++r) static_cast<T*>(a.wP)[r * a.C + c] = hP[r];
+    a.wst[c] = a.hstatus[0];
+}
+
+// phase 1: map bank filter q * C + c = chunk c from its warm-up state, + delta on component q - 1
+// of every chain (q = 0: the guess itself)
+template <typename T, class M>
+__global__ __launch_bounds__(kBlock) void stream_perturb_kernel(const StreamArgs a) {
+    const int64_t f = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    const int64_t B = 4 * a.C;
+    if (f >= B) return;
+    const int q = int(f / a.C);
+    const int64_t c = f % a.C;
+#pragma unroll
+    for (int i = 0; i < M::N; ++i) {
+        const T g = static_cast<const T*>(a.wx)[i * a.C + c];
+        static_cast<T*>(a.mx)[i * B + f] = (q > 0 && state_component<M>(i) == q - 1) ? g + T(a.delta) : g;
+    }
+#pragma unroll
+    for (int r = 0; r < M::NBLK; ++r) static_cast<T*>(a.mP)[r * B + f] = static_cast<const T*>(a.wP)[r * a.C + c];
+    a.mst[f] = a.wst[c];
+}
+
+// phase 2 (blocks of kStreamSeg chunks x NCH chains): per (chunk, chain) the affine map
+// x_end = A x_start + b (fp64; maps[c][a][0:9] = A row-major, [9:12] = b), the covariance
+// seam (the chunk's warm-up covariance against its predecessor's end covariance, relative to
+// the predecessor's largest entry in the chain), and per block and chain the product of its
+// chunk maps in order (segmaps[block][a]), composed in LDS by one thread per chain
+template <class M>
+__device__ __forceinline__ void compose_into(double (&A)[3][3], double (&b)[3], const double* m) {
+    // (A, b) <- m o (A, b): A = Am A, b = Am b + bm
+    double An[3][3], bn[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        double t = m[9 + k];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) t = __builtin_fma(m[k * 3 + q], b[q], t);
+        bn[k] = t;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            double u = 0.0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) u = __builtin_fma(m[k * 3 + q], A[q][j], u);
+            An[k][j] = u;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        b[k] = bn[k];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) A[k][j] = An[k][j];
+    }
+}
+__device__ __forceinline__ void apply_map(double (&x)[3], const double* m) {
+    double xn[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        double t = m[9 + k];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) t = __builtin_fma(m[k * 3 + q], x[q], t);
+        xn[k] = t;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) x[k] = xn[k];
+}
+
+template <typename T, class M>
+__global__ __launch_bounds__(1024) void stream_maps_kernel(const StreamArgs a) {
+    constexpr int NCH = M::NP + M::NA;
+    __shared__ double lm[NCH][kStreamSeg][12];
+    const int tid = int(threadIdx.x);
+    const int ch = tid / kStreamSeg, j = tid % kStreamSeg;
+    const int64_t c = int64_t(blockIdx.x) * kStreamSeg + j;
+    const int64_t B = 4 * a.C;
+    const T* mx = static_cast<const T*>(a.mx);
+    const T* wx = static_cast<const T*>(a.wx);
+    const int ns = ch < M::NP ? 3 : 2;
+    double A[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, b[3] = {};  // past the last chunk: identity
+    if (c < a.C) {
+        double gs[3] = {};
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            if (q < ns) gs[q] = double(wx[chain_state<M>(ch, q) * a.C + c]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (k >= ns) continue;
+            const int i = chain_state<M>(ch, k);
+            const double e0 = double(mx[i * B + c]);
+            double s = e0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                if (q >= ns) continue;
+                A[k][q] = (double(mx[i * B + (q + 1) * a.C + c]) - e0) / a.delta;
+                s = __builtin_fma(-A[k][q], gs[q], s);
+            }
+            b[k] = s;
+        }
+        int bad = 0;
+        if (ch == 0) {
+            bad |= a.wst[c];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bad |= a.mst[q * a.C + c];
+        }
+        if (bad) atomicOr(&a.check->bad, 1);
+        if (c >= 1) {
+            const T* mP = static_cast<const T*>(a.mP);
+            const T* wP = static_cast<const T*>(a.wP);
+            const int r0 = chain_row0<M>(ch), nr = ns == 3 ? 6 : 3;
+            double scale = 0.0, gap = 0.0;
+            for (int r = r0; r < r0 + nr; ++r) {
+                const double pe = double(mP[r * B + (c - 1)]);
+                scale = fmax(scale, fabs(pe));
+                gap = fmax(gap, fabs(pe - double(wP[r * a.C + c])));
+            }
+            const double rel = gap / fmax(scale, 1e-300);
+            if (rel != 0.0 || !(rel == rel)) atomic_max_pos(&a.check->cov_gap, rel);
+        }
+    }
+    double* m = lm[ch][j];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) m[k * 3 + q] = A[k][q];
+        m[9 + k] = b[k];
+    }
+    if (c < a.C) {
+        double* g = a.maps + (c * NCH + ch) * 12;
+#pragma unroll
+        for (int e = 0; e < 12; ++e) g[e] = m[e];
+    }
+    __syncthreads();
+    if (j == 0) {
+        double SA[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, Sb[3] = {0, 0, 0};
+        for (int jj = 0; jj < kStreamSeg; ++jj) compose_into<M>(SA, Sb, lm[ch][jj]);
+        double* g = a.segmaps + (int64_t(blockIdx.x) * NCH + ch) * 12;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) g[k * 3 + q] = SA[k][q];
+            g[9 + k] = Sb[k];
+        }
+    }
+}
+
+// phase 3 (one block): the segment products in order from the handle's state give every
+// segment's start (segstart[block][a]); tiles of kStreamSeg segments are staged through LDS
+template <typename T, class M>
+__global__ __launch_bounds__(1024) void stream_segscan_kernel(const StreamArgs a) {
+    constexpr int NCH = M::NP + M::NA;
+    __shared__ double lm[kStreamSeg * NCH * 12];
+    const int tid = int(threadIdx.x);
+    const int64_t nseg = (a.C + kStreamSeg - 1) / kStreamSeg;
+    double x[3] = {0, 0, 0};
+    if (tid < NCH) {
+        const int ns = tid < M::NP ? 3 : 2;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            if (q < ns) x[q] = double(static_cast<const T*>(a.hx)[chain_state<M>(tid, q)]);
+    }
+    for (int64_t s0 = 0; s0 < nseg; s0 += kStreamSeg) {
+        const int64_t n = (nseg - s0 < kStreamSeg ? nseg - s0 : kStreamSeg) * NCH * 12;
+        __syncthreads();
+        for (int64_t e = tid; e < n; e += blockDim.x) lm[e] = a.segmaps[s0 * NCH * 12 + e];
+        __syncthreads();
+        if (tid < NCH) {
+            for (int64_t s = s0; s < s0 + n / (NCH * 12); ++s) {
+                double* g = a.segstart + (s * NCH + tid) * 3;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) g[k] = x[k];
+                apply_map(x, lm + ((s - s0) * NCH + tid) * 12);
+            }
+        }
+    }
+}
+
+// phase 4 (blocks of kStreamSeg chunks x NCH chains): each block stages its chunk maps in LDS,
+// one thread per chain walks them from its segment's start, writing every chunk start (fp64,
+// and the final bank's x); the final bank's P is the warm-up bank's, its status 0
+template <typename T, class M>
+__global__ __launch_bounds__(1024) void stream_apply_kernel(const StreamArgs a) {
+    constexpr int NCH = M::NP + M::NA;
+    __shared__ double lm[NCH][kStreamSeg][12];
+    const int tid = int(threadIdx.x);
+    const int ch = tid / kStreamSeg, j = tid % kStreamSeg;
+    const int64_t c = int64_t(blockIdx.x) * kStreamSeg + j;
+    if (c < a.C) {
+        const double* g = a.maps + (c * NCH + ch) * 12;
+#pragma unroll
+        for (int e = 0; e < 12; ++e) lm[ch][j][e] = g[e];
+        if (ch == 0) {
+#pragma unroll
+            for (int r = 0; r < M::NBLK; ++r)
+                static_cast<T*>(a.fP)[r * a.C + c] = static_cast<const T*>(a.wP)[r * a.C + c];
+            a.fst[c] = 0;
+        }
+    }
+    __syncthreads();
+    if (j == 0) {
+        const int ns = ch < M::NP ? 3 : 2;
+        const double* g = a.segstart + (int64_t(blockIdx.x) * NCH + ch) * 3;
+        double x[3] = {g[0], g[1], g[2]};
+        const int64_t c0 = int64_t(blockIdx.x) * kStreamSeg;
+        const int n = a.C - c0 < kStreamSeg ? int(a.C - c0) : kStreamSeg;
+        for (int jj = 0; jj < n; ++jj) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                if (k >= ns) continue;
+                const int i = chain_state<M>(ch, k);
+                a.starts[i * a.C + c0 + jj] = x[k];
+                static_cast<T*>(a.fx)[i * a.C + c0 + jj] = T(x[k]);
+            }
+            apply_map(x, lm[ch][jj]);
+        }
+    }
+}
+
+// phase 4 (one block): the state seams and the verdict; a passed run leaves the last chunk's
+// end state in the handle
+template <typename T, class M>
+__global__ __launch_bounds__(1024) void stream_finish_kernel(const StreamArgs a) {
+    __shared__ double red[1024];
+    __shared__ int redb[1024];
+    const int tid = int(threadIdx.x);
+    const T* fx = static_cast<const T*>(a.fx);
+    double gap = 0.0;
+    int bad = 0;
+    for (int64_t c = tid; c < a.C; c += blockDim.x) {
+        bad |= a.fst[c];
+        if (c + 1 < a.C) {
+#pragma unroll
+            for (int i = 0; i < M::N; ++i) {
+                const double st = a.starts[i * a.C + c + 1];
+                const double d = fabs(double(fx[i * a.C + c]) - st) / fmax(fabs(st), 1.0);
+                gap = (d == d) ? fmax(gap, d) : __builtin_inf();
+            }
+        }
+    }
+    red[tid] = gap;
+    redb[tid] = bad;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (tid < w) {
+            red[tid] = fmax(red[tid], red[tid + w]);
+            redb[tid] |= redb[tid + w];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        StreamCheck* k = a.check;
+        k->state_gap = red[0];
+        k->bad |= redb[0];
+        const bool ok = k->bad == 0 && k->cov_gap <= a.tol_cov && red[0] <= a.tol_state;
+        k->ok = ok ? 1 : 0;
+        if (ok) {
+            const int64_t c = a.C - 1;
+            for (int i = 0; i < M::N; ++i) static_cast<T*>(a.hx)[i] = fx[i * a.C + c];
+            for (int r = 0; r < M::NBLK; ++r) static_cast<T*>(a.hP)[r] = static_cast<const T*>(a.fP)[r * a.C + c];
+            a.hstatus[0] = 0;
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1311,11 +1684,11 @@ hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t 
     if (variant == kEventsChain) {
         const dim3 cgrid(static_cast<unsigned>((a.B * kGroup + kBlock - 1) / kBlock));
         if (model == 15) {
-            if (f64) ref_chain_kernel<double, M15><<<cgrid, kBlock, 0, stream>>>(a);
-            else ref_chain_kernel<float, M15><<<cgrid, kBlock, 0, stream>>>(a);
+            if (f64) ref_chain_kernel<double, M15, false><<<cgrid, kBlock, 0, stream>>>(a);
+            else ref_chain_kernel<float, M15, false><<<cgrid, kBlock, 0, stream>>>(a);
         } else if (model == 8) {
-            if (f64) ref_chain_kernel<double, M8><<<cgrid, kBlock, 0, stream>>>(a);
-            else ref_chain_kernel<float, M8><<<cgrid, kBlock, 0, stream>>>(a);
+            if (f64) ref_chain_kernel<double, M8, false><<<cgrid, kBlock, 0, stream>>>(a);
+            else ref_chain_kernel<float, M8, false><<<cgrid, kBlock, 0, stream>>>(a);
         } else {
             return hipErrorInvalidValue;
         }
@@ -1328,6 +1701,50 @@ hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t 
     } else if (model == 8) {
         if (f64) ref_events_kernel<double, M8><<<grid, kBlock, 0, stream>>>(a);
         else ref_events_kernel<float, M8><<<grid, kBlock, 0, stream>>>(a);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_ref_stream(int model, bool f64, const RefArgs& a, hipStream_t stream) {
+    if (a.s_len <= 0 || a.s_nchunks <= 0) return hipErrorInvalidValue;
+    const dim3 cgrid(static_cast<unsigned>((a.B * kGroup + kBlock - 1) / kBlock));
+    if (model == 15) {
+        if (f64) ref_chain_kernel<double, M15, true><<<cgrid, kBlock, 0, stream>>>(a);
+        else ref_chain_kernel<float, M15, true><<<cgrid, kBlock, 0, stream>>>(a);
+    } else if (model == 8) {
+        if (f64) ref_chain_kernel<double, M8, true><<<cgrid, kBlock, 0, stream>>>(a);
+        else ref_chain_kernel<float, M8, true><<<cgrid, kBlock, 0, stream>>>(a);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <typename T, class M>
+void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
+    constexpr int NCH = M::NP + M::NA;
+    auto grid = [](int64_t n) { return dim3(static_cast<unsigned>((n + kBlock - 1) / kBlock)); };
+    const dim3 segs(static_cast<unsigned>((a.C + kStreamSeg - 1) / kStreamSeg));
+    switch (phase) {
+        case 0: stream_init_kernel<T, M><<<grid(a.C), kBlock, 0, stream>>>(a); break;
+        case 1: stream_perturb_kernel<T, M><<<grid(4 * a.C), kBlock, 0, stream>>>(a); break;
+        case 2: stream_maps_kernel<T, M><<<segs, NCH * kStreamSeg, 0, stream>>>(a); break;
+        case 3: stream_segscan_kernel<T, M><<<1, 1024, 0, stream>>>(a); break;
+        case 4: stream_apply_kernel<T, M><<<segs, NCH * kStreamSeg, 0, stream>>>(a); break;
+        default: stream_finish_kernel<T, M><<<1, 1024, 0, stream>>>(a); break;
+    }
+}
+
+hipError_t launch_stream_phase(int model, bool f64, int phase, const StreamArgs& a, hipStream_t stream) {
+    if (a.C < 2 || phase < 0 || phase > 5) return hipErrorInvalidValue;
+    if (model == 15) {
+        if (f64) stream_phase<double, M15>(phase, a, stream);
+        else stream_phase<float, M15>(phase, a, stream);
+    } else if (model == 8) {
+        if (f64) stream_phase<double, M8>(phase, a, stream);
+        else stream_phase<float, M8>(phase, a, stream);
     } else {
         return hipErrorInvalidValue;
     }

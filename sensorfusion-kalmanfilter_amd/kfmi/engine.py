@@ -274,6 +274,34 @@ class BatchedKF:
                                        self._stream()))
         return tr, ld, up, cv
 
+    def run_stream(self, etype, dt, payload, traj=True, logdet=True, updated=False, cov=False, chunk=0,
+                   warmup=-1):
+        """One filter (a handle of batch 1) over a long event stream, parallel over time
+        (kf_run_stream): etype [T] uint8, dt [T] float64, payload [T, 9].  Same outputs as
+        run_events with B = 1 ([T, W, 1], [T, 1], ...).  chunk <= 0 / warmup < 0: the library's
+        defaults.  stream_check() tells whether the chunked records stood or the sequential
+        fallback rewrote them."""
+        if self.model not in REF_MODELS or self.batch != 1:
+            raise ValueError('run_stream needs a ref15 or ref8 handle of one filter')
+        T = int(etype.shape[0])
+        et = self._dev(etype.reshape(T, 1), (T, 1), 'etype', torch.uint8)
+        dtd = self._dev(dt.reshape(T, 1), (T, 1), 'dt', torch.float64)
+        pay = self._dev(payload.reshape(T, 9, 1), (T, 9, 1), 'payload')
+        tr = self.empty(T, TRAJ_WIDTH[self.model], 1) if traj else None
+        ld = self.empty(T, 1) if logdet else None
+        up = torch.empty(T, 1, dtype=torch.uint8, device=self.device) if updated else None
+        cv = self.empty(T, self.ntri, 1) if cov else None
+        check(_lib.lib().kf_run_stream(self.handle, T, _ptr(et), _ptr(dtd), _ptr(pay), _ptr(tr), _ptr(cv), _ptr(ld),
+                                       _ptr(up), int(chunk), int(warmup), self._stream()))
+        return tr, ld, up, cv
+
+    def stream_check(self):
+        """The checks of the last run_stream (kf_stream_check; synchronises the stream)."""
+        out = (ctypes.c_double * 7)()
+        check(_lib.lib().kf_stream_check(self.handle, out, self._stream()))
+        return dict(ok=bool(out[0]), failed_chunk=bool(out[1]), cov_gap=out[2], state_gap=out[3],
+                    chunks=int(out[4]), chunk=int(out[5]), warmup=int(out[6]))
+
     def eval_combos(self, events, init, prev_time, target_end, k, combo_offset=0, logdets=True):
         """KF_MODEL_REF15 brute force (kf_eval_combos): filter f evaluates combination
         combo_offset + f of k out of the n candidate events.  events: host [n, 11] float64

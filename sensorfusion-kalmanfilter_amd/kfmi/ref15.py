@@ -23,7 +23,9 @@ reference itself produces is, exactly (see csrc/kf_ref15.hip).
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import os
 
 import numpy as np
 import torch
@@ -198,13 +200,31 @@ def run_kalman_filter_full(events, start_idx=None, end_idx=None, initial_pt=None
     return states, logdets, from_blocks(Pb[:, 0]), prev
 
 
+@contextlib.contextmanager
+def _stream_route(allowed):
+    """kf_run_events sends a long one-filter run through kf_run_stream by itself; with
+    allowed=False it runs the single filter (KFMI_STREAM=off for the call)."""
+    if allowed:
+        yield
+        return
+    old = os.environ.get('KFMI_STREAM')
+    os.environ['KFMI_STREAM'] = 'off'
+    try:
+        yield
+    finally:
+        if old is None:
+            del os.environ['KFMI_STREAM']
+        else:
+            os.environ['KFMI_STREAM'] = old
+
+
 def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initial_state=None, dtype='f64',
                     cov=False, parallel=True, parallel_min_events=1 << 16):
     """run_kalman_filter_full (kf_workers.py:623-728) over an EventStream window, entirely on
     the device: cold-start fix search, per-event dt with the driver's dt < 0 rule
     (kf_events_dt, KF_DT_FULL) and one single-filter kf_run_events launch — or, for windows of
-    at least ``parallel_min_events`` events, ``run_stream_parallel`` (chunks of the window as
-    filters of one launch; it falls back to the single filter if a check fails).  Returns NumPy
+    at least ``parallel_min_events`` events, kf_run_stream (chunks of the window as filters of
+    one launch, checked on the device, with the single filter as its fallback).  Returns NumPy
     (t [R], traj [R, 6], logdet [R], P 15x15, prev_time) with R = 1 + processed events (plus
     the block-packed per-record covariances [R, 27] with cov=True), or None when a cold window
     holds no fix."""
@@ -244,17 +264,12 @@ def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initi
     et = torch.cat([torch.full((1,), NONE, dtype=torch.uint8, device=dev), et])
     dt = torch.cat([torch.zeros(1, dtype=torch.float64, device=dev), dt])
     pay = torch.cat([torch.zeros(1, 9, dtype=pay.dtype, device=dev), pay])
-    par = None
     if parallel and T + 1 >= parallel_min_events:
-        par = run_stream_parallel(et, dt, pay, x0, to_blocks(P), dtype=dtype, cov=cov)
-    if par is not None:
-        tr, ld, xe, Pe, cv = par
-        tr, ld = tr[:, :, None], ld[:, None]
-        cv = cv[:, :, None] if cov else None
-        x, Pb = xe[:, None], Pe[:, None]
+        tr, ld, _, cv = kf.run_stream(et, dt, pay, cov=cov)
     else:
-        tr, ld, _, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None], cov=cov)
-        x, Pb = kf.state()
+        with _stream_route(parallel):
+            tr, ld, _, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None], cov=cov)
+    x, Pb = kf.state()
     keep = et != NONE
     keep[0] = True
     t_all = torch.cat([torch.full((1,), t_first, dtype=torch.float64, device=dev), t])
@@ -272,150 +287,32 @@ def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initi
 # filter over a whole drive log, kf_workers.py:623-728)
 # --------------------------------------------------------------------------------------------
 
-# state indices of each chain: pva chain a = (pos_a, vel_a, acc_a), aw chain a = (att_a, rate_a)
-_CHAINS = [(a, 6 + a, 12 + a) for a in range(3)] + [(3 + a, 9 + a) for a in range(3)]
-# (row, column, component) of every within-chain entry of a chunk's state map
-_MAP_ENTRIES = [(r, col, q) for ch in _CHAINS for r in ch for q, col in enumerate(ch)]
-
 # the checks of the last run_stream_parallel call (diagnostics)
 parallel_check = {}
-_handles = {}
 
 
-def _cached_handle(B, dtype, dev):
-    """A REF15 handle of B filters kept for reuse (run_stream_parallel runs three launches of
-    fixed widths per call; allocating them per call costs more than the small launches)."""
-    key = (int(B), dtype, dev.index or 0)
-    kf = _handles.get(key)
-    if kf is None:
-        if len(_handles) >= 6:
-            _handles.pop(next(iter(_handles))).close()
-        kf = _handles[key] = BatchedKF('ref15', B, dtype, device=key[2])
-    return kf
-
-
-def run_stream_parallel(et, dt, pay, x0, P0b, chunk=None, warmup=2560, dtype='f64', cov=False, tol=None):
-    """One filter over a long event stream, split over time into C chunks that run as C filters
-    of one launch.  et [T] uint8, dt [T] float64 (the driver's dt rule already applied), pay
-    [T, 9] on the device; x0 [15], P0b [27] block-packed initial state.  Returns
-    (traj [T, 6], logdet [T], x [15], P blocks [27], cov [T, 27] or None) on the device, or None
-    when a check fails (the caller then runs the stream sequentially).
-
-    Exact structure used (no approximation is accepted unchecked):
-    * The covariance recursion does not depend on the measurements, and it forgets its start:
-      run from P0 over the W events before a chunk it reaches the sequential run's covariance
-      (bitwise, after ~1.5k events of the reference's 200 Hz IMU stream).  Warm-up pass: chunk
-      c's W preceding events from (0, P0) give its start covariance; chunks within W of the
-      stream start run from the true (x0, P0) and are exact.
-    * Given the gains, the state recursion is affine, x_k = G_k x_(k-1) + g_k (the IMU
-      pseudo-measurement is built from the predicted state, kf_workers.py:698-706, which keeps
-      it affine).  Main pass: each chunk runs from a guess and from three perturbed guesses (one
-      per chain component), giving its affine map start -> end.  An inclusive scan composes the
-      maps in chunk order from the true x0: the true start state of every chunk.
-    * Final pass: every chunk from its true start state, with the records.
-    * Checks: every warm-up covariance equals the previous chunk's end covariance (relative
-      1e-12 in f64, 1e-5 in f32), every chunk's final end state equals the next chunk's start
-      state (``tol``: 1e-9 relative in f64, 1e-4 in f32), and no filter failed.
-      ``parallel_check`` holds the measured gaps (or the failed check)."""
+def run_stream_parallel(et, dt, pay, x0, P0b, chunk=None, warmup=None, dtype='f64', cov=False):
+    """One filter over a long event stream, parallel over time (kf_run_stream): et [T] uint8,
+    dt [T] float64 (the driver's dt rule already applied), pay [T, 9] on the device; x0 [15], P0b
+    [27] block-packed initial state.  Returns (traj [T, 6], logdet [T], x [15], P blocks [27],
+    cov [T, 27] or None) on the device.  The chunked records stand only if the device checks
+    pass (warm-up covariances meet their predecessors' end covariances, chunk end states meet
+    the next starts, no chunk filter failed); otherwise the library's sequential fallback has
+    rewritten them.  ``parallel_check`` holds the verdict and the measured gaps."""
     dev = et.device
-    tol = (1e-9 if dtype == 'f64' else 1e-4) if tol is None else tol
-    tol_cov = 1e-12 if dtype == 'f64' else 1e-5
-    parallel_check.clear()
-    T = int(et.shape[0])
-    L = int(chunk) if chunk else max(128, -(-T // 2048))  # 4 C filters stay on the chain kernel
-    C = -(-T // L)
-    if C < 2:
-        return None
-    W = int(warmup)
     npd = torch.float64 if dtype == 'f64' else torch.float32
-    # the stream with W NONE events in front and the last chunk padded with NONE
-    pad = C * L - T
-    etw = torch.cat([torch.full((W,), NONE, dtype=torch.uint8, device=dev), et,
-                     torch.full((pad,), NONE, dtype=torch.uint8, device=dev)])
-    dtw = torch.cat([torch.zeros(W, dtype=torch.float64, device=dev), dt,
-                     torch.zeros(pad, dtype=torch.float64, device=dev)])
-    payw = torch.cat([torch.zeros(W, 9, dtype=npd, device=dev), pay.to(npd),
-                      torch.zeros(pad, 9, dtype=npd, device=dev)])
-    x0 = torch.as_tensor(x0, dtype=npd, device=dev).reshape(15)
-    P0b = torch.as_tensor(P0b, dtype=npd, device=dev).reshape(27)
-
-    # warm-up: chunk c >= 1 over the W events before it (columns c - 1); NONE events before
-    # the stream start leave a chunk near it on the true (x0, P0)
-    ew = etw.as_strided((W, C - 1), (1, L), L).contiguous()
-    dw = dtw.as_strided((W, C - 1), (1, L), L).contiguous()
-    pw = payw.as_strided((W, 9, C - 1), (9, 1, 9 * L), 9 * L).contiguous()
-    exact = (torch.arange(1, C, device=dev) * L) <= W
-    kw = _cached_handle(C - 1, dtype, dev)
-    P0ref = torch.as_tensor(to_blocks(P0), dtype=npd, device=dev)
-    kw.set_state(torch.where(exact[None, :], x0[:, None], torch.zeros((), dtype=npd, device=dev)).expand(15, C - 1),
-                 torch.where(exact[None, :], P0b[:, None], P0ref[:, None]).expand(27, C - 1))
-    kw.run_events(ew, dw, pw, traj=False, logdet=False)
-    xw, Pw = kw.state()
-    bad = (kw.status() != 0).sum()
-    xb = torch.cat([x0[:, None], xw], 1)                  # [15, C] start guesses
-    Pb = torch.cat([P0b[:, None], Pw], 1)                 # [27, C] start covariances
-
-    # main pass: base + 3 perturbed starts per chunk -> each chunk's affine map
-    E = etw[W:].view(C, L).T.contiguous()
-    D = dtw[W:].view(C, L).T.contiguous()
-    Pay = payw[W:].view(C, L, 9).permute(1, 2, 0).contiguous()
-    delta = 1024.0  # the maps are affine: a large step only shrinks the roundoff of the differences
-    pert = np.zeros((4, 15))
-    for r, col, q in _MAP_ENTRIES:
-        if r == col:
-            pert[q + 1, col] = delta
-    pert = torch.as_tensor(pert, dtype=npd, device=dev)
-    km = _cached_handle(4 * C, dtype, dev)
-    km.set_state((xb[None] + pert[:, :, None]).permute(1, 0, 2).reshape(15, 4 * C), Pb.repeat(1, 4))
-    km.run_events(E.repeat(1, 4), D.repeat(1, 4), Pay.repeat(1, 1, 4), traj=False, logdet=False)
-    xm, Pm = km.state()
-    bad = bad + (km.status() != 0).sum()
-    # the warm-up must have reached the covariance the previous chunk ends with
-    Pend = Pm[:, :C]
-    scale = Pend[:, :-1].abs().amax(0).clamp(min=1e-300)
-    cov_gap = ((Pend[:, :-1] - Pb[:, 1:]).abs().amax(0) / scale).max()
-
-    # compose the chunk maps in order (float64): chunk c maps its start x to A_c x + b_c,
-    # A_c = Phi_c, b_c = x_end_c - Phi_c guess_c; the true start of chunk c is
-    # (M_(c-1) o ... o M_0)(x0): an inclusive scan over augmented 16x16 maps, log2 C rounds
-    xm64 = xm.double().view(15, 4, C)
-    rows, cols, qs = (torch.tensor(v, device=dev) for v in zip(*_MAP_ENTRIES))
-    M = torch.zeros(C, 16, 16, dtype=torch.float64, device=dev)
-    M[:, rows, cols] = ((xm64[rows, qs + 1, :] - xm64[rows, 0, :]) / delta).T
-    M[:, :15, 15] = xm64[:, 0, :].T - torch.bmm(M[:, :15, :15], xb.double().T[:, :, None])[:, :, 0]
-    M[:, 15, 15] = 1.0
-    s = 1
-    while s < C:  # Hillis-Steele: M_c <- M_c M_(c-s)
-        M[s:] = torch.bmm(M[s:], M[:-s])
-        s *= 2
-    x0d = x0.double()
-    ends = torch.bmm(M[:, :15, :15], x0d.expand(C, 15)[:, :, None])[:, :, 0] + M[:, :15, 15]
-    starts = torch.cat([x0d[None, :], ends[:-1]], 0).T.contiguous()   # [15, C]
-
-    # final pass from the true starts, with the records
-    kf = _cached_handle(C, dtype, dev)
-    kf.set_state(starts.to(npd), Pb)
-    tr, ld, _, cv = kf.run_events(E, D, Pay, cov=cov)
-    xf, Pf = kf.state()
-    bad = bad + (kf.status() != 0).sum()
-    st = starts[:, 1:]
-    gap = ((xf[:, :-1].double() - st).abs() / st.abs().clamp(min=1.0)).max()
-    n_bad, cov_gap, gap = torch.stack([bad.double(), cov_gap.double(), gap]).tolist()
-    parallel_check.update(ok=False, cov_gap=cov_gap, state_gap=gap, chunks=C, chunk=L, warmup=W)
-    if n_bad:
-        parallel_check.update(reason='a chunk filter failed')
-        return None
-    if not cov_gap <= tol_cov:
-        parallel_check.update(reason='covariance warm-up did not converge')
-        return None
-    if not gap <= tol:
-        parallel_check.update(reason='chunk end states do not meet the next starts')
-        return None
-    parallel_check['ok'] = True
-    traj = tr.permute(2, 0, 1).reshape(C * L, 6)[:T]
-    logd = ld.T.reshape(C * L)[:T]
-    covs = cv.permute(2, 0, 1).reshape(C * L, 27)[:T] if cov else None
-    return traj, logd, xf[:, C - 1], Pf[:, C - 1], covs
+    kf = BatchedKF('ref15', 1, dtype, device=dev.index or 0)
+    try:
+        kf.set_state(torch.as_tensor(np.asarray(x0, np.float64).reshape(15, 1), dtype=npd, device=dev),
+                     torch.as_tensor(np.asarray(P0b, np.float64).reshape(27, 1), dtype=npd, device=dev))
+        tr, ld, _, cv = kf.run_stream(et, dt, pay.to(npd), cov=cov, chunk=chunk or 0,
+                                      warmup=-1 if warmup is None else warmup)
+        x, P = kf.state()
+        parallel_check.clear()
+        parallel_check.update(kf.stream_check())
+        return tr[:, :, 0], ld[:, 0], x[:, 0], P[:, 0], (cv[:, :, 0] if cov else None)
+    finally:
+        kf.close()
 
 
 def run_adaptive_threshold_kalman_filter(events, start_idx=None, end_idx=None, R_threshold=None,

@@ -1,5 +1,6 @@
-"""One filter over a long event stream, parallel over time (kfmi.ref15.run_stream_parallel) —
-needs an MI355X.
+"""One filter over a long event stream, parallel over time (kf_run_stream through
+kfmi.ref15.run_stream_parallel, BatchedKF.run_stream and kf_run_events' own route) — needs an
+MI355X.
 
 The chunked run must give the single-filter run's records: the covariance warm-up reaches the
 sequential covariance and the chunk maps are affine, so agreement is at roundoff (checked at
@@ -51,25 +52,32 @@ def _stream(T, seed=1, gps_every=20, keep=0.7, skips=0):
     return et, dt, pay, x0
 
 
-def _sequential(et, dt, pay, x0, dtype='f64'):
-    kf = kfmi.BatchedKF('ref15', 1, dtype)
+def _sequential(et, dt, pay, x0, dtype='f64', model='ref15'):
+    """The single filter (kf_run_events with the stream route off)."""
+    import os
+    kf = kfmi.BatchedKF(model, 1, dtype)
     npd = np.float64 if dtype == 'f64' else np.float32
-    kf.set_state(x0[:, None].astype(npd), ref15.to_blocks(ref15.P0)[:, None].astype(npd))
-    tr, ld, _, _ = kf.run_events(et[:, None], dt[:, None], pay[:, :, None].astype(npd))
+    P0 = ref15.to_blocks(ref15.P0) if model == 'ref15' else kf.state()[1].double().cpu().numpy()[:, 0]
+    kf.set_state(x0[:, None].astype(npd), P0[:, None].astype(npd))
+    old = os.environ.get('KFMI_STREAM')
+    os.environ['KFMI_STREAM'] = 'off'
+    try:
+        tr, ld, up, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None].astype(npd), updated=True, cov=True)
+    finally:
+        if old is None:
+            del os.environ['KFMI_STREAM']
+        else:
+            os.environ['KFMI_STREAM'] = old
     x, P = kf.state()
-    out = tr[:, :, 0].double().cpu().numpy(), ld[:, 0].double().cpu().numpy(), x[:, 0].double().cpu().numpy(), \
-        P[:, 0].double().cpu().numpy()
+    out = tuple(v.double().cpu().numpy() for v in (tr[:, :, 0], ld[:, 0], x[:, 0], P[:, 0], cv[:, :, 0], up[:, 0]))
     kf.close()
     return out
 
 
 def _parallel(et, dt, pay, x0, **kw):
     dev = torch.device('cuda', 0)
-    r = ref15.run_stream_parallel(torch.as_tensor(et, device=dev), torch.as_tensor(dt, device=dev),
-                                  torch.as_tensor(pay, device=dev), x0, ref15.to_blocks(ref15.P0), **kw)
-    if r is None:
-        return None
-    tr, ld, x, P, _ = r
+    tr, ld, x, P, _ = ref15.run_stream_parallel(torch.as_tensor(et, device=dev), torch.as_tensor(dt, device=dev),
+                                                torch.as_tensor(pay, device=dev), x0, ref15.to_blocks(ref15.P0), **kw)
     return tr.double().cpu().numpy(), ld.double().cpu().numpy(), x.double().cpu().numpy(), P.double().cpu().numpy()
 
 
@@ -80,8 +88,9 @@ def test_parallel_equals_single_filter(T, chunk, skips):
     et, dt, pay, x0 = _stream(T, seed=T, skips=skips)
     seq = _sequential(et, dt, pay, x0)
     par = _parallel(et, dt, pay, x0, chunk=chunk)
-    assert par is not None, ref15.parallel_check
-    assert ref15.parallel_check['cov_gap'] == 0.0  # the warm-up reached the covariance bitwise
+    chk = ref15.parallel_check
+    assert chk['ok'] and chk['chunks'] > 1, chk
+    assert chk['cov_gap'] <= 1e-12  # the warm-up reached the covariance (to roundoff)
     for a, b in zip(par, seq):
         assert a.shape == b.shape
         assert _rel(a, b) <= 1e-9
@@ -91,6 +100,7 @@ def test_parallel_vs_oracle():
     """The reference's step (oracle/cpu_kf.c, dense 15x15, its op order) over the whole stream."""
     et, dt, pay, x0 = _stream(30000, seed=7)
     tr, ld, _, _ = _parallel(et, dt, pay, x0, chunk=512)
+    assert ref15.parallel_check['ok']
     rt, rl = cpu_kf.ref15_events(et[:, None], dt[:, None], pay[:, :, None], x0[:, None], ref_kf.P0_REF15, nthreads=4)
     assert _rel(tr, rt[:, :, 0]) <= 1e-6
     assert _rel(ld, rl[:, 0]) <= 1e-6
@@ -100,16 +110,58 @@ def test_parallel_f32():
     et, dt, pay, x0 = _stream(40000, seed=3)
     seq = _sequential(et, dt, pay, x0)
     par = _parallel(et, dt, pay, x0, dtype='f32')
-    assert par is not None, ref15.parallel_check
+    assert ref15.parallel_check['ok'], ref15.parallel_check
     assert _rel(par[0], seq[0]) <= 1e-3 and _rel(par[1], seq[1]) <= 1e-3
 
 
-def test_short_warmup_is_refused():
-    """A warm-up too short for the covariance to converge fails the check (None: the caller
-    falls back to one filter) instead of returning wrong records."""
+def test_short_warmup_falls_back():
+    """A warm-up too short for the covariance to converge fails the device check; the
+    sequential fallback then rewrites every record: the output is still the single filter's."""
     et, dt, pay, x0 = _stream(20000, seed=5)
-    assert _parallel(et, dt, pay, x0, chunk=1000, warmup=16) is None
-    assert ref15.parallel_check['reason'] == 'covariance warm-up did not converge'
+    seq = _sequential(et, dt, pay, x0)
+    par = _parallel(et, dt, pay, x0, chunk=1000, warmup=16)
+    chk = ref15.parallel_check
+    assert not chk['ok'] and chk['cov_gap'] > 1e-12, chk
+    for a, b in zip(par, seq):
+        assert np.array_equal(a, b)
+
+
+def test_nan_fix_falls_back():
+    """A NaN fix mid-stream poisons the state from there on (the covariance is unaffected): the
+    chunk maps carry the NaN, the state seam check fails, and the fallback gives the single
+    filter's records, NaN and all."""
+    et, dt, pay, x0 = _stream(30000, seed=9)
+    g = np.nonzero(et == ref15.GPS)[0]
+    pay[g[len(g) // 2], 0] = np.nan
+    seq = _sequential(et, dt, pay, x0)
+    par = _parallel(et, dt, pay, x0, chunk=300)
+    assert not ref15.parallel_check['ok']
+    assert np.isnan(par[0][-1]).any()
+    for a, b in zip(par, seq):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_records_updated_cov_ref8():
+    """Every record kf_run_events writes (traj, logdet, updated, covariance) and the 8-state
+    model, through the C ABI route kf_run_events takes by itself for T >= 65536."""
+    T = 70000
+    et, dt, pay, x0 = _stream(T, seed=13, skips=20)
+    for model in ('ref15', 'ref8'):
+        n = 15 if model == 'ref15' else 8
+        xs = np.zeros(n)
+        xs[0:2] = x0[0:2]
+        seq = _sequential(et, dt, pay, xs, model=model)
+        kf = kfmi.BatchedKF(model, 1, 'f64')
+        kf.set_state(xs[:, None], kf.state()[1].double().cpu().numpy())
+        tr, ld, up, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None], updated=True, cov=True)
+        chk = kf.stream_check()
+        assert chk['ok'] and chk['chunks'] > 1, chk
+        x, P = kf.state()
+        par = tuple(v.double().cpu().numpy() for v in (tr[:, :, 0], ld[:, 0], x[:, 0], P[:, 0], cv[:, :, 0], up[:, 0]))
+        kf.close()
+        for a, b in zip(par, seq):
+            assert a.shape == b.shape
+            assert _rel(a, b) <= 1e-9
 
 
 def test_run_full_stream_parallel_matches_single_filter():
