@@ -188,25 +188,33 @@ int kf_run_events(kf_batch* handle, int T, const uint8_t* etype, const double* d
 
 /* One filter over a long event stream, parallel over time: kf_run_events for a handle of ONE
  * filter (B = 1, no gate), with the same arguments, outputs and final state, computed as
- * chunks of `chunk` events run as filters of one launch (chunk <= 0: max(128, T / 2048)).  Each
- * chunk's start covariance comes from a warm-up over the `warmup` events before it (< 0:
- * 2048); the state recursion given the gains is affine, so each chunk's map start -> end is
- * measured from a guess and three perturbed guesses and the maps are composed into the true
- * chunk starts.  Checked on the device: the warm-up covariances must meet their predecessors'
- * end covariances (relative 1e-12 in f64, 1e-5 in f32), every chunk's end state its
- * successor's start (1e-9 / 1e-4), and no chunk filter may fail; otherwise the sequential
- * kernel runs the stream as one filter from the handle's state and rewrites every record.
- * Asynchronous on `stream` either way.  kf_run_events takes this route by itself for B = 1,
- * gate = 0 and T >= 65536 (KFMI_STREAM=off disables it).  The run of
- * run_kalman_filter_full (kf_workers.py:623-728) over a whole drive log. */
+ * chunks of `chunk` events run as filters of one launch (chunk <= 0: max(128, T / 2048)).
+ * Each chunk's start covariance comes from the covariance recursion's linear-fractional maps
+ * (per chain and piece of <= 160 events), iterated over all chunks at once from the handle's
+ * covariance (warmup = -1, the default; -2 - k adds k chunks of event warm-up), or from a
+ * warm-up over the `warmup` events before the chunk (warmup >= 0).  The state recursion given
+ * the gains is affine: each chunk runs from a guess and three perturbed guesses, whose ends
+ * give its map start -> end; the maps are composed into the true chunk starts, and the records
+ * are the map pass's (covariance, logdet, updated from the guess; the trajectory as the maps'
+ * value at the true starts).  KFMI_STREAM_FINAL=1 (or a stream too long for the four
+ * trajectory variants' 32-bit offsets) runs a final pass from the true starts instead, with
+ * its own state seam check.  Checked on the device: the start covariances must meet their
+ * predecessors' end covariances (relative 1e-12 in f64, 1e-5 in f32), the chunk starts and end
+ * state must be finite (final pass: every chunk's end state its successor's start, 1e-9 /
+ * 1e-4), and no chunk filter may fail; otherwise the sequential kernel runs the stream as one
+ * filter from the handle's state and rewrites every record.  Asynchronous on `stream` either
+ * way.  kf_run_events takes this route by itself for B = 1, gate = 0 and T >= 65536
+ * (KFMI_STREAM=off disables it).  The run of run_kalman_filter_full (kf_workers.py:623-728)
+ * over a whole drive log. */
 int kf_run_stream(kf_batch* handle, int T, const uint8_t* etype, const double* dt, const void* payload,
                   void* traj, void* cov, void* logdet, uint8_t* updated, int chunk, int warmup,
                   void* stream);
 
 /* The checks of the handle's last kf_run_stream (synchronises `stream`): out[0] = 1 if the
  * chunked run's records stood (0: the sequential fallback ran), out[1] = 1 if a chunk filter
- * failed, out[2] = covariance seam gap, out[3] = state seam gap, out[4] = chunks (1: the stream
- * was too short to split and ran sequentially), out[5] = chunk length, out[6] = warm-up. */
+ * failed, out[2] = covariance seam gap, out[3] = state seam gap (records from the map pass: 0,
+ * or inf for a non-finite chunk start), out[4] = chunks (1: the stream was too short to split
+ * and ran sequentially), out[5] = chunk length, out[6] = events of event warm-up. */
 int kf_stream_check(kf_batch* handle, double* out, void* stream);
 
 /* KF_MODEL_REF15 brute-force search: filter f of the handle evaluates combination number

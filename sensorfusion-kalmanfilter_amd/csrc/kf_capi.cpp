@@ -521,7 +521,13 @@ int run_events_launch(kf_batch* h, int T, const uint8_t* etype, const double* dt
 
 // kf_run_events routes one-filter runs of at least this many events through kf_run_stream
 constexpr int kStreamMinEvents = 65536;
-constexpr int kStreamDefaultWarmup = 2048;
+// default (warmup < 0): covariance maps iterated to cover this many events, then kStreamPolish
+// chunks of event warm-up
+constexpr int64_t kStreamLftEvents = 2048;
+constexpr int kStreamPolish = 0;
+// events per covariance map: the roundoff of a map's evaluation grows with the events it spans
+// (config 1 log: seam gap 4.8e-15 with 285-event maps, 1.5e-11 with 777-event maps)
+constexpr int64_t kStreamLftPiece = 160;
 constexpr int64_t kStreamTargetChunks = 2048;
 
 size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
@@ -554,7 +560,11 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     const hipStream_t st = static_cast<hipStream_t>(stream);
     const int64_t L = chunk > 0 ? chunk : std::max<int64_t>(128, (int64_t(T) + kStreamTargetChunks - 1) / kStreamTargetChunks);
     const int64_t C = (int64_t(T) + L - 1) / L;
-    const int64_t W = warmup >= 0 ? warmup : kStreamDefaultWarmup;
+    // warmup >= 0: W events of warm-up before each chunk from the handle's covariance;
+    // -1: linear-fractional covariance maps + kStreamPolish chunks of warm-up; -2 - k: maps + k chunks
+    const bool lft = warmup < 0;
+    const int kp = !lft ? 0 : warmup == -1 ? kStreamPolish : -(warmup + 2);
+    const int64_t W = lft ? int64_t(kp) * L : warmup;
     const size_t w = elem(h);
     const int nblk = h->np, n = h->n;
     const int nch = h->model == KF_MODEL_REF15 ? 6 : 3;
@@ -572,8 +582,19 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     const size_t bank1 = align256(size_t(n + nblk) * C * w) + align256(sizeof(int32_t) * C);
     const size_t bank4 = align256(size_t(n + nblk) * 4 * C * w) + align256(sizeof(int32_t) * 4 * C);
     const int64_t nseg = (C + kfmi::kStreamSegChunks - 1) / kfmi::kStreamSegChunks;
+    const int np = int((L + kStreamLftPiece - 1) / kStreamLftPiece);
+    const size_t lft_bytes =
+        lft ? align256(sizeof(double) * 36 * nch * C * np) + 2 * align256(sizeof(double) * 9 * nch * C) : 0;
+    // records straight from the map pass (no final pass) unless the four variants' trajectory
+    // rows exceed the 32-bit offsets or KFMI_STREAM_FINAL=1 asks for the final pass
+    const int ntraj = h->model == KF_MODEL_REF15 ? 6 : 3;
+    const int64_t vstride = T + L;
+    const char* fv = std::getenv("KFMI_STREAM_FINAL");
+    const bool map_records = !(fv && !std::strcmp(fv, "1")) && uint64_t(4 * vstride) * ntraj * w < (uint64_t(1) << 31);
+    const size_t rec_bytes = map_records ? align256(size_t(4 * vstride) * ntraj * w) + align256(sizeof(double) * n) : 0;
     const size_t need = 256 + 2 * bank1 + bank4 + align256(sizeof(double) * 12 * nch * C) +
-                        align256(sizeof(double) * 15 * nch * nseg) + align256(sizeof(double) * n * C);
+                        align256(sizeof(double) * 15 * nch * nseg) + align256(sizeof(double) * n * C) + lft_bytes +
+                        rec_bytes;
     if (h->stream_ws_bytes < need) {
         if (h->stream_ws) (void)hipFree(h->stream_ws);
         h->stream_ws = nullptr;
@@ -611,9 +632,36 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     sa.segstart = sa.segmaps + 12 * nch * nseg;
     p += align256(sizeof(double) * 15 * nch * nseg);
     sa.starts = reinterpret_cast<double*>(p);
+    p += align256(sizeof(double) * n * C);
+    double* pbuf[2] = {nullptr, nullptr};
+    if (lft) {
+        sa.phi = reinterpret_cast<double*>(p);
+        p += align256(sizeof(double) * 36 * nch * C * np);
+        pbuf[0] = reinterpret_cast<double*>(p);
+        p += align256(sizeof(double) * 9 * nch * C);
+        pbuf[1] = reinterpret_cast<double*>(p);
+        p += align256(sizeof(double) * 9 * nch * C);
+    }
+    void* traj4 = nullptr;
+    if (map_records) {
+        traj4 = p;
+        p += align256(size_t(4 * vstride) * ntraj * w);
+        sa.xend = reinterpret_cast<double*>(p);
+        sa.traj4 = traj4;
+        sa.vstride = vstride;
+        sa.traj = traj;
+    }
+    sa.etype = etype;
+    sa.dt = dt;
+    sa.S = T;
+    sa.L = L;
+    sa.kp = kp;
+    sa.np = np;
+    sa.lp = (L + np - 1) / np;
 
     const bool f64 = h->dtype == KF_F64;
-    auto chain = [&](int64_t B, void* x, void* P, int32_t* status, int64_t Tc, int64_t shift, bool records) {
+    auto chain = [&](int64_t B, void* x, void* P, int32_t* status, int64_t Tc, int64_t shift, bool records,
+                     void* traj_rec = nullptr, int nvar = 1) {
         kfmi::RefArgs a{};
         a.B = B;
         a.T = int(Tc);
@@ -624,7 +672,9 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
         a.P = P;
         a.status = status;
         if (records) {
-            a.traj = traj;
+            a.traj = traj_rec ? traj_rec : traj;
+            a.s_nvar = nvar;
+            a.s_vstride = nvar > 1 ? vstride : 0;
             a.cov = cov;
             a.logdet = logdet;
             a.updated = updated;
@@ -636,12 +686,34 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
         return kfmi::launch_ref_stream(h->model, f64, a, st);
     };
     hipError_t e = kfmi::launch_stream_phase(h->model, f64, 0, sa, st);
+    if (lft) {
+        // enough iterations for the maps to cover kStreamLftEvents events of forgetting
+        const int iters = int((kStreamLftEvents + L - 1) / L) + 1;
+        if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseLftMaps, sa, st);
+        for (int it = 0; it < iters && e == hipSuccess; ++it) {
+            kfmi::StreamArgs si = sa;
+            si.pcur = it == 0 ? nullptr : pbuf[it & 1];
+            si.pnext = pbuf[(it + 1) & 1];
+            si.last = it + 1 == iters;
+            e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseLftIter, si, st);
+        }
+    }
     if (e == hipSuccess && W > 0) e = chain(C, sa.wx, sa.wP, sa.wst, W, -W, false);
     if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, 1, sa, st);
-    if (e == hipSuccess) e = chain(4 * C, sa.mx, sa.mP, sa.mst, L, 0, false);
-    for (int ph = 2; ph <= 4 && e == hipSuccess; ++ph) e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
-    if (e == hipSuccess) e = chain(C, sa.fx, sa.fP, sa.fst, L, 0, true);
-    if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, 5, sa, st);
+    if (map_records) {
+        // the map pass writes the records (variant 0's covariance, logdet, updated flags, and
+        // every variant's trajectory); the trajectories are then the affine maps' values at the
+        // true chunk starts
+        if (e == hipSuccess) e = chain(4 * C, sa.mx, sa.mP, sa.mst, L, 0, true, traj ? traj4 : nullptr, 4);
+        for (int ph = 2; ph <= 4 && e == hipSuccess; ++ph) e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
+        if (e == hipSuccess && traj) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseRecords, sa, st);
+        if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseFinishMaps, sa, st);
+    } else {
+        if (e == hipSuccess) e = chain(4 * C, sa.mx, sa.mP, sa.mst, L, 0, false);
+        for (int ph = 2; ph <= 4 && e == hipSuccess; ++ph) e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
+        if (e == hipSuccess) e = chain(C, sa.fx, sa.fP, sa.fst, L, 0, true);
+        if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, 5, sa, st);
+    }
     if (e != hipSuccess) return hip_fail(e, "kf_run_stream");
     // the sequential run, which does nothing unless a check failed
     return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, 0, 0.0, &sa.check->ok, stream);

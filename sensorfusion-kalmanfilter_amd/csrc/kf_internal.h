@@ -71,6 +71,8 @@ struct RefArgs {
     int64_t s_chunk;
     int64_t s_shift;
     int64_t s_nchunks;
+    int s_nvar;              // > 1: trajectory records per variant (filter / s_nchunks), s_vstride rows apart
+    int64_t s_vstride;
     const int32_t* skip;     // if non-null and *skip != 0, the launch does nothing
 };
 
@@ -103,12 +105,34 @@ struct StreamArgs {
     double* segstart;        // [C / kStreamSeg][chains][3]: each segment's start
     double* starts;          // [N][C] the chunk starts (fp64)
     StreamCheck* check;
+    // covariance start by linear-fractional maps (kf_run_stream's default warm-up)
+    const uint8_t* etype;    // the stream [S], dt [S]
+    const double* dt;
+    int64_t S, L;            // stream length, chunk length
+    int kp;                  // polish chunks: the warm-up bank starts chunk c from P(c - kp)
+    int np;                  // pieces per chunk (of lp events) with a covariance map each
+    int64_t lp;
+    double* phi;             // [C][np][chains][36]: per piece and chain, the 6x6 covariance map [[A B] [C D]]
+    double* pcur;            // [C][chains][9]: chunk start covariances of the current iteration
+    double* pnext;           // [C][chains][9]
+    int last;                // this is the last iteration: write the warm-up bank's P
+    // records from the map pass (no final pass): the map bank's trajectories per variant
+    const void* traj4;       // [4][vstride][NTRAJ]
+    int64_t vstride;
+    void* traj;              // [S][NTRAJ] the records: variant 0 + sum_q A_q (start - guess)_q
+    double* xend;            // [N] the last chunk's end state (fp64)
 };
 // phase 0: warm-up bank from the handle, check zeroed; 1: map bank from the warm-up bank;
 // 2: chunk maps, segment products, covariance seam check; 3: segment starts; 4: chunk starts
 // into the final bank; 5: state seam check, verdict, and (if it passed) the handle's final state
 constexpr int kStreamSegChunks = 64;  // chunks per segment (kStreamSeg in kf_ref.hip)
 hipError_t launch_stream_phase(int model, bool f64, int phase, const StreamArgs& a, hipStream_t stream);
+// the linear-fractional covariance warm-up: phase 6 = every chunk's covariance map, phase 7 =
+// one iteration P(c) <- map_(c-1)(P(c-1)) over all chunks (pcur -> pnext)
+constexpr int kStreamPhaseLftMaps = 6, kStreamPhaseLftIter = 7;
+// records from the map pass: phase 8 = trajectories from the variants and the chunk starts;
+// phase 9 = the verdict without a final pass (failed filters, non-finite starts, covariance seams)
+constexpr int kStreamPhaseRecords = 8, kStreamPhaseFinishMaps = 9;
 
 // Brute-force search over k-subsets of n candidate events (kf_workers.py:22-97, 1218-1392):
 // lane f evaluates combination number combo_offset + f in itertools.combinations order.

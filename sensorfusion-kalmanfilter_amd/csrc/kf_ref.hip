@@ -589,7 +589,12 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     const uint32_t S = STREAM ? uint32_t(a.s_len) : 0u;
     const auto r_et = bytes_rsrc(a.etype, S), r_dt = bytes_rsrc(a.dt, S * 8u);
     const auto r_pay = bytes_rsrc(a.payload, S * 9u * uint32_t(sizeof(T)));
-    const auto r_str = bytes_rsrc(a.traj, S * uint32_t(M::NTRAJ * sizeof(T)));
+    // filter f is variant f / s_nchunks of its chunk: with s_nvar > 1, variant q's trajectory
+    // records go to rows [q * s_vstride, q * s_vstride + S) (s_vstride >= S + chunk, so a padded
+    // chunk's rows past S stay inside its own variant), and only variant 0 writes the others
+    const int var = STREAM ? int(f / a.s_nchunks) : 0;
+    const uint32_t trows = STREAM ? (a.s_nvar > 1 ? uint32_t(a.s_nvar) * uint32_t(a.s_vstride) : S) : 0u;
+    const auto r_str = bytes_rsrc(a.traj, trows * uint32_t(M::NTRAJ * sizeof(T)));
     const auto r_scv = bytes_rsrc(a.cov, S * uint32_t(M::NBLK * sizeof(T)));
     const auto r_sld = bytes_rsrc(a.logdet, S * uint32_t(sizeof(T)));
     const auto r_sup = bytes_rsrc(a.updated, S);
@@ -599,11 +604,14 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     // into branches around the loads, whose joins drained the prefetch ring with vmcnt(0)).
     // Lanes without a record OR in bit 31 (kf_run_stream keeps (S + W) * rows * w < 2^31).
     const uint32_t m_tr = v_tr != kDropOffset ? 0u : kDropOffset;
-    const uint32_t col_tr = v_tr != kDropOffset ? uint32_t(xi[0]) * uint32_t(sizeof(T)) : 0u;
-    const uint32_t m_ld = c == 0 ? 0u : kDropOffset;
+    const uint32_t col_tr = v_tr != kDropOffset ? (uint32_t(var) * uint32_t(a.s_vstride) * M::NTRAJ + uint32_t(xi[0])) *
+                                                      uint32_t(sizeof(T))
+                                                : 0u;
+    const uint32_t m_ld = c == 0 && var == 0 ? 0u : kDropOffset;
     uint32_t col_cv[6];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) col_cv[k] = pr[k] >= 0 ? uint32_t(pr[k]) * uint32_t(sizeof(T)) : kDropOffset;
+    for (int k = 0; k < 6; ++k)
+        col_cv[k] = pr[k] >= 0 && var == 0 ? uint32_t(pr[k]) * uint32_t(sizeof(T)) : kDropOffset;
     auto load = [&](int t, ChainIn<T>& in) {
         if constexpr (STREAM) {
             const uint32_t ue = uint32_t(e0 + t);
@@ -875,10 +883,12 @@ template <typename T, class M>
 __global__ __launch_bounds__(1024) void stream_maps_kernel(const StreamArgs a) {
     constexpr int NCH = M::NP + M::NA;
     __shared__ double lm[NCH][kStreamSeg][12];
+    __shared__ double red[NCH * kStreamSeg];
     const int tid = int(threadIdx.x);
     const int ch = tid / kStreamSeg, j = tid % kStreamSeg;
     const int64_t c = int64_t(blockIdx.x) * kStreamSeg + j;
     const int64_t B = 4 * a.C;
+    double crel = 0.0;
     const T* mx = static_cast<const T*>(a.mx);
     const T* wx = static_cast<const T*>(a.wx);
     const int ns = ch < M::NP ? 3 : 2;
@@ -920,9 +930,18 @@ __global__ __launch_bounds__(1024) void stream_maps_kernel(const StreamArgs a) {
                 gap = fmax(gap, fabs(pe - double(wP[r * a.C + c])));
             }
             const double rel = gap / fmax(scale, 1e-300);
-            if (rel != 0.0 || !(rel == rel)) atomic_max_pos(&a.check->cov_gap, rel);
+            crel = rel == rel ? rel : __builtin_inf();
         }
     }
+    // one atomic per block (a device-wide atomic per thread serialised ~12k of them)
+    red[tid] = crel;
+    __syncthreads();
+    for (int n = NCH * kStreamSeg; n > 1; n = (n + 1) / 2) {  // NCH * 64 is not a power of two
+        const int h = (n + 1) / 2;
+        if (tid + h < n) red[tid] = fmax(red[tid], red[tid + h]);
+        __syncthreads();
+    }
+    if (tid == 0 && red[0] != 0.0) atomic_max_pos(&a.check->cov_gap, red[0]);
     double* m = lm[ch][j];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -994,7 +1013,7 @@ __global__ __launch_bounds__(1024) void stream_apply_kernel(const StreamArgs a) 
         const double* g = a.maps + (c * NCH + ch) * 12;
 #pragma unroll
         for (int e = 0; e < 12; ++e) lm[ch][j][e] = g[e];
-        if (ch == 0) {
+        if (ch == 0 && !a.xend) {  // the final bank (records from the map pass need none)
 #pragma unroll
             for (int r = 0; r < M::NBLK; ++r)
                 static_cast<T*>(a.fP)[r * a.C + c] = static_cast<const T*>(a.wP)[r * a.C + c];
@@ -1014,10 +1033,312 @@ __global__ __launch_bounds__(1024) void stream_apply_kernel(const StreamArgs a) 
                 if (k >= ns) continue;
                 const int i = chain_state<M>(ch, k);
                 a.starts[i * a.C + c0 + jj] = x[k];
-                static_cast<T*>(a.fx)[i * a.C + c0 + jj] = T(x[k]);
+                if (!a.xend) static_cast<T*>(a.fx)[i * a.C + c0 + jj] = T(x[k]);
             }
             apply_map(x, lm[ch][jj]);
         }
+        if (a.xend && c0 + n == a.C) {  // past the last chunk: the stream's end state
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (k < ns) a.xend[chain_state<M>(ch, k)] = x[k];
+        }
+    }
+}
+
+// phase 8 (records from the map pass): thread per (event, trajectory entry i); entry i (the
+// first component of its chain) = variant 0's + sum_q A_q (start - guess)_q with A_q =
+// (variant q+1 - variant 0) / delta, as the chunk maps
+template <typename T, class M>
+__global__ __launch_bounds__(kBlock) void stream_records_kernel(const StreamArgs a) {
+    constexpr int NCH = M::NP + M::NA;
+    const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;  // e * NTRAJ + i: coalesced rows
+    if (g >= a.S * M::NTRAJ) return;
+    const int64_t e = g / M::NTRAJ;
+    const int i = int(g % M::NTRAJ);
+    const int64_t c = e / a.L;
+    const T* t4 = static_cast<const T*>(a.traj4);
+    const T* wx = static_cast<const T*>(a.wx);
+    int ch = 0;  // the chain whose first component is state i (the trajectory holds those)
+#pragma unroll
+    for (int cc = 0; cc < NCH; ++cc)
+        if (chain_state<M>(cc, 0) == i) ch = cc;
+    const int ns = ch < M::NP ? 3 : 2;
+    const double x0 = double(t4[g]);
+    double acc = x0;
+#pragma unroll
+    for (int qq = 0; qq < 3; ++qq) {
+        if (qq >= ns) continue;
+        const double xq = double(t4[(qq + 1) * a.vstride * M::NTRAJ + g]);
+        const int idx = chain_state<M>(ch, qq);
+        const double d = a.starts[idx * a.C + c] - double(wx[idx * a.C + c]);
+        acc = __builtin_fma((xq - x0) / a.delta, d, acc);
+    }
+    static_cast<T*>(a.traj)[g] = T(acc);
+}
+
+// phase 9 (records from the map pass): the verdict without a final pass: no failed chunk
+// filter, finite chunk starts and end state, covariance seams within tolerance; a passed run
+// leaves the composed end state and the last chunk's end covariance in the handle
+template <typename T, class M>
+__global__ __launch_bounds__(1024) void stream_finish_maps_kernel(const StreamArgs a) {
+    __shared__ int redb[1024];
+    const int tid = int(threadIdx.x);
+    int bad = 0;
+    for (int64_t g = tid; g < a.C * M::N; g += blockDim.x) {
+        const double v = a.starts[g];
+        bad |= (v - v == 0.0) ? 0 : 2;  // NaN or inf
+    }
+    if (tid < M::N) {
+        const double v = a.xend[tid];
+        bad |= (v - v == 0.0) ? 0 : 2;
+    }
+    redb[tid] = bad;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (tid < w) redb[tid] |= redb[tid + w];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        StreamCheck* k = a.check;
+        k->state_gap = redb[0] & 2 ? __builtin_inf() : 0.0;
+        k->bad |= redb[0] & 1;
+        const bool ok = k->bad == 0 && k->cov_gap <= a.tol_cov && !(redb[0] & 2);
+        k->ok = ok ? 1 : 0;
+        if (ok) {
+            const int64_t col = a.C - 1, B = 4 * a.C;  // variant 0 of the last chunk
+            for (int i = 0; i < M::N; ++i) static_cast<T*>(a.hx)[i] = T(a.xend[i]);
+            for (int r = 0; r < M::NBLK; ++r) static_cast<T*>(a.hP)[r] = static_cast<const T*>(a.mP)[r * B + col];
+            a.hstatus[0] = 0;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Covariance warm-up by linear-fractional maps (kf_run_stream's default).  Per axis chain the
+// covariance recursion is P <- (A P + B)(C P + D)^-1 with, per event,
+//   predict  [[F, Q F^-T], [0, F^-T]]      (F P F^T + Q with P = X Y^-1)
+//   update   [[I, 0], [H^T R^-1 H, I]]     ((P^-1 + H^T R^-1 H)^-1, the Joseph form's value)
+// so a chunk's covariance map is the 6x6 product of its events' matrices (an (att, rate)
+// chain carries the chain kernel's inert third state as an identity row and column).  The
+// chunk starts are then the fixed point of P(c) = map_(c-1)(P(c-1)) from P(0) = the handle's
+// P, reached by parallel iterations: the recursion forgets its start (each chunk of the
+// reference's 200 Hz IMU stream contracts an error by ~1e-3), so a few iterations over all
+// chunks at once replace the W-event warm-up; the device seam check still decides.
+// ------------------------------------------------------------------------------------
+template <class M>
+__device__ __forceinline__ void chain_noise(int ch, double (&q)[3], double (&si_imu)[3], double& si_gps) {
+    const bool pva = ch < M::NP;
+    q[0] = pva ? kQPos : kQAtt;
+    q[1] = pva ? kQVel : kQRate;
+    q[2] = pva ? kQAcc : 0.0;
+    si_imu[0] = 1.0 / (pva ? kRPos : kRAtt);
+    si_imu[1] = 1.0 / (pva ? kRVel : kRRate);
+    si_imu[2] = pva ? 1.0 / kRAcc : 0.0;
+    si_gps = pva ? 1.0 / kRGps : 0.0;
+}
+
+// phase 6: the product of each chunk's event matrices per chain.  An event acts on the columns
+// of the 6x6 product independently, so a lane group of 8 holds one (chunk, chain): lane j < 6
+// carries column j.  Rescaled by a power of two (the group's max, DPP) every 16 events, which a
+// linear-fractional map ignores.  Event types and dt are loaded 8 events at a time.
+template <class M>
+__device__ __forceinline__ void lft_event(double (&v)[6], int type, double dt, bool pva, const double (&q)[3],
+                                          const double (&si)[3], double sg) {
+    if (type == 255) return;
+    const double c02 = pva ? 0.5 * dt * dt : 0.0, c12 = pva ? dt : 0.0;
+    const double g20 = dt * c12 - c02;
+    // bottom <- F^-T bottom; top <- F top + Q dt (new bottom)
+    const double b0 = v[3], b1 = __builtin_fma(-dt, v[3], v[4]);
+    const double b2 = __builtin_fma(g20, v[3], __builtin_fma(-c12, v[4], v[5]));
+    const double t0 = __builtin_fma(c02, v[2], __builtin_fma(dt, v[1], v[0]));
+    const double t1 = __builtin_fma(c12, v[2], v[1]);
+    v[0] = __builtin_fma(q[0] * dt, b0, t0);
+    v[1] = __builtin_fma(q[1] * dt, b1, t1);
+    v[2] = __builtin_fma(q[2] * dt, b2, v[2]);
+    v[3] = b0;
+    v[4] = b1;
+    v[5] = b2;
+    if (type == kGps || type == kImu) {  // bottom += H^T R^-1 H top
+        const bool gps = type == kGps;
+        v[3] = __builtin_fma(gps ? sg : si[0], v[0], v[3]);
+        v[4] = __builtin_fma(gps ? 0.0 : si[1], v[1], v[4]);
+        v[5] = __builtin_fma(gps ? 0.0 : si[2], v[2], v[5]);
+    }
+}
+
+template <typename T, class M>
+__global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArgs a) {
+    constexpr int NCH = M::NP + M::NA;
+    const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    const int64_t grp = g / kGroup;
+    if (grp >= a.C * a.np * NCH) return;  // whole groups leave together
+    const int j = int(g % kGroup);
+    const int64_t cp = grp / NCH;  // chunk * np + piece
+    const int ch = int(grp % NCH);
+    const bool pva = ch < M::NP;
+    double q[3], si[3], sg;
+    chain_noise<M>(ch, q, si, sg);
+    double v[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v[i] = i == j ? 1.0 : 0.0;  // lanes 6, 7: zero columns
+    const int64_t c = cp / a.np, piece = cp % a.np;
+    const int64_t cend = (c + 1) * a.L < a.S ? (c + 1) * a.L : a.S;
+    const int64_t e0 = c * a.L + piece * a.lp, e1 = e0 + a.lp < cend ? e0 + a.lp : cend;
+    constexpr int kB = 8;
+    for (int64_t e = e0; e < e1; e += kB) {
+        int ty[kB];
+        double dv[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const bool in = e + k < e1;
+            ty[k] = in ? int(a.etype[e + k]) : 255;
+            dv[k] = in ? a.dt[e + k] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < kB; ++k) lft_event<M>(v, ty[k], dv[k], pva, q, si, sg);
+        if (((e - e0) & 15) == kB) {  // every 16 events
+            double mx = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) mx = fmax(mx, fabs(v[i]));
+            mx = fmax(mx, dpp_d<kDppXor1>(mx));
+            mx = fmax(mx, dpp_d<kDppXor2>(mx));
+            mx = fmax(mx, dpp_d<kDppHalfMirror>(mx));
+            int ex;
+            (void)frexp(mx, &ex);
+            const double sc = ldexp(1.0, -ex);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) v[i] *= sc;
+        }
+    }
+    if (j < 6) {
+        double* o = a.phi + grp * 36;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) o[i * 6 + j] = v[i];
+    }
+}
+
+// a chain's block of the block-packed covariance as a full 3x3 (the inert state: variance 1)
+template <typename T, class M>
+__device__ __forceinline__ void chain_block_full(const T* P, int64_t stride, int64_t col, int ch, double (&p)[3][3]) {
+    const int r0 = chain_row0<M>(ch);
+    if (ch < M::NP) {
+        const double v[6] = {double(P[(r0 + 0) * stride + col]), double(P[(r0 + 1) * stride + col]),
+                             double(P[(r0 + 2) * stride + col]), double(P[(r0 + 3) * stride + col]),
+                             double(P[(r0 + 4) * stride + col]), double(P[(r0 + 5) * stride + col])};
+        p[0][0] = v[0], p[0][1] = p[1][0] = v[1], p[0][2] = p[2][0] = v[2];
+        p[1][1] = v[3], p[1][2] = p[2][1] = v[4], p[2][2] = v[5];
+    } else {
+        const double v[3] = {double(P[(r0 + 0) * stride + col]), double(P[(r0 + 1) * stride + col]),
+                             double(P[(r0 + 2) * stride + col])};
+        p[0][0] = v[0], p[0][1] = p[1][0] = v[1], p[1][1] = v[2];
+        p[0][2] = p[2][0] = p[1][2] = p[2][1] = 0.0;
+        p[2][2] = 1.0;
+    }
+}
+
+// phase 7: one parallel iteration P(c) <- map_(c-1)(P(c-1)), P(0) = the handle's P; the last
+// writes the warm-up bank's covariance: chunk c starts from P(c - kp) (kp polish chunks of
+// event warm-up follow; c < kp: the handle's P, exact)
+template <typename T, class M>
+__global__ __launch_bounds__(kBlock) void stream_lft_iter_kernel(const StreamArgs a) {
+    constexpr int NCH = M::NP + M::NA;
+    const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (g >= a.C * NCH) return;
+    const int64_t c = g / NCH;
+    const int ch = int(g % NCH);
+    double pn[3][3];
+    double ph[3][3];
+    chain_block_full<T, M>(static_cast<const T*>(a.hP), 1, 0, ch, ph);
+    if (c == 0) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) pn[i][j] = ph[i][j];
+    } else {
+        double p[3][3];
+        if (a.pcur) {  // the first iteration guesses the handle's P everywhere
+            const double* pc = a.pcur + (g - NCH) * 9;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) p[i][j] = pc[i * 3 + j];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) p[i][j] = ph[i][j];
+        }
+        // chunk c - 1's piece maps in order (each piece short enough for its map to be well
+        // conditioned; the LFT error grows with the events one product spans)
+        for (int pi = 0; pi < a.np; ++pi) {
+        const double* m = a.phi + (((c - 1) * a.np + pi) * NCH + ch) * 36;
+        double X[3][3], Y[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                double x = m[i * 6 + 3 + j], y = m[(i + 3) * 6 + 3 + j];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    x = __builtin_fma(m[i * 6 + k], p[k][j], x);
+                    y = __builtin_fma(m[(i + 3) * 6 + k], p[k][j], y);
+                }
+                X[i][j] = x;
+                Y[i][j] = y;
+            }
+        // P' = X Y^-1 via the adjugate of Y, then symmetrised
+        const double a00 = Y[1][1] * Y[2][2] - Y[1][2] * Y[2][1], a01 = Y[0][2] * Y[2][1] - Y[0][1] * Y[2][2],
+                     a02 = Y[0][1] * Y[1][2] - Y[0][2] * Y[1][1];
+        const double a10 = Y[1][2] * Y[2][0] - Y[1][0] * Y[2][2], a11 = Y[0][0] * Y[2][2] - Y[0][2] * Y[2][0],
+                     a12 = Y[0][2] * Y[1][0] - Y[0][0] * Y[1][2];
+        const double a20 = Y[1][0] * Y[2][1] - Y[1][1] * Y[2][0], a21 = Y[0][1] * Y[2][0] - Y[0][0] * Y[2][1],
+                     a22 = Y[0][0] * Y[1][1] - Y[0][1] * Y[1][0];
+        const double det = Y[0][0] * a00 + Y[0][1] * a10 + Y[0][2] * a20;
+        const double inv[3][3] = {{a00, a01, a02}, {a10, a11, a12}, {a20, a21, a22}};
+        const double rd = 1.0 / det;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                double s = 0.0;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) s = __builtin_fma(X[i][k], inv[k][j], s);
+                pn[i][j] = s * rd;
+            }
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = i + 1; j < 3; ++j) pn[i][j] = pn[j][i] = 0.5 * (pn[i][j] + pn[j][i]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) p[i][j] = pn[i][j];
+        }
+    }
+    double* o = a.pnext + g * 9;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) o[i * 3 + j] = pn[i][j];
+    if (a.last) {
+        T* wP = static_cast<T*>(a.wP);
+        const int r0 = chain_row0<M>(ch);
+        auto put = [&](int64_t col, const double (&p)[3][3]) {
+            if (ch < M::NP) {
+                wP[(r0 + 0) * a.C + col] = T(p[0][0]);
+                wP[(r0 + 1) * a.C + col] = T(p[0][1]);
+                wP[(r0 + 2) * a.C + col] = T(p[0][2]);
+                wP[(r0 + 3) * a.C + col] = T(p[1][1]);
+                wP[(r0 + 4) * a.C + col] = T(p[1][2]);
+                wP[(r0 + 5) * a.C + col] = T(p[2][2]);
+            } else {
+                wP[(r0 + 0) * a.C + col] = T(p[0][0]);
+                wP[(r0 + 1) * a.C + col] = T(p[0][1]);
+                wP[(r0 + 2) * a.C + col] = T(p[1][1]);
+            }
+        };
+        if (c + a.kp < a.C) put(c + a.kp, pn);
+        if (c < a.kp) put(c, ph);
     }
 }
 
@@ -1733,12 +2054,17 @@ void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
         case 2: stream_maps_kernel<T, M><<<segs, NCH * kStreamSeg, 0, stream>>>(a); break;
         case 3: stream_segscan_kernel<T, M><<<1, 1024, 0, stream>>>(a); break;
         case 4: stream_apply_kernel<T, M><<<segs, NCH * kStreamSeg, 0, stream>>>(a); break;
-        default: stream_finish_kernel<T, M><<<1, 1024, 0, stream>>>(a); break;
+        case kStreamPhaseLftMaps: stream_lft_maps_kernel<T, M><<<grid(a.C * a.np * NCH * kGroup), kBlock, 0, stream>>>(a); break;
+        case kStreamPhaseLftIter: stream_lft_iter_kernel<T, M><<<grid(a.C * NCH), kBlock, 0, stream>>>(a); break;
+        case 5: stream_finish_kernel<T, M><<<1, 1024, 0, stream>>>(a); break;
+        case kStreamPhaseRecords: stream_records_kernel<T, M><<<grid(a.S * M::NTRAJ), kBlock, 0, stream>>>(a); break;
+        case kStreamPhaseFinishMaps: stream_finish_maps_kernel<T, M><<<1, 1024, 0, stream>>>(a); break;
+        default: break;
     }
 }
 
 hipError_t launch_stream_phase(int model, bool f64, int phase, const StreamArgs& a, hipStream_t stream) {
-    if (a.C < 2 || phase < 0 || phase > 5) return hipErrorInvalidValue;
+    if (a.C < 2 || phase < 0 || phase > kStreamPhaseFinishMaps) return hipErrorInvalidValue;
     if (model == 15) {
         if (f64) stream_phase<double, M15>(phase, a, stream);
         else stream_phase<float, M15>(phase, a, stream);

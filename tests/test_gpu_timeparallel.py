@@ -81,13 +81,20 @@ def _parallel(et, dt, pay, x0, **kw):
     return tr.double().cpu().numpy(), ld.double().cpu().numpy(), x.double().cpu().numpy(), P.double().cpu().numpy()
 
 
-@pytest.mark.parametrize('T,chunk,skips', [(60000, None, 0), (45001, 777, 50), (5000, 256, 3)])
-def test_parallel_equals_single_filter(T, chunk, skips):
-    """Records, final state and covariance equal the one-filter run; ragged last chunk, NONE
-    events, and (T = 5000) chunks whose warm-up window reaches the stream start (exact)."""
+@pytest.mark.parametrize('final_pass', [False, True])
+@pytest.mark.parametrize('T,chunk,skips,warmup', [(60000, None, 0, None), (45001, 777, 50, None),
+                                                  (5000, 256, 3, 2560), (30001, 300, 7, -3)])
+def test_parallel_equals_single_filter(T, chunk, skips, warmup, final_pass, monkeypatch):
+    """Records, final state and covariance equal the one-filter run, with the records taken
+    from the map pass (default) or from a final pass over the true starts; the covariance
+    warm-up by linear-fractional maps (default), by events (T = 5000: chunks whose warm-up
+    reaches the stream start are exact) and by maps plus one chunk of events; ragged last
+    chunk, NONE events."""
+    if final_pass:
+        monkeypatch.setenv('KFMI_STREAM_FINAL', '1')
     et, dt, pay, x0 = _stream(T, seed=T, skips=skips)
     seq = _sequential(et, dt, pay, x0)
-    par = _parallel(et, dt, pay, x0, chunk=chunk)
+    par = _parallel(et, dt, pay, x0, chunk=chunk, warmup=warmup)
     chk = ref15.parallel_check
     assert chk['ok'] and chk['chunks'] > 1, chk
     assert chk['cov_gap'] <= 1e-12  # the warm-up reached the covariance (to roundoff)
@@ -141,9 +148,12 @@ def test_nan_fix_falls_back():
         np.testing.assert_array_equal(a, b)
 
 
-def test_records_updated_cov_ref8():
+@pytest.mark.parametrize('final_pass', [False, True])
+def test_records_updated_cov_ref8(final_pass, monkeypatch):
     """Every record kf_run_events writes (traj, logdet, updated, covariance) and the 8-state
     model, through the C ABI route kf_run_events takes by itself for T >= 65536."""
+    if final_pass:
+        monkeypatch.setenv('KFMI_STREAM_FINAL', '1')
     T = 70000
     et, dt, pay, x0 = _stream(T, seed=13, skips=20)
     for model in ('ref15', 'ref8'):

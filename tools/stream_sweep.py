@@ -24,7 +24,7 @@ from kfmi.engine import _ptr  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--warmup', default='1024,1536,2048,2560')
+    ap.add_argument('--warmup', default='-2,-3,-1,1536,2048')
     ap.add_argument('--chunk', default='0')
     ap.add_argument('--reps', type=int, default=5)
     args = ap.parse_args()
