@@ -248,7 +248,7 @@ int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const d
  * of the handle's dtype (n_events <= 30, nullable) receives every evaluated subset's max
  * log-determinant (NaN for a failed filter), indexed by mask.  Level k stores the C(n - 1, k)
  * subsets without the last candidate (the others have no extensions); C(n - 1, k) must stay
- * below 2^28, and the handle's level buffers take 2 * C(n - 1, k) * (43 w + 16) bytes at the
+ * below 2^28, and the handle's level buffers take 2 * C(n - 1, k) * (28 w + 16) bytes at the
  * widest stored level (w = 8 for f64, 4 for f32).  The call synchronises `stream`. */
 int kf_search_combos(kf_batch* handle, int n_events, const double* events, const double* init,
                      double prev_time, double target_end, double threshold, int k_max, int exhaustive,

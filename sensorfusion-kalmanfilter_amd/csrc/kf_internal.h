@@ -160,7 +160,8 @@ struct Ref15ComboArgs {
 // k - 1's stored states.  Levels are in colex order: the subsets whose largest event is j hold
 // ranks [C(j, k), C(j + 1, k)) and child rank = parent rank + C(j, k).  One lane per parent
 // evaluates all of its children.  Level buffer: node blocks of 64 nodes, block b =
-//   [43][64] T       x (15), block-packed P (27), running max log-det (NaN = failed filter)
+//   [28][64] T       block-packed P (27), running max log-det (NaN = failed filter); no state:
+//                    the max log-det depends on the covariance alone
 //   [64] double      time of the last applied event
 //   [64] uint64      subset bit mask
 struct Ref15SearchArgs {
@@ -186,7 +187,8 @@ struct Ref15SearchArgs {
     void* subset_max;        // device [2^n] T: every subset's max log-det by mask, or nullptr
 };
 
-__host__ __device__ constexpr uint64_t search_block_bytes(uint64_t elem) { return 64 * (43 * elem + 16); }
+constexpr int kSearchRows = 28;  // T rows of a search node
+__host__ __device__ constexpr uint64_t search_block_bytes(uint64_t elem) { return 64 * (kSearchRows * elem + 16); }
 __host__ __device__ inline uint64_t search_level_bytes(uint64_t nodes, uint64_t elem) {
     return (nodes + 63) / 64 * search_block_bytes(elem);
 }

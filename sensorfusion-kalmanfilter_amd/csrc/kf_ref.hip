@@ -1520,7 +1520,7 @@ __device__ __forceinline__ T* level_row(char* blk, uint32_t lane, int r) {
 }
 template <typename T>
 __device__ __forceinline__ double* level_tail(char* blk, uint32_t lane, int q) {
-    return reinterpret_cast<double*>(blk + 43 * 64 * int(sizeof(T)) + q * 512) + lane;
+    return reinterpret_cast<double*>(blk + kSearchRows * 64 * int(sizeof(T)) + q * 512) + lane;
 }
 
 // Chains<T, M15>::logdet() accumulated one block at a time, in its order (pva chains, then aw
@@ -1546,8 +1546,12 @@ struct LogdetAcc {
     }
 };
 
-// A stored node of the search: the filter after a subset's events, its running max log-det,
-// the time of its last applied event and its subset mask.
+// A stored node of the search: the covariance after a subset's events, its running max
+// log-det, the time of its last applied event and its subset mask.  The search scores a subset
+// by its max log-det alone, which depends on the covariance alone, and the covariance does not
+// depend on the measurements (nor, so, on the state): the state is not carried (kf_eval_combos
+// carries it for the per-combination API).  x stays as constant zeros, so the state half of
+// every update is dead code the compiler removes.
 template <typename T>
 struct SearchNode {
     T x[15], P[27];
@@ -1584,7 +1588,7 @@ struct SearchNode {
             prev = e[0];
         }
 #pragma unroll
-        for (int i = 0; i < 15; ++i) x[i] = r.x[i];
+        for (int i = 0; i < 15; ++i) x[i] = T(0);
 #pragma unroll
         for (int i = 0; i < 27; ++i) P[i] = r.blk(i);
         T fmax = run;
@@ -1599,10 +1603,10 @@ struct SearchNode {
         char* blk = level_block<T>(level, p);
         const uint32_t lane = uint32_t(p) & 63u;
 #pragma unroll
-        for (int i = 0; i < 15; ++i) x[i] = *level_row<T>(blk, lane, i);
+        for (int i = 0; i < 15; ++i) x[i] = T(0);
 #pragma unroll
-        for (int i = 0; i < 27; ++i) P[i] = *level_row<T>(blk, lane, 15 + i);
-        run = *level_row<T>(blk, lane, 42);
+        for (int i = 0; i < 27; ++i) P[i] = *level_row<T>(blk, lane, i);
+        run = *level_row<T>(blk, lane, 27);
         prev = *level_tail<T>(blk, lane, 0);
         mask = __builtin_bit_cast(uint64_t, *level_tail<T>(blk, lane, 1));
     }
@@ -1676,9 +1680,7 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
         }
         if (cb) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, M15::pva(ch, i)) = xb[i];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) *level_row<T>(cb, cl, 15 + 6 * ch + i) = Pb[i];
+            for (int i = 0; i < 6; ++i) *level_row<T>(cb, cl, 6 * ch + i) = Pb[i];
         }
         rec.add_pva(Pb, ch);
         if (final_predict) C15::template chain_predict<3>(xb, Pb, dte, qpva);
@@ -1700,9 +1702,7 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
         }
         if (cb) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i) *level_row<T>(cb, cl, M15::aw(ch, i)) = xa[i];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, 15 + 6 * M15::NP + 3 * ch + i) = Pa[i];
+            for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, 6 * M15::NP + 3 * ch + i) = Pa[i];
         }
         rec.add_aw(Pa);
         if (final_predict) C15::template chain_predict<2>(xa, Pa, dte, qaw);
@@ -1720,7 +1720,7 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
         fmax = ld > crun ? ld : crun;
     }
     if (cb) {
-        *level_row<T>(cb, cl, 42) = crun;
+        *level_row<T>(cb, cl, 27) = crun;
         *level_tail<T>(cb, cl, 0) = cprev;
         *level_tail<T>(cb, cl, 1) = __builtin_bit_cast(double, cmask);
     }

@@ -531,7 +531,7 @@ def brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype='f64', d
 def search_level_bytes(nodes, dtype):
     """Device bytes of one kf_search_combos level buffer (node blocks of 64, kf_internal.h)."""
     w = 8 if dtype == 'f64' else 4
-    return (nodes + 63) // 64 * 64 * (43 * w + 16)
+    return (nodes + 63) // 64 * 64 * (28 * w + 16)
 
 
 def search_levels(n, dtype='f64', mem_bytes=32 << 30):
