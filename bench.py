@@ -498,7 +498,7 @@ def bf_workload(cfg, args, rank, world, dev):
         # written once and read once as a parent
         lvl = sum(search_level_bytes(math.comb(n - 1, k), 'f64') for k in range(1, n))
         return dict(step=step, units=total_steps, bytes=2 * lvl, bytes_per_unit=2 * lvl / total_combos,
-                    kernel='ref15_search_pm_kernel+ref15_search_cm_kernel (the 25 level launches of one search)', traffic=None, cpu=cpu, gather=None, kf=kf, combos=total_combos,
+                    kernel='ref15_search_pm_kernel+ref15_search_cm_kernel (the 25 level launches of one search)', traffic=load_traffic('bf'), cpu=cpu, gather=None, kf=kf, combos=total_combos,
                     roofline_note='level-buffer bytes only (each stored prefix filter written and read once); the '
                                   'kernel is co-limited by fp64 issue (one event step + final predict per subset)',
                     desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '

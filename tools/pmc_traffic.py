@@ -15,6 +15,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "sensorfusion-kalmanfilter_amd"))
 
 
 def per_kernel(d, counter):
@@ -54,7 +55,26 @@ def main():
     res = {'calibration': {'fetch_size_scale': read_scale, 'write_size_scale': write_scale,
                            'probe': 'tools/probes/bw_probe soa_read/soa_write, 8 B per lane, B=2^20, T=64'}}
     for c in cfgs:
-        kern = 'ref_events_kernel' if c == 'ref15' else 'cv_block_kernel'
+        if c == 'bf':
+            # one search = its n level launches (ref15_search_{cm,pm}_kernel), summed
+            n = CONFIGS['bf']['n']
+            fk = per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE')
+            wk = per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE')
+            f = [v for k, vs in fk.items() if 'ref15_search' in k for v in vs]
+            w = [v for k, vs in wk.items() if 'ref15_search' in k for v in vs]
+            fetch = 1024 * sum(f) / (len(f) / n)
+            write = 1024 * sum(w) / (len(w) / n)
+            from kfmi.ref15 import search_level_bytes
+            import math
+            alg = 2 * sum(search_level_bytes(math.comb(n - 1, k), 'f64') for k in range(1, n))
+            res['configbf'] = {
+                'fetch_bytes_raw': fetch, 'write_bytes_raw': write,
+                'bytes_per_launch': fetch * read_scale + write * write_scale,
+                'algorithmic_bytes_per_launch': alg,
+                'traffic_over_algorithmic': (fetch * read_scale + write * write_scale) / alg,
+                'launches_profiled': len(f), 'note': 'per search: the sum over its n level launches'}
+            continue
+        kern = 'ref_events' if c == 'ref15' else 'cv_block_kernel'
         f = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE'), kern)
         w = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE'), kern)
         fetch = 1024 * sum(f) / len(f)
