@@ -168,12 +168,39 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
                                          'sample': f'{n_np} filters, oracle/ref_kf.run_filter_loop, '
                                                    f'NumPy {np.__version__}'}}
 
+    def pcie(reps=3):
+        """PCIe-inclusive rate: the inputs start in pinned host memory and the
+        trajectory + log-det come back to pinned host memory; H2D, the launch and D2H are timed
+        together on the engine's stream.  Never `value`: `value` is HBM-resident."""
+        hu = u.cpu().pin_memory() if u is not None else None
+        hz = z.cpu().pin_memory()
+        ht, hl = torch.empty(traj.shape, dtype=traj.dtype).pin_memory(), torch.empty(logdet.shape, dtype=logdet.dtype).pin_memory()
+        times = []
+        for _ in range(reps + 1):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            if u is not None:   # the engine launches on torch's current stream
+                u.copy_(hu, non_blocking=True)
+            z.copy_(hz, non_blocking=True)
+            kf.run(u, z, dt=dt, update_every=k, out=(traj, logdet))
+            ht.copy_(traj, non_blocking=True)
+            hl.copy_(logdet, non_blocking=True)
+            torch.cuda.synchronize(dev)
+            times.append(time.perf_counter() - t0)
+        el = min(times[1:])
+        h2d = (hu.numel() * hu.element_size() if hu is not None else 0) + hz.numel() * hz.element_size()
+        d2h = ht.numel() * ht.element_size() + hl.numel() * hl.element_size()
+        return {'value': B * T / el, 'unit': 'KF steps/s', 'ms_per_launch': el * 1e3,
+                'h2d_bytes': h2d, 'd2h_bytes': d2h, 'link_gbs': (h2d + d2h) / el / 1e9,
+                'note': 'inputs u,z from pinned host, trajectory+logdet to pinned host, '
+                        'serial on one stream (no overlap), best of %d' % reps}
+
     d = 2 if cfg['model'] == 'cv2' else 3
     bytes_launch, bytes_step = algorithmic_bytes(cfg)
     kernel = 'cv_block_kernel' if block_kernel_in_use() else 'cv_run_kernel'
     return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_step, kernel=kernel,
                 traffic=load_traffic(cfg_id) if kernel == 'cv_block_kernel' else None, cpu=cpu,
-                gather=gather_payload, kf=kf,
+                gather=gather_payload, kf=kf, pcie=pcie,
                 desc=f"BASELINE config {cfg_id}: {cfg['model']} ({2 * d}-state/{d}-meas), {cfg['dtype']}, "
                      f"B={B} filters/GPU, T={T}, dt={dt}, GPS update every {k} step(s)",
                 extra={'filters_per_gpu': B, 'time_steps_per_launch': T, 'update_every': k})
@@ -522,6 +549,7 @@ def main():
     ap.add_argument('--config', default='3', choices=sorted(CONFIGS))
     ap.add_argument('--batch', type=int, default=None, help='override filters per GPU')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--pcie', action='store_true', help='also report the PCIe-inclusive rate (cv configs, N=1)')
     ap.add_argument('--ablate', choices=['none', 'no-traj', 'no-logdet', 'no-traj-no-logdet'], default='none',
                     help='diagnostics only: skip an output stream (the JSON line says so)')
     args = ap.parse_args()
@@ -628,6 +656,8 @@ def main():
         if gather_ms is not None:
             rec['allgather_ms'] = gather_ms
         rec['cpu_baseline'] = w['cpu']() if (world == 1 and not args.no_cpu_baseline) else None
+        if args.pcie and world == 1 and w.get('pcie'):
+            rec['pcie_inclusive'] = w['pcie']()
         print(json.dumps(rec), flush=True)
     kf.close()
     if dist:
