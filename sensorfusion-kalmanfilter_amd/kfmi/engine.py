@@ -249,6 +249,56 @@ class BatchedKF:
                                 _ptr(md), int(update_every), _ptr(tr), _ptr(ld), self._stream()))
         return tr, ld
 
+    def run_host(self, u, z, dt, update_every=1, chunks=8, traj=None, logdet=None):
+        """``run`` for streams that live in host memory (numpy arrays or CPU tensors, the shapes
+        of ``run``): T is cut into ``chunks`` time chunks and the H2D copy of chunk i+1, the
+        launch on chunk i and the D2H copy of chunk i-1 overlap on three streams (the filter
+        state carries across launches in the handle, so the result is that of one ``run``).
+        traj/logdet: pinned CPU tensors to fill (allocated pinned when None).  Returns them
+        after the last copy has landed.  DESIGN.md §4 gives the measured rate (1.5x serial)."""
+        def host(a, shape, name):
+            if isinstance(a, np.ndarray):
+                a = torch.from_numpy(np.ascontiguousarray(a))
+            if tuple(a.shape) != tuple(shape) or a.dtype != self.torch_dtype or a.device.type != 'cpu':
+                raise ValueError(f'{name}: expected a CPU {self.torch_dtype} array of shape {tuple(shape)}')
+            return a.contiguous() if a.is_pinned() else a.contiguous().pin_memory()
+        T, k = int(u.shape[0]), int(update_every)
+        if T % k:
+            raise ValueError('run_host: T must be a multiple of update_every')
+        while chunks > 1 and T % (chunks * k):
+            chunks -= 1
+        hu = host(u, (T, self.c, self.batch), 'u')
+        hz = host(z, (T // k, self.m, self.batch), 'z')
+        ht = traj if traj is not None else torch.empty(T, self.n, self.batch, dtype=self.torch_dtype).pin_memory()
+        hl = logdet if logdet is not None else torch.empty(T, self.batch, dtype=self.torch_dtype).pin_memory()
+        host(ht, (T, self.n, self.batch), 'traj')
+        host(hl, (T, self.batch), 'logdet')
+        du, dz = self.empty(T, self.c, self.batch), self.empty(T // k, self.m, self.batch)
+        dtr, dld = self.empty(T, self.n, self.batch), self.empty(T, self.batch)
+        sh, sc, sd = (torch.cuda.Stream(self.device) for _ in range(3))
+        prev = torch.cuda.current_stream(self.device)
+        sh.wait_stream(prev)
+        tc = T // chunks
+        for i in range(chunks):
+            a, b = i * tc, (i + 1) * tc
+            with torch.cuda.stream(sh):
+                du[a:b].copy_(hu[a:b], non_blocking=True)
+                dz[a // k:b // k].copy_(hz[a // k:b // k], non_blocking=True)
+                ev_in = torch.cuda.Event()
+                ev_in.record(sh)
+            with torch.cuda.stream(sc):
+                sc.wait_event(ev_in)
+                self.run(du[a:b], dz[a // k:b // k], dt=dt, update_every=k, out=(dtr[a:b], dld[a:b]))
+                ev_run = torch.cuda.Event()
+                ev_run.record(sc)
+            with torch.cuda.stream(sd):
+                sd.wait_event(ev_run)
+                ht[a:b].copy_(dtr[a:b], non_blocking=True)
+                hl[a:b].copy_(dld[a:b], non_blocking=True)
+        sd.synchronize()
+        prev.wait_stream(sc)
+        return ht, hl
+
     # -- reference models: per-filter event streams ----------------------------------------
     def run_events(self, etype, dt, payload, traj=True, logdet=True, updated=False, threshold=None, cov=False):
         """KF_MODEL_REF15 / KF_MODEL_REF8: T events per filter in one launch (kf_run_events).

@@ -162,6 +162,25 @@ def test_chunked_runs_resume_bit_exactly():
     np.testing.assert_array_equal(P.cpu().numpy(), Pf)
 
 
+@pytest.mark.parametrize('dtype,k,chunks', [('f64', 1, 8), ('f32', 2, 4), ('f64', 4, 5)])
+def test_run_host_pipeline_matches_one_run(dtype, k, chunks):
+    """run_host (host streams, H2D | launch | D2H overlapped over time chunks) == one run on
+    device-resident streams, bit for bit; chunks=5 with T=64, k=4 falls back to 4 chunks."""
+    model = ref_kf.CV3
+    B, T = 1031, 64
+    x0, u, z = random_inputs(model, B, T, k, seed=23)
+    tr, ld, xf, Pf, _ = engine_run('cv3', dtype, x0, u, z, k, dt=0.1)
+    kf = kfmi.BatchedKF('cv3', B, dtype)
+    kf.reset(torch.from_numpy(np.ascontiguousarray(x0.T.astype(NP[dtype]))).cuda())
+    ht, hl = kf.run_host(u.astype(NP[dtype]), z.astype(NP[dtype]), dt=0.1, update_every=k, chunks=chunks)
+    assert ht.device.type == 'cpu' and ht.is_pinned()
+    np.testing.assert_array_equal(ht.double().numpy(), tr)
+    np.testing.assert_array_equal(hl.double().numpy(), ld)
+    x, P = kf.state()
+    np.testing.assert_array_equal(P.double().cpu().numpy(), Pf)
+    kf.close()
+
+
 def test_deterministic_repeat():
     model = ref_kf.CV2
     x0, u, z = random_inputs(model, 2048, 32, 1, seed=2)
