@@ -366,8 +366,6 @@ def log_workload(cfg, args, rank, world, dev):
     prev0 = float(t_ev[0])
     L = _lib.lib()
 
-    if not cfg['parallel']:
-        os.environ['KFMI_STREAM'] = 'off'   # kf_run_events would route a one-filter log through kf_run_stream
     stream_check = {}
 
     def step():
@@ -381,8 +379,9 @@ def log_workload(cfg, args, rank, world, dev):
             if not stream_check:  # first (warm-up) step: record the device checks (synchronises)
                 stream_check.update(kf.stream_check())
             return
-        _lib.check(L.kf_run_events(kf.handle, T, _ptr(et), _ptr(dt), _ptr(pay), _ptr(traj), None, _ptr(logdet),
-                                   None, 0, 0.0, kf._stream()))
+        # the single filter (kf_run_events would route a one-filter log through kf_run_stream)
+        _lib.check(L.kf_run_events_seq(kf.handle, T, _ptr(et), _ptr(dt), _ptr(pay), _ptr(traj), None, _ptr(logdet),
+                                       None, 0, 0.0, kf._stream()))
 
     def cpu():
         """One filter cannot use more than one core: the reference's dense event step restated in

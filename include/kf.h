@@ -186,6 +186,14 @@ int kf_run_events(kf_batch* handle, int T, const uint8_t* etype, const double* d
                   void* traj, void* cov, void* logdet, uint8_t* updated, int gate, double threshold,
                   void* stream);
 
+/* kf_run_events without its one-filter route through kf_run_stream: every filter runs its
+ * events in sequence, whatever B and T are (same arguments and outputs).  For callers that want
+ * the sequential single-filter run for one call (A/B, the reference's own op order over a whole
+ * log) without the process-wide KFMI_STREAM=off switch. */
+int kf_run_events_seq(kf_batch* handle, int T, const uint8_t* etype, const double* dt, const void* payload,
+                      void* traj, void* cov, void* logdet, uint8_t* updated, int gate, double threshold,
+                      void* stream);
+
 /* One filter over a long event stream, parallel over time: kf_run_events for a handle of ONE
  * filter (B = 1, no gate), with the same arguments, outputs and final state, computed as
  * chunks of `chunk` events run as filters of one launch (chunk <= 0: max(128, T / 2048)).
@@ -212,8 +220,9 @@ int kf_run_stream(kf_batch* handle, int T, const uint8_t* etype, const double* d
 
 /* The checks of the handle's last kf_run_stream (synchronises `stream`): out[0] = 1 if the
  * chunked run's records stood (0: the sequential fallback ran), out[1] = 1 if a chunk filter
- * failed, out[2] = covariance seam gap, out[3] = state seam gap (records from the map pass: 0,
- * or inf for a non-finite chunk start), out[4] = chunks (1: the stream was too short to split
+ * failed, out[2] = covariance seam gap, out[3] = state seam gap (final pass only; records from
+ * the map pass: NaN = not measured, the chunk starts being the composed maps' values, or inf for
+ * a non-finite chunk start), out[4] = chunks (1: the stream was too short to split
  * and ran sequentially), out[5] = chunk length, out[6] = events of event warm-up. */
 int kf_stream_check(kf_batch* handle, double* out, void* stream);
 
@@ -225,7 +234,8 @@ int kf_stream_check(kf_batch* handle, double* out, void* stream);
  * (t, KF_EVENT_GPS|KF_EVENT_IMU, payload[9]), n_events <= 64.  Outputs per filter: the final
  * state in the handle, logdets device [k+2][B] (records, NaN-padded) and max_logdet device [B]
  * (the brute-force acceptance test max(log_det) < R_threshold, :1353), n_records device [B];
- * status 1 marks lanes past the last combination.  Replaces the Pool(30) fan-out of
+ * status 1 marks lanes past the last combination.  With logdets non-NULL, (k + 2) * B * w must
+ * stay below 4 GiB (KF_EINVAL otherwise; w = 8 for f64, 4 for f32).  Replaces the Pool(30) fan-out of
  * run_brute_force_kalman_filter_no_sampling_min_usage (:1320-1346). */
 int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const double* init,
                    double prev_time, double target_end, int k, uint64_t combo_offset, void* logdets,

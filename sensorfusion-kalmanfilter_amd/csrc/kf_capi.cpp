@@ -534,18 +534,39 @@ size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
 
 }  // namespace
 
+namespace {
+// kf_run_events / kf_run_events_seq arguments; 1 = valid and there is work, 0 = nothing to do
+int check_events_args(const kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload,
+                      const char* what, int* rc) {
+    *rc = check_handle(h);
+    if (*rc) return 0;
+    if (!is_ref(h)) *rc = fail(KF_EINVAL, "%s: needs a KF_MODEL_REF15 or KF_MODEL_REF8 handle", what);
+    else if (T < 0) *rc = fail(KF_EINVAL, "%s: T = %d < 0", what, T);
+    else if (T == 0 || h->B == 0) return 0;
+    else if (!etype || !dt || !payload) *rc = fail(KF_EINVAL, "%s: null etype/dt/payload stream", what);
+    return *rc == KF_OK;
+}
+}  // namespace
+
 int kf_run_events(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload,
                   void* traj, void* cov, void* logdet, uint8_t* updated, int gate, double threshold,
                   void* stream) {
-    if (int rc = check_handle(h)) return rc;
-    if (!is_ref(h)) return fail(KF_EINVAL, "kf_run_events: needs a KF_MODEL_REF15 or KF_MODEL_REF8 handle");
-    if (T < 0) return fail(KF_EINVAL, "kf_run_events: T = %d < 0", T);
-    if (T == 0 || h->B == 0) return KF_OK;
-    if (!etype || !dt || !payload) return fail(KF_EINVAL, "kf_run_events: null etype/dt/payload stream");
-    // one filter over a long stream: parallel over time (checked, with a sequential fallback)
+    int rc = KF_OK;
+    if (!check_events_args(h, T, etype, dt, payload, "kf_run_events", &rc)) return rc;
+    // one filter over a long stream: parallel over time (checked, with a sequential fallback);
+    // KFMI_STREAM=off is a process-wide diagnostic switch, callers that want the sequential
+    // run per call use kf_run_events_seq
     const char* sv = std::getenv("KFMI_STREAM");
     if (h->B == 1 && !gate && T >= kStreamMinEvents && !(sv && !std::strcmp(sv, "off")))
         return kf_run_stream(h, T, etype, dt, payload, traj, cov, logdet, updated, 0, -1, stream);
+    return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, gate, threshold, nullptr, stream);
+}
+
+int kf_run_events_seq(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload,
+                      void* traj, void* cov, void* logdet, uint8_t* updated, int gate, double threshold,
+                      void* stream) {
+    int rc = KF_OK;
+    if (!check_events_args(h, T, etype, dt, payload, "kf_run_events_seq", &rc)) return rc;
     return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, gate, threshold, nullptr, stream);
 }
 
@@ -745,6 +766,11 @@ int kf_eval_combos(kf_batch* h, int n_events, const double* events, const double
     if (int rc = check_handle(h)) return rc;
     if (int rc = check_combo_inputs(h, n_events, events, init, "kf_eval_combos")) return rc;
     if (k < 1 || k > n_events) return fail(KF_EINVAL, "kf_eval_combos: k = %d outside [1, %d]", k, n_events);
+    // the k + 2 logdet record rows are addressed through one buffer descriptor with a 32-bit
+    // byte range and 32-bit lane offsets (ref15_combo_kernel)
+    if (logdets && uint64_t(k + 2) * uint64_t(h->B) * elem(h) >= (uint64_t(1) << 32))
+        return fail(KF_EINVAL, "kf_eval_combos: logdet records of %d rows x %lld filters exceed 4 GiB; "
+                               "use fewer filters per launch or logdets = NULL", k + 2, (long long)h->B);
     if (h->B == 0) return KF_OK;
     const uint64_t n_combos = binom_table()[n_events * (kMaxComboEvents + 1) + k];
     hipStream_t st = static_cast<hipStream_t>(stream);

@@ -1100,7 +1100,9 @@ __global__ __launch_bounds__(1024) void stream_finish_maps_kernel(const StreamAr
     }
     if (tid == 0) {
         StreamCheck* k = a.check;
-        k->state_gap = redb[0] & 2 ? __builtin_inf() : 0.0;
+        // no state seam is measured here: the chunk starts are the composed maps' values, not
+        // runs from the true starts (KFMI_STREAM_FINAL=1 runs them and checks the seams)
+        k->state_gap = redb[0] & 2 ? __builtin_inf() : __builtin_nan("");
         k->bad |= redb[0] & 1;
         const bool ok = k->bad == 0 && k->cov_gap <= a.tol_cov && !(redb[0] & 2);
         k->ok = ok ? 1 : 0;

@@ -84,6 +84,7 @@ SIGNATURES = {
     'kf_run': (_i, [_vp, _i, _d, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     'kf_synth': (_i, [_vp, ctypes.c_uint64, _i64, _i, _d, _i, _vp, _vp, _vp, _vp]),
     'kf_run_events': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _d, _vp]),
+    'kf_run_events_seq': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _d, _vp]),
     'kf_run_stream': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]),
     'kf_stream_check': (_i, [_vp, _vp, _vp]),
     'kf_eval_combos': (_i, [_vp, _i, _vp, _vp, _d, _d, _i, ctypes.c_uint64, _vp, _vp, _vp, _vp]),

@@ -300,14 +300,16 @@ class BatchedKF:
         return ht, hl
 
     # -- reference models: per-filter event streams ----------------------------------------
-    def run_events(self, etype, dt, payload, traj=True, logdet=True, updated=False, threshold=None, cov=False):
+    def run_events(self, etype, dt, payload, traj=True, logdet=True, updated=False, threshold=None, cov=False,
+                   sequential=False):
         """KF_MODEL_REF15 / KF_MODEL_REF8: T events per filter in one launch (kf_run_events).
 
         etype [T, B] uint8 (KF_EVENT_*), dt [T, B] float64, payload [T, 9, B] (GPS: e, n, alt;
         IMU: roll, pitch, yaw, wx, wy, wz, ax, ay, az).  threshold: adaptive-threshold gating
-        (update only if logdet(P_pred) > threshold).  Returns (traj [T, W, B], logdet [T, B],
-        updated [T, B], cov [T, rows, B]) with None for outputs not asked for (W = 6 for ref15,
-        3 for ref8; cov is block-packed)."""
+        (update only if logdet(P_pred) > threshold).  sequential=True: never the time-parallel
+        route kf_run_events takes by itself for one long filter (kf_run_events_seq).  Returns
+        (traj [T, W, B], logdet [T, B], updated [T, B], cov [T, rows, B]) with None for outputs
+        not asked for (W = 6 for ref15, 3 for ref8; cov is block-packed)."""
         if self.model not in REF_MODELS:
             raise ValueError('run_events needs a ref15 or ref8 handle')
         T = int(etype.shape[0])
@@ -319,9 +321,9 @@ class BatchedKF:
         up = torch.empty(T, self.batch, dtype=torch.uint8, device=self.device) if updated else None
         cv = self.empty(T, self.ntri, self.batch) if cov else None
         gate = threshold is not None
-        check(_lib.lib().kf_run_events(self.handle, T, _ptr(et), _ptr(dtd), _ptr(pay), _ptr(tr), _ptr(cv),
-                                       _ptr(ld), _ptr(up), int(gate), float(threshold) if gate else 0.0,
-                                       self._stream()))
+        fn = _lib.lib().kf_run_events_seq if sequential else _lib.lib().kf_run_events
+        check(fn(self.handle, T, _ptr(et), _ptr(dtd), _ptr(pay), _ptr(tr), _ptr(cv), _ptr(ld), _ptr(up), int(gate),
+                 float(threshold) if gate else 0.0, self._stream()))
         return tr, ld, up, cv
 
     def run_stream(self, etype, dt, payload, traj=True, logdet=True, updated=False, cov=False, chunk=0,

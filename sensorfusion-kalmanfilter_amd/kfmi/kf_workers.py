@@ -178,6 +178,8 @@ class Scheduler:
         """kf_workers.py:195-213: index of the first measurement with the largest gain; both sensor
         types are scored in one kernel launch."""
         assert measurements is not None, "measurements should not be None"
+        if len(measurements) == 0:
+            raise ValueError('None is not in list')  # the reference's measurements.index(None) (:213)
         for s in ('GPS', 'IMU'):
             _sensor_of(measurement_cov[s], observation_cov[s])
         g = _score(np.asarray(S_sigma)[None], ['GPS', 'IMU'], False)[0][:, 0]
@@ -186,6 +188,10 @@ class Scheduler:
             v = g[0] if m[1] == 'GPS' else g[1]
             if v > best:
                 best, best_i = v, i
+        if best_i is None:
+            # an empty queue or no gain above -inf (NaN gains): the reference's
+            # measurements.index(None) raises (kf_workers.py:213)
+            raise ValueError('None is not in list')
         return best_i
 
     def randomized_greedy_schedule(self, total_num_sensors, device='cuda'):

@@ -23,9 +23,7 @@ reference itself produces is, exactly (see csrc/kf_ref15.hip).
 """
 from __future__ import annotations
 
-import contextlib
 import math
-import os
 
 import numpy as np
 import torch
@@ -200,24 +198,6 @@ def run_kalman_filter_full(events, start_idx=None, end_idx=None, initial_pt=None
     return states, logdets, from_blocks(Pb[:, 0]), prev
 
 
-@contextlib.contextmanager
-def _stream_route(allowed):
-    """kf_run_events sends a long one-filter run through kf_run_stream by itself; with
-    allowed=False it runs the single filter (KFMI_STREAM=off for the call)."""
-    if allowed:
-        yield
-        return
-    old = os.environ.get('KFMI_STREAM')
-    os.environ['KFMI_STREAM'] = 'off'
-    try:
-        yield
-    finally:
-        if old is None:
-            del os.environ['KFMI_STREAM']
-        else:
-            os.environ['KFMI_STREAM'] = old
-
-
 def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initial_state=None, dtype='f64',
                     cov=False, parallel=True, parallel_min_events=1 << 16):
     """run_kalman_filter_full (kf_workers.py:623-728) over an EventStream window, entirely on
@@ -267,8 +247,8 @@ def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initi
     if parallel and T + 1 >= parallel_min_events:
         tr, ld, _, cv = kf.run_stream(et, dt, pay, cov=cov)
     else:
-        with _stream_route(parallel):
-            tr, ld, _, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None], cov=cov)
+        # parallel=False: the single filter even where kf_run_events would route it over time
+        tr, ld, _, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None], cov=cov, sequential=not parallel)
     x, Pb = kf.state()
     keep = et != NONE
     keep[0] = True
@@ -469,7 +449,9 @@ def unrank_combination(n, k, r):
 
 def brute_force_setup(events, start_idx=0, end_idx=None, initial_pt=None, initial_state=None):
     """The search's inputs as kf_workers.py:1262-1310 sets them up: (candidates, x0, P0,
-    prev_time, target_end, events [n, 11], init [42]), or None without a starting fix."""
+    prev_time, target_end, events [n, 11], init [42]), or None when there is no candidate: a
+    cold window without a starting fix (:1303-1305), or an empty warm-start window, where the
+    reference's size loop (:1325) never runs and it returns None (:1391-1392)."""
     if start_idx is None or start_idx < 0:
         start_idx = 0
     if end_idx is None or end_idx > len(events):
@@ -489,8 +471,8 @@ def brute_force_setup(events, start_idx=0, end_idx=None, initial_pt=None, initia
                 started, prev_time = True, t
             if started:
                 cand.append((idx, stype, t, sdata))
-        if not cand:
-            return None
+    if not cand:
+        return None
     target_end = events[end_idx - 1][2]
     n = len(cand)
     if n > 64:

@@ -53,21 +53,13 @@ def _stream(T, seed=1, gps_every=20, keep=0.7, skips=0):
 
 
 def _sequential(et, dt, pay, x0, dtype='f64', model='ref15'):
-    """The single filter (kf_run_events with the stream route off)."""
-    import os
+    """The single filter (kf_run_events_seq: never the stream route)."""
     kf = kfmi.BatchedKF(model, 1, dtype)
     npd = np.float64 if dtype == 'f64' else np.float32
     P0 = ref15.to_blocks(ref15.P0) if model == 'ref15' else kf.state()[1].double().cpu().numpy()[:, 0]
     kf.set_state(x0[:, None].astype(npd), P0[:, None].astype(npd))
-    old = os.environ.get('KFMI_STREAM')
-    os.environ['KFMI_STREAM'] = 'off'
-    try:
-        tr, ld, up, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None].astype(npd), updated=True, cov=True)
-    finally:
-        if old is None:
-            del os.environ['KFMI_STREAM']
-        else:
-            os.environ['KFMI_STREAM'] = old
+    tr, ld, up, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None].astype(npd), updated=True, cov=True,
+                                   sequential=True)
     x, P = kf.state()
     out = tuple(v.double().cpu().numpy() for v in (tr[:, :, 0], ld[:, 0], x[:, 0], P[:, 0], cv[:, :, 0], up[:, 0]))
     kf.close()
@@ -98,6 +90,10 @@ def test_parallel_equals_single_filter(T, chunk, skips, warmup, final_pass, monk
     chk = ref15.parallel_check
     assert chk['ok'] and chk['chunks'] > 1, chk
     assert chk['cov_gap'] <= 1e-12  # the warm-up reached the covariance (to roundoff)
+    if final_pass:
+        assert chk['state_gap'] <= 1e-9  # every chunk's end state meets its successor's start
+    else:
+        assert np.isnan(chk['state_gap'])  # records from the maps: no state seam is measured
     for a, b in zip(par, seq):
         assert a.shape == b.shape
         assert _rel(a, b) <= 1e-9

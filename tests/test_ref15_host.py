@@ -51,3 +51,37 @@ def test_event_payload_layout(golden_dir):
     imu = next(e for e in events if e[1] == 'IMU')
     assert ref15.event_payload('GPS', gps[3])[:3] == [gps[3]['easting'], gps[3]['northing'], gps[3]['altitude']]
     assert ref15.event_payload('IMU', imu[3]) == [float(v) for v in imu[3][1:10]]
+
+
+def test_empty_warm_window_returns_none(golden_dir):
+    """A warm start over an empty window (start_idx >= end_idx) has no candidate: the
+    reference's size loop never runs and it returns None (kf_workers.py:1325, 1391); so do the
+    single-GPU search and both sharded searches, before any device work."""
+    import socket
+
+    import torch.distributed as dist
+
+    from kfmi import dist as kdist
+    events = unpack_events(np.load(f'{golden_dir}/ref15_bruteforce.npz'))
+    st = (events[5][2], 1.0, 2.0, 3.0, 0.0, 0.0, 0.0)
+    kw = dict(R_threshold=0.0, initial_pt=ref15.P0, initial_state=st)
+    assert ref15.brute_force_setup(events, 10, 10, ref15.P0, st) is None
+    assert ref15.run_brute_force_kalman_filter_no_sampling_min_usage(events, 10, 10, **kw) is None
+    assert ref15.run_brute_force_kalman_filter_no_sampling_min_usage(events, 12, 10, **kw) is None
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1)
+    try:
+        assert kdist.brute_force_search(events, 10, 10, **kw) is None
+        assert kdist.brute_force_search_ranks(events, 10, 10, **kw) is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_greedy_schedule_empty_queue_raises():
+    """Scheduler.greedy_schedule on an empty queue: the reference ends in
+    measurements.index(None), a ValueError (kf_workers.py:213)."""
+    from kfmi.kf_workers import Scheduler
+    with pytest.raises(ValueError, match='None is not in list'):
+        Scheduler().greedy_schedule([], ref15.P0, None, None)
