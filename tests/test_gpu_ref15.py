@@ -244,6 +244,22 @@ def test_search_combos_rejects_bad_arguments():
     cv.close()
 
 
+def test_eval_combos_rejects_logdets_past_4gib():
+    """The k + 2 logdet rows share one buffer descriptor with a 32-bit range: 64 rows of 2^23
+    f64 filters (exactly 4 GiB) are refused instead of wrapping; without records the launch runs."""
+    B, n, k = 1 << 23, 64, 62
+    ev = np.zeros((n, 11))
+    ev[:, 0] = np.arange(n)
+    ev[:, 1] = ref15.IMU
+    init = np.concatenate([np.zeros(15), ref15.to_blocks(ref15.P0)])
+    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    with pytest.raises(kfmi.KFError, match='4 GiB'):
+        kf.eval_combos(ev, init, 0.0, float(n), k, logdets=True)
+    mx, _, nrec = kf.eval_combos(ev, init, 0.0, float(n), k, logdets=False)
+    assert torch.isfinite(mx[:math.comb(n, k)]).all() and int(nrec[0]) == k + 2  # P0, k events, final predict
+    kf.close()
+
+
 @pytest.mark.parametrize('n,k', [(10, 1), (10, 4), (12, 6)])
 def test_eval_combos_kernel_vs_oracle(golden_dir, n, k):
     """Every k-subset of n candidates, unranked in-kernel, against the oracle's worker: record
