@@ -528,7 +528,14 @@ constexpr int kStreamPolish = 0;
 // events per covariance map: the roundoff of a map's evaluation grows with the events it spans
 // (config 1 log: seam gap 4.8e-15 with 285-event maps, 1.5e-11 with 777-event maps)
 constexpr int64_t kStreamLftPiece = 160;
-constexpr int64_t kStreamTargetChunks = 2048;
+// default split: T / kStreamTargetChunks events per chunk, at least kStreamMinChunk.  The map
+// pass runs a chunk's four variants in one 8-lane group: 8192 chunks are 1024 waves, one per
+// SIMD, and the pass's time is its chunk length in sequence (KFMI_STREAM_CHUNKS overrides the
+// target, for sweeps)
+constexpr int64_t kStreamTargetChunks = 8192;
+constexpr int64_t kStreamMinChunk = 32;
+// piece maps (36 doubles) the start kernel stages in LDS per block: 64 KB
+constexpr int64_t kStreamStartLdsMaps = 65536 / (36 * 8);
 
 size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
 
@@ -579,7 +586,9 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     if (T == 0) return KF_OK;
     if (!etype || !dt || !payload) return fail(KF_EINVAL, "kf_run_stream: null etype/dt/payload stream");
     const hipStream_t st = static_cast<hipStream_t>(stream);
-    const int64_t L = chunk > 0 ? chunk : std::max<int64_t>(128, (int64_t(T) + kStreamTargetChunks - 1) / kStreamTargetChunks);
+    int64_t target = kStreamTargetChunks;
+    if (const char* v = std::getenv("KFMI_STREAM_CHUNKS")) target = std::max<int64_t>(2, std::atoll(v));
+    const int64_t L = chunk > 0 ? chunk : std::max<int64_t>(kStreamMinChunk, (int64_t(T) + target - 1) / target);
     const int64_t C = (int64_t(T) + L - 1) / L;
     // warmup >= 0: W events of warm-up before each chunk from the handle's covariance;
     // -1: linear-fractional covariance maps + kStreamPolish chunks of warm-up; -2 - k: maps + k chunks
@@ -602,10 +611,8 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     // workspace: check | banks W (C), M (4C), F (C) | maps | starts
     const size_t bank1 = align256(size_t(n + nblk) * C * w) + align256(sizeof(int32_t) * C);
     const size_t bank4 = align256(size_t(n + nblk) * 4 * C * w) + align256(sizeof(int32_t) * 4 * C);
-    const int64_t nseg = (C + kfmi::kStreamSegChunks - 1) / kfmi::kStreamSegChunks;
     const int np = int((L + kStreamLftPiece - 1) / kStreamLftPiece);
-    const size_t lft_bytes =
-        lft ? align256(sizeof(double) * 36 * nch * C * np) + 2 * align256(sizeof(double) * 9 * nch * C) : 0;
+    const size_t lft_bytes = lft ? align256(sizeof(double) * 36 * nch * C * np) : 0;
     // records straight from the map pass (no final pass) unless the four variants' trajectory
     // rows exceed the 32-bit offsets or KFMI_STREAM_FINAL=1 asks for the final pass
     const int ntraj = h->model == KF_MODEL_REF15 ? 6 : 3;
@@ -613,8 +620,9 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     const char* fv = std::getenv("KFMI_STREAM_FINAL");
     const bool map_records = !(fv && !std::strcmp(fv, "1")) && uint64_t(4 * vstride) * ntraj * w < (uint64_t(1) << 31);
     const size_t rec_bytes = map_records ? align256(size_t(4 * vstride) * ntraj * w) + align256(sizeof(double) * n) : 0;
-    const size_t need = 256 + 2 * bank1 + bank4 + align256(sizeof(double) * 12 * nch * C) +
-                        align256(sizeof(double) * 15 * nch * nseg) + align256(sizeof(double) * n * C) + lft_bytes +
+    const int64_t ntiles = (C + kfmi::kStreamScanTile - 1) / kfmi::kStreamScanTile;
+    const size_t need = 256 + 2 * bank1 + bank4 + 2 * align256(sizeof(double) * 12 * nch * C) +
+                        align256(sizeof(double) * 15 * nch * ntiles) + align256(sizeof(double) * n * C) + lft_bytes +
                         rec_bytes;
     if (h->stream_ws_bytes < need) {
         if (h->stream_ws) (void)hipFree(h->stream_ws);
@@ -649,19 +657,16 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     bank(C, sa.fx, sa.fP, sa.fst);
     sa.maps = reinterpret_cast<double*>(p);
     p += align256(sizeof(double) * 12 * nch * C);
-    sa.segmaps = reinterpret_cast<double*>(p);
-    sa.segstart = sa.segmaps + 12 * nch * nseg;
-    p += align256(sizeof(double) * 15 * nch * nseg);
+    sa.pref = reinterpret_cast<double*>(p);
+    p += align256(sizeof(double) * 12 * nch * C);
+    sa.tiles = reinterpret_cast<double*>(p);
+    sa.tstart = sa.tiles + 12 * nch * ntiles;
+    p += align256(sizeof(double) * 15 * nch * ntiles);
     sa.starts = reinterpret_cast<double*>(p);
     p += align256(sizeof(double) * n * C);
-    double* pbuf[2] = {nullptr, nullptr};
     if (lft) {
         sa.phi = reinterpret_cast<double*>(p);
         p += align256(sizeof(double) * 36 * nch * C * np);
-        pbuf[0] = reinterpret_cast<double*>(p);
-        p += align256(sizeof(double) * 9 * nch * C);
-        pbuf[1] = reinterpret_cast<double*>(p);
-        p += align256(sizeof(double) * 9 * nch * C);
     }
     void* traj4 = nullptr;
     if (map_records) {
@@ -681,8 +686,9 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     sa.lp = (L + np - 1) / np;
 
     const bool f64 = h->dtype == KF_F64;
+    // nv = 4: the map pass, B = C filters of four state variants each (banks of 4C columns)
     auto chain = [&](int64_t B, void* x, void* P, int32_t* status, int64_t Tc, int64_t shift, bool records,
-                     void* traj_rec = nullptr, int nvar = 1) {
+                     void* traj_rec = nullptr, int nvar = 1, int nv = 1) {
         kfmi::RefArgs a{};
         a.B = B;
         a.T = int(Tc);
@@ -704,36 +710,47 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
         a.s_chunk = L;
         a.s_shift = shift;
         a.s_nchunks = C;
-        return kfmi::launch_ref_stream(h->model, f64, a, st);
-    };
-    hipError_t e = kfmi::launch_stream_phase(h->model, f64, 0, sa, st);
-    if (lft) {
-        // enough iterations for the maps to cover kStreamLftEvents events of forgetting
-        const int iters = int((kStreamLftEvents + L - 1) / L) + 1;
-        if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseLftMaps, sa, st);
-        for (int it = 0; it < iters && e == hipSuccess; ++it) {
-            kfmi::StreamArgs si = sa;
-            si.pcur = it == 0 ? nullptr : pbuf[it & 1];
-            si.pnext = pbuf[(it + 1) & 1];
-            si.last = it + 1 == iters;
-            e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseLftIter, si, st);
+        if (nv == 4) {  // the map pass: its epilogue writes the chunk maps and checks the seams
+            a.s_maps = sa.maps;
+            a.s_delta = sa.delta;
+            a.s_wnext = sa.wP;
+            a.s_check = sa.check;
         }
+        return kfmi::launch_ref_stream(h->model, f64, a, st, nv);
+    };
+    hipError_t e = hipSuccess;
+    if (lft) {
+        // every chunk start from at least `iters` chunks of maps: kStreamLftEvents events of
+        // forgetting; one start thread walks iters + G chunks
+        sa.iters = int((kStreamLftEvents + L - 1) / L) + 1;
+        // chunks per block of the start kernel: its window's piece maps, (G + iters) * np of
+        // them, must fit 64 KB of LDS (0: read them from global memory)
+        const int64_t fit = kStreamStartLdsMaps / np - sa.iters;
+        sa.G = fit >= 16 ? std::min<int64_t>(fit, 256) : 0;
+        e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseLftMaps, sa, st);
+        // the start kernel also zeroes the check and fills the warm-up bank (and, without event
+        // warm-up, the map bank)
+        if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseLftStart, sa, st);
+    } else {
+        e = kfmi::launch_stream_phase(h->model, f64, 0, sa, st);
     }
     if (e == hipSuccess && W > 0) e = chain(C, sa.wx, sa.wP, sa.wst, W, -W, false);
-    if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, 1, sa, st);
+    if (e == hipSuccess && (!lft || W > 0)) e = kfmi::launch_stream_phase(h->model, f64, 1, sa, st);
     if (map_records) {
         // the map pass writes the records (variant 0's covariance, logdet, updated flags, and
         // every variant's trajectory); the trajectories are then the affine maps' values at the
         // true chunk starts
-        if (e == hipSuccess) e = chain(4 * C, sa.mx, sa.mP, sa.mst, L, 0, true, traj ? traj4 : nullptr, 4);
-        for (int ph = 2; ph <= 4 && e == hipSuccess; ++ph) e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
+        if (e == hipSuccess) e = chain(C, sa.mx, sa.mP, sa.mst, L, 0, true, traj ? traj4 : nullptr, 4, 4);
+        // the maps composed into the chunk starts, and the verdict
+        for (int ph = kfmi::kStreamPhaseScanTiles; ph <= kfmi::kStreamPhaseStarts && e == hipSuccess; ++ph)
+            e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
         if (e == hipSuccess && traj) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseRecords, sa, st);
-        if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseFinishMaps, sa, st);
     } else {
-        if (e == hipSuccess) e = chain(4 * C, sa.mx, sa.mP, sa.mst, L, 0, false);
-        for (int ph = 2; ph <= 4 && e == hipSuccess; ++ph) e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
+        if (e == hipSuccess) e = chain(C, sa.mx, sa.mP, sa.mst, L, 0, false, nullptr, 1, 4);
+        for (int ph = kfmi::kStreamPhaseScanTiles; ph <= kfmi::kStreamPhaseStarts && e == hipSuccess; ++ph)
+            e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
         if (e == hipSuccess) e = chain(C, sa.fx, sa.fP, sa.fst, L, 0, true);
-        if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, 5, sa, st);
+        if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseFinish, sa, st);
     }
     if (e != hipSuccess) return hip_fail(e, "kf_run_stream");
     // the sequential run, which does nothing unless a check failed
@@ -751,7 +768,7 @@ int kf_stream_check(kf_batch* h, double* out, void* stream) {
         if (e != hipSuccess) return hip_fail(e, "kf_stream_check");
     }
     out[0] = k.ok;
-    out[1] = k.bad ? 1.0 : 0.0;
+    out[1] = (k.bad & ~kfmi::kStreamBadStart) ? 1.0 : 0.0;
     out[2] = k.cov_gap;
     out[3] = k.state_gap;
     out[4] = double(h->s_chunks);

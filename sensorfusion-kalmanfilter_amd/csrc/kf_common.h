@@ -168,9 +168,12 @@ __device__ __forceinline__ T logdet_ldl(const T (&P)[N * (N + 1) / 2]) {
 // block and general constant-velocity kernels stay bit-identical).
 // POISON = false: a non-positive pivot is only reported (return value), for callers that
 // replace the whole filter with NaN themselves (saves a select per reciprocal).
-template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2, bool POISON = true>
-__device__ __forceinline__ bool sel_update(T (&x)[N], T (&P)[N * (N + 1) / 2], const T (&z)[M],
-                                           const T (&R)[M * (M + 1) / 2]) {
+// NV > 1: NV state vectors share the covariance (filters that differ only in their state, as
+// kf_run_stream's map variants do): S, K and P+ are computed once, every x_v[v] is updated with
+// the same K, each term in the same order as the single-state update.
+template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2, bool POISON = true, int NV = 1>
+__device__ __forceinline__ bool sel_update_nv(T (&xv)[NV][N], T (&P)[N * (N + 1) / 2], const T (&zv)[NV][M],
+                                              const T (&R)[M * (M + 1) / 2]) {
     constexpr int MT = M * (M + 1) / 2;
     // S = H P H^T + R, then its LDL^T
     T S[MT];
@@ -224,15 +227,18 @@ __device__ __forceinline__ bool sel_update(T (&x)[N], T (&P)[N * (N + 1) / 2], c
         }
     }
     // x += K (z - H x)
-    T y[M];
 #pragma unroll
-    for (int a = 0; a < M; ++a) y[a] = z[a] - x[a];
+    for (int v = 0; v < NV; ++v) {
+        T y[M];
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-        T s = x[i];
+        for (int a = 0; a < M; ++a) y[a] = zv[v][a] - xv[v][a];
 #pragma unroll
-        for (int a = 0; a < M; ++a) s = fmaT(K[i][a], y[a], s);
-        x[i] = s;
+        for (int i = 0; i < N; ++i) {
+            T s = xv[v][i];
+#pragma unroll
+            for (int a = 0; a < M; ++a) s = fmaT(K[i][a], y[a], s);
+            xv[v][i] = s;
+        }
     }
     // Joseph: P+ = (I-KH) P (I-KH)^T + K R K^T = (P - K G^T) + E K^T with G = P H^T and
     // E = K S - G, an identity for ANY K (E is the residual of the gain equation K S = G,
@@ -268,6 +274,20 @@ __device__ __forceinline__ bool sel_update(T (&x)[N], T (&P)[N * (N + 1) / 2], c
     for (int i = 0; i < M; ++i)
 #pragma unroll
         for (int j = i; j < N; ++j) P[tri<N>(i, j)] = top[i][j];
+    return ok;
+}
+
+template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2, bool POISON = true>
+__device__ __forceinline__ bool sel_update(T (&x)[N], T (&P)[N * (N + 1) / 2], const T (&z)[M],
+                                           const T (&R)[M * (M + 1) / 2]) {
+    T xv[1][N], zv[1][M];
+#pragma unroll
+    for (int i = 0; i < N; ++i) xv[0][i] = x[i];
+#pragma unroll
+    for (int a = 0; a < M; ++a) zv[0][a] = z[a];
+    const bool ok = sel_update_nv<N, M, DIAG_R, T, NEWTON, POISON, 1>(xv, P, zv, R);
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = xv[0][i];
     return ok;
 }
 

@@ -43,6 +43,8 @@ struct SynthArgs {
     void* z;                 // [U][m][B]
 };
 
+struct StreamCheck;
+
 // Reference chain models on per-filter event streams: KF_MODEL_REF15 (kf_workers.py:493-614,
 // N = 15, NBLK = 27, NTRAJ = 6) and KF_MODEL_REF8 (hw5_2.py:219-311, N = 8, NBLK = 15, NTRAJ = 3).
 // Event codes in etype: 0 GPS fix, 1 IMU sample, 2 predict only, 255 no event (padding).
@@ -74,6 +76,14 @@ struct RefArgs {
     int s_nvar;              // > 1: trajectory records per variant (filter / s_nchunks), s_vstride rows apart
     int64_t s_vstride;
     const int32_t* skip;     // if non-null and *skip != 0, the launch does nothing
+    // the map pass of kf_run_stream (4 state variants per filter): its epilogue writes each
+    // chunk's affine state map per chain, [C][chains][12] = A (3x3 row-major), b, from the
+    // variants' end states (their starts differ by s_delta on one chain component), and checks
+    // the covariance seam against the next chunk's start covariance s_wnext ([NBLK][C])
+    double* s_maps;
+    double s_delta;
+    const void* s_wnext;
+    StreamCheck* s_check;
 };
 
 // Time-parallel run of one filter over a long event stream (kf_run_stream): the state banks of
@@ -83,6 +93,8 @@ struct StreamCheck {
     int32_t bad;             // a chunk filter failed (non-SPD)
     double cov_gap;          // max over chunk seams of the warm-up covariance's relative gap
     double state_gap;        // max over chunk seams of |end state - next start| / max(|start|, 1)
+    int32_t done;            // chain blocks of the scan phase that have finished (the last decides)
+    int32_t pad;
 };
 struct StreamArgs {
     int64_t C;               // chunks
@@ -101,8 +113,9 @@ struct StreamArgs {
     void* fP;
     int32_t* fst;
     double* maps;            // [C][chains][12]: per chunk and chain, A (3x3) and b of x_end = A x_start + b
-    double* segmaps;         // [C / kStreamSeg][chains][12]: the product of a segment's chunk maps
-    double* segstart;        // [C / kStreamSeg][chains][3]: each segment's start
+    double* pref;            // [C][chains][12]: the product of the chunk maps before c in c's tile
+    double* tiles;           // [C / kScanTile][chains][12]: each tile's product
+    double* tstart;          // [C / kScanTile][chains][3]: each tile's start
     double* starts;          // [N][C] the chunk starts (fp64)
     StreamCheck* check;
     // covariance start by linear-fractional maps (kf_run_stream's default warm-up)
@@ -113,9 +126,8 @@ struct StreamArgs {
     int np;                  // pieces per chunk (of lp events) with a covariance map each
     int64_t lp;
     double* phi;             // [C][np][chains][36]: per piece and chain, the 6x6 covariance map [[A B] [C D]]
-    double* pcur;            // [C][chains][9]: chunk start covariances of the current iteration
-    double* pnext;           // [C][chains][9]
-    int last;                // this is the last iteration: write the warm-up bank's P
+    int iters;               // chunk maps (at least) behind every chunk start
+    int64_t G;               // chunks per block of the start kernel (their maps staged in LDS); 0: no LDS
     // records from the map pass (no final pass): the map bank's trajectories per variant
     const void* traj4;       // [4][vstride][NTRAJ]
     int64_t vstride;
@@ -123,16 +135,20 @@ struct StreamArgs {
     double* xend;            // [N] the last chunk's end state (fp64)
 };
 // phase 0: warm-up bank from the handle, check zeroed; 1: map bank from the warm-up bank;
-// 2: chunk maps, segment products, covariance seam check; 3: segment starts; 4: chunk starts
-// into the final bank; 5: state seam check, verdict, and (if it passed) the handle's final state
-constexpr int kStreamSegChunks = 64;  // chunks per segment (kStreamSeg in kf_ref.hip)
+// 2-4: the chunk maps (written by the map pass) composed into every chunk start by a parallel
+// scan (tiles, tile starts, chunk starts; then the final bank's starts, or with records from
+// the map pass the verdict); 5: state seam check, verdict, and (if it passed) the handle's
+// final state after a final pass
 hipError_t launch_stream_phase(int model, bool f64, int phase, const StreamArgs& a, hipStream_t stream);
 // the linear-fractional covariance warm-up: phase 6 = every chunk's covariance map, phase 7 =
-// one iteration P(c) <- map_(c-1)(P(c-1)) over all chunks (pcur -> pnext)
-constexpr int kStreamPhaseLftMaps = 6, kStreamPhaseLftIter = 7;
-// records from the map pass: phase 8 = trajectories from the variants and the chunk starts;
-// phase 9 = the verdict without a final pass (failed filters, non-finite starts, covariance seams)
-constexpr int kStreamPhaseRecords = 8, kStreamPhaseFinishMaps = 9;
+// every chunk's start covariance from the maps (and the warm-up / map banks, the zeroed check)
+constexpr int kStreamPhaseLftMaps = 6, kStreamPhaseLftStart = 7;
+// check->bad bits: a chunk filter failed / a chunk start or the end state is not finite
+constexpr int kStreamBadFilter = 1, kStreamBadStart = 2;
+// records from the map pass: phase 8 = trajectories from the variants and the chunk starts
+constexpr int kStreamPhaseScanTiles = 2, kStreamPhaseScanTop = 3, kStreamPhaseStarts = 4, kStreamPhaseFinish = 5,
+              kStreamPhaseRecords = 8;
+constexpr int64_t kStreamScanTile = 256;  // chunks per scan tile (kScanTile in kf_ref.hip)
 
 // Brute-force search over k-subsets of n candidate events (kf_workers.py:22-97, 1218-1392):
 // lane f evaluates combination number combo_offset + f in itertools.combinations order.
@@ -238,8 +254,9 @@ hipError_t launch_synth(int axes, bool f64, const SynthArgs& a, hipStream_t stre
 // per axis chain (few filters), one lane per filter with inputs staged through LDS by DMA
 constexpr int kEventsLane = 0, kEventsChain = 1, kEventsLds = 2;
 hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, int variant);
-// the chain kernel in stream mode (a.s_len > 0)
-hipError_t launch_ref_stream(int model, bool f64, const RefArgs& a, hipStream_t stream);
+// the chain kernel in stream mode (a.s_len > 0); nv = 4: the map pass, four state variants per
+// filter sharing its covariance (state bank of 4 B columns)
+hipError_t launch_ref_stream(int model, bool f64, const RefArgs& a, hipStream_t stream, int nv = 1);
 hipError_t launch_ref_reset(int model, bool f64, const RefArgs& a, hipStream_t stream);
 hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream);
 // child_major: one wave per (parent block, child event) instead of one lane per parent

@@ -480,6 +480,11 @@ constexpr int kChainDepth = KF_CHAIN_DEPTH;  // input ring of ref_chain_kernel
 #define KF_STREAM_DEPTH 8
 #endif
 constexpr int kStreamDepth = KF_STREAM_DEPTH;  // its input ring in stream mode (kf_run_stream)
+#ifndef KF_STREAM_VAR_DEPTH
+#define KF_STREAM_VAR_DEPTH 4
+#endif
+// the map pass's ring (4 state variants per lane): shallower, so the lane fits 2 waves per SIMD
+constexpr int kStreamVarDepth = KF_STREAM_VAR_DEPTH;
 
 // Sums / ORs over the 8-lane group with DPP (a VALU-latency lane exchange, no LDS round trip):
 // quad_perm [1,0,3,2] (xor 1), quad_perm [2,3,0,1] (xor 2), then row_half_mirror (lane i <-> 7-i
@@ -528,6 +533,12 @@ __device__ __forceinline__ T chain_log_det(const T (&P)[6]) {
     return ok ? ld : quiet_nan<T>();
 }
 
+// non-negative doubles (and +NaN) order as their bit patterns: atomic max via uint64
+__device__ __forceinline__ void atomic_max_pos(double* p, double v) {
+    if (!(v >= 0.0)) v = __builtin_nan("");
+    atomicMax(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v));
+}
+
 // Inputs of one event for one lane.
 template <typename T>
 struct ChainIn {
@@ -536,8 +547,16 @@ struct ChainIn {
     T va, vb;
 };
 
-template <typename T, class M, bool STREAM>
+// NV > 1 (stream mode only): NV variants of each filter that differ only in their start state
+// (kf_run_stream's map pass: a chunk from its guess and from the guess + delta on each chain
+// component) share one lane.  The covariance recursion does not read the state, so P, S and K
+// are computed once per event and every variant's state is updated with them (sel_update_nv);
+// each variant's arithmetic is the single-state lane's, term for term.  Variant v's state is
+// column v * B + f of a state bank of NV * B columns (the covariance: column f), and its
+// trajectory records go to rows v * s_vstride.
+template <typename T, class M, bool STREAM, int NV = 1>
 __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
+    static_assert(NV == 1 || STREAM, "state variants are a stream-mode feature");
     if (a.skip && *a.skip) return;  // the sequential fallback of a stream run that passed its checks
     const int64_t g = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     const int64_t f = g / kGroup;
@@ -548,6 +567,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     const int ca = pva ? c : (live ? c - M::NP : 0);
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
+    const uint32_t rbank = uint32_t(NV) * rb;  // row stride of the state / covariance bank
     const uint32_t rb8 = uint32_t(a.B) * 8u;
     const uint32_t off8 = uint32_t(f) * 8u;
     // this lane's state indices and block rows (-1: none), as voffsets into row spans
@@ -561,9 +581,9 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     }
     uint32_t vx[3], vp[6];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) vx[k] = xi[k] >= 0 ? uint32_t(xi[k]) * rb + off : kDropOffset;
+    for (int k = 0; k < 3; ++k) vx[k] = xi[k] >= 0 ? uint32_t(xi[k]) * rbank + off : kDropOffset;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) vp[k] = pr[k] >= 0 ? uint32_t(pr[k]) * rb + off : kDropOffset;
+    for (int k = 0; k < 6; ++k) vp[k] = pr[k] >= 0 ? uint32_t(pr[k]) * rbank + off : kDropOffset;
     const uint32_t v_tr = (xi[0] >= 0 && xi[0] < M::NTRAJ) ? uint32_t(xi[0]) * rb + off : kDropOffset;
     const uint32_t v_ld = c == 0 ? off : kDropOffset;
     const int ia = pva ? ca : M::imu_att(ca);              // GPS position / IMU attitude column
@@ -572,14 +592,19 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     const T q[3] = {T(pva ? kQPos : kQAtt), T(pva ? kQVel : kQRate), T(pva ? kQAcc : 0.0)};
     const T Rimu[6] = {T(pva ? kRPos : kRAtt), T(0), T(0), T(pva ? kRVel : kRRate), T(0), T(pva ? kRAcc : 1.0)};
 
-    T x[3], P[6];
+    T x[NV][3], P[6];
     {
-        const auto rx = span_rsrc(a.x, 0, rb, M::N), rp = span_rsrc(a.P, 0, rb, M::NBLK);
+        const auto rx = span_rsrc(a.x, 0, rbank, M::N), rp = span_rsrc(a.P, 0, rbank, M::NBLK);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) x[k] = ldv(rx, vx[k], T(0));
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) x[v][k] = ldv(rx, vx[k] == kDropOffset ? kDropOffset : vx[k] + uint32_t(v) * rb, T(0));
 #pragma unroll
         for (int k = 0; k < 6; ++k) P[k] = pr[k] >= 0 ? ldv(rp, vp[k], T(0)) : T(k == 0 || k == 3 || k == 5 ? 1 : 0);
     }
+    T xs0[3];  // variant 0's start (the map pass's guess)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) xs0[k] = x[0][k];
     int32_t st = a.status[f];
     const bool need_ld = a.logdet != nullptr;
 
@@ -589,9 +614,10 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     const uint32_t S = STREAM ? uint32_t(a.s_len) : 0u;
     const auto r_et = bytes_rsrc(a.etype, S), r_dt = bytes_rsrc(a.dt, S * 8u);
     const auto r_pay = bytes_rsrc(a.payload, S * 9u * uint32_t(sizeof(T)));
-    // filter f is variant f / s_nchunks of its chunk: with s_nvar > 1, variant q's trajectory
-    // records go to rows [q * s_vstride, q * s_vstride + S) (s_vstride >= S + chunk, so a padded
-    // chunk's rows past S stay inside its own variant), and only variant 0 writes the others
+    // filter f is variant f / s_nchunks of its chunk (NV = 1) or carries variants 0 .. NV - 1:
+    // with s_nvar > 1, variant q's trajectory records go to rows [q * s_vstride, q * s_vstride +
+    // S) (s_vstride >= S + chunk, so a padded chunk's rows past S stay inside its own variant),
+    // and only variant 0 writes the others
     const int var = STREAM ? int(f / a.s_nchunks) : 0;
     const uint32_t trows = STREAM ? (a.s_nvar > 1 ? uint32_t(a.s_nvar) * uint32_t(a.s_vstride) : S) : 0u;
     const auto r_str = bytes_rsrc(a.traj, trows * uint32_t(M::NTRAJ * sizeof(T)));
@@ -607,6 +633,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     const uint32_t col_tr = v_tr != kDropOffset ? (uint32_t(var) * uint32_t(a.s_vstride) * M::NTRAJ + uint32_t(xi[0])) *
                                                       uint32_t(sizeof(T))
                                                 : 0u;
+    const uint32_t vstep_tr = uint32_t(a.s_vstride) * uint32_t(M::NTRAJ * sizeof(T));  // next variant's rows
     const uint32_t m_ld = c == 0 && var == 0 ? 0u : kDropOffset;
     uint32_t col_cv[6];
 #pragma unroll
@@ -637,8 +664,13 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
             // predict: F = [[1, dt, c02], [0, 1, c12], [0, 0, 1]] (c02 = c12 = 0 on an aw lane)
             const T c02 = pva ? T(0.5) * dt * dt : T(0);
             const T c12 = pva ? dt : T(0);
-            const T xn0 = fmaT(c02, x[2], fmaT(dt, x[1], x[0]));
-            const T xn1 = fmaT(c12, x[2], x[1]);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const T xn0 = fmaT(c02, x[v][2], fmaT(dt, x[v][1], x[v][0]));
+                const T xn1 = fmaT(c12, x[v][2], x[v][1]);
+                x[v][0] = xn0;
+                x[v][1] = xn1;
+            }
             T FP[3][3];
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
@@ -655,25 +687,32 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
                     if (j == 1) s = fmaT(FP[i][2], c12, s);
                     P[tri<3>(i, j)] = (i == j) ? s + q[i] * dt : s;
                 }
-            x[0] = xn0;
-            x[1] = xn1;
             applied = (type == kGps || type == kImu);
             if (a.gate && applied) applied = group_sum(live ? chain_log_det(P) : T(0)) > T(a.threshold);
             bool ok = true;
             if (applied) {
                 if (type == kGps) {
                     if (pva) {
-                        const T zb[1] = {va};
+                        T zb[NV][1];
+#pragma unroll
+                        for (int v = 0; v < NV; ++v) zb[v][0] = va;
                         const T R[1] = {T(kRGps)};
-                        ok = sel_update<3, 1, true, T, kRefNewton>(x, P, zb, R);
+                        ok = sel_update_nv<3, 1, true, T, kRefNewton, true, NV>(x, P, zb, R);
                     }
                 } else {
-                    const T V = fmaT(vb, dt, x[1]);
-                    const T X = fmaT(V, dt, x[0]);
-                    const T zb[3] = {pva ? X : va, pva ? V : vb, pva ? vb : T(0)};
-                    ok = sel_update<3, 3, true, T, kRefNewton>(x, P, zb, Rimu);
+                    T zb[NV][3];
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        const T V = fmaT(vb, dt, x[v][1]);
+                        const T X = fmaT(V, dt, x[v][0]);
+                        zb[v][0] = pva ? X : va;
+                        zb[v][1] = pva ? V : vb;
+                        zb[v][2] = pva ? vb : T(0);
+                    }
+                    ok = sel_update_nv<3, 3, true, T, kRefNewton, true, NV>(x, P, zb, Rimu);
                     if (!pva) {  // reset the inert state
-                        x[2] = T(0);
+#pragma unroll
+                        for (int v = 0; v < NV; ++v) x[v][2] = T(0);
                         P[5] = T(1);
                     }
                 }
@@ -681,14 +720,18 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
             if (group_any(!ok)) {
                 st = kNotSpd;
 #pragma unroll
-                for (int k = 0; k < 3; ++k) x[k] = quiet_nan<T>();
+                for (int v = 0; v < NV; ++v)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) x[v][k] = quiet_nan<T>();
 #pragma unroll
                 for (int k = 0; k < 6; ++k) P[k] = quiet_nan<T>();
             }
         }
         if constexpr (STREAM) {
             const uint32_t ue = uint32_t(e0 + t);
-            stv(r_str, (ue * uint32_t(M::NTRAJ * sizeof(T)) + col_tr) | m_tr, x[0]);
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                stv(r_str, (ue * uint32_t(M::NTRAJ * sizeof(T)) + col_tr + uint32_t(v) * vstep_tr) | m_tr, x[v][0]);
 #pragma unroll
             for (int k = 0; k < 6; ++k) stv(r_scv, (ue * uint32_t(M::NBLK * sizeof(T)) + col_cv[k]) | (col_cv[k] & kDropOffset), P[k]);
             if (need_ld) {
@@ -698,7 +741,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
             }
             __builtin_amdgcn_raw_buffer_store_b8(applied ? uint8_t(1) : uint8_t(0), r_sup, ue | m_ld, 0, 0);
         } else {
-            stv(span_rsrc(a.traj, int64_t(t) * M::NTRAJ, rb, M::NTRAJ), v_tr, x[0]);
+            stv(span_rsrc(a.traj, int64_t(t) * M::NTRAJ, rb, M::NTRAJ), v_tr, x[0][0]);
             {
                 const auto rc = span_rsrc(a.cov, int64_t(t) * M::NBLK, rb, M::NBLK);
 #pragma unroll
@@ -722,7 +765,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     // (48 KB of code at 8), so the default stays at 2.
     // stream mode gathers each filter's events from its own part of the stream (a cache line
     // per 1.8 events, lines differ per filter), so its loads see HBM latency: a deeper ring
-    constexpr int D = STREAM ? kStreamDepth : kChainDepth;
+    constexpr int D = STREAM ? (NV > 1 ? kStreamVarDepth : kStreamDepth) : kChainDepth;
     const int T_ = a.T;
     auto load_c = [&](int t, ChainIn<T>& in) { load(t < T_ ? t : T_ - 1, in); };
     if (T_ > 0) {
@@ -743,13 +786,69 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
             if (t + j < T_) step(t + j, buf[j]);
     }
     {
-        const auto rx = span_rsrc(a.x, 0, rb, M::N), rp = span_rsrc(a.P, 0, rb, M::NBLK);
+        const auto rx = span_rsrc(a.x, 0, rbank, M::N), rp = span_rsrc(a.P, 0, rbank, M::NBLK);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) stv(rx, vx[k], x[k]);
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) stv(rx, vx[k] == kDropOffset ? kDropOffset : vx[k] + uint32_t(v) * rb, x[v][k]);
 #pragma unroll
         for (int k = 0; k < 6; ++k) stv(rp, vp[k], P[k]);
     }
     if (c == 0) a.status[f] = st;
+    if constexpr (NV == 4) {
+        // the map pass's epilogue (kf_run_stream): this chunk's affine map per chain, x_end =
+        // A x_start + b (fp64), A by differences of the variants (variant q + 1 started at the
+        // guess + delta on component q), b = x_end(guess) - A guess; then the covariance seam:
+        // this chunk's end covariance against the next chunk's start covariance, relative to
+        // the end covariance's largest entry in the chain (one atomic per wave)
+        constexpr int NCH = M::NP + M::NA;
+        const int ns = pva ? 3 : 2;
+        double crel = 0.0;
+        if (live && a.s_maps) {
+            double A[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, b[3] = {0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                if (k >= ns) continue;
+                const double e0v = double(x[0][k]);
+                double sacc = e0v;
+#pragma unroll
+                for (int qq = 0; qq < 3; ++qq) {
+                    if (qq >= ns) continue;
+                    A[k][qq] = (double(x[qq + 1][k]) - e0v) / a.s_delta;
+                    sacc = __builtin_fma(-A[k][qq], double(xs0[qq]), sacc);
+                }
+                b[k] = sacc;
+            }
+            double* mo = a.s_maps + (f * NCH + c) * 12;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+#pragma unroll
+                for (int qq = 0; qq < 3; ++qq) mo[k * 3 + qq] = A[k][qq];
+                mo[9 + k] = b[k];
+            }
+            if (f + 1 < a.B) {
+                const T* wn = static_cast<const T*>(a.s_wnext);
+                double scale = 0.0, gap = 0.0;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    if (pr[k] < 0) continue;
+                    const double pe = double(P[k]);
+                    scale = fmax(scale, fabs(pe));
+                    gap = fmax(gap, fabs(pe - double(wn[int64_t(pr[k]) * a.B + f + 1])));
+                }
+                const double rel = gap / fmax(scale, 1e-300);
+                crel = rel == rel ? rel : __builtin_inf();
+            }
+        }
+        if (a.s_check) {
+            // the group's max (DPP; the whole group is live), one atomic per chunk
+            crel = fmax(crel, dpp_d<kDppXor1>(crel));
+            crel = fmax(crel, dpp_d<kDppXor2>(crel));
+            crel = fmax(crel, dpp_d<kDppHalfMirror>(crel));
+            if (c == 0 && crel != 0.0) atomic_max_pos(&a.s_check->cov_gap, crel);
+            if (c == 0 && st != 0) atomicOr(&a.s_check->bad, kStreamBadFilter);
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -771,8 +870,6 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
 //    handle take the last chunk's end state; otherwise the sequential chain kernel, launched
 //    after these with skip = &check.ok, runs the stream as one filter and rewrites every record.
 // ------------------------------------------------------------------------------------
-constexpr int kStreamSeg = kStreamSegChunks;  // chunks per segment of the map composition
-
 template <class M>
 __device__ __forceinline__ int chain_state(int a, int q) {  // chain a (pva chains first), component q; -1: none
     return a < M::NP ? M::pva(a, q) : (q < 2 ? M::aw(a - M::NP, q) : -1);
@@ -790,11 +887,6 @@ __device__ __forceinline__ int state_component(int i) {  // component of state i
         for (int q = 0; q < 3; ++q)
             if (chain_state<M>(a, q) == i) comp = q;
     return comp;
-}
-// non-negative doubles (and +NaN) order as their bit patterns: atomic max via uint64
-__device__ __forceinline__ void atomic_max_pos(double* p, double v) {
-    if (!(v >= 0.0)) v = __builtin_nan("");
-    atomicMax(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v));
 }
 
 // phase 0: every chunk of the warm-up bank starts from the handle's state; check zeroed
@@ -836,11 +928,6 @@ __global__ __launch_bounds__(kBlock) void stream_perturb_kernel(const StreamArgs
     a.mst[f] = a.wst[c];
 }
 
-// phase 2 (blocks of kStreamSeg chunks x NCH chains): per (chunk, chain) the affine map
-// x_end = A x_start + b (fp64; maps[c][a][0:9] = A row-major, [9:12] = b), the covariance
-// seam (the chunk's warm-up covariance against its predecessor's end covariance, relative to
-// the predecessor's largest entry in the chain), and per block and chain the product of its
-// chunk maps in order (segmaps[block][a]), composed in LDS by one thread per chain
 template <class M>
 __device__ __forceinline__ void compose_into(double (&A)[3][3], double (&b)[3], const double* m) {
     // (A, b) <- m o (A, b): A = Am A, b = Am b + bm
@@ -879,169 +966,210 @@ __device__ __forceinline__ void apply_map(double (&x)[3], const double* m) {
     for (int k = 0; k < 3; ++k) x[k] = xn[k];
 }
 
-template <typename T, class M>
-__global__ __launch_bounds__(1024) void stream_maps_kernel(const StreamArgs a) {
-    constexpr int NCH = M::NP + M::NA;
-    __shared__ double lm[NCH][kStreamSeg][12];
-    __shared__ double red[NCH * kStreamSeg];
-    const int tid = int(threadIdx.x);
-    const int ch = tid / kStreamSeg, j = tid % kStreamSeg;
-    const int64_t c = int64_t(blockIdx.x) * kStreamSeg + j;
-    const int64_t B = 4 * a.C;
-    double crel = 0.0;
-    const T* mx = static_cast<const T*>(a.mx);
-    const T* wx = static_cast<const T*>(a.wx);
-    const int ns = ch < M::NP ? 3 : 2;
-    double A[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, b[3] = {};  // past the last chunk: identity
-    if (c < a.C) {
-        double gs[3] = {};
+// phases 2-4: the chunk maps (written by the map pass's epilogue) composed into every chunk's
+// true start, as a three-kernel parallel scan per chain (a dependent walk over the maps waits
+// ~1 us per map load):
+//   2  tiles of kScanTile chunks: thread c loads chunk c's map, a Kogge-Stone scan in LDS gives
+//      its exclusive in-tile prefix E_c (stored) and the tile's product (stored);
+//   3  one block per chain: the same scan over the tile products (rounds of kScanTile tiles with a
+//      carry) applied to the handle's state gives every tile's start, and the stream's end state;
+//   4  thread per (chunk, chain): start = E_c(tile start), stored (before a final pass also the
+//      final bank's state, covariance and status) and checked finite.  The last block to finish
+//      (a counter; release / acquire fences) gives the verdict when the records come from the map
+//      pass (a.xend): no failed chunk filter, finite starts and end state, covariance seams within
+//      tolerance; a passed run leaves the end state and the last chunk's end covariance in the
+//      handle.  No state seam is measured there (the starts are the maps' values, not runs from
+//      them; KFMI_STREAM_FINAL=1 runs them and checks the seams in phase 5).
+constexpr int kScanTile = 256;
+__device__ __forceinline__ void affine_compose(double (&o)[12], const double (&l)[12], const double (&e)[12]) {
+    // o = l o e: A = A_l A_e, b = A_l b_e + b_l
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-            if (q < ns) gs[q] = double(wx[chain_state<M>(ch, q) * a.C + c]);
+    for (int k = 0; k < 3; ++k) {
+        double t = l[9 + k];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) t = __builtin_fma(l[k * 3 + q], e[9 + q], t);
+        o[9 + k] = t;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            double u = 0.0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) u = __builtin_fma(l[k * 3 + q], e[q * 3 + j], u);
+            o[k * 3 + j] = u;
+        }
+    }
+}
+
+__device__ __forceinline__ void affine_identity(double (&m)[12]) {
+#pragma unroll
+    for (int e = 0; e < 12; ++e) m[e] = (e == 0 || e == 4 || e == 8) ? 1.0 : 0.0;
+}
+
+// Inclusive Kogge-Stone scan of one affine map per thread over the block (LDS, struct of
+// arrays): v <- v_t o ... o v_0.  The caller syncs before reusing `pre`.
+__device__ __forceinline__ void block_scan_affine(double (&v)[12], double (*pre)[kScanTile], int tid) {
+#pragma unroll
+    for (int e = 0; e < 12; ++e) pre[e][tid] = v[e];
+    __syncthreads();
+    for (int d = 1; d < kScanTile; d <<= 1) {
+        double earlier[12];
+        const bool has = tid >= d;
+        if (has) {
+#pragma unroll
+            for (int e = 0; e < 12; ++e) earlier[e] = pre[e][tid - d];
+        }
+        __syncthreads();
+        if (has) {
+            double o[12];
+            affine_compose(o, v, earlier);
+#pragma unroll
+            for (int e = 0; e < 12; ++e) {
+                v[e] = o[e];
+                pre[e][tid] = o[e];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// phase 2: grid (tiles, chains)
+template <typename T, class M>
+__global__ __launch_bounds__(kScanTile) void stream_scan_tiles_kernel(const StreamArgs a) {
+    constexpr int NCH = M::NP + M::NA;
+    __shared__ double pre[12][kScanTile];
+    const int tid = int(threadIdx.x);
+    const int ch = int(blockIdx.y);
+    const int64_t tile = blockIdx.x, c = tile * kScanTile + tid;
+    double v[12];
+    if (c < a.C) {
+#pragma unroll
+        for (int e = 0; e < 12; ++e) v[e] = a.maps[(c * NCH + ch) * 12 + e];
+    } else {
+        affine_identity(v);
+    }
+    block_scan_affine(v, pre, tid);
+    if (c < a.C) {
+        double* o = a.pref + (c * NCH + ch) * 12;
+        if (tid == 0) {
+            double id[12];
+            affine_identity(id);
+#pragma unroll
+            for (int e = 0; e < 12; ++e) o[e] = id[e];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 12; ++e) o[e] = pre[e][tid - 1];
+        }
+    }
+    if (tid == kScanTile - 1) {
+        double* o = a.tiles + (tile * NCH + ch) * 12;
+#pragma unroll
+        for (int e = 0; e < 12; ++e) o[e] = v[e];
+    }
+}
+
+// phase 3: one block per chain
+template <typename T, class M>
+__global__ __launch_bounds__(kScanTile) void stream_scan_top_kernel(const StreamArgs a) {
+    constexpr int NCH = M::NP + M::NA;
+    __shared__ double pre[12][kScanTile];
+    __shared__ double carry[3];
+    const int tid = int(threadIdx.x);
+    const int ch = int(blockIdx.x);
+    const int ns = ch < M::NP ? 3 : 2;
+    const int64_t ntiles = (a.C + kScanTile - 1) / kScanTile;
+    if (tid < 3) carry[tid] = tid < ns ? double(static_cast<const T*>(a.hx)[chain_state<M>(ch, tid)]) : 0.0;
+    for (int64_t r0 = 0; r0 < ntiles; r0 += kScanTile) {
+        const int64_t t = r0 + tid;
+        double v[12];
+        if (t < ntiles) {
+#pragma unroll
+            for (int e = 0; e < 12; ++e) v[e] = a.tiles[(t * NCH + ch) * 12 + e];
+        } else {
+            affine_identity(v);
+        }
+        __syncthreads();  // the previous round's readers of pre / carry are done
+        block_scan_affine(v, pre, tid);
+        double x[3] = {carry[0], carry[1], carry[2]};
+        if (tid > 0) {
+            double e1[12];
+#pragma unroll
+            for (int e = 0; e < 12; ++e) e1[e] = pre[e][tid - 1];
+            apply_map(x, e1);
+        }
+        if (t < ntiles) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) a.tstart[(t * NCH + ch) * 3 + k] = x[k];
+        }
+        __syncthreads();  // every thread has read carry
+        if (tid == kScanTile - 1) {  // past the round (identity maps past the last tile)
+            double xe[3] = {carry[0], carry[1], carry[2]};
+            apply_map(xe, v);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) carry[k] = xe[k];
+        }
+    }
+    __syncthreads();
+    if (tid == 0 && a.xend) {  // the stream's end state
+        bool fin = true;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (k >= ns) continue;
+            a.xend[chain_state<M>(ch, k)] = carry[k];
+            fin = fin && (carry[k] - carry[k] == 0.0);
+        }
+        if (!fin) atomicOr(&a.check->bad, kStreamBadStart);
+    }
+}
+
+// phase 4: grid (tiles, chains)
+template <typename T, class M>
+__global__ __launch_bounds__(kScanTile) void stream_starts_kernel(const StreamArgs a) {
+    constexpr int NCH = M::NP + M::NA;
+    const int tid = int(threadIdx.x);
+    const int ch = int(blockIdx.y);
+    const int ns = ch < M::NP ? 3 : 2;
+    const int64_t tile = blockIdx.x, c = tile * kScanTile + tid;
+    bool fin = true;
+    if (c < a.C) {
+        double x[3], e1[12];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) x[k] = a.tstart[(tile * NCH + ch) * 3 + k];
+#pragma unroll
+        for (int e = 0; e < 12; ++e) e1[e] = a.pref[(c * NCH + ch) * 12 + e];
+        apply_map(x, e1);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             if (k >= ns) continue;
             const int i = chain_state<M>(ch, k);
-            const double e0 = double(mx[i * B + c]);
-            double s = e0;
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                if (q >= ns) continue;
-                A[k][q] = (double(mx[i * B + (q + 1) * a.C + c]) - e0) / a.delta;
-                s = __builtin_fma(-A[k][q], gs[q], s);
-            }
-            b[k] = s;
+            a.starts[i * a.C + c] = x[k];
+            fin = fin && (x[k] - x[k] == 0.0);  // NaN or inf fails
+            if (!a.xend) static_cast<T*>(a.fx)[i * a.C + c] = T(x[k]);
         }
-        int bad = 0;
-        if (ch == 0) {
-            bad |= a.wst[c];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) bad |= a.mst[q * a.C + c];
-        }
-        if (bad) atomicOr(&a.check->bad, 1);
-        if (c >= 1) {
-            const T* mP = static_cast<const T*>(a.mP);
-            const T* wP = static_cast<const T*>(a.wP);
+        if (!a.xend) {  // the final bank: the warm-up covariance, status 0
             const int r0 = chain_row0<M>(ch), nr = ns == 3 ? 6 : 3;
-            double scale = 0.0, gap = 0.0;
-            for (int r = r0; r < r0 + nr; ++r) {
-                const double pe = double(mP[r * B + (c - 1)]);
-                scale = fmax(scale, fabs(pe));
-                gap = fmax(gap, fabs(pe - double(wP[r * a.C + c])));
-            }
-            const double rel = gap / fmax(scale, 1e-300);
-            crel = rel == rel ? rel : __builtin_inf();
-        }
-    }
-    // one atomic per block (a device-wide atomic per thread serialised ~12k of them)
-    red[tid] = crel;
-    __syncthreads();
-    for (int n = NCH * kStreamSeg; n > 1; n = (n + 1) / 2) {  // NCH * 64 is not a power of two
-        const int h = (n + 1) / 2;
-        if (tid + h < n) red[tid] = fmax(red[tid], red[tid + h]);
-        __syncthreads();
-    }
-    if (tid == 0 && red[0] != 0.0) atomic_max_pos(&a.check->cov_gap, red[0]);
-    double* m = lm[ch][j];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) m[k * 3 + q] = A[k][q];
-        m[9 + k] = b[k];
-    }
-    if (c < a.C) {
-        double* g = a.maps + (c * NCH + ch) * 12;
-#pragma unroll
-        for (int e = 0; e < 12; ++e) g[e] = m[e];
-    }
-    __syncthreads();
-    if (j == 0) {
-        double SA[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, Sb[3] = {0, 0, 0};
-        for (int jj = 0; jj < kStreamSeg; ++jj) compose_into<M>(SA, Sb, lm[ch][jj]);
-        double* g = a.segmaps + (int64_t(blockIdx.x) * NCH + ch) * 12;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-#pragma unroll
-            for (int q = 0; q < 3; ++q) g[k * 3 + q] = SA[k][q];
-            g[9 + k] = Sb[k];
-        }
-    }
-}
-
-// phase 3 (one block): the segment products in order from the handle's state give every
-// segment's start (segstart[block][a]); tiles of kStreamSeg segments are staged through LDS
-template <typename T, class M>
-__global__ __launch_bounds__(1024) void stream_segscan_kernel(const StreamArgs a) {
-    constexpr int NCH = M::NP + M::NA;
-    __shared__ double lm[kStreamSeg * NCH * 12];
-    const int tid = int(threadIdx.x);
-    const int64_t nseg = (a.C + kStreamSeg - 1) / kStreamSeg;
-    double x[3] = {0, 0, 0};
-    if (tid < NCH) {
-        const int ns = tid < M::NP ? 3 : 2;
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-            if (q < ns) x[q] = double(static_cast<const T*>(a.hx)[chain_state<M>(tid, q)]);
-    }
-    for (int64_t s0 = 0; s0 < nseg; s0 += kStreamSeg) {
-        const int64_t n = (nseg - s0 < kStreamSeg ? nseg - s0 : kStreamSeg) * NCH * 12;
-        __syncthreads();
-        for (int64_t e = tid; e < n; e += blockDim.x) lm[e] = a.segmaps[s0 * NCH * 12 + e];
-        __syncthreads();
-        if (tid < NCH) {
-            for (int64_t s = s0; s < s0 + n / (NCH * 12); ++s) {
-                double* g = a.segstart + (s * NCH + tid) * 3;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) g[k] = x[k];
-                apply_map(x, lm + ((s - s0) * NCH + tid) * 12);
-            }
-        }
-    }
-}
-
-// phase 4 (blocks of kStreamSeg chunks x NCH chains): each block stages its chunk maps in LDS,
-// one thread per chain walks them from its segment's start, writing every chunk start (fp64,
-// and the final bank's x); the final bank's P is the warm-up bank's, its status 0
-template <typename T, class M>
-__global__ __launch_bounds__(1024) void stream_apply_kernel(const StreamArgs a) {
-    constexpr int NCH = M::NP + M::NA;
-    __shared__ double lm[NCH][kStreamSeg][12];
-    const int tid = int(threadIdx.x);
-    const int ch = tid / kStreamSeg, j = tid % kStreamSeg;
-    const int64_t c = int64_t(blockIdx.x) * kStreamSeg + j;
-    if (c < a.C) {
-        const double* g = a.maps + (c * NCH + ch) * 12;
-#pragma unroll
-        for (int e = 0; e < 12; ++e) lm[ch][j][e] = g[e];
-        if (ch == 0 && !a.xend) {  // the final bank (records from the map pass need none)
-#pragma unroll
-            for (int r = 0; r < M::NBLK; ++r)
+            for (int r = r0; r < r0 + nr; ++r)
                 static_cast<T*>(a.fP)[r * a.C + c] = static_cast<const T*>(a.wP)[r * a.C + c];
-            a.fst[c] = 0;
+            if (ch == 0) a.fst[c] = 0;
         }
     }
-    __syncthreads();
-    if (j == 0) {
-        const int ns = ch < M::NP ? 3 : 2;
-        const double* g = a.segstart + (int64_t(blockIdx.x) * NCH + ch) * 3;
-        double x[3] = {g[0], g[1], g[2]};
-        const int64_t c0 = int64_t(blockIdx.x) * kStreamSeg;
-        const int n = a.C - c0 < kStreamSeg ? int(a.C - c0) : kStreamSeg;
-        for (int jj = 0; jj < n; ++jj) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                if (k >= ns) continue;
-                const int i = chain_state<M>(ch, k);
-                a.starts[i * a.C + c0 + jj] = x[k];
-                if (!a.xend) static_cast<T*>(a.fx)[i * a.C + c0 + jj] = T(x[k]);
-            }
-            apply_map(x, lm[ch][jj]);
-        }
-        if (a.xend && c0 + n == a.C) {  // past the last chunk: the stream's end state
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-                if (k < ns) a.xend[chain_state<M>(ch, k)] = x[k];
-        }
+    const bool all_fin = __syncthreads_and(fin ? 1 : 0) != 0;
+    if (tid != 0) return;
+    StreamCheck* k = a.check;
+    if (!all_fin) atomicOr(&k->bad, kStreamBadStart);
+    if (!a.xend) return;  // a final pass follows: phase 5 decides
+    __threadfence();  // release this block's stores and flags before the count
+    const int blocks = int(gridDim.x * gridDim.y);
+    if (atomicAdd(&k->done, 1) != blocks - 1) return;
+    __threadfence();  // acquire: every block's stores and flags are visible
+    const int bad = atomicOr(&k->bad, 0);
+    const double cov_gap = __longlong_as_double(atomicOr(reinterpret_cast<unsigned long long*>(&k->cov_gap), 0ull));
+    k->state_gap = bad & kStreamBadStart ? __builtin_inf() : __builtin_nan("");
+    const bool ok = bad == 0 && cov_gap <= a.tol_cov;
+    k->ok = ok ? 1 : 0;
+    if (ok) {
+        const int64_t col = a.C - 1, B4 = 4 * a.C;  // the last chunk's end covariance
+        for (int i = 0; i < M::N; ++i) static_cast<T*>(a.hx)[i] = T(a.xend[i]);
+        for (int r = 0; r < M::NBLK; ++r) static_cast<T*>(a.hP)[r] = static_cast<const T*>(a.mP)[r * B4 + col];
+        a.hstatus[0] = 0;
     }
 }
 
@@ -1074,45 +1202,6 @@ __global__ __launch_bounds__(kBlock) void stream_records_kernel(const StreamArgs
         acc = __builtin_fma((xq - x0) / a.delta, d, acc);
     }
     static_cast<T*>(a.traj)[g] = T(acc);
-}
-
-// phase 9 (records from the map pass): the verdict without a final pass: no failed chunk
-// filter, finite chunk starts and end state, covariance seams within tolerance; a passed run
-// leaves the composed end state and the last chunk's end covariance in the handle
-template <typename T, class M>
-__global__ __launch_bounds__(1024) void stream_finish_maps_kernel(const StreamArgs a) {
-    __shared__ int redb[1024];
-    const int tid = int(threadIdx.x);
-    int bad = 0;
-    for (int64_t g = tid; g < a.C * M::N; g += blockDim.x) {
-        const double v = a.starts[g];
-        bad |= (v - v == 0.0) ? 0 : 2;  // NaN or inf
-    }
-    if (tid < M::N) {
-        const double v = a.xend[tid];
-        bad |= (v - v == 0.0) ? 0 : 2;
-    }
-    redb[tid] = bad;
-    __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (tid < w) redb[tid] |= redb[tid + w];
-        __syncthreads();
-    }
-    if (tid == 0) {
-        StreamCheck* k = a.check;
-        // no state seam is measured here: the chunk starts are the composed maps' values, not
-        // runs from the true starts (KFMI_STREAM_FINAL=1 runs them and checks the seams)
-        k->state_gap = redb[0] & 2 ? __builtin_inf() : __builtin_nan("");
-        k->bad |= redb[0] & 1;
-        const bool ok = k->bad == 0 && k->cov_gap <= a.tol_cov && !(redb[0] & 2);
-        k->ok = ok ? 1 : 0;
-        if (ok) {
-            const int64_t col = a.C - 1, B = 4 * a.C;  // variant 0 of the last chunk
-            for (int i = 0; i < M::N; ++i) static_cast<T*>(a.hx)[i] = T(a.xend[i]);
-            for (int r = 0; r < M::NBLK; ++r) static_cast<T*>(a.hP)[r] = static_cast<const T*>(a.mP)[r * B + col];
-            a.hstatus[0] = 0;
-        }
-    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1186,16 +1275,28 @@ __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArg
     const int64_t c = cp / a.np, piece = cp % a.np;
     const int64_t cend = (c + 1) * a.L < a.S ? (c + 1) * a.L : a.S;
     const int64_t e0 = c * a.L + piece * a.lp, e1 = e0 + a.lp < cend ? e0 + a.lp : cend;
+    // events in batches of 8, the next batch's type and dt loaded while this one computes
     constexpr int kB = 8;
+    int tyn[kB];
+    double dvn[kB];
+    auto fetch = [&](int64_t e) {
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const bool in = e + k < e1;
+            tyn[k] = in ? int(a.etype[e + k]) : 255;
+            dvn[k] = in ? a.dt[e + k] : 0.0;
+        }
+    };
+    fetch(e0);
     for (int64_t e = e0; e < e1; e += kB) {
         int ty[kB];
         double dv[kB];
 #pragma unroll
         for (int k = 0; k < kB; ++k) {
-            const bool in = e + k < e1;
-            ty[k] = in ? int(a.etype[e + k]) : 255;
-            dv[k] = in ? a.dt[e + k] : 0.0;
+            ty[k] = tyn[k];
+            dv[k] = dvn[k];
         }
+        fetch(e + kB);
 #pragma unroll
         for (int k = 0; k < kB; ++k) lft_event<M>(v, ty[k], dv[k], pva, q, si, sg);
         if (((e - e0) & 15) == kB) {  // every 16 events
@@ -1238,109 +1339,154 @@ __device__ __forceinline__ void chain_block_full(const T* P, int64_t stride, int
     }
 }
 
-// phase 7: one parallel iteration P(c) <- map_(c-1)(P(c-1)), P(0) = the handle's P; the last
-// writes the warm-up bank's covariance: chunk c starts from P(c - kp) (kp polish chunks of
-// event warm-up follow; c < kp: the handle's P, exact)
-template <typename T, class M>
-__global__ __launch_bounds__(kBlock) void stream_lft_iter_kernel(const StreamArgs a) {
-    constexpr int NCH = M::NP + M::NA;
-    const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (g >= a.C * NCH) return;
-    const int64_t c = g / NCH;
-    const int ch = int(g % NCH);
-    double pn[3][3];
-    double ph[3][3];
-    chain_block_full<T, M>(static_cast<const T*>(a.hP), 1, 0, ch, ph);
-    if (c == 0) {
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) pn[i][j] = ph[i][j];
-    } else {
-        double p[3][3];
-        if (a.pcur) {  // the first iteration guesses the handle's P everywhere
-            const double* pc = a.pcur + (g - NCH) * 9;
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) p[i][j] = pc[i * 3 + j];
-        } else {
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) p[i][j] = ph[i][j];
-        }
-        // chunk c - 1's piece maps in order (each piece short enough for its map to be well
-        // conditioned; the LFT error grows with the events one product spans)
-        for (int pi = 0; pi < a.np; ++pi) {
-        const double* m = a.phi + (((c - 1) * a.np + pi) * NCH + ch) * 36;
-        double X[3][3], Y[3][3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                double x = m[i * 6 + 3 + j], y = m[(i + 3) * 6 + 3 + j];
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    x = __builtin_fma(m[i * 6 + k], p[k][j], x);
-                    y = __builtin_fma(m[(i + 3) * 6 + k], p[k][j], y);
-                }
-                X[i][j] = x;
-                Y[i][j] = y;
-            }
-        // P' = X Y^-1 via the adjugate of Y, then symmetrised
-        const double a00 = Y[1][1] * Y[2][2] - Y[1][2] * Y[2][1], a01 = Y[0][2] * Y[2][1] - Y[0][1] * Y[2][2],
-                     a02 = Y[0][1] * Y[1][2] - Y[0][2] * Y[1][1];
-        const double a10 = Y[1][2] * Y[2][0] - Y[1][0] * Y[2][2], a11 = Y[0][0] * Y[2][2] - Y[0][2] * Y[2][0],
-                     a12 = Y[0][2] * Y[1][0] - Y[0][0] * Y[1][2];
-        const double a20 = Y[1][0] * Y[2][1] - Y[1][1] * Y[2][0], a21 = Y[0][1] * Y[2][0] - Y[0][0] * Y[2][1],
-                     a22 = Y[0][0] * Y[1][1] - Y[0][1] * Y[1][0];
-        const double det = Y[0][0] * a00 + Y[0][1] * a10 + Y[0][2] * a20;
-        const double inv[3][3] = {{a00, a01, a02}, {a10, a11, a12}, {a20, a21, a22}};
-        const double rd = 1.0 / det;
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                double s = 0.0;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) s = __builtin_fma(X[i][k], inv[k][j], s);
-                pn[i][j] = s * rd;
-            }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = i + 1; j < 3; ++j) pn[i][j] = pn[j][i] = 0.5 * (pn[i][j] + pn[j][i]);
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) p[i][j] = pn[i][j];
-        }
-    }
-    double* o = a.pnext + g * 9;
+// one piece map applied to a chain covariance p (3x3, in place): P' = X Y^-1 with
+// [X; Y] = [[A, B], [C, D]] [P; I], via the adjugate of Y, then symmetrised
+__device__ __forceinline__ void lft_apply(double (&p)[3][3], const double (&m)[36]) {
+    double X[3][3], Y[3][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) o[i * 3 + j] = pn[i][j];
-    if (a.last) {
-        T* wP = static_cast<T*>(a.wP);
-        const int r0 = chain_row0<M>(ch);
-        auto put = [&](int64_t col, const double (&p)[3][3]) {
-            if (ch < M::NP) {
-                wP[(r0 + 0) * a.C + col] = T(p[0][0]);
-                wP[(r0 + 1) * a.C + col] = T(p[0][1]);
-                wP[(r0 + 2) * a.C + col] = T(p[0][2]);
-                wP[(r0 + 3) * a.C + col] = T(p[1][1]);
-                wP[(r0 + 4) * a.C + col] = T(p[1][2]);
-                wP[(r0 + 5) * a.C + col] = T(p[2][2]);
-            } else {
-                wP[(r0 + 0) * a.C + col] = T(p[0][0]);
-                wP[(r0 + 1) * a.C + col] = T(p[0][1]);
-                wP[(r0 + 2) * a.C + col] = T(p[1][1]);
+        for (int j = 0; j < 3; ++j) {
+            double x = m[i * 6 + 3 + j], y = m[(i + 3) * 6 + 3 + j];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                x = __builtin_fma(m[i * 6 + k], p[k][j], x);
+                y = __builtin_fma(m[(i + 3) * 6 + k], p[k][j], y);
             }
-        };
-        if (c + a.kp < a.C) put(c + a.kp, pn);
-        if (c < a.kp) put(c, ph);
+            X[i][j] = x;
+            Y[i][j] = y;
+        }
+    const double a00 = Y[1][1] * Y[2][2] - Y[1][2] * Y[2][1], a01 = Y[0][2] * Y[2][1] - Y[0][1] * Y[2][2],
+                 a02 = Y[0][1] * Y[1][2] - Y[0][2] * Y[1][1];
+    const double a10 = Y[1][2] * Y[2][0] - Y[1][0] * Y[2][2], a11 = Y[0][0] * Y[2][2] - Y[0][2] * Y[2][0],
+                 a12 = Y[0][2] * Y[1][0] - Y[0][0] * Y[1][2];
+    const double a20 = Y[1][0] * Y[2][1] - Y[1][1] * Y[2][0], a21 = Y[0][1] * Y[2][0] - Y[0][0] * Y[2][1],
+                 a22 = Y[0][0] * Y[1][1] - Y[0][1] * Y[1][0];
+    const double det = Y[0][0] * a00 + Y[0][1] * a10 + Y[0][2] * a20;
+    const double inv[3][3] = {{a00, a01, a02}, {a10, a11, a12}, {a20, a21, a22}};
+    const double rd = 1.0 / det;
+    double pn[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) s = __builtin_fma(X[i][k], inv[k][j], s);
+            pn[i][j] = s * rd;
+        }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = i + 1; j < 3; ++j) pn[i][j] = pn[j][i] = 0.5 * (pn[i][j] + pn[j][i]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) p[i][j] = pn[i][j];
+}
+
+// phase 7: every chunk's start covariance from the maps, in ONE launch: chunk c starts from the
+// handle's P advanced by the piece maps of chunks max(0, c - iters) .. c - 1 (every chunk from
+// the stream start when c < iters: exact), which covers the recursion's forgetting — the value
+// the round-1 Jacobi iteration (one launch per step over all chunks) reached after `iters`
+// launches, bit for bit.  Block (x, chain) owns chunks [b0, b0 + a.G) of one chain: its threads
+// first stage every piece map the window needs, [max(0, b0 - iters), b0 + G - 1) x np, into LDS
+// with coalesced loads, then thread t walks chunk b0 + t's window from LDS (a dependent walk
+// over global memory waited ~2 us per map).  a.G = 0: no LDS (windows too long), maps read from
+// global memory.  Thread t also writes its chunk of the warm-up bank (the handle's state as the
+// guess, its status) and, without event warm-up (a.kp == 0), the map bank itself: every
+// variant's covariance column (the map pass reads column c) and the guesses, variant q + 1 with
+// + delta on component q of every chain.  Thread 0 of block 0 zeroes the check.
+template <typename T, class M>
+__global__ __launch_bounds__(kBlock) void stream_lft_start_kernel(const StreamArgs a) {
+    extern __shared__ double lmap[];  // [36][nu]: element e of the block's nu = (G + iters) * np window maps
+    constexpr int NCH = M::NP + M::NA;
+    const int tid = int(threadIdx.x);
+    const int ch = int(blockIdx.y);
+    if (blockIdx.x == 0 && ch == 0 && tid == 0) {
+        a.check->ok = 0;
+        a.check->bad = 0;
+        a.check->cov_gap = 0.0;
+        a.check->state_gap = 0.0;
+        a.check->done = 0;
+    }
+    const bool lds = a.G > 0;
+    const int64_t BC = lds ? a.G : kBlock;
+    const int64_t b0 = int64_t(blockIdx.x) * BC;
+    const int64_t ws = b0 - a.iters > 0 ? b0 - a.iters : 0;  // first chunk whose maps the block reads
+    // struct of arrays: at each step of the walks, consecutive threads read consecutive maps
+    const int64_t nu = (a.G + a.iters) * a.np;
+    if (lds) {
+        const int64_t we = (b0 + BC < a.C ? b0 + BC : a.C) - 1;  // maps of chunks [ws, we)
+        const int64_t n = (we > ws ? we - ws : 0) * a.np * 36;
+        for (int64_t e = tid; e < n; e += blockDim.x) {
+            const int64_t u = ws * a.np + e / 36;
+            lmap[(e % 36) * nu + e / 36] = a.phi[(u * NCH + ch) * 36 + e % 36];
+        }
+        __syncthreads();
+    }
+    const int64_t c = b0 + tid;
+    if (tid >= BC || c >= a.C) return;
+    const int ns = ch < M::NP ? 3 : 2;
+    double ph[3][3];
+    chain_block_full<T, M>(static_cast<const T*>(a.hP), 1, 0, ch, ph);
+    double p[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) p[i][j] = ph[i][j];
+    const int64_t cs = c - a.iters > 0 ? c - a.iters : 0;
+    for (int64_t u = cs * a.np; u < c * a.np; ++u) {
+        // chunk u / np's piece maps in order (each piece short enough for its map to be well
+        // conditioned; the LFT error grows with the events one product spans)
+        double m[36];
+        if (lds) {
+            const double* src = lmap + (u - ws * a.np);
+#pragma unroll
+            for (int e = 0; e < 36; ++e) m[e] = src[e * nu];
+        } else {
+            const double* src = a.phi + (u * NCH + ch) * 36;
+#pragma unroll
+            for (int e = 0; e < 36; ++e) m[e] = src[e];
+        }
+        lft_apply(p, m);
+    }
+    const int r0 = chain_row0<M>(ch);
+    const int64_t B4 = 4 * a.C;
+    auto put = [&](T* P, int64_t stride, int64_t col, const double (&q)[3][3]) {
+        if (ch < M::NP) {
+            P[(r0 + 0) * stride + col] = T(q[0][0]);
+            P[(r0 + 1) * stride + col] = T(q[0][1]);
+            P[(r0 + 2) * stride + col] = T(q[0][2]);
+            P[(r0 + 3) * stride + col] = T(q[1][1]);
+            P[(r0 + 4) * stride + col] = T(q[1][2]);
+            P[(r0 + 5) * stride + col] = T(q[2][2]);
+        } else {
+            P[(r0 + 0) * stride + col] = T(q[0][0]);
+            P[(r0 + 1) * stride + col] = T(q[0][1]);
+            P[(r0 + 2) * stride + col] = T(q[1][1]);
+        }
+    };
+    // chunk c's start; with polish chunks, the warm-up bank runs chunk c + kp from it
+    if (c + a.kp < a.C) put(static_cast<T*>(a.wP), a.C, c + a.kp, p);
+    if (c < a.kp) put(static_cast<T*>(a.wP), a.C, c, ph);
+    const T* hx = static_cast<const T*>(a.hx);
+    const int32_t hst = a.hstatus[0];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (k < ns) static_cast<T*>(a.wx)[chain_state<M>(ch, k) * a.C + c] = hx[chain_state<M>(ch, k)];
+    if (ch == 0) a.wst[c] = hst;
+    if (a.kp == 0) {
+        put(static_cast<T*>(a.mP), B4, c, p);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (k < ns) {
+                    const T g = hx[chain_state<M>(ch, k)];
+                    static_cast<T*>(a.mx)[chain_state<M>(ch, k) * B4 + q * a.C + c] = (q > 0 && k == q - 1) ? g + T(a.delta) : g;
+                }
+        if (ch == 0) a.mst[c] = hst;
     }
 }
 
@@ -2030,15 +2176,25 @@ hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t 
     return hipGetLastError();
 }
 
-hipError_t launch_ref_stream(int model, bool f64, const RefArgs& a, hipStream_t stream) {
-    if (a.s_len <= 0 || a.s_nchunks <= 0) return hipErrorInvalidValue;
+hipError_t launch_ref_stream(int model, bool f64, const RefArgs& a, hipStream_t stream, int nv) {
+    if (a.s_len <= 0 || a.s_nchunks <= 0 || (nv != 1 && nv != 4)) return hipErrorInvalidValue;
     const dim3 cgrid(static_cast<unsigned>((a.B * kGroup + kBlock - 1) / kBlock));
     if (model == 15) {
-        if (f64) ref_chain_kernel<double, M15, true><<<cgrid, kBlock, 0, stream>>>(a);
-        else ref_chain_kernel<float, M15, true><<<cgrid, kBlock, 0, stream>>>(a);
+        if (nv == 4) {
+            if (f64) ref_chain_kernel<double, M15, true, 4><<<cgrid, kBlock, 0, stream>>>(a);
+            else ref_chain_kernel<float, M15, true, 4><<<cgrid, kBlock, 0, stream>>>(a);
+        } else {
+            if (f64) ref_chain_kernel<double, M15, true><<<cgrid, kBlock, 0, stream>>>(a);
+            else ref_chain_kernel<float, M15, true><<<cgrid, kBlock, 0, stream>>>(a);
+        }
     } else if (model == 8) {
-        if (f64) ref_chain_kernel<double, M8, true><<<cgrid, kBlock, 0, stream>>>(a);
-        else ref_chain_kernel<float, M8, true><<<cgrid, kBlock, 0, stream>>>(a);
+        if (nv == 4) {
+            if (f64) ref_chain_kernel<double, M8, true, 4><<<cgrid, kBlock, 0, stream>>>(a);
+            else ref_chain_kernel<float, M8, true, 4><<<cgrid, kBlock, 0, stream>>>(a);
+        } else {
+            if (f64) ref_chain_kernel<double, M8, true><<<cgrid, kBlock, 0, stream>>>(a);
+            else ref_chain_kernel<float, M8, true><<<cgrid, kBlock, 0, stream>>>(a);
+        }
     } else {
         return hipErrorInvalidValue;
     }
@@ -2049,24 +2205,35 @@ template <typename T, class M>
 void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
     constexpr int NCH = M::NP + M::NA;
     auto grid = [](int64_t n) { return dim3(static_cast<unsigned>((n + kBlock - 1) / kBlock)); };
-    const dim3 segs(static_cast<unsigned>((a.C + kStreamSeg - 1) / kStreamSeg));
     switch (phase) {
         case 0: stream_init_kernel<T, M><<<grid(a.C), kBlock, 0, stream>>>(a); break;
         case 1: stream_perturb_kernel<T, M><<<grid(4 * a.C), kBlock, 0, stream>>>(a); break;
-        case 2: stream_maps_kernel<T, M><<<segs, NCH * kStreamSeg, 0, stream>>>(a); break;
-        case 3: stream_segscan_kernel<T, M><<<1, 1024, 0, stream>>>(a); break;
-        case 4: stream_apply_kernel<T, M><<<segs, NCH * kStreamSeg, 0, stream>>>(a); break;
+        case kStreamPhaseScanTiles: {
+            const dim3 g(unsigned((a.C + kScanTile - 1) / kScanTile), NCH);
+            stream_scan_tiles_kernel<T, M><<<g, kScanTile, 0, stream>>>(a);
+            break;
+        }
+        case kStreamPhaseScanTop: stream_scan_top_kernel<T, M><<<NCH, kScanTile, 0, stream>>>(a); break;
+        case kStreamPhaseStarts: {
+            const dim3 g(unsigned((a.C + kScanTile - 1) / kScanTile), NCH);
+            stream_starts_kernel<T, M><<<g, kScanTile, 0, stream>>>(a);
+            break;
+        }
         case kStreamPhaseLftMaps: stream_lft_maps_kernel<T, M><<<grid(a.C * a.np * NCH * kGroup), kBlock, 0, stream>>>(a); break;
-        case kStreamPhaseLftIter: stream_lft_iter_kernel<T, M><<<grid(a.C * NCH), kBlock, 0, stream>>>(a); break;
+        case kStreamPhaseLftStart: {
+            const int64_t bc = a.G > 0 ? a.G : kBlock;
+            const size_t lds = a.G > 0 ? size_t(a.G + a.iters) * a.np * 36 * sizeof(double) : 0;
+            stream_lft_start_kernel<T, M><<<dim3(unsigned((a.C + bc - 1) / bc), NCH), kBlock, lds, stream>>>(a);
+            break;
+        }
         case 5: stream_finish_kernel<T, M><<<1, 1024, 0, stream>>>(a); break;
         case kStreamPhaseRecords: stream_records_kernel<T, M><<<grid(a.S * M::NTRAJ), kBlock, 0, stream>>>(a); break;
-        case kStreamPhaseFinishMaps: stream_finish_maps_kernel<T, M><<<1, 1024, 0, stream>>>(a); break;
         default: break;
     }
 }
 
 hipError_t launch_stream_phase(int model, bool f64, int phase, const StreamArgs& a, hipStream_t stream) {
-    if (a.C < 2 || phase < 0 || phase > kStreamPhaseFinishMaps) return hipErrorInvalidValue;
+    if (a.C < 2 || phase < 0 || phase > kStreamPhaseRecords) return hipErrorInvalidValue;
     if (model == 15) {
         if (f64) stream_phase<double, M15>(phase, a, stream);
         else stream_phase<float, M15>(phase, a, stream);
