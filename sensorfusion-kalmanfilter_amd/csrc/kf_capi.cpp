@@ -638,6 +638,7 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     kfmi::StreamArgs sa{};
     sa.C = C;
     sa.delta = 1024.0;  // the maps are affine: a large step only shrinks the roundoff of the differences
+    sa.rdelta = 1.0 / sa.delta;  // exact: delta is a power of two
     sa.tol_state = h->dtype == KF_F64 ? 1e-9 : 1e-4;
     sa.tol_cov = h->dtype == KF_F64 ? 1e-12 : 1e-5;
     sa.hx = h->x;
@@ -723,10 +724,12 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
         // every chunk start from at least `iters` chunks of maps: kStreamLftEvents events of
         // forgetting; one start thread walks iters + G chunks
         sa.iters = int((kStreamLftEvents + L - 1) / L) + 1;
-        // chunks per block of the start kernel: its window's piece maps, (G + iters) * np of
-        // them, must fit 64 KB of LDS (0: read them from global memory)
+        // the start kernel: a block of 64 threads, g chunks each, stages the piece maps of its
+        // windows, (64 g + iters) * np of them, in 64 KB of LDS; g = 0: no LDS (one chunk per
+        // thread, maps from global memory)
         const int64_t fit = kStreamStartLdsMaps / np - sa.iters;
-        sa.G = fit >= 16 ? std::min<int64_t>(fit, 256) : 0;
+        sa.g = fit >= 64 ? std::min<int64_t>(fit / 64, 4) : 0;  // kStartMaxG
+        sa.G = 64 * sa.g;
         e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseLftMaps, sa, st);
         // the start kernel also zeroes the check and fills the warm-up bank (and, without event
         // warm-up, the map bank)

@@ -98,7 +98,8 @@ struct StreamCheck {
 };
 struct StreamArgs {
     int64_t C;               // chunks
-    double delta;            // state perturbation of the map pass
+    double delta;            // state perturbation of the map pass (a power of two)
+    double rdelta;           // 1 / delta (exact)
     double tol_state, tol_cov;
     void* hx;                // handle state (one filter): [N], [NBLK], status
     void* hP;
@@ -127,7 +128,8 @@ struct StreamArgs {
     int64_t lp;
     double* phi;             // [C][np][chains][36]: per piece and chain, the 6x6 covariance map [[A B] [C D]]
     int iters;               // chunk maps (at least) behind every chunk start
-    int64_t G;               // chunks per block of the start kernel (their maps staged in LDS); 0: no LDS
+    int64_t G;               // chunks per block of the start kernel (their windows' maps staged in LDS)
+    int64_t g;               // chunks per thread of the start kernel; 0: no LDS, one chunk per thread
     // records from the map pass (no final pass): the map bank's trajectories per variant
     const void* traj4;       // [4][vstride][NTRAJ]
     int64_t vstride;

@@ -1181,9 +1181,10 @@ __global__ __launch_bounds__(kBlock) void stream_records_kernel(const StreamArgs
     constexpr int NCH = M::NP + M::NA;
     const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;  // e * NTRAJ + i: coalesced rows
     if (g >= a.S * M::NTRAJ) return;
-    const int64_t e = g / M::NTRAJ;
-    const int i = int(g % M::NTRAJ);
-    const int64_t c = e / a.L;
+    // 32-bit divisions (S * NTRAJ < 2^31: kf_run_stream's offsets are 32-bit)
+    const uint32_t e = uint32_t(g) / uint32_t(M::NTRAJ);
+    const int i = int(uint32_t(g) - e * uint32_t(M::NTRAJ));
+    const int64_t c = e / uint32_t(a.L);
     const T* t4 = static_cast<const T*>(a.traj4);
     const T* wx = static_cast<const T*>(a.wx);
     int ch = 0;  // the chain whose first component is state i (the trajectory holds those)
@@ -1199,7 +1200,7 @@ __global__ __launch_bounds__(kBlock) void stream_records_kernel(const StreamArgs
         const double xq = double(t4[(qq + 1) * a.vstride * M::NTRAJ + g]);
         const int idx = chain_state<M>(ch, qq);
         const double d = a.starts[idx * a.C + c] - double(wx[idx * a.C + c]);
-        acc = __builtin_fma((xq - x0) / a.delta, d, acc);
+        acc = __builtin_fma((xq - x0) * a.rdelta, d, acc);  // delta is a power of two: exact
     }
     static_cast<T*>(a.traj)[g] = T(acc);
 }
@@ -1228,10 +1229,10 @@ __device__ __forceinline__ void chain_noise(int ch, double (&q)[3], double (&si_
     si_gps = pva ? 1.0 / kRGps : 0.0;
 }
 
-// phase 6: the product of each chunk's event matrices per chain.  An event acts on the columns
-// of the 6x6 product independently, so a lane group of 8 holds one (chunk, chain): lane j < 6
-// carries column j.  Rescaled by a power of two (the group's max, DPP) every 16 events, which a
-// linear-fractional map ignores.  Event types and dt are loaded 8 events at a time.
+// phase 6: the product of each chunk piece's event matrices per chain, one lane per (piece,
+// chain) holding the 6x6 product (an event acts on its columns independently).  Rescaled by a
+// power of two (the product's max) every 16 events, which a linear-fractional map ignores.
+// Event types and dt are loaded 8 events at a time, one batch ahead.
 template <class M>
 __device__ __forceinline__ void lft_event(double (&v)[6], int type, double dt, bool pva, const double (&q)[3],
                                           const double (&si)[3], double sg) {
@@ -1260,18 +1261,21 @@ __device__ __forceinline__ void lft_event(double (&v)[6], int type, double dt, b
 template <typename T, class M>
 __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArgs a) {
     constexpr int NCH = M::NP + M::NA;
-    const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-    const int64_t grp = g / kGroup;
-    if (grp >= a.C * a.np * NCH) return;  // whole groups leave together
-    const int j = int(g % kGroup);
+    // one lane per (chunk piece, chain), carrying all six columns of the 6x6 product: an event's
+    // type / dt handling is paid once for the six columns (the round-1 kernel ran one column per
+    // lane of an 8-lane group, two lanes idle)
+    const int64_t grp = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (grp >= a.C * a.np * NCH) return;
     const int64_t cp = grp / NCH;  // chunk * np + piece
     const int ch = int(grp % NCH);
     const bool pva = ch < M::NP;
     double q[3], si[3], sg;
     chain_noise<M>(ch, q, si, sg);
-    double v[6];
+    double v[6][6];  // v[j] = column j
 #pragma unroll
-    for (int i = 0; i < 6; ++i) v[i] = i == j ? 1.0 : 0.0;  // lanes 6, 7: zero columns
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v[j][i] = i == j ? 1.0 : 0.0;
     const int64_t c = cp / a.np, piece = cp % a.np;
     const int64_t cend = (c + 1) * a.L < a.S ? (c + 1) * a.L : a.S;
     const int64_t e0 = c * a.L + piece * a.lp, e1 = e0 + a.lp < cend ? e0 + a.lp : cend;
@@ -1298,26 +1302,29 @@ __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArg
         }
         fetch(e + kB);
 #pragma unroll
-        for (int k = 0; k < kB; ++k) lft_event<M>(v, ty[k], dv[k], pva, q, si, sg);
-        if (((e - e0) & 15) == kB) {  // every 16 events
+        for (int k = 0; k < kB; ++k)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) lft_event<M>(v[j], ty[k], dv[k], pva, q, si, sg);
+        if (((e - e0) & 15) == kB) {  // every 16 events: rescale by a power of two (the max)
             double mx = 0.0;
 #pragma unroll
-            for (int i = 0; i < 6; ++i) mx = fmax(mx, fabs(v[i]));
-            mx = fmax(mx, dpp_d<kDppXor1>(mx));
-            mx = fmax(mx, dpp_d<kDppXor2>(mx));
-            mx = fmax(mx, dpp_d<kDppHalfMirror>(mx));
+            for (int j = 0; j < 6; ++j)
+#pragma unroll
+                for (int i = 0; i < 6; ++i) mx = fmax(mx, fabs(v[j][i]));
             int ex;
             (void)frexp(mx, &ex);
             const double sc = ldexp(1.0, -ex);
 #pragma unroll
-            for (int i = 0; i < 6; ++i) v[i] *= sc;
+            for (int j = 0; j < 6; ++j)
+#pragma unroll
+                for (int i = 0; i < 6; ++i) v[j][i] *= sc;
         }
     }
-    if (j < 6) {
-        double* o = a.phi + grp * 36;
+    double* o = a.phi + grp * 36;
 #pragma unroll
-        for (int i = 0; i < 6; ++i) o[i * 6 + j] = v[i];
-    }
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) o[i * 6 + j] = v[j][i];
 }
 
 // a chain's block of the block-packed covariance as a full 3x3 (the inert state: variance 1)
@@ -1386,18 +1393,20 @@ __device__ __forceinline__ void lft_apply(double (&p)[3][3], const double (&m)[3
 }
 
 // phase 7: every chunk's start covariance from the maps, in ONE launch: chunk c starts from the
-// handle's P advanced by the piece maps of chunks max(0, c - iters) .. c - 1 (every chunk from
-// the stream start when c < iters: exact), which covers the recursion's forgetting — the value
-// the round-1 Jacobi iteration (one launch per step over all chunks) reached after `iters`
-// launches, bit for bit.  Block (x, chain) owns chunks [b0, b0 + a.G) of one chain: its threads
-// first stage every piece map the window needs, [max(0, b0 - iters), b0 + G - 1) x np, into LDS
-// with coalesced loads, then thread t walks chunk b0 + t's window from LDS (a dependent walk
-// over global memory waited ~2 us per map).  a.G = 0: no LDS (windows too long), maps read from
-// global memory.  Thread t also writes its chunk of the warm-up bank (the handle's state as the
-// guess, its status) and, without event warm-up (a.kp == 0), the map bank itself: every
-// variant's covariance column (the map pass reads column c) and the guesses, variant q + 1 with
-// + delta on component q of every chain.  Thread 0 of block 0 zeroes the check.
-template <typename T, class M>
+// handle's P advanced by the piece maps of at least the `iters` chunks before it (every chunk
+// from the stream start when c < iters: exact), which covers the recursion's forgetting.  Block
+// (x, chain) owns chunks [b0, b0 + a.G) of one chain, a.g consecutive chunks per thread: its
+// threads first stage every piece map the windows need, [max(0, b0 - iters), b0 + G - 1) x np,
+// into LDS (struct of arrays) with coalesced loads (a dependent walk over global memory waited
+// ~2 us per map), then thread t walks from max(0, c_t - iters) through its g chunks, recording
+// each start: (iters + g - 1) maps for g chunks.  a.g = 0: no LDS (windows too long for it), one
+// chunk per thread, maps read from global memory.  For every chunk it also writes the warm-up
+// bank (the handle's state as the guess, its status) and, without event warm-up (a.kp == 0),
+// the map bank itself: every variant's covariance column (the map pass reads column c) and the
+// guesses, variant q + 1 with + delta on component q of every chain.  Thread 0 of block 0
+// zeroes the check.
+constexpr int kStartMaxG = 4;  // chunks per thread of the start kernel (their starts stay in registers)
+template <typename T, class M, bool LDS>
 __global__ __launch_bounds__(kBlock) void stream_lft_start_kernel(const StreamArgs a) {
     extern __shared__ double lmap[];  // [36][nu]: element e of the block's nu = (G + iters) * np window maps
     constexpr int NCH = M::NP + M::NA;
@@ -1410,47 +1419,84 @@ __global__ __launch_bounds__(kBlock) void stream_lft_start_kernel(const StreamAr
         a.check->state_gap = 0.0;
         a.check->done = 0;
     }
-    const bool lds = a.G > 0;
-    const int64_t BC = lds ? a.G : kBlock;
+    const int64_t gt = LDS ? a.g : 1;                  // chunks per thread
+    const int64_t BC = LDS ? a.G : int64_t(blockDim.x);  // chunks per block
     const int64_t b0 = int64_t(blockIdx.x) * BC;
     const int64_t ws = b0 - a.iters > 0 ? b0 - a.iters : 0;  // first chunk whose maps the block reads
-    // struct of arrays: at each step of the walks, consecutive threads read consecutive maps
-    const int64_t nu = (a.G + a.iters) * a.np;
-    if (lds) {
+    // struct of arrays: at each step of the walks, consecutive threads read maps g apart
+    const uint32_t nu = uint32_t((BC + a.iters) * a.np);
+    if constexpr (LDS) {
         const int64_t we = (b0 + BC < a.C ? b0 + BC : a.C) - 1;  // maps of chunks [ws, we)
-        const int64_t n = (we > ws ? we - ws : 0) * a.np * 36;
-        for (int64_t e = tid; e < n; e += blockDim.x) {
-            const int64_t u = ws * a.np + e / 36;
-            lmap[(e % 36) * nu + e / 36] = a.phi[(u * NCH + ch) * 36 + e % 36];
+        // 32-bit indices (a 64-bit division is a ~100-instruction sequence per element), 16 loads
+        // in flight per thread (a load-store loop waited one memory latency per element)
+        const uint32_t n = uint32_t(we > ws ? we - ws : 0) * uint32_t(a.np) * 36u;
+        const double* src = a.phi + (ws * a.np * NCH + ch) * 36;
+        constexpr int kU = 16;
+        const uint32_t nt = blockDim.x;
+        for (uint32_t e0 = uint32_t(tid); e0 < n; e0 += kU * nt) {
+            double v[kU];
+#pragma unroll
+            for (int j = 0; j < kU; ++j) {
+                const uint32_t e = e0 + uint32_t(j) * nt;
+                const uint32_t u = e / 36u, k = e - u * 36u;
+                v[j] = e < n ? src[u * uint32_t(NCH * 36) + k] : 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < kU; ++j) {
+                const uint32_t e = e0 + uint32_t(j) * nt;
+                const uint32_t u = e / 36u, k = e - u * 36u;
+                if (e < n) lmap[k * nu + u] = v[j];
+            }
         }
         __syncthreads();
     }
-    const int64_t c = b0 + tid;
-    if (tid >= BC || c >= a.C) return;
+    const int64_t ct = b0 + tid * gt;  // this thread's first chunk
+    if (ct >= a.C || ct >= b0 + BC) return;
+    const int64_t ce = ct + gt < a.C ? ct + gt : a.C;
     const int ns = ch < M::NP ? 3 : 2;
+    // every global read before the first store (a load after a store to a pointer that may
+    // alias it waits for the store)
     double ph[3][3];
     chain_block_full<T, M>(static_cast<const T*>(a.hP), 1, 0, ch, ph);
-    double p[3][3];
+    T gx[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gx[k] = k < ns ? static_cast<const T*>(a.hx)[chain_state<M>(ch, k)] : T(0);
+    const int32_t hst = a.hstatus[0];
+    double p[3][3], ps[kStartMaxG][3][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) p[i][j] = ph[i][j];
-    const int64_t cs = c - a.iters > 0 ? c - a.iters : 0;
-    for (int64_t u = cs * a.np; u < c * a.np; ++u) {
-        // chunk u / np's piece maps in order (each piece short enough for its map to be well
-        // conditioned; the LFT error grows with the events one product spans)
-        double m[36];
-        if (lds) {
-            const double* src = lmap + (u - ws * a.np);
+    const int64_t cs = ct - a.iters > 0 ? ct - a.iters : 0;
+    for (int64_t c = cs; c < ce; ++c) {
+        if (c >= ct) {
+            const int r = int(c - ct);
 #pragma unroll
-            for (int e = 0; e < 36; ++e) m[e] = src[e * nu];
-        } else {
-            const double* src = a.phi + (u * NCH + ch) * 36;
+            for (int rr = 0; rr < kStartMaxG; ++rr)
+                if (rr == r)
 #pragma unroll
-            for (int e = 0; e < 36; ++e) m[e] = src[e];
+                    for (int i = 0; i < 3; ++i)
+#pragma unroll
+                        for (int j = 0; j < 3; ++j) ps[rr][i][j] = p[i][j];
         }
-        lft_apply(p, m);
+        if (c + 1 >= ce) break;
+        // chunk c's piece maps in order (each piece short enough for its map to be well
+        // conditioned; the LFT error grows with the events one product spans)
+        for (int64_t u = c * a.np; u < (c + 1) * a.np; ++u) {
+            double m[36];
+            if constexpr (LDS) {
+                const double* src = lmap + uint32_t(u - ws * a.np);
+#pragma unroll
+                for (int e = 0; e < 36; ++e) m[e] = src[uint32_t(e) * nu];
+            } else {
+                const double* src = a.phi + (u * NCH + ch) * 36;
+#pragma unroll
+                for (int e = 0; e < 36; ++e) m[e] = src[e];
+            }
+            lft_apply(p, m);
+        }
     }
+    // the starts and the banks; with polish chunks, the warm-up bank runs chunk c + kp from c's
     const int r0 = chain_row0<M>(ch);
     const int64_t B4 = 4 * a.C;
     auto put = [&](T* P, int64_t stride, int64_t col, const double (&q)[3][3]) {
@@ -1467,26 +1513,27 @@ __global__ __launch_bounds__(kBlock) void stream_lft_start_kernel(const StreamAr
             P[(r0 + 2) * stride + col] = T(q[1][1]);
         }
     };
-    // chunk c's start; with polish chunks, the warm-up bank runs chunk c + kp from it
-    if (c + a.kp < a.C) put(static_cast<T*>(a.wP), a.C, c + a.kp, p);
-    if (c < a.kp) put(static_cast<T*>(a.wP), a.C, c, ph);
-    const T* hx = static_cast<const T*>(a.hx);
-    const int32_t hst = a.hstatus[0];
 #pragma unroll
-    for (int k = 0; k < 3; ++k)
-        if (k < ns) static_cast<T*>(a.wx)[chain_state<M>(ch, k) * a.C + c] = hx[chain_state<M>(ch, k)];
-    if (ch == 0) a.wst[c] = hst;
-    if (a.kp == 0) {
-        put(static_cast<T*>(a.mP), B4, c, p);
+    for (int r = 0; r < kStartMaxG; ++r) {
+        const int64_t c = ct + r;
+        if (c >= ce) break;
+        if (c + a.kp < a.C) put(static_cast<T*>(a.wP), a.C, c + a.kp, ps[r]);
+        if (c < a.kp) put(static_cast<T*>(a.wP), a.C, c, ph);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int k = 0; k < 3; ++k)
+            if (k < ns) static_cast<T*>(a.wx)[chain_state<M>(ch, k) * a.C + c] = gx[k];
+        if (ch == 0) a.wst[c] = hst;
+        if (a.kp == 0) {
+            put(static_cast<T*>(a.mP), B4, c, ps[r]);
 #pragma unroll
-            for (int k = 0; k < 3; ++k)
-                if (k < ns) {
-                    const T g = hx[chain_state<M>(ch, k)];
-                    static_cast<T*>(a.mx)[chain_state<M>(ch, k) * B4 + q * a.C + c] = (q > 0 && k == q - 1) ? g + T(a.delta) : g;
-                }
-        if (ch == 0) a.mst[c] = hst;
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    if (k < ns)
+                        static_cast<T*>(a.mx)[chain_state<M>(ch, k) * B4 + q * a.C + c] =
+                            (q > 0 && k == q - 1) ? gx[k] + T(a.delta) : gx[k];
+            if (ch == 0) a.mst[c] = hst;
+        }
     }
 }
 
@@ -2219,11 +2266,14 @@ void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
             stream_starts_kernel<T, M><<<g, kScanTile, 0, stream>>>(a);
             break;
         }
-        case kStreamPhaseLftMaps: stream_lft_maps_kernel<T, M><<<grid(a.C * a.np * NCH * kGroup), kBlock, 0, stream>>>(a); break;
+        case kStreamPhaseLftMaps: stream_lft_maps_kernel<T, M><<<grid(a.C * a.np * NCH), kBlock, 0, stream>>>(a); break;
         case kStreamPhaseLftStart: {
-            const int64_t bc = a.G > 0 ? a.G : kBlock;
-            const size_t lds = a.G > 0 ? size_t(a.G + a.iters) * a.np * 36 * sizeof(double) : 0;
-            stream_lft_start_kernel<T, M><<<dim3(unsigned((a.C + bc - 1) / bc), NCH), kBlock, lds, stream>>>(a);
+            const int64_t bc = a.g > 0 ? a.G : kBlock;
+            const unsigned threads = a.g > 0 ? unsigned((a.G + a.g - 1) / a.g) : unsigned(kBlock);
+            const size_t lds = a.g > 0 ? size_t(a.G + a.iters) * a.np * 36 * sizeof(double) : 0;
+            const dim3 g(unsigned((a.C + bc - 1) / bc), NCH);
+            if (a.g > 0) stream_lft_start_kernel<T, M, true><<<g, threads, lds, stream>>>(a);
+            else stream_lft_start_kernel<T, M, false><<<g, threads, 0, stream>>>(a);
             break;
         }
         case 5: stream_finish_kernel<T, M><<<1, 1024, 0, stream>>>(a); break;
