@@ -209,12 +209,42 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
                               'link_gbs': (h2d + d2h) / pel / 1e9,
                               'note': 'BatchedKF.run_host: time chunks on 3 streams, H2D | launch | D2H overlapped'}}
 
+    def probe(reps):
+        """The access pattern's ceiling on these very buffers (tools/probes/pattern_probe.hip:
+        the block kernel's loads and stores through the same ring, the arithmetic reduced to a
+        sum): GB/s of its stream bytes, HIP events on the engine's stream.  None without the
+        probe library (a diagnostic, built by __graft_entry__.build())."""
+        import ctypes
+        path = os.path.join(ROOT, 'tools', 'probes', 'libpattern_probe.so')
+        if not os.path.exists(path):
+            return None
+        lib = ctypes.CDLL(path)
+        lib.kfprobe_pattern.restype = ctypes.c_int
+        lib.kfprobe_pattern.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4 + \
+            [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        stream = torch.cuda.current_stream(dev)
+        run = lambda: lib.kfprobe_pattern(d, int(cfg['dtype'] == 'f64'), u.data_ptr(), z.data_ptr(), traj.data_ptr(),
+                                          logdet.data_ptr(), B, T, k, ctypes.c_void_p(stream.cuda_stream))
+        for _ in range(3):
+            if run() != 0:
+                return None
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for s, e in ev:
+            s.record(stream)
+            run()
+            e.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+        w = 8 if cfg['dtype'] == 'f64' else 4
+        nbytes = B * (T * (d + 2 * d + 1) * w + (T // k) * d * w)
+        return {'gbs': nbytes / (ms * 1e-3) / 1e9, 'ms': ms, 'bytes': nbytes}
+
     d = 2 if cfg['model'] == 'cv2' else 3
     bytes_launch, bytes_step = algorithmic_bytes(cfg)
     kernel = 'cv_block_kernel' if block_kernel_in_use() else 'cv_run_kernel'
     return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_step, kernel=kernel,
                 traffic=load_traffic(cfg_id) if kernel == 'cv_block_kernel' else None, cpu=cpu,
-                gather=gather_payload, kf=kf, pcie=pcie,
+                gather=gather_payload, kf=kf, pcie=pcie, probe=probe,
                 desc=f"BASELINE config {cfg_id}: {cfg['model']} ({2 * d}-state/{d}-meas), {cfg['dtype']}, "
                      f"B={B} filters/GPU, T={T}, dt={dt}, GPS update every {k} step(s)",
                 extra={'filters_per_gpu': B, 'time_steps_per_launch': T, 'update_every': k})
@@ -657,6 +687,16 @@ def main():
                                'algorithmic_bytes_per_step': w['bytes_per_unit']}
             if w.get('roofline_note'):
                 rec['roofline']['note'] = w['roofline_note']
+            if world == 1 and w.get('probe') and args.ablate == 'none':
+                # the same access pattern without the filter arithmetic, on the same buffers, right
+                # after the timed region: the ceiling this box's HBM placement gives the pattern
+                pr = w['probe'](max(args.steps, 5))
+                if pr:
+                    rec['roofline']['pattern_ceiling'] = {
+                        'achieved': pr['gbs'], 'unit': 'GB/s', 'probe_ms': pr['ms'],
+                        'frac': achieved / pr['gbs'],
+                        'probe': 'tools/probes/pattern_probe.hip: the bench kernel\'s loads and stores (same '
+                                 'ring, same rows, same buffers) with the arithmetic reduced to a sum'}
         else:
             rec['roofline'] = {'bound': 'hbm', 'achieved': None, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': None,
                                'traffic': None, 'kernel': w['kernel'], 'kernel_ms': kern_ms,
