@@ -380,6 +380,11 @@ def log_workload(cfg, args, rank, world, dev):
     stream = ingest.ingest_arrays(gcols, icols, device=dev.index)
     torch.cuda.synchronize(dev)
     t2 = time.perf_counter()
+    # the first call also loads the library's code objects and warms torch's allocator: the
+    # ingest itself is the second call's time (both reported)
+    stream = ingest.ingest_arrays(gcols, icols, device=dev.index)
+    torch.cuda.synchronize(dev)
+    t3 = time.perf_counter()
     N = len(stream)
     first = int(torch.nonzero(stream.etype == _lib.KF_EVENT_GPS)[0, 0])
     T = N - first
@@ -463,7 +468,7 @@ def log_workload(cfg, args, rank, world, dev):
                          f'covariance warm-up + affine state maps composed on the device, checked, sequential '
                          f"fallback); synthetic log with the reference log's shape",
                     extra={'events': N, 'events_filtered': T, 'csv_parse_ms': (t1 - t0) * 1e3,
-                           'kf_ingest_ms': (t2 - t1) * 1e3, 'filters': 1, 'stream_check': stream_check})
+                           'kf_ingest_ms': (t3 - t2) * 1e3, 'kf_ingest_first_call_ms': (t2 - t1) * 1e3, 'filters': 1, 'stream_check': stream_check})
     return dict(step=step, units=T, bytes=per_event * T, bytes_per_unit=per_event, kernel='ref_chain_kernel',
                 traffic=None, cpu=cpu, gather=None, kf=kf,
                 roofline_note='one filter: one wave whose per-event dependency chain bounds the rate (8 lanes, '
@@ -472,7 +477,7 @@ def log_workload(cfg, args, rank, world, dev):
                      f'whole drive log, {N} merged events ({stream.n_fixes} fixes + {stream.n_imu} IMU at 200 Hz), '
                      f'f64; synthetic log with the reference log\'s shape',
                 extra={'events': N, 'events_filtered': T, 'csv_parse_ms': (t1 - t0) * 1e3,
-                       'kf_ingest_ms': (t2 - t1) * 1e3, 'filters': 1})
+                       'kf_ingest_ms': (t3 - t2) * 1e3, 'kf_ingest_first_call_ms': (t2 - t1) * 1e3, 'filters': 1})
 
 
 def bf_workload(cfg, args, rank, world, dev):

@@ -162,8 +162,18 @@ __global__ void bias_kernel(const IngestArgs a) {
     const unsigned long long f = a.first[0];
     const int64_t cnt = static_cast<int64_t>(f < static_cast<unsigned long long>(a.n_imu) ? f : a.n_imu);
     const double* col = a.imu + (5 + k) * a.ld_imu;
+    // rows added one after another (NumPy's axis-0 order), their loads issued 32 at a time (a
+    // load-add loop waited one memory latency per row: 0.5 ms for the config 1 log)
     double s = 0.0;
-    for (int64_t r = 0; r < cnt; ++r) s += col[r];
+    int64_t r = 0;
+    for (; r + 32 <= cnt; r += 32) {
+        double v[32];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) v[j] = col[r + j];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) s += v[j];
+    }
+    for (; r < cnt; ++r) s += col[r];
     a.bias[k] = s / static_cast<double>(cnt);
 }
 

@@ -898,6 +898,7 @@ __global__ __launch_bounds__(kBlock) void stream_init_kernel(const StreamArgs a)
         a.check->bad = 0;
         a.check->cov_gap = 0.0;
         a.check->state_gap = 0.0;
+        a.check->done = 0;
     }
     if (c >= a.C) return;
     const T* hx = static_cast<const T*>(a.hx);
@@ -1156,10 +1157,13 @@ __global__ __launch_bounds__(kScanTile) void stream_starts_kernel(const StreamAr
     StreamCheck* k = a.check;
     if (!all_fin) atomicOr(&k->bad, kStreamBadStart);
     if (!a.xend) return;  // a final pass follows: phase 5 decides
-    __threadfence();  // release this block's stores and flags before the count
+    // Everything the verdict reads from this launch travels by device-scope atomics (bad here,
+    // cov_gap and bad from the map pass and the end state from earlier launches), so no fence:
+    // the wave only drains its own atomic before it counts itself (an agent-scope release per
+    // block wrote its XCD's L2 back and cost more than the kernel's work)
+    __builtin_amdgcn_s_waitcnt(0);
     const int blocks = int(gridDim.x * gridDim.y);
     if (atomicAdd(&k->done, 1) != blocks - 1) return;
-    __threadfence();  // acquire: every block's stores and flags are visible
     const int bad = atomicOr(&k->bad, 0);
     const double cov_gap = __longlong_as_double(atomicOr(reinterpret_cast<unsigned long long*>(&k->cov_gap), 0ull));
     k->state_gap = bad & kStreamBadStart ? __builtin_inf() : __builtin_nan("");
