@@ -856,19 +856,22 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
 // use of run_kalman_filter_full, kf_workers.py:623-728, is one filter over a whole drive log).
 // The stream is cut into C chunks of L events that run as filters of the chain kernel:
 //  * the covariance recursion does not depend on the measurements and forgets its start, so
-//    chunk c's start covariance is the warm-up bank's: chunk c run over the W events before it
-//    from the handle's state (chunks within W of the stream start begin at event 0: exact);
+//    chunk c's start covariance is the handle's P carried over the chunks before it by their
+//    linear-fractional covariance maps (phases 6-7; or an event warm-up over the W events before
+//    it, the warm-up bank);
 //  * given the gains, the state recursion is affine (the IMU pseudo-measurement is built from
 //    the predicted state, kf_workers.py:698-706, which keeps it affine), and block-diagonal
-//    over the axis chains: the map bank runs each chunk from a guess and from three perturbed
-//    guesses (one per chain component), giving x_end = A x_start + b per chunk and chain;
-//  * the maps are composed from the handle's state (segment products, then the segments in
-//    order) into every chunk's true start, and the final bank runs the chunks from them with
-//    the records;
-//  * checks: each warm-up covariance equals the previous chunk's end covariance, each chunk's
-//    final end state its successor's start, no chunk filter failed.  Only then does the
-//    handle take the last chunk's end state; otherwise the sequential chain kernel, launched
-//    after these with skip = &check.ok, runs the stream as one filter and rewrites every record.
+//    over the axis chains: the map pass runs each chunk from a guess and from three perturbed
+//    guesses (one per chain component; the four variants share one lane and one covariance),
+//    its epilogue giving x_end = A x_start + b per chunk and chain;
+//  * the maps are composed from the handle's state by a parallel scan (phases 2-4) into every
+//    chunk's true start; the records are the map pass's, the trajectory evaluated at the true
+//    starts (phase 8), or a final pass runs the chunks from them (KFMI_STREAM_FINAL=1);
+//  * checks: each chunk's start covariance equals the previous chunk's end covariance, the
+//    starts and the end state are finite (a final pass: each chunk's end state is its
+//    successor's start), no chunk filter failed.  Only then does the handle take the end
+//    state; otherwise the sequential chain kernel, launched after these with skip = &check.ok,
+//    runs the stream as one filter and rewrites every record.
 // ------------------------------------------------------------------------------------
 template <class M>
 __device__ __forceinline__ int chain_state(int a, int q) {  // chain a (pva chains first), component q; -1: none

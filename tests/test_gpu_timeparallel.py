@@ -190,3 +190,25 @@ def test_run_full_stream_parallel_matches_single_filter():
     for u, v in zip(a[1:4], b[1:4]):
         assert _rel(u, v) <= 1e-9
     assert a[4] == b[4]
+
+
+@pytest.mark.parametrize('warmup', [-1, 1024])
+def test_repeated_runs_on_one_handle(warmup):
+    """The check words (verdict, gaps, the scan's block counter) are re-initialised by every
+    call: a second run_stream on the same handle (its workspace reused) passes its checks and
+    gives the same records (covariance maps, and an event warm-up)."""
+    et, dt, pay, x0 = _stream(20000, seed=17)
+    dev = torch.device('cuda', 0)
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    P0b = ref15.to_blocks(ref15.P0)[:, None]
+    outs = []
+    for _ in range(2):
+        kf.set_state(x0[:, None], P0b)
+        tr, ld, _, _ = kf.run_stream(torch.as_tensor(et, device=dev), torch.as_tensor(dt, device=dev),
+                                     torch.as_tensor(pay, device=dev), chunk=200, warmup=warmup)
+        chk = kf.stream_check()
+        assert chk['ok'] and chk['chunks'] > 1, chk
+        outs.append((tr.cpu().numpy(), ld.cpu().numpy()))
+    kf.close()
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
