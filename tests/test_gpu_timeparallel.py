@@ -192,7 +192,7 @@ def test_run_full_stream_parallel_matches_single_filter():
     assert a[4] == b[4]
 
 
-@pytest.mark.parametrize('warmup', [-1, 1024])
+@pytest.mark.parametrize('warmup', [-1, 2048])
 def test_repeated_runs_on_one_handle(warmup):
     """The check words (verdict, gaps, the scan's block counter) are re-initialised by every
     call: a second run_stream on the same handle (its workspace reused) passes its checks and
