@@ -399,11 +399,11 @@ def log_workload(cfg, args, rank, world, dev):
     traj = kf.empty(T, 6, 1)
     logdet = kf.empty(T, 1)
     prev0 = float(t_ev[0])
-    L = _lib.lib()
 
     stream_check = {}
 
     def step():
+        L = _lib.lib()  # looked up per step: tools/ab_inproc.py swaps libraries between launches
         kf.reset(x0)
         _lib.check(L.kf_events_dt(T, _ptr(t_ev), _ptr(e_ev), prev0, _lib.KF_DT_FULL, _ptr(dt), _ptr(et),
                                   kf._stream()))

@@ -732,14 +732,19 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
 #pragma unroll
             for (int v = 0; v < NV; ++v)
                 stv(r_str, (ue * uint32_t(M::NTRAJ * sizeof(T)) + col_tr + uint32_t(v) * vstep_tr) | m_tr, x[v][0]);
+            // absent records: skipped by a wave-uniform branch (a store to a zero-length
+            // descriptor is dropped, but it is still issued)
+            if (a.cov) {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) stv(r_scv, (ue * uint32_t(M::NBLK * sizeof(T)) + col_cv[k]) | (col_cv[k] & kDropOffset), P[k]);
+                for (int k = 0; k < 6; ++k)
+                    stv(r_scv, (ue * uint32_t(M::NBLK * sizeof(T)) + col_cv[k]) | (col_cv[k] & kDropOffset), P[k]);
+            }
             if (need_ld) {
                 const T ld = group_sum(live ? chain_log_det(P) : T(0));
                 st = (ld == ld) ? st : kNotSpd;
                 stv(r_sld, (ue * uint32_t(sizeof(T))) | m_ld, ld);
             }
-            __builtin_amdgcn_raw_buffer_store_b8(applied ? uint8_t(1) : uint8_t(0), r_sup, ue | m_ld, 0, 0);
+            if (a.updated) __builtin_amdgcn_raw_buffer_store_b8(applied ? uint8_t(1) : uint8_t(0), r_sup, ue | m_ld, 0, 0);
         } else {
             stv(span_rsrc(a.traj, int64_t(t) * M::NTRAJ, rb, M::NTRAJ), v_tr, x[0][0]);
             {
