@@ -77,6 +77,22 @@ int main(int argc, char** argv) {
             for (int m = 0; m < 3; ++m) timeit(names[m], rep, pin[m], pout[m]);
         return 0;
     }
+    if (mode == 3) {
+        // order check: one arena allocated FIRST, then two plain buffers, then each timed 3x
+        char* ar = nullptr;
+        CK(hipMalloc((void**)&ar, a2 + nout));
+        double *pin = nullptr, *pout = nullptr;
+        CK(hipMalloc(&pin, nin));
+        CK(hipMalloc(&pout, nout));
+        CK(hipMemset(ar, 0, a2 + nout));
+        CK(hipMemset(pin, 0, nin));
+        CK(hipMemset(pout, 0, nout));
+        for (int rep = 0; rep < 3; ++rep) {
+            timeit("arena1st", rep, (const double*)ar, (double*)(ar + a2));
+            timeit("plain2nd", rep, pin, pout);
+        }
+        return 0;
+    }
     if (mode == 2) {
         // walk one arena through the device memory: time it, free it, keep an 8 GiB spacer, repeat
         for (int step = 0; step < 12; ++step) {
