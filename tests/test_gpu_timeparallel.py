@@ -212,3 +212,17 @@ def test_repeated_runs_on_one_handle(warmup):
     kf.close()
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
+
+
+def test_many_chunks_multi_round_scan():
+    """More chunks than one scan round holds (256 x 256 tiles): 1.1M events in chunks of 16 give
+    68,750 chunks, so the tile-start scan carries over two rounds; records, final state and
+    covariance equal the single filter's."""
+    et, dt, pay, x0 = _stream(1_100_000, seed=23, skips=100)
+    seq = _sequential(et, dt, pay, x0)
+    par = _parallel(et, dt, pay, x0, chunk=16)
+    chk = ref15.parallel_check
+    assert chk['ok'] and chk['chunks'] > 65536, chk
+    for a, b in zip(par, seq):
+        assert a.shape == b.shape
+        assert _rel(a, b) <= 1e-9
