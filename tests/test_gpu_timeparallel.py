@@ -226,3 +226,40 @@ def test_many_chunks_multi_round_scan():
     for a, b in zip(par, seq):
         assert a.shape == b.shape
         assert _rel(a, b) <= 1e-9
+
+
+def test_stream_run_replays_as_a_hip_graph():
+    """kf_run_stream's launches (after a first eager call has sized the workspace) capture into a
+    hipGraph as they are — no host synchronisation or allocation — and the replay gives the
+    eager run's records and final state."""
+    et, dt, pay, x0 = _stream(40000, seed=29, skips=30)
+    dev = torch.device('cuda', 0)
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    P0b = torch.as_tensor(ref15.to_blocks(ref15.P0)[:, None], device=dev)
+    x0d = torch.as_tensor(x0[:, None], device=dev)
+    etd, dtd, payd = (torch.as_tensor(v, device=dev) for v in (et, dt, pay))
+    T = len(et)
+    tr, ld = kf.empty(T, 6, 1), kf.empty(T, 1)
+
+    def run():
+        kf.set_state(x0d, P0b)
+        out = kf.run_stream(etd, dtd, payd)
+        tr.copy_(out[0])
+        ld.copy_(out[1])
+
+    run()
+    torch.cuda.synchronize()
+    eager = (tr.cpu().numpy().copy(), ld.cpu().numpy().copy(), kf.state()[0].cpu().numpy())
+    assert kf.stream_check()['ok']
+    tr.zero_()
+    ld.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        run()
+    g.replay()
+    torch.cuda.synchronize()
+    replay = (tr.cpu().numpy(), ld.cpu().numpy(), kf.state()[0].cpu().numpy())
+    for a, b in zip(replay, eager):
+        np.testing.assert_array_equal(a, b)
+    assert kf.stream_check()['ok']
+    kf.close()
