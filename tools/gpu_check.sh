@@ -22,7 +22,7 @@ step() {
 }
 cd "$ROOT"
 rocm-smi --showproductname > "$OUT/device.txt" 2>&1 || true
-step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
+step pytest_gpu 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py "$@"
 cd /tmp
