@@ -589,9 +589,9 @@ def bf_workload(cfg, args, rank, world, dev):
 
     if search:
         from kfmi.ref15 import search_level_bytes
-        # every stored node (the C(n-1, k) subsets of size k < n without the last candidate) is
-        # written once and read once as a parent
-        lvl = sum(search_level_bytes(math.comb(n - 1, k), 'f64') for k in range(1, n))
+        # every stored node (the C(n-2, k) subsets of size k < n whose largest candidate is
+        # <= n - 3) is written once and read once as a parent
+        lvl = sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in range(1, n))
         return dict(step=step, units=total_steps, bytes=2 * lvl, bytes_per_unit=2 * lvl / total_combos,
                     kernel='ref15_search_pm_kernel+ref15_search_cm_kernel (the 25 level launches of one search)', traffic=load_traffic('bf'), cpu=cpu, gather=None, kf=kf, combos=total_combos,
                     roofline_note='level-buffer bytes only (each stored prefix filter written and read once); the '

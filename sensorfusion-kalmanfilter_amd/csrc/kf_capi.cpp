@@ -837,14 +837,16 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
     const int kf_max = k_max - k_base < n ? k_max - k_base : n;  // free levels searched
     const uint64_t* binom = binom_table();
     auto C = [&](int a, int b) { return binom[a * (kMaxComboEvents + 1) + b]; };
-    // Free levels 1 .. kf_max - 1 are stored, and of each only the subsets without the last
-    // candidate (the others have no children): the colex ranks below C(n - 1, k).
+    // Free levels 1 .. kf_max - 1 are stored, and of each only the subsets whose largest free
+    // candidate is <= n - 3 (the colex ranks below C(n - 2, k)): a subset holding candidate n - 1
+    // has no children, and one holding n - 2 (but not n - 1) has the single child that adds
+    // n - 1, which the launch creating it scores from registers (Ref15SearchArgs::tail).
     uint64_t widest = 0;
-    for (int k = 1; k < kf_max; ++k) widest = C(n - 1, k) > widest ? C(n - 1, k) : widest;
-    for (int k = 1; k <= kf_max; ++k)
-        if (C(n - 1, k - 1) >= (1ull << 28))
+    for (int k = 1; k < kf_max; ++k) widest = n >= 2 && C(n - 2, k) > widest ? C(n - 2, k) : widest;
+    for (int k = 2; k <= kf_max; ++k)
+        if (n >= 2 && C(n - 2, k - 1) >= (1ull << 28))
             return fail(KF_EINVAL, "kf_search_combos: level %d has C(%d, %d) = %llu parents (limit 2^28); lower k_max",
-                        k, n - 1, k - 1, static_cast<unsigned long long>(C(n - 1, k - 1)));
+                        k, n - 2, k - 1, static_cast<unsigned long long>(C(n - 2, k - 1)));
     const int esz = static_cast<int>(elem(h));
     const size_t head = 4096;  // best[65], n_acc[65]
     const size_t level = widest ? static_cast<size_t>(kfmi::search_level_bytes(widest, esz)) : 0;
@@ -878,7 +880,7 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.k_base = k_base;
         a.root_mask = fixed_mask;
         a.ev_all = reinterpret_cast<const double*>(ws);
-        a.n_par = k == 1 ? 1 : C(n - 1, k - 1);  // the parents with children
+        a.n_par = k == 1 ? 1 : C(n - 2, k - 1);  // the stored parents (n >= 2 when k >= 2)
         a.n_child = C(n, k);
         a.ev = reinterpret_cast<const double*>(ws) + 11 * n_fixed;
         a.binom = reinterpret_cast<const uint64_t*>(ws + kWsEvents);
@@ -892,8 +894,12 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.best = d_best;
         a.n_acc = d_acc;
         a.subset_max = subset_max;
-        e = kfmi::launch_ref15_search(h->dtype == KF_F64, a, search_child_major(a.n_par), st);
-        if (e != hipSuccess) return hip_fail(e, "kf_search_combos: level launch");
+        a.tail = k < kf_max;
+        // a level without stored parents was scored whole by the previous launch's tail
+        if (a.n_par) {
+            e = kfmi::launch_ref15_search(h->dtype == KF_F64, a, search_child_major(a.n_par), st);
+            if (e != hipSuccess) return hip_fail(e, "kf_search_combos: level launch");
+        }
         last = k_base + k;
         if (!exhaustive) {  // the reference stops at the first size with an acceptable subset
             // (the first launch also scores the fixed root itself, size k_base)

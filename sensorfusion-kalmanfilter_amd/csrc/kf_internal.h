@@ -189,7 +189,7 @@ struct Ref15SearchArgs {
     int k_base;              // popcount(root_mask): level k holds subsets of size k_base + k
     uint64_t root_mask;      // the fixed candidates every subset of this search contains
     const double* ev_all;    // device [shift + n_events][11]
-    uint64_t n_par;          // C(n, k - 1) parents, one lane each
+    uint64_t n_par;          // C(n - 2, k - 1) stored parents (largest event <= n - 3), one lane each
     uint64_t n_child;        // C(n, k)
     const double* ev;        // device [n_events][11]: the free candidates (t, type, payload[9])
     const uint64_t* binom;   // device [65][65]
@@ -203,6 +203,8 @@ struct Ref15SearchArgs {
     uint64_t* best;          // device [65]: per subset size, max over accepted subsets of bitrev(mask)
     uint64_t* n_acc;         // device [65]: per subset size, number of accepted subsets
     void* subset_max;        // device [2^n] T: every subset's max log-det by mask, or nullptr
+    int tail;                // level k + 1 is searched: a child holding event n - 2 is not stored, its
+                             // only child (plus event n - 1) is scored by this launch (size k + 1)
 };
 
 constexpr int kSearchRows = 28;  // T rows of a search node

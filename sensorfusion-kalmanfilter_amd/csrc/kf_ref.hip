@@ -1836,15 +1836,22 @@ __device__ __forceinline__ void search_score(const Ref15SearchArgs& a, uint64_t 
     }
 }
 
-// Child j (> the parent's largest event) of node `par`, colex rank c at level a.k: its filter
-// (stored when a.child is set and the child has children), its max log-det with the worker's
-// final predict, and the acceptance test folded into (best, cnt).  Chains::event runs chain by
-// chain (each chain's predict and update touch only that chain); the record's log-det and the
-// final predict's are accumulated in Chains::logdet's block order, so the numbers are
-// kf_eval_combos's.
+// Event j applied to a node (covariance Pin, running max log-det run_in, last time prev_in):
+// the child's covariance, running max and time, and its max log-det with the worker's final
+// predict (fmax; the final predict runs on a copy, so P stays the child's covariance).
+// Chains::event runs chain by chain (each chain's predict and update touch only that chain);
+// the record's log-det and the final predict's are accumulated in Chains::logdet's block order,
+// so the numbers are kf_eval_combos's.
 template <typename T>
-__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const SearchNode<T>& par, int j, uint64_t c,
-                                             uint64_t& best, uint64_t& cnt) {
+struct SearchStep {
+    T P[27];
+    T run, fmax;
+    double prev;
+};
+
+template <typename T>
+__device__ __forceinline__ void search_apply(const Ref15SearchArgs& a, const T (&Pin)[27], T run_in, double prev_in,
+                                             int j, SearchStep<T>& o) {
     using C15 = Chains<T, M15>;
     const T qpva[3] = {T(kQPos), T(kQVel), T(kQAcc)};
     const T qaw[2] = {T(kQAtt), T(kQRate)};
@@ -1853,25 +1860,20 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
     const T Ra[3] = {T(kRAtt), T(0), T(kRRate)};
     const double* e = a.ev + j * 11;
     const int type = int(e[1]);
-    const uint64_t cmask = par.mask | (uint64_t(1) << (j + a.shift));
-    const double dtd = e[0] - par.prev;
+    const double dtd = e[0] - prev_in;
     const bool step = dtd >= 0.0;  // kf_workers.py:38-40: a negative dt is skipped, time unchanged
     const T dt = T(dtd);
-    const double cprev = step ? e[0] : par.prev;
-    const bool final_predict = cprev < a.target_end - 1e-8;  // kf_workers.py:74-82
-    const T dte = T(a.target_end - cprev);
-    // a subset holding event n - 1 has no children and is not stored
-    char* cb = (a.child && j < a.n_events - 1) ? level_block<T>(a.child, c) : nullptr;
-    const uint32_t cl = uint32_t(c) & 63u;
+    o.prev = step ? e[0] : prev_in;
+    const bool final_predict = o.prev < a.target_end - 1e-8;  // kf_workers.py:74-82
+    const T dte = T(a.target_end - o.prev);
     LogdetAcc<T> rec, fin;
     bool ok = true;
 #pragma unroll
     for (int ch = 0; ch < M15::NP; ++ch) {
-        T xb[3], Pb[6];
+        // the state is not carried (SearchNode): constant zeros, dead code after inlining
+        T xb[3] = {T(0), T(0), T(0)}, Pb[6];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) xb[i] = par.x[M15::pva(ch, i)];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) Pb[i] = par.P[6 * ch + i];
+        for (int i = 0; i < 6; ++i) Pb[i] = Pin[6 * ch + i];
         if (step) {
             C15::template chain_predict<3>(xb, Pb, dt, qpva);
             if (type == kGps) {
@@ -1885,21 +1887,17 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
                 ok = sel_update<3, 3, true, T, kRefNewton, true>(xb, Pb, zb, Rp) && ok;
             }
         }
-        if (cb) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) *level_row<T>(cb, cl, 6 * ch + i) = Pb[i];
-        }
+        for (int i = 0; i < 6; ++i) o.P[6 * ch + i] = Pb[i];
         rec.add_pva(Pb, ch);
         if (final_predict) C15::template chain_predict<3>(xb, Pb, dte, qpva);
         fin.add_pva(Pb, ch);
     }
 #pragma unroll
     for (int ch = 0; ch < M15::NA; ++ch) {
-        T xa[2], Pa[3];
+        T xa[2] = {T(0), T(0)}, Pa[3];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) xa[i] = par.x[M15::aw(ch, i)];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) Pa[i] = par.P[6 * M15::NP + 3 * ch + i];
+        for (int i = 0; i < 3; ++i) Pa[i] = Pin[6 * M15::NP + 3 * ch + i];
         if (step) {
             C15::template chain_predict<2>(xa, Pa, dt, qaw);
             if (type != kGps) {  // a GPS fix updates the pva chains only
@@ -1907,31 +1905,49 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
                 ok = sel_update<2, 2, true, T, kRefNewton, true>(xa, Pa, za, Ra) && ok;
             }
         }
-        if (cb) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, 6 * M15::NP + 3 * ch + i) = Pa[i];
-        }
+        for (int i = 0; i < 3; ++i) o.P[6 * M15::NP + 3 * ch + i] = Pa[i];
         rec.add_aw(Pa);
         if (final_predict) C15::template chain_predict<2>(xa, Pa, dte, qaw);
         fin.add_aw(Pa);
     }
-    T crun = par.run;
+    o.run = run_in;
     if (step) {
         const T ld = rec.finish();
-        crun = ld > par.run ? ld : par.run;
-        crun = ok ? crun : quiet_nan<T>();  // a failed filter (kf_eval_combos: KF_ENOTSPD)
+        o.run = ld > run_in ? ld : run_in;
+        o.run = ok ? o.run : quiet_nan<T>();  // a failed filter (kf_eval_combos: KF_ENOTSPD)
     }
-    T fmax = crun;
+    o.fmax = o.run;
     if (final_predict) {
         const T ld = fin.finish();
-        fmax = ld > crun ? ld : crun;
+        o.fmax = ld > o.run ? ld : o.run;
     }
-    if (cb) {
-        *level_row<T>(cb, cl, 27) = crun;
-        *level_tail<T>(cb, cl, 0) = cprev;
+}
+
+// Child j (> the parent's largest event) of node `par`, colex rank c at level a.k: scored into
+// (best, cnt), and stored when a.child is set and the child has stored children (largest event
+// <= n - 3).  With a.tail, the child holding event n - 2 is not stored: its only child (it plus
+// event n - 1, level k + 1) is evaluated here from the registers and scored into (best1, cnt1).
+template <typename T>
+__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const SearchNode<T>& par, int j, uint64_t c,
+                                             uint64_t& best, uint64_t& cnt, uint64_t& best1, uint64_t& cnt1) {
+    SearchStep<T> s;
+    search_apply<T>(a, par.P, par.run, par.prev, j, s);
+    const uint64_t cmask = par.mask | (uint64_t(1) << (j + a.shift));
+    search_score(a, cmask, s.fmax, best, cnt);
+    if (a.child && j < a.n_events - 2) {
+        char* cb = level_block<T>(a.child, c);
+        const uint32_t cl = uint32_t(c) & 63u;
+#pragma unroll
+        for (int i = 0; i < 27; ++i) *level_row<T>(cb, cl, i) = s.P[i];
+        *level_row<T>(cb, cl, 27) = s.run;
+        *level_tail<T>(cb, cl, 0) = s.prev;
         *level_tail<T>(cb, cl, 1) = __builtin_bit_cast(double, cmask);
+    } else if (a.tail && j == a.n_events - 2) {  // wave-uniform (j is)
+        SearchStep<T> g;
+        search_apply<T>(a, s.P, s.run, s.prev, j + 1, g);
+        search_score(a, cmask | (uint64_t(1) << (j + 1 + a.shift)), g.fmax, best1, cnt1);
     }
-    search_score(a, cmask, fmax, best, cnt);
 }
 
 // one atomic pair per wave, and only from waves with an accepted subset; k = local level
@@ -1964,12 +1980,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     }
     const int m = par.max_event(a.shift);
     const int j0 = wave_uniform(m) + 1;  // colex order: the first lane holds the smallest max
-    uint64_t best = 0, cnt = 0;
+    uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0;
     for (int j = j0; j < a.n_events; ++j) {
         if (j <= m) continue;
-        search_child<T>(a, par, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt);
+        search_child<T>(a, par, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt, best1, cnt1);
     }
     search_publish(a, a.k, best, cnt);
+    if (a.tail) search_publish(a, a.k + 1, best1, cnt1);
 }
 
 // Child-major: one wave per (parent block of 64, child event) work item, one child per lane,
@@ -1996,7 +2013,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
         const uint64_t b1 = k == 1 ? 1 : (binom(v + 1, k - 1) + 63) / 64;
         nb = b1 - b0;
         const uint64_t span = nb * uint64_t(n - 1 - v);
-        if (item < start + span || v >= n - 2) break;
+        if (item < start + span || v >= n - 3) break;
         start += span;
     }
     const uint64_t r = item - start;
@@ -2014,9 +2031,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
     } else {
         par.load(a.par, p);
     }
-    uint64_t best = 0, cnt = 0;
-    if (par.max_event(a.shift) < j) search_child<T>(a, par, j, p + binom(j, k), best, cnt);
+    uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0;
+    if (par.max_event(a.shift) < j) search_child<T>(a, par, j, p + binom(j, k), best, cnt, best1, cnt1);
     search_publish(a, a.k, best, cnt);
+    if (a.tail) search_publish(a, a.k + 1, best1, cnt1);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2343,7 +2361,7 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
         if (k == 1) {
             items = uint64_t(n);
         } else {
-            for (int v = k - 2; v <= n - 2; ++v) {
+            for (int v = k - 2; v <= n - 3; ++v) {
                 const uint64_t b0 = (C[v * (kMaxEvents + 1) + k - 1] + 63) / 64;
                 const uint64_t b1 = (C[(v + 1) * (kMaxEvents + 1) + k - 1] + 63) / 64;
                 items += (b1 - b0) * uint64_t(n - 1 - v);

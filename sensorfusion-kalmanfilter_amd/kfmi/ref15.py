@@ -518,14 +518,15 @@ def search_level_bytes(nodes, dtype):
 
 def search_levels(n, dtype='f64', mem_bytes=32 << 30):
     """Largest k_max for which kf_search_combos' level buffers (two of the widest stored level:
-    the C(n - 1, k) subsets of size k < k_max without the last candidate) fit in ``mem_bytes``
-    and every level stays below 2^28 parents."""
+    the C(n - 2, k) subsets of size k < k_max whose largest candidate is <= n - 3) fit in
+    ``mem_bytes`` and every level stays below 2^28 stored parents."""
     k_max, widest = 0, 0
     for k in range(1, n + 1):
-        if math.comb(n - 1, k - 1) >= 1 << 28:
-            break
         if k > 1:
-            widest = max(widest, math.comb(n - 1, k - 1))
+            par = math.comb(n - 2, k - 1)
+            if par >= 1 << 28:
+                break
+            widest = max(widest, par)
         if 2 * search_level_bytes(widest, dtype) + 4096 > mem_bytes:
             break
         k_max = k

@@ -151,6 +151,32 @@ def test_search_subset_max_equals_eval_combos(golden_dir, dtype, kernel, monkeyp
 
 
 @pytest.mark.parametrize('kernel', ['cm', 'pm'])
+@pytest.mark.parametrize('n,k_max', [(1, 1), (2, 2), (3, 3), (4, 4), (9, 3), (9, 8), (9, 9)])
+def test_search_small_and_cut_levels(golden_dir, n, k_max, kernel, monkeypatch):
+    """Edge cases of the stored levels: with n <= 3 some levels have no stored parents (scored
+    whole by the previous launch's tail); with k_max < n no subset larger than k_max is scored
+    (the tail stops at k_max).  Every subset up to k_max gets the per-subset kernel's score."""
+    monkeypatch.setenv('KFMI_SEARCH_KERNEL', kernel)
+    cand, ev, init, t0, target = _search_case(golden_dir, n, swap=n > 6)
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    kfound, win, acc, sm = kf.search_combos(ev, init, t0, target, threshold=-1e30, k_max=k_max, exhaustive=True,
+                                            subset_max=True)
+    kf.close()
+    assert kfound == 0 and win is None and int(acc.sum()) == 0
+    sm = sm.cpu().numpy()
+    sizes = np.array([bin(m).count('1') for m in range(1 << n)])
+    assert np.isnan(sm[sizes > k_max]).all() and np.isnan(sm[0])
+    for k in range(1, k_max + 1):
+        combos = list(combinations(range(n), k))
+        kc = kfmi.BatchedKF('ref15', len(combos), 'f64')
+        mx, _, _ = kc.eval_combos(ev, init, t0, target, k, logdets=False)
+        mx = mx.cpu().numpy()
+        kc.close()
+        got = sm[np.array([sum(1 << i for i in c) for c in combos])]
+        assert np.max(np.abs(got - mx) / np.maximum(np.abs(mx), 1.0)) <= 1e-12, k
+
+
+@pytest.mark.parametrize('kernel', ['cm', 'pm'])
 @pytest.mark.parametrize('q', [0.0, 0.01, 0.3, 0.9])
 def test_search_winner_matches_per_subset_search(golden_dir, q, kernel, monkeypatch):
     """The search's winner and per-size accepted counts at thresholds across the distribution of

@@ -66,7 +66,7 @@ def main():
             write = 1024 * sum(w) / (len(w) / n)
             from kfmi.ref15 import search_level_bytes
             import math
-            alg = 2 * sum(search_level_bytes(math.comb(n - 1, k), 'f64') for k in range(1, n))
+            alg = 2 * sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in range(1, n))
             res['configbf'] = {
                 'fetch_bytes_raw': fetch, 'write_bytes_raw': write,
                 'bytes_per_launch': fetch * read_scale + write * write_scale,

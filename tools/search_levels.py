@@ -13,6 +13,6 @@ for k, r in enumerate(last, 1):
     d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
     tot += d
     kind = 'cm' if 'cm_kernel' in r['Kernel_Name'] else 'pm'
-    print(f'{k:3d} {kind} {d:9.1f} us  subsets {math.comb(n, k):9d}  parents {math.comb(n - 1, k - 1) if k > 1 else 1:9d}')
+    print(f'{k:3d} {kind} {d:9.1f} us  subsets {math.comb(n, k):9d}  parents {math.comb(n - 2, k - 1) if k > 1 else 1:9d}')
 span = (int(last[-1]['End_Timestamp']) - int(last[0]['Start_Timestamp'])) / 1e3
 print(f'kernels {tot:.1f} us, span {span:.1f} us')
