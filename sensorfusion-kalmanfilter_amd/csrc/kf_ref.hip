@@ -19,6 +19,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "kf_common.h"
 #include "kf_internal.h"
 
@@ -1836,117 +1839,189 @@ __device__ __forceinline__ void search_score(const Ref15SearchArgs& a, uint64_t 
     }
 }
 
-// Event j applied to a node (covariance Pin, running max log-det run_in, last time prev_in):
-// the child's covariance, running max and time, and its max log-det with the worker's final
-// predict (fmax; the final predict runs on a copy, so P stays the child's covariance).
-// Chains::event runs chain by chain (each chain's predict and update touch only that chain);
-// the record's log-det and the final predict's are accumulated in Chains::logdet's block order,
-// so the numbers are kf_eval_combos's.
-template <typename T>
-struct SearchStep {
-    T P[27];
-    T run, fmax;
-    double prev;
+// Event j applied to a node whose last applied event is at prev_in (kf_workers.py:36-82): a
+// negative dt skips the event and keeps the time; the worker's final predict to target_end runs
+// when the new time is before it.
+struct SearchEvent {
+    const double* e;
+    int type;
+    bool step, final_predict;
+    double dt, dte, prev;  // prev: the time after the event
 };
 
+__device__ __forceinline__ SearchEvent search_event(const Ref15SearchArgs& a, int j, double prev_in) {
+    SearchEvent v;
+    v.e = a.ev + j * 11;
+    v.type = int(v.e[1]);
+    v.dt = v.e[0] - prev_in;
+    v.step = v.dt >= 0.0;  // kf_workers.py:38-40
+    v.prev = v.step ? v.e[0] : prev_in;
+    v.final_predict = v.prev < a.target_end - 1e-8;  // kf_workers.py:74-82
+    v.dte = a.target_end - v.prev;
+    return v;
+}
+
+// One chain of the 15-state filter through one event, Chains::event's operations for that
+// chain (each chain's predict and update touch only that chain); the state is not carried
+// (SearchNode), so xb is constant zeros and the state half is dead code after inlining.
 template <typename T>
-__device__ __forceinline__ void search_apply(const Ref15SearchArgs& a, const T (&Pin)[27], T run_in, double prev_in,
-                                             int j, SearchStep<T>& o) {
+__device__ __forceinline__ void search_pva(const SearchEvent& v, int ch, T (&Pb)[6], bool& ok) {
     using C15 = Chains<T, M15>;
     const T qpva[3] = {T(kQPos), T(kQVel), T(kQAcc)};
-    const T qaw[2] = {T(kQAtt), T(kQRate)};
     const T Rg[1] = {T(kRGps)};
     const T Rp[6] = {T(kRPos), T(0), T(0), T(kRVel), T(0), T(kRAcc)};
-    const T Ra[3] = {T(kRAtt), T(0), T(kRRate)};
-    const double* e = a.ev + j * 11;
-    const int type = int(e[1]);
-    const double dtd = e[0] - prev_in;
-    const bool step = dtd >= 0.0;  // kf_workers.py:38-40: a negative dt is skipped, time unchanged
-    const T dt = T(dtd);
-    o.prev = step ? e[0] : prev_in;
-    const bool final_predict = o.prev < a.target_end - 1e-8;  // kf_workers.py:74-82
-    const T dte = T(a.target_end - o.prev);
-    LogdetAcc<T> rec, fin;
-    bool ok = true;
-#pragma unroll
-    for (int ch = 0; ch < M15::NP; ++ch) {
-        // the state is not carried (SearchNode): constant zeros, dead code after inlining
-        T xb[3] = {T(0), T(0), T(0)}, Pb[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) Pb[i] = Pin[6 * ch + i];
-        if (step) {
-            C15::template chain_predict<3>(xb, Pb, dt, qpva);
-            if (type == kGps) {
-                const T zb[1] = {T(e[2 + ch])};
-                ok = sel_update<3, 1, true, T, kRefNewton, true>(xb, Pb, zb, Rg) && ok;
-            } else {
-                const T acc = T(e[2 + M15::imu_acc(ch)]);
-                const T V = fmaT(acc, dt, xb[1]);
-                const T X = fmaT(V, dt, xb[0]);
-                const T zb[3] = {X, V, acc};
-                ok = sel_update<3, 3, true, T, kRefNewton, true>(xb, Pb, zb, Rp) && ok;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) o.P[6 * ch + i] = Pb[i];
-        rec.add_pva(Pb, ch);
-        if (final_predict) C15::template chain_predict<3>(xb, Pb, dte, qpva);
-        fin.add_pva(Pb, ch);
-    }
-#pragma unroll
-    for (int ch = 0; ch < M15::NA; ++ch) {
-        T xa[2] = {T(0), T(0)}, Pa[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) Pa[i] = Pin[6 * M15::NP + 3 * ch + i];
-        if (step) {
-            C15::template chain_predict<2>(xa, Pa, dt, qaw);
-            if (type != kGps) {  // a GPS fix updates the pva chains only
-                const T za[2] = {T(e[2 + M15::imu_att(ch)]), T(e[2 + M15::imu_rate(ch)])};
-                ok = sel_update<2, 2, true, T, kRefNewton, true>(xa, Pa, za, Ra) && ok;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) o.P[6 * M15::NP + 3 * ch + i] = Pa[i];
-        rec.add_aw(Pa);
-        if (final_predict) C15::template chain_predict<2>(xa, Pa, dte, qaw);
-        fin.add_aw(Pa);
-    }
-    o.run = run_in;
-    if (step) {
-        const T ld = rec.finish();
-        o.run = ld > run_in ? ld : run_in;
-        o.run = ok ? o.run : quiet_nan<T>();  // a failed filter (kf_eval_combos: KF_ENOTSPD)
-    }
-    o.fmax = o.run;
-    if (final_predict) {
-        const T ld = fin.finish();
-        o.fmax = ld > o.run ? ld : o.run;
+    if (!v.step) return;
+    const T dt = T(v.dt);
+    T xb[3] = {T(0), T(0), T(0)};
+    C15::template chain_predict<3>(xb, Pb, dt, qpva);
+    if (v.type == kGps) {
+        const T zb[1] = {T(v.e[2 + ch])};
+        ok = sel_update<3, 1, true, T, kRefNewton, true>(xb, Pb, zb, Rg) && ok;
+    } else {
+        const T acc = T(v.e[2 + M15::imu_acc(ch)]);
+        const T V = fmaT(acc, dt, xb[1]);
+        const T X = fmaT(V, dt, xb[0]);
+        const T zb[3] = {X, V, acc};
+        ok = sel_update<3, 3, true, T, kRefNewton, true>(xb, Pb, zb, Rp) && ok;
     }
 }
+
+template <typename T>
+__device__ __forceinline__ void search_aw(const SearchEvent& v, int ch, T (&Pa)[3], bool& ok) {
+    using C15 = Chains<T, M15>;
+    const T qaw[2] = {T(kQAtt), T(kQRate)};
+    const T Ra[3] = {T(kRAtt), T(0), T(kRRate)};
+    if (!v.step) return;
+    T xa[2] = {T(0), T(0)};
+    C15::template chain_predict<2>(xa, Pa, T(v.dt), qaw);
+    if (v.type != kGps) {  // a GPS fix updates the pva chains only
+        const T za[2] = {T(v.e[2 + M15::imu_att(ch)]), T(v.e[2 + M15::imu_rate(ch)])};
+        ok = sel_update<2, 2, true, T, kRefNewton, true>(xa, Pa, za, Ra) && ok;
+    }
+}
+
+// The log-dets of one subset: its record after the event (rec) and after the worker's final
+// predict (fin), accumulated chain by chain in Chains::logdet's block order, so the numbers are
+// kf_eval_combos's.
+template <typename T>
+struct SearchScore {
+    LogdetAcc<T> rec, fin;
+    bool ok = true;
+    __device__ __forceinline__ void add_pva(const SearchEvent& v, const T (&Pb)[6], int ch) {
+        using C15 = Chains<T, M15>;
+        const T qpva[3] = {T(kQPos), T(kQVel), T(kQAcc)};
+        rec.add_pva(Pb, ch);
+        T Pf[6], xf[3] = {T(0), T(0), T(0)};
+#pragma unroll
+        for (int i = 0; i < 6; ++i) Pf[i] = Pb[i];
+        if (v.final_predict) C15::template chain_predict<3>(xf, Pf, T(v.dte), qpva);
+        fin.add_pva(Pf, ch);
+    }
+    __device__ __forceinline__ void add_aw(const SearchEvent& v, const T (&Pa)[3]) {
+        using C15 = Chains<T, M15>;
+        const T qaw[2] = {T(kQAtt), T(kQRate)};
+        rec.add_aw(Pa);
+        T Pf[3], xf[2] = {T(0), T(0)};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Pf[i] = Pa[i];
+        if (v.final_predict) C15::template chain_predict<2>(xf, Pf, T(v.dte), qaw);
+        fin.add_aw(Pf);
+    }
+    // the running max log-det after the event (NaN for a failed filter, kf_eval_combos:
+    // KF_ENOTSPD), and into fmax the subset's max log-det with the final predict
+    __device__ __forceinline__ T finish(const SearchEvent& v, T run_in, T& fmax) {
+        T run = run_in;
+        if (v.step) {
+            const T ld = rec.finish();
+            run = ld > run_in ? ld : run_in;
+            run = ok ? run : quiet_nan<T>();
+        }
+        fmax = run;
+        if (v.final_predict) {
+            const T ld = fin.finish();
+            fmax = ld > run ? ld : run;
+        }
+        return run;
+    }
+};
 
 // Child j (> the parent's largest event) of node `par`, colex rank c at level a.k: scored into
 // (best, cnt), and stored when a.child is set and the child has stored children (largest event
 // <= n - 3).  With a.tail, the child holding event n - 2 is not stored: its only child (it plus
-// event n - 1, level k + 1) is evaluated here from the registers and scored into (best1, cnt1).
+// event n - 1, level k + 1) is evaluated from the registers and scored into (best1, cnt1).
+// Chain by chain: a chain's child covariance is stored (or carried through event n - 1) as soon
+// as it is computed, so only one chain of the child and grandchild is live at a time.
+// The parent's covariance as search_child reads it: from registers, or from a lane's LDS column
+// (the parent-major kernel's LDS variant, which frees the registers that hold it across the
+// loop over children).
 template <typename T>
-__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const SearchNode<T>& par, int j, uint64_t c,
-                                             uint64_t& best, uint64_t& cnt, uint64_t& best1, uint64_t& cnt1) {
-    SearchStep<T> s;
-    search_apply<T>(a, par.P, par.run, par.prev, j, s);
-    const uint64_t cmask = par.mask | (uint64_t(1) << (j + a.shift));
-    search_score(a, cmask, s.fmax, best, cnt);
-    if (a.child && j < a.n_events - 2) {
-        char* cb = level_block<T>(a.child, c);
-        const uint32_t cl = uint32_t(c) & 63u;
+struct ParRegs {
+    const T* P;
+    __device__ __forceinline__ T operator()(int i) const { return P[i]; }
+};
+template <typename T>
+struct ParLds {
+    const T* col;  // row i at col[i * 64]
+    __device__ __forceinline__ T operator()(int i) const { return col[i * 64]; }
+};
+
+template <typename T, class PS>
+__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const SearchNode<T>& par, const PS& pp, int j,
+                                             uint64_t c, uint64_t& best, uint64_t& cnt, uint64_t& best1,
+                                             uint64_t& cnt1) {
+    const SearchEvent vs = search_event(a, j, par.prev);
+    const bool store = a.child && j < a.n_events - 2;
+    const bool tail = a.tail && j == a.n_events - 2;  // wave-uniform (j is)
+    SearchEvent vg;
+    if (tail) vg = search_event(a, j + 1, vs.prev);
+    char* cb = store ? level_block<T>(a.child, c) : nullptr;
+    const uint32_t cl = uint32_t(c) & 63u;
+    SearchScore<T> ss, sg;
 #pragma unroll
-        for (int i = 0; i < 27; ++i) *level_row<T>(cb, cl, i) = s.P[i];
-        *level_row<T>(cb, cl, 27) = s.run;
-        *level_tail<T>(cb, cl, 0) = s.prev;
+    for (int ch = 0; ch < M15::NP; ++ch) {
+        T Pb[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) Pb[i] = pp(6 * ch + i);
+        search_pva(vs, ch, Pb, ss.ok);
+        if (store) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) *level_row<T>(cb, cl, 6 * ch + i) = Pb[i];
+        }
+        ss.add_pva(vs, Pb, ch);
+        if (tail) {
+            search_pva(vg, ch, Pb, sg.ok);
+            sg.add_pva(vg, Pb, ch);
+        }
+    }
+#pragma unroll
+    for (int ch = 0; ch < M15::NA; ++ch) {
+        T Pa[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Pa[i] = pp(6 * M15::NP + 3 * ch + i);
+        search_aw(vs, ch, Pa, ss.ok);
+        if (store) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, 6 * M15::NP + 3 * ch + i) = Pa[i];
+        }
+        ss.add_aw(vs, Pa);
+        if (tail) {
+            search_aw(vg, ch, Pa, sg.ok);
+            sg.add_aw(vg, Pa);
+        }
+    }
+    T fmax;
+    const T run = ss.finish(vs, par.run, fmax);
+    const uint64_t cmask = par.mask | (uint64_t(1) << (j + a.shift));
+    if (store) {
+        *level_row<T>(cb, cl, 27) = run;
+        *level_tail<T>(cb, cl, 0) = vs.prev;
         *level_tail<T>(cb, cl, 1) = __builtin_bit_cast(double, cmask);
-    } else if (a.tail && j == a.n_events - 2) {  // wave-uniform (j is)
-        SearchStep<T> g;
-        search_apply<T>(a, s.P, s.run, s.prev, j + 1, g);
-        search_score(a, cmask | (uint64_t(1) << (j + 1 + a.shift)), g.fmax, best1, cnt1);
+    }
+    search_score(a, cmask, fmax, best, cnt);
+    if (tail) {
+        T gmax;
+        (void)sg.finish(vg, run, gmax);
+        search_score(a, cmask | (uint64_t(1) << (j + 1 + a.shift)), gmax, best1, cnt1);
     }
 }
 
@@ -1965,9 +2040,16 @@ __device__ __forceinline__ void search_publish(const Ref15SearchArgs& a, int k, 
 // Parent-major: one lane per parent, its children in a wave-uniform loop over j (parents of a
 // wave share their largest event except at run boundaries, so event j is the same for every
 // active lane: scalar loads, a uniform GPS/IMU branch).  For the wide levels.
-template <typename T>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void ref15_search_pm_kernel(const Ref15SearchArgs a) {
-    const int64_t p = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+#ifndef KF_SEARCH_PM_WAVES
+#define KF_SEARCH_PM_WAVES 2  // waves per SIMD of the register variant (its VGPR budget)
+#endif
+// PLDS: the parent's covariance lives in LDS (one 64-lane block per workgroup, [27][64] T),
+// which fits the kernel in 3 waves per SIMD without spills; otherwise in registers.
+template <typename T, bool PLDS>
+__global__ __launch_bounds__(PLDS ? 64 : kBlock) __attribute__((amdgpu_waves_per_eu(PLDS ? 3 : KF_SEARCH_PM_WAVES))) void
+ref15_search_pm_kernel(const Ref15SearchArgs a) {
+    constexpr int NT = PLDS ? 64 : kBlock;
+    const int64_t p = static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x;
     if (uint64_t(p) >= a.n_par) return;
     SearchNode<T> par;
     if (a.k == 1) {
@@ -1981,9 +2063,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     const int m = par.max_event(a.shift);
     const int j0 = wave_uniform(m) + 1;  // colex order: the first lane holds the smallest max
     uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0;
-    for (int j = j0; j < a.n_events; ++j) {
-        if (j <= m) continue;
-        search_child<T>(a, par, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt, best1, cnt1);
+    if constexpr (PLDS) {
+        __shared__ T sP[27 * 64];
+        T* col = sP + threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < 27; ++i) col[i * 64] = par.P[i];  // read back by this lane only
+        const ParLds<T> pp{col};
+#pragma unroll 1
+        for (int j = j0; j < a.n_events; ++j) {
+            if (j <= m) continue;
+            search_child<T>(a, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt, best1, cnt1);
+        }
+    } else {
+        const ParRegs<T> pp{par.P};
+#pragma unroll 1
+        for (int j = j0; j < a.n_events; ++j) {
+            if (j <= m) continue;
+            search_child<T>(a, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt, best1, cnt1);
+        }
     }
     search_publish(a, a.k, best, cnt);
     if (a.tail) search_publish(a, a.k + 1, best1, cnt1);
@@ -2032,7 +2129,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
         par.load(a.par, p);
     }
     uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0;
-    if (par.max_event(a.shift) < j) search_child<T>(a, par, j, p + binom(j, k), best, cnt, best1, cnt1);
+    if (par.max_event(a.shift) < j) search_child<T>(a, par, ParRegs<T>{par.P}, j, p + binom(j, k), best, cnt, best1, cnt1);
     search_publish(a, a.k, best, cnt);
     if (a.tail) search_publish(a, a.k + 1, best1, cnt1);
 }
@@ -2348,6 +2445,12 @@ hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t st
     return hipGetLastError();
 }
 
+// KFMI_SEARCH_PM=lds|regs picks the parent-major variant (A/B runs); default: lds
+bool search_pm_lds() {
+    const char* v = std::getenv("KFMI_SEARCH_PM");
+    return !(v && !std::strcmp(v, "regs"));
+}
+
 hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream) {
     // node offsets are 32-bit byte offsets (buffer voffset)
     if (a.n_events > kMaxEvents || a.k < 1 || a.k > a.n_events || a.n_par == 0 || a.n_par >= (1ull << 28) ||
@@ -2373,9 +2476,15 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
         else ref15_search_cm_kernel<float><<<dim3(unsigned(waves)), 64, 0, stream>>>(a, items);
         return hipGetLastError();
     }
-    const dim3 grid(static_cast<unsigned>((a.n_par + kBlock - 1) / kBlock));
-    if (f64) ref15_search_pm_kernel<double><<<grid, kBlock, 0, stream>>>(a);
-    else ref15_search_pm_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    if (search_pm_lds()) {
+        const dim3 grid(static_cast<unsigned>((a.n_par + 63) / 64));
+        if (f64) ref15_search_pm_kernel<double, true><<<grid, 64, 0, stream>>>(a);
+        else ref15_search_pm_kernel<float, true><<<grid, 64, 0, stream>>>(a);
+    } else {
+        const dim3 grid(static_cast<unsigned>((a.n_par + kBlock - 1) / kBlock));
+        if (f64) ref15_search_pm_kernel<double, false><<<grid, kBlock, 0, stream>>>(a);
+        else ref15_search_pm_kernel<float, false><<<grid, kBlock, 0, stream>>>(a);
+    }
     return hipGetLastError();
 }
 

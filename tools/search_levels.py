@@ -7,7 +7,9 @@ import sys
 path = sys.argv[1]
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 25
 rows = [r for r in csv.DictReader(open(path)) if 'ref15_search' in r['Kernel_Name']]
-last = rows[-n:]
+# levels without stored parents (k = n) are scored by the previous launch and not launched
+nl = sum(1 for k in range(1, n + 1) if k == 1 or math.comb(n - 2, k - 1) > 0)
+last = rows[-nl:]
 tot = 0.0
 for k, r in enumerate(last, 1):
     d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
