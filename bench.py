@@ -237,7 +237,9 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
         ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
         w = 8 if cfg['dtype'] == 'f64' else 4
         nbytes = B * (T * (d + 2 * d + 1) * w + (T // k) * d * w)
-        return {'gbs': nbytes / (ms * 1e-3) / 1e9, 'ms': ms, 'bytes': nbytes}
+        return {'gbs': nbytes / (ms * 1e-3) / 1e9, 'ms': ms, 'bytes': nbytes,
+                'desc': 'tools/probes/pattern_probe.hip: the bench kernel\'s loads and stores (same ring, same '
+                        'rows, same buffers) with the arithmetic reduced to a sum'}
 
     d = 2 if cfg['model'] == 'cv2' else 3
     bytes_launch, bytes_step = algorithmic_bytes(cfg)
@@ -321,7 +323,45 @@ def ref15_workload(cfg, args, rank, world, dev):
                                                    f'NumPy {np.__version__}'}}
 
     bytes_launch, bytes_event = ref15_algorithmic_bytes(cfg)
-    return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_event,
+
+    def probe(reps):
+        """ref_events_lds_kernel's access pattern on these event streams and output rows
+        (tools/probes/pattern_probe.hip: the same LDS-DMA loads, waits and row stores, the event
+        arithmetic reduced to a sum; scratch state rows, so the handle is untouched)."""
+        import ctypes
+        path = os.path.join(ROOT, 'tools', 'probes', 'libpattern_probe.so')
+        if not os.path.exists(path) or B % 64:
+            return None
+        lib = ctypes.CDLL(path)
+        if not hasattr(lib, 'kfprobe_ref_pattern'):
+            return None
+        lib.kfprobe_ref_pattern.restype = ctypes.c_int
+        lib.kfprobe_ref_pattern.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 7 + \
+            [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
+        xs, Ps = kf.empty(15, B), kf.empty(27, B)
+        xs.zero_()
+        Ps.zero_()
+        stream = torch.cuda.current_stream(dev)
+        run = lambda: lib.kfprobe_ref_pattern(1, etype.data_ptr(), dts.data_ptr(), pay.data_ptr(), xs.data_ptr(),
+                                              Ps.data_ptr(), traj.data_ptr(), logdet.data_ptr(), B, T,
+                                              ctypes.c_void_p(stream.cuda_stream))
+        for _ in range(3):
+            if run() != 0:
+                return None
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for s_, e_ in ev:
+            s_.record(stream)
+            run()
+            e_.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in ev]))
+        nbytes = bytes_launch - 8 * B  # the probe has no status row
+        del xs, Ps
+        return {'gbs': nbytes / (ms * 1e-3) / 1e9, 'ms': ms, 'bytes': nbytes,
+                'desc': 'tools/probes/pattern_probe.hip: ref_events_lds_kernel\'s LDS-DMA event loads, waits and '
+                        'row stores on the same buffers, the event arithmetic reduced to a sum'}
+
+    return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_event, probe=probe,
                 kernel='ref_events_lds_kernel', traffic=load_traffic('ref15'), cpu=cpu, gather=gather_payload, kf=kf,
                 desc=f'SURVEY 8f row 2: reference 15-state model (kf_workers.py:493-614), f64, B={B} filters/GPU, '
                      f'T={T} events (IMU 200 Hz, GPS fix every {k}th event), dt={dt}',
@@ -721,9 +761,7 @@ def main():
                 if pr:
                     rec['roofline']['pattern_ceiling'] = {
                         'achieved': pr['gbs'], 'unit': 'GB/s', 'probe_ms': pr['ms'],
-                        'frac': achieved / pr['gbs'],
-                        'probe': 'tools/probes/pattern_probe.hip: the bench kernel\'s loads and stores (same '
-                                 'ring, same rows, same buffers) with the arithmetic reduced to a sum'}
+                        'frac': achieved / pr['gbs'], 'probe': pr['desc']}
         else:
             rec['roofline'] = {'bound': 'hbm', 'achieved': None, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': None,
                                'traffic': None, 'kernel': w['kernel'], 'kernel_ms': kern_ms,

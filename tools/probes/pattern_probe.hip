@@ -70,6 +70,77 @@ __global__ __launch_bounds__(256) void pattern_kernel(const void* u, const void*
         if (t + j < T_) step(t + j, buf[j]);
 }
 
+// ref_events_lds_kernel's memory instructions (kf_ref.hip): the state rows loaded once and
+// stored once, each event's payload / dt / type moved HBM -> LDS by buffer_load ... lds into
+// one of two per-wave images while the previous event is consumed, the same counted waits, and
+// per event the six trajectory rows, the log-det row and the (zero-length) updated row stored.
+// The 15-state event arithmetic is reduced to a sum of the event's inputs.
+constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void ref_pattern_kernel(const uint8_t* etype, const double* dtp, const void* payload,
+                                                          void* x, void* P, void* traj, void* logdet, int64_t B,
+                                                          int T_) {
+    constexpr int W = int(sizeof(T));
+    constexpr int PAY = 9 * 64 * W;
+    constexpr int NIP = (PAY + 1023) / 1024;
+    constexpr int LPR = 4 * W;
+    constexpr int DT_OFF = NIP * 1024, ET_OFF = DT_OFF + 1024, IMG = ET_OFF + 64;
+    constexpr int NDMA = NIP + 2;
+    constexpr int NST = 6 + 2;  // traj, logdet, updated
+    __shared__ __attribute__((aligned(16))) unsigned char lds[4 * 2 * IMG];
+    const int lane = int(threadIdx.x & 63);
+    const int wave = wave_uniform(int(threadIdx.x >> 6));
+    const int64_t f0 = int64_t(blockIdx.x) * 256 + int64_t(wave) * 64;
+    if (f0 >= B) return;
+    unsigned char* const img0 = lds + wave * 2 * IMG;
+    const uint32_t off = uint32_t(f0 + lane) * uint32_t(W);
+    const uint32_t rb = uint32_t(B) * uint32_t(W);
+    T st[42];
+#pragma unroll
+    for (int i = 0; i < 15; ++i) st[i] = ldb<T>(x, i, rb, off);
+#pragma unroll
+    for (int i = 0; i < 27; ++i) st[15 + i] = ldb<T>(P, i, rb, off);
+    waitcnt<vmcnt_imm(0)>();
+    const uint32_t voff_pay = uint32_t(lane / LPR) * rb + uint32_t(lane % LPR) * 16u;
+    auto issue = [&](int t, unsigned char* img) {
+        const char* pb = reinterpret_cast<const char*>(payload) + int64_t(t) * 9 * int64_t(rb) + f0 * W;
+        const __amdgpu_buffer_rsrc_t rp = bytes_rsrc(pb, 9u * rb - uint32_t(f0) * W);
+#pragma unroll
+        for (int k = 0; k < NIP; ++k)
+            if (k + 1 < NIP || k * 1024 + lane * 16 < PAY) lds_dma16(rp, img + k * 1024, voff_pay, k * (16 / W) * int(rb));
+        const char* db = reinterpret_cast<const char*>(dtp) + int64_t(t) * B * 8 + f0 * 8;
+        if (lane < 32) lds_dma16(bytes_rsrc(db, uint32_t(B - f0) * 8u), img + DT_OFF, uint32_t(lane) * 16u, 0);
+        const char* eb = reinterpret_cast<const char*>(etype) + int64_t(t) * B + f0;
+        if (lane < 4) lds_dma16(bytes_rsrc(eb, uint32_t(B - f0)), img + ET_OFF, uint32_t(lane) * 16u, 0);
+    };
+    issue(0, img0);
+    waitcnt<vmcnt_imm(0)>();
+    T acc = T(0);
+    for (int t = 0; t < T_; ++t) {
+        unsigned char* const img = img0 + (t & 1) * IMG;
+        if (t + 1 < T_) {
+            issue(t + 1, img0 + ((t + 1) & 1) * IMG);
+            waitcnt<vmcnt_imm(NST + NDMA)>();
+        } else {
+            waitcnt<vmcnt_imm(NST)>();
+        }
+        const int type = img[ET_OFF + lane];
+        acc += T(reinterpret_cast<const double*>(img + DT_OFF)[lane]) + T(type);
+        const T* pay = reinterpret_cast<const T*>(img) + lane;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) acc += pay[i * 64];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) stb(traj, int64_t(t) * 6 + i, rb, off, acc + T(i));
+        stb(logdet, t, rb, off, acc);
+        stb_u8(nullptr, t, 0u, uint32_t(f0 + lane), uint8_t(type != 255));
+    }
+#pragma unroll
+    for (int i = 0; i < 15; ++i) stb(x, i, rb, off, st[i] + acc);
+#pragma unroll
+    for (int i = 0; i < 27; ++i) stb(P, i, rb, off, st[15 + i] + acc);
+}
+
 template <int D, typename T>
 hipError_t launch(const void* u, const void* z, void* traj, void* logdet, int64_t B, int T_, int k, hipStream_t st) {
     pattern_kernel<D, T, 8><<<dim3(unsigned((B + 255) / 256)), 256, 0, st>>>(u, z, traj, logdet, B, T_, k);
@@ -90,4 +161,18 @@ extern "C" int kfprobe_pattern(int axes, int f64, const void* u, const void* z, 
     else e = f64 ? launch<2, double>(u, z, traj, logdet, B, T, update_every, st)
                  : launch<2, float>(u, z, traj, logdet, B, T, update_every, st);
     return int(e);
+}
+
+// etype [T][B] u8, dt [T][B] f64, payload [T][9][B], x [15][B], P [27][B], traj [T][6][B],
+// logdet [T][B] (device; element type f64 ? double : float).  B % 64 == 0.
+extern "C" int kfprobe_ref_pattern(int f64, const void* etype, const void* dt, const void* payload, void* x, void* P,
+                                   void* traj, void* logdet, int64_t B, int T, void* stream) {
+    if (B <= 0 || B % 64 != 0 || T <= 0 || 9 * B * 8 >= (int64_t(1) << 32)) return int(hipErrorInvalidValue);
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const dim3 grid(unsigned((B + 255) / 256));
+    const uint8_t* et = static_cast<const uint8_t*>(etype);
+    const double* d = static_cast<const double*>(dt);
+    if (f64) ref_pattern_kernel<double><<<grid, 256, 0, st>>>(et, d, payload, x, P, traj, logdet, B, T);
+    else ref_pattern_kernel<float><<<grid, 256, 0, st>>>(et, d, payload, x, P, traj, logdet, B, T);
+    return int(hipGetLastError());
 }
