@@ -209,6 +209,46 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
                               'link_gbs': (h2d + d2h) / pel / 1e9,
                               'note': 'BatchedKF.run_host: time chunks on 3 streams, H2D | launch | D2H overlapped'}}
 
+    def per_step(reps=2):
+        """The reference's call shape: T steps of BatchedKF.predict(dt, u[t]) then
+        BatchedKF.update(z[t]) (its log-det returned), one launch each, the state round-tripping
+        through HBM every call; against kf_run's fused launch on the same streams.  Never `value`."""
+        if k != 1:
+            return None
+        kf.reset(x0)
+        times = []
+        for _ in range(reps + 1):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for t in range(T):
+                kf.predict(dt, u=u[t])
+                kf.update(z[t])
+            torch.cuda.synchronize(dev)
+            times.append(time.perf_counter() - t0)
+        el = min(times[1:])
+        # the same steps as T launches of kf_run with T = 1 (predict + update fused, one state
+        # round trip per step, trajectory and log-det rows written)
+        kf.reset(x0)
+        times1 = []
+        for _ in range(reps + 1):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for t in range(T):
+                kf.run(u[t:t + 1], z[t:t + 1], dt=dt, out=(traj[t:t + 1], logdet[t:t + 1]))
+            torch.cuda.synchronize(dev)
+            times1.append(time.perf_counter() - t0)
+        el1 = min(times1[1:])
+        w = 8 if cfg['dtype'] == 'f64' else 4
+        nt = kf.n * (kf.n + 1) // 2
+        # predict: state + u in, state out; update: state + z in, state + log-det out
+        nbytes = B * T * w * ((kf.n + nt) * 4 + 2 * d + 1)
+        return {'value': B * T / el, 'unit': 'KF steps/s', 'ms_per_step': el / T * 1e3,
+                'gbs': nbytes / el / 1e9, 'launches': 2 * T,
+                'note': 'kf_predict + kf_update per time step through BatchedKF (no trajectory kept), best of %d'
+                        % reps,
+                'run_t1': {'value': B * T / el1, 'ms_per_step': el1 / T * 1e3, 'launches': T,
+                           'note': 'BatchedKF.run on one step at a time (kf_run, T = 1: predict + update fused)'}}
+
     def probe(reps):
         """The access pattern's ceiling on these very buffers (tools/probes/pattern_probe.hip:
         the block kernel's loads and stores through the same ring, the arithmetic reduced to a
@@ -246,7 +286,7 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
     kernel = 'cv_block_kernel' if block_kernel_in_use() else 'cv_run_kernel'
     return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_step, kernel=kernel,
                 traffic=load_traffic(cfg_id) if kernel == 'cv_block_kernel' else None, cpu=cpu,
-                gather=gather_payload, kf=kf, pcie=pcie, probe=probe,
+                gather=gather_payload, kf=kf, pcie=pcie, probe=probe, per_step=per_step,
                 desc=f"BASELINE config {cfg_id}: {cfg['model']} ({2 * d}-state/{d}-meas), {cfg['dtype']}, "
                      f"B={B} filters/GPU, T={T}, dt={dt}, GPS update every {k} step(s)",
                 extra={'filters_per_gpu': B, 'time_steps_per_launch': T, 'update_every': k})
@@ -658,6 +698,8 @@ def main():
     ap.add_argument('--batch', type=int, default=None, help='override filters per GPU')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--pcie', action='store_true', help='also report the PCIe-inclusive rate (cv configs, N=1)')
+    ap.add_argument('--per-step', action='store_true',
+                    help='cv configs, N=1: also time the per-step predict()/update() call shape')
     ap.add_argument('--graph', action='store_true',
                     help='config 1: replay the step as a hipGraph (measured no faster than eager launches)')
     ap.add_argument('--ablate', choices=['none', 'no-traj', 'no-logdet', 'no-traj-no-logdet'], default='none',
@@ -776,6 +818,8 @@ def main():
         rec['cpu_baseline'] = w['cpu']() if (world == 1 and not args.no_cpu_baseline) else None
         if args.pcie and world == 1 and w.get('pcie'):
             rec['pcie_inclusive'] = w['pcie']()
+        if args.per_step and world == 1 and w.get('per_step'):
+            rec['per_step_api'] = w['per_step']()
         print(json.dumps(rec), flush=True)
     kf.close()
     if dist:
