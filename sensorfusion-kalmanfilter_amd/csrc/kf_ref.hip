@@ -608,6 +608,17 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     T xs0[3];  // variant 0's start (the map pass's guess)
 #pragma unroll
     for (int k = 0; k < 3; ++k) xs0[k] = x[0][k];
+    // the map pass's seam check reads the next chunk's start covariance: loaded here, before
+    // any of this lane's stores (a later load would wait for all of them, vmcnt being in order)
+    double wnx[6] = {0, 0, 0, 0, 0, 0};
+    if constexpr (NV == 4) {
+        if (live && a.s_maps && a.s_check && f + 1 < a.B) {
+            const T* wn = static_cast<const T*>(a.s_wnext);
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                if (pr[k] >= 0) wnx[k] = double(wn[int64_t(pr[k]) * a.B + f + 1]);
+        }
+    }
     int32_t st = a.status[f];
     const bool need_ld = a.logdet != nullptr;
 
@@ -814,6 +825,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
         double crel = 0.0;
         if (live && a.s_maps) {
             double A[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, b[3] = {0, 0, 0};
+            const double rdelta = 1.0 / a.s_delta;  // delta is a power of two: exact
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 if (k >= ns) continue;
@@ -822,7 +834,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
 #pragma unroll
                 for (int qq = 0; qq < 3; ++qq) {
                     if (qq >= ns) continue;
-                    A[k][qq] = (double(x[qq + 1][k]) - e0v) / a.s_delta;
+                    A[k][qq] = (double(x[qq + 1][k]) - e0v) * rdelta;
                     sacc = __builtin_fma(-A[k][qq], double(xs0[qq]), sacc);
                 }
                 b[k] = sacc;
@@ -834,27 +846,40 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
                 for (int qq = 0; qq < 3; ++qq) mo[k * 3 + qq] = A[k][qq];
                 mo[9 + k] = b[k];
             }
-            if (f + 1 < a.B) {
-                const T* wn = static_cast<const T*>(a.s_wnext);
+            if (a.s_check && f + 1 < a.B) {
                 double scale = 0.0, gap = 0.0;
 #pragma unroll
                 for (int k = 0; k < 6; ++k) {
                     if (pr[k] < 0) continue;
                     const double pe = double(P[k]);
                     scale = fmax(scale, fabs(pe));
-                    gap = fmax(gap, fabs(pe - double(wn[int64_t(pr[k]) * a.B + f + 1])));
+                    gap = fmax(gap, fabs(pe - wnx[k]));
                 }
                 const double rel = gap / fmax(scale, 1e-300);
                 crel = rel == rel ? rel : __builtin_inf();
             }
         }
         if (a.s_check) {
-            // the group's max (DPP; the whole group is live), one atomic per chunk
+            // the wave's max over its chunks (DPP inside a group; lanes of finished groups hold
+            // 0), one atomic per wave: every chunk's lanes finish together, and one atomic per
+            // chunk on the same address queued up behind each other at the end of the pass
             crel = fmax(crel, dpp_d<kDppXor1>(crel));
             crel = fmax(crel, dpp_d<kDppXor2>(crel));
             crel = fmax(crel, dpp_d<kDppHalfMirror>(crel));
-            if (c == 0 && crel != 0.0) atomic_max_pos(&a.s_check->cov_gap, crel);
-            if (c == 0 && st != 0) atomicOr(&a.s_check->bad, kStreamBadFilter);
+            // a wave whose chunks all exist has every lane here (a partial last wave lost its
+            // dead groups at the top, so it keeps one atomic per chunk)
+            const bool full = (g & ~int64_t(63)) / kGroup + 64 / kGroup <= a.B;  // wave-uniform
+            if (full) {
+#pragma unroll
+                for (int sh = kGroup; sh < 64; sh <<= 1) crel = fmax(crel, __shfl_xor(crel, sh, 64));
+                const bool lane0 = (threadIdx.x & 63) == 0;
+                if (lane0 && crel != 0.0) atomic_max_pos(&a.s_check->cov_gap, crel);
+                const bool any_bad = __builtin_amdgcn_ballot_w64(c == 0 && st != 0) != 0;
+                if (lane0 && any_bad) atomicOr(&a.s_check->bad, kStreamBadFilter);
+            } else {
+                if (c == 0 && crel != 0.0) atomic_max_pos(&a.s_check->cov_gap, crel);
+                if (c == 0 && st != 0) atomicOr(&a.s_check->bad, kStreamBadFilter);
+            }
         }
     }
 }
