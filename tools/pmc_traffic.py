@@ -62,17 +62,20 @@ def main():
             wk = per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE')
             f = [v for k, vs in fk.items() if 'ref15_search' in k for v in vs]
             w = [v for k, vs in wk.items() if 'ref15_search' in k for v in vs]
-            fetch = 1024 * sum(f) / (len(f) / n)
-            write = 1024 * sum(w) / (len(w) / n)
             from kfmi.ref15 import search_level_bytes
             import math
+            # launches per search: the levels with stored parents (level n is scored by the
+            # tail of level n - 1 and not launched)
+            nl = sum(1 for k in range(1, n + 1) if k == 1 or math.comb(n - 2, k - 1) > 0)
+            fetch = 1024 * sum(f) / (len(f) / nl)
+            write = 1024 * sum(w) / (len(w) / nl)
             alg = 2 * sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in range(1, n))
             res['configbf'] = {
                 'fetch_bytes_raw': fetch, 'write_bytes_raw': write,
                 'bytes_per_launch': fetch * read_scale + write * write_scale,
                 'algorithmic_bytes_per_launch': alg,
                 'traffic_over_algorithmic': (fetch * read_scale + write * write_scale) / alg,
-                'launches_profiled': len(f), 'note': 'per search: the sum over its n level launches'}
+                'launches_profiled': len(f), 'note': f'per search: the sum over its {nl} level launches'}
             continue
         kern = 'ref_events' if c == 'ref15' else 'cv_block_kernel'
         f = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE'), kern)
