@@ -256,10 +256,12 @@ int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const d
  * evenly, kfmi.dist), k_max counting the fixed candidates,
  * n_accepted host [k_max + 1] (nullable) accepted subsets per size.  subset_max: device [2^n]
  * of the handle's dtype (n_events <= 30, nullable) receives every evaluated subset's max
- * log-determinant (NaN for a failed filter), indexed by mask.  Level k stores the C(n - 1, k)
- * subsets without the last candidate (the others have no extensions); C(n - 1, k) must stay
- * below 2^28, and the handle's level buffers take 2 * C(n - 1, k) * (28 w + 16) bytes at the
- * widest stored level (w = 8 for f64, 4 for f32).  The call synchronises `stream`. */
+ * log-determinant (NaN for a failed filter), indexed by mask.  Level k stores the C(n - 2, k)
+ * subsets whose largest free candidate is <= n - 3 (a subset holding n - 1 has no extensions,
+ * one holding n - 2 only the one adding n - 1, which is scored from registers); C(n - 2, k)
+ * must stay below 2^28, and the handle's level buffers take 2 * C(n - 2, k) * (28 w + 16)
+ * bytes at the widest stored level (w = 8 for f64, 4 for f32; n = free candidates).  The call
+ * synchronises `stream`. */
 int kf_search_combos(kf_batch* handle, int n_events, const double* events, const double* init,
                      double prev_time, double target_end, double threshold, int k_max, int exhaustive,
                      int n_fixed, uint64_t fixed_mask, uint64_t* winner, int* k_found,
