@@ -673,9 +673,11 @@ def bf_workload(cfg, args, rank, world, dev):
         # <= n - 3) is written once and read once as a parent
         lvl = sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in range(1, n))
         return dict(step=step, units=total_steps, bytes=2 * lvl, bytes_per_unit=2 * lvl / total_combos,
-                    kernel='ref15_search_pm_kernel+ref15_search_cm_kernel (the 25 level launches of one search)', traffic=load_traffic('bf'), cpu=cpu, gather=None, kf=kf, combos=total_combos,
-                    roofline_note='level-buffer bytes only (each stored prefix filter written and read once); the '
-                                  'kernel is co-limited by fp64 issue (one event step + final predict per subset)',
+                    kernel='ref15_search_pm_kernel+ref15_search_cm_kernel (the n-1 level launches of one search)', traffic=load_traffic('bf'), cpu=cpu, gather=None, kf=kf, combos=total_combos,
+                    roofline_note='level-buffer bytes only (each stored prefix filter written and read once, the '
+                                  'subsets holding candidate n-2 scored from registers); the search is fp64 issue / '
+                                  'latency-bound: ~940 VALU instructions per subset (one event step, the final '
+                                  'predict, two log-dets), profiles/r02_bf/',
                     desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '
                          f'all 2^{n}-1 subsets, reference 15-state model, f64, shared-prefix search '
                          f'(kf_search_combos: one event step + final predict per subset, {n} level launches); '
