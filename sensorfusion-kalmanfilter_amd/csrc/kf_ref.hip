@@ -1785,11 +1785,11 @@ struct LogdetAcc {
 // log-det, the time of its last applied event and its subset mask.  The search scores a subset
 // by its max log-det alone, which depends on the covariance alone, and the covariance does not
 // depend on the measurements (nor, so, on the state): the state is not carried (kf_eval_combos
-// carries it for the per-combination API).  x stays as constant zeros, so the state half of
-// every update is dead code the compiler removes.
+// carries it for the per-combination API).  The updates see a constant zero state (search_pva,
+// search_aw), so their state half is dead code the compiler removes.
 template <typename T>
 struct SearchNode {
-    T x[15], P[27];
+    T P[27];
     T run;
     double prev;
     uint64_t mask;
@@ -1823,8 +1823,6 @@ struct SearchNode {
             prev = e[0];
         }
 #pragma unroll
-        for (int i = 0; i < 15; ++i) x[i] = T(0);
-#pragma unroll
         for (int i = 0; i < 27; ++i) P[i] = r.blk(i);
         T fmax = run;
         if (eval && prev < a.target_end - 1e-8) {  // kf_workers.py:74-82
@@ -1837,8 +1835,6 @@ struct SearchNode {
     __device__ __forceinline__ void load(const void* level, uint64_t p) {
         char* blk = level_block<T>(level, p);
         const uint32_t lane = uint32_t(p) & 63u;
-#pragma unroll
-        for (int i = 0; i < 15; ++i) x[i] = T(0);
 #pragma unroll
         for (int i = 0; i < 27; ++i) P[i] = *level_row<T>(blk, lane, i);
         run = *level_row<T>(blk, lane, 27);
@@ -2421,7 +2417,13 @@ void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
         case kStreamPhaseLftMaps: stream_lft_maps_kernel<T, M><<<grid(a.C * a.np * NCH), kBlock, 0, stream>>>(a); break;
         case kStreamPhaseLftStart: {
             const int64_t bc = a.g > 0 ? a.G : kBlock;
-            const unsigned threads = a.g > 0 ? unsigned((a.G + a.g - 1) / a.g) : unsigned(kBlock);
+            // LDS variant: G / g threads walk, but the whole block stages the window maps (more
+            // loads in flight; the extra threads leave after the staging)
+            const char* ev = std::getenv("KFMI_START_THREADS");
+            const unsigned walkers = a.g > 0 ? unsigned((a.G + a.g - 1) / a.g) : unsigned(kBlock);
+            const unsigned want = ev ? unsigned(std::atoi(ev)) : unsigned(kBlock);
+            const unsigned threads = a.g > 0 ? (want > walkers && want <= unsigned(kBlock) ? want : walkers)
+                                             : unsigned(kBlock);
             const size_t lds = a.g > 0 ? size_t(a.G + a.iters) * a.np * 36 * sizeof(double) : 0;
             const dim3 g(unsigned((a.C + bc - 1) / bc), NCH);
             if (a.g > 0) stream_lft_start_kernel<T, M, true><<<g, threads, lds, stream>>>(a);
