@@ -1411,7 +1411,7 @@ __device__ __forceinline__ void lft_apply(double (&p)[3][3], const double (&m)[3
                  a22 = Y[0][0] * Y[1][1] - Y[0][1] * Y[1][0];
     const double det = Y[0][0] * a00 + Y[0][1] * a10 + Y[0][2] * a20;
     const double inv[3][3] = {{a00, a01, a02}, {a10, a11, a12}, {a20, a21, a22}};
-    const double rd = 1.0 / det;
+    const double rd = rcp_nr<2>(det);  // Newton-refined reciprocal: an IEEE division is ~10 dependent ops
     double pn[3][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
