@@ -205,6 +205,12 @@ struct Ref15SearchArgs {
     void* subset_max;        // device [2^n] T: every subset's max log-det by mask, or nullptr
     int tail;                // level k + 1 is searched: a child holding event n - 2 is not stored, its
                              // only child (plus event n - 1) is scored by this launch (size k + 1)
+    // child-major work items (k >= 2; filled by launch_ref15_search): group i holds the parent
+    // blocks whose first parent's largest event is v = v_lo + i, blocks [gblk[i], gblk[i + 1]),
+    // each with n - 1 - v items (child events v + 1 .. n - 1); its first item is gitem[i]
+    int v_lo, n_groups;
+    uint64_t gitem[66];
+    uint64_t gblk[66];
 };
 
 constexpr int kSearchRows = 28;  // T rows of a search node

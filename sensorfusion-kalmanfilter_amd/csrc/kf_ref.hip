@@ -2122,21 +2122,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
     const int n = a.n_events, k = a.k;
     const uint64_t* C = a.binom;
     auto binom = [&](int x, int y) -> uint64_t { return x < 0 ? (y == 0 ? 1 : 0) : C[x * (kMaxEvents + 1) + y]; };
-    // find the item's group v (scalar loop): group v holds blocks [ceil(C(v, k-1)/64), ceil(C(v+1, k-1)/64))
-    int v = k == 1 ? -1 : k - 2;
-    uint64_t start = 0;
-    uint64_t b0 = 0, nb = 1;
-    for (;; ++v) {
-        b0 = k == 1 ? 0 : (binom(v, k - 1) + 63) / 64;
-        const uint64_t b1 = k == 1 ? 1 : (binom(v + 1, k - 1) + 63) / 64;
-        nb = b1 - b0;
-        const uint64_t span = nb * uint64_t(n - 1 - v);
-        if (item < start + span || v >= n - 3) break;
-        start += span;
+    // the item's group (the host's table in the kernel arguments: a binary search over
+    // constant-cache loads, instead of a walk whose every step waited on a binomial load)
+    int v = -1;
+    uint64_t blk = 0;
+    int j = int(item);  // k == 1: item j is the root's child j
+    if (k > 1) {
+        int lo = 0, hi = a.n_groups - 1;  // the last group whose first item is <= item
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (a.gitem[mid] <= item) lo = mid;
+            else hi = mid - 1;
+        }
+        v = a.v_lo + lo;
+        const uint32_t r = uint32_t(item - a.gitem[lo]), w = uint32_t(n - 1 - v);  // r < 2^31 (host check)
+        const uint32_t q = r / w;
+        blk = a.gblk[lo] + q;
+        j = v + 1 + int(r - q * w);
     }
-    const uint64_t r = item - start;
-    const uint64_t blk = b0 + r / uint64_t(n - 1 - v);
-    const int j = v + 1 + int(r % uint64_t(n - 1 - v));
     const uint64_t p = blk * 64 + threadIdx.x;
     if (p >= a.n_par) return;
     SearchNode<T> par;
@@ -2484,23 +2487,35 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
         a.n_child >= (1ull << 28))
         return hipErrorInvalidValue;
     if (child_major) {
-        // work items: per group v of parent blocks, blocks x (n - 1 - v) child events
+        // work items: per group v of parent blocks, blocks x (n - 1 - v) child events; group v
+        // holds blocks [ceil(C(v, k-1)/64), ceil(C(v+1, k-1)/64)) (the stored parents have
+        // largest event <= n - 3)
         const uint64_t* C = a.binom_host;
         const int n = a.n_events, k = a.k;
+        Ref15SearchArgs b = a;
         uint64_t items = 0;
         if (k == 1) {
             items = uint64_t(n);
+            b.n_groups = 0;
         } else {
-            for (int v = k - 2; v <= n - 3; ++v) {
+            b.v_lo = k - 2;
+            int i = 0;
+            for (int v = k - 2; v <= n - 3; ++v, ++i) {
                 const uint64_t b0 = (C[v * (kMaxEvents + 1) + k - 1] + 63) / 64;
                 const uint64_t b1 = (C[(v + 1) * (kMaxEvents + 1) + k - 1] + 63) / 64;
-                items += (b1 - b0) * uint64_t(n - 1 - v);
+                b.gitem[i] = items;
+                b.gblk[i] = b0;
+                const uint64_t span = (b1 - b0) * uint64_t(n - 1 - v);
+                if (span >= (1ull << 31)) return hipErrorInvalidValue;  // 32-bit item offsets in a group
+                items += span;
             }
+            b.n_groups = i;
+            if (i == 0) return hipErrorInvalidValue;
         }
         const uint64_t waves = (items + 7) / 8 * 8;
         if (waves >= (1ull << 31)) return hipErrorInvalidValue;
-        if (f64) ref15_search_cm_kernel<double><<<dim3(unsigned(waves)), 64, 0, stream>>>(a, items);
-        else ref15_search_cm_kernel<float><<<dim3(unsigned(waves)), 64, 0, stream>>>(a, items);
+        if (f64) ref15_search_cm_kernel<double><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
+        else ref15_search_cm_kernel<float><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
         return hipGetLastError();
     }
     if (search_pm_lds()) {
