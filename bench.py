@@ -52,6 +52,8 @@ CONFIGS = {
     'ref15': dict(model='ref15', dtype='f64', B=1048576, T=256, dt=0.005, k=20),
     'bf': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=True),
     'bf_subsets': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=False),
+    'sched': dict(model='ref15', dtype='f64', B=1048576, T=256, dt=0.005, k=20,
+                  rates=(10, 20, 30, 40, 50, 60, 70, 80, 90, 100, 110, 120)),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 SEED = 20251015
@@ -580,6 +582,91 @@ def log_workload(cfg, args, rank, world, dev):
                        'kf_ingest_ms': (t3 - t2) * 1e3, 'kf_ingest_first_call_ms': (t2 - t1) * 1e3, 'filters': 1})
 
 
+def sched_workload(cfg, args, rank, world, dev):
+    """the rate-decimated greedy scheduled filter (kf_workers.py:826-957,
+    Scheduler.greedy_schedule :195-213) over B event streams, the reference's sampling sweep
+    (one filter per processing rate, 10..120 Hz, kf_plot_{10..120}.png) replicated across the
+    batch, 64 filters per rate: kf_run_scheduled, one launch.  A unit is one input event examined."""
+    import kfmi
+    from kfmi import _lib
+    from kfmi.engine import _ptr
+    B, T, dt, k = cfg['B'], cfg['T'], cfg['dt'], cfg['k']
+    kf = kfmi.BatchedKF('ref15', B, 'f64', device=dev.index)
+    g = torch.Generator(device=dev).manual_seed(SEED + rank)
+    t0 = 1697739278.761565
+    etype = torch.ones(T, B, dtype=torch.uint8, device=dev)
+    etype[k - 1::k] = 0
+    # 200 Hz with +-0.5 ms jitter per filter and event
+    tt = (t0 + dt * torch.arange(1, T + 1, dtype=torch.float64, device=dev)[:, None]
+          + 5e-4 * (torch.rand(T, B, dtype=torch.float64, device=dev, generator=g) - 0.5))
+    pay = torch.randn(T, 9, B, dtype=torch.float64, device=dev, generator=g)
+    pay[:, 0:3] *= 0.05
+    pay[:, 3:6] *= 0.01
+    pay[:, 6:9] *= 0.3
+    gps = (etype == 0)[:, None, :]
+    pay[:, 0:3] = torch.where(gps, pay[:, 0:3] * 60.0, pay[:, 0:3])
+    rates = torch.tensor(cfg['rates'], dtype=torch.float64, device=dev)
+    # one rate per 64 consecutive filters (a wave): the sweep's filters batched by rate, so the
+    # lanes of a wave reach their processing windows together (the jitter aside)
+    freq = rates[(torch.arange(B, device=dev) // 64) % len(cfg['rates'])].contiguous()
+    prev = torch.full((B,), t0, dtype=torch.float64, device=dev)
+    traj = kf.empty(T, 6, B)
+    logdet = kf.empty(T, B)
+    sel_time = torch.empty(T, B, dtype=torch.float64, device=dev)
+    n_sel = torch.empty(B, dtype=torch.int32, device=dev)
+
+    def step():
+        _lib.check(_lib.lib().kf_run_scheduled(kf.handle, T, _ptr(tt), _ptr(etype), _ptr(pay), _ptr(prev), _ptr(freq),
+                                                0.0, _ptr(traj), _ptr(logdet), _ptr(sel_time), _ptr(n_sel),
+                                                kf._stream()))
+
+    step()
+    torch.cuda.synchronize(dev)
+    n_selected = int(n_sel.long().sum().item())
+
+    def cpu():
+        """The oracle's NumPy restatement of the scheduled driver (oracle/ref_kf.
+        run_kalman_filter_scheduled, kf_workers.py:826-957: Scheduler.gain per queued candidate
+        with np.linalg.inv, step15, slogdet) on 1 core, streams of this workload."""
+        from oracle import ref_kf
+        et = etype.cpu().numpy()
+        ts = tt.cpu().numpy()
+        pa = pay.cpu().numpy()
+        fr = freq.cpu().numpy()
+        done, t1 = 0, time.perf_counter()
+        f = 0
+        while time.perf_counter() - t1 < 10.0 and f < B:
+            ev = [(0, 'GPS', t0, {'easting': 0.0, 'northing': 0.0, 'altitude': 0.0})]
+            for i in range(T):
+                if et[i, f] == 0:
+                    ev.append((i + 1, 'GPS', ts[i, f], {'easting': pa[i, 0, f], 'northing': pa[i, 1, f],
+                                                        'altitude': pa[i, 2, f]}))
+                else:
+                    ev.append((i + 1, 'IMU', ts[i, f], ['t', *pa[i, :, f]]))
+            ref_kf.run_kalman_filter_scheduled(ev, 0, len(ev), ref_kf.P0_REF15.copy(), (t0, 0, 0, 0, 0, 0, 0),
+                                               'greedy', float(fr[f]))
+            done += T
+            f += 1
+        el = time.perf_counter() - t1
+        return {'value': done / el, 'unit': 'KF events/s', 'cores': 1, 'kind': 'port', 'seconds': round(el, 2),
+                'sample': f'{f} filters x {T} events of these streams (their rates, 10..120 Hz) through '
+                          f'oracle/ref_kf.run_kalman_filter_scheduled (NumPy {np.__version__}, greedy), 1 core, '
+                          f'{host_cpu()}'}
+
+    # per event examined: t 8 + etype 1 read; per selection: payload 72 read, traj 48 + logdet 8 +
+    # sel_time 8 written; per filter: state (15 + 27) x 8 loaded and stored, prev / freq read,
+    # status read + written, n_sel written
+    nbytes = B * T * 9 + n_selected * (72 + 64) + B * (2 * 42 * 8 + 8 + 8 + 8 + 4)
+    return dict(step=step, units=B * T, bytes=nbytes, bytes_per_unit=nbytes / (B * T),
+                kernel='ref15_sched_kernel', traffic=None, cpu=cpu, gather=None, kf=kf,
+                roofline_note=f'{n_selected / (B * T):.3f} of the examined events are selected and applied; '
+                              'the queue scan re-reads the window\'s types from cache',
+                desc=f'SURVEY 8f row 3: rate-decimated greedy scheduled filter (kf_workers.py:826-957), reference '
+                     f'15-state model, f64, B={B} filters/GPU, T={T} events at 200 Hz (GPS every {k}th), '
+                     f'processing rates {cfg["rates"][0]}..{cfg["rates"][-1]} Hz across the batch (64 filters per rate)',
+                extra={'filters_per_gpu': B, 'events_per_launch': T, 'selected_events': n_selected})
+
+
 def bf_workload(cfg, args, rank, world, dev):
     """Exhaustive brute-force search (kf_workers.py:1218-1392 without the early exit): every
     k-subset, k = 1..n, of n candidate events after a warm start, through kf_eval_combos.  Each
@@ -727,6 +814,8 @@ def main():
         w = log_workload(cfg, args, rank, world, dev)
     elif args.config == 'ref15':
         w = ref15_workload(cfg, args, rank, world, dev)
+    elif args.config == 'sched':
+        w = sched_workload(cfg, args, rank, world, dev)
     elif args.config in ('bf', 'bf_subsets'):
         w = bf_workload(cfg, args, rank, world, dev)
     else:

@@ -2236,71 +2236,103 @@ __global__ __launch_bounds__(kBlock) void ref15_score_kernel(const Ref15ScoreArg
     }
 }
 
+// The greedy pick needs no scan of the queue: a candidate's gain depends only on its sensor
+// type and the current covariance, so the first candidate with the largest gain is the first
+// queued GPS fix or the first queued other event (ties: whichever came first; a NaN gain is
+// never picked, and with none pickable the queue's first event is, as the reference's loop
+// leaves best_i at its start).  Each lane tracks those two candidates (index, type, time) as
+// events are queued, and reads the payload of the picked one only.  The event types and times
+// are prefetched kSchedDepth events ahead (their loads do not depend on the lane's branches).
+#ifndef KF_SCHED_DEPTH
+#define KF_SCHED_DEPTH 1
+#endif
+constexpr int kSchedDepth = KF_SCHED_DEPTH;
+#ifndef KF_SCHED_WAVES
+#define KF_SCHED_WAVES 2
+#endif
 template <typename T>
-__global__ __launch_bounds__(kBlock) void ref15_sched_kernel(const Ref15SchedArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED_WAVES))) void ref15_sched_kernel(
+    const Ref15SchedArgs a) {
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
     const int64_t B = a.B;
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(B) * uint32_t(sizeof(T));
-    // compacted per-selection records are addressed per lane below
     Ref15<T> s;
     s.load(a.x, a.P, rb, off);
     int32_t st = a.status[f];
     double prev = a.prev_time[f];
     const double period = 1.0 / (a.freq ? a.freq[f] : a.freq_all);  // kf_workers.py:880
-    int q_start = 0, q_len = 0, nsel = 0;
-    for (int i = 0; i < a.T; ++i) {
-        const int ty = a.etype[int64_t(i) * B + f];
-        if (ty == 255) continue;  // padding of a ragged stream
-        const double ti = a.t[int64_t(i) * B + f];
-        if (ti - prev < period) {  // still inside the window: queue it
-            if (q_len == 0) q_start = i;
-            ++q_len;
-            continue;
-        }
-        if (q_len == 0) {  // gap larger than the window: the current event alone
-            q_start = i;
-            q_len = 1;
-        }
-        // greedy_schedule (kf_workers.py:195-213): first queued candidate with the largest
-        // gain = trace of the S=[1] posterior on the current covariance
-        const T g_gps = first_row_gain(s, kGps);
-        const T g_imu = first_row_gain(s, kImu);
-        T best = -__builtin_inf();
-        int sel = q_start;
-        for (int j = q_start; j < q_start + q_len; ++j) {
-            const int tj = a.etype[int64_t(j) * B + f];
-            if (tj == 255) continue;
-            const T g = tj == kGps ? g_gps : g_imu;
-            if (g > best) {
-                best = g;
-                sel = j;
+    // the queue: its length and, per class (0: GPS fix, 1: any other event), the first queued
+    // event's index, type and time
+    int q_len = 0, nsel = 0;
+    int qi[2] = {-1, -1}, qt[2] = {0, 0};
+    double qtime[2] = {0.0, 0.0};
+    int tyr[kSchedDepth];
+    double tr[kSchedDepth];
+#pragma unroll
+    for (int d = 0; d < kSchedDepth; ++d) {
+        tyr[d] = d < a.T ? a.etype[int64_t(d) * B + f] : 255;
+        tr[d] = d < a.T ? a.t[int64_t(d) * B + f] : 0.0;
+    }
+    for (int i0 = 0; i0 < a.T; i0 += kSchedDepth) {
+#pragma unroll
+        for (int d = 0; d < kSchedDepth; ++d) {
+            const int i = i0 + d;
+            if (i >= a.T) break;
+            const int ty = tyr[d];
+            const double ti = tr[d];
+            const int in = i + kSchedDepth;
+            tyr[d] = in < a.T ? a.etype[int64_t(in) * B + f] : 255;
+            tr[d] = in < a.T ? a.t[int64_t(in) * B + f] : 0.0;
+            if (ty == 255) continue;  // padding of a ragged stream
+            const int cls = ty == kGps ? 0 : 1;
+            const bool window = ti - prev < period;  // still inside the window: queue it
+            if (window || q_len == 0) {  // a trigger with an empty queue is its own candidate
+                if (qi[cls] < 0) {
+                    qi[cls] = i;
+                    qt[cls] = ty;
+                    qtime[cls] = ti;
+                }
+                ++q_len;
+                if (window) continue;
             }
-        }
-        q_len = 0;
-        const double tsel = a.t[int64_t(sel) * B + f];
-        T pay[9];
-        // the selected event differs per lane: plain 64-bit addressing (a buffer descriptor per
-        // lane would be a waterfall loop)
-        const T* ps = static_cast<const T*>(a.payload) + int64_t(sel) * 9 * B + f;
+            // greedy_schedule (kf_workers.py:195-213)
+            const T g0 = qi[0] >= 0 ? first_row_gain(s, kGps) : T(0);
+            const T g1 = qi[1] >= 0 ? first_row_gain(s, kImu) : T(0);
+            const bool v0 = qi[0] >= 0 && g0 == g0, v1 = qi[1] >= 0 && g1 == g1;
+            int c;
+            if (v0 && v1) c = g0 > g1 ? 0 : (g1 > g0 ? 1 : (qi[0] < qi[1] ? 0 : 1));
+            else if (v0) c = 0;
+            else if (v1) c = 1;
+            else c = (qi[0] >= 0 && (qi[1] < 0 || qi[0] < qi[1])) ? 0 : 1;  // the queue's first
+            const int sel = qi[c];
+            const double tsel = qtime[c];
+            const int tsel_type = qt[c];
+            q_len = 0;
+            qi[0] = qi[1] = -1;
+            T pay[9];
+            // the selected event differs per lane: plain 64-bit addressing (a buffer descriptor per
+            // lane would be a waterfall loop)
+            const T* ps = static_cast<const T*>(a.payload) + int64_t(sel) * 9 * B + f;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) pay[k] = ps[int64_t(k) * B];
-        bool ok = true;
-        s.template event<false>(a.etype[int64_t(sel) * B + f], T(tsel - prev), pay, false, T(0), ok);
-        if (!ok) {
-            st = kNotSpd;
-            s.fill_nan();
-        }
-        if (a.traj) {
-            T* tr = static_cast<T*>(a.traj) + int64_t(nsel) * 6 * B + f;
+            for (int k = 0; k < 9; ++k) pay[k] = ps[int64_t(k) * B];
+            bool ok = true;
+            s.template event<false>(tsel_type, T(tsel - prev), pay, false, T(0), ok);
+            if (!ok) {
+                st = kNotSpd;
+                s.fill_nan();
+            }
+            if (a.traj) {
+                T* tro = static_cast<T*>(a.traj) + int64_t(nsel) * 6 * B + f;
 #pragma unroll
-            for (int k = 0; k < 6; ++k) tr[int64_t(k) * B] = s.x[k];
+                for (int k = 0; k < 6; ++k) tro[int64_t(k) * B] = s.x[k];
+            }
+            if (a.logdet) static_cast<T*>(a.logdet)[int64_t(nsel) * B + f] = s.logdet();
+            if (a.sel_time) a.sel_time[int64_t(nsel) * B + f] = tsel;
+            ++nsel;
+            prev = tsel;
         }
-        if (a.logdet) static_cast<T*>(a.logdet)[int64_t(nsel) * B + f] = s.logdet();
-        if (a.sel_time) a.sel_time[int64_t(nsel) * B + f] = tsel;
-        ++nsel;
-        prev = tsel;
     }
     if (a.n_sel) a.n_sel[f] = nsel;
     s.store(a.x, a.P, rb, off);

@@ -436,6 +436,52 @@ def test_sampling_sweep_one_launch(golden_dir):
         assert _rel(P, rP) <= TOL, f
 
 
+@pytest.mark.parametrize('seed', [0, 1])
+def test_scheduled_random_streams_vs_oracle(seed):
+    """kf_run_scheduled over independent random streams (a GPS fix at random positions, 200 Hz
+    with jitter, ragged ends, every lane its own rate, so the lanes of a wave trigger at
+    different events), each filter against the oracle's greedy driver (kf_workers.py:826-957)
+    from the same warm start."""
+    rng = np.random.default_rng(seed)
+    B, T = 48, 120
+    t0 = 1697739278.761565
+    rates = rng.choice([10, 20, 35, 50, 75, 120, 160, 400], B).astype(np.float64)
+    etype = np.where(rng.random((T, B)) < 0.15, 0, 1).astype(np.uint8)
+    tt = t0 + np.cumsum(rng.uniform(0.003, 0.007, (T, B)), axis=0)
+    pay = rng.normal(0, 1, (T, 9, B))
+    pay[:, 0:3] *= 0.05
+    pay[:, 6:9] *= 0.3
+    pay[:, 0:3] = np.where((etype == 0)[:, None, :], pay[:, 0:3] * 60, pay[:, 0:3])
+    lens = rng.integers(T // 2, T + 1, B)
+    for f in range(B):
+        etype[lens[f]:, f] = 255
+    x0 = np.zeros((15, B))
+    x0[0:6] = rng.normal(0, 2, (6, B))
+    Pblk = np.repeat(ref15.to_blocks(ref_kf.P0_REF15)[:, None], B, axis=1)
+    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    kf.set_state(x0, Pblk)
+    tr, ld, stt, ns = kf.run_scheduled(tt, etype, pay, np.full(B, t0), rates)
+    tr, ld, stt, ns = (v.cpu().numpy() for v in (tr, ld, stt, ns))
+    kf.close()
+    for f in range(B):
+        ev = [(0, 'GPS', t0, {'easting': 0.0, 'northing': 0.0, 'altitude': 0.0})]  # skipped (warm start)
+        for i in range(lens[f]):
+            if etype[i, f] == 0:
+                ev.append((i + 1, 'GPS', tt[i, f], {'easting': pay[i, 0, f], 'northing': pay[i, 1, f],
+                                                    'altitude': pay[i, 2, f]}))
+            else:
+                ev.append((i + 1, 'IMU', tt[i, f], ['t', *pay[i, :, f]]))
+        rs, rl, _ = ref_kf.run_kalman_filter_scheduled(ev, 0, len(ev), ref_kf.P0_REF15.copy(),
+                                                       (t0, *x0[0:6, f]), 'greedy', rates[f])
+        n = int(ns[f])
+        assert n == len(rs) - 1, f
+        if n == 0:
+            continue
+        assert _rel(stt[:n, f], [r[0] for r in rs[1:]]) <= 1e-12, f
+        assert _rel(tr[:n, :, f], np.array([r[1:7] for r in rs[1:]])) <= TOL, f
+        assert _rel(ld[:n, f], rl[1:]) <= TOL, f
+
+
 def test_score_candidates_random_batch():
     """kf_score_candidates over a batch of random block-diagonal covariances vs the oracle's
     Scheduler.cov_matrix trace (first row and full)."""

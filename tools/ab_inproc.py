@@ -58,6 +58,8 @@ def main():
         w = bench.bf_workload(cfg, ns, 0, 1, dev)
     elif args.config == '1':
         w = bench.log_workload(cfg, ns, 0, 1, dev)
+    elif args.config == 'sched':
+        w = bench.sched_workload(cfg, ns, 0, 1, dev)
     else:
         w = bench.cv_workload(args.config, cfg, ns, 0, 1, dev)
     stream = torch.cuda.current_stream(dev)
