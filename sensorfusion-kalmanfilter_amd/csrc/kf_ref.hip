@@ -2241,15 +2241,75 @@ __global__ __launch_bounds__(kBlock) void ref15_score_kernel(const Ref15ScoreArg
 // queued GPS fix or the first queued other event (ties: whichever came first; a NaN gain is
 // never picked, and with none pickable the queue's first event is, as the reference's loop
 // leaves best_i at its start).  Each lane tracks those two candidates (index, type, time) as
-// events are queued, and reads the payload of the picked one only.  The event types and times
-// are prefetched kSchedDepth events ahead (their loads do not depend on the lane's branches).
-#ifndef KF_SCHED_DEPTH
-#define KF_SCHED_DEPTH 1
-#endif
-constexpr int kSchedDepth = KF_SCHED_DEPTH;
+// events are queued, and reads the payload of the picked one only.
+template <typename T>
+struct SchedLane {
+    Ref15<T> s;
+    int32_t st;
+    double prev, period;
+    int q_len = 0, nsel = 0;
+    int qi[2] = {-1, -1}, qt[2] = {0, 0};  // per class (0: GPS fix, 1: any other event)
+    double qtime[2] = {0.0, 0.0};
+
+    // event i (type ty at time ti) of filter f (kf_workers.py:870-957)
+    __device__ __forceinline__ void event(const Ref15SchedArgs& a, int64_t f, int i, int ty, double ti) {
+        if (ty == 255) return;  // padding of a ragged stream
+        const int64_t B = a.B;
+        const int cls = ty == kGps ? 0 : 1;
+        const bool window = ti - prev < period;  // still inside the window: queue it
+        if (window || q_len == 0) {  // a trigger with an empty queue is its own candidate
+            if (qi[cls] < 0) {
+                qi[cls] = i;
+                qt[cls] = ty;
+                qtime[cls] = ti;
+            }
+            ++q_len;
+            if (window) return;
+        }
+        // greedy_schedule (kf_workers.py:195-213); with one class queued its first event is
+        // the pick whatever the gain (a NaN gain leaves the queue's first, the same event)
+        int c = qi[0] >= 0 ? 0 : 1;
+        if (qi[0] >= 0 && qi[1] >= 0) {
+            const T g0 = first_row_gain(s, kGps), g1 = first_row_gain(s, kImu);
+            const bool v0 = g0 == g0, v1 = g1 == g1;
+            if (v0 && v1) c = g0 > g1 ? 0 : (g1 > g0 ? 1 : (qi[0] < qi[1] ? 0 : 1));
+            else if (v0) c = 0;
+            else if (v1) c = 1;
+            else c = qi[0] < qi[1] ? 0 : 1;  // the queue's first
+        }
+        const int sel = qi[c];
+        const double tsel = qtime[c];
+        const int tsel_type = qt[c];
+        q_len = 0;
+        qi[0] = qi[1] = -1;
+        T pay[9];
+        // the selected event differs per lane: plain 64-bit addressing (a buffer descriptor per
+        // lane would be a waterfall loop)
+        const T* ps = static_cast<const T*>(a.payload) + int64_t(sel) * 9 * B + f;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) pay[k] = ps[int64_t(k) * B];
+        bool ok = true;
+        s.template event<false>(tsel_type, T(tsel - prev), pay, false, T(0), ok);
+        if (!ok) {
+            st = kNotSpd;
+            s.fill_nan();
+        }
+        if (a.traj) {
+            T* tro = static_cast<T*>(a.traj) + int64_t(nsel) * 6 * B + f;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) tro[int64_t(k) * B] = s.x[k];
+        }
+        if (a.logdet) static_cast<T*>(a.logdet)[int64_t(nsel) * B + f] = s.logdet();
+        if (a.sel_time) a.sel_time[int64_t(nsel) * B + f] = tsel;
+        ++nsel;
+        prev = tsel;
+    }
+};
+
 #ifndef KF_SCHED_WAVES
 #define KF_SCHED_WAVES 2
 #endif
+// Any B: the next event's type and time are loaded one event ahead in registers.
 template <typename T>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED_WAVES))) void ref15_sched_kernel(
     const Ref15SchedArgs a) {
@@ -2258,85 +2318,88 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED
     const int64_t B = a.B;
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(B) * uint32_t(sizeof(T));
-    Ref15<T> s;
-    s.load(a.x, a.P, rb, off);
-    int32_t st = a.status[f];
-    double prev = a.prev_time[f];
-    const double period = 1.0 / (a.freq ? a.freq[f] : a.freq_all);  // kf_workers.py:880
-    // the queue: its length and, per class (0: GPS fix, 1: any other event), the first queued
-    // event's index, type and time
-    int q_len = 0, nsel = 0;
-    int qi[2] = {-1, -1}, qt[2] = {0, 0};
-    double qtime[2] = {0.0, 0.0};
-    int tyr[kSchedDepth];
-    double tr[kSchedDepth];
-#pragma unroll
-    for (int d = 0; d < kSchedDepth; ++d) {
-        tyr[d] = d < a.T ? a.etype[int64_t(d) * B + f] : 255;
-        tr[d] = d < a.T ? a.t[int64_t(d) * B + f] : 0.0;
-    }
-    for (int i0 = 0; i0 < a.T; i0 += kSchedDepth) {
-#pragma unroll
-        for (int d = 0; d < kSchedDepth; ++d) {
-            const int i = i0 + d;
-            if (i >= a.T) break;
-            const int ty = tyr[d];
-            const double ti = tr[d];
-            const int in = i + kSchedDepth;
-            tyr[d] = in < a.T ? a.etype[int64_t(in) * B + f] : 255;
-            tr[d] = in < a.T ? a.t[int64_t(in) * B + f] : 0.0;
-            if (ty == 255) continue;  // padding of a ragged stream
-            const int cls = ty == kGps ? 0 : 1;
-            const bool window = ti - prev < period;  // still inside the window: queue it
-            if (window || q_len == 0) {  // a trigger with an empty queue is its own candidate
-                if (qi[cls] < 0) {
-                    qi[cls] = i;
-                    qt[cls] = ty;
-                    qtime[cls] = ti;
-                }
-                ++q_len;
-                if (window) continue;
-            }
-            // greedy_schedule (kf_workers.py:195-213)
-            const T g0 = qi[0] >= 0 ? first_row_gain(s, kGps) : T(0);
-            const T g1 = qi[1] >= 0 ? first_row_gain(s, kImu) : T(0);
-            const bool v0 = qi[0] >= 0 && g0 == g0, v1 = qi[1] >= 0 && g1 == g1;
-            int c;
-            if (v0 && v1) c = g0 > g1 ? 0 : (g1 > g0 ? 1 : (qi[0] < qi[1] ? 0 : 1));
-            else if (v0) c = 0;
-            else if (v1) c = 1;
-            else c = (qi[0] >= 0 && (qi[1] < 0 || qi[0] < qi[1])) ? 0 : 1;  // the queue's first
-            const int sel = qi[c];
-            const double tsel = qtime[c];
-            const int tsel_type = qt[c];
-            q_len = 0;
-            qi[0] = qi[1] = -1;
-            T pay[9];
-            // the selected event differs per lane: plain 64-bit addressing (a buffer descriptor per
-            // lane would be a waterfall loop)
-            const T* ps = static_cast<const T*>(a.payload) + int64_t(sel) * 9 * B + f;
-#pragma unroll
-            for (int k = 0; k < 9; ++k) pay[k] = ps[int64_t(k) * B];
-            bool ok = true;
-            s.template event<false>(tsel_type, T(tsel - prev), pay, false, T(0), ok);
-            if (!ok) {
-                st = kNotSpd;
-                s.fill_nan();
-            }
-            if (a.traj) {
-                T* tro = static_cast<T*>(a.traj) + int64_t(nsel) * 6 * B + f;
-#pragma unroll
-                for (int k = 0; k < 6; ++k) tro[int64_t(k) * B] = s.x[k];
-            }
-            if (a.logdet) static_cast<T*>(a.logdet)[int64_t(nsel) * B + f] = s.logdet();
-            if (a.sel_time) a.sel_time[int64_t(nsel) * B + f] = tsel;
-            ++nsel;
-            prev = tsel;
+    SchedLane<T> L;
+    L.s.load(a.x, a.P, rb, off);
+    L.st = a.status[f];
+    L.prev = a.prev_time[f];
+    L.period = 1.0 / (a.freq ? a.freq[f] : a.freq_all);  // kf_workers.py:880
+    int tyn = a.T > 0 ? a.etype[f] : 255;
+    double tn = a.T > 0 ? a.t[f] : 0.0;
+    for (int i = 0; i < a.T; ++i) {
+        const int ty = tyn;
+        const double ti = tn;
+        if (i + 1 < a.T) {
+            tyn = a.etype[int64_t(i + 1) * B + f];
+            tn = a.t[int64_t(i + 1) * B + f];
         }
+        L.event(a, f, i, ty, ti);
     }
-    if (a.n_sel) a.n_sel[f] = nsel;
-    s.store(a.x, a.P, rb, off);
-    a.status[f] = st;
+    if (a.n_sel) a.n_sel[f] = L.nsel;
+    L.s.store(a.x, a.P, rb, off);
+    a.status[f] = L.st;
+}
+
+// B % 64 == 0: the event types and times travel HBM -> LDS by buffer_load ... lds, kSchedChunk
+// events at a time into one of two per-wave images while the previous chunk is consumed (the
+// queueing iterations are a few instructions each, so a register prefetch one event ahead
+// waited a memory latency per event, and a deeper one did not fit the registers).
+//   image: t rows [kSchedChunk][64] f64, then etype rows [kSchedChunk][64] u8
+constexpr int kSchedChunk = 16;
+constexpr int kSchedImg = kSchedChunk * 512 + kSchedChunk * 64;
+template <typename T>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED_WAVES))) void ref15_sched_lds_kernel(
+    const Ref15SchedArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * 2 * kSchedImg];
+    const int lane = int(threadIdx.x & 63);
+    const int wave = wave_uniform(int(threadIdx.x >> 6));
+    const int64_t f0 = int64_t(blockIdx.x) * kBlock + int64_t(wave) * 64;
+    if (f0 >= a.B) return;  // whole waves (B % 64 == 0)
+    const int64_t f = f0 + lane;
+    const int64_t B = a.B;
+    unsigned char* const img0 = lds + wave * 2 * kSchedImg;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(B) * uint32_t(sizeof(T));
+    SchedLane<T> L;
+    L.s.load(a.x, a.P, rb, off);
+    L.st = a.status[f];
+    L.prev = a.prev_time[f];
+    L.period = 1.0 / (a.freq ? a.freq[f] : a.freq_all);
+    waitcnt<vmcnt_imm(0)>();
+    // t: one 16-B-per-lane DMA moves two rows (lanes 0-31 row r, 32-63 row r + 1); etype: one
+    // moves 16 rows of 64 bytes (4 lanes per row)
+    const uint32_t voff_t = uint32_t(lane >> 5) * uint32_t(B) * 8u + uint32_t(lane & 31) * 16u;
+    const uint32_t voff_e = uint32_t(lane >> 2) * uint32_t(B) + uint32_t(lane & 3) * 16u;
+    auto issue = [&](int c, unsigned char* img) {
+        const int r0 = c * kSchedChunk;
+        const int nr = a.T - r0 < kSchedChunk ? a.T - r0 : kSchedChunk;  // rows of this chunk (>= 1)
+#pragma unroll
+        for (int k = 0; k < kSchedChunk / 2; ++k) {
+            if (2 * k >= nr) break;  // wave-uniform
+            const char* tb = reinterpret_cast<const char*>(a.t) + (int64_t(r0 + 2 * k) * B + f0) * 8;
+            const uint32_t span = 2 * k + 1 < nr ? uint32_t(B) * 8u + 512u : 512u;
+            lds_dma16(bytes_rsrc(tb, span), img + k * 1024, voff_t, 0);
+        }
+        const char* eb = reinterpret_cast<const char*>(a.etype) + int64_t(r0) * B + f0;
+        lds_dma16(bytes_rsrc(eb, uint32_t(nr - 1) * uint32_t(B) + 64u), img + kSchedChunk * 512, voff_e, 0);
+    };
+    const int nch = (a.T + kSchedChunk - 1) / kSchedChunk;
+    if (nch > 0) issue(0, img0);
+    for (int c = 0; c < nch; ++c) {
+        // this chunk's image has landed, the other image's reads are done (vmcnt also counts
+        // the stores of the chunk before: once per chunk)
+        waitcnt<0>();
+        unsigned char* const img = img0 + (c & 1) * kSchedImg;
+        if (c + 1 < nch) issue(c + 1, img0 + ((c + 1) & 1) * kSchedImg);
+        const double* ti_img = reinterpret_cast<const double*>(img) + lane;
+        const unsigned char* ty_img = img + kSchedChunk * 512 + lane;
+        const int r0 = c * kSchedChunk;
+        const int nr = a.T - r0 < kSchedChunk ? a.T - r0 : kSchedChunk;
+#pragma unroll 1
+        for (int d = 0; d < nr; ++d) L.event(a, f, r0 + d, int(ty_img[d * 64]), ti_img[d * 64]);
+    }
+    if (a.n_sel) a.n_sel[f] = L.nsel;
+    L.s.store(a.x, a.P, rb, off);
+    a.status[f] = L.st;
 }
 
 }  // namespace
@@ -2350,8 +2413,18 @@ hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t str
 
 hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream) {
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-    if (f64) ref15_sched_kernel<double><<<grid, kBlock, 0, stream>>>(a);
-    else ref15_sched_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    // the LDS variant's descriptors: whole waves, and a chunk's row spans within 32-bit ranges
+    const char* v = std::getenv("KFMI_SCHED");
+    const bool lds = a.B % 64 == 0 && uint64_t(a.B) * 8 * 2 < (uint64_t(1) << 32) &&
+                     reinterpret_cast<uintptr_t>(a.t) % 16 == 0 && reinterpret_cast<uintptr_t>(a.etype) % 16 == 0 &&
+                     uint64_t(a.B) * kSchedChunk < (uint64_t(1) << 32) && !(v && !std::strcmp(v, "regs"));
+    if (lds) {
+        if (f64) ref15_sched_lds_kernel<double><<<grid, kBlock, 0, stream>>>(a);
+        else ref15_sched_lds_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    } else {
+        if (f64) ref15_sched_kernel<double><<<grid, kBlock, 0, stream>>>(a);
+        else ref15_sched_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    }
     return hipGetLastError();
 }
 
