@@ -2248,40 +2248,47 @@ struct SchedLane {
     int32_t st;
     double prev, period;
     int q_len = 0, nsel = 0;
-    int qi[2] = {-1, -1}, qt[2] = {0, 0};  // per class (0: GPS fix, 1: any other event)
-    double qtime[2] = {0.0, 0.0};
+    // per class (0: GPS fix, 1: any other event) the first queued event's index (-1: none),
+    // type and time; named scalars, not arrays (an array indexed by a runtime class went to
+    // scratch memory)
+    int qi0 = -1, qi1 = -1, qt0 = 0, qt1 = 0;
+    double qtime0 = 0.0, qtime1 = 0.0;
 
     // event i (type ty at time ti) of filter f (kf_workers.py:870-957)
     __device__ __forceinline__ void event(const Ref15SchedArgs& a, int64_t f, int i, int ty, double ti) {
         if (ty == 255) return;  // padding of a ragged stream
         const int64_t B = a.B;
-        const int cls = ty == kGps ? 0 : 1;
+        const bool gps = ty == kGps;
         const bool window = ti - prev < period;  // still inside the window: queue it
         if (window || q_len == 0) {  // a trigger with an empty queue is its own candidate
-            if (qi[cls] < 0) {
-                qi[cls] = i;
-                qt[cls] = ty;
-                qtime[cls] = ti;
+            if (gps && qi0 < 0) {
+                qi0 = i;
+                qt0 = ty;
+                qtime0 = ti;
+            }
+            if (!gps && qi1 < 0) {
+                qi1 = i;
+                qt1 = ty;
+                qtime1 = ti;
             }
             ++q_len;
             if (window) return;
         }
         // greedy_schedule (kf_workers.py:195-213); with one class queued its first event is
         // the pick whatever the gain (a NaN gain leaves the queue's first, the same event)
-        int c = qi[0] >= 0 ? 0 : 1;
-        if (qi[0] >= 0 && qi[1] >= 0) {
+        bool pick0 = qi0 >= 0;
+        if (qi0 >= 0 && qi1 >= 0) {
             const T g0 = first_row_gain(s, kGps), g1 = first_row_gain(s, kImu);
             const bool v0 = g0 == g0, v1 = g1 == g1;
-            if (v0 && v1) c = g0 > g1 ? 0 : (g1 > g0 ? 1 : (qi[0] < qi[1] ? 0 : 1));
-            else if (v0) c = 0;
-            else if (v1) c = 1;
-            else c = qi[0] < qi[1] ? 0 : 1;  // the queue's first
+            if (v0 && v1) pick0 = g0 > g1 ? true : (g1 > g0 ? false : qi0 < qi1);
+            else if (v0 != v1) pick0 = v0;
+            else pick0 = qi0 < qi1;  // the queue's first
         }
-        const int sel = qi[c];
-        const double tsel = qtime[c];
-        const int tsel_type = qt[c];
+        const int sel = pick0 ? qi0 : qi1;
+        const double tsel = pick0 ? qtime0 : qtime1;
+        const int tsel_type = pick0 ? qt0 : qt1;
         q_len = 0;
-        qi[0] = qi[1] = -1;
+        qi0 = qi1 = -1;
         T pay[9];
         // the selected event differs per lane: plain 64-bit addressing (a buffer descriptor per
         // lane would be a waterfall loop)
