@@ -658,9 +658,11 @@ def sched_workload(cfg, args, rank, world, dev):
     # status read + written, n_sel written
     nbytes = B * T * 9 + n_selected * (72 + 64) + B * (2 * 42 * 8 + 8 + 8 + 8 + 4)
     return dict(step=step, units=B * T, bytes=nbytes, bytes_per_unit=nbytes / (B * T),
-                kernel='ref15_sched_kernel', traffic=None, cpu=cpu, gather=None, kf=kf,
-                roofline_note=f'{n_selected / (B * T):.3f} of the examined events are selected and applied; '
-                              'the queue scan re-reads the window\'s types from cache',
+                kernel='ref15_sched_lds_kernel' if B % 64 == 0 else 'ref15_sched_kernel', traffic=None, cpu=cpu,
+                gather=None, kf=kf,
+                roofline_note=f'{n_selected / (B * T):.3f} of the examined events are selected and applied (a '
+                              f'full 15-state event each, its payload gathered per lane); latency / issue-bound at '
+                              f'2 waves per SIMD',
                 desc=f'SURVEY 8f row 3: rate-decimated greedy scheduled filter (kf_workers.py:826-957), reference '
                      f'15-state model, f64, B={B} filters/GPU, T={T} events at 200 Hz (GPS every {k}th), '
                      f'processing rates {cfg["rates"][0]}..{cfg["rates"][-1]} Hz across the batch (64 filters per rate)',
