@@ -33,3 +33,12 @@ for rep in range(3):
     t2 = time.perf_counter()
     print(f'rep {rep}: H2D {1e3 * (t1 - t0):.1f} ms, ingest_arrays (device columns) {1e3 * (t2 - t1):.1f} ms, '
           f'{len(s)} events')
+
+# the oracle's restatement of the reference's ingest (oracle/ref_ingest.ingest: csv module,
+# per-row Python loops as kf_workers.py:290-385) on the same files, 1 core: the CPU baseline
+sys.path.insert(0, ROOT)
+from oracle import ref_ingest  # noqa: E402
+t0 = time.perf_counter()
+ev = ref_ingest.ingest(gp, ip)[0]
+el = time.perf_counter() - t0
+print(f'oracle ingest (Python, 1 core): {1e3 * el:.0f} ms, {len(ev)} events, {len(ev) / el:.3g} events/s')
