@@ -133,6 +133,37 @@ int n_threads(size_t bytes) {
     return std::max(1, std::min<int>(t, static_cast<int>(bytes / per) + 1));
 }
 
+// newline-aligned chunks of [b, e), one per thread
+std::vector<std::pair<const char*, const char*>> split_lines(const char* b, const char* e) {
+    const int nt = n_threads(static_cast<size_t>(e - b));
+    std::vector<std::pair<const char*, const char*>> ch;
+    const char* s = b;
+    for (int i = 0; i < nt && s < e; ++i) {
+        const char* t = (i == nt - 1) ? e : b + (e - b) * (i + 1) / nt;
+        if (t < s) t = s;
+        if (t < e) {
+            const char* nl = static_cast<const char*>(std::memchr(t, '\n', e - t));
+            t = nl ? nl + 1 : e;
+        }
+        ch.emplace_back(s, t);
+        s = t;
+    }
+    return ch;
+}
+
+// count_rows over newline-aligned chunks in parallel (a line never straddles two chunks, so the
+// per-chunk counts add up)
+int64_t count_rows_parallel(const char* b, const char* e) {
+    const auto ch = split_lines(b, e);
+    std::vector<int64_t> n(ch.size(), 0);
+    std::vector<std::thread> th;
+    for (size_t i = 0; i < ch.size(); ++i) th.emplace_back([&, i] { n[i] = count_rows(ch[i].first, ch[i].second); });
+    for (auto& t : th) t.join();
+    int64_t total = 0;
+    for (int64_t v : n) total += v;
+    return total;
+}
+
 }  // namespace
 
 extern "C" {
@@ -142,7 +173,7 @@ int kf_csv_shape(const char* path, int has_header, int64_t* rows, int* cols) {
     if (int rc = map_file(path, m)) return rc;
     const char *b, *e;
     data_range(m, has_header, b, e);
-    int64_t n = count_rows(b, e);
+    int64_t n = count_rows_parallel(b, e);
     // trailing blank lines (a file ending in "\n\n") are not rows of data
     while (n > 0) {
         const char* le = e;
@@ -173,19 +204,8 @@ int kf_csv_read(const char* path, int has_header, int ncols, double* out, int64_
     const char *b, *e;
     data_range(m, has_header, b, e);
     // newline-aligned chunks, one per thread
-    const int nt = n_threads(static_cast<size_t>(e - b));
     std::vector<Chunk> ch;
-    const char* s = b;
-    for (int i = 0; i < nt && s < e; ++i) {
-        const char* t = (i == nt - 1) ? e : b + (e - b) * (i + 1) / nt;
-        if (t < s) t = s;
-        if (t < e) {
-            const char* nl = static_cast<const char*>(std::memchr(t, '\n', e - t));
-            t = nl ? nl + 1 : e;
-        }
-        ch.push_back(Chunk{s, t, 0, 0});
-        s = t;
-    }
+    for (const auto& c : split_lines(b, e)) ch.push_back(Chunk{c.first, c.second, 0, 0});
     {
         std::vector<std::thread> th;
         for (auto& c : ch) th.emplace_back([&c] { c.rows = count_rows(c.b, c.e); });
