@@ -241,7 +241,8 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
             times1.append(time.perf_counter() - t0)
         el1 = min(times1[1:])
         w = 8 if cfg['dtype'] == 'f64' else 4
-        nt = kf.n * (kf.n + 1) // 2
+        # the per-axis blocks of P (block-diagonal handle: kf_predict / kf_update move only them)
+        nt = 3 * d
         # predict: state + u in, state out; update: state + z in, state + log-det out
         nbytes = B * T * w * ((kf.n + nt) * 4 + 2 * d + 1)
         return {'value': B * T / el, 'unit': 'KF steps/s', 'ms_per_step': el / T * 1e3,

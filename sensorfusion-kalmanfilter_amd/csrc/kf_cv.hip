@@ -100,6 +100,35 @@ __device__ __forceinline__ void store_state(const CvArgs& a, uint32_t rb, uint32
     for (int k = 0; k < D * (2 * D + 1); ++k) stb(a.P, k, rb, off, P[k]);
 }
 
+// BLOCK: P is block-diagonal over the axes (CvArgs::block_p: the handle's P started so and a
+// diagonal R keeps it so), so only the same-axis entries are read and written; the others are
+// compile-time zeros, which also removes their arithmetic.
+template <int D, typename T, bool BLOCK>
+__device__ __forceinline__ void load_state_b(const CvArgs& a, uint32_t rb, uint32_t off, T (&x)[2 * D],
+                                             T (&P)[D * (2 * D + 1)]) {
+    constexpr int N = 2 * D;
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = ldb<T>(a.x, i, rb, off);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = i; j < N; ++j)
+            P[tri<N>(i, j)] = (!BLOCK || i % D == j % D) ? ldb<T>(a.P, tri<N>(i, j), rb, off) : T(0);
+}
+
+template <int D, typename T, bool BLOCK>
+__device__ __forceinline__ void store_state_b(const CvArgs& a, uint32_t rb, uint32_t off, const T (&x)[2 * D],
+                                              const T (&P)[D * (2 * D + 1)]) {
+    constexpr int N = 2 * D;
+#pragma unroll
+    for (int i = 0; i < N; ++i) stb(a.x, i, rb, off, x[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = i; j < N; ++j)
+            if (!BLOCK || i % D == j % D) stb(a.P, tri<N>(i, j), rb, off, P[tri<N>(i, j)]);
+}
+
 template <int D, typename T>
 __device__ __forceinline__ void load_R(const CvArgs& a, T (&R)[D * (D + 1) / 2]) {
 #pragma unroll
@@ -417,7 +446,7 @@ __global__ __launch_bounds__(kBlock) void cv_offblock_kernel(const CvArgs a, int
 }
 
 // Single predict step (kf_predict): optional per-filter dt and logdet of the prediction.
-template <int D, typename T>
+template <int D, typename T, bool BLOCK>
 __global__ __launch_bounds__(kBlock) void cv_predict_kernel(const CvArgs a) {
     using K = Cv<D, T>;
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -425,13 +454,13 @@ __global__ __launch_bounds__(kBlock) void cv_predict_kernel(const CvArgs a) {
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
     T x[K::N], P[K::NT];
-    load_state<D, T>(a, rb, off, x, P);
+    load_state_b<D, T, BLOCK>(a, rb, off, x, P);
     T u[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) u[i] = a.u ? ldb<T>(a.u, i, rb, off) : T(0);
     const double dtd = a.dt_filter ? a.dt_filter[f] : a.dt;
     K::predict(x, P, T(dtd), u, T(a.q_pos * dtd), T(a.q_vel * dtd));
-    store_state<D, T>(a, rb, off, x, P);
+    store_state_b<D, T, BLOCK>(a, rb, off, x, P);
     if (a.logdet) {
         const T ld = logdet_ldl<K::N, T>(P);
         stb(a.logdet, 0, rb, off, ld);
@@ -440,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void cv_predict_kernel(const CvArgs a) {
 }
 
 // Single GPS update (kf_update).
-template <int D, typename T>
+template <int D, typename T, bool BLOCK>
 __global__ __launch_bounds__(kBlock) void cv_update_kernel(const CvArgs a) {
     using K = Cv<D, T>;
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -448,7 +477,7 @@ __global__ __launch_bounds__(kBlock) void cv_update_kernel(const CvArgs a) {
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
     T x[K::N], P[K::NT];
-    load_state<D, T>(a, rb, off, x, P);
+    load_state_b<D, T, BLOCK>(a, rb, off, x, P);
     T R[K::MT];
     load_R<D, T>(a, R);
     T z[K::M];
@@ -456,9 +485,9 @@ __global__ __launch_bounds__(kBlock) void cv_update_kernel(const CvArgs a) {
     for (int i = 0; i < K::M; ++i) z[i] = ldb<T>(a.z, i, rb, off);
     int32_t st = a.status[f];
     if (!a.mask || a.mask[f] != 0) {
-        if (!K::template update<false>(x, P, z, R)) st = kNotSpd;
+        if (!K::template update<BLOCK>(x, P, z, R)) st = kNotSpd;
     }
-    store_state<D, T>(a, rb, off, x, P);
+    store_state_b<D, T, BLOCK>(a, rb, off, x, P);
     if (a.logdet) {
         const T ld = logdet_ldl<K::N, T>(P);
         if (!(ld == ld)) st = kNotSpd;
@@ -593,8 +622,14 @@ hipError_t launch_cv_t(Op op, const CvArgs& a, hipStream_t st) {
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
     switch (op) {
         case Op::Run: return launch_run<D, T>(a, grid, st);
-        case Op::Predict: cv_predict_kernel<D, T><<<grid, kBlock, 0, st>>>(a); break;
-        case Op::Update: cv_update_kernel<D, T><<<grid, kBlock, 0, st>>>(a); break;
+        case Op::Predict:
+            if (a.block_p) cv_predict_kernel<D, T, true><<<grid, kBlock, 0, st>>>(a);
+            else cv_predict_kernel<D, T, false><<<grid, kBlock, 0, st>>>(a);
+            break;
+        case Op::Update:
+            if (a.block_p) cv_update_kernel<D, T, true><<<grid, kBlock, 0, st>>>(a);
+            else cv_update_kernel<D, T, false><<<grid, kBlock, 0, st>>>(a);
+            break;
         case Op::Reset: cv_reset_kernel<D, T><<<grid, kBlock, 0, st>>>(a); break;
     }
     return hipGetLastError();
