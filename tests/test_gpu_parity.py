@@ -386,3 +386,37 @@ def test_block_check_falls_back_for_coupled_covariance():
         rt, rl, _, _ = ref_kf.run_batch(model, x0, P, np.full(T, 0.1), u, z, 1)
         ex, el = ref_kf.parity_errors(tr, ld, rt, rl)
         assert ex <= 1e-6 and el <= 1e-6 and (st == 0).all()
+
+
+@pytest.mark.parametrize('name,dtype', [('cv3', 'f64'), ('cv2', 'f32'), ('cv3', 'f32')])
+@pytest.mark.parametrize('coupled', [False, True])
+def test_per_step_calls_block_and_coupled(name, dtype, coupled):
+    """predict()/update() per step from a set_state P: block-diagonal (the calls move only the
+    per-axis blocks) or coupling the axes (the calls move all of P), against the oracle loop."""
+    model = MODEL[name]
+    n, d = model.n, model.d
+    B, T = 96, 20
+    x0, u, z = random_inputs(model, B, T, 1, seed=11)
+    rng = np.random.default_rng(12)
+    A = rng.normal(size=(B, n, n))
+    P = np.einsum('bij,bkj->bik', A, A) + 50 * np.eye(n)
+    if not coupled:
+        for i in range(n):
+            for j in range(n):
+                if i % d != j % d:
+                    P[:, i, j] = 0.0
+    if dtype == 'f32':
+        x0, u, z, P = (rounded(v, 'f32') for v in (x0, u, z, P))
+    kf = kfmi.BatchedKF(name, B, dtype)
+    kf.set_state(torch.from_numpy(np.ascontiguousarray(x0.T.astype(NP[dtype]))).cuda(),
+                 torch.from_numpy(ref_kf.tri_pack(P).astype(NP[dtype])).cuda())
+    xs, lds = [], []
+    for t in range(T):
+        kf.predict(0.1, torch.from_numpy(np.ascontiguousarray(u[t].astype(NP[dtype]))).cuda())
+        lds.append(kf.update(torch.from_numpy(np.ascontiguousarray(z[t].astype(NP[dtype]))).cuda())
+                   .double().cpu().numpy())
+        xs.append(kf.state()[0].double().cpu().numpy())
+    kf.close()
+    rt, rl, _, _ = ref_kf.run_batch(model, x0, P, np.full(T, 0.1), u, z, 1)
+    ex, el = ref_kf.parity_errors(np.array(xs), np.array(lds), rt, rl)
+    assert ex <= TOL[dtype] and el <= TOL[dtype], (ex, el)
