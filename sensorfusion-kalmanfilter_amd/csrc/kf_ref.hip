@@ -1634,8 +1634,12 @@ constexpr int kMaxEvents = 64;
 template <typename T>
 using Ref15 = Chains<T, M15>;
 
+#ifndef KF_COMBO_WAVES
+#define KF_COMBO_WAVES 3  // waves per SIMD the one-filter-per-subset kernel is compiled for
+#endif
 template <typename T>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void ref15_combo_kernel(const Ref15ComboArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_COMBO_WAVES))) void ref15_combo_kernel(
+    const Ref15ComboArgs a) {
     __shared__ double s_ev[kMaxEvents * 11];
     __shared__ uint64_t s_binom[(kMaxEvents + 1) * (kMaxEvents + 1)];
     const int n = a.n_events;

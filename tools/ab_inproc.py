@@ -54,7 +54,7 @@ def main():
     ns = argparse.Namespace(ablate='none', gpus=1, no_cpu_baseline=True)
     if args.config == 'ref15':
         w = bench.ref15_workload(cfg, ns, 0, 1, dev)
-    elif args.config == 'bf':
+    elif args.config in ('bf', 'bf_subsets'):
         w = bench.bf_workload(cfg, ns, 0, 1, dev)
     elif args.config == '1':
         w = bench.log_workload(cfg, ns, 0, 1, dev)
