@@ -110,6 +110,13 @@ inline bool parse_field(const char* s, const char* t, double& v) {
     }
     if (s == t || *s == '+' || *s == '-') return false;
     auto r = std::from_chars(s, t, v, std::chars_format::general);
+    if (r.ec == std::errc::result_out_of_range && r.ptr == t) {
+        // float() gives inf, 0.0 or a subnormal there; from_chars leaves v unset: strtod rounds
+        // it (the C locale's '.', a NUL-terminated copy of the field)
+        const std::string f(s, t);
+        v = std::strtod(f.c_str(), nullptr);
+        r.ec = std::errc();
+    }
     if (r.ec != std::errc() || r.ptr != t) return false;
     if (neg) v = -v;
     return true;

@@ -167,3 +167,15 @@ def test_compat_model_matrices_are_the_reference_model():
     np.testing.assert_array_equal(sf.get_imu_measurement_noise_covariance_matrix(), ref_kf.R_imu15())
     t = kfw.CsvTable(np.array([[1.5, 2.0], [np.nan, 3.25]]))
     assert t[0] == ['1.5', 'nan'] and t[-1] == ['2.0', '3.25'] and len(t) == 2 and t[:1] == [t[0]]
+
+
+def test_csv_reader_out_of_range_like_float(tmp_path):
+    """Fields beyond the double range parse as float() parses them (inf, 0.0, subnormals), not
+    as errors: from_chars reports them out of range, the reader then rounds them with strtod."""
+    vals = ['1e400', '-1e400', '1e-400', '4.9406564584124654e-324', '2.2250738585072011e-308',
+            '123456789012345678901234567890e-350', '1.7976931348623159e308', '0.5']
+    p = tmp_path / 'r.csv'
+    p.write_text('v\n' + '\n'.join(vals) + '\n')
+    got = ingest.read_csv(str(p), 1)[0]
+    want = np.array([float(v) for v in vals])
+    assert (got.view(np.uint64) == want.view(np.uint64)).all(), (got, want)

@@ -102,6 +102,40 @@ int main(int argc, char** argv) {
         if (p[-1] == '\r') ++p;
     }
     CHECK(bad == 0);
-    std::printf("csv_asan: %d failure(s), %lld rows checked\n", failures, (long long)rows);
+    // decimal -> double edge shapes, one value per row, against strtod: every significant-digit
+    // count 1..21, exponents across the whole range (subnormals, overflow), halfway cases
+    std::string hard = "v\n";
+    std::vector<std::string> vals = {"9007199254740993", "9007199254740995", "2.2250738585072011e-308",
+                                     "2.2250738585072012e-308", "4.9406564584124654e-324", "2.4703282292062327e-324",
+                                     "2.4703282292062328e-324", "1.7976931348623157e308", "1.7976931348623159e308",
+                                     "1e400", "1e-400", "0.1", "0.30000000000000004", "123456789012345678901",
+                                     "0.000000000000000000000000000000000001", "1.", ".5", "0", "00.00e5",
+                                     "7.038531e-26", "1448997445238699", "9223372036854775808",
+                                     "1.00000000000000011102230246251565404236316680908203125",
+                                     "8.98846567431158e307", "5e-324", "3e-324", "-0.0", "+1.5E+3"};
+    const int nhard = argc > 2 ? std::atoi(argv[2]) : 300000;
+    for (int i = 0; i < nhard; ++i) {
+        const int nd = 1 + int(rnd() % 21);
+        std::string m;
+        for (int k = 0; k < nd; ++k) m += char('0' + (k == 0 ? 1 + rnd() % 9 : rnd() % 10));
+        const int dot = int(rnd() % (nd + 1));
+        if (dot < nd) m.insert(m.begin() + dot, '.');
+        const int e = int(rnd() % 680) - 360;
+        m += "e" + std::to_string(e);
+        vals.push_back(m);
+    }
+    for (auto& x : vals) hard += x + "\n";
+    const std::string ph = write_file(dir, "hard.csv", hard);
+    CHECK(read_all(ph, 1, 1, out, rows) == 0 && rows == int64_t(vals.size()));
+    int64_t bad2 = 0;
+    for (size_t i = 0; i < vals.size() && int64_t(i) < rows; ++i) {
+        const double w = std::strtod(vals[i].c_str(), nullptr);
+        if (std::memcmp(&w, &out[i], 8) != 0) {
+            if (bad2 < 5) std::fprintf(stderr, "mismatch %s: %.17g vs strtod %.17g\n", vals[i].c_str(), out[i], w);
+            ++bad2;
+        }
+    }
+    CHECK(bad2 == 0);
+    std::printf("csv_asan: %d failure(s), %lld + %zu values checked\n", failures, (long long)nbig * 4, vals.size());
     return failures ? 1 : 0;
 }
