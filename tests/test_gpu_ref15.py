@@ -528,3 +528,41 @@ def test_sharded_brute_force_single_rank(golden_dir):
     cand = events[s:e]
     assert [cand.index(ev) for ev in out['selected_sensors']] == list(g['selected'])
     assert _rel(out['log_determinants'], g['log_determinants']) <= TOL
+
+
+def test_search_full_size_sampled_vs_per_subset():
+    """The bench's full-size search (n = 25, all 2^25 - 1 subsets, exhaustive) against the
+    per-subset kernel: every subset of the smallest and largest sizes, and a 4096-subset window
+    of each middle size, compared through the search's subset_max (≤ 1e-12)."""
+    rng = np.random.default_rng(2025)
+    n = 25
+    t0 = 1697739552.3362827
+    ev = np.zeros((n, 11))
+    ev[:, 0] = t0 + 0.005 * np.arange(1, n + 1)
+    ev[:, 1] = 1
+    ev[::20, 1] = 0
+    ev[:, 2:5] = rng.normal(0, 0.05, (n, 3))
+    ev[:, 5:8] = rng.normal(0, 0.01, (n, 3))
+    ev[:, 8:11] = rng.normal(0, 0.3, (n, 3))
+    ev[ev[:, 1] == 0, 2:5] = rng.normal(0, 3, (int((ev[:, 1] == 0).sum()), 3))
+    Pw = np.diag([0.9, 0.9, 0.9, 0.02, 0.02, 0.02, 0.5, 0.5, 0.5, 0.05, 0.05, 0.05, 20.0, 20.0, 20.0])
+    init = np.concatenate([np.zeros(15), ref15.to_blocks(Pw)])
+    t_end = t0 + 0.005 * (n + 1)
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    kfound, _, acc, sm = kf.search_combos(ev, init, t0, t_end, -1e30, exhaustive=True, subset_max=True)
+    kf.close()
+    assert kfound == 0 and int(acc.sum()) == 0
+    sm = sm.cpu().numpy()
+    assert np.isnan(sm[0]) and np.isfinite(sm[1:]).all()
+    W = 4096
+    for k in range(1, n + 1):
+        total = math.comb(n, k)
+        off = 0 if total <= W else int(rng.integers(0, total - W))
+        cnt = min(W, total)
+        kc = kfmi.BatchedKF('ref15', cnt, 'f64')
+        mx, _, _ = kc.eval_combos(ev, init, t0, t_end, k, combo_offset=off, logdets=False)
+        mx = mx.cpu().numpy()
+        kc.close()
+        masks = np.array([sum(1 << i for i in ref15.unrank_combination(n, k, off + r)) for r in range(cnt)])
+        got = sm[masks]
+        assert np.max(np.abs(got - mx) / np.maximum(np.abs(mx), 1.0)) <= 1e-12, k
