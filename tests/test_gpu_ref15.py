@@ -566,3 +566,42 @@ def test_search_full_size_sampled_vs_per_subset():
         masks = np.array([sum(1 << i for i in ref15.unrank_combination(n, k, off + r)) for r in range(cnt)])
         got = sm[masks]
         assert np.max(np.abs(got - mx) / np.maximum(np.abs(mx), 1.0)) <= 1e-12, k
+
+
+def test_ref15_bench_size_sampled():
+    """The ref15 bench workload at its full size (2^20 filters x 256 events, GPS every 20th,
+    the LDS-staged kernel), 48 filters spread over the batch against the oracle's step15 loop."""
+    import bench
+    dev = torch.device('cuda', 0)
+    cfg = dict(bench.CONFIGS['ref15'])
+    B, T, k, dt = cfg['B'], cfg['T'], cfg['k'], cfg['dt']
+    g = torch.Generator(device=dev).manual_seed(7)
+    etype = torch.ones(T, B, dtype=torch.uint8, device=dev)
+    etype[k - 1::k] = 0
+    dts = torch.full((T, B), dt, dtype=torch.float64, device=dev)
+    pay = torch.randn(T, 9, B, dtype=torch.float64, device=dev, generator=g)
+    pay[:, 0:3] *= 0.05
+    pay[:, 3:6] *= 0.01
+    pay[:, 6:9] *= 0.3
+    pay[:, 0:3] = torch.where((etype == 0)[:, None, :], pay[:, 0:3] * 60.0, pay[:, 0:3])
+    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    tr, ld, _, _ = kf.run_events(etype, dts, pay)
+    idx = torch.linspace(0, B - 1, 48).long().to(dev)
+    tr = tr[:, :, idx].cpu().numpy()
+    ld = ld[:, idx].cpu().numpy()
+    et, pa = etype[:, idx].cpu().numpy(), pay[:, :, idx].cpu().numpy()
+    assert int((kf.status() != 0).sum()) == 0
+    kf.close()
+    worst = 0.0
+    for j in range(idx.numel()):
+        x, P = np.zeros(15), ref_kf.P0_REF15.copy()
+        for t in range(T):
+            if et[t, j] == 0:
+                sd = {'easting': pa[t, 0, j], 'northing': pa[t, 1, j], 'altitude': pa[t, 2, j]}
+                x, P = ref_kf.step15(x, P, 'GPS', sd, dt)
+            else:
+                x, P = ref_kf.step15(x, P, 'IMU', ['t', *pa[t, :, j]], dt)
+            lr = np.linalg.slogdet(P)[1]
+            worst = max(worst, float(np.max(np.abs(tr[t, :, j] - x[:6]) / np.maximum(np.abs(x[:6]), 1.0))),
+                        abs(ld[t, j] - lr) / max(1.0, abs(lr)))
+    assert worst <= TOL, worst
