@@ -605,3 +605,44 @@ def test_ref15_bench_size_sampled():
             worst = max(worst, float(np.max(np.abs(tr[t, :, j] - x[:6]) / np.maximum(np.abs(x[:6]), 1.0))),
                         abs(ld[t, j] - lr) / max(1.0, abs(lr)))
     assert worst <= TOL, worst
+
+
+def test_sched_bench_size_sampled():
+    """The sched bench workload at its full size (2^20 filters x 256 events, 64 filters per rate,
+    the LDS-staged kernel), 24 filters spread over the batch against the oracle's greedy driver."""
+    dev = torch.device('cuda', 0)
+    B, T, k = 1 << 20, 256, 20
+    rates_all = (10, 20, 30, 40, 50, 60, 70, 80, 90, 100, 110, 120)
+    g = torch.Generator(device=dev).manual_seed(9)
+    t0 = 1697739278.761565
+    etype = torch.ones(T, B, dtype=torch.uint8, device=dev)
+    etype[k - 1::k] = 0
+    tt = (t0 + 0.005 * torch.arange(1, T + 1, dtype=torch.float64, device=dev)[:, None]
+          + 5e-4 * (torch.rand(T, B, dtype=torch.float64, device=dev, generator=g) - 0.5))
+    pay = torch.randn(T, 9, B, dtype=torch.float64, device=dev, generator=g)
+    pay[:, 0:3] *= 0.05
+    pay[:, 6:9] *= 0.3
+    pay[:, 0:3] = torch.where((etype == 0)[:, None, :], pay[:, 0:3] * 60.0, pay[:, 0:3])
+    rates = torch.tensor(rates_all, dtype=torch.float64, device=dev)
+    freq = rates[(torch.arange(B, device=dev) // 64) % len(rates_all)].contiguous()
+    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    tr, ld, stt, ns = kf.run_scheduled(tt, etype, pay, torch.full((B,), t0, dtype=torch.float64, device=dev), freq)
+    idx = torch.linspace(0, B - 1, 24).long().to(dev)
+    tr, ld, stt, ns = (v[..., idx].cpu().numpy() for v in (tr, ld, stt, ns))
+    et, ts, pa, fr = (v[..., idx].cpu().numpy() for v in (etype, tt, pay, freq))
+    kf.close()
+    for j in range(idx.numel()):
+        ev = [(0, 'GPS', t0, {'easting': 0.0, 'northing': 0.0, 'altitude': 0.0})]  # skipped (warm start)
+        for i in range(T):
+            if et[i, j] == 0:
+                ev.append((i + 1, 'GPS', ts[i, j], {'easting': pa[i, 0, j], 'northing': pa[i, 1, j],
+                                                    'altitude': pa[i, 2, j]}))
+            else:
+                ev.append((i + 1, 'IMU', ts[i, j], ['t', *pa[i, :, j]]))
+        rs, rl, _ = ref_kf.run_kalman_filter_scheduled(ev, 0, len(ev), ref_kf.P0_REF15.copy(),
+                                                       (t0, 0, 0, 0, 0, 0, 0), 'greedy', float(fr[j]))
+        n = int(ns[j])
+        assert n == len(rs) - 1, j
+        assert _rel(stt[:n, j], [r[0] for r in rs[1:]]) <= 1e-12, j
+        assert _rel(tr[:n, :, j], np.array([r[1:7] for r in rs[1:]])) <= TOL, j
+        assert _rel(ld[:n, j], rl[1:]) <= TOL, j
