@@ -2355,7 +2355,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED
 // queueing iterations are a few instructions each, so a register prefetch one event ahead
 // waited a memory latency per event, and a deeper one did not fit the registers).
 //   image: t rows [kSchedChunk][64] f64, then etype rows [kSchedChunk][64] u8
-constexpr int kSchedChunk = 16;
+#ifndef KF_SCHED_CHUNK
+#define KF_SCHED_CHUNK 16
+#endif
+constexpr int kSchedChunk = KF_SCHED_CHUNK;
 constexpr int kSchedImg = kSchedChunk * 512 + kSchedChunk * 64;
 template <typename T>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED_WAVES))) void ref15_sched_lds_kernel(
