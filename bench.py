@@ -804,10 +804,21 @@ def main():
     if args.gpus != world and world > 1:
         raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}')
     dist = None
+    # RCCL ('nccl') over xGMI, one GPU per rank.  KFMI_BENCH_DIST_BACKEND=gloo is a rehearsal
+    # switch only: it lets N ranks share the one GPU of a test box (RCCL refuses two ranks on one
+    # device) so the N>1 code path — shards, max-over-ranks timing, the final all-gather — runs
+    backend = os.environ.get('KFMI_BENCH_DIST_BACKEND', 'nccl')
+    if backend not in ('nccl', 'gloo'):
+        raise SystemExit(f'KFMI_BENCH_DIST_BACKEND={backend}: expected nccl or gloo')
+    if world > 1 and backend == 'gloo':
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group('gloo')
     dev = torch.device('cuda', local)
 
     cfg = dict(CONFIGS[args.config])
@@ -861,8 +872,12 @@ def main():
             g0 = time.perf_counter()
             gathered = kdist.gather_shards(local_out, world * kf.batch)
             torch.cuda.synchronize(dev)
-            assert gathered.shape[-1] == world * kf.batch
             gather_ms = (time.perf_counter() - g0) * 1e3
+            # every rank finds its own shard at its global offset in the reassembled array
+            off, cnt = kdist.shard_range(world * kf.batch, rank, world)
+            if gathered.shape[-1] != world * kf.batch or not torch.equal(  # bitwise (NaN-safe)
+                    gathered[..., off:off + cnt].contiguous().view(torch.uint8), local_out.view(torch.uint8)):
+                raise SystemExit(f'rank {rank}: the all-gathered shards do not reassemble')
 
     if rank == 0:
         rec = {

@@ -50,10 +50,15 @@ def gather_shards(local, total, group=None):
         padded[..., :local.shape[-1]] = local
     # gather along a new leading rank axis, then lay the shards side by side
     flat = padded.reshape(-1, width).contiguous()
+    # gloo collectives take host tensors (a CUDA tensor only appears here under gloo in the
+    # bench's one-GPU rehearsal, KFMI_BENCH_DIST_BACKEND=gloo); RCCL gathers in HBM
+    home = flat.device
+    if dist.get_backend(group) == 'gloo':
+        flat = flat.cpu()
     rows = flat.shape[0]
     out = torch.empty((world * rows, width), dtype=flat.dtype, device=flat.device)
     dist.all_gather_into_tensor(out, flat, group=group)
-    out = out.reshape(world, rows, width)
+    out = out.to(home).reshape(world, rows, width)
     parts = [out[r, :, :counts[r]] for r in range(world)]
     return torch.cat(parts, dim=-1).reshape(lead + (total,))
 
@@ -61,6 +66,8 @@ def gather_shards(local, total, group=None):
 def max_over_ranks(values, device, group=None):
     """Element-wise max of a list of floats over all ranks (timing: the slowest rank counts)."""
     import torch.distributed as dist
+    if dist.get_backend(group) == 'gloo':
+        device = 'cpu'
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return [float(v) for v in t.tolist()]

@@ -1,0 +1,23 @@
+#!/bin/bash
+# One-GPU rehearsal of bench.py's N>1 path (shards, max-over-ranks timing, the final all-gather
+# and its reassembly check): N ranks share the box's one GPU over gloo, since RCCL refuses two
+# ranks on one device.  The numbers are NOT scaling results (the ranks split one GPU's HBM).
+#   gpurun -- bash tools/dist_rehearsal.sh TAG
+set -u
+TAG=${1:-dist}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp KFMI_BENCH_DIST_BACKEND=gloo
+cd "$ROOT"
+for cfg in 3 ref15; do
+  for n in 2 4; do
+    timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+      --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --steps 3 --warmup 1 \
+      --config $cfg --batch 262144 > "$OUT/c${cfg}_n$n.log" 2>&1
+    rc=$?
+    echo "config $cfg n=$n rc=$rc" | tee -a "$OUT/steps.txt"
+    grep '^{"metric"' "$OUT/c${cfg}_n$n.log" | tail -1 >> "$OUT/lines.jsonl" || true
+    [ $rc -eq 0 ] || { tail -30 "$OUT/c${cfg}_n$n.log"; exit $rc; }
+  done
+done
