@@ -141,6 +141,67 @@ __global__ __launch_bounds__(256) void ref_pattern_kernel(const uint8_t* etype, 
     for (int i = 0; i < 27; ++i) stb(P, i, rb, off, st[15 + i] + acc);
 }
 
+// Candidate pattern for the cv kernels (round 2 A/B): the same u, z row loads moved HBM -> LDS by
+// buffer_load_dwordx4 ... lds (16 B per lane, 1 KiB per instruction: two 512-B rows) into
+// per-wave images of PAIR steps, double-buffered, instead of 8 B per lane into an 8-deep
+// register ring.  fp64, update every step.  Per image: u rows 3 PAIR consecutive rows of the
+// [T*3][B] array, z likewise; row r of the image at img + r * 512.
+template <int PAIR>
+__global__ __launch_bounds__(256) void pattern_lds_kernel(const void* u, const void* z, void* traj, void* logdet,
+                                                          int64_t B, int T_) {
+    constexpr int D = 3, N = 6, W = 8;
+    constexpr int ROWS = D * PAIR;              // u rows (and z rows) per image
+    constexpr int NI = (ROWS + 1) / 2;          // DMA instructions per array per image
+    constexpr int IMG = 2 * NI * 1024;          // u part then z part
+    constexpr int NDMA = 2 * NI, NST = PAIR * (N + 1);
+    static_assert(ROWS % 2 == 0, "whole 1-KiB DMA instructions only");
+    __shared__ __attribute__((aligned(16))) unsigned char lds[4 * 2 * IMG];
+    const int lane = int(threadIdx.x & 63);
+    const int wave = wave_uniform(int(threadIdx.x >> 6));
+    const int64_t f0 = int64_t(blockIdx.x) * 256 + int64_t(wave) * 64;
+    if (f0 >= B) return;
+    unsigned char* const img0 = lds + wave * 2 * IMG;
+    const uint32_t off = uint32_t(f0 + lane) * uint32_t(W);
+    const uint32_t rb = uint32_t(B) * uint32_t(W);
+    const uint32_t voff = uint32_t(lane >> 5) * rb + uint32_t(lane & 31) * 16u;
+    const int NP = T_ / PAIR;
+    auto issue = [&](int p, unsigned char* img) {
+        const int64_t r0 = int64_t(p) * ROWS;
+        const uint32_t len = uint32_t(ROWS) * rb - uint32_t(f0) * W;
+        const __amdgpu_buffer_rsrc_t ru =
+            bytes_rsrc(reinterpret_cast<const char*>(u) + r0 * int64_t(rb) + f0 * W, len);
+        const __amdgpu_buffer_rsrc_t rz =
+            bytes_rsrc(reinterpret_cast<const char*>(z) + r0 * int64_t(rb) + f0 * W, len);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) lds_dma16(ru, img + k * 1024, voff, 2 * k * int(rb));
+#pragma unroll
+        for (int k = 0; k < NI; ++k) lds_dma16(rz, img + (NI + k) * 1024, voff, 2 * k * int(rb));
+    };
+    issue(0, img0);
+    waitcnt<vmcnt_imm(0)>();
+    double acc = 0.0;
+    for (int p = 0; p < NP; ++p) {
+        unsigned char* const img = img0 + (p & 1) * IMG;
+        if (p + 1 < NP) {
+            issue(p + 1, img0 + ((p + 1) & 1) * IMG);
+            waitcnt<vmcnt_imm(NST + NDMA)>();
+        } else {
+            waitcnt<vmcnt_imm(NST)>();
+        }
+        const double* iu = reinterpret_cast<const double*>(img) + lane;
+        const double* iz = reinterpret_cast<const double*>(img + NI * 1024) + lane;
+#pragma unroll
+        for (int s = 0; s < PAIR; ++s) {
+            const int t = p * PAIR + s;
+#pragma unroll
+            for (int i = 0; i < D; ++i) acc += iu[(s * D + i) * 64] + iz[(s * D + i) * 64];
+#pragma unroll
+            for (int i = 0; i < N; ++i) stb(traj, int64_t(t) * N + i, rb, off, acc + double(i));
+            stb(logdet, t, rb, off, acc);
+        }
+    }
+}
+
 template <int D, typename T>
 hipError_t launch(const void* u, const void* z, void* traj, void* logdet, int64_t B, int T_, int k, hipStream_t st) {
     pattern_kernel<D, T, 8><<<dim3(unsigned((B + 255) / 256)), 256, 0, st>>>(u, z, traj, logdet, B, T_, k);
@@ -174,5 +235,16 @@ extern "C" int kfprobe_ref_pattern(int f64, const void* etype, const void* dt, c
     const double* d = static_cast<const double*>(dt);
     if (f64) ref_pattern_kernel<double><<<grid, 256, 0, st>>>(et, d, payload, x, P, traj, logdet, B, T);
     else ref_pattern_kernel<float><<<grid, 256, 0, st>>>(et, d, payload, x, P, traj, logdet, B, T);
+    return int(hipGetLastError());
+}
+
+// pattern_lds_kernel<2> on cv3 f64 buffers, update every step (u, z [T][3][B], traj [T][6][B],
+// logdet [T][B]); B % 64 == 0, T even.
+extern "C" int kfprobe_pattern_lds(const void* u, const void* z, void* traj, void* logdet, int64_t B, int T,
+                                   void* stream) {
+    if (B <= 0 || B % 64 != 0 || T <= 0 || T % 2 != 0 || 6 * B * 8 >= (int64_t(1) << 32))
+        return int(hipErrorInvalidValue);
+    pattern_lds_kernel<2><<<dim3(unsigned((B + 255) / 256)), 256, 0, static_cast<hipStream_t>(stream)>>>(
+        u, z, traj, logdet, B, T);
     return int(hipGetLastError());
 }
