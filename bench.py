@@ -110,6 +110,20 @@ def load_traffic(cfg_id):
         return None
 
 
+def load_valu(cfg_id):
+    """VALU issue of the dominant kernel from the committed rocprofv3 SQ-counter summary
+    (tools/pmc_valu.sh; SURVEY.md §8d asks for the VALU fraction beside the HBM roofline)."""
+    try:
+        with open(os.path.join(ROOT, 'profiles', 'r02_valu', 'pmc_valu.json')) as f:
+            rec = json.load(f).get(f'config{cfg_id}')
+        return None if rec is None else {
+            'issue_frac': rec['valu_issue_frac'], 'valu_insts_per_wave_step': rec['valu_per_wave_step'],
+            'issue_stall_frac_of_wave_cycles': rec['wave_cycles_issue_stall_frac'],
+            'source': 'profiles/r02_valu/pmc_valu.json (SQ_INSTS_VALU x 4 cycles / (kernel time x 2.4 GHz x 1024 SIMDs))'}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 # --------------------------------------------------------------------------------------------
 # Workloads: each returns dict(step, units, bytes, kernel, cpu, gather, desc, extra, ...)
 # --------------------------------------------------------------------------------------------
@@ -289,7 +303,8 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
     kernel = 'cv_block_kernel' if block_kernel_in_use() else 'cv_run_kernel'
     return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_step, kernel=kernel,
                 traffic=load_traffic(cfg_id) if kernel == 'cv_block_kernel' else None, cpu=cpu,
-                gather=gather_payload, kf=kf, pcie=pcie, probe=probe, per_step=per_step,
+                valu=load_valu(cfg_id) if kernel == 'cv_block_kernel' else None,
+                gather=gather_payload, kf=kf, pcie=pcie, probe=probe, per_step=per_step, update_every=k,
                 desc=f"BASELINE config {cfg_id}: {cfg['model']} ({2 * d}-state/{d}-meas), {cfg['dtype']}, "
                      f"B={B} filters/GPU, T={T}, dt={dt}, GPS update every {k} step(s)",
                 extra={'filters_per_gpu': B, 'time_steps_per_launch': T, 'update_every': k})
@@ -405,7 +420,7 @@ def ref15_workload(cfg, args, rank, world, dev):
                         'row stores on the same buffers, the event arithmetic reduced to a sum'}
 
     return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_event, probe=probe,
-                kernel='ref_events_lds_kernel', traffic=load_traffic('ref15'), cpu=cpu, gather=gather_payload, kf=kf,
+                kernel='ref_events_lds_kernel', traffic=load_traffic('ref15'), valu=load_valu('ref15'), cpu=cpu, gather=gather_payload, kf=kf,
                 desc=f'SURVEY 8f row 2: reference 15-state model (kf_workers.py:493-614), f64, B={B} filters/GPU, '
                      f'T={T} events (IMU 200 Hz, GPS fix every {k}th event), dt={dt}',
                 extra={'filters_per_gpu': B, 'events_per_launch': T})
@@ -903,6 +918,8 @@ def main():
                                'frac': achieved / HBM_PEAK_GBS, 'traffic': w['traffic'], 'kernel': w['kernel'],
                                'kernel_ms': kern_ms, 'algorithmic_bytes_per_launch': w['bytes'],
                                'algorithmic_bytes_per_step': w['bytes_per_unit']}
+            if w.get('valu'):
+                rec['roofline']['valu'] = w['valu']
             if w.get('roofline_note'):
                 rec['roofline']['note'] = w['roofline_note']
             if world == 1 and w.get('probe') and args.ablate == 'none':
@@ -917,6 +934,10 @@ def main():
             rec['roofline'] = {'bound': 'hbm', 'achieved': None, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': None,
                                'traffic': None, 'kernel': w['kernel'], 'kernel_ms': kern_ms,
                                'note': 'compute-bound search: events in LDS, ~350 B of HBM traffic per subset'}
+        if w.get('update_every', 1) > 1:
+            # the async config: predict-steps/s (= value) and update-steps/s apart
+            rec['predict_steps_per_s'] = rec['value']
+            rec['update_steps_per_s'] = world * (w['units'] // w['update_every']) * args.steps / elapsed
         if 'combos' in w:
             rec['combinations_per_s'] = world * w['combos'] * args.steps / elapsed
         rec['failed_filters'] = bad

@@ -1,0 +1,56 @@
+"""Reduce tools/pmc_valu.sh's SQ counters to VALU issue per launch of each config's dominant kernel.
+
+usage: python tools/pmc_valu.py OUTDIR CFG [CFG ...]   -> writes OUTDIR/pmc_valu.json
+
+valu_issue_frac = SQ_INSTS_VALU x 4 cycles / (kernel time x 2.4 GHz x 1024 SIMDs): the share of
+the chip's VALU issue slots the kernel's wave instructions fill (a wave64 VALU instruction
+occupies its 16-lane SIMD 4 cycles; fp64 FMA is full rate on gfx950, 78.6 TFLOP/s; transcendental
+and f64 rcp instructions take longer, so this is a floor on the VALU busy share).  The kernel
+time is the HIP-event time of the same profiled process (its bench JSON line).
+"""
+import json
+import os
+import sys
+
+from pmc_traffic import per_kernel, pick
+
+CLK, SIMDS, CYC = 2.4e9, 1024, 4
+COUNTERS = ['SQ_WAVES', 'SQ_INSTS_VALU', 'SQ_ACTIVE_INST_VALU', 'SQ_WAVE_CYCLES', 'SQ_BUSY_CYCLES', 'SQ_WAIT_ANY',
+            'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_ANY', 'GRBM_GUI_ACTIVE']
+
+
+def bench_line(path):
+    with open(path) as f:
+        for line in f:
+            if line.startswith('{"metric"'):
+                rec = json.loads(line)
+    return rec
+
+
+def main():
+    out_dir, cfgs = sys.argv[1], sys.argv[2:]
+    res = {'note': ' '.join(__doc__.split('\n\n')[2].split())}
+    for c in cfgs:
+        kern = 'ref_events' if c == 'ref15' else 'cv_block_kernel'
+        d = os.path.join(out_dir, f'cfg{c}')
+        vals = {}
+        for ctr in COUNTERS:
+            v = pick(per_kernel(d, ctr), kern)
+            vals[ctr] = sum(v) / len(v)
+        rec = bench_line(os.path.join(out_dir, f'cfg{c}.log'))
+        ms = rec['roofline']['kernel_ms']
+        units = rec['value'] * rec['ms_per_step'] * 1e-3        # filter-steps (events) per launch
+        wave_steps = units / 64
+        res[f'config{c}'] = dict(
+            counters_per_launch=vals, kernel_ms=ms, launches_profiled=len(v),
+            valu_per_wave_step=vals['SQ_INSTS_VALU'] / wave_steps,
+            valu_issue_frac=vals['SQ_INSTS_VALU'] * CYC / (ms * 1e-3 * CLK * SIMDS),
+            wave_cycles_waiting_frac=vals['SQ_WAIT_ANY'] / vals['SQ_WAVE_CYCLES'],
+            wave_cycles_issue_stall_frac=vals['SQ_WAIT_INST_ANY'] / vals['SQ_WAVE_CYCLES'])
+    with open(os.path.join(out_dir, 'pmc_valu.json'), 'w') as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == '__main__':
+    main()
