@@ -227,21 +227,36 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
 
     def per_step(reps=2):
         """The reference's call shape: T steps of BatchedKF.predict(dt, u[t]) then
-        BatchedKF.update(z[t]) (its log-det returned), one launch each, the state round-tripping
-        through HBM every call; against kf_run's fused launch on the same streams.  Never `value`."""
+        BatchedKF.update(z[t]) (its log-det returned).  By default kf_predict is held back and
+        runs fused with the next kf_update (one state round trip per step, plus a copy of u);
+        KFMI_PREDICT=eager launches each call on its own (two round trips).  Against kf_run's
+        fused launch on the same streams.  Never `value`."""
         if k != 1:
             return None
-        kf.reset(x0)
-        times = []
-        for _ in range(reps + 1):
-            torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
-            for t in range(T):
-                kf.predict(dt, u=u[t])
-                kf.update(z[t])
-            torch.cuda.synchronize(dev)
-            times.append(time.perf_counter() - t0)
-        el = min(times[1:])
+
+        def loop(mode):
+            old = os.environ.get('KFMI_PREDICT')
+            os.environ['KFMI_PREDICT'] = mode
+            try:
+                kf.reset(x0)
+                times = []
+                for _ in range(reps + 1):
+                    torch.cuda.synchronize(dev)
+                    t0 = time.perf_counter()
+                    for t in range(T):
+                        kf.predict(dt, u=u[t])
+                        kf.update(z[t])
+                    torch.cuda.synchronize(dev)
+                    times.append(time.perf_counter() - t0)
+                return min(times[1:])
+            finally:
+                if old is None:
+                    os.environ.pop('KFMI_PREDICT')
+                else:
+                    os.environ['KFMI_PREDICT'] = old
+
+        el = loop('deferred')
+        el_eager = loop('eager')
         # the same steps as T launches of kf_run with T = 1 (predict + update fused, one state
         # round trip per step, trajectory and log-det rows written)
         kf.reset(x0)
@@ -255,14 +270,19 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
             times1.append(time.perf_counter() - t0)
         el1 = min(times1[1:])
         w = 8 if cfg['dtype'] == 'f64' else 4
-        # the per-axis blocks of P (block-diagonal handle: kf_predict / kf_update move only them)
+        # the per-axis blocks of P (block-diagonal handle: the calls move only them)
         nt = 3 * d
-        # predict: state + u in, state out; update: state + z in, state + log-det out
-        nbytes = B * T * w * ((kf.n + nt) * 4 + 2 * d + 1)
+        # deferred: u copied (in + out), then state + u + z in, state + log-det out
+        nbytes = B * T * w * ((kf.n + nt) * 2 + 4 * d + 1)
+        # eager: predict state + u in, state out; update state + z in, state + log-det out
+        nbytes_eager = B * T * w * ((kf.n + nt) * 4 + 2 * d + 1)
         return {'value': B * T / el, 'unit': 'KF steps/s', 'ms_per_step': el / T * 1e3,
-                'gbs': nbytes / el / 1e9, 'launches': 2 * T,
-                'note': 'kf_predict + kf_update per time step through BatchedKF (no trajectory kept), best of %d'
-                        % reps,
+                'gbs': nbytes / el / 1e9, 'launches': T, 'copies': T,
+                'note': 'kf_predict + kf_update per time step through BatchedKF (no trajectory kept), the '
+                        'predict held back and fused into the update; best of %d' % reps,
+                'eager': {'value': B * T / el_eager, 'ms_per_step': el_eager / T * 1e3,
+                          'gbs': nbytes_eager / el_eager / 1e9, 'launches': 2 * T,
+                          'note': 'KFMI_PREDICT=eager: one kernel per call'},
                 'run_t1': {'value': B * T / el1, 'ms_per_step': el1 / T * 1e3, 'launches': T,
                            'note': 'BatchedKF.run on one step at a time (kf_run, T = 1: predict + update fused)'}}
 

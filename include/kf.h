@@ -135,7 +135,13 @@ int kf_get_status(const kf_batch* handle, int32_t* status, int on_device, void* 
  * logdet_out: device [B] (NULL = skip), logdet of the predicted P, as the adaptive-threshold
  * driver uses it (kf_workers.py:1023).
  * Replaces get_state_transition_matrix + get_process_noise_covariance_matrix +
- * x = np.dot(F, x) + predict_covariance (kf_workers.py:493-549, 688-691). */
+ * x = np.dot(F, x) + predict_covariance (kf_workers.py:493-549, 688-691).
+ * With a scalar dt and no logdet_out the step is held back and runs fused with the next
+ * kf_update (one kernel, the state read and written once); u is copied on `stream` before the
+ * call returns, so the caller may reuse its buffer at once.  Any other call that reads or
+ * replaces the state (kf_get_state, kf_get_status, kf_set_state, kf_run, another kf_predict)
+ * runs a held-back predict first, on its own stream; kf_reset discards it.  Results are those
+ * of the two separate kernels (KFMI_PREDICT=eager). */
 int kf_predict(kf_batch* handle, double dt, const double* dt_per_filter, const void* u,
                void* logdet_out, void* stream);
 

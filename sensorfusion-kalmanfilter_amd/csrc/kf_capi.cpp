@@ -35,6 +35,16 @@ struct kf_batch {
     void* stream_ws;  // kf_run_stream: chunk banks, maps, check (grown on demand)
     size_t stream_ws_bytes;
     int64_t s_chunks, s_len, s_warm;  // the last kf_run_stream's split (s_chunks = 1: sequential)
+    // BASELINE models: a kf_predict held back so the next kf_update runs predict + update as one
+    // fused step (the state crosses HBM once instead of twice).  The control is copied into
+    // pend_u on the predict's stream, so the caller may reuse its u buffer at once.
+    bool pend;
+    bool pend_has_u;
+    double pend_dt;
+    void* pend_u;          // [c][B] (allocated on first use)
+    hipEvent_t pend_done;    // orders a control copy after the last kernel that read pend_u
+    hipStream_t pend_reader; // the stream of that kernel
+    bool pend_read;
 };
 
 namespace {
@@ -189,6 +199,34 @@ kfmi::RefArgs ref_args(const kf_batch* h) {
     return a;
 }
 
+// KFMI_PREDICT=eager turns the deferral off (tests, A/B)
+bool defer_predicts() {
+    const char* v = std::getenv("KFMI_PREDICT");
+    return !(v && !std::strcmp(v, "eager"));
+}
+
+// After a kernel on `stream` read pend_u: remember the stream.  A later control copy on another
+// stream first waits for an event recorded on this one at that time (all the stream's work so
+// far, the read included), so the common one-stream loop makes no event calls.
+int note_pend_reader(kf_batch* h, void* stream, const char*) {
+    if (!h->pend_has_u) return KF_OK;
+    h->pend_reader = static_cast<hipStream_t>(stream);
+    h->pend_read = true;
+    return KF_OK;
+}
+
+// Runs a held-back kf_predict on `stream` (the stream of the call that needs the state: a caller
+// that orders that call after its kf_predict has also ordered it after the control copy).
+int flush_predict(kf_batch* h, void* stream, const char* what) {
+    if (!h->pend) return KF_OK;
+    h->pend = false;
+    kfmi::CvArgs a = base_args(h);
+    a.dt = h->pend_dt;
+    a.u = h->pend_has_u ? h->pend_u : nullptr;
+    if (int rc = launch(h, kfmi::Op::Predict, a, stream, what)) return rc;
+    return note_pend_reader(h, stream, what);
+}
+
 }  // namespace
 
 namespace kfmi {
@@ -320,6 +358,8 @@ int kf_free(kf_batch* h) {
     if (h->search_ws) (void)hipFree(h->search_ws);
     if (h->flag) (void)hipFree(h->flag);
     if (h->stream_ws) (void)hipFree(h->stream_ws);
+    if (h->pend_u) (void)hipFree(h->pend_u);
+    if (h->pend_done) (void)hipEventDestroy(h->pend_done);
     delete h;
     return KF_OK;
 }
@@ -343,6 +383,7 @@ int kf_reset(kf_batch* h, const void* x0, void* stream) {
         hipError_t e = kfmi::launch_ref_reset(h->model, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
         return e == hipSuccess ? KF_OK : hip_fail(e, "kf_reset");
     }
+    h->pend = false;  // a predict followed by a reset leaves the reset state
     kfmi::CvArgs a = base_args(h);
     a.x0 = x0;
     h->block_p = true;  // P = P0 is diagonal
@@ -352,6 +393,8 @@ int kf_reset(kf_batch* h, const void* x0, void* stream) {
 int kf_set_state(kf_batch* h, const void* x, const void* P, int on_device, void* stream) {
     if (int rc = check_handle(h)) return rc;
     if (!x && !P) return fail(KF_EINVAL, "kf_set_state: x and P both null");
+    if (x && P) h->pend = false;  // both overwritten: a held-back predict has no effect
+    else if (int rc = flush_predict(h, stream, "kf_set_state")) return rc;
     const hipMemcpyKind kind = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     const size_t w = elem(h), nb = static_cast<size_t>(h->B);
     hipError_t e = hipSuccess;
@@ -384,6 +427,8 @@ int kf_set_state(kf_batch* h, const void* x, const void* P, int on_device, void*
 
 int kf_get_state(const kf_batch* h, void* x, void* P, int on_device, void* stream) {
     if (int rc = check_handle(h)) return rc;
+    // the handle is logically const: running a held-back predict does not change its state
+    if (int rc = flush_predict(const_cast<kf_batch*>(h), stream, "kf_get_state")) return rc;
     const hipMemcpyKind kind = on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     const size_t w = elem(h), nb = static_cast<size_t>(h->B);
     hipError_t e = hipSuccess;
@@ -398,6 +443,7 @@ int kf_get_state(const kf_batch* h, void* x, void* P, int on_device, void* strea
 int kf_get_status(const kf_batch* h, int32_t* status, int on_device, void* stream) {
     if (int rc = check_handle(h)) return rc;
     if (!status) return fail(KF_EINVAL, "kf_get_status: null output");
+    if (int rc = flush_predict(const_cast<kf_batch*>(h), stream, "kf_get_status")) return rc;
     const size_t nb = static_cast<size_t>(h->B);
     if (!nb) return KF_OK;
     hipError_t e = hipMemcpyAsync(status, h->status, sizeof(int32_t) * nb,
@@ -413,6 +459,39 @@ int kf_predict(kf_batch* h, double dt, const double* dt_per_filter, const void* 
     if (int rc = check_handle(h)) return rc;
     if (int rc = need_cv(h, "kf_predict")) return rc;
     if (!dt_per_filter && !(dt >= 0.0)) return fail(KF_EINVAL, "kf_predict: dt must be >= 0 (got %g)", dt);
+    if (int rc = flush_predict(h, stream, "kf_predict")) return rc;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    if (h->B && !dt_per_filter && !logdet_out && defer_predicts()) {
+        // hold it back for a fused step with the next kf_update (the reference's loop calls
+        // predict then update every step, kf_workers.py:688-711)
+        const size_t bytes = elem(h) * h->c * static_cast<size_t>(h->B);
+        hipError_t e = hipSuccess;
+        if (u && !h->pend_u) {
+            e = hipMalloc(&h->pend_u, bytes);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&h->pend_done, hipEventDisableTiming);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                if (h->pend_u) (void)hipFree(h->pend_u);
+                h->pend_u = nullptr;
+                h->pend_done = nullptr;
+            }
+        }
+        if (!u || h->pend_u) {
+            if (u) {
+                // the copy overwrites pend_u: wait for the last kernel that read it
+                if (h->pend_read && h->pend_reader != st) {
+                    e = hipEventRecord(h->pend_done, h->pend_reader);
+                    if (e == hipSuccess) e = hipStreamWaitEvent(st, h->pend_done, 0);
+                }
+                if (e == hipSuccess) e = kfmi::launch_copy(h->pend_u, u, bytes, st);
+                if (e != hipSuccess) return hip_fail(e, "kf_predict control copy");
+            }
+            h->pend = true;
+            h->pend_has_u = u != nullptr;
+            h->pend_dt = dt;
+            return KF_OK;
+        }
+    }
     kfmi::CvArgs a = base_args(h);
     a.dt = dt;
     a.dt_filter = dt_per_filter;
@@ -429,6 +508,14 @@ int kf_update(kf_batch* h, const void* z, const uint8_t* mask, void* logdet_out,
     a.z = z;
     a.mask = mask;
     a.logdet = logdet_out;
+    if (h->pend) {
+        // the held-back predict and this update as one kernel (cv_step_kernel)
+        h->pend = false;
+        a.dt = h->pend_dt;
+        a.u = h->pend_has_u ? h->pend_u : nullptr;
+        if (int rc = launch(h, kfmi::Op::Step, a, stream, "kf_update (fused with the predict)")) return rc;
+        return note_pend_reader(h, stream, "kf_update");
+    }
     return launch(h, kfmi::Op::Update, a, stream, "kf_update");
 }
 
@@ -441,6 +528,7 @@ int kf_run(kf_batch* h, int T, double dt, const double* dt_steps, const void* u,
     if (!dt_steps && !(dt >= 0.0)) return fail(KF_EINVAL, "kf_run: dt must be >= 0 (got %g)", dt);
     const int U = T / update_every;
     if (U > 0 && !z && h->B) return fail(KF_EINVAL, "kf_run: %d updates need a z stream", U);
+    if (int rc = flush_predict(h, stream, "kf_run")) return rc;
     if (T == 0) return KF_OK;
     kfmi::CvArgs a = base_args(h);
     a.T = T;

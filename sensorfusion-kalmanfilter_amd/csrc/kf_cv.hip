@@ -21,6 +21,8 @@
 // filter without a branch (status KF_ENOTSPD); the other lanes are unaffected.
 #include <hip/hip_runtime.h>
 #include <math.h>
+
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -496,6 +498,49 @@ __global__ __launch_bounds__(kBlock) void cv_update_kernel(const CvArgs a) {
     a.status[f] = st;
 }
 
+// kf_predict held back and fused with the next kf_update (kf_capi.cpp): the two kernels above
+// in one, so the state crosses HBM once per step.  u is the control copied at kf_predict time.
+template <int D, typename T, bool BLOCK>
+__global__ __launch_bounds__(kBlock) void cv_step_kernel(const CvArgs a) {
+    using K = Cv<D, T>;
+    const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (f >= a.B) return;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
+    T x[K::N], P[K::NT];
+    load_state_b<D, T, BLOCK>(a, rb, off, x, P);
+    T u[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) u[i] = a.u ? ldb<T>(a.u, i, rb, off) : T(0);
+    T R[K::MT];
+    load_R<D, T>(a, R);
+    T z[K::M];
+#pragma unroll
+    for (int i = 0; i < K::M; ++i) z[i] = ldb<T>(a.z, i, rb, off);
+    int32_t st = a.status[f];
+    const double dtd = a.dt;
+    K::predict(x, P, T(dtd), u, T(a.q_pos * dtd), T(a.q_vel * dtd));
+    if (!a.mask || a.mask[f] != 0) {
+        if (!K::template update<BLOCK>(x, P, z, R)) st = kNotSpd;
+    }
+    store_state_b<D, T, BLOCK>(a, rb, off, x, P);
+    if (a.logdet) {
+        const T ld = logdet_ldl<K::N, T>(P);
+        if (!(ld == ld)) st = kNotSpd;
+        stb(a.logdet, 0, rb, off, ld);
+    }
+    a.status[f] = st;
+}
+
+// Device copy with the shader (kf_predict's control snapshot): hipMemcpyAsync of device memory
+// goes to an SDMA engine, several times slower than a kernel for tens of MB.
+template <typename W>
+__global__ __launch_bounds__(kBlock) void copy_kernel(W* __restrict__ dst, const W* __restrict__ src, int64_t n) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * kBlock)
+        dst[i] = src[i];
+}
+
 // x = x0 (or 0), P = diag(p0_pos I, p0_vel I), status = OK.
 template <int D, typename T>
 __global__ __launch_bounds__(kBlock) void cv_reset_kernel(const CvArgs a) {
@@ -630,6 +675,10 @@ hipError_t launch_cv_t(Op op, const CvArgs& a, hipStream_t st) {
             if (a.block_p) cv_update_kernel<D, T, true><<<grid, kBlock, 0, st>>>(a);
             else cv_update_kernel<D, T, false><<<grid, kBlock, 0, st>>>(a);
             break;
+        case Op::Step:
+            if (a.block_p) cv_step_kernel<D, T, true><<<grid, kBlock, 0, st>>>(a);
+            else cv_step_kernel<D, T, false><<<grid, kBlock, 0, st>>>(a);
+            break;
         case Op::Reset: cv_reset_kernel<D, T><<<grid, kBlock, 0, st>>>(a); break;
     }
     return hipGetLastError();
@@ -651,6 +700,22 @@ hipError_t launch_cv_offblock(int axes, bool f64, const CvArgs& a, int* flag, hi
         if (f64) cv_offblock_kernel<3, double><<<grid, kBlock, 0, stream>>>(a, flag);
         else cv_offblock_kernel<3, float><<<grid, kBlock, 0, stream>>>(a, flag);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+    if (!bytes) return hipSuccess;
+    const bool wide = (reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | bytes) % 16 == 0;
+    const int64_t n = static_cast<int64_t>(wide ? bytes / 16 : bytes / 4);
+    // one chunk per lane: a small copy (65,536 filters: 48 K chunks) is a single HBM round trip
+    // per lane instead of a grid-stride chain of them
+    const int64_t blocks = std::min<int64_t>((n + kBlock - 1) / kBlock, int64_t(1) << 20);
+    if (wide)
+        copy_kernel<uint4><<<dim3(unsigned(blocks)), kBlock, 0, stream>>>(
+            static_cast<uint4*>(dst), static_cast<const uint4*>(src), n);
+    else
+        copy_kernel<uint32_t><<<dim3(unsigned(blocks)), kBlock, 0, stream>>>(
+            static_cast<uint32_t*>(dst), static_cast<const uint32_t*>(src), n);
     return hipGetLastError();
 }
 

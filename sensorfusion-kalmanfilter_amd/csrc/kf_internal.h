@@ -252,13 +252,15 @@ struct Ref15SchedArgs {
     int32_t* n_sel;          // [B]
 };
 
-enum class Op { Run, Predict, Update, Reset };
+enum class Op { Run, Predict, Update, Step, Reset };  // Step: predict + update (kf_capi's deferral)
 
 // Launchers (kf_cv.hip, kf_ref.hip).  Return hipSuccess or the launch error.
 hipError_t launch_cv(int axes, bool f64, Op op, const CvArgs& a, hipStream_t stream);
 // *flag |= 1 if any filter's P couples different axes (flag: device int, zeroed by the caller).
 hipError_t launch_cv_offblock(int axes, bool f64, const CvArgs& a, int* flag, hipStream_t stream);
 hipError_t launch_synth(int axes, bool f64, const SynthArgs& a, hipStream_t stream);
+// bytes (a multiple of 4) from src to dst on the stream, by a kernel
+hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
 // chain = true: the chain-parallel kernel (kGroup lanes per filter), for few filters.
 // kf_run_events kernel variants: one lane per filter (inputs loaded to registers), one lane
 // per axis chain (few filters), one lane per filter with inputs staged through LDS by DMA
