@@ -141,7 +141,9 @@ int kf_get_status(const kf_batch* handle, int32_t* status, int on_device, void* 
  * call returns, so the caller may reuse its buffer at once.  Any other call that reads or
  * replaces the state (kf_get_state, kf_get_status, kf_set_state, kf_run, another kf_predict)
  * runs a held-back predict first, on its own stream; kf_reset discards it.  Results are those
- * of the two separate kernels (KFMI_PREDICT=eager). */
+ * of the two separate kernels (KFMI_PREDICT=eager).  The control buffer is allocated by kf_alloc,
+ * so a predict/update loop allocates nothing and can be captured into a graph (capture whole
+ * predict + update pairs: a predict left pending at the end of a capture runs outside it). */
 int kf_predict(kf_batch* handle, double dt, const double* dt_per_filter, const void* u,
                void* logdet_out, void* stream);
 

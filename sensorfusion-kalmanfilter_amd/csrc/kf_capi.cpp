@@ -41,7 +41,7 @@ struct kf_batch {
     bool pend;
     bool pend_has_u;
     double pend_dt;
-    void* pend_u;          // [c][B] (allocated on first use)
+    void* pend_u;          // [c][B] (allocated by kf_alloc)
     hipEvent_t pend_done;    // orders a control copy after the last kernel that read pend_u
     hipStream_t pend_reader; // the stream of that kernel
     bool pend_read;
@@ -331,6 +331,15 @@ int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_pa
             return fail(KF_ENOMEM, "hipMalloc of %zu filters failed", nb);
         }
     }
+    // the held-back predict's control copy (kf_predict), allocated here so that a per-step loop
+    // never allocates (and can be captured into a graph)
+    if (!is_ref(model) && nb &&
+        (hipMalloc(&h->pend_u, w * h->c * nb) != hipSuccess ||
+         hipEventCreateWithFlags(&h->pend_done, hipEventDisableTiming) != hipSuccess)) {
+        (void)hipGetLastError();
+        kf_free(h);
+        return fail(KF_ENOMEM, "hipMalloc of the control copy of %zu filters failed", nb);
+    }
     if (model == KF_MODEL_REF15 && hipMalloc(&h->ws, kWsEvents + kWsBinom + kWsInit) != hipSuccess) {
         (void)hipGetLastError();
         kf_free(h);
@@ -464,33 +473,20 @@ int kf_predict(kf_batch* h, double dt, const double* dt_per_filter, const void* 
     if (h->B && !dt_per_filter && !logdet_out && defer_predicts()) {
         // hold it back for a fused step with the next kf_update (the reference's loop calls
         // predict then update every step, kf_workers.py:688-711)
-        const size_t bytes = elem(h) * h->c * static_cast<size_t>(h->B);
-        hipError_t e = hipSuccess;
-        if (u && !h->pend_u) {
-            e = hipMalloc(&h->pend_u, bytes);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&h->pend_done, hipEventDisableTiming);
-            if (e != hipSuccess) {
-                (void)hipGetLastError();
-                if (h->pend_u) (void)hipFree(h->pend_u);
-                h->pend_u = nullptr;
-                h->pend_done = nullptr;
+        if (u) {
+            // the copy overwrites pend_u (kf_alloc): wait for the last kernel that read it
+            hipError_t e = hipSuccess;
+            if (h->pend_read && h->pend_reader != st) {
+                e = hipEventRecord(h->pend_done, h->pend_reader);
+                if (e == hipSuccess) e = hipStreamWaitEvent(st, h->pend_done, 0);
             }
+            if (e == hipSuccess) e = kfmi::launch_copy(h->pend_u, u, elem(h) * h->c * static_cast<size_t>(h->B), st);
+            if (e != hipSuccess) return hip_fail(e, "kf_predict control copy");
         }
-        if (!u || h->pend_u) {
-            if (u) {
-                // the copy overwrites pend_u: wait for the last kernel that read it
-                if (h->pend_read && h->pend_reader != st) {
-                    e = hipEventRecord(h->pend_done, h->pend_reader);
-                    if (e == hipSuccess) e = hipStreamWaitEvent(st, h->pend_done, 0);
-                }
-                if (e == hipSuccess) e = kfmi::launch_copy(h->pend_u, u, bytes, st);
-                if (e != hipSuccess) return hip_fail(e, "kf_predict control copy");
-            }
-            h->pend = true;
-            h->pend_has_u = u != nullptr;
-            h->pend_dt = dt;
-            return KF_OK;
-        }
+        h->pend = true;
+        h->pend_has_u = u != nullptr;
+        h->pend_dt = dt;
+        return KF_OK;
     }
     kfmi::CvArgs a = base_args(h);
     a.dt = dt;

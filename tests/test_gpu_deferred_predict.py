@@ -188,3 +188,45 @@ def test_predict_and_update_on_two_streams():
     got, ref = run_script('cv3', 'f64', x0, script)
     for a, b in zip(got, ref):
         close(a, b, 'f64')
+
+
+def test_graph_capture_of_the_per_step_loop():
+    """A captured predict/update loop replays the control copies and fused steps (the handle
+    allocates its control buffer up front, so nothing allocates or synchronises in the loop)."""
+    B, T = 1024, 4
+    x0, u, z = inputs('cv3', 'f64', B, T, seed=9)
+    kf = kfmi.BatchedKF('cv3', B, 'f64')
+    ld = [kf.empty(B) for _ in range(T)]
+    lib = _lib.lib()
+
+    def loop():
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for t in range(T):
+            _lib.check(lib.kf_predict(kf.handle, 0.1, None, ctypes.c_void_p(u[t].data_ptr()), None, st))
+            _lib.check(lib.kf_update(kf.handle, ctypes.c_void_p(z[t].data_ptr()), None,
+                                     ctypes.c_void_p(ld[t].data_ptr()), st))
+
+    # no warm-up: the C ABI needs none, and a first loop on another stream would make the
+    # capture wait on that stream's event (not capturable)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        loop()
+    kf.reset(x0)
+    g.replay()
+    torch.cuda.synchronize()
+    got = [l.clone() for l in ld] + list(kf.state())
+    kf.close()
+
+    with eager():
+        kf = kfmi.BatchedKF('cv3', B, 'f64')
+        kf.reset(x0)
+        ref = []
+        for t in range(T):
+            kf.predict(0.1, u[t])
+            ref.append(kf.update(z[t]))
+        ref += list(kf.state())
+        torch.cuda.synchronize()
+        kf.close()
+    for a, b in zip(got, ref):
+        close(a, b, 'f64')
