@@ -649,8 +649,10 @@ def sched_workload(cfg, args, rank, world, dev):
     pay[:, 0:3] = torch.where(gps, pay[:, 0:3] * 60.0, pay[:, 0:3])
     rates = torch.tensor(cfg['rates'], dtype=torch.float64, device=dev)
     # one rate per 64 consecutive filters (a wave): the sweep's filters batched by rate, so the
-    # lanes of a wave reach their processing windows together (the jitter aside)
-    freq = rates[(torch.arange(B, device=dev) // 64) % len(cfg['rates'])].contiguous()
+    # lanes of a wave reach their processing windows together (the jitter aside);
+    # --rate-block 1 gives every lane of a wave its own rate (the divergent case)
+    rb = max(1, int(getattr(args, 'rate_block', 64) or 64))
+    freq = rates[(torch.arange(B, device=dev) // rb) % len(cfg['rates'])].contiguous()
     prev = torch.full((B,), t0, dtype=torch.float64, device=dev)
     traj = kf.empty(T, 6, B)
     logdet = kf.empty(T, B)
@@ -833,6 +835,8 @@ def main():
     ap.add_argument('--pcie', action='store_true', help='also report the PCIe-inclusive rate (cv configs, N=1)')
     ap.add_argument('--per-step', action='store_true',
                     help='cv configs, N=1: also time the per-step predict()/update() call shape')
+    ap.add_argument('--rate-block', type=int, default=64,
+                    help='config sched: consecutive filters sharing a processing rate (1 = per-lane rates)')
     ap.add_argument('--graph', action='store_true',
                     help='config 1: replay the step as a hipGraph (measured no faster than eager launches)')
     ap.add_argument('--ablate', choices=['none', 'no-traj', 'no-logdet', 'no-traj-no-logdet'], default='none',

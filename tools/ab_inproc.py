@@ -27,6 +27,7 @@ def main():
     ap.add_argument('--config', default='ref15')
     ap.add_argument('--arms', required=True)
     ap.add_argument('--rounds', type=int, default=6)
+    ap.add_argument('--rate-block', type=int, default=64, help='config sched: filters per processing rate')
     ap.add_argument('--launches', type=int, default=10)
     args = ap.parse_args()
     import torch
@@ -51,7 +52,7 @@ def main():
                 fn.argtypes = argt
             arms.append((a, h, None))
     cfg = dict(bench.CONFIGS[args.config])
-    ns = argparse.Namespace(ablate='none', gpus=1, no_cpu_baseline=True)
+    ns = argparse.Namespace(ablate='none', gpus=1, no_cpu_baseline=True, rate_block=args.rate_block)
     if args.config == 'ref15':
         w = bench.ref15_workload(cfg, ns, 0, 1, dev)
     elif args.config in ('bf', 'bf_subsets'):

@@ -31,7 +31,7 @@ def main():
     out_dir, cfgs = sys.argv[1], sys.argv[2:]
     res = {'note': ' '.join(__doc__.split('\n\n')[2].split())}
     for c in cfgs:
-        kern = 'ref_events' if c == 'ref15' else 'cv_block_kernel'
+        kern = {'ref15': 'ref_events', 'sched': 'ref15_sched', '1': 'ref_chain_kernel'}.get(c, 'cv_block_kernel')
         d = os.path.join(out_dir, f'cfg{c}')
         vals = {}
         for ctr in COUNTERS:
