@@ -202,6 +202,38 @@ __global__ __launch_bounds__(256) void pattern_lds_kernel(const void* u, const v
     }
 }
 
+// SURVEY.md §7's alternative mapping, one filter per wavefront (the north_star's wording), as an
+// arithmetic-free pattern on the same [T][c][B] streams: wave w owns filter w; per step lanes
+// 0-2 load u, lanes 3-5 load z (8 B each from rows B * 8 bytes apart), the six values meet in
+// an LDS tile (the filter's shared state), and lanes 0-5 store the trajectory, lane 6 the
+// log-det.  fp64, cv3, update every step.  Compared with the lane-per-filter ring above it says
+// what the layout alone allows this mapping.
+__global__ __launch_bounds__(256) void pattern_wave_kernel(const double* __restrict__ u, const double* __restrict__ z,
+                                                           double* __restrict__ traj, double* __restrict__ logdet,
+                                                           int64_t B, int T_) {
+    __shared__ double tile[4][8];
+    const int lane = int(threadIdx.x & 63);
+    const int wave = int(threadIdx.x >> 6);
+    const int64_t f = int64_t(blockIdx.x) * 4 + wave;
+    if (f >= B) return;
+    double acc = 0.0;
+    for (int t = 0; t < T_; ++t) {
+        double v = 0.0;
+        if (lane < 3) v = u[(int64_t(t) * 3 + lane) * B + f];
+        else if (lane < 6) v = z[(int64_t(t) * 3 + lane - 3) * B + f];
+        if (lane < 6) tile[wave][lane] = v;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) s += tile[wave][i];
+        acc += s;
+        if (lane < 6) traj[(int64_t(t) * 6 + lane) * B + f] = acc + double(lane);
+        else if (lane == 6) logdet[int64_t(t) * B + f] = acc;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 template <int D, typename T>
 hipError_t launch(const void* u, const void* z, void* traj, void* logdet, int64_t B, int T_, int k, hipStream_t st) {
     pattern_kernel<D, T, 8><<<dim3(unsigned((B + 255) / 256)), 256, 0, st>>>(u, z, traj, logdet, B, T_, k);
@@ -246,5 +278,15 @@ extern "C" int kfprobe_pattern_lds(const void* u, const void* z, void* traj, voi
         return int(hipErrorInvalidValue);
     pattern_lds_kernel<2><<<dim3(unsigned((B + 255) / 256)), 256, 0, static_cast<hipStream_t>(stream)>>>(
         u, z, traj, logdet, B, T);
+    return int(hipGetLastError());
+}
+
+// pattern_wave_kernel on cv3 f64 buffers (as kfprobe_pattern_lds).
+extern "C" int kfprobe_pattern_wave(const void* u, const void* z, void* traj, void* logdet, int64_t B, int T,
+                                    void* stream) {
+    if (B <= 0 || T <= 0) return int(hipErrorInvalidValue);
+    pattern_wave_kernel<<<dim3(unsigned((B + 3) / 4)), 256, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<const double*>(u), static_cast<const double*>(z), static_cast<double*>(traj),
+        static_cast<double*>(logdet), B, T);
     return int(hipGetLastError());
 }
