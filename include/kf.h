@@ -23,6 +23,10 @@
  * describes the failure (thread-local).  Launching entry points are asynchronous on
  * the given hipStream_t (NULL = the null stream) and never synchronise, allocate or
  * free, so they can be captured into a hipGraph.
+ *
+ * Threading: distinct handles may be used from different threads at once; one handle is used
+ * by one thread at a time.  That includes the calls that only read it (kf_get_state,
+ * kf_get_status): they run a held-back kf_predict first (see kf_predict).
  */
 #ifndef KFMI_KF_H
 #define KFMI_KF_H
