@@ -313,6 +313,21 @@ class KF_SensorFusion:
         r = ingest.quaternion_to_euler(np.array([[x], [y], [z], [w]], dtype=np.float64), self.device)
         return tuple(float(v) for v in r[:, 0].cpu().numpy())
 
+    def compute_stationary_orientation(self, first_valid_index):
+        """kf_workers.py:427-439: mean roll, pitch, yaw of the unbiased IMU rows before
+        first_valid_index (the reference slices the IMU rows with that GPS index; kept)."""
+        rows = self.unbias_imu_data
+        pay = rows.h['payload'][rows.k[:first_valid_index]]
+        return tuple(np.mean([float(v) for v in pay[:, c]]) for c in range(3))
+
+    def euler_to_rotation_matrix(self, roll, pitch, yaw):
+        """kf_workers.py:441-458: R = Rz(yaw) Ry(pitch) Rx(roll)."""
+        cr, sr, cp, sp, cy, sy = np.cos(roll), np.sin(roll), np.cos(pitch), np.sin(pitch), np.cos(yaw), np.sin(yaw)
+        rx = np.array([[1, 0, 0], [0, cr, -sr], [0, sr, cr]])
+        ry = np.array([[cp, 0, sp], [0, 1, 0], [-sp, 0, cp]])
+        rz = np.array([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1]])
+        return rz @ ry @ rx
+
     def get_utm_data(self):
         return self.utm_data
 

@@ -52,6 +52,12 @@ def test_main_sequence(csvs, golden_dir, capsys):
     sf.unbias_imu_data(bw, ba)
     assert len(sf.unbias_imu_data) == 2500
     np.testing.assert_array_equal([r[4:10] for r in sf.unbias_imu_data[:50]], g['imu_values'][:50, 3:])
+    # kf_workers.py:427-439 as the reference computes it, over the façade's rows
+    rows = sf.unbias_imu_data[:fvi]
+    ref_orient = tuple(np.mean([e[c] for e in rows]) for c in (1, 2, 3))
+    assert sf.compute_stationary_orientation(fvi) == ref_orient
+    R = sf.euler_to_rotation_matrix(*ref_orient)
+    np.testing.assert_allclose(R @ R.T, np.eye(3), atol=1e-15)
     sf.combine_sensor_data()
     ev = sf.indexed_sensor_data
     assert len(ev) == len(g['ev_time'])

@@ -85,3 +85,20 @@ def test_greedy_schedule_empty_queue_raises():
     from kfmi.kf_workers import Scheduler
     with pytest.raises(ValueError, match='None is not in list'):
         Scheduler().greedy_schedule([], ref15.P0, None, None)
+
+
+def test_euler_to_rotation_matrix_composition():
+    """kf_workers.py:441-458: R = Rz(yaw) Ry(pitch) Rx(roll), a proper rotation."""
+    from kfmi import kf_workers as kfw
+    sf = object.__new__(kfw.KF_SensorFusion)  # host-only method: no GPU, no data
+    a = 0.7
+    np.testing.assert_allclose(sf.euler_to_rotation_matrix(0.0, 0.0, a),
+                               [[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]], atol=1e-15)
+    np.testing.assert_allclose(sf.euler_to_rotation_matrix(a, 0.0, 0.0),
+                               [[1, 0, 0], [0, np.cos(a), -np.sin(a)], [0, np.sin(a), np.cos(a)]], atol=1e-15)
+    R = sf.euler_to_rotation_matrix(0.1, -0.2, 0.3)
+    np.testing.assert_allclose(R @ R.T, np.eye(3), atol=1e-15)
+    assert abs(np.linalg.det(R) - 1.0) < 1e-15
+    # the x axis after a pitch then a yaw
+    np.testing.assert_allclose(sf.euler_to_rotation_matrix(0.0, a, a) @ [1, 0, 0],
+                               [np.cos(a) * np.cos(a), np.sin(a) * np.cos(a), -np.sin(a)], atol=1e-15)
