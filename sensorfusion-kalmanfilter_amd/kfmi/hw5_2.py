@@ -14,6 +14,28 @@ from .kf_workers import CsvTable, EventList, ImuRows, KF_SensorFusion as _KF15
 __all__ = ['KF_SensorFusion']
 
 
+# The 8-state model (x, y, theta, vx, vy, theta_dot, ax, ay) as hw5_2.py:219-311 defines it, for
+# callers that build their own step from the getters (the device kernels never materialise them).
+def _F8(dt):
+    F = np.eye(8)
+    for p, v, a in ((0, 3, 6), (1, 4, 7)):   # x, y: position, velocity, acceleration chains
+        F[p, v] = dt
+        F[p, a] = 0.5 * dt ** 2
+        F[v, a] = dt
+    F[2, 5] = dt                              # theta from theta_dot
+    return F
+
+
+def _Q8(dt):
+    return np.diag([5 * dt, 5 * dt, 0.05 * dt, 1 * dt, 1 * dt, 0.1 * dt, 2 * dt, 2 * dt])
+
+
+_H_GPS8 = np.eye(8, dtype=np.int64)[:2]
+_H_IMU8 = np.eye(8, dtype=np.int64)
+_R_GPS8 = np.diag([3, 3])
+_R_IMU8 = np.diag([50, 50, 0.05, 10, 10, 0.1, 100, 100])
+
+
 class KF_SensorFusion:
     def __init__(self, gps_csv_file, imu_csv_file, dtype='f64', device=0):
         self.gps_csv_file = gps_csv_file
@@ -52,6 +74,37 @@ class KF_SensorFusion:
     def quaternion_to_euler(self, x, y, z, w):
         r = ingest.quaternion_to_euler(np.array([[x], [y], [z], [w]], dtype=np.float64), self.device)
         return tuple(float(v) for v in r[:, 0].cpu().numpy())
+
+    def compute_stationary_orientation(self, first_valid_index):
+        """hw5_2.py:149-164 without its plot: mean roll, pitch, yaw of the unbiased IMU rows."""
+        return _KF15.compute_stationary_orientation(self, first_valid_index)
+
+    euler_to_rotation_matrix = _KF15.euler_to_rotation_matrix  # hw5_2.py:166-184
+
+    # -- model (hw5_2.py:219-311) -----------------------------------------------------------
+    def get_state_transition_matrix(self, dt):
+        return _F8(dt)
+
+    def get_process_noise_covariance_matrix(self, dt):
+        return _Q8(dt)
+
+    def predict_covariance(self, Pt, F, Qt):
+        return np.dot(np.dot(F, Pt), F.T) + Qt
+
+    def get_gps_observation_matrix(self):
+        return _H_GPS8.copy()
+
+    def get_imu_observation_matrix(self):
+        return _H_IMU8.copy()
+
+    def get_gps_measurement_noise_covariance_matrix(self):
+        return _R_GPS8.copy()
+
+    def get_imu_measurement_noise_covariance_matrix(self):
+        return _R_IMU8.copy()
+
+    def calculate_kalman_gain(self, P_next, H, R):
+        return np.dot(np.dot(P_next, H.T), np.linalg.inv(np.dot(np.dot(H, P_next), H.T) + R))
 
     def run_kalman_filter(self):
         """hw5_2.py:313-380: [(x, y, theta), ...]."""

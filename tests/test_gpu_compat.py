@@ -122,8 +122,10 @@ def test_hw5_2_sequence(csvs):
     sf.load_data()
     sf.gps_to_utm()
     assert all('altitude' not in u for u in sf.utm_data)
-    bw, ba, _ = sf.compute_imu_biases(sf.gps_data, sf.imu_data)
+    bw, ba, fvi = sf.compute_imu_biases(sf.gps_data, sf.imu_data)
     sf.unbias_imu_data(bw, ba)
+    rows = sf.unbias_imu_data[:fvi]
+    assert sf.compute_stationary_orientation(fvi) == tuple(np.mean([e[c] for e in rows]) for c in (1, 2, 3))
     sf.combine_sensor_data()
     st = sf.run_kalman_filter()
     events, _, _ = ref_ingest.ingest(*csvs, with_altitude=False)

@@ -271,3 +271,23 @@ def test_c_ref15_events_vs_numpy_oracle(cpu_kf):
                 x, P = ref_kf.step15(x, P, 'GPS' if ty == 0 else 'IMU', sd, dt[t, f])
             assert _rel(tr[t, :, f], x[:6]) < 1e-10
             assert abs(ld[t, f] - np.linalg.slogdet(P)[1]) < 1e-10 * max(1, abs(np.linalg.slogdet(P)[1]))
+
+
+def test_hw5_2_facade_model_getters_match_the_oracle():
+    """kfmi.hw5_2's host model getters (hw5_2.py:219-311) equal the oracle's 8-state model."""
+    from kfmi import hw5_2 as khw5
+    sf = object.__new__(khw5.KF_SensorFusion)  # host-only methods: no GPU, no data
+    for dt in (0.0, 0.005, 0.1, 1.7):
+        np.testing.assert_array_equal(sf.get_state_transition_matrix(dt), ref_kf.F_ref8(dt))
+        np.testing.assert_array_equal(sf.get_process_noise_covariance_matrix(dt), ref_kf.Q_ref8(dt))
+    np.testing.assert_array_equal(sf.get_gps_observation_matrix(), ref_kf.H_gps8())
+    np.testing.assert_array_equal(sf.get_imu_observation_matrix(), ref_kf.H_imu8())
+    np.testing.assert_array_equal(sf.get_gps_measurement_noise_covariance_matrix(), ref_kf.R_gps8())
+    np.testing.assert_array_equal(sf.get_imu_measurement_noise_covariance_matrix(), ref_kf.R_imu8())
+    rng = np.random.default_rng(3)
+    A = rng.normal(size=(8, 8))
+    P = A @ A.T + 8 * np.eye(8)
+    H, R = ref_kf.H_gps8(), ref_kf.R_gps8()
+    np.testing.assert_array_equal(sf.calculate_kalman_gain(P, H, R), ref_kf.calculate_kalman_gain(P, H, R))
+    F, Q = ref_kf.F_ref8(0.1), ref_kf.Q_ref8(0.1)
+    np.testing.assert_array_equal(sf.predict_covariance(P, F, Q), ref_kf.predict_covariance(P, F, Q))
