@@ -50,6 +50,7 @@ CONFIGS = {
     '4': dict(model='cv3', dtype='f32', B=1048576, T=256, dt=0.1, k=1),
     '5': dict(model='cv3', dtype='f64', B=1048576, T=500, dt=0.01, k=10),
     'ref15': dict(model='ref15', dtype='f64', B=1048576, T=256, dt=0.005, k=20),
+    'ref15f32': dict(model='ref15', dtype='f32', B=1048576, T=256, dt=0.005, k=20),
     'bf': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=True),
     'bf_subsets': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=False),
     'sched': dict(model='ref15', dtype='f64', B=1048576, T=256, dt=0.005, k=20,
@@ -82,10 +83,12 @@ def algorithmic_bytes(cfg, block=None):
 
 def ref15_algorithmic_bytes(cfg):
     """Bytes one kf_run_events launch must move for the 15-state model: per filter per event
-    etype 1 + dt 8 + payload 72 read, traj 48 + logdet 8 written; per filter per launch the
-    state (15 + 27 block rows) loaded and stored and status read + written."""
+    etype 1 + dt 8 (always f64) + payload 9 w read, traj 6 w + logdet w written (w = 8 in f64, 4
+    in f32); per filter per launch the state (15 + 27 block rows) loaded and stored and status
+    read + written."""
     T, B = cfg['T'], cfg['B']
-    per_filter = T * (1 + 8 + 72 + 48 + 8) + 2 * (15 + 27) * 8 + 8
+    w = 8 if cfg['dtype'] == 'f64' else 4
+    per_filter = T * (1 + 8 + 9 * w + 6 * w + w) + 2 * (15 + 27) * w + 8
     return per_filter * B, per_filter / T
 
 
@@ -344,7 +347,7 @@ def ref15_workload(cfg, args, rank, world, dev):
     from kfmi import _lib
     from kfmi.engine import _ptr
     B, T, dt, k = cfg['B'], cfg['T'], cfg['dt'], cfg['k']
-    kf = kfmi.BatchedKF('ref15', B, 'f64', device=dev.index)
+    kf = kfmi.BatchedKF('ref15', B, cfg['dtype'], device=dev.index)
     g = torch.Generator(device=dev).manual_seed(SEED + rank)
     etype = torch.ones(T, B, dtype=torch.uint8, device=dev)
     etype[k - 1::k] = 0
@@ -355,6 +358,7 @@ def ref15_workload(cfg, args, rank, world, dev):
     pay[:, 6:9] *= 0.3    # accelerations
     gps = (etype == 0)[:, None, :]
     pay[:, 0:3] = torch.where(gps, pay[:, 0:3] * 60.0, pay[:, 0:3])  # GPS fixes within ~3 m
+    pay = pay.to(kf.torch_dtype)  # the fp32 row: the same draws rounded once
     traj = kf.empty(T, 6, B)
     logdet = kf.empty(T, B)
 
@@ -375,7 +379,7 @@ def ref15_workload(cfg, args, rank, world, dev):
         nf = min(B, 1 << 15)
         et = etype[:, :nf].cpu().numpy()
         dd = dts[:, :nf].cpu().numpy()
-        pa = pay[:, :, :nf].cpu().numpy()
+        pa = pay[:, :, :nf].double().cpu().numpy()
         x0 = np.zeros((15, nf))
         done, t0 = 0, time.perf_counter()
         chunk = max(nth * 16, 64)
@@ -426,7 +430,7 @@ def ref15_workload(cfg, args, rank, world, dev):
         xs.zero_()
         Ps.zero_()
         stream = torch.cuda.current_stream(dev)
-        run = lambda: lib.kfprobe_ref_pattern(1, etype.data_ptr(), dts.data_ptr(), pay.data_ptr(), xs.data_ptr(),
+        run = lambda: lib.kfprobe_ref_pattern(int(cfg['dtype'] == 'f64'), etype.data_ptr(), dts.data_ptr(), pay.data_ptr(), xs.data_ptr(),
                                               Ps.data_ptr(), traj.data_ptr(), logdet.data_ptr(), B, T,
                                               ctypes.c_void_p(stream.cuda_stream))
         for _ in range(3):
@@ -446,8 +450,10 @@ def ref15_workload(cfg, args, rank, world, dev):
                         'row stores on the same buffers, the event arithmetic reduced to a sum'}
 
     return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_event, probe=probe,
-                kernel='ref_events_lds_kernel', traffic=load_traffic('ref15'), valu=load_valu('ref15'), cpu=cpu, gather=gather_payload, kf=kf,
-                desc=f'SURVEY 8f row 2: reference 15-state model (kf_workers.py:493-614), f64, B={B} filters/GPU, '
+                kernel='ref_events_lds_kernel',
+                traffic=load_traffic('ref15') if cfg['dtype'] == 'f64' else None,
+                valu=load_valu('ref15') if cfg['dtype'] == 'f64' else None, cpu=cpu, gather=gather_payload, kf=kf,
+                desc=f'SURVEY 8f row 2: reference 15-state model (kf_workers.py:493-614), {cfg["dtype"]}, B={B} filters/GPU, '
                      f'T={T} events (IMU 200 Hz, GPS fix every {k}th event), dt={dt}',
                 extra={'filters_per_gpu': B, 'events_per_launch': T})
 
@@ -871,7 +877,7 @@ def main():
         cfg['B'] = args.batch
     if args.config in ('1', '1seq'):
         w = log_workload(cfg, args, rank, world, dev)
-    elif args.config == 'ref15':
+    elif args.config in ('ref15', 'ref15f32'):
         w = ref15_workload(cfg, args, rank, world, dev)
     elif args.config == 'sched':
         w = sched_workload(cfg, args, rank, world, dev)
