@@ -53,7 +53,7 @@ def main():
             arms.append((a, h, None))
     cfg = dict(bench.CONFIGS[args.config])
     ns = argparse.Namespace(ablate='none', gpus=1, no_cpu_baseline=True, rate_block=args.rate_block)
-    if args.config == 'ref15':
+    if args.config in ('ref15', 'ref15f32'):
         w = bench.ref15_workload(cfg, ns, 0, 1, dev)
     elif args.config in ('bf', 'bf_subsets'):
         w = bench.bf_workload(cfg, ns, 0, 1, dev)
