@@ -385,6 +385,22 @@ __device__ __forceinline__ void stb(void* base, int64_t r, uint32_t row_bytes, u
 __device__ __forceinline__ void stb(void* base, int64_t r, uint32_t row_bytes, uint32_t off, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), row_rsrc(base, r, row_bytes), off, 0, 0);
 }
+// Per-step record rows of the fused run (trajectory, log-det): written once, read by nobody in the
+// launch, tens of GB per launch — stored non-temporal.  In-process A/Bs on two boxes
+// (profiles/r02_ab/store_nt_ab*.txt): config 3 -1.2..-1.6%, config 2 -1.9..-2.3%, config 5
+// -0.9%, config 4 -0.4%.  Other stores keep the default policy (state and buffers that a later
+// launch reads back can still hit the caches).  -DKF_REC_CPOL=0 restores the default.
+#ifndef KF_REC_CPOL
+#define KF_REC_CPOL 2
+#endif
+__device__ __forceinline__ void stb_rec(void* base, int64_t r, uint32_t row_bytes, uint32_t off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), row_rsrc(base, r, row_bytes), off, 0,
+                                          KF_REC_CPOL);
+}
+__device__ __forceinline__ void stb_rec(void* base, int64_t r, uint32_t row_bytes, uint32_t off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), row_rsrc(base, r, row_bytes), off, 0,
+                                          KF_REC_CPOL);
+}
 
 // ------------------------------------------------------------------------------------
 // Synthetic GPS+IMU streams: Philox4x32-10 (Salmon et al., SC'11), counter = (t, draw,

@@ -243,11 +243,11 @@ __global__ __launch_bounds__(kBlock, (RunOcc<D, T>::value)) void cv_run_kernel(c
             }
         }
 #pragma unroll
-        for (int i = 0; i < N; ++i) stb_stream(a.traj, int64_t(t) * N + i, rb_tr, off, x[i]);
+        for (int i = 0; i < N; ++i) stb_rec(a.traj, int64_t(t) * N + i, rb_tr, off, x[i]);
         if (has_ld) {
             const T ld = logdet_ldl<N, T>(P);
             st = (ld == ld) ? st : kNotSpd;
-            stb_stream(a.logdet, t, rb, off, ld);
+            stb_rec(a.logdet, t, rb, off, ld);
         }
     };
 
@@ -371,8 +371,8 @@ __global__ __launch_bounds__(kBlock) void cv_block_kernel(const CvArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            stb(a.traj, int64_t(t) * N + i, rb, off, xp[i]);
-            stb(a.traj, int64_t(t) * N + D + i, rb, off, xv[i]);
+            stb_rec(a.traj, int64_t(t) * N + i, rb, off, xp[i]);
+            stb_rec(a.traj, int64_t(t) * N + D + i, rb, off, xv[i]);
         }
         // logdet: LDL pivots in the general 6x6 order (positions, then velocities)
         T prod = T(1);
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(kBlock) void cv_block_kernel(const CvArgs a) {
         ex += e;
         const T ld = pd ? log_mant(prod, ex) : quiet_nan<T>();
         st = (ld == ld) ? st : kNotSpd;
-        stb(a.logdet, t, rb, off, ld);
+        stb_rec(a.logdet, t, rb, off, ld);
     };
     // Inputs are prefetched DEPTH - 1 steps ahead through a ring of DEPTH named buffers (the
     // ring is fully unrolled, so every buffer index is static and nothing is copied): with few

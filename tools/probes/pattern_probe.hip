@@ -50,8 +50,8 @@ __global__ __launch_bounds__(256) void pattern_kernel(const void* u, const void*
 #pragma unroll
         for (int i = 0; i < D; ++i) acc += in.u[i] + in.z[i];
 #pragma unroll
-        for (int i = 0; i < N; ++i) stb(traj, int64_t(t) * N + i, rb, off, acc + T(i));
-        stb(logdet, t, rb, off, acc);
+        for (int i = 0; i < N; ++i) stb_rec(traj, int64_t(t) * N + i, rb, off, acc + T(i));
+        stb_rec(logdet, t, rb, off, acc);
     };
     ProbeIn<D, T> buf[DEPTH];
 #pragma unroll
