@@ -327,11 +327,13 @@ __device__ __forceinline__ void stv(__amdgpu_buffer_rsrc_t r, uint32_t voff, flo
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, voff, 0, 0);
 }
 
-// Cache policy of the once-touched streams (inputs read once, records written once).  Default
-// policy: nt (aux = 2) was A/B-measured mixed (config 2 +3 %, config 4 -2 %, configs 3/5 within
-// box noise; profiles/r01_ab/nt_streams_ab.txt).  -DKF_STREAM_CPOL=2 builds the nt variant.
+// Cache policy of the once-touched input streams (u, z: read once per launch).  nt (aux = 2):
+// round 1 measured it mixed across processes (profiles/r01_ab/nt_streams_ab.txt); late round 2's
+// in-process A/Bs, arms in both orders, give config 3 -0.6..-0.8 %, config 5 -0.5..-0.7 %,
+// configs 2 and 4 within noise (profiles/r02_ab/load_nt_ab*.txt), so nt is the default.
+// -DKF_STREAM_CPOL=0 builds the default-policy variant.
 #ifndef KF_STREAM_CPOL
-#define KF_STREAM_CPOL 0
+#define KF_STREAM_CPOL 2
 #endif
 __device__ __forceinline__ double ldb_stream(const void* base, int64_t r, uint32_t row_bytes, uint32_t off, double) {
     return __builtin_bit_cast(double, (v2u)__builtin_amdgcn_raw_buffer_load_b64(row_rsrc(base, r, row_bytes), off, 0,
