@@ -354,8 +354,14 @@ __device__ __forceinline__ void stb_stream(void* base, int64_t r, uint32_t row_b
 
 // LDS-DMA: 64 lanes x 16 B from a row-span descriptor (the lane's chunk at voff + soff) to the
 // wave-uniform LDS address `lds` + lane * 16 (buffer_load_dwordx4 ... lds).
+// Cache policy of the LDS-DMA input loads.  nt (-DKF_DMA_CPOL=2) made the ref15 event kernel
+// 2 % slower and left sched, bf and config 1 unchanged (profiles/r02_ab/dma_nt_ab.txt).
+#ifndef KF_DMA_CPOL
+#define KF_DMA_CPOL 0
+#endif
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, unsigned char* lds, uint32_t voff, int soff) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0,
+                                             KF_DMA_CPOL);
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t bytes_rsrc(const void* p, uint32_t nbytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, p ? nbytes : 0u, 0x00020000);
