@@ -330,7 +330,8 @@ __device__ __forceinline__ void stv(__amdgpu_buffer_rsrc_t r, uint32_t voff, flo
 // Cache policy of the once-touched input streams (u, z: read once per launch).  nt (aux = 2):
 // round 1 measured it mixed across processes (profiles/r01_ab/nt_streams_ab.txt); late round 2's
 // in-process A/Bs, arms in both orders, give config 3 -0.6..-0.8 %, config 5 -0.5..-0.7 %,
-// configs 2 and 4 within noise (profiles/r02_ab/load_nt_ab*.txt), so nt is the default.
+// configs 2 and 4 within noise on slow-placement boxes and config 3 / 5 -2.1 / -2.2 % on a
+// fast one (profiles/r02_ab/load_nt_ab*.txt), so nt is the default.
 // -DKF_STREAM_CPOL=0 builds the default-policy variant.
 #ifndef KF_STREAM_CPOL
 #define KF_STREAM_CPOL 2
