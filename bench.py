@@ -18,9 +18,13 @@ Configs (BASELINE.json / SURVEY.md §8d); per GPU (weak scaling: each rank owns 
 SURVEY.md §8f rows on the same engine (not BASELINE lines):
     ref15  the reference's 15-state model, fp64, B=1,048,576 filters, T=256 events of a 200 Hz
            IMU + 10 Hz GPS stream (kf_run_events)
+    ref15f32  the same in fp32
     bf     the reference's brute-force search: every k-subset (k = 1..25) of n = 25 candidate
            events (kf_workers.py:2311), 2^25 - 1 filters (kf_eval_combos)
-Rank 0 prints ONE JSON line.
+    sched  the rate-decimated greedy scheduled filter, B=1,048,576, rates 10..120 Hz
+           (--rate-block 1: every lane its own rate)
+Rank 0 prints ONE JSON line.  KFMI_BENCH_DIST_BACKEND=gloo (rehearsal only) lets N ranks share
+one GPU (tools/dist_rehearsal.sh); the real N>1 run is RCCL, one GPU per rank.
 """
 from __future__ import annotations
 
