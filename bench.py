@@ -3,6 +3,12 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
     torchrun --nproc-per-node N bench.py --gpus N ...        (multi-GPU, RCCL)
 
+`python bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment) starts the N ranks itself
+as child processes (torch.distributed.run, rendezvous on 127.0.0.1) before anything touches the
+GPU, and exits with their status; the JSON line records `ranks_seen`, and a rank count other
+than --gpus is an error.  For N > 1 the final all-gather reassembles every shard's final state,
+last log-det and trajectory decimated every --gather-traj-every steps (`allgather`).
+
 One bench *step* = one launch of the hot path over one batch of synthetic input that is
 resident in HBM before timing starts.  Consecutive steps continue the same filters (warm
 start, like the reference's windowed runs, kf_workers.py:2316-2323) over the same inputs.
@@ -23,8 +29,9 @@ SURVEY.md §8f rows on the same engine (not BASELINE lines):
            events (kf_workers.py:2311), 2^25 - 1 filters (kf_eval_combos)
     sched  the rate-decimated greedy scheduled filter, B=1,048,576, rates 10..120 Hz
            (--rate-block 1: every lane its own rate)
-Rank 0 prints ONE JSON line.  KFMI_BENCH_DIST_BACKEND=gloo (rehearsal only) lets N ranks share
-one GPU (tools/dist_rehearsal.sh); the real N>1 run is RCCL, one GPU per rank.
+Rank 0 prints ONE JSON line.  --dist-backend gloo (rehearsal only) lets N ranks share one GPU
+(tools/dist_rehearsal.sh); the real N>1 run is RCCL, one GPU per rank.  --opt NAME=VALUE sets a
+kf_set_option on the workload's handle (A/B runs; the library reads no environment).
 """
 from __future__ import annotations
 
@@ -53,6 +60,9 @@ CONFIGS = {
     '3': dict(model='cv3', dtype='f64', B=1048576, T=256, dt=0.1, k=1),
     '4': dict(model='cv3', dtype='f32', B=1048576, T=256, dt=0.1, k=1),
     '5': dict(model='cv3', dtype='f64', B=1048576, T=500, dt=0.01, k=10),
+    # config 3 with the axes coupled: correlated GPS noise R and a coupled initial P (a caller's
+    # class_args / warm start), so every filter runs the general kernel (cv_run_kernel)
+    '3gen': dict(model='cv3', dtype='f64', B=1048576, T=256, dt=0.1, k=1, coupled=True),
     'ref15': dict(model='ref15', dtype='f64', B=1048576, T=256, dt=0.005, k=20),
     'ref15f32': dict(model='ref15', dtype='f32', B=1048576, T=256, dt=0.005, k=20),
     'bf': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=True),
@@ -62,11 +72,35 @@ CONFIGS = {
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 SEED = 20251015
+# config 3gen's coupling: GPS noise correlated across the axes, and an initial covariance with
+# 0.2 correlation between axes and 0.1 between each position and the velocities
+R_COUPLED = [[3.0, 1.0, 0.5], [1.0, 3.0, 1.0], [0.5, 1.0, 3.0]]
 
 
-def block_kernel_in_use():
-    """kf_run takes cv_block_kernel for the bench's handles (diagonal R, P = P0) unless forced."""
-    return os.environ.get('KFMI_CV_KERNEL', 'auto') != 'general'
+def coupled_p0(d=3):
+    """The reference P0 (kf_workers.py:651) with cross-axis correlation (SPD)."""
+    sd = np.sqrt(np.r_[[1e4] * d, [1e3] * d])
+    C = np.full((d, d), 0.2) + 0.8 * np.eye(d)
+    corr = np.block([[C, 0.1 * np.eye(d)], [0.1 * np.eye(d), C]])
+    return corr * np.outer(sd, sd)
+
+
+def cv_params(cfg):
+    """kf_params of the config's handle: the reference constants, or R_COUPLED for 3gen."""
+    if not cfg.get('coupled'):
+        return None
+    from kfmi.engine import default_params
+    p = default_params(cfg['model'])
+    for i in range(3):
+        for j in range(3):
+            p.r[i * 3 + j] = R_COUPLED[i][j]
+    return p
+
+
+def block_kernel_in_use(cfg):
+    """kf_run takes cv_block_kernel for the bench's handles (diagonal R, P = P0) unless the
+    handle's cv_kernel option forces the general kernel or the config couples the axes."""
+    return cfg.get('opts', {}).get('cv_kernel', 'auto') not in ('general', 1) and not cfg.get('coupled')
 
 
 def algorithmic_bytes(cfg, block=None):
@@ -79,7 +113,7 @@ def algorithmic_bytes(cfg, block=None):
     w = 8 if cfg['dtype'] == 'f64' else 4
     T, k, B = cfg['T'], cfg['k'], cfg['B']
     U = T // k
-    block = block_kernel_in_use() if block is None else block
+    block = block_kernel_in_use(cfg) if block is None else block
     p_entries = 3 * d if block else n * (n + 1) // 2
     per_filter = T * (c + n + 1) * w + U * m * w + 2 * (n + p_entries) * w + 2 * 4
     return per_filter * B, per_filter / T
@@ -121,12 +155,12 @@ def load_valu(cfg_id):
     """VALU issue of the dominant kernel from the committed rocprofv3 SQ-counter summary
     (tools/pmc_valu.sh; SURVEY.md §8d asks for the VALU fraction beside the HBM roofline)."""
     try:
-        with open(os.path.join(ROOT, 'profiles', 'r02_valu', 'pmc_valu.json')) as f:
+        with open(os.path.join(ROOT, 'profiles', 'pmc_valu.json')) as f:
             rec = json.load(f).get(f'config{cfg_id}')
         return None if rec is None else {
             'issue_frac': rec['valu_issue_frac'], 'valu_insts_per_wave_step': rec['valu_per_wave_step'],
             'issue_stall_frac_of_wave_cycles': rec['wave_cycles_issue_stall_frac'],
-            'source': 'profiles/r02_valu/pmc_valu.json (SQ_INSTS_VALU x 4 cycles / (kernel time x 2.4 GHz x 1024 SIMDs))'}
+            'source': 'profiles/pmc_valu.json (SQ_INSTS_VALU x 4 cycles / (kernel time x 2.4 GHz x 1024 SIMDs))'}
     except (OSError, ValueError, KeyError):
         return None
 
@@ -139,13 +173,19 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
     import kfmi
     from kfmi import dist as kdist
     B, T, k, dt = cfg['B'], cfg['T'], cfg['k'], cfg['dt']
-    kf = kfmi.BatchedKF(cfg['model'], B, cfg['dtype'], device=dev.index)
+    kf = kfmi.BatchedKF(cfg['model'], B, cfg['dtype'], device=dev.index, params=cv_params(cfg),
+                        options=cfg.get('opts'))
     # weak scaling: world*B filters in total; shard r owns a contiguous slice and regenerates
     # its own streams from the counter-based generator (keyed by the global filter index)
     offset, count = kdist.shard_range(world * B, rank, world)
     assert count == B
     x0, u, z = kf.synth(T=T, dt=dt, update_every=k, seed=SEED, filter_offset=offset)
     kf.reset(x0)
+    P0 = coupled_p0() if cfg.get('coupled') else None
+    if P0 is not None:
+        iu = np.triu_indices(P0.shape[0])  # the handle's packed upper triangle, row-major (include/kf.h)
+        rows = torch.as_tensor(P0[iu], dtype=kf.torch_dtype, device=dev)
+        kf.set_state(x0, rows[:, None].expand(-1, B).contiguous())
     traj = kf.empty(T, kf.n, B)
     logdet = kf.empty(T, B)
     out = (None if 'no-traj' in args.ablate else traj, None if 'no-logdet' in args.ablate else logdet)
@@ -155,16 +195,17 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
 
     def gather_payload():
         xf, _ = kf.state()
-        return torch.cat([xf, logdet[-1:]], dim=0).contiguous()
+        return xf, logdet[-1], (None if out[0] is None else traj)
 
     def cpu():
         """The reference's per-filter step restated in C (oracle/cpu_kf.c: dense matrices in the
         reference's op order, OpenMP over filters) on this host's allotted cores for ~10 s of
         this workload; plus the NumPy reference loop (oracle/ref_kf.run_filter_loop) on 1 core."""
-        from oracle import cpu_kf, ref_kf
-        model = ref_kf.CV2 if cfg['model'] == 'cv2' else ref_kf.CV3
+        from oracle import cpu_kf, numpy_pool
         d = 2 if cfg['model'] == 'cv2' else 3
         nth = cpu_kf.threads()
+        P0h = coupled_p0() if cfg.get('coupled') else np.diag([kf.params.p0_pos] * d + [kf.params.p0_vel] * d)
+        Rh = np.array(R_COUPLED) if cfg.get('coupled') else None
         nf = min(B, 1 << 17)   # ~10 s on 16 cores; the loop below stops at 10 s regardless
         idx = torch.linspace(0, B - 1, nf).long().to(u.device)
         xs = x0[:, idx].double().cpu().numpy()
@@ -174,22 +215,23 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
         chunk = max(nth * 64, 256)
         while done < nf and time.perf_counter() - t0 < 10.0:
             hi = min(nf, done + chunk)
-            cpu_kf.cv_run(d, xs, model.P0(), dt, us, zs, k, filters=(done, hi), nthreads=nth)
+            cpu_kf.cv_run(d, xs, P0h, dt, us, zs, k, filters=(done, hi), nthreads=nth, R=Rh)
             done = hi
         el = time.perf_counter() - t0
-        # the NumPy reference loop, 1 core, ~3 s
-        n_np, t1 = 0, time.perf_counter()
-        while n_np < nf and time.perf_counter() - t1 < 3.0:
-            ref_kf.run_filter_loop(model, xs[:, n_np], model.P0(), np.full(T, dt), us[:, :, n_np], zs[:, :, n_np], k)
-            n_np += 1
-        el_np = time.perf_counter() - t1
+        # the NumPy reference loop on every allotted core (the reference's Pool fan-out), ~3 s:
+        # each worker its own slice of the sampled filters
+        per = min(nf // nth, -(-130000 * 3 // T))
+        shards = [dict(d=d, x0=xs[:, r * per:(r + 1) * per], P0=P0h, R=Rh, dt=dt, k=k, n=per,
+                       u=us[:, :, r * per:(r + 1) * per], z=zs[:, :, r * per:(r + 1) * per]) for r in range(nth)]
+        npl = numpy_pool.run('cv', shards, seconds=3.0)
         return {'value': done * T / el, 'unit': 'KF steps/s', 'cores': nth, 'kind': 'port',
                 'sample': f'{done} filters x {T} steps of this workload (same synthetic streams) through '
                           f'oracle/cpu_kf.c (the reference step, dense, C -O3 OpenMP) on {nth} threads, {host_cpu()}',
                 'seconds': round(el, 2),
-                'numpy_reference_loop': {'value': n_np * T / el_np, 'cores': 1,
-                                         'sample': f'{n_np} filters, oracle/ref_kf.run_filter_loop, '
-                                                   f'NumPy {np.__version__}'}}
+                'numpy_reference_loop': dict(npl, sample=f"{npl['filters']} filters of this workload, "
+                                             f"oracle/ref_kf.run_filter_loop (the reference's per-step NumPy calls) "
+                                             f"in a spawn Pool of {npl['cores']} processes, one BLAS thread each, "
+                                             f"NumPy {np.__version__}")}
 
     def pcie(reps=3):
         """PCIe-inclusive rate: the inputs start in pinned host memory and the
@@ -236,11 +278,10 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
         """The reference's call shape: T steps of BatchedKF.predict(dt, u[t]) then
         BatchedKF.update(z[t]) (its log-det returned).  By default kf_predict is held back and
         runs fused with the next kf_update (one state round trip per step, plus a copy of u);
-        KFMI_PREDICT=eager launches each call on its own (two round trips).  Against kf_run's
-        fused launch on the same streams.  Never `value`."""
+        the handle option predict='eager' launches each call on its own (two round trips).
+        Against kf_run's fused launch on the same streams.  Never `value`."""
         def loop(mode):
-            old = os.environ.get('KFMI_PREDICT')
-            os.environ['KFMI_PREDICT'] = mode
+            kf.set_option('predict', mode)
             try:
                 kf.reset(x0)
                 times = []
@@ -255,10 +296,7 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
                     times.append(time.perf_counter() - t0)
                 return min(times[1:])
             finally:
-                if old is None:
-                    os.environ.pop('KFMI_PREDICT')
-                else:
-                    os.environ['KFMI_PREDICT'] = old
+                kf.set_option('predict', cfg.get('opts', {}).get('predict', 'auto'))
 
         el = loop('deferred')
         el_eager = loop('eager')
@@ -269,7 +307,7 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
                     'update_every': k, 'note': 'predict every step, update every %d-th, through BatchedKF; '
                     'best of %d' % (k, reps),
                     'eager': {'value': B * T / el_eager, 'ms_per_step': el_eager / T * 1e3,
-                              'note': 'KFMI_PREDICT=eager: one kernel per call'}}
+                              'note': "option predict='eager': one kernel per call"}}
         # the same steps as T launches of kf_run with T = 1 (predict + update fused, one state
         # round trip per step, trajectory and log-det rows written)
         kf.reset(x0)
@@ -295,7 +333,7 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
                         'predict held back and fused into the update; best of %d' % reps,
                 'eager': {'value': B * T / el_eager, 'ms_per_step': el_eager / T * 1e3,
                           'gbs': nbytes_eager / el_eager / 1e9, 'launches': 2 * T,
-                          'note': 'KFMI_PREDICT=eager: one kernel per call'},
+                          'note': "option predict='eager': one kernel per call"},
                 'run_t1': {'value': B * T / el1, 'ms_per_step': el1 / T * 1e3, 'launches': T,
                            'note': 'BatchedKF.run on one step at a time (kf_run, T = 1: predict + update fused)'}}
 
@@ -333,7 +371,7 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
 
     d = 2 if cfg['model'] == 'cv2' else 3
     bytes_launch, bytes_step = algorithmic_bytes(cfg)
-    kernel = 'cv_block_kernel' if block_kernel_in_use() else 'cv_run_kernel'
+    kernel = 'cv_block_kernel' if block_kernel_in_use(cfg) else 'cv_run_kernel'
     return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_step, kernel=kernel,
                 traffic=load_traffic(cfg_id) if kernel == 'cv_block_kernel' else None, cpu=cpu,
                 valu=load_valu(cfg_id) if kernel == 'cv_block_kernel' else None,
@@ -351,7 +389,7 @@ def ref15_workload(cfg, args, rank, world, dev):
     from kfmi import _lib
     from kfmi.engine import _ptr
     B, T, dt, k = cfg['B'], cfg['T'], cfg['dt'], cfg['k']
-    kf = kfmi.BatchedKF('ref15', B, cfg['dtype'], device=dev.index)
+    kf = kfmi.BatchedKF('ref15', B, cfg['dtype'], device=dev.index, options=cfg.get('opts'))
     g = torch.Generator(device=dev).manual_seed(SEED + rank)
     etype = torch.ones(T, B, dtype=torch.uint8, device=dev)
     etype[k - 1::k] = 0
@@ -372,7 +410,7 @@ def ref15_workload(cfg, args, rank, world, dev):
 
     def gather_payload():
         xf, _ = kf.state()
-        return torch.cat([xf, logdet[-1:]], dim=0).contiguous()
+        return xf, logdet[-1], traj
 
     def cpu():
         """The reference's dense 15x15 event step restated in C (oracle/cpu_kf.c) on this host's
@@ -392,27 +430,18 @@ def ref15_workload(cfg, args, rank, world, dev):
             cpu_kf.ref15_events(et, dd, pa, x0, ref_kf.P0_REF15, filters=(done, hi), nthreads=nth)
             done = hi
         el = time.perf_counter() - t0
-        steps, t1 = 0, time.perf_counter()
-        for f in range(nf):
-            x, P = np.zeros(15), ref_kf.P0_REF15.copy()
-            for t in range(T):
-                if et[t, f] == 0:
-                    sd = {'easting': pa[t, 0, f], 'northing': pa[t, 1, f], 'altitude': pa[t, 2, f]}
-                    x, P = ref_kf.step15(x, P, 'GPS', sd, dt)
-                else:
-                    x, P = ref_kf.step15(x, P, 'IMU', ['t', *pa[t, :, f]], dt)
-                np.linalg.slogdet(P)
-                steps += 1
-            if time.perf_counter() - t1 > 3.0:
-                break
-        el_np = time.perf_counter() - t1
+        from oracle import numpy_pool
+        per = min(nf // nth, -(-60000 * 3 // T))
+        shards = [dict(et=et[:, r * per:(r + 1) * per], dt=dd[:, r * per:(r + 1) * per],
+                       pay=pa[:, :, r * per:(r + 1) * per], n=per) for r in range(nth)]
+        npl = numpy_pool.run('ref15', shards, seconds=3.0)
         return {'value': done * T / el, 'unit': 'KF events/s', 'cores': nth, 'kind': 'port',
                 'sample': f'{done} filters x {T} events of these streams through oracle/cpu_kf.c (the reference '
                           f'step, dense 15x15, C -O3 OpenMP) on {nth} threads, {host_cpu()}',
                 'seconds': round(el, 2),
-                'numpy_reference_loop': {'value': steps / el_np, 'cores': 1,
-                                         'sample': f'{steps} events, oracle/ref_kf.step15 + slogdet, '
-                                                   f'NumPy {np.__version__}'}}
+                'numpy_reference_loop': dict(npl, sample=f"{npl['filters']} filters of these streams, "
+                                             f"oracle/ref_kf.step15 + slogdet (kf_workers.py:688-717) in a spawn Pool "
+                                             f"of {npl['cores']} processes, NumPy {np.__version__}")}
 
     bytes_launch, bytes_event = ref15_algorithmic_bytes(cfg)
 
@@ -527,7 +556,7 @@ def log_workload(cfg, args, rank, world, dev):
     pay = stream.payload[first:].contiguous()
     x0 = torch.zeros(15, 1, dtype=torch.float64, device=dev)
     x0[0:3, 0] = pay[0, 0:3]
-    kf = kfmi.BatchedKF('ref15', 1, 'f64', device=dev.index)
+    kf = kfmi.BatchedKF('ref15', 1, 'f64', device=dev.index, options=cfg.get('opts'))
     dt = torch.empty(T, dtype=torch.float64, device=dev)
     et = torch.empty(T, dtype=torch.uint8, device=dev)
     traj = kf.empty(T, 6, 1)
@@ -643,7 +672,7 @@ def sched_workload(cfg, args, rank, world, dev):
     from kfmi import _lib
     from kfmi.engine import _ptr
     B, T, dt, k = cfg['B'], cfg['T'], cfg['dt'], cfg['k']
-    kf = kfmi.BatchedKF('ref15', B, 'f64', device=dev.index)
+    kf = kfmi.BatchedKF('ref15', B, 'f64', device=dev.index, options=cfg.get('opts'))
     g = torch.Generator(device=dev).manual_seed(SEED + rank)
     t0 = 1697739278.761565
     etype = torch.ones(T, B, dtype=torch.uint8, device=dev)
@@ -682,30 +711,22 @@ def sched_workload(cfg, args, rank, world, dev):
         """The oracle's NumPy restatement of the scheduled driver (oracle/ref_kf.
         run_kalman_filter_scheduled, kf_workers.py:826-957: Scheduler.gain per queued candidate
         with np.linalg.inv, step15, slogdet) on 1 core, streams of this workload."""
-        from oracle import ref_kf
-        et = etype.cpu().numpy()
-        ts = tt.cpu().numpy()
-        pa = pay.cpu().numpy()
-        fr = freq.cpu().numpy()
-        done, t1 = 0, time.perf_counter()
-        f = 0
-        while time.perf_counter() - t1 < 10.0 and f < B:
-            ev = [(0, 'GPS', t0, {'easting': 0.0, 'northing': 0.0, 'altitude': 0.0})]
-            for i in range(T):
-                if et[i, f] == 0:
-                    ev.append((i + 1, 'GPS', ts[i, f], {'easting': pa[i, 0, f], 'northing': pa[i, 1, f],
-                                                        'altitude': pa[i, 2, f]}))
-                else:
-                    ev.append((i + 1, 'IMU', ts[i, f], ['t', *pa[i, :, f]]))
-            ref_kf.run_kalman_filter_scheduled(ev, 0, len(ev), ref_kf.P0_REF15.copy(), (t0, 0, 0, 0, 0, 0, 0),
-                                               'greedy', float(fr[f]))
-            done += T
-            f += 1
-        el = time.perf_counter() - t1
-        return {'value': done / el, 'unit': 'KF events/s', 'cores': 1, 'kind': 'port', 'seconds': round(el, 2),
-                'sample': f'{f} filters x {T} events of these streams (their rates, 10..120 Hz) through '
-                          f'oracle/ref_kf.run_kalman_filter_scheduled (NumPy {np.__version__}, greedy), 1 core, '
-                          f'{host_cpu()}'}
+        from oracle import numpy_pool
+        nth = numpy_pool.cores()
+        # spread the sample over the rates: worker r takes every nth block of 64 filters
+        per = -(-60000 * 4 // T)
+        cols = [np.concatenate([np.arange(b * 64, b * 64 + 64) for b in range(r, B // 64, nth)])[:per]
+                for r in range(nth)]
+        idx = [torch.as_tensor(c, device=dev) for c in cols]
+        shards = [dict(et=etype[:, i].cpu().numpy(), t=tt[:, i].cpu().numpy(), pay=pay[:, :, i].cpu().numpy(),
+                       freq=freq[i].cpu().numpy(), t0=t0, n=len(c)) for i, c in zip(idx, cols)]
+        npl = numpy_pool.run('sched', shards, seconds=4.0)
+        return {'value': npl['value'], 'unit': 'KF events/s', 'cores': npl['cores'], 'kind': 'port',
+                'seconds': round(npl['seconds'], 2), 'filters': npl['filters'],
+                'sample': f"{npl['filters']} filters x {T} events of these streams (their rates, 10..120 Hz) "
+                          f"through oracle/ref_kf.run_kalman_filter_scheduled (NumPy {np.__version__}, greedy: "
+                          f"Scheduler.gain per queued candidate, kf_workers.py:826-957) in a spawn Pool of "
+                          f"{npl['cores']} processes, {host_cpu()}"}
 
     # per event examined: t 8 + etype 1 read; per selection: payload 72 read, traj 48 + logdet 8 +
     # sel_time 8 written; per filter: state (15 + 27) x 8 loaded and stored, prev / freq read,
@@ -753,7 +774,7 @@ def bf_workload(cfg, args, rank, world, dev):
     search = cfg['search']
     if search:
         kf.close()
-        kf = kfmi.BatchedKF('ref15', 1, 'f64', device=dev.index)
+        kf = kfmi.BatchedKF('ref15', 1, 'f64', device=dev.index, options=cfg.get('opts'))
 
     def step():
         if search:
@@ -795,20 +816,21 @@ def bf_workload(cfg, args, rank, world, dev):
         cand = [(i, 'GPS' if ev[i, 1] == 0 else 'IMU', ev[i, 0],
                  ({'easting': ev[i, 2], 'northing': ev[i, 3], 'altitude': ev[i, 4]} if ev[i, 1] == 0
                   else ['t', *ev[i, 2:]])) for i in range(n)]
-        n_np, t1 = 0, time.perf_counter()
-        for combo in islice(combinations(cand, kk), 100000):
-            ref_kf.evaluate_combo_chunk([combo], np.zeros(15), Pw, t0, t_end)
-            n_np += 1
-            if time.perf_counter() - t1 > 3.0:
-                break
-        el_np = time.perf_counter() - t1
+        # the worker's NumPy loop over the 12-subsets, each Pool process its own range of them
+        # (the reference's Pool fan-out, kf_workers.py:1320-1346)
+        from oracle import numpy_pool
+        per = 4000
+        shards = [dict(cand=cand, k=kk, lo=r * per, n=per, x0=np.zeros(15), P0=Pw, t0=t0, t_end=t_end)
+                  for r in range(nth)]
+        npl = numpy_pool.run('bf', shards, seconds=3.0)
         return {'value': done * (kk + 1) / el, 'unit': 'KF steps/s', 'combinations_per_s': done / el, 'cores': nth,
                 'kind': 'port', 'sample': f'{done} {kk}-subsets of the {n} candidates as event streams through '
                                           f'oracle/cpu_kf.c (the reference step, dense 15x15, C -O3 OpenMP) on '
                                           f'{nth} threads, {host_cpu()}', 'seconds': round(el, 2),
-                'numpy_reference_loop': {'value': n_np * (kk + 1) / el_np, 'combinations_per_s': n_np / el_np,
-                                         'cores': 1, 'sample': f'{n_np} subsets, oracle/ref_kf.evaluate_combo_chunk, '
-                                                               f'NumPy {np.__version__}'}}
+                'numpy_reference_loop': dict(npl, combinations_per_s=npl['value'] / (kk + 1),
+                                             sample=f"{npl['filters']} {kk}-subsets, oracle/ref_kf."
+                                                    f"evaluate_combo_chunk (kf_workers.py:22-97) in a spawn Pool of "
+                                                    f"{npl['cores']} processes, NumPy {np.__version__}")}
 
     if search:
         from kfmi.ref15 import search_level_bytes
@@ -834,6 +856,53 @@ def bf_workload(cfg, args, rank, world, dev):
                 extra={'candidate_events': n, 'combinations': total_combos, 'launch_width': width})
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(gpus, env, argv, script=None, port=None):
+    """How `python bench.py --gpus N` runs: None = in this process (one rank, or a rank that a
+    launcher already started: WORLD_SIZE set); otherwise the command that starts the N ranks as
+    fresh child processes (torch.distributed.run, one GPU per rank, rendezvous on 127.0.0.1).
+    The parent never touches the GPU: it waits for the launcher and exits with its status (the
+    worst rank's).  Replaces the reference's Pool(30) fan-out (kf_workers.py:1320-1346) with one
+    process per GPU.  A WORLD_SIZE that disagrees with --gpus is an error, never a silent
+    one-rank run."""
+    if gpus < 1:
+        raise SystemExit(f'--gpus {gpus}: need at least one GPU')
+    world = env.get('WORLD_SIZE')
+    if world is not None:
+        if int(world) != gpus:
+            raise SystemExit(f'--gpus {gpus} but WORLD_SIZE={world}')
+        return None
+    if gpus == 1:
+        return None
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={gpus}',
+            '--master-addr=127.0.0.1', f'--master-port={port or _free_port()}',
+            script or os.path.abspath(__file__)] + list(argv)
+
+
+def launch_check(world, rank):
+    """--launch-check: each rank joins a gloo group (no GPU) and rank 0 reports the ranks it
+    sees; tests/test_bench_launch.py drives `bench.py --gpus N --launch-check` on the CPU."""
+    import torch.distributed as dist
+    seen = 1
+    if world > 1:
+        dist.init_process_group('gloo')
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        seen = int(t.item())
+        assert seen == dist.get_world_size()
+    if rank == 0:
+        print(json.dumps({'launch_check': True, 'ranks_seen': seen, 'world_size': world}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return seen
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -851,20 +920,39 @@ def main():
                     help='config 1: replay the step as a hipGraph (measured no faster than eager launches)')
     ap.add_argument('--ablate', choices=['none', 'no-traj', 'no-logdet', 'no-traj-no-logdet'], default='none',
                     help='diagnostics only: skip an output stream (the JSON line says so)')
+    ap.add_argument('--gather-traj-every', type=int, default=16,
+                    help='N>1: the final all-gather also reassembles the trajectory decimated every k steps '
+                         '(0 = final states and log-dets only); timed apart as allgather_ms')
+    ap.add_argument('--opt', action='append', default=[], metavar='NAME=VALUE',
+                    help='a kf_set_option of the workload\'s handle (kfmi.engine.OPTIONS), e.g. cv_kernel=general; '
+                         'A/B runs only (the JSON line lists them)')
+    ap.add_argument('--dist-backend', choices=['nccl', 'gloo'], default='nccl',
+                    help='N>1: nccl = RCCL over xGMI, one GPU per rank; gloo = rehearsal only (N ranks share '
+                         'one GPU, tools/dist_rehearsal.sh)')
+    ap.add_argument('--launch-check', action='store_true',
+                    help='start the ranks and report ranks_seen over gloo, no GPU work (tests)')
     args = ap.parse_args()
+
+    cmd = launch_plan(args.gpus, os.environ, sys.argv[1:])
+    if cmd is not None:
+        # N ranks requested from a plain `python bench.py --gpus N`: start them as children
+        import subprocess
+        rc = subprocess.run(cmd).returncode
+        if rc:
+            print(f'bench.py: {args.gpus}-rank launch exited with status {rc}', file=sys.stderr, flush=True)
+        raise SystemExit(rc)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if args.gpus != world and world > 1:
-        raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}')
+    if args.launch_check:
+        seen = launch_check(world, rank)
+        raise SystemExit(0 if seen == args.gpus else 3)
     dist = None
-    # RCCL ('nccl') over xGMI, one GPU per rank.  KFMI_BENCH_DIST_BACKEND=gloo is a rehearsal
-    # switch only: it lets N ranks share the one GPU of a test box (RCCL refuses two ranks on one
+    # RCCL ('nccl') over xGMI, one GPU per rank.  --dist-backend gloo is a rehearsal switch
+    # only: it lets N ranks share the one GPU of a test box (RCCL refuses two ranks on one
     # device) so the N>1 code path — shards, max-over-ranks timing, the final all-gather — runs
-    backend = os.environ.get('KFMI_BENCH_DIST_BACKEND', 'nccl')
-    if backend not in ('nccl', 'gloo'):
-        raise SystemExit(f'KFMI_BENCH_DIST_BACKEND={backend}: expected nccl or gloo')
+    backend = args.dist_backend
     if world > 1 and backend == 'gloo':
         local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
@@ -874,11 +962,18 @@ def main():
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
             dist.init_process_group('gloo')
+    ranks_seen = dist.get_world_size() if dist else 1
+    if ranks_seen != args.gpus:
+        raise SystemExit(f'--gpus {args.gpus} but {ranks_seen} rank(s) joined')
     dev = torch.device('cuda', local)
 
     cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg['B'] = args.batch
+    cfg['opts'] = {}
+    for o in args.opt:
+        name, _, val = o.partition('=')
+        cfg['opts'][name] = int(val) if val.lstrip('-').isdigit() else val
     if args.config in ('1', '1seq'):
         w = log_workload(cfg, args, rank, world, dev)
     elif args.config in ('ref15', 'ref15f32'):
@@ -913,26 +1008,38 @@ def main():
 
     kf = w['kf']
     bad = int((kf.status() != 0).sum().item()) if not args.config.startswith('bf') else 0
-    gather_ms = None
+    gather_ms = gather_info = None
     if dist:
         from kfmi import dist as kdist
         elapsed, kern_ms, bad = kdist.max_over_ranks([elapsed, kern_ms, bad], dev)
         bad = int(bad)
         if w['gather'] is not None:
-            # reassemble the final states + logdets of every shard on every rank (RCCL over
+            # reassemble the final states + logdets (+ the trajectory decimated every
+            # --gather-traj-every steps) of every shard on every rank, one all-gather (RCCL over
             # xGMI); timed separately: a once-per-job reassembly, not the hot path
-            local_out = w['gather']()
+            xl, ldl, trl = w['gather']()
+            every = max(0, args.gather_traj_every)
+            total = world * kf.batch
             torch.cuda.synchronize(dev)
             dist.barrier()
             g0 = time.perf_counter()
-            gathered = kdist.gather_shards(local_out, world * kf.batch)
+            res = kdist.gather_run_outputs(xl, ldl, trl, every, total)
             torch.cuda.synchronize(dev)
             gather_ms = (time.perf_counter() - g0) * 1e3
-            # every rank finds its own shard at its global offset in the reassembled array
-            off, cnt = kdist.shard_range(world * kf.batch, rank, world)
-            if gathered.shape[-1] != world * kf.batch or not torch.equal(  # bitwise (NaN-safe)
-                    gathered[..., off:off + cnt].contiguous().view(torch.uint8), local_out.view(torch.uint8)):
+            # every rank finds its own shard at its global offset in the reassembled arrays
+            off, cnt = kdist.shard_range(total, rank, world)
+            same = lambda a, b: torch.equal(a.contiguous().view(torch.uint8), b.contiguous().view(torch.uint8))
+            steps = kdist.decimated_steps(trl.shape[0], every) if trl is not None else []
+            ok = (res['x'].shape[-1] == total and same(res['x'][:, off:off + cnt], xl)
+                  and same(res['logdet'][off:off + cnt], ldl)
+                  and (not steps or same(res['traj'][:, :, off:off + cnt], trl[steps])))
+            if not ok:
                 raise SystemExit(f'rank {rank}: the all-gathered shards do not reassemble')
+            gather_info = {'ms': gather_ms, 'traj_every': every, 'traj_steps': len(steps),
+                           'rows': res['rows'], 'bytes_per_rank': res['bytes_per_rank'],
+                           'bytes_gathered': res['bytes_per_rank'] * world,
+                           'checked': 'bitwise: every rank finds its shard at its global offset'}
+            del res
 
     if rank == 0:
         rec = {
@@ -983,8 +1090,14 @@ def main():
         rec['failed_filters'] = bad
         if args.ablate != 'none':
             rec['ablation'] = args.ablate + ' (diagnostic run: NOT the benchmark workload)'
+        rec['ranks_seen'] = ranks_seen
+        if cfg['opts']:
+            rec['options'] = cfg['opts']
+        from kfmi import _lib as _kl
+        rec['build'] = _kl.build_info()
         if gather_ms is not None:
             rec['allgather_ms'] = gather_ms
+            rec['allgather'] = gather_info
         rec['cpu_baseline'] = w['cpu']() if (world == 1 and not args.no_cpu_baseline) else None
         if args.pcie and world == 1 and w.get('pcie'):
             rec['pcie_inclusive'] = w['pcie']()

@@ -26,7 +26,8 @@
  *
  * Threading: distinct handles may be used from different threads at once; one handle is used
  * by one thread at a time.  That includes the calls that only read it (kf_get_state,
- * kf_get_status): they run a held-back kf_predict first (see kf_predict).
+ * kf_get_status, which therefore take a non-const handle): they run a held-back kf_predict
+ * first (see kf_predict).
  */
 #ifndef KFMI_KF_H
 #define KFMI_KF_H
@@ -92,8 +93,48 @@ typedef struct kf_params {
 
 typedef struct kf_batch kf_batch;
 
-/* Library version string. */
+/* Library version string: "kfmi <version> (gfx950) src:<hash>", where <hash> is the first 16 hex
+ * digits of the SHA-256 of the sources the library was built from (the .cpp, .h and .hip files of
+ * csrc in name order, then include/kf.h).  The Python binding refuses a library whose hash
+ * differs from the tree it is loaded from (a stale or foreign build). */
 const char* kf_version(void);
+
+/* Per-handle options: the variant choices the library otherwise makes by itself, for A/B runs
+ * and tests.  0 is the library's choice for every option, and a new handle starts with all 0.
+ * Nothing is read from the environment.
+ *   KF_OPT_PREDICT        0 = hold a scalar-dt kf_predict back and fuse it into the next
+ *                         kf_update; 1 = eager (one kernel per call)
+ *   KF_OPT_CV_KERNEL      kf_run on the BASELINE models: 0 = auto (cv_block_kernel when P is
+ *                         block-diagonal and R diagonal), 1 = the general kernel,
+ *                         2 / 4 / 8 = the block kernel with that input-ring depth (where legal)
+ *   KF_OPT_BLOCKS_PER_CU  kf_run: cap resident workgroups per CU at 2..8 (reserving unused LDS);
+ *                         0 = no cap
+ *   KF_OPT_EVENTS_KERNEL  kf_run_events: 0 = auto, 1 = one lane per filter (inputs in registers),
+ *                         2 = one lane per axis chain, 3 = LDS-staged inputs (where legal)
+ *   KF_OPT_STREAM         kf_run_events: 0 = route one long filter through kf_run_stream,
+ *                         1 = never (every filter in sequence)
+ *   KF_OPT_STREAM_CHUNKS  kf_run_stream: target chunk count (>= 2); 0 = 8192
+ *   KF_OPT_STREAM_FINAL   kf_run_stream: 0 = records from the map pass, 1 = a final pass from the
+ *                         true chunk starts
+ *   KF_OPT_START_THREADS  kf_run_stream: threads per block of the start kernel; 0 = 256
+ *   KF_OPT_SEARCH_KERNEL  kf_search_combos: 0 = per level, 1 = child-major, 2 = parent-major
+ *   KF_OPT_SEARCH_PM      kf_search_combos' parent-major kernel: 0 = parent in LDS, 1 = registers
+ *   KF_OPT_SCHED_KERNEL   kf_run_scheduled: 0 = auto, 1 = the register-input kernel
+ * KF_EINVAL for an unknown option or an out-of-range value. */
+#define KF_OPT_PREDICT        1
+#define KF_OPT_CV_KERNEL      2
+#define KF_OPT_BLOCKS_PER_CU  3
+#define KF_OPT_EVENTS_KERNEL  4
+#define KF_OPT_STREAM         5
+#define KF_OPT_STREAM_CHUNKS  6
+#define KF_OPT_STREAM_FINAL   7
+#define KF_OPT_START_THREADS  8
+#define KF_OPT_SEARCH_KERNEL  9
+#define KF_OPT_SEARCH_PM      10
+#define KF_OPT_SCHED_KERNEL   11
+#define KF_OPT_COUNT          12
+int kf_set_option(kf_batch* handle, int option, int64_t value);
+int kf_get_option(const kf_batch* handle, int option, int64_t* value);
 
 /* Thread-local description of the last failure on this thread ("" if none). */
 const char* kf_last_error(void);
@@ -130,8 +171,8 @@ int kf_reset(kf_batch* handle, const void* x0, void* stream);
  * on_device == 0: host pointers (synchronous).  The warm start of the reference
  * (initial_pt / initial_state, kf_workers.py:643-649) maps to kf_set_state. */
 int kf_set_state(kf_batch* handle, const void* x, const void* P, int on_device, void* stream);
-int kf_get_state(const kf_batch* handle, void* x, void* P, int on_device, void* stream);
-int kf_get_status(const kf_batch* handle, int32_t* status, int on_device, void* stream);
+int kf_get_state(kf_batch* handle, void* x, void* P, int on_device, void* stream);
+int kf_get_status(kf_batch* handle, int32_t* status, int on_device, void* stream);
 
 /* One predict step for every filter: x = F(dt) x + G(dt) u, P = F P F^T + Q(dt).
  * dt_per_filter: device [B] double (NULL = scalar dt for all filters; the brute-force caller
@@ -141,13 +182,18 @@ int kf_get_status(const kf_batch* handle, int32_t* status, int on_device, void* 
  * Replaces get_state_transition_matrix + get_process_noise_covariance_matrix +
  * x = np.dot(F, x) + predict_covariance (kf_workers.py:493-549, 688-691).
  * With a scalar dt and no logdet_out the step is held back and runs fused with the next
- * kf_update (one kernel, the state read and written once); u is copied on `stream` before the
- * call returns, so the caller may reuse its buffer at once.  Any other call that reads or
- * replaces the state (kf_get_state, kf_get_status, kf_set_state, kf_run, another kf_predict)
- * runs a held-back predict first, on its own stream; kf_reset discards it.  Results are those
- * of the two separate kernels (KFMI_PREDICT=eager).  The control buffer is allocated by kf_alloc,
- * so a predict/update loop allocates nothing and can be captured into a graph (capture whole
- * predict + update pairs: a predict left pending at the end of a capture runs outside it). */
+ * kf_update (one kernel, the state read and written once); a copy of u into the handle is
+ * queued on `stream`, so the caller may overwrite u with work ordered after this call on
+ * `stream`; a host write to u (pinned or managed memory) or a write on another stream must
+ * first synchronise with `stream`.  Any other call that reads or replaces the state
+ * (kf_get_state, kf_get_status, kf_set_state, kf_run, another kf_predict) runs a held-back
+ * predict first, on its own stream; kf_reset discards it.  Results are those of the two
+ * separate kernels (KF_OPT_PREDICT = 1).  The control buffer is allocated by kf_alloc, so a
+ * predict/update loop allocates nothing and can be captured into a graph (capture whole
+ * predict + update pairs: a predict left pending at the end of a capture runs outside it).
+ * Warm-up on one stream and capture on another (the torch.cuda.graph pattern) works: a predict
+ * whose control copy would have to wait for a kernel recorded outside the capture runs eagerly
+ * instead (the same results). */
 int kf_predict(kf_batch* handle, double dt, const double* dt_per_filter, const void* u,
                void* logdet_out, void* stream);
 
@@ -201,7 +247,7 @@ int kf_run_events(kf_batch* handle, int T, const uint8_t* etype, const double* d
 /* kf_run_events without its one-filter route through kf_run_stream: every filter runs its
  * events in sequence, whatever B and T are (same arguments and outputs).  For callers that want
  * the sequential single-filter run for one call (A/B, the reference's own op order over a whole
- * log) without the process-wide KFMI_STREAM=off switch. */
+ * log) without the handle-wide KF_OPT_STREAM = 1. */
 int kf_run_events_seq(kf_batch* handle, int T, const uint8_t* etype, const double* dt, const void* payload,
                       void* traj, void* cov, void* logdet, uint8_t* updated, int gate, double threshold,
                       void* stream);
@@ -216,7 +262,7 @@ int kf_run_events_seq(kf_batch* handle, int T, const uint8_t* etype, const doubl
  * the gains is affine: each chunk runs from a guess and three perturbed guesses, whose ends
  * give its map start -> end; the maps are composed into the true chunk starts, and the records
  * are the map pass's (covariance, logdet, updated from the guess; the trajectory as the maps'
- * value at the true starts).  KFMI_STREAM_FINAL=1 (or a stream too long for the four
+ * value at the true starts).  KF_OPT_STREAM_FINAL = 1 (or a stream too long for the four
  * trajectory variants' 32-bit offsets) runs a final pass from the true starts instead, with
  * its own state seam check.  Checked on the device: the start covariances must meet their
  * predecessors' end covariances (relative 1e-12 in f64, 1e-5 in f32), the chunk starts and end
@@ -224,7 +270,7 @@ int kf_run_events_seq(kf_batch* handle, int T, const uint8_t* etype, const doubl
  * 1e-4), and no chunk filter may fail; otherwise the sequential kernel runs the stream as one
  * filter from the handle's state and rewrites every record.  Asynchronous on `stream` either
  * way.  kf_run_events takes this route by itself for B = 1, gate = 0 and T >= 65536
- * (KFMI_STREAM=off disables it).  The run of run_kalman_filter_full (kf_workers.py:623-728)
+ * (KF_OPT_STREAM = 1 disables it).  The run of run_kalman_filter_full (kf_workers.py:623-728)
  * over a whole drive log. */
 int kf_run_stream(kf_batch* handle, int T, const uint8_t* etype, const double* dt, const void* payload,
                   void* traj, void* cov, void* logdet, uint8_t* updated, int chunk, int warmup,

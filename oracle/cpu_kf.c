@@ -177,8 +177,9 @@ static void cv_model(int d, double dt, double q_pos, double q_vel, double* F, do
 }
 
 void cpu_cv_run(int d, int64_t B, int T, double dt0, const double* dt_steps, int k, const double* u, const double* z,
-                const double* x0, const double* P0, double q_pos, double q_vel, double r_gps, double* traj,
-                double* logdet_out, double* x_out, double* P_out, int64_t f0, int64_t f1, int nthreads) {
+                const double* x0, const double* P0, double q_pos, double q_vel, double r_gps, const double* R_full,
+                double* traj, double* logdet_out, double* x_out, double* P_out, int64_t f0, int64_t f1, int nthreads) {
+    /* R_full: d x d row-major measurement noise, or NULL for r_gps I (kf_workers.py:581-585) */
     const int n = 2 * d;
     double F0[NMAX * NMAX], Q0[NMAX * NMAX], H[NMAX * NMAX] = {0}, R[NMAX * NMAX] = {0};
     cv_model(d, dt0, q_pos, q_vel, F0, Q0);
@@ -186,6 +187,7 @@ void cpu_cv_run(int d, int64_t B, int T, double dt0, const double* dt_steps, int
         H[i * n + i] = 1.0;
         R[i * d + i] = r_gps;
     }
+    if (R_full) memcpy(R, R_full, sizeof(double) * d * d);
 #pragma omp parallel for num_threads(nthreads) schedule(static)
     for (int64_t f = f0; f < f1; ++f) {
         double x[NMAX], P[NMAX * NMAX], Fs[NMAX * NMAX], Qs[NMAX * NMAX];

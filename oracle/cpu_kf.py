@@ -23,7 +23,8 @@ def lib():
             raise FileNotFoundError(f'{LIB} not built: make -C oracle')
         L = ctypes.CDLL(LIB)
         vp, i32, i64, f64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
-        L.cpu_cv_run.argtypes = [i32, i64, i32, f64, vp, i32, vp, vp, vp, vp, f64, f64, f64, vp, vp, vp, vp, i64, i64, i32]
+        L.cpu_cv_run.argtypes = [i32, i64, i32, f64, vp, i32, vp, vp, vp, vp, f64, f64, f64, vp, vp, vp, vp, vp, i64, i64,
+                                 i32]
         L.cpu_cv_run.restype = None
         L.cpu_ref15_events.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32]
         L.cpu_ref15_events.restype = None
@@ -49,9 +50,9 @@ def threads():
 
 
 def cv_run(d, x0, P0, dt, u, z, update_every=1, q_pos=5.0, q_vel=1.0, r_gps=3.0, filters=None, nthreads=None,
-           records=True):
+           records=True, R=None):
     """BASELINE 4/2 (d = 2) / 6/3 (d = 3) filters: x0 [n, B], P0 [n, n], u [T, d, B],
-    z [T // k, d, B], dt scalar or [T].  Returns (traj [T, n, B], logdet [T, B], x [n, B],
+    z [T // k, d, B], dt scalar or [T]; R [d, d] (None: r_gps I).  Returns (traj [T, n, B], logdet [T, B], x [n, B],
     P [B, n, n]) for the filter range ``filters`` = (f0, f1) (others left zero)."""
     n = 2 * d
     x0, P0, u, z = _c(x0), _c(P0), _c(u), _c(z)
@@ -63,7 +64,7 @@ def cv_run(d, x0, P0, dt, u, z, update_every=1, q_pos=5.0, q_vel=1.0, r_gps=3.0,
     x = np.zeros((n, B))
     P = np.zeros((B, n, n))
     lib().cpu_cv_run(d, B, T, float(dt) if dts is None else 0.0, _p(dts), int(update_every), _p(u), _p(z), _p(x0),
-                     _p(P0), q_pos, q_vel, r_gps,
+                     _p(P0), q_pos, q_vel, r_gps, _p(None if R is None else _c(R)),
                      _p(traj), _p(ld), _p(x), _p(P), f0, f1, nthreads or threads())
     return traj, ld, x, P
 

@@ -137,8 +137,11 @@ class CVModel:
     R = r_gps I (``kf_workers.py:583``).
     """
 
-    def __init__(self, d, q_pos=5.0, q_vel=1.0, r_gps=3.0, p0_pos=None, p0_vel=None):
+    def __init__(self, d, q_pos=5.0, q_vel=1.0, r_gps=3.0, p0_pos=None, p0_vel=None, r_full=None):
         self.d = d
+        # r_full: a d x d measurement noise in place of r_gps I (the class_args override of
+        # get_gps_measurement_noise_covariance_matrix, kf_workers.py:581-585, 1242-1251)
+        self.r_full = None if r_full is None else np.array(r_full, dtype=np.float64)
         self.n = 2 * d
         self.m = d
         self.c = d
@@ -173,7 +176,7 @@ class CVModel:
         return np.eye(self.n)[: self.d]
 
     def R(self):
-        return np.diag([self.r_gps] * self.d)
+        return self.r_full.copy() if self.r_full is not None else np.diag([self.r_gps] * self.d)
 
     def P0(self):
         return np.diag([self.p0_pos] * self.d + [self.p0_vel] * self.d)

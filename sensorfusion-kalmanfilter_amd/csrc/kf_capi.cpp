@@ -42,10 +42,12 @@ struct kf_batch {
     bool pend_has_u;
     double pend_dt;
     void* pend_u;          // [c][B] (allocated by kf_alloc)
-    hipEvent_t pend_done;    // orders a control copy after the last kernel that read pend_u
-    hipStream_t pend_reader; // the stream of that kernel
-    bool pend_read;
+    hipEvent_t pend_done;    // recorded right after each kernel that reads pend_u (outside a capture)
+    hipStream_t pend_reader; // the stream of the last such kernel (compared, never used in a call)
+    bool pend_read;          // a kernel has read pend_u
+    bool pend_evt;           // pend_done marks that read (false: it was captured into a graph)
     bool last_predict;       // the handle's last state call was kf_predict
+    int64_t opt[KF_OPT_COUNT];  // kf_set_option values (0 = the library's choice)
 };
 
 namespace {
@@ -80,6 +82,8 @@ constexpr size_t kWsInit = sizeof(double) * 42;
 // levels with at most this many parents run child-major (see search_child_major)
 constexpr uint64_t kSearchChildMajorParents = 200000;
 
+int64_t opt(const kf_batch* h, int o) { return h->opt[o]; }
+
 bool is_ref15(const kf_batch* h) { return h->model == KF_MODEL_REF15; }
 
 // binomial table C(a, b), a, b <= 64 (exact in uint64; C(64, 32) < 2^63)
@@ -112,11 +116,10 @@ int upload_combo_inputs(kf_batch* h, int n_events, const double* events, const d
 // for the narrow levels, where one lane per parent would walk up to n - 1 children in sequence;
 // parent-major (one lane per parent, its children in a wave-uniform loop) for the wide ones,
 // where it reads each parent once and keeps it in registers (interleaved A/B:
-// profiles/r01_ab/search_kernels_ab.txt).  KFMI_SEARCH_KERNEL=cm|pm forces one.
-bool search_child_major(uint64_t n_par) {
-    const char* v = std::getenv("KFMI_SEARCH_KERNEL");
-    if (v && !std::strcmp(v, "cm")) return true;
-    if (v && !std::strcmp(v, "pm")) return false;
+// profiles/r01_ab/search_kernels_ab.txt).  KF_OPT_SEARCH_KERNEL = 1 | 2 forces one.
+bool search_child_major(const kf_batch* h, uint64_t n_par) {
+    if (opt(h, KF_OPT_SEARCH_KERNEL) == 1) return true;
+    if (opt(h, KF_OPT_SEARCH_KERNEL) == 2) return false;
     return n_par <= kSearchChildMajorParents;
 }
 
@@ -156,16 +159,15 @@ kfmi::CvArgs base_args(const kf_batch* h) {
     a.p0_pos = h->params.p0_pos;
     a.p0_vel = h->params.p0_vel;
     // the block kernel needs a block-diagonal P (kept so by a diagonal R);
-    // KFMI_CV_KERNEL=general forces the general kernel (tests, A/B)
-    const char* v = std::getenv("KFMI_CV_KERNEL");
-    a.block_p = (h->block_p && h->r_diag && !(v && !std::strcmp(v, "general"))) ? 1 : 0;
+    // KF_OPT_CV_KERNEL = 1 forces the general kernel (tests, A/B)
+    const int64_t v = opt(h, KF_OPT_CV_KERNEL);
+    a.block_p = (h->block_p && h->r_diag && v != 1) ? 1 : 0;
     // the block kernel keeps 7 steps of inputs in flight per lane: with one filter per lane a
     // small batch is one or two waves per SIMD, too few to cover HBM latency with 1-step
     // prefetch, and at 2^20 filters depth 8 still measured ~1.5% ahead of depth 2
-    // (profiles/r01_ab/prefetch_depth_ab.txt); KFMI_CV_KERNEL=block2|block4 forces the depth
-    a.prefetch_depth = 8;
-    if (v && !std::strcmp(v, "block2")) a.prefetch_depth = 2;
-    if (v && !std::strcmp(v, "block4")) a.prefetch_depth = 4;
+    // (profiles/r01_ab/prefetch_depth_ab.txt); KF_OPT_CV_KERNEL = 2 | 4 forces the depth
+    a.prefetch_depth = (v == 2 || v == 4) ? int(v) : 8;
+    a.blocks_per_cu = int(opt(h, KF_OPT_BLOCKS_PER_CU));
     return a;
 }
 
@@ -200,19 +202,28 @@ kfmi::RefArgs ref_args(const kf_batch* h) {
     return a;
 }
 
-// KFMI_PREDICT=eager turns the deferral off (tests, A/B)
-bool defer_predicts() {
-    const char* v = std::getenv("KFMI_PREDICT");
-    return !(v && !std::strcmp(v, "eager"));
+// KF_OPT_PREDICT = 1 turns the deferral off (tests, A/B)
+bool defer_predicts(const kf_batch* h) { return opt(h, KF_OPT_PREDICT) == 0; }
+
+bool capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
 
-// After a kernel on `stream` read pend_u: remember the stream.  A later control copy on another
-// stream first waits for an event recorded on this one at that time (all the stream's work so
-// far, the read included), so the common one-stream loop makes no event calls.
-int note_pend_reader(kf_batch* h, void* stream, const char*) {
+// After a kernel on `stream` read pend_u: record pend_done there at once, so a later control
+// copy on another stream can wait for the read without this call keeping the stream for later
+// (the caller may destroy it).  Inside a graph capture nothing is recorded: a later deferral on
+// another stream then runs its predict eagerly instead (kf_predict).
+int note_pend_reader(kf_batch* h, void* stream, const char* what) {
     if (!h->pend_has_u) return KF_OK;
-    h->pend_reader = static_cast<hipStream_t>(stream);
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    h->pend_reader = st;
     h->pend_read = true;
+    h->pend_evt = !capturing(st);
+    if (h->pend_evt) {
+        hipError_t e = hipEventRecord(h->pend_done, st);
+        if (e != hipSuccess) return hip_fail(e, what);
+    }
     return KF_OK;
 }
 
@@ -244,7 +255,42 @@ int set_error(int code, const char* fmt, ...) {
 
 extern "C" {
 
-const char* kf_version(void) { return "kfmi 0.1.0 (gfx950)"; }
+#ifndef KFMI_SRC_HASH
+#define KFMI_SRC_HASH "unknown"
+#endif
+const char* kf_version(void) { return "kfmi 0.3.0 (gfx950) src:" KFMI_SRC_HASH; }
+
+int kf_set_option(kf_batch* h, int option, int64_t value) {
+    if (int rc = check_handle(h)) return rc;
+    bool ok = false;
+    switch (option) {
+        case KF_OPT_PREDICT:
+        case KF_OPT_STREAM:
+        case KF_OPT_STREAM_FINAL:
+        case KF_OPT_SEARCH_PM:
+        case KF_OPT_SCHED_KERNEL: ok = value == 0 || value == 1; break;
+        case KF_OPT_CV_KERNEL: ok = value == 0 || value == 1 || value == 2 || value == 4 || value == 8; break;
+        case KF_OPT_BLOCKS_PER_CU: ok = value == 0 || (value >= 2 && value <= 8); break;
+        case KF_OPT_EVENTS_KERNEL: ok = value >= 0 && value <= 3; break;
+        case KF_OPT_STREAM_CHUNKS: ok = value == 0 || (value >= 2 && value <= (int64_t(1) << 24)); break;
+        case KF_OPT_START_THREADS: ok = value == 0 || (value >= 1 && value <= kfmi::kBlock); break;
+        case KF_OPT_SEARCH_KERNEL: ok = value >= 0 && value <= 2; break;
+        default: return fail(KF_EINVAL, "kf_set_option: unknown option %d", option);
+    }
+    if (!ok) return fail(KF_EINVAL, "kf_set_option: value %lld out of range for option %d", (long long)value, option);
+    // (a predict already held back stays so: the next call that needs the state runs it, as
+    // before; the option governs the predicts that follow)
+    h->opt[option] = value;
+    return KF_OK;
+}
+
+int kf_get_option(const kf_batch* h, int option, int64_t* value) {
+    if (int rc = check_handle(h)) return rc;
+    if (option < 1 || option >= KF_OPT_COUNT) return fail(KF_EINVAL, "kf_get_option: unknown option %d", option);
+    if (!value) return fail(KF_EINVAL, "kf_get_option: null output");
+    *value = h->opt[option];
+    return KF_OK;
+}
 
 const char* kf_last_error(void) { return g_err.c_str(); }
 
@@ -395,6 +441,8 @@ int kf_reset(kf_batch* h, const void* x0, void* stream) {
     }
     h->pend = false;  // a predict followed by a reset leaves the reset state
     h->last_predict = false;
+    // (pend_read stays: a kernel that read pend_u may still be running on another stream, and
+    // pend_done, recorded right after it, is what the next control copy waits for)
     kfmi::CvArgs a = base_args(h);
     a.x0 = x0;
     h->block_p = true;  // P = P0 is diagonal
@@ -437,10 +485,9 @@ int kf_set_state(kf_batch* h, const void* x, const void* P, int on_device, void*
     return KF_OK;
 }
 
-int kf_get_state(const kf_batch* h, void* x, void* P, int on_device, void* stream) {
+int kf_get_state(kf_batch* h, void* x, void* P, int on_device, void* stream) {
     if (int rc = check_handle(h)) return rc;
-    // the handle is logically const: running a held-back predict does not change its state
-    if (int rc = flush_predict(const_cast<kf_batch*>(h), stream, "kf_get_state")) return rc;
+    if (int rc = flush_predict(h, stream, "kf_get_state")) return rc;
     const hipMemcpyKind kind = on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     const size_t w = elem(h), nb = static_cast<size_t>(h->B);
     hipError_t e = hipSuccess;
@@ -452,10 +499,10 @@ int kf_get_state(const kf_batch* h, void* x, void* P, int on_device, void* strea
     return KF_OK;
 }
 
-int kf_get_status(const kf_batch* h, int32_t* status, int on_device, void* stream) {
+int kf_get_status(kf_batch* h, int32_t* status, int on_device, void* stream) {
     if (int rc = check_handle(h)) return rc;
     if (!status) return fail(KF_EINVAL, "kf_get_status: null output");
-    if (int rc = flush_predict(const_cast<kf_batch*>(h), stream, "kf_get_status")) return rc;
+    if (int rc = flush_predict(h, stream, "kf_get_status")) return rc;
     const size_t nb = static_cast<size_t>(h->B);
     if (!nb) return KF_OK;
     hipError_t e = hipMemcpyAsync(status, h->status, sizeof(int32_t) * nb,
@@ -478,16 +525,18 @@ int kf_predict(kf_batch* h, double dt, const double* dt_per_filter, const void* 
     // control copy, since the next call is another predict
     const bool after_predict = h->last_predict;
     h->last_predict = true;
-    if (h->B && !dt_per_filter && !logdet_out && !after_predict && defer_predicts()) {
+    // the control copy overwrites pend_u (kf_alloc), so it must follow the last kernel that read
+    // it: on the same stream that is stream order; on another stream a wait for pend_done, which
+    // a capture cannot take when that read was recorded outside it (or captured itself) — then
+    // this predict runs eagerly and pend_u is not written
+    const bool cross = u && h->pend_read && h->pend_reader != st;
+    const bool can_defer = !cross || (h->pend_evt && !capturing(st));
+    if (h->B && !dt_per_filter && !logdet_out && !after_predict && defer_predicts(h) && can_defer) {
         // hold it back for a fused step with the next kf_update (the reference's loop calls
         // predict then update every step, kf_workers.py:688-711)
         if (u) {
-            // the copy overwrites pend_u (kf_alloc): wait for the last kernel that read it
             hipError_t e = hipSuccess;
-            if (h->pend_read && h->pend_reader != st) {
-                e = hipEventRecord(h->pend_done, h->pend_reader);
-                if (e == hipSuccess) e = hipStreamWaitEvent(st, h->pend_done, 0);
-            }
+            if (cross) e = hipStreamWaitEvent(st, h->pend_done, 0);
             if (e == hipSuccess) e = kfmi::launch_copy(h->pend_u, u, elem(h) * h->c * static_cast<size_t>(h->B), st);
             if (e != hipSuccess) return hip_fail(e, "kf_predict control copy");
         }
@@ -593,8 +642,8 @@ int run_events_launch(kf_batch* h, int T, const uint8_t* etype, const double* dt
     a.skip = skip;
     // Few filters cannot fill the chip one lane each: give every axis chain its own lane
     // (8 lanes per filter).  Otherwise one lane per filter, with the inputs staged through LDS
-    // by DMA where its layout conditions hold.  KFMI_EVENTS_KERNEL=lane|chain|lds forces a
-    // variant (tests, A/B) where it is legal.
+    // by DMA where its layout conditions hold.  KF_OPT_EVENTS_KERNEL = 1 | 2 | 3 (lane, chain,
+    // lds) forces a variant (tests, A/B) where it is legal.
     const uint64_t span = static_cast<uint64_t>(h->B) * elem(h);
     // the chain kernel addresses up to 27 [B] rows through one descriptor (32-bit byte count);
     // the LDS kernel moves 16-B chunks (B % 16 == 0: none straddles B) of a 9-row payload span
@@ -603,11 +652,10 @@ int run_events_launch(kf_batch* h, int T, const uint8_t* etype, const double* dt
     int variant = h->B < kChainMaxFilters && chain_ok ? kfmi::kEventsChain
                   : lds_ok                            ? kfmi::kEventsLds
                                                       : kfmi::kEventsLane;
-    if (const char* v = std::getenv("KFMI_EVENTS_KERNEL")) {
-        if (!std::strcmp(v, "chain") && chain_ok) variant = kfmi::kEventsChain;
-        else if (!std::strcmp(v, "lane")) variant = kfmi::kEventsLane;
-        else if (!std::strcmp(v, "lds") && lds_ok) variant = kfmi::kEventsLds;
-    }
+    const int64_t v = opt(h, KF_OPT_EVENTS_KERNEL);
+    if (v == 2 && chain_ok) variant = kfmi::kEventsChain;
+    else if (v == 1) variant = kfmi::kEventsLane;
+    else if (v == 3 && lds_ok) variant = kfmi::kEventsLds;
     if (skip && variant != kfmi::kEventsChain) return fail(KF_EINVAL, "kf_run_stream: fallback needs the chain kernel");
     hipError_t e = kfmi::launch_ref_events(h->model, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream), variant);
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_run_events");
@@ -624,8 +672,8 @@ constexpr int kStreamPolish = 0;
 constexpr int64_t kStreamLftPiece = 160;
 // default split: T / kStreamTargetChunks events per chunk, at least kStreamMinChunk.  The map
 // pass runs a chunk's four variants in one 8-lane group: 8192 chunks are 1024 waves, one per
-// SIMD, and the pass's time is its chunk length in sequence (KFMI_STREAM_CHUNKS overrides the
-// target, for sweeps)
+// SIMD, and the pass's time is its chunk length in sequence (KF_OPT_STREAM_CHUNKS overrides the
+// target, for sweeps: KF_OPT_STREAM_CHUNKS)
 constexpr int64_t kStreamTargetChunks = 8192;
 constexpr int64_t kStreamMinChunk = 32;
 // piece maps (36 doubles) the start kernel stages in LDS per block: 64 KB
@@ -655,10 +703,8 @@ int kf_run_events(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     int rc = KF_OK;
     if (!check_events_args(h, T, etype, dt, payload, "kf_run_events", &rc)) return rc;
     // one filter over a long stream: parallel over time (checked, with a sequential fallback);
-    // KFMI_STREAM=off is a process-wide diagnostic switch, callers that want the sequential
-    // run per call use kf_run_events_seq
-    const char* sv = std::getenv("KFMI_STREAM");
-    if (h->B == 1 && !gate && T >= kStreamMinEvents && !(sv && !std::strcmp(sv, "off")))
+    // KF_OPT_STREAM = 1 turns the route off for the handle, kf_run_events_seq for one call
+    if (h->B == 1 && !gate && T >= kStreamMinEvents && opt(h, KF_OPT_STREAM) == 0)
         return kf_run_stream(h, T, etype, dt, payload, traj, cov, logdet, updated, 0, -1, stream);
     return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, gate, threshold, nullptr, stream);
 }
@@ -681,7 +727,7 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     if (!etype || !dt || !payload) return fail(KF_EINVAL, "kf_run_stream: null etype/dt/payload stream");
     const hipStream_t st = static_cast<hipStream_t>(stream);
     int64_t target = kStreamTargetChunks;
-    if (const char* v = std::getenv("KFMI_STREAM_CHUNKS")) target = std::max<int64_t>(2, std::atoll(v));
+    if (opt(h, KF_OPT_STREAM_CHUNKS) > 0) target = std::max<int64_t>(2, opt(h, KF_OPT_STREAM_CHUNKS));
     const int64_t L = chunk > 0 ? chunk : std::max<int64_t>(kStreamMinChunk, (int64_t(T) + target - 1) / target);
     const int64_t C = (int64_t(T) + L - 1) / L;
     // warmup >= 0: W events of warm-up before each chunk from the handle's covariance;
@@ -708,11 +754,10 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     const int np = int((L + kStreamLftPiece - 1) / kStreamLftPiece);
     const size_t lft_bytes = lft ? align256(sizeof(double) * 36 * nch * C * np) : 0;
     // records straight from the map pass (no final pass) unless the four variants' trajectory
-    // rows exceed the 32-bit offsets or KFMI_STREAM_FINAL=1 asks for the final pass
+    // rows exceed the 32-bit offsets or KF_OPT_STREAM_FINAL = 1 asks for the final pass
     const int ntraj = h->model == KF_MODEL_REF15 ? 6 : 3;
     const int64_t vstride = T + L;
-    const char* fv = std::getenv("KFMI_STREAM_FINAL");
-    const bool map_records = !(fv && !std::strcmp(fv, "1")) && uint64_t(4 * vstride) * ntraj * w < (uint64_t(1) << 31);
+    const bool map_records = opt(h, KF_OPT_STREAM_FINAL) == 0 && uint64_t(4 * vstride) * ntraj * w < (uint64_t(1) << 31);
     const size_t rec_bytes = map_records ? align256(size_t(4 * vstride) * ntraj * w) + align256(sizeof(double) * n) : 0;
     const int64_t ntiles = (C + kfmi::kStreamScanTile - 1) / kfmi::kStreamScanTile;
     const size_t need = 256 + 2 * bank1 + bank4 + 2 * align256(sizeof(double) * 12 * nch * C) +
@@ -735,6 +780,7 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     sa.rdelta = 1.0 / sa.delta;  // exact: delta is a power of two
     sa.tol_state = h->dtype == KF_F64 ? 1e-9 : 1e-4;
     sa.tol_cov = h->dtype == KF_F64 ? 1e-12 : 1e-5;
+    sa.start_threads = int(opt(h, KF_OPT_START_THREADS));
     sa.hx = h->x;
     sa.hP = h->P;
     sa.hstatus = h->status;
@@ -991,7 +1037,8 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.tail = k < kf_max;
         // a level without stored parents was scored whole by the previous launch's tail
         if (a.n_par) {
-            e = kfmi::launch_ref15_search(h->dtype == KF_F64, a, search_child_major(a.n_par), st);
+            a.pm_regs = opt(h, KF_OPT_SEARCH_PM) == 1;
+            e = kfmi::launch_ref15_search(h->dtype == KF_F64, a, search_child_major(h, a.n_par), st);
             if (e != hipSuccess) return hip_fail(e, "kf_search_combos: level launch");
         }
         last = k_base + k;
@@ -1066,6 +1113,7 @@ int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, 
     a.logdet = logdet;
     a.sel_time = sel_time;
     a.n_sel = n_sel;
+    a.regs = opt(h, KF_OPT_SCHED_KERNEL) == 1;
     hipError_t e = kfmi::launch_ref15_scheduled(h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_run_scheduled");
 }

@@ -621,21 +621,16 @@ __global__ __launch_bounds__(kBlock) void cv_synth_kernel(const SynthArgs a) {
 }
 
 // Optional cap on resident workgroups per CU for the run kernel (experiments / tail tuning):
-// KFMI_BLOCKS_PER_CU=k reserves 160 KiB / (k + 0.5) of (unused) LDS per workgroup so at most
-// k workgroups (k waves per SIMD) fit on a CU.  Unset = no cap.
-size_t lds_cap_bytes() {
-    static const size_t bytes = [] {
-        const char* e = getenv("KFMI_BLOCKS_PER_CU");
-        const int k = e ? atoi(e) : 0;
-        if (k < 2 || k > 8) return size_t(0);
-        return (size_t(160 * 1024) * 2 / (2 * k + 1) + 15) / 16 * 16;
-    }();
-    return bytes;
+// KF_OPT_BLOCKS_PER_CU = k reserves 160 KiB / (k + 0.5) of (unused) LDS per workgroup so at most
+// k workgroups (k waves per SIMD) fit on a CU.  0 = no cap.
+size_t lds_cap_bytes(int k) {
+    if (k < 2 || k > 8) return size_t(0);
+    return (size_t(160 * 1024) * 2 / (2 * k + 1) + 15) / 16 * 16;
 }
 
 template <int D, typename T>
 hipError_t launch_run(const CvArgs& a, dim3 grid, hipStream_t st) {
-    const size_t lds = lds_cap_bytes();
+    const size_t lds = lds_cap_bytes(a.blocks_per_cu);
     const bool fast = a.dt_steps == nullptr && a.u != nullptr && a.mask == nullptr &&
                       a.traj != nullptr && a.logdet != nullptr;
     bool diag = true;

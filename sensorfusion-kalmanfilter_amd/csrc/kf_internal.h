@@ -29,6 +29,7 @@ struct CvArgs {
     double p0_pos, p0_vel;   // reset covariance
     int block_p;             // P is block-diagonal over the axes (kf_run may use cv_block_kernel)
     int prefetch_depth;      // cv_block_kernel's input ring: 2, 4 or 8 steps
+    int blocks_per_cu;       // 2..8: cap resident workgroups per CU (KF_OPT_BLOCKS_PER_CU); 0 = none
 };
 
 struct SynthArgs {
@@ -130,6 +131,7 @@ struct StreamArgs {
     int iters;               // chunk maps (at least) behind every chunk start
     int64_t G;               // chunks per block of the start kernel (their windows' maps staged in LDS)
     int64_t g;               // chunks per thread of the start kernel; 0: no LDS, one chunk per thread
+    int start_threads;       // threads per block of the start kernel (KF_OPT_START_THREADS); 0 = kBlock
     // records from the map pass (no final pass): the map bank's trajectories per variant
     const void* traj4;       // [4][vstride][NTRAJ]
     int64_t vstride;
@@ -211,6 +213,7 @@ struct Ref15SearchArgs {
     int v_lo, n_groups;
     uint64_t gitem[66];
     uint64_t gblk[66];
+    bool pm_regs;            // parent-major: the parent's covariance in registers, not LDS (KF_OPT_SEARCH_PM)
 };
 
 constexpr int kSearchRows = 28;  // T rows of a search node
@@ -250,6 +253,7 @@ struct Ref15SchedArgs {
     void* logdet;            // [T][B]
     double* sel_time;        // [T][B]
     int32_t* n_sel;          // [B]
+    bool regs;               // the register-input kernel even where the LDS one is legal (KF_OPT_SCHED_KERNEL)
 };
 
 enum class Op { Run, Predict, Update, Step, Reset };  // Step: predict + update (kf_capi's deferral)

@@ -899,7 +899,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
 //    its epilogue giving x_end = A x_start + b per chunk and chain;
 //  * the maps are composed from the handle's state by a parallel scan (phases 2-4) into every
 //    chunk's true start; the records are the map pass's, the trajectory evaluated at the true
-//    starts (phase 8), or a final pass runs the chunks from them (KFMI_STREAM_FINAL=1);
+//    starts (phase 8), or a final pass runs the chunks from them (KF_OPT_STREAM_FINAL = 1);
 //  * checks: each chunk's start covariance equals the previous chunk's end covariance, the
 //    starts and the end state are finite (a final pass: each chunk's end state is its
 //    successor's start), no chunk filter failed.  Only then does the handle take the end
@@ -1016,7 +1016,7 @@ __device__ __forceinline__ void apply_map(double (&x)[3], const double* m) {
 //      pass (a.xend): no failed chunk filter, finite starts and end state, covariance seams within
 //      tolerance; a passed run leaves the end state and the last chunk's end covariance in the
 //      handle.  No state seam is measured there (the starts are the maps' values, not runs from
-//      them; KFMI_STREAM_FINAL=1 runs them and checks the seams in phase 5).
+//      them; KF_OPT_STREAM_FINAL = 1 runs them and checks the seams in phase 5).
 constexpr int kScanTile = 256;
 __device__ __forceinline__ void affine_compose(double (&o)[12], const double (&l)[12], const double (&e)[12]) {
     // o = l o e: A = A_l A_e, b = A_l b_e + b_l
@@ -1196,10 +1196,14 @@ __global__ __launch_bounds__(kScanTile) void stream_starts_kernel(const StreamAr
     // Everything the verdict reads from this launch travels by device-scope atomics (bad here,
     // cov_gap and bad from the map pass and the end state from earlier launches), so no fence:
     // the wave only drains its own atomic before it counts itself (an agent-scope release per
-    // block wrote its XCD's L2 back and cost more than the kernel's work)
+    // block wrote its XCD's L2 back and cost more than the kernel's work).  The empty asm with a
+    // memory clobber keeps the compiler from moving the bad update past the count (s_waitcnt
+    // alone is not a compiler barrier); the wait then drains it in the hardware.
+    asm volatile("" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0);
     const int blocks = int(gridDim.x * gridDim.y);
     if (atomicAdd(&k->done, 1) != blocks - 1) return;
+    asm volatile("" ::: "memory");  // the verdict's reads stay after the count
     const int bad = atomicOr(&k->bad, 0);
     const double cov_gap = __longlong_as_double(atomicOr(reinterpret_cast<unsigned long long*>(&k->cov_gap), 0ull));
     k->state_gap = bad & kStreamBadStart ? __builtin_inf() : __builtin_nan("");
@@ -2428,10 +2432,9 @@ hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t str
 hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream) {
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
     // the LDS variant's descriptors: whole waves, and a chunk's row spans within 32-bit ranges
-    const char* v = std::getenv("KFMI_SCHED");
     const bool lds = a.B % 64 == 0 && uint64_t(a.B) * 8 * 2 < (uint64_t(1) << 32) &&
                      reinterpret_cast<uintptr_t>(a.t) % 16 == 0 && reinterpret_cast<uintptr_t>(a.etype) % 16 == 0 &&
-                     uint64_t(a.B) * kSchedChunk < (uint64_t(1) << 32) && !(v && !std::strcmp(v, "regs"));
+                     uint64_t(a.B) * kSchedChunk < (uint64_t(1) << 32) && !a.regs;
     if (lds) {
         if (f64) ref15_sched_lds_kernel<double><<<grid, kBlock, 0, stream>>>(a);
         else ref15_sched_lds_kernel<float><<<grid, kBlock, 0, stream>>>(a);
@@ -2541,9 +2544,8 @@ void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
             const int64_t bc = a.g > 0 ? a.G : kBlock;
             // LDS variant: G / g threads walk, but the whole block stages the window maps (more
             // loads in flight; the extra threads leave after the staging)
-            const char* ev = std::getenv("KFMI_START_THREADS");
             const unsigned walkers = a.g > 0 ? unsigned((a.G + a.g - 1) / a.g) : unsigned(kBlock);
-            const unsigned want = ev ? unsigned(std::atoi(ev)) : unsigned(kBlock);
+            const unsigned want = a.start_threads > 0 ? unsigned(a.start_threads) : unsigned(kBlock);
             const unsigned threads = a.g > 0 ? (want > walkers && want <= unsigned(kBlock) ? want : walkers)
                                              : unsigned(kBlock);
             const size_t lds = a.g > 0 ? size_t(a.G + a.iters) * a.np * 36 * sizeof(double) : 0;
@@ -2594,11 +2596,6 @@ hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t st
     return hipGetLastError();
 }
 
-// KFMI_SEARCH_PM=lds|regs picks the parent-major variant (A/B runs); default: lds
-bool search_pm_lds() {
-    const char* v = std::getenv("KFMI_SEARCH_PM");
-    return !(v && !std::strcmp(v, "regs"));
-}
 
 hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream) {
     // node offsets are 32-bit byte offsets (buffer voffset)
@@ -2637,7 +2634,7 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
         else ref15_search_cm_kernel<float><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
         return hipGetLastError();
     }
-    if (search_pm_lds()) {
+    if (!a.pm_regs) {
         const dim3 grid(static_cast<unsigned>((a.n_par + 63) / 64));
         if (f64) ref15_search_pm_kernel<double, true><<<grid, 64, 0, stream>>>(a);
         else ref15_search_pm_kernel<float, true><<<grid, 64, 0, stream>>>(a);

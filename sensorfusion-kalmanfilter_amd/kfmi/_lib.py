@@ -6,6 +6,8 @@ unloadable library raises ``KFError`` — there is no CPU fallback anywhere in `
 from __future__ import annotations
 
 import ctypes
+import glob
+import hashlib
 import os
 import re
 
@@ -13,6 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # KFMI_LIB selects an alternative build (e.g. an occupancy variant); relative to the cwd.
 LIB_PATH = os.path.abspath(os.environ.get('KFMI_LIB') or os.path.join(HERE, 'libkfmi.so'))
 HEADER = os.path.normpath(os.path.join(HERE, '..', '..', 'include', 'kf.h'))
+CSRC = os.path.normpath(os.path.join(HERE, '..', 'csrc'))
 
 KF_OK = 0
 KF_EINVAL = -1
@@ -34,6 +37,18 @@ KF_INGEST_GPS_ALTITUDE = 1
 KF_DT_FULL = 0
 KF_DT_MONOTONE = 1
 KF_DT_RAW = 2
+
+KF_OPT_PREDICT = 1
+KF_OPT_CV_KERNEL = 2
+KF_OPT_BLOCKS_PER_CU = 3
+KF_OPT_EVENTS_KERNEL = 4
+KF_OPT_STREAM = 5
+KF_OPT_STREAM_CHUNKS = 6
+KF_OPT_STREAM_FINAL = 7
+KF_OPT_START_THREADS = 8
+KF_OPT_SEARCH_KERNEL = 9
+KF_OPT_SEARCH_PM = 10
+KF_OPT_SCHED_KERNEL = 11
 
 _ERRNAMES = {KF_EINVAL: 'KF_EINVAL', KF_EHIP: 'KF_EHIP', KF_ENOTSPD: 'KF_ENOTSPD',
              KF_ENODEV: 'KF_ENODEV', KF_ENOMEM: 'KF_ENOMEM'}
@@ -67,6 +82,8 @@ _d = ctypes.c_double
 # name -> (restype, argtypes); must match include/kf.h exactly (tests/test_capi.py checks).
 SIGNATURES = {
     'kf_version': (ctypes.c_char_p, []),
+    'kf_set_option': (_i, [_vp, _i, _i64]),
+    'kf_get_option': (_i, [_vp, _i, ctypes.POINTER(_i64)]),
     'kf_last_error': (ctypes.c_char_p, []),
     'kf_default_params': (_i, [_i, ctypes.POINTER(kf_params)]),
     'kf_device_count': (_i, [ctypes.POINTER(_i)]),
@@ -110,8 +127,25 @@ def header_functions(path=HEADER):
     return sorted(set(re.findall(r'\b(kf_\w+)\s*\(', text)))
 
 
+def source_hash():
+    """SHA-256 (16 hex) of the sources in this tree that libkfmi.so is built from, in the
+    Makefile's order (HASHED): csrc/*.cpp, *.h, *.hip sorted by name, then include/kf.h."""
+    files = sorted(p for ext in ('cpp', 'h', 'hip') for p in glob.glob(os.path.join(CSRC, '*.' + ext)))
+    h = hashlib.sha256()
+    for p in files + [HEADER]:
+        with open(p, 'rb') as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def library_hash(handle):
+    v = handle.kf_version().decode()
+    return v.rsplit('src:', 1)[1] if 'src:' in v else None
+
+
 def lib():
-    """Load libkfmi.so once and bind every entry point; raise KFError if it is missing."""
+    """Load libkfmi.so once and bind every entry point; raise KFError if it is missing or was
+    built from other sources than this tree's (a stale build would test and time old code)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -126,8 +160,21 @@ def lib():
         fn = getattr(handle, name)
         fn.restype = res
         fn.argtypes = args
+    built, tree = library_hash(handle), source_hash()
+    if built != tree and os.environ.get('KFMI_ALLOW_FOREIGN_LIB') != '1':
+        raise KFError(KF_ENODEV, f'{LIB_PATH} was built from sources {built}, this tree is {tree}: rebuild '
+                                 f'(make -C sensorfusion-kalmanfilter_amd); KFMI_ALLOW_FOREIGN_LIB=1 loads it '
+                                 f'anyway (A/B of another revision only)')
     _lib = handle
     return _lib
+
+
+def build_info():
+    """Provenance of the loaded library, for the bench line."""
+    L = lib()
+    built, tree = library_hash(L), source_hash()
+    return {'lib': os.path.relpath(LIB_PATH, os.path.join(HERE, '..', '..')), 'version': L.kf_version().decode(),
+            'src_hash': built, 'tree_hash': tree, 'match': built == tree}
 
 
 def last_error():

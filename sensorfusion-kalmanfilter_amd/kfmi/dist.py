@@ -63,6 +63,35 @@ def gather_shards(local, total, group=None):
     return torch.cat(parts, dim=-1).reshape(lead + (total,))
 
 
+def decimated_steps(T, every):
+    """Time steps kept by a trajectory decimated every ``every`` steps: every-1, 2 every-1, ...
+    (the last step whenever every divides T); none for every <= 0."""
+    return list(range(every - 1, T, every)) if every > 0 else []
+
+
+def gather_run_outputs(x, logdet_last, traj=None, every=0, total=None, group=None):
+    """Reassemble a sharded run on every rank (north_star: the RCCL all-gather "to reassemble
+    the final trajectory array"; the brute-force parent's tuples carry each combination's
+    trajectory, kf_workers.py:86, 1349-1371).  x [n, b] final states, logdet_last [b] last
+    log-dets, traj [T, W, b] (optional) decimated to ``decimated_steps(T, every)``: all packed
+    into one [rows, b] tensor and moved by ONE all-gather.  Returns dict(x [n, total], logdet
+    [total], traj [R, W, total] or None, rows, bytes_per_rank) in global filter order."""
+    b = x.shape[-1]
+    total = b if total is None else int(total)
+    parts = [x.reshape(-1, b), logdet_last.reshape(1, b)]
+    steps = decimated_steps(traj.shape[0], every) if traj is not None else []
+    if steps:
+        parts.append(traj[steps[0]::every][:len(steps)].reshape(-1, b))
+    packed = torch.cat(parts, dim=0).contiguous()
+    full = gather_shards(packed, total, group=group)
+    n = x.shape[0]
+    out = dict(x=full[:n], logdet=full[n], traj=None, rows=packed.shape[0],
+               bytes_per_rank=packed.numel() * packed.element_size())
+    if steps:
+        out['traj'] = full[n + 1:].reshape(len(steps), traj.shape[1], total)
+    return out
+
+
 def max_over_ranks(values, device, group=None):
     """Element-wise max of a list of floats over all ranks (timing: the slowest rank counts)."""
     import torch.distributed as dist

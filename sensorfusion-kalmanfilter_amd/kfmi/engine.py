@@ -27,6 +27,22 @@ TRAJ_WIDTH = {'ref15': 6, 'ref8': 3}  # kf_workers.py:714 (x, y, z, roll, pitch,
 DTYPES = {'f32': (_lib.KF_F32, torch.float32, np.float32), 'f64': (_lib.KF_F64, torch.float64, np.float64)}
 
 
+# kf_set_option (include/kf.h): option name -> (id, value names); 0 = the library's choice
+OPTIONS = {
+    'predict': (_lib.KF_OPT_PREDICT, {'auto': 0, 'deferred': 0, 'eager': 1}),
+    'cv_kernel': (_lib.KF_OPT_CV_KERNEL, {'auto': 0, 'general': 1, 'block2': 2, 'block4': 4, 'block8': 8}),
+    'blocks_per_cu': (_lib.KF_OPT_BLOCKS_PER_CU, {'auto': 0}),
+    'events_kernel': (_lib.KF_OPT_EVENTS_KERNEL, {'auto': 0, 'lane': 1, 'chain': 2, 'lds': 3}),
+    'stream': (_lib.KF_OPT_STREAM, {'auto': 0, 'off': 1}),
+    'stream_chunks': (_lib.KF_OPT_STREAM_CHUNKS, {'auto': 0}),
+    'stream_final': (_lib.KF_OPT_STREAM_FINAL, {'auto': 0, 'off': 0, 'on': 1}),
+    'start_threads': (_lib.KF_OPT_START_THREADS, {'auto': 0}),
+    'search_kernel': (_lib.KF_OPT_SEARCH_KERNEL, {'auto': 0, 'cm': 1, 'pm': 2}),
+    'search_pm': (_lib.KF_OPT_SEARCH_PM, {'auto': 0, 'lds': 0, 'regs': 1}),
+    'sched_kernel': (_lib.KF_OPT_SCHED_KERNEL, {'auto': 0, 'regs': 1}),
+}
+
+
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -50,7 +66,7 @@ class BatchedKF:
     triangle packed row-major), status [B] int32.
     """
 
-    def __init__(self, model='cv3', batch=1, dtype='f64', device=0, params=None):
+    def __init__(self, model='cv3', batch=1, dtype='f64', device=0, params=None, options=None):
         if model not in MODELS:
             raise ValueError(f'unknown model {model!r}; choose from {sorted(MODELS)}')
         if dtype not in DTYPES:
@@ -76,6 +92,8 @@ class BatchedKF:
         check(L.kf_alloc(ctypes.byref(h), MODELS[model][0], self.batch, DTYPES[dtype][0],
                          ctypes.byref(self.params) if self.params is not None else None))
         self._h = h
+        for k, v in (options or {}).items():
+            self.set_option(k, v)
 
     # -- lifecycle ---------------------------------------------------------------------
     def close(self):
@@ -103,6 +121,20 @@ class BatchedKF:
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # -- options (kf_set_option): per handle, nothing is read from the environment --------
+    def set_option(self, name, value):
+        """Select a kernel variant for this handle (A/B runs, tests); ``name`` is one of
+        OPTIONS, ``value`` an int or one of that option's names (``'auto'`` = 0 everywhere)."""
+        opt, names = OPTIONS[name]
+        v = names[value] if isinstance(value, str) else int(value)
+        check(_lib.lib().kf_set_option(self.handle, opt, v))
+        return self
+
+    def get_option(self, name):
+        out = ctypes.c_int64(0)
+        check(_lib.lib().kf_get_option(self.handle, OPTIONS[name][0], ctypes.byref(out)))
+        return out.value
 
     # -- buffers -------------------------------------------------------------------------
     def empty(self, *shape, dtype=None):

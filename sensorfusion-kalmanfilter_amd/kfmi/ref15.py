@@ -271,17 +271,18 @@ def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initi
 parallel_check = {}
 
 
-def run_stream_parallel(et, dt, pay, x0, P0b, chunk=None, warmup=None, dtype='f64', cov=False):
+def run_stream_parallel(et, dt, pay, x0, P0b, chunk=None, warmup=None, dtype='f64', cov=False, options=None):
     """One filter over a long event stream, parallel over time (kf_run_stream): et [T] uint8,
     dt [T] float64 (the driver's dt rule already applied), pay [T, 9] on the device; x0 [15], P0b
     [27] block-packed initial state.  Returns (traj [T, 6], logdet [T], x [15], P blocks [27],
     cov [T, 27] or None) on the device.  The chunked records stand only if the device checks
     pass (warm-up covariances meet their predecessors' end covariances, chunk end states meet
     the next starts, no chunk filter failed); otherwise the library's sequential fallback has
-    rewritten them.  ``parallel_check`` holds the verdict and the measured gaps."""
+    rewritten them.  ``parallel_check`` holds the verdict and the measured gaps.  ``options``:
+    BatchedKF options of the handle (e.g. stream_final='on')."""
     dev = et.device
     npd = torch.float64 if dtype == 'f64' else torch.float32
-    kf = BatchedKF('ref15', 1, dtype, device=dev.index or 0)
+    kf = BatchedKF('ref15', 1, dtype, device=dev.index or 0, options=options)
     try:
         kf.set_state(torch.as_tensor(np.asarray(x0, np.float64).reshape(15, 1), dtype=npd, device=dev),
                      torch.as_tensor(np.asarray(P0b, np.float64).reshape(27, 1), dtype=npd, device=dev))

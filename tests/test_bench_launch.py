@@ -1,0 +1,59 @@
+"""bench.py's rank launch (CPU, gloo): `python bench.py --gpus N` must run N ranks, never a
+silent single rank.  --launch-check stops each rank after the process group
+forms, before any GPU work, so the real launch path runs here."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_plan_single_rank_runs_in_process():
+    assert bench.launch_plan(1, {}, []) is None
+    assert bench.launch_plan(4, {'WORLD_SIZE': '4'}, []) is None   # a launcher already started us
+
+
+def test_plan_starts_n_ranks():
+    cmd = bench.launch_plan(8, {}, ['--gpus', '8', '--steps', '5'], script='/x/bench.py', port=29512)
+    assert cmd[:3] == [sys.executable, '-m', 'torch.distributed.run']
+    assert '--nproc-per-node=8' in cmd and '--master-addr=127.0.0.1' in cmd and '--master-port=29512' in cmd
+    assert cmd[-4:] == ['--gpus', '8', '--steps', '5'] and cmd[-5] == '/x/bench.py'
+
+
+@pytest.mark.parametrize('gpus,world', [(2, '1'), (8, '4'), (1, '2')])
+def test_plan_rejects_world_mismatch(gpus, world):
+    with pytest.raises(SystemExit):
+        bench.launch_plan(gpus, {'WORLD_SIZE': world}, [])
+
+
+def test_plan_rejects_zero_gpus():
+    with pytest.raises(SystemExit):
+        bench.launch_plan(0, {}, [])
+
+
+def _run(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK')}
+    env.update(env_extra or {})
+    env.setdefault('OMP_NUM_THREADS', '1')
+    return subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args, env=env, cwd=ROOT,
+                          capture_output=True, text=True, timeout=240)
+
+
+@pytest.mark.parametrize('n', [1, 2, 3])
+def test_bench_starts_its_own_ranks(n):
+    p = _run(['--gpus', str(n), '--launch-check'])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, p.stdout            # rank 0 alone prints, once
+    assert lines[0]['ranks_seen'] == n and lines[0]['world_size'] == n
+
+
+def test_bench_world_mismatch_exits_nonzero():
+    p = _run(['--gpus', '2', '--launch-check'], {'WORLD_SIZE': '1', 'RANK': '0', 'LOCAL_RANK': '0'})
+    assert p.returncode != 0
+    assert 'WORLD_SIZE=1' in p.stderr

@@ -76,6 +76,60 @@ def test_gloo_world2_shard_and_gather(total):
     assert slow == [1.5, 0.0]
 
 
+def _traj_worker(rank, world, port, total, T, every, out_q):
+    """gather_run_outputs: final x, last log-det and the trajectory decimated every `every`
+    steps, one all-gather, against the unsharded oracle run."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(321)
+        model = ref_kf.CV3
+        x0 = rng.normal(0, 100, (total, 6))
+        u = rng.normal(0, 0.3, (T, 3, total))
+        z = rng.normal(0, 30, (T, 3, total))
+        off, cnt = kdist.shard_range(total, rank, world)
+        sl = slice(off, off + cnt)
+        tr, ld, x, _ = ref_kf.run_batch(model, x0[sl], model.P0(), np.full(T, 0.1), u[:, :, sl], z[:, :, sl], 1)
+        res = kdist.gather_run_outputs(torch.from_numpy(np.ascontiguousarray(x.T)), torch.from_numpy(ld[-1].copy()),
+                                       torch.from_numpy(tr), every, total)
+        if rank == 0:
+            trg, ldg, xg, _ = ref_kf.run_batch(model, x0, model.P0(), np.full(T, 0.1), u, z, 1)
+            steps = kdist.decimated_steps(T, every)
+            errs = [np.abs(res['x'].numpy() - xg.T).max(), np.abs(res['logdet'].numpy() - ldg[-1]).max()]
+            if steps:
+                errs.append(np.abs(res['traj'].numpy() - trg[steps]).max())
+            else:
+                errs.append(0.0 if res['traj'] is None else np.inf)
+            out_q.put((errs, res['rows'], len(steps)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,total,T,every', [(2, 11, 8, 4), (3, 10, 9, 4), (3, 7, 6, 0), (2, 5, 5, 1)])
+def test_gloo_gather_decimated_trajectory(world, total, T, every):
+    """Uneven shards (11 over 2, 10 and 7 over 3), T not a multiple of every, no trajectory."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_traj_worker, args=(r, world, port, total, T, every, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    assert [p.exitcode for p in procs] == [0] * world
+    errs, rows, nsteps = q.get(timeout=10)
+    assert nsteps == len(range(every - 1, T, every)) if every else nsteps == 0
+    assert rows == 6 + 1 + 6 * nsteps
+    assert max(errs) == 0.0, errs  # the gather moves bits; the shards ran the same arithmetic
+
+
+def test_decimated_steps():
+    assert kdist.decimated_steps(256, 16) == list(range(15, 256, 16))
+    assert kdist.decimated_steps(10, 4) == [3, 7]
+    assert kdist.decimated_steps(10, 0) == []
+    assert kdist.decimated_steps(3, 1) == [0, 1, 2]
+
+
 def _bf_worker(rank, world, port, golden, thr, out_q):
     """kfmi.dist.brute_force_search on gloo with the oracle as the per-rank evaluator."""
     import sys

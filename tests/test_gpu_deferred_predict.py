@@ -1,13 +1,11 @@
 """kf_predict held back and fused into the next kf_update (the reference's per-step call shape,
 kf_workers.py:688-711, run as one kernel step): the same results as eager predict + update
-kernels (KFMI_PREDICT=eager), whatever the caller does between the two calls — needs an MI355X.
+kernels (option predict='eager'), whatever the caller does between the two calls — needs an MI355X.
 
 Tolerance: the fused step is the kf_run kernel's step and the eager pair the per-op kernels;
 they evaluate the same expressions, compared at 1e-12 (fp64) / 1e-5 (fp32) relative.
 """
-import contextlib
 import ctypes
-import os
 
 import numpy as np
 import pytest
@@ -20,19 +18,6 @@ pytestmark = pytest.mark.gpu
 
 RTOL = {'f64': 1e-12, 'f32': 1e-5}
 NP = {'f64': np.float64, 'f32': np.float32}
-
-
-@contextlib.contextmanager
-def eager():
-    old = os.environ.get('KFMI_PREDICT')
-    os.environ['KFMI_PREDICT'] = 'eager'
-    try:
-        yield
-    finally:
-        if old is None:
-            del os.environ['KFMI_PREDICT']
-        else:
-            os.environ['KFMI_PREDICT'] = old
 
 
 def inputs(name, dtype, B, T, seed):
@@ -55,15 +40,13 @@ def run_script(name, dtype, x0, script):
     """script(kf) -> list of tensors to compare; run once deferred, once eager."""
     outs = []
     for mode in ('deferred', 'eager'):
-        ctx = eager() if mode == 'eager' else contextlib.nullcontext()
-        with ctx:
-            kf = kfmi.BatchedKF(name, x0.shape[1], dtype)
-            kf.reset(x0)
-            res = [r.clone() for r in script(kf)]
-            x, P = kf.state()
-            res += [x, P, kf.status()]
-            torch.cuda.synchronize()
-            kf.close()
+        kf = kfmi.BatchedKF(name, x0.shape[1], dtype, options={'predict': mode})
+        kf.reset(x0)
+        res = [r.clone() for r in script(kf)]
+        x, P = kf.state()
+        res += [x, P, kf.status()]
+        torch.cuda.synchronize()
+        kf.close()
         outs.append(res)
     return outs
 
@@ -218,15 +201,93 @@ def test_graph_capture_of_the_per_step_loop():
     got = [l.clone() for l in ld] + list(kf.state())
     kf.close()
 
-    with eager():
-        kf = kfmi.BatchedKF('cv3', B, 'f64')
-        kf.reset(x0)
-        ref = []
-        for t in range(T):
-            kf.predict(0.1, u[t])
-            ref.append(kf.update(z[t]))
-        ref += list(kf.state())
-        torch.cuda.synchronize()
-        kf.close()
+    kf = kfmi.BatchedKF('cv3', B, 'f64', options={'predict': 'eager'})
+    kf.reset(x0)
+    ref = []
+    for t in range(T):
+        kf.predict(0.1, u[t])
+        ref.append(kf.update(z[t]))
+    ref += list(kf.state())
+    torch.cuda.synchronize()
+    kf.close()
     for a, b in zip(got, ref):
+        close(a, b, 'f64')
+
+
+def test_warmup_on_one_stream_then_capture_on_another():
+    """The torch.cuda.graph pattern: run the per-step loop eagerly on the default
+    stream, then capture it (torch captures on a side stream).  The first captured predict's
+    control copy would have to wait for the eager loop's last fused step, recorded outside the
+    capture: it runs eagerly instead, and the replayed graph gives the eager results."""
+    B, T = 1024, 4
+    x0, u, z = inputs('cv3', 'f64', B, T, seed=19)
+    kf = kfmi.BatchedKF('cv3', B, 'f64')
+    ld = [kf.empty(B) for _ in range(T)]
+    lib = _lib.lib()
+
+    def loop():
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for t in range(T):
+            _lib.check(lib.kf_predict(kf.handle, 0.1, None, ctypes.c_void_p(u[t].data_ptr()), None, st))
+            _lib.check(lib.kf_update(kf.handle, ctypes.c_void_p(z[t].data_ptr()), None,
+                                     ctypes.c_void_p(ld[t].data_ptr()), st))
+
+    kf.reset(x0)
+    loop()                       # warm-up on the default stream: its fused steps read pend_u
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):    # capture on torch's side stream
+        loop()
+    kf.reset(x0)
+    g.replay()
+    torch.cuda.synchronize()
+    got = [l.clone() for l in ld] + list(kf.state())
+    kf.close()
+
+    kf = kfmi.BatchedKF('cv3', B, 'f64', options={'predict': 'eager'})
+    kf.reset(x0)
+    ref = []
+    for t in range(T):
+        kf.predict(0.1, u[t])
+        ref.append(kf.update(z[t]))
+    ref += list(kf.state())
+    torch.cuda.synchronize()
+    kf.close()
+    for a, b in zip(got, ref):
+        close(a, b, 'f64')
+
+
+def test_reader_stream_destroyed_before_next_predict():
+    """A fused step on a side stream that the caller then destroys: the next deferred predict
+    on the default stream waits on the event recorded right after that read, never on the
+    destroyed stream."""
+    B, T = 512, 3
+    x0, u, z = inputs('cv3', 'f64', B, T, seed=21)
+    kf = kfmi.BatchedKF('cv3', B, 'f64')
+    kf.reset(x0)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        kf.predict(0.1, u[0])
+        l0 = kf.update(z[0])
+    torch.cuda.current_stream().wait_stream(s)
+    del s
+    torch.cuda.synchronize()
+    out = [l0]
+    for t in range(1, T):
+        kf.predict(0.1, u[t])
+        out.append(kf.update(z[t]))
+    out += list(kf.state())
+    torch.cuda.synchronize()
+    kf.close()
+    kf = kfmi.BatchedKF('cv3', B, 'f64', options={'predict': 'eager'})
+    kf.reset(x0)
+    ref = []
+    for t in range(T):
+        kf.predict(0.1, u[t])
+        ref.append(kf.update(z[t]))
+    ref += list(kf.state())
+    torch.cuda.synchronize()
+    kf.close()
+    for a, b in zip(out, ref):
         close(a, b, 'f64')

@@ -266,34 +266,57 @@ def test_synth_statistics():
     assert torch.isfinite(z).all()
 
 
-@pytest.mark.parametrize('dtype', ['f64', 'f32'])
-def test_full_size_config_sampled(dtype):
-    """BASELINE config 3 (fp64) / config 4's per-GPU shard (fp32): B = 1,048,576 6/3 filters,
-    T = 256, dt = 0.1 s, update every step, on synthetic streams.  Oracle on 4096 sampled
-    filters (spread + both ends), size-independent properties on all of them."""
-    B, T = 1 << 20, 256
-    kf = kfmi.BatchedKF('cv3', B, dtype)
-    x0, u, z = kf.synth(T=T, dt=0.1, update_every=1, seed=20251015)
+FULL_SIZE = {
+    # BASELINE.json configs at the sizes bench.py times: name, dtype, B, T, dt, k
+    'config2': ('cv2', 'f32', 1 << 16, 1024, 0.1, 1),
+    'config3': ('cv3', 'f64', 1 << 20, 256, 0.1, 1),
+    'config4': ('cv3', 'f32', 1 << 20, 256, 0.1, 1),   # config 4's per-GPU shard
+    'config5': ('cv3', 'f64', 1 << 20, 500, 0.01, 10),  # 100 Hz predict, 10 Hz GPS update
+}
+
+
+@pytest.mark.parametrize('config', sorted(FULL_SIZE))
+def test_full_size_config_sampled(config):
+    """Every BASELINE GPU config at its bench size, on synthetic streams: the oracle (the
+    reference step, kf_workers.py:688-717, fed the same — for fp32 fp32-rounded — inputs) on
+    >= 4096 sampled filters spread over the batch plus the wave and batch edges, per step
+    (every predict-only step of config 5 and every update step's log-det), and size-independent
+    properties on all filters.  Config 2's fp32 drift over 1024 steps is the case the 1e-3 gate
+    could bite."""
+    name, dtype, B, T, dt, k = FULL_SIZE[config]
+    model = MODEL[name]
+    kf = kfmi.BatchedKF(name, B, dtype)
+    x0, u, z = kf.synth(T=T, dt=dt, update_every=k, seed=20251015)
     kf.reset(x0)
-    tr, ld = kf.run(u, z, dt=0.1)
+    tr, ld = kf.run(u, z, dt=dt, update_every=k)
     st = kf.status()
     assert int((st != 0).sum()) == 0
-    assert bool(torch.isfinite(ld).all())
-    idx = np.unique(np.concatenate([np.linspace(0, B - 1, 4090).astype(np.int64),
-                                    [0, 1, 63, 64, B - 65, B - 1]]))
+    assert bool(torch.isfinite(ld).all()) and bool(torch.isfinite(tr).all())
+    edges = [0, 1, 62, 63, 64, 65, 127, 128, 255, 256, B // 2 - 1, B // 2, B - 129, B - 65, B - 64, B - 2, B - 1]
+    idx = np.unique(np.concatenate([np.linspace(0, B - 1, 4096).astype(np.int64), edges]))
+    assert len(idx) >= 4096
     it = torch.from_numpy(idx).cuda()
     xs = x0[:, it].double().cpu().numpy().T
     us = u[:, :, it].double().cpu().numpy()
     zs = z[:, :, it].double().cpu().numpy()
-    ref_tr, ref_ld, _, _ = ref_kf.run_batch(ref_kf.CV3, xs, ref_kf.CV3.P0(), np.full(T, 0.1), us, zs, 1)
-    ex, el = ref_kf.parity_errors(tr[:, :, it].double().cpu().numpy(), ld[:, it].double().cpu().numpy(),
-                                  ref_tr, ref_ld)
+    ref_tr, ref_ld, _, _ = ref_kf.run_batch(model, xs, model.P0(), np.full(T, dt), us, zs, k)
+    got_tr, got_ld = tr[:, :, it].double().cpu().numpy(), ld[:, it].double().cpu().numpy()
+    ex, el = ref_kf.parity_errors(got_tr, got_ld, ref_tr, ref_ld)
     assert ex <= TOL[dtype], ex
     assert el <= TOL[dtype], el
+    if k > 1:  # the update steps on their own (10 Hz GPS): logdet drops there
+        up = np.arange(k - 1, T, k)
+        _, el_up = ref_kf.parity_errors(got_tr[up], got_ld[up], ref_tr[up], ref_ld[up])
+        assert el_up <= TOL[dtype], el_up
+        assert (np.diff(ref_ld, axis=0)[up - 1] < 0).all()
     # logdet is identical across filters that share dt/P0 when no filter fails (P does not
     # depend on the data in a linear KF): a checksum across the whole batch
     spread = (ld.max(dim=1).values - ld.min(dim=1).values).abs().max().item()
     assert spread <= (1e-9 if dtype == 'f64' else 1e-3)
+    # the handle's final state is the last trajectory row, for every filter
+    x, _ = kf.state()
+    assert torch.equal(x, tr[-1])
+    kf.close()
 
 
 @pytest.mark.parametrize('dtype', ['f64', 'f32'])
@@ -328,23 +351,17 @@ def test_logdet_kernel_on_random_spd(dtype, name, wide):
 
 
 def _run_with_kernel(kernel, name, dtype, x0, u, z, k, dt, P=None):
-    old = os.environ.get('KFMI_CV_KERNEL')
-    os.environ['KFMI_CV_KERNEL'] = kernel
-    try:
-        B = x0.shape[0]
-        kf = kfmi.BatchedKF(name, B, dtype)
-        kf.reset(torch.from_numpy(np.ascontiguousarray(x0.T.astype(NP[dtype]))).cuda())
-        if P is not None:
-            kf.set_state(np.ascontiguousarray(x0.T.astype(NP[dtype])), np.ascontiguousarray(P.astype(NP[dtype])))
-        tr, ld = kf.run(torch.from_numpy(u.astype(NP[dtype])).cuda(), torch.from_numpy(z.astype(NP[dtype])).cuda(),
-                        dt=dt, update_every=k)
-        x, Pp = kf.state()
-        return [v.cpu().numpy() for v in (tr, ld, x, Pp, kf.status())]
-    finally:
-        if old is None:
-            del os.environ['KFMI_CV_KERNEL']
-        else:
-            os.environ['KFMI_CV_KERNEL'] = old
+    B = x0.shape[0]
+    kf = kfmi.BatchedKF(name, B, dtype, options={'cv_kernel': kernel})
+    kf.reset(torch.from_numpy(np.ascontiguousarray(x0.T.astype(NP[dtype]))).cuda())
+    if P is not None:
+        kf.set_state(np.ascontiguousarray(x0.T.astype(NP[dtype])), np.ascontiguousarray(P.astype(NP[dtype])))
+    tr, ld = kf.run(torch.from_numpy(u.astype(NP[dtype])).cuda(), torch.from_numpy(z.astype(NP[dtype])).cuda(),
+                    dt=dt, update_every=k)
+    x, Pp = kf.state()
+    out = [v.cpu().numpy() for v in (tr, ld, x, Pp, kf.status())]
+    kf.close()
+    return out
 
 
 @pytest.mark.parametrize('dtype', ['f64', 'f32'])

@@ -120,14 +120,13 @@ def _search_case(golden_dir, n, swap=True):
 
 @pytest.mark.parametrize('kernel', ['cm', 'pm'])
 @pytest.mark.parametrize('dtype', ['f64', 'f32'])
-def test_search_subset_max_equals_eval_combos(golden_dir, dtype, kernel, monkeypatch):
+def test_search_subset_max_equals_eval_combos(golden_dir, dtype, kernel):
     """kf_search_combos (one event step per subset, from the stored prefix) gives every subset the
     max log-det the per-subset kernel gives (same operations in the same order), with either
     search kernel (child-major / parent-major levels)."""
-    monkeypatch.setenv('KFMI_SEARCH_KERNEL', kernel)
     n = 12
     cand, ev, init, t0, target = _search_case(golden_dir, n)
-    kf = kfmi.BatchedKF('ref15', 1, dtype)
+    kf = kfmi.BatchedKF('ref15', 1, dtype, options={'search_kernel': kernel})
     kfound, win, acc, sm = kf.search_combos(ev, init, t0, target, threshold=-1e30, exhaustive=True, subset_max=True)
     kf.close()
     assert kfound == 0 and win is None and int(acc.sum()) == 0
@@ -152,13 +151,12 @@ def test_search_subset_max_equals_eval_combos(golden_dir, dtype, kernel, monkeyp
 
 @pytest.mark.parametrize('kernel', ['cm', 'pm'])
 @pytest.mark.parametrize('n,k_max', [(1, 1), (2, 2), (3, 3), (4, 4), (9, 3), (9, 8), (9, 9)])
-def test_search_small_and_cut_levels(golden_dir, n, k_max, kernel, monkeypatch):
+def test_search_small_and_cut_levels(golden_dir, n, k_max, kernel):
     """Edge cases of the stored levels: with n <= 3 some levels have no stored parents (scored
     whole by the previous launch's tail); with k_max < n no subset larger than k_max is scored
     (the tail stops at k_max).  Every subset up to k_max gets the per-subset kernel's score."""
-    monkeypatch.setenv('KFMI_SEARCH_KERNEL', kernel)
     cand, ev, init, t0, target = _search_case(golden_dir, n, swap=n > 6)
-    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    kf = kfmi.BatchedKF('ref15', 1, 'f64', options={'search_kernel': kernel})
     kfound, win, acc, sm = kf.search_combos(ev, init, t0, target, threshold=-1e30, k_max=k_max, exhaustive=True,
                                             subset_max=True)
     kf.close()
@@ -178,14 +176,13 @@ def test_search_small_and_cut_levels(golden_dir, n, k_max, kernel, monkeypatch):
 
 @pytest.mark.parametrize('kernel', ['cm', 'pm'])
 @pytest.mark.parametrize('q', [0.0, 0.01, 0.3, 0.9])
-def test_search_winner_matches_per_subset_search(golden_dir, q, kernel, monkeypatch):
+def test_search_winner_matches_per_subset_search(golden_dir, q, kernel):
     """The search's winner and per-size accepted counts at thresholds across the distribution of
     subset scores equal the per-subset kernel's (first acceptable subset in itertools order of
     the smallest size)."""
-    monkeypatch.setenv('KFMI_SEARCH_KERNEL', kernel)
     n = 11
     cand, ev, init, t0, target = _search_case(golden_dir, n)
-    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    kf = kfmi.BatchedKF('ref15', 1, 'f64', options={'search_kernel': kernel})
     _, _, _, sm = kf.search_combos(ev, init, t0, target, threshold=-1e30, exhaustive=True, subset_max=True)
     vals = np.sort(sm.cpu().numpy()[1:])
     thr = float(vals[int(q * (len(vals) - 1))]) + (1e-9 if q > 0 else -1.0)

@@ -126,26 +126,17 @@ def test_ref8_handle_rejects_ref15_only_entry_points():
 
 
 def _events_run(model, kernel, etype, dt, pay, x0, P0b, threshold=None, dtype='f64', records=True):
-    import os as _os
-    old = _os.environ.get('KFMI_EVENTS_KERNEL')
-    _os.environ['KFMI_EVENTS_KERNEL'] = kernel
-    try:
-        B = etype.shape[1]
-        kf = kfmi.BatchedKF(model, B, dtype)
-        npd = np.float64 if dtype == 'f64' else np.float32
-        kf.set_state(np.ascontiguousarray(x0.T, npd), np.ascontiguousarray(P0b.T, npd))
-        tr, ld, up, cv = kf.run_events(etype, dt, np.ascontiguousarray(pay, npd), updated=records, cov=records,
-                                       threshold=threshold)
-        x, Pb = kf.state()
-        out = [None if v is None else v.double().cpu().numpy() if v.is_floating_point() else v.cpu().numpy()
-               for v in (tr, ld, up, cv, x, Pb, kf.status())]
-        kf.close()
-        return out
-    finally:
-        if old is None:
-            del _os.environ['KFMI_EVENTS_KERNEL']
-        else:
-            _os.environ['KFMI_EVENTS_KERNEL'] = old
+    B = etype.shape[1]
+    kf = kfmi.BatchedKF(model, B, dtype, options={'events_kernel': kernel})
+    npd = np.float64 if dtype == 'f64' else np.float32
+    kf.set_state(np.ascontiguousarray(x0.T, npd), np.ascontiguousarray(P0b.T, npd))
+    tr, ld, up, cv = kf.run_events(etype, dt, np.ascontiguousarray(pay, npd), updated=records, cov=records,
+                                   threshold=threshold)
+    x, Pb = kf.state()
+    out = [None if v is None else v.double().cpu().numpy() if v.is_floating_point() else v.cpu().numpy()
+           for v in (tr, ld, up, cv, x, Pb, kf.status())]
+    kf.close()
+    return out
 
 
 @pytest.mark.parametrize('model', ['ref15', 'ref8'])
@@ -248,17 +239,10 @@ def test_ref15_fp32_events_vs_fp64_oracle(kernel):
     gps = etype == 0
     pay[:, 0:3] = np.where(gps[:, None, :], rng.normal(0, 3, (T, 3, B)), pay[:, 0:3])
     pay32 = pay.astype(np.float32)
-    old = _os.environ.get('KFMI_EVENTS_KERNEL')
-    _os.environ['KFMI_EVENTS_KERNEL'] = kernel
-    try:
-        kf = kfmi.BatchedKF('ref15', B, 'f32')
-        tr, ld, _, _ = kf.run_events(etype, dt, pay32)
-        tr, ld = tr.double().cpu().numpy(), ld.double().cpu().numpy()
-    finally:
-        if old is None:
-            del _os.environ['KFMI_EVENTS_KERNEL']
-        else:
-            _os.environ['KFMI_EVENTS_KERNEL'] = old
+    kf = kfmi.BatchedKF('ref15', B, 'f32', options={'events_kernel': kernel})
+    tr, ld, _, _ = kf.run_events(etype, dt, pay32)
+    tr, ld = tr.double().cpu().numpy(), ld.double().cpu().numpy()
+    kf.close()
     worst_x = worst_l = 0.0
     for f in range(0, B, 11):
         x, P = np.zeros(15), ref_kf.P0_REF15.copy()

@@ -76,17 +76,15 @@ def _parallel(et, dt, pay, x0, **kw):
 @pytest.mark.parametrize('final_pass', [False, True])
 @pytest.mark.parametrize('T,chunk,skips,warmup', [(60000, None, 0, None), (45001, 777, 50, None),
                                                   (5000, 256, 3, 2560), (30001, 300, 7, -3)])
-def test_parallel_equals_single_filter(T, chunk, skips, warmup, final_pass, monkeypatch):
+def test_parallel_equals_single_filter(T, chunk, skips, warmup, final_pass):
     """Records, final state and covariance equal the one-filter run, with the records taken
     from the map pass (default) or from a final pass over the true starts; the covariance
     warm-up by linear-fractional maps (default), by events (T = 5000: chunks whose warm-up
     reaches the stream start are exact) and by maps plus one chunk of events; ragged last
     chunk, NONE events."""
-    if final_pass:
-        monkeypatch.setenv('KFMI_STREAM_FINAL', '1')
     et, dt, pay, x0 = _stream(T, seed=T, skips=skips)
     seq = _sequential(et, dt, pay, x0)
-    par = _parallel(et, dt, pay, x0, chunk=chunk, warmup=warmup)
+    par = _parallel(et, dt, pay, x0, chunk=chunk, warmup=warmup, options={'stream_final': int(final_pass)})
     chk = ref15.parallel_check
     assert chk['ok'] and chk['chunks'] > 1, chk
     assert chk['cov_gap'] <= 1e-12  # the warm-up reached the covariance (to roundoff)
@@ -145,11 +143,9 @@ def test_nan_fix_falls_back():
 
 
 @pytest.mark.parametrize('final_pass', [False, True])
-def test_records_updated_cov_ref8(final_pass, monkeypatch):
+def test_records_updated_cov_ref8(final_pass):
     """Every record kf_run_events writes (traj, logdet, updated, covariance) and the 8-state
     model, through the C ABI route kf_run_events takes by itself for T >= 65536."""
-    if final_pass:
-        monkeypatch.setenv('KFMI_STREAM_FINAL', '1')
     T = 70000
     et, dt, pay, x0 = _stream(T, seed=13, skips=20)
     for model in ('ref15', 'ref8'):
@@ -157,7 +153,7 @@ def test_records_updated_cov_ref8(final_pass, monkeypatch):
         xs = np.zeros(n)
         xs[0:2] = x0[0:2]
         seq = _sequential(et, dt, pay, xs, model=model)
-        kf = kfmi.BatchedKF(model, 1, 'f64')
+        kf = kfmi.BatchedKF(model, 1, 'f64', options={'stream_final': int(final_pass)})
         kf.set_state(xs[:, None], kf.state()[1].double().cpu().numpy())
         tr, ld, up, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None], updated=True, cov=True)
         chk = kf.stream_check()

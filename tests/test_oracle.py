@@ -291,3 +291,17 @@ def test_hw5_2_facade_model_getters_match_the_oracle():
     np.testing.assert_array_equal(sf.calculate_kalman_gain(P, H, R), ref_kf.calculate_kalman_gain(P, H, R))
     F, Q = ref_kf.F_ref8(0.1), ref_kf.Q_ref8(0.1)
     np.testing.assert_array_equal(sf.predict_covariance(P, F, Q), ref_kf.predict_covariance(P, F, Q))
+
+
+def test_numpy_pool_runs_the_reference_loop_on_all_workers():
+    """bench.py's all-core NumPy baseline (oracle/numpy_pool.py): every worker runs its own
+    shard of filters through the reference-order loop and the rates add up."""
+    from oracle import numpy_pool
+    rng = np.random.default_rng(0)
+    T, nf = 16, 6
+    shards = [dict(d=3, x0=rng.normal(0, 100, (6, nf)), P0=ref_kf.CV3.P0(), R=None, dt=0.1, k=1, n=nf,
+                   u=rng.normal(0, 0.3, (T, 3, nf)), z=rng.normal(0, 30, (T, 3, nf))) for _ in range(2)]
+    out = numpy_pool.run('cv', shards, seconds=30.0)
+    assert out['cores'] == 2 and out['filters'] == 2 * nf and out['units'] == 2 * nf * T
+    assert out['value'] > 0
+    assert numpy_pool.split(10, 3) == [(0, 4), (4, 7), (7, 10)]

@@ -8,7 +8,7 @@ and alternates launches between the arms on the same handle and buffers.
 
 An arm is a library path (loaded side by side; valid while `kf_batch`'s layout is the same in
 both builds, i.e. for kernel-side changes), `default` (the in-tree libkfmi.so), or NAME=VALUE
-(the in-tree library with that environment setting, read by the C ABI at launch time).
+(the in-tree library with that kf_set_option on the workload's handle, kfmi.engine.OPTIONS).
 Prints the median kernel time per arm and the per-round times.
 """
 import argparse
@@ -52,6 +52,7 @@ def main():
                 fn.argtypes = argt
             arms.append((a, h, None))
     cfg = dict(bench.CONFIGS[args.config])
+    cfg['opts'] = {}
     ns = argparse.Namespace(ablate='none', gpus=1, no_cpu_baseline=True, rate_block=args.rate_block)
     if args.config in ('ref15', 'ref15f32'):
         w = bench.ref15_workload(cfg, ns, 0, 1, dev)
@@ -64,15 +65,16 @@ def main():
     else:
         w = bench.cv_workload(args.config, cfg, ns, 0, 1, dev)
     stream = torch.cuda.current_stream(dev)
-    env0 = dict(os.environ)
+    opt_names = {a[2][0] for a in arms if a[2]}
 
     def use(arm):
-        name, h, env = arm
+        name, h, opt = arm
         _lib._lib = h
-        for k in [k for k in os.environ if k.startswith('KFMI_') and k not in env0]:
-            del os.environ[k]
-        if env:
-            os.environ[env[0]] = env[1]
+        for k in opt_names:
+            w['kf'].set_option(k, 0)
+        if opt:
+            v = opt[1]
+            w['kf'].set_option(opt[0], int(v) if v.lstrip('-').isdigit() else v)
 
     times = {a[0]: [] for a in arms}
     for arm in arms:   # warm every arm once (module load, first-launch costs)

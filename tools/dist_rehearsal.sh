@@ -8,13 +8,13 @@ TAG=${1:-dist}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
-export TMPDIR=/tmp KFMI_BENCH_DIST_BACKEND=gloo
+export TMPDIR=/tmp
 cd "$ROOT"
 for cfg in 3 ref15; do
   for n in 2 4; do
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
       --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --steps 3 --warmup 1 \
-      --config $cfg --batch 262144 > "$OUT/c${cfg}_n$n.log" 2>&1
+      --config $cfg --batch 262144 --dist-backend gloo > "$OUT/c${cfg}_n$n.log" 2>&1
     rc=$?
     echo "config $cfg n=$n rc=$rc" | tee -a "$OUT/steps.txt"
     grep '^{"metric"' "$OUT/c${cfg}_n$n.log" | tail -1 >> "$OUT/lines.jsonl" || true

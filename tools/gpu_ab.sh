@@ -1,8 +1,8 @@
 #!/bin/bash
 # A/B bench sweep on the GPU box:  gpurun -- bash tools/gpu_ab.sh TAG "LIB1 LIB2 ..." "CFG1 CFG2 ..."
 # Runs bench.py for each (library, config) pair, interleaved over ROUNDS rounds, one line each.
-# A LIB entry of the form NAME=VALUE is an environment setting for the default library instead
-# (e.g. "KFMI_CV_KERNEL=general KFMI_CV_KERNEL=auto").
+# A LIB entry of the form NAME=VALUE is a handle option of the default library instead
+# (bench.py --opt, e.g. "cv_kernel=general cv_kernel=auto").
 set -u
 TAG=$1; LIBS=$2; CFGS=$3; ROUNDS=${ROUNDS:-2}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -12,7 +12,7 @@ for r in $(seq 1 "$ROUNDS"); do
   for lib in $LIBS; do
     for c in $CFGS; do
       if [[ "$lib" == *=* ]]; then
-        env "$lib" timeout -k 10 300 python bench.py --config "$c" --steps 20 --warmup 10 --no-cpu-baseline > "$OUT/tmp.json" 2> "$OUT/err_${c}.log"
+        timeout -k 10 300 python bench.py --opt "$lib" --config "$c" --steps 20 --warmup 10 --no-cpu-baseline > "$OUT/tmp.json" 2> "$OUT/err_${c}.log"
       else
         KFMI_LIB=$lib timeout -k 10 300 python bench.py --config "$c" --steps 20 --warmup 10 --no-cpu-baseline > "$OUT/tmp.json" 2> "$OUT/err_${c}.log"
       fi
