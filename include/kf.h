@@ -58,9 +58,9 @@ extern "C" {
 #define KF_MODEL_CV3 3
 
 /* The reference's own 15-state GPS+IMU model (kf_workers.py:493-614): state
- * [pos(3), att(3), vel(3), rate(3), acc(3)], GPS fix m=3, IMU pseudo-measurement m=15, all
- * constants as in the reference (kf_params must be NULL).  Every covariance reachable from the
- * reference's diagonal P0 is exactly block-diagonal over the axis chains (pos,vel,acc) and
+ * [pos(3), att(3), vel(3), rate(3), acc(3)], GPS fix m=3, IMU pseudo-measurement m=15, the
+ * reference's constants (kf_params NULL) or a caller's diagonal ones (kf_params.ref_*).  Every
+ * covariance reachable from a diagonal P0 is exactly block-diagonal over the axis chains (pos,vel,acc) and
  * (att,rate), so the handle stores P as 27 block-packed rows ([27][B]):
  *   rows 6i..6i+5   axis i (pos_i, vel_i, acc_i) upper triangle (pp pv pa vv va aa)
  *   rows 18+3i..+2  axis i (att_i, rate_i) upper triangle (tt tw ww)
@@ -82,13 +82,24 @@ extern "C" {
 #define KF_EVENT_PREDICT 2    /* predict only (the worker's final propagation)            */
 #define KF_EVENT_NONE    255  /* no event: state unchanged (padding of ragged streams)    */
 
-/* Model constants; kf_default_params() fills the reference's values. */
+/* Model constants; kf_default_params() fills the reference's values.
+ * KF_MODEL_CV2 / CV3 read q_pos .. p0_vel; KF_MODEL_REF15 / REF8 read the ref_* arrays: diagonal
+ * Q rates, R_imu, R_gps and P0 per state, in the model's state order (REF8: the first 8 / 2
+ * entries).  Diagonal constants keep every covariance block-diagonal over the axis chains, which
+ * the handle's block-packed P requires.  The reference's getters hard-code them
+ * (kf_workers.py:519-614, P0 :651; hw5_2.py:233-304, P0 :317-326) and its class_args dict of
+ * callables lets a caller replace them (kf_workers.py:1242-1251).  A handle whose constants
+ * equal the reference's runs the kernels compiled with the reference's literals. */
 typedef struct kf_params {
     double q_pos;   /* Q = diag(q_pos*dt I, q_vel*dt I): 5, 1   (kf_workers.py:521,523)        */
     double q_vel;
     double r[9];    /* R, m x m row-major, symmetric: 3 I       (kf_workers.py:581-585)        */
     double p0_pos;  /* initial P = diag(p0_pos I, p0_vel I): CV3 1e4/1e3 (kf_workers.py:651), */
     double p0_vel;  /*                                         CV2 1000/100 (hw5_2.py:317-326) */
+    double ref_q[15];      /* Q = diag(ref_q * dt), >= 0                                         */
+    double ref_r_imu[15];  /* R_imu = diag(ref_r_imu), > 0                                       */
+    double ref_r_gps[3];   /* R_gps = diag(ref_r_gps), > 0                                       */
+    double ref_p0[15];     /* P0 = diag(ref_p0), > 0 (kf_reset / kf_alloc)                      */
 } kf_params;
 
 typedef struct kf_batch kf_batch;
@@ -139,9 +150,9 @@ int kf_get_option(const kf_batch* handle, int option, int64_t* value);
 /* Thread-local description of the last failure on this thread ("" if none). */
 const char* kf_last_error(void);
 
-/* Reference constants for a model.  Replaces the hard-coded getters
- * get_process_noise_covariance_matrix / get_gps_measurement_noise_covariance_matrix
- * (kf_workers.py:519-544, 581-585) and the P0 literal (kf_workers.py:651). */
+/* Reference constants for a model (every model; the ref_* arrays for REF15 / REF8).  Replaces the
+ * hard-coded getters get_process_noise_covariance_matrix / get_*_measurement_noise_covariance_matrix
+ * (kf_workers.py:519-614, hw5_2.py:233-304) and the P0 literals (kf_workers.py:651, hw5_2.py:317-326). */
 int kf_default_params(int model, kf_params* out);
 
 /* Number of visible HIP devices (0 on a host without a GPU). */
@@ -152,7 +163,8 @@ int kf_device_count(int* count);
 int kf_init(int device);
 
 /* Create a handle for `batch` filters of `model` in `dtype` on the current device, with
- * x = 0, P = P0, status = KF_OK.  params may be NULL (reference constants).
+ * x = 0, P = P0, status = KF_OK.  params may be NULL (reference constants); KF_EINVAL for a
+ * negative or non-finite Q rate or a non-positive R or P0 entry of a reference model.
  * Replaces KF_SensorFusion.__init__ + the per-run initial state (kf_workers.py:641-651). */
 int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_params* params);
 int kf_free(kf_batch* handle);
@@ -333,6 +345,15 @@ int kf_search_combos(kf_batch* handle, int n_events, const double* events, const
  * device [n_types][27][B] block-packed posterior covariances (Scheduler.cov_matrix), or NULL. */
 int kf_score_candidates(kf_batch* handle, int n_types, const int32_t* types, int full, void* gain,
                         void* post, void* stream);
+
+/* KF_MODEL_REF15 Scheduler.cov_matrix for any measurement rows S (kf_workers.py:112-147: H_hat =
+ * H[S], R_hat = R[S, S]): candidate c is sensor types[c] (KF_EVENT_GPS | KF_EVENT_IMU) with the rows
+ * of row_masks[c] (host, bit i = 1-based row i + 1 of that sensor's H: GPS rows 1..3 = pos x, y, z;
+ * IMU rows 1..15 = the 15 states; non-zero).  gain device [n_cand][B] = trace of the posterior,
+ * post device [n_cand][27][B] the block-packed posterior (nullable).  R is the handle's (diagonal)
+ * R_gps / R_imu, so the rows are independent and each chain takes its own.  n_cand <= 16. */
+int kf_score_rows(kf_batch* handle, int n_cand, const int32_t* types, const uint32_t* row_masks, void* gain,
+                  void* post, void* stream);
 
 /* KF_MODEL_REF15 rate-decimated greedy filter (run_kalman_filter_scheduled with
  * selection_method='greedy', kf_workers.py:826-957), per filter in one launch.  Streams:

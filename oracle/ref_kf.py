@@ -236,18 +236,31 @@ def imu_pseudo_measurement8(x_pred, sdata, dt):
     return [X, Y, theta, Vx, Vy, theta_dot, ax, ay]
 
 
-def step15(x, P, stype, sdata, dt):
-    """One event of ``run_kalman_filter_full`` (kf_workers.py:688-711)."""
+def consts_matrices(K, n):
+    """Custom diagonal constants K = dict(q, r_imu, r_gps, p0) per state (the class_args override
+    of the model getters, kf_workers.py:1242-1251) -> (Q(dt), R_gps, R_imu, P0)."""
+    q = np.asarray(K['q'], np.float64)[:n]
+    return (lambda dt: np.diag(q * dt)), np.diag(np.asarray(K['r_gps'], np.float64)), \
+        np.diag(np.asarray(K['r_imu'], np.float64)[:n]), np.diag(np.asarray(K['p0'], np.float64)[:n])
+
+
+def step15(x, P, stype, sdata, dt, K=None):
+    """One event of ``run_kalman_filter_full`` (kf_workers.py:688-711); K: custom diagonal
+    constants (consts_matrices) instead of the reference's getters."""
     F = F_ref15(dt)
-    Qt = Q_ref15(dt)
+    if K is None:
+        Qt, Rg, Ri = Q_ref15(dt), R_gps15(), R_imu15()
+    else:
+        Qf, Rg, Ri, _ = consts_matrices(K, 15)
+        Qt = Qf(dt)
     x = np.dot(F, x)
     P = predict_covariance(P, F, Qt)
     if stype == 'GPS':
-        H, R = H_gps15(), R_gps15()
+        H, R = H_gps15(), Rg
         Z = [sdata['easting'], sdata['northing'], sdata['altitude']]
     else:
         Z = imu_pseudo_measurement15(x, sdata, dt)
-        H, R = H_imu15(), R_imu15()
+        H, R = H_imu15(), Ri
     return update(x, P, H, R, Z)
 
 
@@ -255,7 +268,7 @@ def step15(x, P, stype, sdata, dt):
 # Reference drivers (event-list form, same tuple layout as the reference)
 # --------------------------------------------------------------------------------------
 
-def run_kalman_filter_full(events, start_idx=0, end_idx=None, initial_pt=None, initial_state=None):
+def run_kalman_filter_full(events, start_idx=0, end_idx=None, initial_pt=None, initial_state=None, K=None):
     """kf_workers.py:623-728. ``events`` = [(idx, 'GPS'|'IMU', t, payload), ...] as built by
     ``combine_sensor_data`` (kf_workers.py:375-385). Returns (states, logdets, P, prev_time)."""
     if end_idx is None or end_idx > len(events):
@@ -267,7 +280,7 @@ def run_kalman_filter_full(events, start_idx=0, end_idx=None, initial_pt=None, i
         prev_time = initial_state[0]
         start_off = start_idx
     else:
-        Pt = P0_REF15.copy()
+        Pt = P0_REF15.copy() if K is None else consts_matrices(K, 15)[3]
         start_off = -1
         prev_time = None
         for i, (_, stype, t, sdata) in enumerate(events[start_idx:end_idx + 1]):
@@ -288,7 +301,7 @@ def run_kalman_filter_full(events, start_idx=0, end_idx=None, initial_pt=None, i
         if dt < 0:  # kf_workers.py:683-685
             prev_time = t
             continue
-        xt, Pt = step15(xt, Pt, stype, sdata, dt)
+        xt, Pt = step15(xt, Pt, stype, sdata, dt, K)
         states.append((t, *xt[:6]))
         logdets.append(np.linalg.slogdet(Pt)[1])
         prev_time = t
@@ -362,8 +375,8 @@ def run_no_update(events, start_idx=None, end_idx=None, initial_pt=None, initial
     return states, logdets, Pt, prev, mtimes
 
 
-def evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time):
-    """kf_workers.py:22-97 with the 15-state class_args bound in.
+def evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time, K=None):
+    """kf_workers.py:22-97 with the 15-state class_args bound in (K: custom diagonal constants).
 
     Returns [(0, traj, combo, x_final, None, log_det, k), ...]."""
     results = []
@@ -378,7 +391,7 @@ def evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time):
             dt = t - cur
             if dt < 0:
                 continue
-            x, P = step15(x, P, stype, sdata, dt)
+            x, P = step15(x, P, stype, sdata, dt, K)
             traj.append((t, *x[:6]))
             cur = t
             s, l = np.linalg.slogdet(P)
@@ -387,7 +400,7 @@ def evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time):
             dt = target_end_time - cur
             F = F_ref15(dt)
             x = np.dot(F, x)
-            P = predict_covariance(P, F, Q_ref15(dt))
+            P = predict_covariance(P, F, Q_ref15(dt) if K is None else consts_matrices(K, 15)[0](dt))
             traj.append((target_end_time, *x[:6]))
             s, l = np.linalg.slogdet(P)
             log_det.append(s * l)
@@ -449,14 +462,19 @@ def run_adaptive_threshold(events, start_idx=0, end_idx=None, R_threshold=-np.in
     return states, logdets, Pt, prev, times
 
 
-def step8(x, P, stype, sdata, dt):
-    """One event of hw5_2.run_kalman_filter (hw5_2.py:336-366)."""
+def step8(x, P, stype, sdata, dt, K=None):
+    """One event of hw5_2.run_kalman_filter (hw5_2.py:336-366); K: custom diagonal constants."""
     I = np.eye(8)
     F = F_ref8(dt)
     x = np.dot(F, x)
-    P = predict_covariance(P, F, Q_ref8(dt))
+    if K is None:
+        Qt, Rg, Ri = Q_ref8(dt), R_gps8(), R_imu8()
+    else:
+        Qf, Rg, Ri, _ = consts_matrices(K, 8)
+        Qt = Qf(dt)
+    P = predict_covariance(P, F, Qt)
     if stype == 'GPS':
-        H, R = H_gps8(), R_gps8()
+        H, R = H_gps8(), Rg
         Z = [sdata['easting'], sdata['northing']]
         K = calculate_kalman_gain(P, H, R)
         y = Z - np.dot(H, x)
@@ -464,7 +482,7 @@ def step8(x, P, stype, sdata, dt):
         P = np.dot(I - np.dot(K, H), P)
     elif stype == 'IMU':
         Z = imu_pseudo_measurement8(x, sdata, dt)
-        H, R = H_imu8(), R_imu8()
+        H, R = H_imu8(), Ri
         K = calculate_kalman_gain(P, H, R)
         y = np.array(Z) - np.dot(H, x)
         x = x + np.dot(K, y)
@@ -636,25 +654,26 @@ def scheduler_cov_matrix(S, Sigma_prev, R, H):
     return Sigma_prev - np.dot(np.dot(K, H_hat), Sigma_prev)
 
 
-def scheduler_gain(stype, Sigma):
+def scheduler_gain(stype, Sigma, K=None):
     """Scheduler.gain (kf_workers.py:174-185): trace of cov_matrix(S=[1]) for the sensor."""
+    Rg, Ri = (R_gps15(), R_imu15()) if K is None else consts_matrices(K, 15)[1:3]
     if stype == 'GPS':
-        return np.trace(scheduler_cov_matrix([1], Sigma, R_gps15(), H_gps15()))
-    return np.trace(scheduler_cov_matrix([1], Sigma, R_imu15(), H_imu15()))
+        return np.trace(scheduler_cov_matrix([1], Sigma, Rg, H_gps15()))
+    return np.trace(scheduler_cov_matrix([1], Sigma, Ri, H_imu15()))
 
 
-def greedy_schedule(queue, Sigma):
+def greedy_schedule(queue, Sigma, K=None):
     """Scheduler.greedy_schedule (kf_workers.py:195-213): first candidate with the largest gain."""
     best, best_i = -np.inf, None
     for i, (_, stype, _, _) in enumerate(queue):
-        g = scheduler_gain(stype, Sigma)
+        g = scheduler_gain(stype, Sigma, K)
         if g > best:
             best, best_i = g, i
     return best_i
 
 
 def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt=None, initial_state=None,
-                                selection_method=None, processing_frequency=None, rng_choice=None):
+                                selection_method=None, processing_frequency=None, rng_choice=None, K=None):
     """kf_workers.py:826-957: events whose time is within 1/f of the last processed one are
     queued; the next event past the window triggers a selection from the queue (random or
     greedy), then one predict over the accumulated dt and one update on the selection.  The
@@ -674,7 +693,7 @@ def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt
         start_off = start_idx
         prev = initial_state[0]
     else:
-        Pt = P0_REF15.copy()
+        Pt = P0_REF15.copy() if K is None else consts_matrices(K, 15)[3]
         prev, start_off = None, 0
         for i, (_, stype, t, sdata) in enumerate(events[start_idx:end_idx]):
             if stype == 'GPS':
@@ -698,11 +717,11 @@ def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt
         if selection_method == 'random':
             sel = choice(len(queue))
         else:
-            sel = greedy_schedule(queue, Pt)
+            sel = greedy_schedule(queue, Pt, K)
         (_, s_type, s_t, s_data) = queue[sel]
         queue = []
         dt = s_t - prev
-        xt, Pt = step15(xt, Pt, s_type, s_data, dt)
+        xt, Pt = step15(xt, Pt, s_type, s_data, dt, K)
         states.append((s_t, *xt[:6]))
         logdets.append(np.linalg.slogdet(Pt)[1])
         prev = s_t

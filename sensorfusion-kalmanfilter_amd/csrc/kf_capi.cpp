@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <climits>
 #include <cstdarg>
 #include <cstdlib>
@@ -48,6 +49,9 @@ struct kf_batch {
     bool pend_evt;           // pend_done marks that read (false: it was captured into a graph)
     bool last_predict;       // the handle's last state call was kf_predict
     int64_t opt[KF_OPT_COUNT];  // kf_set_option values (0 = the library's choice)
+    // reference models: the caller's noise constants on the device when they differ from the
+    // reference's (kf_params.ref_*), else nullptr and the kernels built on the reference's literals
+    kfmi::RefConsts* kc;
 };
 
 namespace {
@@ -199,7 +203,28 @@ kfmi::RefArgs ref_args(const kf_batch* h) {
     a.x = h->x;
     a.P = h->P;
     a.status = h->status;
+    a.kc = h->kc;
     return a;
+}
+
+// The reference's diagonal noise constants per state (kf_workers.py:519-614, P0 :651;
+// hw5_2.py:233-304, P0 :317-326), by state group: pos, att, vel, rate, acc.
+void ref_default_consts(int model, kf_params* p) {
+    static const double q[5] = {5.0, 0.05, 1.0, 0.1, 2.0};
+    static const double r[5] = {50.0, 0.05, 10.0, 0.1, 100.0};
+    static const int g15[15] = {0, 0, 0, 1, 1, 1, 2, 2, 2, 3, 3, 3, 4, 4, 4};
+    static const int g8[8] = {0, 0, 1, 2, 2, 3, 4, 4};  // x, y, theta, vx, vy, theta_dot, ax, ay
+    const bool m15 = model == KF_MODEL_REF15;
+    const int n = m15 ? 15 : 8;
+    static const double p15[5] = {10000.0, 1000.0, 1000.0, 1000.0, 10000.0};
+    static const double p8[5] = {1000.0, 100.0, 100.0, 100.0, 1000.0};
+    for (int i = 0; i < n; ++i) {
+        const int g = m15 ? g15[i] : g8[i];
+        p->ref_q[i] = q[g];
+        p->ref_r_imu[i] = r[g];
+        p->ref_p0[i] = m15 ? p15[g] : p8[g];
+    }
+    for (int i = 0; i < (m15 ? 3 : 2); ++i) p->ref_r_gps[i] = 3.0;
 }
 
 // KF_OPT_PREDICT = 1 turns the deferral off (tests, A/B)
@@ -297,9 +322,12 @@ const char* kf_last_error(void) { return g_err.c_str(); }
 int kf_default_params(int model, kf_params* out) {
     const int d = model_axes(model);
     if (!d) return fail(KF_EINVAL, "unknown model %d", model);
-    if (is_ref(model)) return fail(KF_EINVAL, "the reference models use the reference constants; no kf_params");
     if (!out) return fail(KF_EINVAL, "null params");
     std::memset(out, 0, sizeof *out);
+    if (is_ref(model)) {
+        ref_default_consts(model, out);
+        return KF_OK;
+    }
     out->q_pos = 5.0;  // position_noise = 5 * dt   (kf_workers.py:521)
     out->q_vel = 1.0;  // velocity_noise = 1 * dt   (kf_workers.py:523)
     for (int i = 0; i < d; ++i) out->r[i * d + i] = 3.0;  // gps variance 3 (kf_workers.py:583)
@@ -344,7 +372,27 @@ int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_pa
     if (batch < 0) return fail(KF_EINVAL, "negative batch %lld", static_cast<long long>(batch));
     if (batch * 8 >= (int64_t(1) << 31))
         return fail(KF_EINVAL, "batch %lld too large (one [B] row must stay below 2 GiB)", static_cast<long long>(batch));
-    if (is_ref(model) && params) return fail(KF_EINVAL, "model %d takes no kf_params (reference constants)", model);
+    const int nref = model == KF_MODEL_REF15 ? 15 : 8, ngps = model == KF_MODEL_REF15 ? 3 : 2;
+    bool custom = false;
+    if (is_ref(model) && params) {
+        kf_params ref{};
+        ref_default_consts(model, &ref);
+        for (int i = 0; i < nref; ++i) {
+            if (!(params->ref_q[i] >= 0.0) || !std::isfinite(params->ref_q[i]))
+                return fail(KF_EINVAL, "kf_alloc: ref_q[%d] = %g (need a finite rate >= 0)", i, params->ref_q[i]);
+            if (!(params->ref_r_imu[i] > 0.0) || !std::isfinite(params->ref_r_imu[i]))
+                return fail(KF_EINVAL, "kf_alloc: ref_r_imu[%d] = %g (need a finite variance > 0)", i, params->ref_r_imu[i]);
+            if (!(params->ref_p0[i] > 0.0) || !std::isfinite(params->ref_p0[i]))
+                return fail(KF_EINVAL, "kf_alloc: ref_p0[%d] = %g (need a finite variance > 0)", i, params->ref_p0[i]);
+            custom = custom || params->ref_q[i] != ref.ref_q[i] || params->ref_r_imu[i] != ref.ref_r_imu[i] ||
+                     params->ref_p0[i] != ref.ref_p0[i];
+        }
+        for (int i = 0; i < ngps; ++i) {
+            if (!(params->ref_r_gps[i] > 0.0) || !std::isfinite(params->ref_r_gps[i]))
+                return fail(KF_EINVAL, "kf_alloc: ref_r_gps[%d] = %g (need a finite variance > 0)", i, params->ref_r_gps[i]);
+            custom = custom || params->ref_r_gps[i] != ref.ref_r_gps[i];
+        }
+    }
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return fail(KF_ENODEV, "no current HIP device: %s", hipGetErrorString(e));
@@ -358,11 +406,8 @@ int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_pa
     h->dtype = dtype;
     h->B = batch;
     h->device = dev;
-    if (params) {
-        h->params = *params;
-    } else if (!is_ref(model)) {
-        kf_default_params(model, &h->params);
-    }
+    if (params) h->params = *params;
+    else kf_default_params(model, &h->params);
     h->r_diag = true;
     for (int i = 0; i < h->m; ++i)
         for (int j = 0; j < h->m; ++j)
@@ -392,6 +437,21 @@ int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_pa
         kf_free(h);
         return fail(KF_ENOMEM, "hipMalloc of the combination workspace failed");
     }
+    if (custom) {  // the caller's constants, read by the kernels compiled for them
+        kfmi::RefConsts k{};
+        for (int i = 0; i < nref; ++i) {
+            k.q[i] = params->ref_q[i];
+            k.r_imu[i] = params->ref_r_imu[i];
+            k.p0[i] = params->ref_p0[i];
+        }
+        for (int i = 0; i < ngps; ++i) k.r_gps[i] = params->ref_r_gps[i];
+        if (hipMalloc(reinterpret_cast<void**>(&h->kc), sizeof k) != hipSuccess ||
+            hipMemcpy(h->kc, &k, sizeof k, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipGetLastError();
+            kf_free(h);
+            return fail(KF_ENOMEM, "kf_alloc: device copy of the noise constants failed");
+        }
+    }
     int rc = kf_reset(h, nullptr, nullptr);
     if (rc == KF_OK && nb) {
         e = hipStreamSynchronize(nullptr);
@@ -416,6 +476,7 @@ int kf_free(kf_batch* h) {
     if (h->stream_ws) (void)hipFree(h->stream_ws);
     if (h->pend_u) (void)hipFree(h->pend_u);
     if (h->pend_done) (void)hipEventDestroy(h->pend_done);
+    if (h->kc) (void)hipFree(h->kc);
     delete h;
     return KF_OK;
 }
@@ -781,6 +842,7 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     sa.tol_state = h->dtype == KF_F64 ? 1e-9 : 1e-4;
     sa.tol_cov = h->dtype == KF_F64 ? 1e-12 : 1e-5;
     sa.start_threads = int(opt(h, KF_OPT_START_THREADS));
+    sa.kc = h->kc;
     sa.hx = h->x;
     sa.hP = h->P;
     sa.hstatus = h->status;
@@ -832,6 +894,7 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
                      void* traj_rec = nullptr, int nvar = 1, int nv = 1) {
         kfmi::RefArgs a{};
         a.B = B;
+        a.kc = h->kc;
         a.T = int(Tc);
         a.etype = etype;
         a.dt = dt;
@@ -938,6 +1001,7 @@ int kf_eval_combos(kf_batch* h, int n_events, const double* events, const double
     char* ws = static_cast<char*>(h->ws);
     kfmi::Ref15ComboArgs a{};
     a.B = h->B;
+    a.kc = h->kc;
     a.n_events = n_events;
     a.k = k;
     a.combo_offset = combo_offset;
@@ -1014,6 +1078,7 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
     int found = 0, last = 0;
     for (int k = 1; k <= kf_max; ++k) {
         kfmi::Ref15SearchArgs a{};
+        a.kc = h->kc;
         a.n_events = n;
         a.k = k;
         a.shift = n_fixed;
@@ -1073,6 +1138,7 @@ int kf_score_candidates(kf_batch* h, int n_types, const int32_t* types, int full
     if (h->B == 0) return KF_OK;
     kfmi::Ref15ScoreArgs a{};
     a.B = h->B;
+    a.kc = h->kc;
     a.n_types = n_types;
     a.full = full;
     for (int i = 0; i < n_types; ++i) {
@@ -1088,6 +1154,37 @@ int kf_score_candidates(kf_batch* h, int n_types, const int32_t* types, int full
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_score_candidates");
 }
 
+int kf_score_rows(kf_batch* h, int n_cand, const int32_t* types, const uint32_t* row_masks, void* gain, void* post,
+                  void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (!is_ref15(h)) return fail(KF_EINVAL, "kf_score_rows: needs a KF_MODEL_REF15 handle");
+    if (n_cand < 1 || n_cand > 16) return fail(KF_EINVAL, "kf_score_rows: n_cand = %d outside [1, 16]", n_cand);
+    if (!types || !row_masks || !gain) return fail(KF_EINVAL, "kf_score_rows: null types/row_masks/gain");
+    kfmi::Ref15ScoreArgs a{};
+    a.B = h->B;
+    a.kc = h->kc;
+    a.n_types = n_cand;
+    a.rows = 1;
+    for (int i = 0; i < n_cand; ++i) {
+        const bool gps = types[i] == KF_EVENT_GPS;
+        if (!gps && types[i] != KF_EVENT_IMU)
+            return fail(KF_EINVAL, "kf_score_rows: candidate %d has type %d (GPS=0 or IMU=1)", i, types[i]);
+        const uint32_t rows = gps ? 3u : 15u;
+        if (row_masks[i] == 0 || (row_masks[i] >> rows) != 0)
+            return fail(KF_EINVAL, "kf_score_rows: candidate %d row mask 0x%x is empty or names a row beyond %u", i,
+                        row_masks[i], rows);
+        a.types[i] = static_cast<int8_t>(types[i]);
+        a.masks[i] = row_masks[i];
+    }
+    if (h->B == 0) return KF_OK;
+    a.x = h->x;
+    a.P = h->P;
+    a.gain = gain;
+    a.post = post;
+    hipError_t e = kfmi::launch_ref15_score(h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? KF_OK : hip_fail(e, "kf_score_rows");
+}
+
 int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, const void* payload,
                      const double* prev_time, const double* freq, double freq_all, void* traj, void* logdet,
                      double* sel_time, int32_t* n_sel, void* stream) {
@@ -1099,6 +1196,7 @@ int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, 
     if (!t || !etype || !payload || !prev_time) return fail(KF_EINVAL, "kf_run_scheduled: null input stream");
     kfmi::Ref15SchedArgs a{};
     a.B = h->B;
+    a.kc = h->kc;
     a.T = T;
     a.t = t;
     a.etype = etype;

@@ -46,6 +46,18 @@ struct SynthArgs {
 
 struct StreamCheck;
 
+// A reference-model handle's noise constants when the caller set its own (kf_params): diagonal,
+// per state in the model's state order (REF8 uses the first 8 / 2 entries).  Q = diag(q dt)
+// (kf_workers.py:519-544), R_imu = diag(r_imu) (:587-614), R_gps = diag(r_gps) (:581-585),
+// P0 = diag(p0) (:651).  Kernels read them through a device pointer (kc below); kc = nullptr
+// selects the kernels compiled with the reference's constants.
+struct RefConsts {
+    double q[15];
+    double r_imu[15];
+    double r_gps[3];
+    double p0[15];
+};
+
 // Reference chain models on per-filter event streams: KF_MODEL_REF15 (kf_workers.py:493-614,
 // N = 15, NBLK = 27, NTRAJ = 6) and KF_MODEL_REF8 (hw5_2.py:219-311, N = 8, NBLK = 15, NTRAJ = 3).
 // Event codes in etype: 0 GPS fix, 1 IMU sample, 2 predict only, 255 no event (padding).
@@ -77,6 +89,7 @@ struct RefArgs {
     int s_nvar;              // > 1: trajectory records per variant (filter / s_nchunks), s_vstride rows apart
     int64_t s_vstride;
     const int32_t* skip;     // if non-null and *skip != 0, the launch does nothing
+    const RefConsts* kc;     // the handle's own noise constants (device), or nullptr: the reference's
     // the map pass of kf_run_stream (4 state variants per filter): its epilogue writes each
     // chunk's affine state map per chain, [C][chains][12] = A (3x3 row-major), b, from the
     // variants' end states (their starts differ by s_delta on one chain component), and checks
@@ -132,6 +145,7 @@ struct StreamArgs {
     int64_t G;               // chunks per block of the start kernel (their windows' maps staged in LDS)
     int64_t g;               // chunks per thread of the start kernel; 0: no LDS, one chunk per thread
     int start_threads;       // threads per block of the start kernel (KF_OPT_START_THREADS); 0 = kBlock
+    const RefConsts* kc;     // the handle's noise constants, or nullptr (the reference's)
     // records from the map pass (no final pass): the map bank's trajectories per variant
     const void* traj4;       // [4][vstride][NTRAJ]
     int64_t vstride;
@@ -173,6 +187,7 @@ struct Ref15ComboArgs {
     void* logdets;           // [k+2][B] record list (NaN-padded) or nullptr
     void* max_logdet;        // [B] or nullptr
     int32_t* n_records;      // [B] or nullptr
+    const RefConsts* kc;     // the handle's noise constants, or nullptr (the reference's)
 };
 
 // Brute-force search with shared prefixes (kf_search_combos): the filter of a k-subset S is its
@@ -214,6 +229,7 @@ struct Ref15SearchArgs {
     uint64_t gitem[66];
     uint64_t gblk[66];
     bool pm_regs;            // parent-major: the parent's covariance in registers, not LDS (KF_OPT_SEARCH_PM)
+    const RefConsts* kc;     // the handle's noise constants, or nullptr (the reference's)
 };
 
 constexpr int kSearchRows = 28;  // T rows of a search node
@@ -234,6 +250,9 @@ struct Ref15ScoreArgs {
     const void* P;
     void* gain;              // [n_types][B]
     void* post;              // [n_types][27][B] posterior covariance blocks, or nullptr
+    const RefConsts* kc;     // the handle's noise constants, or nullptr (the reference's)
+    int rows;                // 1: candidate c updates with the measurement rows masks[c] (kf_score_rows)
+    uint32_t masks[16];      //    bit i = row i + 1 of the sensor's H (Scheduler.cov_matrix's S)
 };
 
 // Rate-decimated greedy driver (run_kalman_filter_scheduled, kf_workers.py:826-957), per filter.
@@ -254,6 +273,7 @@ struct Ref15SchedArgs {
     double* sel_time;        // [T][B]
     int32_t* n_sel;          // [B]
     bool regs;               // the register-input kernel even where the LDS one is legal (KF_OPT_SCHED_KERNEL)
+    const RefConsts* kc;     // the handle's noise constants, or nullptr (the reference's)
 };
 
 enum class Op { Run, Predict, Update, Step, Reset };  // Step: predict + update (kf_capi's deferral)

@@ -66,11 +66,52 @@ struct M8 {
                             P0Acc = 1000.0;  // hw5_2.py:317-326
 };
 
-template <typename T, class M>
+// Noise constants of a chain.  CUSTOM = false: the reference's, compile-time literals (the
+// default, and the code every bench row runs); CUSTOM = true: a caller's diagonal Q rates, R_imu,
+// R_gps and P0 per state (kf_params -> RefConsts, the handle's device copy at kc), read by
+// wave-uniform scalar loads.  Both give Chains the same operations in the same order.
+template <bool CUSTOM, class M, typename T>
+__device__ __forceinline__ void pva_noise(const RefConsts* kc, int c, T (&q)[3], T (&r)[6], T& rg) {
+    if constexpr (CUSTOM) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) q[k] = T(kc->q[M::pva(c, k)]);
+        r[0] = T(kc->r_imu[M::pva(c, 0)]);
+        r[3] = T(kc->r_imu[M::pva(c, 1)]);
+        r[5] = T(kc->r_imu[M::pva(c, 2)]);
+        rg = T(kc->r_gps[c]);
+    } else {
+        q[0] = T(kQPos);
+        q[1] = T(kQVel);
+        q[2] = T(kQAcc);
+        r[0] = T(kRPos);
+        r[3] = T(kRVel);
+        r[5] = T(kRAcc);
+        rg = T(kRGps);
+    }
+    r[1] = r[2] = r[4] = T(0);
+}
+template <bool CUSTOM, class M, typename T>
+__device__ __forceinline__ void aw_noise(const RefConsts* kc, int c, T (&q)[2], T (&r)[3]) {
+    if constexpr (CUSTOM) {
+        q[0] = T(kc->q[M::aw(c, 0)]);
+        q[1] = T(kc->q[M::aw(c, 1)]);
+        r[0] = T(kc->r_imu[M::aw(c, 0)]);
+        r[2] = T(kc->r_imu[M::aw(c, 1)]);
+    } else {
+        q[0] = T(kQAtt);
+        q[1] = T(kQRate);
+        r[0] = T(kRAtt);
+        r[2] = T(kRRate);
+    }
+    r[1] = T(0);
+}
+
+template <typename T, class M, bool CUSTOM = false>
 struct Chains {
     T x[M::N];
     T pva[M::NP][6];  // per chain: (pos, vel, acc) packed upper 3x3
     T aw[M::NA][3];   // per chain: (att, rate) packed upper 2x2
+    const RefConsts* kc = nullptr;  // CUSTOM: the noise constants (kf_params)
     // Chain predict x = F x, P = F P F^T + Q for a block whose F row i is
     // e_i + dt e_{i+1} + dt^2/2 e_{i+2} (kf_workers.py:500-516).
     template <int NB>
@@ -114,10 +155,10 @@ struct Chains {
     }
 
     __device__ __forceinline__ void predict(T dt) {
-        const T qpva[3] = {T(kQPos), T(kQVel), T(kQAcc)};
-        const T qaw[2] = {T(kQAtt), T(kQRate)};
 #pragma unroll
         for (int c = 0; c < M::NP; ++c) {
+            T qpva[3], r[6], rg;
+            pva_noise<CUSTOM, M>(kc, c, qpva, r, rg);
             T xb[3];
             get_pva(c, xb);
             chain_predict<3>(xb, pva[c], dt, qpva);
@@ -125,6 +166,8 @@ struct Chains {
         }
 #pragma unroll
         for (int c = 0; c < M::NA; ++c) {
+            T qaw[2], r[3];
+            aw_noise<CUSTOM, M>(kc, c, qaw, r);
             T xa[2];
             get_aw(c, xa);
             chain_predict<2>(xa, aw[c], dt, qaw);
@@ -154,9 +197,11 @@ struct Chains {
     template <bool POISON = true>
     __device__ __forceinline__ bool update_gps(const T (&z)[3]) {
         bool ok = true;
-        const T R[1] = {T(kRGps)};
 #pragma unroll
         for (int c = 0; c < M::NP; ++c) {
+            T q[3], r[6], rg;
+            pva_noise<CUSTOM, M>(kc, c, q, r, rg);
+            const T R[1] = {rg};
             T xb[3];
             get_pva(c, xb);
             const T zb[1] = {z[c]};
@@ -173,10 +218,10 @@ struct Chains {
     template <bool POISON = true, class Pay>
     __device__ __forceinline__ bool update_imu(const Pay& imu, T dt) {
         bool ok = true;
-        const T Rp[6] = {T(kRPos), T(0), T(0), T(kRVel), T(0), T(kRAcc)};
-        const T Ra[3] = {T(kRAtt), T(0), T(kRRate)};
 #pragma unroll
         for (int c = 0; c < M::NP; ++c) {
+            T q[3], Rp[6], rg;
+            pva_noise<CUSTOM, M>(kc, c, q, Rp, rg);
             T xb[3];
             get_pva(c, xb);
             const T a = imu[M::imu_acc(c)];
@@ -188,6 +233,8 @@ struct Chains {
         }
 #pragma unroll
         for (int c = 0; c < M::NA; ++c) {
+            T q[2], Ra[3];
+            aw_noise<CUSTOM, M>(kc, c, q, Ra);
             T xa[2];
             get_aw(c, xa);
             const T za[2] = {imu[M::imu_att(c)], imu[M::imu_rate(c)]};
@@ -232,6 +279,19 @@ struct Chains {
         for (int c = 0; c < M::NA; ++c)
 #pragma unroll
             for (int k = 0; k < 3; ++k) aw[c][k] = w[k];
+        if constexpr (CUSTOM) {  // P0 = diag(p0) in the model's state order
+#pragma unroll
+            for (int c = 0; c < M::NP; ++c) {
+                pva[c][0] = T(kc->p0[M::pva(c, 0)]);
+                pva[c][3] = T(kc->p0[M::pva(c, 1)]);
+                pva[c][5] = T(kc->p0[M::pva(c, 2)]);
+            }
+#pragma unroll
+            for (int c = 0; c < M::NA; ++c) {
+                aw[c][0] = T(kc->p0[M::aw(c, 0)]);
+                aw[c][2] = T(kc->p0[M::aw(c, 1)]);
+            }
+        }
     }
 
     // block-packed covariance row r (see the file comment)
@@ -289,7 +349,7 @@ struct Chains {
 // ------------------------------------------------------------------------------------
 // Per-filter event streams (kf_run_events).
 // ------------------------------------------------------------------------------------
-template <typename T, class M>
+template <typename T, class M, bool CUSTOM>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void ref_events_kernel(const RefArgs a) {
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
@@ -297,7 +357,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
     const uint32_t rb8 = uint32_t(a.B) * 8u;
     const uint32_t off8 = uint32_t(f) * 8u;
-    Chains<T, M> s;
+    Chains<T, M, CUSTOM> s;
+    s.kc = a.kc;
     s.load(a.x, a.P, rb, off);
     int32_t st = a.status[f];
     const uint32_t rb_tr = a.traj ? rb : 0u, rb_ld = a.logdet ? rb : 0u, rb_cv = a.cov ? rb : 0u;
@@ -368,7 +429,7 @@ struct LdsPayload {
     __device__ __forceinline__ T operator[](int i) const { return img[i * 64]; }
 };
 
-template <typename T, class M, bool COV>
+template <typename T, class M, bool COV, bool CUSTOM>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void ref_events_lds_kernel(
     const RefArgs a) {
     constexpr int W = int(sizeof(T));
@@ -388,7 +449,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     unsigned char* const img0 = lds + wave * 2 * IMG;
     const uint32_t off = uint32_t(f) * uint32_t(W);  // dead lanes: beyond every row
     const uint32_t rb = uint32_t(a.B) * uint32_t(W);
-    Chains<T, M> s;
+    Chains<T, M, CUSTOM> s;
+    s.kc = a.kc;
     s.load(a.x, a.P, rb, off);
     int32_t st = f < a.B ? a.status[f] : 0;
     const uint32_t rb_tr = a.traj ? rb : 0u, rb_ld = a.logdet ? rb : 0u, rb_cv = a.cov ? rb : 0u;
@@ -449,13 +511,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     if (f < a.B) a.status[f] = st;
 }
 
-template <typename T, class M>
+template <typename T, class M, bool CUSTOM>
 __global__ __launch_bounds__(kBlock) void ref_reset_kernel(const RefArgs a) {
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
-    Chains<T, M> s;
+    Chains<T, M, CUSTOM> s;
+    s.kc = a.kc;
 #pragma unroll
     for (int i = 0; i < M::N; ++i) s.x[i] = a.x0 ? ldb<T>(a.x0, i, rb, off) : T(0);
     s.reset_cov();
@@ -557,7 +620,7 @@ struct ChainIn {
 // each variant's arithmetic is the single-state lane's, term for term.  Variant v's state is
 // column v * B + f of a state bank of NV * B columns (the covariance: column f), and its
 // trajectory records go to rows v * s_vstride.
-template <typename T, class M, bool STREAM, int NV = 1>
+template <typename T, class M, bool STREAM, bool CUSTOM, int NV = 1>
 __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     static_assert(NV == 1 || STREAM, "state variants are a stream-mode feature");
     if (a.skip && *a.skip) return;  // the sequential fallback of a stream run that passed its checks
@@ -592,8 +655,19 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     const int ia = pva ? ca : M::imu_att(ca);              // GPS position / IMU attitude column
     const int ib = pva ? M::imu_acc(ca) : M::imu_rate(ca);  // IMU acceleration / rate column
     const uint32_t v_a = uint32_t(ia) * rb + off, v_b = uint32_t(ib) * rb + off;
-    const T q[3] = {T(pva ? kQPos : kQAtt), T(pva ? kQVel : kQRate), T(pva ? kQAcc : 0.0)};
-    const T Rimu[6] = {T(pva ? kRPos : kRAtt), T(0), T(0), T(pva ? kRVel : kRRate), T(0), T(pva ? kRAcc : 1.0)};
+    T q[3] = {T(pva ? kQPos : kQAtt), T(pva ? kQVel : kQRate), T(pva ? kQAcc : 0.0)};
+    T Rimu[6] = {T(pva ? kRPos : kRAtt), T(0), T(0), T(pva ? kRVel : kRRate), T(0), T(pva ? kRAcc : 1.0)};
+    T Rgps = T(kRGps);
+    if constexpr (CUSTOM) {  // this lane's chain states (the inert third state of an aw lane keeps 0 / 1)
+        const RefConsts* kc = a.kc;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            if (xi[k] >= 0) {
+                q[k] = T(kc->q[xi[k]]);
+                Rimu[k == 0 ? 0 : k == 1 ? 3 : 5] = T(kc->r_imu[xi[k]]);
+            }
+        if (pva) Rgps = T(kc->r_gps[ca]);
+    }
 
     T x[NV][3], P[6];
     {
@@ -710,7 +784,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
                         T zb[NV][1];
 #pragma unroll
                         for (int v = 0; v < NV; ++v) zb[v][0] = va;
-                        const T R[1] = {T(kRGps)};
+                        const T R[1] = {Rgps};
                         ok = sel_update_nv<3, 1, true, T, kRefNewton, true, NV>(x, P, zb, R);
                     }
                 } else {
@@ -1261,9 +1335,20 @@ __global__ __launch_bounds__(kBlock) void stream_records_kernel(const StreamArgs
 // reference's 200 Hz IMU stream contracts an error by ~1e-3), so a few iterations over all
 // chunks at once replace the W-event warm-up; the device seam check still decides.
 // ------------------------------------------------------------------------------------
-template <class M>
-__device__ __forceinline__ void chain_noise(int ch, double (&q)[3], double (&si_imu)[3], double& si_gps) {
+template <class M, bool CUSTOM>
+__device__ __forceinline__ void chain_noise(int ch, double (&q)[3], double (&si_imu)[3], double& si_gps,
+                                            const RefConsts* kc) {
     const bool pva = ch < M::NP;
+    if constexpr (CUSTOM) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int i = chain_state<M>(ch, k);
+            q[k] = i >= 0 ? kc->q[i] : 0.0;
+            si_imu[k] = i >= 0 ? 1.0 / kc->r_imu[i] : 0.0;
+        }
+        si_gps = pva ? 1.0 / kc->r_gps[ch] : 0.0;
+        return;
+    }
     q[0] = pva ? kQPos : kQAtt;
     q[1] = pva ? kQVel : kQRate;
     q[2] = pva ? kQAcc : 0.0;
@@ -1302,7 +1387,7 @@ __device__ __forceinline__ void lft_event(double (&v)[6], int type, double dt, b
     }
 }
 
-template <typename T, class M>
+template <typename T, class M, bool CUSTOM>
 __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArgs a) {
     constexpr int NCH = M::NP + M::NA;
     // one lane per (chunk piece, chain), carrying all six columns of the 6x6 product: an event's
@@ -1314,7 +1399,7 @@ __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArg
     const int ch = int(grp % NCH);
     const bool pva = ch < M::NP;
     double q[3], si[3], sg;
-    chain_noise<M>(ch, q, si, sg);
+    chain_noise<M, CUSTOM>(ch, q, si, sg, a.kc);
     double v[6][6];  // v[j] = column j
 #pragma unroll
     for (int j = 0; j < 6; ++j)
@@ -1635,13 +1720,13 @@ __global__ __launch_bounds__(1024) void stream_finish_kernel(const StreamArgs a)
 // ------------------------------------------------------------------------------------
 constexpr int kMaxEvents = 64;
 
-template <typename T>
-using Ref15 = Chains<T, M15>;
+template <typename T, bool CUSTOM = false>
+using Ref15 = Chains<T, M15, CUSTOM>;
 
 #ifndef KF_COMBO_WAVES
 #define KF_COMBO_WAVES 3  // waves per SIMD the one-filter-per-subset kernel is compiled for
 #endif
-template <typename T>
+template <typename T, bool CUSTOM>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_COMBO_WAVES))) void ref15_combo_kernel(
     const Ref15ComboArgs a) {
     __shared__ double s_ev[kMaxEvents * 11];
@@ -1660,7 +1745,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_COMBO
     // records land at a per-lane row (a skipped event shifts them): one span over the k+2 rows
     const auto r_ld = span_rsrc(a.logdets, 0, rb, uint32_t(a.k + 2));
 
-    Ref15<T> s;
+    Ref15<T, CUSTOM> s;
+    s.kc = a.kc;
 #pragma unroll
     for (int i = 0; i < 15; ++i) s.x[i] = T(a.init[i]);
 #pragma unroll
@@ -1795,7 +1881,7 @@ struct LogdetAcc {
 // depend on the measurements (nor, so, on the state): the state is not carried (kf_eval_combos
 // carries it for the per-combination API).  The updates see a constant zero state (search_pva,
 // search_aw), so their state half is dead code the compiler removes.
-template <typename T>
+template <typename T, bool CUSTOM>
 struct SearchNode {
     T P[27];
     T run;
@@ -1807,7 +1893,8 @@ struct SearchNode {
     // (kf_workers.py:36-71); record 0 is the logdet of the initial covariance (:32).  With
     // `eval`, the root subset itself is also scored (its max log-det with the final predict).
     __device__ __forceinline__ T root(const Ref15SearchArgs& a, bool eval) {
-        Ref15<T> r;
+        Ref15<T, CUSTOM> r;
+        r.kc = a.kc;
 #pragma unroll
         for (int i = 0; i < 15; ++i) r.x[i] = T(a.init[i]);
 #pragma unroll
@@ -1893,12 +1980,12 @@ __device__ __forceinline__ SearchEvent search_event(const Ref15SearchArgs& a, in
 // One chain of the 15-state filter through one event, Chains::event's operations for that
 // chain (each chain's predict and update touch only that chain); the state is not carried
 // (SearchNode), so xb is constant zeros and the state half is dead code after inlining.
-template <typename T>
-__device__ __forceinline__ void search_pva(const SearchEvent& v, int ch, T (&Pb)[6], bool& ok) {
+template <typename T, bool CUSTOM>
+__device__ __forceinline__ void search_pva(const SearchEvent& v, int ch, T (&Pb)[6], bool& ok, const RefConsts* kc) {
     using C15 = Chains<T, M15>;
-    const T qpva[3] = {T(kQPos), T(kQVel), T(kQAcc)};
-    const T Rg[1] = {T(kRGps)};
-    const T Rp[6] = {T(kRPos), T(0), T(0), T(kRVel), T(0), T(kRAcc)};
+    T qpva[3], Rp[6], rg;
+    pva_noise<CUSTOM, M15>(kc, ch, qpva, Rp, rg);
+    const T Rg[1] = {rg};
     if (!v.step) return;
     const T dt = T(v.dt);
     T xb[3] = {T(0), T(0), T(0)};
@@ -1915,11 +2002,11 @@ __device__ __forceinline__ void search_pva(const SearchEvent& v, int ch, T (&Pb)
     }
 }
 
-template <typename T>
-__device__ __forceinline__ void search_aw(const SearchEvent& v, int ch, T (&Pa)[3], bool& ok) {
+template <typename T, bool CUSTOM>
+__device__ __forceinline__ void search_aw(const SearchEvent& v, int ch, T (&Pa)[3], bool& ok, const RefConsts* kc) {
     using C15 = Chains<T, M15>;
-    const T qaw[2] = {T(kQAtt), T(kQRate)};
-    const T Ra[3] = {T(kRAtt), T(0), T(kRRate)};
+    T qaw[2], Ra[3];
+    aw_noise<CUSTOM, M15>(kc, ch, qaw, Ra);
     if (!v.step) return;
     T xa[2] = {T(0), T(0)};
     C15::template chain_predict<2>(xa, Pa, T(v.dt), qaw);
@@ -1932,13 +2019,15 @@ __device__ __forceinline__ void search_aw(const SearchEvent& v, int ch, T (&Pa)[
 // The log-dets of one subset: its record after the event (rec) and after the worker's final
 // predict (fin), accumulated chain by chain in Chains::logdet's block order, so the numbers are
 // kf_eval_combos's.
-template <typename T>
+template <typename T, bool CUSTOM>
 struct SearchScore {
     LogdetAcc<T> rec, fin;
     bool ok = true;
+    const RefConsts* kc = nullptr;
     __device__ __forceinline__ void add_pva(const SearchEvent& v, const T (&Pb)[6], int ch) {
         using C15 = Chains<T, M15>;
-        const T qpva[3] = {T(kQPos), T(kQVel), T(kQAcc)};
+        T qpva[3], Rp[6], rg;
+        pva_noise<CUSTOM, M15>(kc, ch, qpva, Rp, rg);
         rec.add_pva(Pb, ch);
         T Pf[6], xf[3] = {T(0), T(0), T(0)};
 #pragma unroll
@@ -1946,9 +2035,10 @@ struct SearchScore {
         if (v.final_predict) C15::template chain_predict<3>(xf, Pf, T(v.dte), qpva);
         fin.add_pva(Pf, ch);
     }
-    __device__ __forceinline__ void add_aw(const SearchEvent& v, const T (&Pa)[3]) {
+    __device__ __forceinline__ void add_aw(const SearchEvent& v, const T (&Pa)[3], int ch) {
         using C15 = Chains<T, M15>;
-        const T qaw[2] = {T(kQAtt), T(kQRate)};
+        T qaw[2], Ra[3];
+        aw_noise<CUSTOM, M15>(kc, ch, qaw, Ra);
         rec.add_aw(Pa);
         T Pf[3], xf[2] = {T(0), T(0)};
 #pragma unroll
@@ -1994,8 +2084,8 @@ struct ParLds {
     __device__ __forceinline__ T operator()(int i) const { return col[i * 64]; }
 };
 
-template <typename T, class PS>
-__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const SearchNode<T>& par, const PS& pp, int j,
+template <typename T, bool CUSTOM, class PS>
+__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const SearchNode<T, CUSTOM>& par, const PS& pp, int j,
                                              uint64_t c, uint64_t& best, uint64_t& cnt, uint64_t& best1,
                                              uint64_t& cnt1) {
     const SearchEvent vs = search_event(a, j, par.prev);
@@ -2005,20 +2095,21 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
     if (tail) vg = search_event(a, j + 1, vs.prev);
     char* cb = store ? level_block<T>(a.child, c) : nullptr;
     const uint32_t cl = uint32_t(c) & 63u;
-    SearchScore<T> ss, sg;
+    SearchScore<T, CUSTOM> ss, sg;
+    ss.kc = sg.kc = a.kc;
 #pragma unroll
     for (int ch = 0; ch < M15::NP; ++ch) {
         T Pb[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) Pb[i] = pp(6 * ch + i);
-        search_pva(vs, ch, Pb, ss.ok);
+        search_pva<T, CUSTOM>(vs, ch, Pb, ss.ok, a.kc);
         if (store) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) *level_row<T>(cb, cl, 6 * ch + i) = Pb[i];
         }
         ss.add_pva(vs, Pb, ch);
         if (tail) {
-            search_pva(vg, ch, Pb, sg.ok);
+            search_pva<T, CUSTOM>(vg, ch, Pb, sg.ok, a.kc);
             sg.add_pva(vg, Pb, ch);
         }
     }
@@ -2027,15 +2118,15 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
         T Pa[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) Pa[i] = pp(6 * M15::NP + 3 * ch + i);
-        search_aw(vs, ch, Pa, ss.ok);
+        search_aw<T, CUSTOM>(vs, ch, Pa, ss.ok, a.kc);
         if (store) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, 6 * M15::NP + 3 * ch + i) = Pa[i];
         }
-        ss.add_aw(vs, Pa);
+        ss.add_aw(vs, Pa, ch);
         if (tail) {
-            search_aw(vg, ch, Pa, sg.ok);
-            sg.add_aw(vg, Pa);
+            search_aw<T, CUSTOM>(vg, ch, Pa, sg.ok, a.kc);
+            sg.add_aw(vg, Pa, ch);
         }
     }
     T fmax;
@@ -2074,13 +2165,13 @@ __device__ __forceinline__ void search_publish(const Ref15SearchArgs& a, int k, 
 #endif
 // PLDS: the parent's covariance lives in LDS (one 64-lane block per workgroup, [27][64] T),
 // which fits the kernel in 3 waves per SIMD without spills; otherwise in registers.
-template <typename T, bool PLDS>
+template <typename T, bool PLDS, bool CUSTOM>
 __global__ __launch_bounds__(PLDS ? 64 : kBlock) __attribute__((amdgpu_waves_per_eu(PLDS ? 3 : KF_SEARCH_PM_WAVES))) void
 ref15_search_pm_kernel(const Ref15SearchArgs a) {
     constexpr int NT = PLDS ? 64 : kBlock;
     const int64_t p = static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x;
     if (uint64_t(p) >= a.n_par) return;
-    SearchNode<T> par;
+    SearchNode<T, CUSTOM> par;
     if (a.k == 1) {
         uint64_t rb = 0, rc = 0;  // a fixed root is itself one of the subsets searched
         const T f = par.root(a, a.root_mask != 0);
@@ -2101,14 +2192,16 @@ ref15_search_pm_kernel(const Ref15SearchArgs a) {
 #pragma unroll 1
         for (int j = j0; j < a.n_events; ++j) {
             if (j <= m) continue;
-            search_child<T>(a, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt, best1, cnt1);
+            search_child<T, CUSTOM>(a, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt, best1,
+                                    cnt1);
         }
     } else {
         const ParRegs<T> pp{par.P};
 #pragma unroll 1
         for (int j = j0; j < a.n_events; ++j) {
             if (j <= m) continue;
-            search_child<T>(a, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt, best1, cnt1);
+            search_child<T, CUSTOM>(a, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt, best1,
+                                    cnt1);
         }
     }
     search_publish(a, a.k, best, cnt);
@@ -2121,7 +2214,7 @@ ref15_search_pm_kernel(const Ref15SearchArgs a) {
 // contiguous ranges, so the items that read one parent block run back to back on one XCD and
 // re-read it from that XCD's L2.  Blocks are grouped by their first parent's largest event v
 // (non-decreasing in colex order); a block of group v has items j = v + 1 .. n - 1.
-template <typename T>
+template <typename T, bool CUSTOM>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void ref15_search_cm_kernel(const Ref15SearchArgs a,
                                                                                                      uint64_t n_items) {
     const uint64_t per_xcd = (n_items + 7) / 8;
@@ -2150,7 +2243,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
     }
     const uint64_t p = blk * 64 + threadIdx.x;
     if (p >= a.n_par) return;
-    SearchNode<T> par;
+    SearchNode<T, CUSTOM> par;
     if (k == 1) {
         uint64_t rb = 0, rc = 0;  // a fixed root is itself one of the subsets searched (item 0 scores it)
         const bool eval = a.root_mask != 0 && item == 0;
@@ -2161,7 +2254,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
         par.load(a.par, p);
     }
     uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0;
-    if (par.max_event(a.shift) < j) search_child<T>(a, par, ParRegs<T>{par.P}, j, p + binom(j, k), best, cnt, best1, cnt1);
+    if (par.max_event(a.shift) < j)
+        search_child<T, CUSTOM>(a, par, ParRegs<T>{par.P}, j, p + binom(j, k), best, cnt, best1, cnt1);
     search_publish(a, a.k, best, cnt);
     if (a.tail) search_publish(a, a.k + 1, best1, cnt1);
 }
@@ -2169,8 +2263,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
 // ------------------------------------------------------------------------------------
 // Scheduler scoring and the rate-decimated greedy driver (kf_workers.py:99-213, 826-957).
 // ------------------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ T cov_trace(const Ref15<T>& s) {
+template <typename T, bool CUSTOM>
+__device__ __forceinline__ T cov_trace(const Ref15<T, CUSTOM>& s) {
     T tr = T(0);
 #pragma unroll
     for (int i = 0; i < 3; ++i) tr += s.pva[i][0] + s.pva[i][3] + s.pva[i][5];
@@ -2182,15 +2276,17 @@ __device__ __forceinline__ T cov_trace(const Ref15<T>& s) {
 // trace of Scheduler.cov_matrix (kf_workers.py:112-147) for one candidate sensor.  The first
 // row of both H_gps and H_imu is e_0 (pos_x), with R[0,0] = 3 (GPS) or 50 (IMU); a full update
 // uses every row.  The state vector is not needed, so a zero one is carried through.
-template <typename T>
-__device__ __forceinline__ Ref15<T> posterior(const Ref15<T>& s0, int type, bool full) {
-    Ref15<T> c = s0;
+template <typename T, bool CUSTOM>
+__device__ __forceinline__ Ref15<T, CUSTOM> posterior(const Ref15<T, CUSTOM>& s0, int type, bool full) {
+    Ref15<T, CUSTOM> c = s0;
 #pragma unroll
     for (int i = 0; i < 15; ++i) c.x[i] = T(0);
     if (!full) {
         T xb[3] = {T(0), T(0), T(0)};
         const T z[1] = {T(0)};
-        const T R[1] = {T(type == kGps ? kRGps : kRPos)};
+        T q[3], Rp[6], rg;
+        pva_noise<CUSTOM, M15>(s0.kc, 0, q, Rp, rg);
+        const T R[1] = {type == kGps ? rg : Rp[0]};
         sel_update<3, 1, true, T, kRefNewton>(xb, c.pva[0], z, R);
     } else if (type == kGps) {
         const T z[3] = {T(0), T(0), T(0)};
@@ -2204,21 +2300,72 @@ __device__ __forceinline__ Ref15<T> posterior(const Ref15<T>& s0, int type, bool
     return c;
 }
 
-template <typename T>
-__device__ __forceinline__ T posterior_trace(const Ref15<T>& s0, int type, bool full) {
+template <typename T, bool CUSTOM>
+__device__ __forceinline__ T posterior_trace(const Ref15<T, CUSTOM>& s0, int type, bool full) {
     return cov_trace(posterior(s0, type, full));
+}
+
+// One scalar measurement of state k of a chain block with variance r: P -= P e_k e_k^T P / (P_kk + r)
+// (Scheduler.cov_matrix's Sigma - K H Sigma for a one-row H, kf_workers.py:121-147)
+template <int NB, typename T>
+__device__ __forceinline__ void chain_scalar_update(T (&Pb)[NB * (NB + 1) / 2], int k, T r) {
+    T g[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) g[i] = Pb[tri<NB>(i, k)];
+    const T inv = T(1) / (g[k] + r);
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = i; j < NB; ++j) Pb[tri<NB>(i, j)] = fmaT(-g[i] * inv, g[j], Pb[tri<NB>(i, j)]);
+}
+
+// Scheduler.cov_matrix(S, Sigma, R, H) for any set S of measurement rows (kf_workers.py:121-138:
+// H_hat = H[S], R_hat = R[S, S]).  H's rows select states and R is diagonal, so the rows are
+// independent measurements and, P being block-diagonal over the chains, each chain takes its own
+// rows: sequential scalar updates in row order give the joint update's value.  mask bit i = row
+// i + 1 of the sensor's H (GPS: pos_x, pos_y, pos_z; IMU: state i).
+template <typename T, bool CUSTOM>
+__device__ __forceinline__ Ref15<T, CUSTOM> posterior_rows(const Ref15<T, CUSTOM>& s0, int type, uint32_t mask) {
+    Ref15<T, CUSTOM> c = s0;
+#pragma unroll
+    for (int ch = 0; ch < M15::NP; ++ch) {
+        T q[3], Rp[6], rg;
+        pva_noise<CUSTOM, M15>(s0.kc, ch, q, Rp, rg);
+        if (type == kGps) {
+            if (mask >> ch & 1u) chain_scalar_update<3>(c.pva[ch], 0, rg);
+        } else {
+            const T r[3] = {Rp[0], Rp[3], Rp[5]};
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (mask >> M15::pva(ch, k) & 1u) chain_scalar_update<3>(c.pva[ch], k, r[k]);
+        }
+    }
+    if (type != kGps) {
+#pragma unroll
+        for (int ch = 0; ch < M15::NA; ++ch) {
+            T q[2], Ra[3];
+            aw_noise<CUSTOM, M15>(s0.kc, ch, q, Ra);
+            const T r[2] = {Ra[0], Ra[2]};
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (mask >> M15::aw(ch, k) & 1u) chain_scalar_update<2>(c.aw[ch], k, r[k]);
+        }
+    }
+    return c;
 }
 
 // The greedy scheduler's gain (S = [1]): only the x-axis (pos, vel, acc) block changes, so the
 // trace is the current one with that block's diagonal replaced — no copy of the whole state.
-template <typename T>
-__device__ __forceinline__ T first_row_gain(const Ref15<T>& s, int type) {
+template <typename T, bool CUSTOM>
+__device__ __forceinline__ T first_row_gain(const Ref15<T, CUSTOM>& s, int type) {
     T p[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) p[k] = s.pva[0][k];
     T xb[3] = {T(0), T(0), T(0)};
     const T z[1] = {T(0)};
-    const T R[1] = {T(type == kGps ? kRGps : kRPos)};
+    T q[3], Rp[6], rg;
+    pva_noise<CUSTOM, M15>(s.kc, 0, q, Rp, rg);
+    const T R[1] = {type == kGps ? rg : Rp[0]};
     sel_update<3, 1, true, T, kRefNewton>(xb, p, z, R);
     T tr = p[0] + p[3] + p[5];
 #pragma unroll
@@ -2228,17 +2375,19 @@ __device__ __forceinline__ T first_row_gain(const Ref15<T>& s, int type) {
     return tr;
 }
 
-template <typename T>
+template <typename T, bool CUSTOM>
 __global__ __launch_bounds__(kBlock) void ref15_score_kernel(const Ref15ScoreArgs a) {
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(a.B) * uint32_t(sizeof(T));
     const uint32_t rb_post = a.post ? rb : 0u;
-    Ref15<T> s;
+    Ref15<T, CUSTOM> s;
+    s.kc = a.kc;
     s.load(a.x, a.P, rb, off);
     for (int c = 0; c < a.n_types; ++c) {
-        const Ref15<T> p = posterior(s, int(a.types[c]), a.full != 0);
+        const Ref15<T, CUSTOM> p = a.rows ? posterior_rows(s, int(a.types[c]), a.masks[c])
+                                          : posterior(s, int(a.types[c]), a.full != 0);
         stb(a.gain, c, rb, off, cov_trace(p));
         p.store_cov(a.post, int64_t(c) * 27, rb_post, off);
     }
@@ -2250,9 +2399,9 @@ __global__ __launch_bounds__(kBlock) void ref15_score_kernel(const Ref15ScoreArg
 // never picked, and with none pickable the queue's first event is, as the reference's loop
 // leaves best_i at its start).  Each lane tracks those two candidates (index, type, time) as
 // events are queued, and reads the payload of the picked one only.
-template <typename T>
+template <typename T, bool CUSTOM>
 struct SchedLane {
-    Ref15<T> s;
+    Ref15<T, CUSTOM> s;
     int32_t st;
     double prev, period;
     int q_len = 0, nsel = 0;
@@ -2325,7 +2474,7 @@ struct SchedLane {
 #define KF_SCHED_WAVES 2
 #endif
 // Any B: the next event's type and time are loaded one event ahead in registers.
-template <typename T>
+template <typename T, bool CUSTOM>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED_WAVES))) void ref15_sched_kernel(
     const Ref15SchedArgs a) {
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -2333,7 +2482,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED
     const int64_t B = a.B;
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(B) * uint32_t(sizeof(T));
-    SchedLane<T> L;
+    SchedLane<T, CUSTOM> L;
+    L.s.kc = a.kc;
     L.s.load(a.x, a.P, rb, off);
     L.st = a.status[f];
     L.prev = a.prev_time[f];
@@ -2364,7 +2514,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED
 #endif
 constexpr int kSchedChunk = KF_SCHED_CHUNK;
 constexpr int kSchedImg = kSchedChunk * 512 + kSchedChunk * 64;
-template <typename T>
+template <typename T, bool CUSTOM>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED_WAVES))) void ref15_sched_lds_kernel(
     const Ref15SchedArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * 2 * kSchedImg];
@@ -2377,7 +2527,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED
     unsigned char* const img0 = lds + wave * 2 * kSchedImg;
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(B) * uint32_t(sizeof(T));
-    SchedLane<T> L;
+    SchedLane<T, CUSTOM> L;
+    L.s.kc = a.kc;
     L.s.load(a.x, a.P, rb, off);
     L.st = a.status[f];
     L.prev = a.prev_time[f];
@@ -2422,10 +2573,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED
 
 }  // namespace
 
+// kernel<..., CUSTOM> for a launch: the reference's constants (kc == nullptr) or the handle's
+#define KF_CUSTOM_DISPATCH(kc, ...)         \
+    do {                                    \
+        if (kc) {                           \
+            constexpr bool CUSTOM = true;   \
+            __VA_ARGS__;                    \
+        } else {                            \
+            constexpr bool CUSTOM = false;  \
+            __VA_ARGS__;                    \
+        }                                   \
+    } while (0)
+
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream) {
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-    if (f64) ref15_score_kernel<double><<<grid, kBlock, 0, stream>>>(a);
-    else ref15_score_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    KF_CUSTOM_DISPATCH(a.kc, {
+        if (f64) ref15_score_kernel<double, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+        else ref15_score_kernel<float, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+    });
     return hipGetLastError();
 }
 
@@ -2435,89 +2600,67 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
     const bool lds = a.B % 64 == 0 && uint64_t(a.B) * 8 * 2 < (uint64_t(1) << 32) &&
                      reinterpret_cast<uintptr_t>(a.t) % 16 == 0 && reinterpret_cast<uintptr_t>(a.etype) % 16 == 0 &&
                      uint64_t(a.B) * kSchedChunk < (uint64_t(1) << 32) && !a.regs;
-    if (lds) {
-        if (f64) ref15_sched_lds_kernel<double><<<grid, kBlock, 0, stream>>>(a);
-        else ref15_sched_lds_kernel<float><<<grid, kBlock, 0, stream>>>(a);
-    } else {
-        if (f64) ref15_sched_kernel<double><<<grid, kBlock, 0, stream>>>(a);
-        else ref15_sched_kernel<float><<<grid, kBlock, 0, stream>>>(a);
-    }
+    KF_CUSTOM_DISPATCH(a.kc, {
+        if (lds) {
+            if (f64) ref15_sched_lds_kernel<double, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+            else ref15_sched_lds_kernel<float, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+        } else {
+            if (f64) ref15_sched_kernel<double, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+            else ref15_sched_kernel<float, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+        }
+    });
     return hipGetLastError();
 }
 
-hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, int variant) {
+namespace {
+template <typename T, class M, bool CUSTOM>
+void ref_events_t(const RefArgs& a, hipStream_t stream, int variant) {
     if (variant == kEventsLds) {
         const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-        const bool cov = a.cov != nullptr;
-        if (model == 15) {
-            if (f64) {
-                if (cov) ref_events_lds_kernel<double, M15, true><<<grid, kBlock, 0, stream>>>(a);
-                else ref_events_lds_kernel<double, M15, false><<<grid, kBlock, 0, stream>>>(a);
-            } else {
-                if (cov) ref_events_lds_kernel<float, M15, true><<<grid, kBlock, 0, stream>>>(a);
-                else ref_events_lds_kernel<float, M15, false><<<grid, kBlock, 0, stream>>>(a);
-            }
-        } else if (model == 8) {
-            if (f64) {
-                if (cov) ref_events_lds_kernel<double, M8, true><<<grid, kBlock, 0, stream>>>(a);
-                else ref_events_lds_kernel<double, M8, false><<<grid, kBlock, 0, stream>>>(a);
-            } else {
-                if (cov) ref_events_lds_kernel<float, M8, true><<<grid, kBlock, 0, stream>>>(a);
-                else ref_events_lds_kernel<float, M8, false><<<grid, kBlock, 0, stream>>>(a);
-            }
-        } else {
-            return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
-    if (variant == kEventsChain) {
+        if (a.cov) ref_events_lds_kernel<T, M, true, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+        else ref_events_lds_kernel<T, M, false, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+    } else if (variant == kEventsChain) {
         const dim3 cgrid(static_cast<unsigned>((a.B * kGroup + kBlock - 1) / kBlock));
-        if (model == 15) {
-            if (f64) ref_chain_kernel<double, M15, false><<<cgrid, kBlock, 0, stream>>>(a);
-            else ref_chain_kernel<float, M15, false><<<cgrid, kBlock, 0, stream>>>(a);
-        } else if (model == 8) {
-            if (f64) ref_chain_kernel<double, M8, false><<<cgrid, kBlock, 0, stream>>>(a);
-            else ref_chain_kernel<float, M8, false><<<cgrid, kBlock, 0, stream>>>(a);
-        } else {
-            return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
-    const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-    if (model == 15) {
-        if (f64) ref_events_kernel<double, M15><<<grid, kBlock, 0, stream>>>(a);
-        else ref_events_kernel<float, M15><<<grid, kBlock, 0, stream>>>(a);
-    } else if (model == 8) {
-        if (f64) ref_events_kernel<double, M8><<<grid, kBlock, 0, stream>>>(a);
-        else ref_events_kernel<float, M8><<<grid, kBlock, 0, stream>>>(a);
+        ref_chain_kernel<T, M, false, CUSTOM><<<cgrid, kBlock, 0, stream>>>(a);
     } else {
-        return hipErrorInvalidValue;
+        const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
+        ref_events_kernel<T, M, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
     }
+}
+template <typename T, class M, bool CUSTOM>
+void ref_stream_t(const RefArgs& a, hipStream_t stream, int nv) {
+    const dim3 cgrid(static_cast<unsigned>((a.B * kGroup + kBlock - 1) / kBlock));
+    if (nv == 4) ref_chain_kernel<T, M, true, CUSTOM, 4><<<cgrid, kBlock, 0, stream>>>(a);
+    else ref_chain_kernel<T, M, true, CUSTOM><<<cgrid, kBlock, 0, stream>>>(a);
+}
+}  // namespace
+
+hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, int variant) {
+    if (model != 15 && model != 8) return hipErrorInvalidValue;
+    KF_CUSTOM_DISPATCH(a.kc, {
+        if (model == 15) {
+            if (f64) ref_events_t<double, M15, CUSTOM>(a, stream, variant);
+            else ref_events_t<float, M15, CUSTOM>(a, stream, variant);
+        } else {
+            if (f64) ref_events_t<double, M8, CUSTOM>(a, stream, variant);
+            else ref_events_t<float, M8, CUSTOM>(a, stream, variant);
+        }
+    });
     return hipGetLastError();
 }
 
 hipError_t launch_ref_stream(int model, bool f64, const RefArgs& a, hipStream_t stream, int nv) {
     if (a.s_len <= 0 || a.s_nchunks <= 0 || (nv != 1 && nv != 4)) return hipErrorInvalidValue;
-    const dim3 cgrid(static_cast<unsigned>((a.B * kGroup + kBlock - 1) / kBlock));
-    if (model == 15) {
-        if (nv == 4) {
-            if (f64) ref_chain_kernel<double, M15, true, 4><<<cgrid, kBlock, 0, stream>>>(a);
-            else ref_chain_kernel<float, M15, true, 4><<<cgrid, kBlock, 0, stream>>>(a);
+    if (model != 15 && model != 8) return hipErrorInvalidValue;
+    KF_CUSTOM_DISPATCH(a.kc, {
+        if (model == 15) {
+            if (f64) ref_stream_t<double, M15, CUSTOM>(a, stream, nv);
+            else ref_stream_t<float, M15, CUSTOM>(a, stream, nv);
         } else {
-            if (f64) ref_chain_kernel<double, M15, true><<<cgrid, kBlock, 0, stream>>>(a);
-            else ref_chain_kernel<float, M15, true><<<cgrid, kBlock, 0, stream>>>(a);
+            if (f64) ref_stream_t<double, M8, CUSTOM>(a, stream, nv);
+            else ref_stream_t<float, M8, CUSTOM>(a, stream, nv);
         }
-    } else if (model == 8) {
-        if (nv == 4) {
-            if (f64) ref_chain_kernel<double, M8, true, 4><<<cgrid, kBlock, 0, stream>>>(a);
-            else ref_chain_kernel<float, M8, true, 4><<<cgrid, kBlock, 0, stream>>>(a);
-        } else {
-            if (f64) ref_chain_kernel<double, M8, true><<<cgrid, kBlock, 0, stream>>>(a);
-            else ref_chain_kernel<float, M8, true><<<cgrid, kBlock, 0, stream>>>(a);
-        }
-    } else {
-        return hipErrorInvalidValue;
-    }
+    });
     return hipGetLastError();
 }
 
@@ -2539,7 +2682,10 @@ void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
             stream_starts_kernel<T, M><<<g, kScanTile, 0, stream>>>(a);
             break;
         }
-        case kStreamPhaseLftMaps: stream_lft_maps_kernel<T, M><<<grid(a.C * a.np * NCH), kBlock, 0, stream>>>(a); break;
+        case kStreamPhaseLftMaps:
+            if (a.kc) stream_lft_maps_kernel<T, M, true><<<grid(a.C * a.np * NCH), kBlock, 0, stream>>>(a);
+            else stream_lft_maps_kernel<T, M, false><<<grid(a.C * a.np * NCH), kBlock, 0, stream>>>(a);
+            break;
         case kStreamPhaseLftStart: {
             const int64_t bc = a.g > 0 ? a.G : kBlock;
             // LDS variant: G / g threads walk, but the whole block stages the window maps (more
@@ -2576,23 +2722,26 @@ hipError_t launch_stream_phase(int model, bool f64, int phase, const StreamArgs&
 
 hipError_t launch_ref_reset(int model, bool f64, const RefArgs& a, hipStream_t stream) {
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-    if (model == 15) {
-        if (f64) ref_reset_kernel<double, M15><<<grid, kBlock, 0, stream>>>(a);
-        else ref_reset_kernel<float, M15><<<grid, kBlock, 0, stream>>>(a);
-    } else if (model == 8) {
-        if (f64) ref_reset_kernel<double, M8><<<grid, kBlock, 0, stream>>>(a);
-        else ref_reset_kernel<float, M8><<<grid, kBlock, 0, stream>>>(a);
-    } else {
-        return hipErrorInvalidValue;
-    }
+    if (model != 15 && model != 8) return hipErrorInvalidValue;
+    KF_CUSTOM_DISPATCH(a.kc, {
+        if (model == 15) {
+            if (f64) ref_reset_kernel<double, M15, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+            else ref_reset_kernel<float, M15, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+        } else {
+            if (f64) ref_reset_kernel<double, M8, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+            else ref_reset_kernel<float, M8, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+        }
+    });
     return hipGetLastError();
 }
 
 hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream) {
     if (a.n_events > kMaxEvents) return hipErrorInvalidValue;
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-    if (f64) ref15_combo_kernel<double><<<grid, kBlock, 0, stream>>>(a);
-    else ref15_combo_kernel<float><<<grid, kBlock, 0, stream>>>(a);
+    KF_CUSTOM_DISPATCH(a.kc, {
+        if (f64) ref15_combo_kernel<double, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+        else ref15_combo_kernel<float, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+    });
     return hipGetLastError();
 }
 
@@ -2630,19 +2779,23 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
         }
         const uint64_t waves = (items + 7) / 8 * 8;
         if (waves >= (1ull << 31)) return hipErrorInvalidValue;
-        if (f64) ref15_search_cm_kernel<double><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
-        else ref15_search_cm_kernel<float><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
+        KF_CUSTOM_DISPATCH(a.kc, {
+            if (f64) ref15_search_cm_kernel<double, CUSTOM><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
+            else ref15_search_cm_kernel<float, CUSTOM><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
+        });
         return hipGetLastError();
     }
-    if (!a.pm_regs) {
-        const dim3 grid(static_cast<unsigned>((a.n_par + 63) / 64));
-        if (f64) ref15_search_pm_kernel<double, true><<<grid, 64, 0, stream>>>(a);
-        else ref15_search_pm_kernel<float, true><<<grid, 64, 0, stream>>>(a);
-    } else {
-        const dim3 grid(static_cast<unsigned>((a.n_par + kBlock - 1) / kBlock));
-        if (f64) ref15_search_pm_kernel<double, false><<<grid, kBlock, 0, stream>>>(a);
-        else ref15_search_pm_kernel<float, false><<<grid, kBlock, 0, stream>>>(a);
-    }
+    KF_CUSTOM_DISPATCH(a.kc, {
+        if (!a.pm_regs) {
+            const dim3 grid(static_cast<unsigned>((a.n_par + 63) / 64));
+            if (f64) ref15_search_pm_kernel<double, true, CUSTOM><<<grid, 64, 0, stream>>>(a);
+            else ref15_search_pm_kernel<float, true, CUSTOM><<<grid, 64, 0, stream>>>(a);
+        } else {
+            const dim3 grid(static_cast<unsigned>((a.n_par + kBlock - 1) / kBlock));
+            if (f64) ref15_search_pm_kernel<double, false, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+            else ref15_search_pm_kernel<float, false, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+        }
+    });
     return hipGetLastError();
 }
 

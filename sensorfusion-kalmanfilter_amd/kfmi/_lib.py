@@ -64,7 +64,9 @@ class KFError(RuntimeError):
 
 class kf_params(ctypes.Structure):
     _fields_ = [('q_pos', ctypes.c_double), ('q_vel', ctypes.c_double),
-                ('r', ctypes.c_double * 9), ('p0_pos', ctypes.c_double), ('p0_vel', ctypes.c_double)]
+                ('r', ctypes.c_double * 9), ('p0_pos', ctypes.c_double), ('p0_vel', ctypes.c_double),
+                ('ref_q', ctypes.c_double * 15), ('ref_r_imu', ctypes.c_double * 15),
+                ('ref_r_gps', ctypes.c_double * 3), ('ref_p0', ctypes.c_double * 15)]
 
 
 class kf_ingest_info(ctypes.Structure):
@@ -108,6 +110,7 @@ SIGNATURES = {
     'kf_search_combos': (_i, [_vp, _i, _vp, _vp, _d, _d, _d, _i, _i, _i, ctypes.c_uint64,
                               ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_i), _vp, _vp, _vp]),
     'kf_score_candidates': (_i, [_vp, _i, _vp, _i, _vp, _vp, _vp]),
+    'kf_score_rows': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp]),
     'kf_run_scheduled': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _d, _vp, _vp, _vp, _vp, _vp]),
     'kf_csv_shape': (_i, [ctypes.c_char_p, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i)]),
     'kf_csv_read': (_i, [ctypes.c_char_p, _i, _i, _vp, _i64, _i64]),

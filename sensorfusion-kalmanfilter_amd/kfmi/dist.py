@@ -51,7 +51,7 @@ def gather_shards(local, total, group=None):
     # gather along a new leading rank axis, then lay the shards side by side
     flat = padded.reshape(-1, width).contiguous()
     # gloo collectives take host tensors (a CUDA tensor only appears here under gloo in the
-    # bench's one-GPU rehearsal, KFMI_BENCH_DIST_BACKEND=gloo); RCCL gathers in HBM
+    # bench's one-GPU rehearsal, bench.py --dist-backend gloo); RCCL gathers in HBM
     home = flat.device
     if dist.get_backend(group) == 'gloo':
         flat = flat.cpu()
@@ -117,7 +117,7 @@ def search_classes(n, world):
 
 def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, initial_pt=None, initial_state=None,
                        max_combos_in_memory=1 << 22, dtype='f64', device=0, group=None, search_class=None,
-                       finish=None, search_mem_bytes=32 << 30):
+                       finish=None, search_mem_bytes=32 << 30, consts=None):
     """run_brute_force_kalman_filter_no_sampling_min_usage sharded over the ranks of ``group``
     with the shared-prefix search (kf_search_combos): the subsets are split into 2^w classes by
     their intersection with the first w candidates (``search_classes``); each rank searches its
@@ -128,14 +128,15 @@ def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, init
     ``brute_force_search_ranks`` when a class's levels would not fit in ``search_mem_bytes``.
 
     ``search_class(n_fixed, fixed_mask) -> (k, indices or None)`` / ``finish(k, indices)``
-    replace the GPU evaluation (tests drive the reduction logic with the CPU oracle on gloo)."""
+    replace the GPU evaluation (tests drive the reduction logic with the CPU oracle on gloo).
+    consts: a ref15.ModelConsts (the reference's constants by default)."""
     import torch.distributed as dist
 
     from . import ref15
     if R_threshold is None:
         raise ValueError('R_threshold must be specified for brute force KF.')
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    st = ref15.brute_force_setup(events, start_idx, end_idx, initial_pt, initial_state)
+    st = ref15.brute_force_setup(events, start_idx, end_idx, initial_pt, initial_state, consts)
     if st is None:
         return None
     cand, xt, Pt, prev_time, target_end, ev, init = st
@@ -143,10 +144,10 @@ def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, init
     w = search_classes(n, world)
     if search_class is None and ref15.search_levels(n - w, dtype, search_mem_bytes) < n - w:
         return brute_force_search_ranks(events, start_idx, end_idx, R_threshold, initial_pt, initial_state,
-                                        max_combos_in_memory, dtype, device, group)
+                                        max_combos_in_memory, dtype, device, group, consts=consts)
     kf = None
     if search_class is None:
-        kf = ref15.BatchedKF('ref15', 1, dtype, device=device)
+        kf = ref15.BatchedKF('ref15', 1, dtype, device=device, params=ref15._params(consts))
 
         def search_class(n_fixed, fixed_mask):
             k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=n,
@@ -155,7 +156,7 @@ def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, init
     if finish is None:
         def finish(k, idx):
             return ref15.brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device,
-                                            indices=idx)
+                                            indices=idx, consts=consts)
     backend = dist.get_backend(group)
     tdev = torch.device('cuda', torch.cuda.current_device()) if backend == 'nccl' else torch.device('cpu')
     try:
@@ -190,7 +191,7 @@ def _bitrev64(v):
 
 def brute_force_search_ranks(events, start_idx=0, end_idx=None, R_threshold=None, initial_pt=None,
                              initial_state=None, max_combos_in_memory=1 << 22, dtype='f64', device=0, group=None,
-                             first_valid=None, finish=None):
+                             first_valid=None, finish=None, consts=None):
     """run_brute_force_kalman_filter_no_sampling_min_usage sharded over the ranks of ``group``,
     one filter per subset: for k = 1..n, rank r scans combination ranks
     shard_range(C(n, k), r, world) on its GPU (kf_eval_combos), then an all-reduce MIN of the
@@ -208,7 +209,7 @@ def brute_force_search_ranks(events, start_idx=0, end_idx=None, R_threshold=None
     if R_threshold is None:
         raise ValueError('R_threshold must be specified for brute force KF.')
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    st = ref15.brute_force_setup(events, start_idx, end_idx, initial_pt, initial_state)
+    st = ref15.brute_force_setup(events, start_idx, end_idx, initial_pt, initial_state, consts)
     if st is None:
         return None
     cand, xt, Pt, prev_time, target_end, ev, init = st
@@ -217,13 +218,13 @@ def brute_force_search_ranks(events, start_idx=0, end_idx=None, R_threshold=None
     if first_valid is None:
         width = max(1, min(max_combos_in_memory, max(shard_range(math.comb(n, k), rank, world)[1]
                                                      for k in range(1, n + 1))))
-        kf = ref15.BatchedKF('ref15', width, dtype, device=device)
+        kf = ref15.BatchedKF('ref15', width, dtype, device=device, params=ref15._params(consts))
 
         def first_valid(k, lo, hi):
             return ref15.first_valid_rank(kf, ev, init, prev_time, target_end, k, lo, hi, R_threshold)
     if finish is None:
         def finish(k, r):
-            return ref15.brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype, device)
+            return ref15.brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype, device, consts=consts)
     backend = dist.get_backend(group)
     tdev = torch.device('cuda', torch.cuda.current_device()) if backend == 'nccl' else torch.device('cpu')
     try:

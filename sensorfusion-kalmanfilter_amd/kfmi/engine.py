@@ -82,12 +82,9 @@ class BatchedKF:
         L = _lib.lib()
         check(L.kf_init(device))
         torch.cuda.set_device(self.device)
-        if model in REF_MODELS:
-            if params is not None:
-                raise ValueError(f'{model} uses the reference constants; params must be None')
-            self.params = None
-        else:
-            self.params = params if params is not None else default_params(model)
+        # reference models: params carries the caller's diagonal constants (kf_params.ref_*,
+        # e.g. kfmi.ref15.ModelConsts(...).params()), None = the reference's
+        self.params = params if params is not None else (None if model in REF_MODELS else default_params(model))
         h = ctypes.c_void_p()
         check(L.kf_alloc(ctypes.byref(h), MODELS[model][0], self.batch, DTYPES[dtype][0],
                          ctypes.byref(self.params) if self.params is not None else None))
@@ -450,6 +447,23 @@ class BatchedKF:
         post = self.empty(len(ty), 27, self.batch) if posterior else None
         check(_lib.lib().kf_score_candidates(self.handle, len(ty), ty.ctypes.data_as(ctypes.c_void_p), int(full),
                                              _ptr(out), _ptr(post), self._stream()))
+        return (out, post) if posterior else out
+
+    def score_rows(self, types, row_masks, posterior=False):
+        """KF_MODEL_REF15 Scheduler.cov_matrix for any measurement rows (kf_score_rows):
+        candidate c is sensor types[c] updated with the rows of row_masks[c] (bit i = 1-based row
+        i + 1 of its H).  Returns gain [n, B] (posterior traces) and, with posterior=True, the
+        block-packed posteriors [n, 27, B]."""
+        if self.model != 'ref15':
+            raise ValueError('score_rows needs a ref15 handle')
+        ty = np.ascontiguousarray(types, dtype=np.int32)
+        mk = np.ascontiguousarray(row_masks, dtype=np.uint32)
+        if ty.shape != mk.shape or ty.ndim != 1:
+            raise ValueError('score_rows: types and row_masks must be 1-D of one length')
+        out = self.empty(len(ty), self.batch)
+        post = self.empty(len(ty), 27, self.batch) if posterior else None
+        check(_lib.lib().kf_score_rows(self.handle, len(ty), ty.ctypes.data_as(ctypes.c_void_p),
+                                       mk.ctypes.data_as(ctypes.c_void_p), _ptr(out), _ptr(post), self._stream()))
         return (out, post) if posterior else out
 
     def run_scheduled(self, t, etype, payload, prev_time, freq):

@@ -107,8 +107,16 @@ class KF_SensorFusion:
         return np.dot(np.dot(P_next, H.T), np.linalg.inv(np.dot(np.dot(H, P_next), H.T) + R))
 
     def run_kalman_filter(self):
-        """hw5_2.py:313-380: [(x, y, theta), ...]."""
-        return ref8.run_kalman_filter(self.indexed_sensor_data, self.dtype, self.device)
+        """hw5_2.py:313-380: [(x, y, theta), ...], with the constants of this object's getters
+        (a subclass may replace them with diagonal ones) and ``self.P0``."""
+        from .ref15 import ModelConsts
+        c = ModelConsts.from_matrices('ref8', F=self.get_state_transition_matrix,
+                                      Q=self.get_process_noise_covariance_matrix,
+                                      H_gps=self.get_gps_observation_matrix(), H_imu=self.get_imu_observation_matrix(),
+                                      R_gps=self.get_gps_measurement_noise_covariance_matrix(),
+                                      R_imu=self.get_imu_measurement_noise_covariance_matrix(),
+                                      P0=getattr(self, 'P0', None))
+        return ref8.run_kalman_filter(self.indexed_sensor_data, self.dtype, self.device, consts=c)
 
     def run_dead_reckoning_for_IMU(self):
         raise NotImplementedError('hw5_2.run_dead_reckoning_for_IMU is a plotting aid, out of scope')

@@ -123,14 +123,21 @@ class CovList(Sequence):
 # Scheduler (kf_workers.py:99-233)
 # ------------------------------------------------------------------------------------------
 
-def _sensor_of(R, H):
-    """Which of the model's sensors (R, H) describe; custom matrices are rejected (the kernels
-    carry the reference's constants)."""
+def _sensor_of(R, H, consts=None):
+    """(sensor, constants) for a sensor's (R, H): H must be the model's GPS or IMU observation
+    matrix (the engine's update selects those states), R a diagonal noise of its size — the
+    reference's or a caller's (kf_workers.py:112-147 takes any R, H; a coupled R or another H
+    raises ValueError).  consts: the ModelConsts to extend (the other sensor's R)."""
     for name, (r, h) in _MODEL_RH.items():
-        if np.shape(R) == r.shape and np.shape(H) == h.shape and np.array_equal(R, r) and np.array_equal(H, h):
-            return name
-    raise ValueError('Scheduler: R/H are not the reference model\'s GPS or IMU matrices; the engine scores '
-                     'the reference constants only')
+        if np.shape(H) == h.shape and np.array_equal(np.asarray(H, np.float64), h):
+            if np.shape(R) != r.shape:
+                raise ValueError(f'Scheduler: R is {np.shape(R)}, the {name} sensor has {r.shape[0]} rows')
+            base = consts or ref15.ModelConsts('ref15')
+            kw = dict(q=base.q, r_imu=base.r_imu, r_gps=base.r_gps, p0=base.p0)
+            c = ref15.ModelConsts.from_matrices('ref15', **{'R_gps' if name == 'GPS' else 'R_imu': R})
+            kw['r_gps' if name == 'GPS' else 'r_imu'] = c.r_gps if name == 'GPS' else c.r_imu
+            return name, ref15.ModelConsts('ref15', **kw)
+    raise ValueError('Scheduler: H is not the reference model\'s GPS or IMU observation matrix')
 
 
 class Scheduler:
@@ -139,21 +146,21 @@ class Scheduler:
 
     def cov_matrix(_, S, Sigma_prev, R, H, device='cuda'):
         """Posterior covariance after an update with measurement rows S (1-based) of the sensor
-        (R, H) — the reference only uses S = [1] and S = all rows (kf_workers.py:112-172)."""
+        (R, H) (kf_workers.py:112-172): S = [1] and S = every row as the reference's own callers
+        use them, any other subset through kf_score_rows (H_hat = H[S], R_hat = R[S, S])."""
         assert type(S) == list, "S should be a list"
         assert len(S) > 0, "S should not be empty"
         assert type(Sigma_prev) == np.ndarray, "Sigma_prev should be a np.ndarray array"
         assert type(R) == np.ndarray, "R should be a np.ndarray array"
         assert type(H) == np.ndarray, "H should be a np.ndarray array"
-        sensor = _sensor_of(R, H)
+        sensor, consts = _sensor_of(R, H)
         rows = sorted(S)
-        if rows == list(range(1, R.shape[0] + 1)):
-            full = True
-        elif rows == [1]:
-            full = False
+        if not all(1 <= r <= R.shape[0] for r in rows):
+            raise IndexError(f'cov_matrix: rows {rows} outside 1..{R.shape[0]}')
+        if rows == list(range(1, R.shape[0] + 1)) or rows == [1]:
+            _, post = _score(Sigma_prev[None], [sensor], rows != [1], posterior=True, consts=consts)
         else:
-            raise NotImplementedError('cov_matrix: S must be [1] or every row (the reference uses only those)')
-        _, post = _score(Sigma_prev[None], [sensor], full, posterior=True)
+            _, post = _score_rows(Sigma_prev[None], [sensor], [sum(1 << (r - 1) for r in set(rows))], consts)
         return from_blocks(post[0, :, 0])
 
     def gain(self, measurement=None, S_sigma=None, measurement_cov=(tuple), observation_cov=(tuple), device='cuda'):
@@ -165,8 +172,8 @@ class Scheduler:
         s = measurement[1]
         if s not in ('GPS', 'IMU'):
             return None
-        _sensor_of(measurement_cov[s], observation_cov[s])
-        return float(_score(np.asarray(S_sigma)[None], [s], False)[0][0, 0])
+        _, consts = _sensor_of(measurement_cov[s], observation_cov[s])
+        return float(_score(np.asarray(S_sigma)[None], [s], False, consts=consts)[0][0, 0])
 
     def random_schedule(self, num_measurements=None):
         """kf_workers.py:188-193 (the global NumPy RNG, as the reference)."""
@@ -180,9 +187,10 @@ class Scheduler:
         assert measurements is not None, "measurements should not be None"
         if len(measurements) == 0:
             raise ValueError('None is not in list')  # the reference's measurements.index(None) (:213)
+        consts = None
         for s in ('GPS', 'IMU'):
-            _sensor_of(measurement_cov[s], observation_cov[s])
-        g = _score(np.asarray(S_sigma)[None], ['GPS', 'IMU'], False)[0][:, 0]
+            _, consts = _sensor_of(measurement_cov[s], observation_cov[s], consts)
+        g = _score(np.asarray(S_sigma)[None], ['GPS', 'IMU'], False, consts=consts)[0][:, 0]
         best, best_i = -np.inf, None
         for i, m in enumerate(measurements):
             v = g[0] if m[1] == 'GPS' else g[1]
@@ -198,10 +206,10 @@ class Scheduler:
         return None  # the reference's is a stub (kf_workers.py:215-216)
 
 
-def _score(Ps, sensors, full, posterior=False, dtype='f64', device=0):
+def _score(Ps, sensors, full, posterior=False, dtype='f64', device=0, consts=None):
     Ps = np.asarray(Ps, np.float64)
     B = Ps.shape[0]
-    kf = ref15.BatchedKF('ref15', B, dtype, device=device)
+    kf = ref15.BatchedKF('ref15', B, dtype, device=device, params=ref15._params(consts))
     kf.set_state(np.zeros((15, B)), np.ascontiguousarray(ref15.to_blocks(Ps).T))
     ty = [_lib.KF_EVENT_GPS if s == 'GPS' else _lib.KF_EVENT_IMU for s in sensors]
     r = kf.score_candidates(ty, full=full, posterior=posterior)
@@ -209,6 +217,20 @@ def _score(Ps, sensors, full, posterior=False, dtype='f64', device=0):
         out = (r[0].double().cpu().numpy(), r[1].double().cpu().numpy())
     else:
         out = (r.double().cpu().numpy(), None)
+    kf.close()
+    return out
+
+
+def _score_rows(Ps, sensors, masks, consts=None, dtype='f64', device=0):
+    """(gain [n, B], posterior blocks [n, 27, B]) for candidates (sensor, row mask) on covariances
+    Ps [B, 15, 15] (kf_score_rows)."""
+    Ps = np.asarray(Ps, np.float64)
+    B = Ps.shape[0]
+    kf = ref15.BatchedKF('ref15', B, dtype, device=device, params=ref15._params(consts))
+    kf.set_state(np.zeros((15, B)), np.ascontiguousarray(ref15.to_blocks(Ps).T))
+    ty = [_lib.KF_EVENT_GPS if s == 'GPS' else _lib.KF_EVENT_IMU for s in sensors]
+    g, post = kf.score_rows(ty, masks, posterior=True)
+    out = (g.double().cpu().numpy(), post.double().cpu().numpy())
     kf.close()
     return out
 
@@ -254,6 +276,10 @@ class KF_SensorFusion:
         self.dtype = dtype
         self.device = device
         self.events = None  # the EventStream behind indexed_sensor_data, once combined
+        # the drivers' cold-start covariance (the reference's literal, kf_workers.py:651); a
+        # diagonal replacement (e.g. the notebook's diag(1000, 100, ..., 1000),
+        # KF_SensorFusion.ipynb:814) runs on the engine too
+        self.P0 = ref15.P0.copy()
 
     def set_processing_frequency(self, frequency):
         self.processing_frequency = frequency
@@ -357,6 +383,20 @@ class KF_SensorFusion:
         return np.dot(np.dot(P_next, H.T), np.linalg.inv(np.dot(np.dot(H, P_next), H.T) + R))
 
     # -- drivers ---------------------------------------------------------------------------
+    def _consts(self):
+        """The model constants the drivers run with, read from this object's getters (which a
+        subclass or a class_args caller may replace, kf_workers.py:1242-1251) and P0."""
+        return _consts_of({'get_state_transition_matrix': self.get_state_transition_matrix,
+                           'get_process_noise_covariance_matrix': self.get_process_noise_covariance_matrix,
+                           'predict_covariance': self.predict_covariance,
+                           'get_gps_observation_matrix': self.get_gps_observation_matrix,
+                           'get_gps_measurement_noise_covariance_matrix':
+                               self.get_gps_measurement_noise_covariance_matrix,
+                           'get_imu_observation_matrix': self.get_imu_observation_matrix,
+                           'get_imu_measurement_noise_covariance_matrix':
+                               self.get_imu_measurement_noise_covariance_matrix,
+                           'calculate_kalman_gain': self.calculate_kalman_gain}, self.P0)
+
     def _ev(self):
         return self.events if self.events is not None else self.indexed_sensor_data
 
@@ -365,7 +405,8 @@ class KF_SensorFusion:
         """kf_workers.py:623-728; also keeps _ground_truth / _ground_truth_cov (:723-724)."""
         ev = self._ev()
         if isinstance(ev, ingest.EventStream):
-            r = ref15.run_full_stream(ev, start_idx, end_idx, initial_pt, initial_state, self.dtype, cov=True)
+            r = ref15.run_full_stream(ev, start_idx, end_idx, initial_pt, initial_state, self.dtype, cov=True,
+                                      consts=self._consts())
             if r is None:
                 return [], [], []
             t, traj, ld, P, prev, covb = r
@@ -376,7 +417,7 @@ class KF_SensorFusion:
                 print(f"Full Kalman Filter (GPU): processed {len(t) - 1} measurements")
         else:
             out = ref15.run_kalman_filter_full(ev, start_idx, end_idx, initial_pt, initial_state, print_output,
-                                               self.dtype, self.device)
+                                               self.dtype, self.device, consts=self._consts())
             if len(out) == 3:
                 return out
             states, logdets, P, prev = out
@@ -391,31 +432,33 @@ class KF_SensorFusion:
         return None
 
     def run_kalman_filter(self, start_idx, end_idx):
-        return ref15.run_kalman_filter(self.indexed_sensor_data, start_idx, end_idx, self.dtype, self.device)
+        return ref15.run_kalman_filter(self.indexed_sensor_data, start_idx, end_idx, self.dtype, self.device,
+                                       consts=self._consts())
 
     def run_kalman_filter_scheduled(self, start_idx=None, end_idx=None, initial_pt=None, initial_state=None,
                                     selection_method=None, print_output=False):
         return ref15.run_kalman_filter_scheduled(self.indexed_sensor_data, start_idx, end_idx, initial_pt,
                                                  initial_state, selection_method, self.processing_frequency,
-                                                 print_output, self.dtype, self.device)
+                                                 print_output, self.dtype, self.device, consts=self._consts())
 
     def run_adaptive_threshold_kalman_filter(self, start_idx=None, end_idx=None, R_threshold=None, initial_pt=None,
                                              initial_state=None, print_output=False):
         return ref15.run_adaptive_threshold_kalman_filter(self.indexed_sensor_data, start_idx, end_idx, R_threshold,
                                                           initial_pt, initial_state, print_output, self.dtype,
-                                                          self.device)
+                                                          self.device, consts=self._consts())
 
     def run_no_update_kalman_filter(self, start_idx=None, end_idx=None, R_threshold=None, initial_pt=None,
                                     initial_state=None, print_output=False):
         return ref15.run_no_update_kalman_filter(self.indexed_sensor_data, start_idx, end_idx, R_threshold,
-                                                 initial_pt, initial_state, print_output, self.dtype, self.device)
+                                                 initial_pt, initial_state, print_output, self.dtype, self.device,
+                                                 consts=self._consts())
 
     def run_brute_force_kalman_filter_no_sampling_min_usage(self, start_idx=0, end_idx=None, R_threshold=None,
                                                             initial_pt=None, initial_state=None,
                                                             max_combos_in_memory=10000):
         return ref15.run_brute_force_kalman_filter_no_sampling_min_usage(
             self.indexed_sensor_data, start_idx, end_idx, R_threshold, initial_pt, initial_state,
-            max_combos_in_memory=max_combos_in_memory, dtype=self.dtype, device=self.device)
+            max_combos_in_memory=max_combos_in_memory, dtype=self.dtype, device=self.device, consts=self._consts())
 
     def run_dead_reckoning_for_IMU(self):
         return []  # the reference's body is commented out and returns an empty list (kf_workers.py:1394-1425)
@@ -451,19 +494,40 @@ class KF_SensorFusion:
 # module-level helpers
 # ------------------------------------------------------------------------------------------
 
+def _consts_of(class_args, P0=None):
+    """ModelConsts from a class_args dict of the model's callables (kf_workers.py:1242-1251):
+    the reference's F and H with any diagonal Q(dt) = diag(q dt), R_gps, R_imu (and P0).
+    predict_covariance / calculate_kalman_gain must compute the reference's formulas (checked on
+    a probe).  Anything else raises ValueError — the engine's kernels run that model."""
+    get = class_args.get
+    for name, fn, want in (('predict_covariance', get('predict_covariance'), None),
+                           ('calculate_kalman_gain', get('calculate_kalman_gain'), None)):
+        if fn is None:
+            continue
+        rng = np.random.default_rng(7)
+        A = rng.normal(size=(15, 15))
+        P = A @ A.T + 15 * np.eye(15)
+        if name == 'predict_covariance':
+            Fm, Qm = _F(0.37), _Q(0.37)
+            ok = np.allclose(fn(P, Fm, Qm), np.dot(np.dot(Fm, P), Fm.T) + Qm, rtol=1e-12, atol=1e-9)
+        else:
+            ok = np.allclose(fn(P, _H_IMU, _R_IMU), np.dot(np.dot(P, _H_IMU.T),
+                                                            np.linalg.inv(np.dot(np.dot(_H_IMU, P), _H_IMU.T) + _R_IMU)),
+                             rtol=1e-9, atol=1e-12)
+        if not ok:
+            raise ValueError(f'class_args[{name!r}] is not the reference formula (kf_workers.py:546-549, 616-621)')
+    call = lambda k: get(k)() if get(k) is not None else None
+    return ref15.ModelConsts.from_matrices(
+        'ref15', F=get('get_state_transition_matrix'), Q=get('get_process_noise_covariance_matrix'),
+        H_gps=call('get_gps_observation_matrix'), H_imu=call('get_imu_observation_matrix'),
+        R_gps=call('get_gps_measurement_noise_covariance_matrix'),
+        R_imu=call('get_imu_measurement_noise_covariance_matrix'), P0=P0)
+
+
 def evaluate_combo_chunk_worker(chunk, xt, Pt, class_args, prev_time, target_end_time):
-    """kf_workers.py:22-97 for a whole chunk in one kernel launch.  class_args must describe the
-    reference's 15-state model (checked at a probe dt); the kernels carry its constants."""
-    probe = 0.0123
-    checks = [('get_state_transition_matrix', (probe,), _F(probe)),
-              ('get_process_noise_covariance_matrix', (probe,), _Q(probe)),
-              ('get_gps_observation_matrix', (), _H_GPS), ('get_imu_observation_matrix', (), _H_IMU),
-              ('get_gps_measurement_noise_covariance_matrix', (), _R_GPS),
-              ('get_imu_measurement_noise_covariance_matrix', (), _R_IMU)]
-    for name, args, want in checks:
-        if name in class_args and not np.array_equal(class_args[name](*args), want):
-            raise ValueError(f'evaluate_combo_chunk_worker: class_args[{name!r}] is not the reference model')
-    return ref15.evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time)
+    """kf_workers.py:22-97 for a whole chunk in one kernel launch, with the model constants
+    class_args gives (diagonal Q, R: _consts_of; any other model raises ValueError)."""
+    return ref15.evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time, consts=_consts_of(class_args))
 
 
 def find_start_idx_for_time_offset(sensor_fusion, target_seconds):

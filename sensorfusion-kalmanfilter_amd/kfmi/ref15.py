@@ -60,6 +60,130 @@ _ROWS = _LAYOUT[15][0]
 # reference P0 (kf_workers.py:651)
 P0 = np.diag([10000.0] * 3 + [1000.0] * 3 + [1000.0] * 3 + [1000.0] * 3 + [10000.0] * 3)
 
+# H of the models (kf_workers.py:551-579, hw5_2.py:258-278): the engine's update selects these rows
+_H = {15: (np.eye(15)[:3], np.eye(15)), 8: (np.eye(8)[:2], np.eye(8))}
+
+
+class ModelConsts:
+    """Diagonal noise constants of a reference model (include/kf.h kf_params.ref_*): Q rates,
+    R_imu, R_gps and P0 per state, in the model's state order.  The reference hard-codes them in
+    its getters (kf_workers.py:519-614, P0 :651; hw5_2.py:233-304, P0 :317-326) and lets a
+    caller replace the getters through its class_args dict (kf_workers.py:1242-1251); any
+    diagonal choice keeps the covariance block-diagonal over the axis chains, which the engine
+    stores.  ``ModelConsts('ref15')`` is the reference's."""
+
+    def __init__(self, model='ref15', q=None, r_imu=None, r_gps=None, p0=None):
+        from .engine import default_params
+        if model not in ('ref15', 'ref8'):
+            raise ValueError(f'ModelConsts: {model!r} is not a reference model')
+        self.model = model
+        self.n = 15 if model == 'ref15' else 8
+        d = default_params(model)
+        n, g = self.n, 3 if model == 'ref15' else 2
+
+        def vec(v, ref, k, name):
+            a = np.array(ref[:k] if v is None else v, dtype=np.float64).reshape(-1)
+            if a.shape != (k,):
+                raise ValueError(f'ModelConsts: {name} needs {k} values, got {a.shape}')
+            return a
+        self.q = vec(q, d.ref_q, n, 'q')
+        self.r_imu = vec(r_imu, d.ref_r_imu, n, 'r_imu')
+        self.r_gps = vec(r_gps, d.ref_r_gps, g, 'r_gps')
+        self.p0 = vec(p0, d.ref_p0, n, 'p0')
+
+    @property
+    def P0(self):
+        return np.diag(self.p0)
+
+    def Q(self, dt):
+        return np.diag(self.q * dt)
+
+    @property
+    def R_gps(self):
+        return np.diag(self.r_gps)
+
+    @property
+    def R_imu(self):
+        return np.diag(self.r_imu)
+
+    def is_reference(self):
+        return self == ModelConsts(self.model)
+
+    def __eq__(self, other):
+        return isinstance(other, ModelConsts) and self.model == other.model and all(
+            np.array_equal(getattr(self, k), getattr(other, k)) for k in ('q', 'r_imu', 'r_gps', 'p0'))
+
+    def params(self):
+        """kf_params for BatchedKF(model, ..., params=...), or None for the reference's."""
+        if self.is_reference():
+            return None
+        p = _lib.kf_params()
+        for name, v in (('ref_q', self.q), ('ref_r_imu', self.r_imu), ('ref_r_gps', self.r_gps),
+                        ('ref_p0', self.p0)):
+            arr = getattr(p, name)
+            for i, x in enumerate(v):
+                arr[i] = float(x)
+        return p
+
+    def oracle(self):
+        """The same constants as oracle/ref_kf.py's K argument (tests)."""
+        return dict(q=self.q, r_imu=self.r_imu, r_gps=self.r_gps, p0=self.p0)
+
+    @classmethod
+    def from_matrices(cls, model='ref15', F=None, Q=None, H_gps=None, H_imu=None, R_gps=None, R_imu=None, P0=None):
+        """Constants from the reference's getters or a caller's replacements (the class_args
+        callables, kf_workers.py:1242-1251): F(dt), Q(dt) callables, H / R matrices, P0.  Any
+        argument may be None (the reference's).  The engine runs the reference's F and H (a
+        kinematic chain per axis) with Q = diag(q dt) and diagonal R, P0: anything else — a
+        different F or H, a Q not of that form, an R or P0 with an off-diagonal entry — raises
+        ValueError, before any GPU work."""
+        c = cls(model)
+        n = c.n
+        if F is not None:
+            from .kf_workers import _F
+            from .hw5_2 import _F8
+            ref_f = _F if n == 15 else _F8
+            for dt in (0.5, 0.0123, 2.0):
+                if not np.array_equal(np.asarray(F(dt), np.float64), ref_f(dt)):
+                    raise ValueError('ModelConsts: the state transition is not the reference model\'s F(dt) '
+                                     '(the engine\'s kernels run its kinematic chains)')
+        for name, Hm, ref in (('H_gps', H_gps, _H[n][0]), ('H_imu', H_imu, _H[n][1])):
+            if Hm is not None and not (np.shape(Hm) == ref.shape and np.array_equal(np.asarray(Hm, np.float64), ref)):
+                raise ValueError(f'ModelConsts: {name} is not the reference model\'s observation matrix')
+
+        def diag_of(M, k, name):
+            M = np.asarray(M, np.float64)
+            if M.shape != (k, k):
+                raise ValueError(f'ModelConsts: {name} must be {k}x{k}, got {M.shape}')
+            if np.any(M - np.diag(np.diag(M))):
+                raise ValueError(f'ModelConsts: {name} has off-diagonal entries; the engine takes diagonal '
+                                 f'noise and initial covariances (block-diagonal P over the axis chains)')
+            return np.diag(M).copy()
+        if Q is not None:
+            q = diag_of(Q(1.0), n, 'Q(1)')
+            for dt in (0.5, 0.0123, 2.0):
+                if not np.allclose(diag_of(Q(dt), n, f'Q({dt})'), q * dt, rtol=1e-12, atol=0.0):
+                    raise ValueError('ModelConsts: Q(dt) is not diag(q * dt), the reference\'s form '
+                                     '(kf_workers.py:519-544)')
+            c.q = q
+        if R_gps is not None:
+            c.r_gps = diag_of(R_gps, 3 if n == 15 else 2, 'R_gps')
+        if R_imu is not None:
+            c.r_imu = diag_of(R_imu, n, 'R_imu')
+        if P0 is not None:
+            c.p0 = diag_of(P0, n, 'P0')
+        if np.any(c.q < 0) or np.any(c.r_gps <= 0) or np.any(c.r_imu <= 0) or np.any(c.p0 <= 0):
+            raise ValueError('ModelConsts: Q rates must be >= 0 and R, P0 variances > 0')
+        return c
+
+
+def _params(consts):
+    return consts.params() if consts is not None else None
+
+
+def _p0(consts):
+    return consts.P0 if consts is not None else P0
+
 
 def to_blocks(P):
     """n x n (or [..., n, n]) covariance of REF15 (n = 15) or REF8 (n = 8) -> block-packed
@@ -95,14 +219,14 @@ def event_payload(stype, sdata):
     return [float(v) for v in sdata[1:10]]
 
 
-def _run_streams(streams, x0, P0b, dtype='f64', device=0, threshold=None, model='ref15', cov=False):
+def _run_streams(streams, x0, P0b, dtype='f64', device=0, threshold=None, model='ref15', cov=False, consts=None):
     """Run one event list per filter in ONE kf_run_events launch.
 
     streams: list (per filter) of [(type, dt, payload9)]; each stream is preceded by a NONE
     event so row 0 of the outputs holds the initial state and logdet.  x0 [B, n] and P0b
     [B, rows] are the initial states.  Returns traj [T, W, B], logdet [T, B], updated [T, B],
     x [n, B], P blocks [rows, B], status [B] (and cov [T, rows, B] with cov=True) as NumPy
-    arrays."""
+    arrays.  consts: a ModelConsts (None = the reference's constants)."""
     B = len(streams)
     T = 1 + max((len(s) for s in streams), default=0)
     etype = np.full((T, B), NONE, np.uint8)
@@ -113,7 +237,7 @@ def _run_streams(streams, x0, P0b, dtype='f64', device=0, threshold=None, model=
             etype[t, f] = ty
             dt[t, f] = d
             pay[t, :, f] = p
-    kf = BatchedKF(model, B, dtype, device=device)
+    kf = BatchedKF(model, B, dtype, device=device, params=_params(consts))
     npd = np.float64 if dtype == 'f64' else np.float32
     kf.set_state(np.ascontiguousarray(np.asarray(x0, np.float64).T.astype(npd)),
                  np.ascontiguousarray(np.asarray(P0b, np.float64).T.astype(npd)))
@@ -149,14 +273,14 @@ def _cold_start(events, start_idx, stop):
 
 
 def run_kalman_filter_full(events, start_idx=None, end_idx=None, initial_pt=None, initial_state=None,
-                           print_output=False, dtype='f64', device=0):
+                           print_output=False, dtype='f64', device=0, consts=None):
     """kf_workers.py:623-728 on the GPU: returns (states, logdets, P, prev_time) in the
     reference's layout (states = [(t, x, y, z, roll, pitch, yaw), ...]).  ``events`` is the
     reference's event list or a kfmi.ingest.EventStream (then the whole window runs from HBM:
     run_full_stream, with the lists built from its arrays)."""
     from .ingest import EventStream
     if isinstance(events, EventStream):
-        r = run_full_stream(events, start_idx, end_idx, initial_pt, initial_state, dtype)
+        r = run_full_stream(events, start_idx, end_idx, initial_pt, initial_state, dtype, consts=consts)
         if r is None:
             return [], [], []
         t, traj, ld, P, prev = r
@@ -174,7 +298,7 @@ def run_kalman_filter_full(events, start_idx=None, end_idx=None, initial_pt=None
         prev = initial_state[0]
         start_off = start_idx
     else:
-        P = P0
+        P = _p0(consts)
         cs = _cold_start(events, start_idx, end_idx + 1)
         if cs is None:
             return [], [], []
@@ -188,7 +312,7 @@ def run_kalman_filter_full(events, start_idx=None, end_idx=None, initial_pt=None
         stream.append((GPS if stype == 'GPS' else IMU, dt, event_payload(stype, sdata)))
         times.append(t)
         prev = t
-    tr, ld, _, x, Pb, st = _run_streams([stream], x0[None], to_blocks(P)[None], dtype, device)
+    tr, ld, _, x, Pb, st = _run_streams([stream], x0[None], to_blocks(P)[None], dtype, device, consts=consts)
     states = [(initial_state[0] if (initial_pt is not None and initial_state is not None) else
                events[start_off][2], *tr[0, :, 0])]
     states += [(t, *tr[i + 1, :, 0]) for i, t in enumerate(times)]
@@ -199,7 +323,7 @@ def run_kalman_filter_full(events, start_idx=None, end_idx=None, initial_pt=None
 
 
 def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initial_state=None, dtype='f64',
-                    cov=False, parallel=True, parallel_min_events=1 << 16):
+                    cov=False, parallel=True, parallel_min_events=1 << 16, consts=None):
     """run_kalman_filter_full (kf_workers.py:623-728) over an EventStream window, entirely on
     the device: cold-start fix search, per-event dt with the driver's dt < 0 rule
     (kf_events_dt, KF_DT_FULL) and one single-filter kf_run_events launch — or, for windows of
@@ -221,7 +345,7 @@ def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initi
         start_off = start_idx
         t_first = prev0
     else:
-        P = P0
+        P = _p0(consts)
         win = stream.etype[start_idx:min(end_idx + 1, n)]  # the reference searches [start, end] (:655)
         hit = torch.nonzero(win == GPS)
         if hit.numel() == 0:
@@ -232,7 +356,7 @@ def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initi
         prev0 = float(stream.t[start_off])
         t_first = prev0
     T = max(end_idx - start_off, 0)
-    kf = BatchedKF('ref15', 1, dtype, device=dev.index or 0)
+    kf = BatchedKF('ref15', 1, dtype, device=dev.index or 0, params=_params(consts))
     npd = np.float64 if dtype == 'f64' else np.float32
     kf.set_state(x0[:, None].astype(npd), to_blocks(P)[:, None].astype(npd))
     t = stream.t[start_off:start_off + T]
@@ -271,7 +395,8 @@ def run_full_stream(stream, start_idx=None, end_idx=None, initial_pt=None, initi
 parallel_check = {}
 
 
-def run_stream_parallel(et, dt, pay, x0, P0b, chunk=None, warmup=None, dtype='f64', cov=False, options=None):
+def run_stream_parallel(et, dt, pay, x0, P0b, chunk=None, warmup=None, dtype='f64', cov=False, options=None,
+                        consts=None):
     """One filter over a long event stream, parallel over time (kf_run_stream): et [T] uint8,
     dt [T] float64 (the driver's dt rule already applied), pay [T, 9] on the device; x0 [15], P0b
     [27] block-packed initial state.  Returns (traj [T, 6], logdet [T], x [15], P blocks [27],
@@ -282,7 +407,7 @@ def run_stream_parallel(et, dt, pay, x0, P0b, chunk=None, warmup=None, dtype='f6
     BatchedKF options of the handle (e.g. stream_final='on')."""
     dev = et.device
     npd = torch.float64 if dtype == 'f64' else torch.float32
-    kf = BatchedKF('ref15', 1, dtype, device=dev.index or 0, options=options)
+    kf = BatchedKF('ref15', 1, dtype, device=dev.index or 0, options=options, params=_params(consts))
     try:
         kf.set_state(torch.as_tensor(np.asarray(x0, np.float64).reshape(15, 1), dtype=npd, device=dev),
                      torch.as_tensor(np.asarray(P0b, np.float64).reshape(27, 1), dtype=npd, device=dev))
@@ -298,7 +423,7 @@ def run_stream_parallel(et, dt, pay, x0, P0b, chunk=None, warmup=None, dtype='f6
 
 def run_adaptive_threshold_kalman_filter(events, start_idx=None, end_idx=None, R_threshold=None,
                                          initial_pt=None, initial_state=None, print_output=False,
-                                         dtype='f64', device=0):
+                                         dtype='f64', device=0, consts=None):
     """kf_workers.py:959-1058 on the GPU: the update is applied only when logdet(P_pred) >
     R_threshold.  Returns (states, logdets, P, previous_time, measurement_times)."""
     start_idx, end_idx = _window(events, start_idx, end_idx)
@@ -312,7 +437,7 @@ def run_adaptive_threshold_kalman_filter(events, start_idx=None, end_idx=None, R
         prev = initial_state[0]
         start_off = start_idx
     else:
-        P = P0
+        P = _p0(consts)
         cs = _cold_start(events, start_idx, end_idx)
         if cs is None:
             return None
@@ -329,7 +454,7 @@ def run_adaptive_threshold_kalman_filter(events, start_idx=None, end_idx=None, R
         times.append(t)
         prev = t
     tr, ld, up, x, Pb, st = _run_streams([stream], x0[None], to_blocks(P)[None], dtype, device,
-                                         threshold=float(R_threshold))
+                                         threshold=float(R_threshold), consts=consts)
     states = [(t_first, *tr[0, :, 0])] + [(t, *tr[i + 1, :, 0]) for i, t in enumerate(times)]
     logdets = [float(v) for v in ld[:len(times) + 1, 0]]
     mtimes += [t for i, t in enumerate(times) if up[i + 1, 0]]
@@ -338,7 +463,7 @@ def run_adaptive_threshold_kalman_filter(events, start_idx=None, end_idx=None, R
     return states, logdets, from_blocks(Pb[:, 0]), prev, mtimes
 
 
-def run_kalman_filter(events, start_idx, end_idx, dtype='f64', device=0):
+def run_kalman_filter(events, start_idx, end_idx, dtype='f64', device=0, consts=None):
     """kf_workers.py:738-824 on the GPU: x0 = 0, the reference's P0, the window's events from
     its first GPS fix on (that fix at dt = 0), no dt < 0 guard.  Returns (states,
     covariances) — states[0] = (0, 0, 0, 0, 0, 0, 0) and one 15x15 covariance per record, the
@@ -353,14 +478,15 @@ def run_kalman_filter(events, start_idx, end_idx, dtype='f64', device=0):
         stream.append((GPS if stype == 'GPS' else IMU, t - prev, event_payload(stype, sdata)))
         times.append(t)
         prev = t
-    tr, _, _, _, _, _, cv = _run_streams([stream], np.zeros((1, 15)), to_blocks(P0)[None], dtype, device, cov=True)
+    tr, _, _, _, _, _, cv = _run_streams([stream], np.zeros((1, 15)), to_blocks(_p0(consts))[None], dtype, device,
+                                         cov=True, consts=consts)
     states = [(0, *tr[0, :, 0])] + [(t, *tr[i + 1, :, 0]) for i, t in enumerate(times)]
     covs = list(from_blocks(cv[:len(times) + 1, :, 0]))
     return states, covs
 
 
 def run_no_update_kalman_filter(events, start_idx=None, end_idx=None, R_threshold=None, initial_pt=None,
-                                initial_state=None, print_output=False, dtype='f64', device=0):
+                                initial_state=None, print_output=False, dtype='f64', device=0, consts=None):
     """kf_workers.py:1060-1160 on the GPU: the window as KF_EVENT_PREDICT events (every update
     of the reference's loop is commented out), logdet after each.  A dt < 0 event is skipped
     without advancing the previous time (:1113-1116).  Returns (states, logdets, P,
@@ -374,7 +500,7 @@ def run_no_update_kalman_filter(events, start_idx=None, end_idx=None, R_threshol
         prev = initial_state[0]
         start_off = start_idx
     else:
-        P = P0
+        P = _p0(consts)
         cs = _cold_start(events, start_idx, end_idx)
         if cs is None:
             return None
@@ -389,7 +515,7 @@ def run_no_update_kalman_filter(events, start_idx=None, end_idx=None, R_threshol
         stream.append((PREDICT, dt, [0.0] * 9))
         times.append(t)
         prev = t
-    tr, ld, _, _, Pb, _ = _run_streams([stream], x0[None], to_blocks(P)[None], dtype, device)
+    tr, ld, _, _, Pb, _ = _run_streams([stream], x0[None], to_blocks(P)[None], dtype, device, consts=consts)
     states = [(t_first, *tr[0, :, 0])] + [(t, *tr[i + 1, :, 0]) for i, t in enumerate(times)]
     logdets = [float(v) for v in ld[:len(times) + 1, 0]]
     if print_output:
@@ -414,7 +540,7 @@ def _combo_stream(combo, prev_time, target_end):
     return s, times
 
 
-def evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time, dtype='f64', device=0):
+def evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time, dtype='f64', device=0, consts=None):
     """evaluate_combo_chunk_worker (kf_workers.py:22-97) for a whole chunk in ONE launch, one
     filter per combination.  Returns [(0, traj, combo, x_final, None, log_det, k), ...]."""
     if not chunk:
@@ -422,7 +548,7 @@ def evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time, dtype='f64',
     built = [_combo_stream(c, prev_time, target_end_time) for c in chunk]
     B = len(chunk)
     tr, ld, _, x, Pb, st = _run_streams([b[0] for b in built], np.broadcast_to(np.asarray(xt, np.float64), (B, 15)),
-                                        np.broadcast_to(to_blocks(Pt), (B, 27)), dtype, device)
+                                        np.broadcast_to(to_blocks(Pt), (B, 27)), dtype, device, consts=consts)
     results = []
     for f, (combo, (s, times)) in enumerate(zip(chunk, built)):
         if st[f] != 0:  # the worker skips a combination that raised (kf_workers.py:88-91)
@@ -448,7 +574,7 @@ def unrank_combination(n, k, r):
     return out
 
 
-def brute_force_setup(events, start_idx=0, end_idx=None, initial_pt=None, initial_state=None):
+def brute_force_setup(events, start_idx=0, end_idx=None, initial_pt=None, initial_state=None, consts=None):
     """The search's inputs as kf_workers.py:1262-1310 sets them up: (candidates, x0, P0,
     prev_time, target_end, events [n, 11], init [42]), or None when there is no candidate: a
     cold window without a starting fix (:1303-1305), or an empty warm-start window, where the
@@ -464,7 +590,7 @@ def brute_force_setup(events, start_idx=0, end_idx=None, initial_pt=None, initia
         prev_time = initial_state[0]
         cand = list(events[start_idx:end_idx])
     else:
-        Pt = P0
+        Pt = _p0(consts)
         cand, prev_time, started = [], None, False
         for (idx, stype, t, sdata) in events[start_idx:end_idx + 1]:  # the reference's +1 slice
             if not started and stype == 'GPS':
@@ -500,13 +626,13 @@ def first_valid_rank(kf, ev, init, prev_time, target_end, k, lo, hi, threshold):
     return None
 
 
-def brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype='f64', device=0, indices=None):
+def brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype='f64', device=0, indices=None, consts=None):
     """The reference's result dict (kf_workers.py:1358-1367) for combination rank r of size k
     (or the candidate ``indices`` of the subset)."""
     idx = unrank_combination(len(cand), k, r) if indices is None else indices
     combo = tuple(cand[i] for i in idx)
     metric, traj, combo, x_bf, P_bf, log_det, used = evaluate_combo_chunk([combo], xt, Pt, prev_time, target_end,
-                                                                          dtype, device)[0]
+                                                                          dtype, device, consts)[0]
     return {'selected_sensors': combo, 'final_state': x_bf, 'final_covariance': P_bf, 'trajectory': traj,
             'accuracy_metric': metric, 'log_determinants': log_det, 'num_measurements_used': used}
 
@@ -537,7 +663,7 @@ def search_levels(n, dtype='f64', mem_bytes=32 << 30):
 def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end_idx=None, R_threshold=None,
                                                        initial_pt=None, initial_state=None,
                                                        max_combos_in_memory=1 << 22, dtype='f64', device=0,
-                                                       search_mem_bytes=32 << 30):
+                                                       search_mem_bytes=32 << 30, consts=None):
     """kf_workers.py:1218-1392 on the GPU: for k = 1..n, evaluate every k-subset of the candidate
     events and return the first subset, in itertools.combinations order, whose max
     log-determinant is below R_threshold — the reference's result dict — or None.  Sizes whose
@@ -547,7 +673,7 @@ def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end
     kfmi.dist.brute_force_search."""
     if R_threshold is None:
         raise ValueError('R_threshold must be specified for brute force KF.')
-    st = brute_force_setup(events, start_idx, end_idx, initial_pt, initial_state)
+    st = brute_force_setup(events, start_idx, end_idx, initial_pt, initial_state, consts)
     if st is None:
         return None
     cand, xt, Pt, prev_time, target_end, ev, init = st
@@ -556,22 +682,23 @@ def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end
     # buffers would not fit) one filter per subset (kf_eval_combos)
     k_search = search_levels(n, dtype, search_mem_bytes)
     if k_search:
-        kf = BatchedKF('ref15', 1, dtype, device=device)
+        kf = BatchedKF('ref15', 1, dtype, device=device, params=_params(consts))
         try:
             k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=k_search)
         finally:
             kf.close()
         if k:
-            return brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device, indices=idx)
+            return brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device, indices=idx,
+                                      consts=consts)
         if k_search == n:
             return None
     width = int(min(max_combos_in_memory, max(math.comb(n, k) for k in range(k_search + 1, n + 1))))
-    kf = BatchedKF('ref15', width, dtype, device=device)
+    kf = BatchedKF('ref15', width, dtype, device=device, params=_params(consts))
     try:
         for k in range(k_search + 1, n + 1):
             r = first_valid_rank(kf, ev, init, prev_time, target_end, k, 0, math.comb(n, k), R_threshold)
             if r is not None:
-                return brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype, device)
+                return brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype, device, consts=consts)
     finally:
         kf.close()
     return None
@@ -581,7 +708,7 @@ def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end
 # Sensor scheduling (kf_workers.py:99-213, 826-957)
 # --------------------------------------------------------------------------------------------
 
-def scheduler_gain(covariances, types=('GPS', 'IMU'), full=False, dtype='f64', device=0):
+def scheduler_gain(covariances, types=('GPS', 'IMU'), full=False, dtype='f64', device=0, consts=None):
     """Scheduler.gain (kf_workers.py:174-185) for a batch: covariances [B, 15, 15] (block-diagonal)
     -> [B, len(types)] traces of the posterior covariance after a candidate of each type
     (full=False: the reference's cov_matrix(S=[1]); full=True: every row of the sensor),
@@ -590,7 +717,7 @@ def scheduler_gain(covariances, types=('GPS', 'IMU'), full=False, dtype='f64', d
     if Ps.ndim == 2:
         Ps = Ps[None]
     B = Ps.shape[0]
-    kf = BatchedKF('ref15', B, dtype, device=device)
+    kf = BatchedKF('ref15', B, dtype, device=device, params=_params(consts))
     npd = np.float64 if dtype == 'f64' else np.float32
     kf.set_state(np.zeros((15, B), npd), np.ascontiguousarray(to_blocks(Ps).T.astype(npd)))
     g = kf.score_candidates([GPS if s == 'GPS' else IMU for s in types], full=full)
@@ -599,7 +726,7 @@ def scheduler_gain(covariances, types=('GPS', 'IMU'), full=False, dtype='f64', d
     return out
 
 
-def _scheduled_window_events(events, start_idx, end_idx, initial_pt, initial_state):
+def _scheduled_window_events(events, start_idx, end_idx, initial_pt, initial_state, consts=None):
     """Start state and candidate list exactly as run_kalman_filter_scheduled sets them up
     (kf_workers.py:828-877).  Returns (x0, P, prev_time, candidates) or None."""
     if start_idx is None or start_idx < 0:
@@ -612,7 +739,7 @@ def _scheduled_window_events(events, start_idx, end_idx, initial_pt, initial_sta
         x0[0:6] = initial_state[1:7]
         start_off, prev = start_idx, initial_state[0]
     else:
-        P = P0
+        P = _p0(consts)
         cs = _cold_start(events, start_idx, end_idx)
         if cs is None:
             return None
@@ -636,7 +763,7 @@ def _stream_arrays(cands, B=1):
 
 def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt=None, initial_state=None,
                                 selection_method=None, processing_frequency=None, print_output=False,
-                                dtype='f64', device=0):
+                                dtype='f64', device=0, consts=None):
     """kf_workers.py:826-957 on the GPU.  'greedy': windowing, Scheduler scoring and the filter
     all run in kf_run_scheduled; 'random': the pick is np.random.choice over the queue, drawn
     from the global NumPy RNG in the same order as the reference (the windows do not depend on
@@ -645,20 +772,20 @@ def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt
     if selection_method not in ('random', 'greedy'):
         print("Invalid selection_method. Choose either 'random' or 'greedy'.")
         return None
-    w = _scheduled_window_events(events, start_idx, end_idx, initial_pt, initial_state)
+    w = _scheduled_window_events(events, start_idx, end_idx, initial_pt, initial_state, consts)
     if w is None:
         return None, None
     x0, P, prev0, cands = w
     f = float(processing_frequency)
     if selection_method == 'greedy':
-        kf = BatchedKF('ref15', 1, dtype, device=device)
+        kf = BatchedKF('ref15', 1, dtype, device=device, params=_params(consts))
         npd = np.float64 if dtype == 'f64' else np.float32
         kf.set_state(x0[:, None].astype(npd), to_blocks(P)[:, None].astype(npd))
         t, et, pay = _stream_arrays(cands)
         tr, ld, stt, ns = kf.run_scheduled(t[:len(cands) or 1], et[:len(cands) or 1], pay.astype(npd)[:len(cands) or 1],
                                            np.array([prev0]), f)
         # the handle's initial logdet comes from a zero-event pass of the same kernels
-        ld0 = _run_streams([[]], x0[None], to_blocks(P)[None], dtype, device)[1][0, 0]
+        ld0 = _run_streams([[]], x0[None], to_blocks(P)[None], dtype, device, consts=consts)[1][0, 0]
         n = int(ns[0])
         tr, ld, stt = tr.double().cpu().numpy(), ld.double().cpu().numpy(), stt.cpu().numpy()
         xf, Pb = kf.state()
@@ -678,7 +805,8 @@ def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt
             queue = []
             selected.append((GPS if sel[1] == 'GPS' else IMU, sel[2] - prev, event_payload(sel[1], sel[3]), sel[2]))
             prev = sel[2]
-        tr, ld, _, x, Pb, st = _run_streams([[s[:3] for s in selected]], x0[None], to_blocks(P)[None], dtype, device)
+        tr, ld, _, x, Pb, st = _run_streams([[s[:3] for s in selected]], x0[None], to_blocks(P)[None], dtype, device,
+                                            consts=consts)
         states = [(prev0, *tr[0, :, 0])] + [(s[3], *tr[i + 1, :, 0]) for i, s in enumerate(selected)]
         logdets = [float(v) for v in ld[:len(selected) + 1, 0]]
         Pf = from_blocks(Pb[:, 0])
@@ -688,22 +816,22 @@ def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt
 
 
 def sampling_sweep(events, frequencies, start_idx=None, end_idx=None, initial_pt=None, initial_state=None,
-                   dtype='f64', device=0):
+                   dtype='f64', device=0, consts=None):
     """The greedy scheduled filter at every processing frequency in ONE kf_run_scheduled launch
     (one filter per frequency) — the experiment behind the reference's
     sampling_sweep/kf_plot_{10..120}.png.  Returns {f: (states, logdets, P)}."""
-    w = _scheduled_window_events(events, start_idx, end_idx, initial_pt, initial_state)
+    w = _scheduled_window_events(events, start_idx, end_idx, initial_pt, initial_state, consts)
     if w is None:
         return {}
     x0, P, prev0, cands = w
     freqs = np.asarray(frequencies, np.float64)
     B = len(freqs)
     npd = np.float64 if dtype == 'f64' else np.float32
-    kf = BatchedKF('ref15', B, dtype, device=device)
+    kf = BatchedKF('ref15', B, dtype, device=device, params=_params(consts))
     kf.set_state(np.repeat(x0[:, None], B, 1).astype(npd), np.repeat(to_blocks(P)[:, None], B, 1).astype(npd))
     t, et, pay = _stream_arrays(cands, B)
     tr, ld, stt, ns = kf.run_scheduled(t, et, pay.astype(npd), np.full(B, prev0), freqs)
-    ld0 = _run_streams([[]], x0[None], to_blocks(P)[None], dtype, device)[1][0, 0]
+    ld0 = _run_streams([[]], x0[None], to_blocks(P)[None], dtype, device, consts=consts)[1][0, 0]
     tr, ld, stt, ns = tr.double().cpu().numpy(), ld.double().cpu().numpy(), stt.cpu().numpy(), ns.cpu().numpy()
     _, Pb = kf.state()
     Pb = Pb.double().cpu().numpy()

@@ -19,11 +19,12 @@ from .ref15 import GPS, IMU, _run_streams, event_payload, to_blocks
 P0 = np.diag([1000.0, 1000.0, 100.0, 100.0, 100.0, 100.0, 1000.0, 1000.0])
 
 
-def run_kalman_filter(events, dtype='f64', device=0, return_covariance=False):
+def run_kalman_filter(events, dtype='f64', device=0, return_covariance=False, consts=None):
     """hw5_2.py:313-380 on the GPU: x0 = 0, events from the first GPS fix on (that fix at
     dt = 0), no dt < 0 guard (a negative dt is predicted over, as the reference does).
     Returns sf_KF_state = [(x, y, theta), ...] with the initial (0, 0, 0) first (and the final
-    8x8 covariance with return_covariance=True)."""
+    8x8 covariance with return_covariance=True).  consts: a ModelConsts('ref8', ...) (the
+    reference's by default)."""
     stream = []
     prev = None
     for (_, stype, t, sdata) in events:
@@ -33,8 +34,9 @@ def run_kalman_filter(events, dtype='f64', device=0, return_covariance=False):
             continue
         stream.append((GPS if stype == 'GPS' else IMU, t - prev, event_payload(stype, sdata)))
         prev = t
-    tr, _, _, _, Pb, _ = _run_streams([stream], np.zeros((1, 8)), to_blocks(P0)[None], dtype, device,
-                                      model='ref8')
+    P = consts.P0 if consts is not None else P0
+    tr, _, _, _, Pb, _ = _run_streams([stream], np.zeros((1, 8)), to_blocks(P)[None], dtype, device,
+                                      model='ref8', consts=consts)
     states = [tuple(tr[i, :, 0]) for i in range(len(stream) + 1)]
     if return_covariance:
         from .ref15 import from_blocks

@@ -102,3 +102,60 @@ def test_euler_to_rotation_matrix_composition():
     # the x axis after a pitch then a yaw
     np.testing.assert_allclose(sf.euler_to_rotation_matrix(0.0, a, a) @ [1, 0, 0],
                                [np.cos(a) * np.cos(a), np.sin(a) * np.cos(a), -np.sin(a)], atol=1e-15)
+
+
+# ------------------------------------------------------------------------------------------
+# model constants (kf_params.ref_*): the class_args / getter replacements the engine accepts
+# ------------------------------------------------------------------------------------------
+
+def test_model_consts_reference_values():
+    """kf_default_params for the reference models = the getters' constants (kf_workers.py:519-614,
+    :651; hw5_2.py:233-304, :317-326); the reference's constants hand the handle no params."""
+    from oracle import ref_kf
+    c = ref15.ModelConsts('ref15')
+    np.testing.assert_array_equal(c.Q(0.37), ref_kf.Q_ref15(0.37))
+    np.testing.assert_array_equal(c.R_imu, ref_kf.R_imu15())
+    np.testing.assert_array_equal(c.R_gps, ref_kf.R_gps15())
+    np.testing.assert_array_equal(c.P0, ref_kf.P0_REF15)
+    assert c.is_reference() and c.params() is None
+    c8 = ref15.ModelConsts('ref8')
+    np.testing.assert_array_equal(c8.Q(0.37), ref_kf.Q_ref8(0.37))
+    np.testing.assert_array_equal(c8.R_imu, ref_kf.R_imu8())
+    np.testing.assert_array_equal(c8.P0, ref_kf.P0_REF8)
+    custom = ref15.ModelConsts('ref15', p0=np.r_[[1000.0] * 3, [100.0] * 9, [1000.0] * 3])  # KF_SensorFusion.ipynb:814
+    p = custom.params()
+    assert p is not None and list(p.ref_p0)[:3] == [1000.0] * 3 and list(p.ref_q)[:3] == [5.0] * 3
+
+
+def test_model_consts_from_getters_accepts_diagonal_rejects_coupling():
+    from kfmi import kf_workers as kw
+    c = ref15.ModelConsts.from_matrices('ref15', F=kw._F, Q=kw._Q, H_gps=kw._H_GPS, H_imu=kw._H_IMU,
+                                        R_gps=kw._R_GPS, R_imu=kw._R_IMU)
+    assert c.is_reference()
+    q2 = lambda dt: 2.0 * kw._Q(dt)
+    c = ref15.ModelConsts.from_matrices('ref15', Q=q2, R_gps=np.diag([1.0, 2.0, 4.0]))
+    np.testing.assert_array_equal(c.q, 2 * ref15.ModelConsts('ref15').q)
+    np.testing.assert_array_equal(c.r_gps, [1.0, 2.0, 4.0])
+    with pytest.raises(ValueError, match='off-diagonal'):
+        R = np.diag([3.0, 3.0, 3.0])
+        R[0, 1] = R[1, 0] = 0.5   # correlated GPS axes couple chains
+        ref15.ModelConsts.from_matrices('ref15', R_gps=R)
+    with pytest.raises(ValueError, match='diag'):
+        ref15.ModelConsts.from_matrices('ref15', Q=lambda dt: kw._Q(dt) + np.eye(15) * 0.1)  # not q * dt
+    with pytest.raises(ValueError, match='observation'):
+        ref15.ModelConsts.from_matrices('ref15', H_gps=np.eye(15)[3:6])
+    with pytest.raises(ValueError, match='transition'):
+        ref15.ModelConsts.from_matrices('ref15', F=lambda dt: np.eye(15))
+    with pytest.raises(ValueError):
+        ref15.ModelConsts.from_matrices('ref15', R_imu=np.diag([0.0] + [1.0] * 14))
+
+
+def test_class_args_worker_checks_formulas():
+    from kfmi import kf_workers as kw
+    bad = {'calculate_kalman_gain': lambda P, H, R: np.dot(P, H.T)}
+    with pytest.raises(ValueError, match='calculate_kalman_gain'):
+        kw._consts_of(bad)
+    ok = {'predict_covariance': lambda P, F, Q: F @ P @ F.T + Q,
+          'get_imu_measurement_noise_covariance_matrix': lambda: np.diag(np.arange(1.0, 16.0))}
+    c = kw._consts_of(ok)
+    np.testing.assert_array_equal(c.r_imu, np.arange(1.0, 16.0))
