@@ -130,7 +130,8 @@ const char* kf_version(void);
  *   KF_OPT_START_THREADS  kf_run_stream: threads per block of the start kernel; 0 = 256
  *   KF_OPT_SEARCH_KERNEL  kf_search_combos: 0 = per level, 1 = child-major, 2 = parent-major
  *   KF_OPT_SEARCH_PM      kf_search_combos' parent-major kernel: 0 = parent in LDS, 1 = registers
- *   KF_OPT_SCHED_KERNEL   kf_run_scheduled: 0 = auto, 1 = the register-input kernel
+ *   KF_OPT_SCHED_KERNEL   kf_run_scheduled: 0 = auto (the two-pass run where legal), 1 = the fused
+ *                         register-input kernel, 2 = the fused LDS-input kernel
  * KF_EINVAL for an unknown option or an out-of-range value. */
 #define KF_OPT_PREDICT        1
 #define KF_OPT_CV_KERNEL      2
@@ -356,7 +357,11 @@ int kf_score_rows(kf_batch* handle, int n_cand, const int32_t* types, const uint
                   void* post, void* stream);
 
 /* KF_MODEL_REF15 rate-decimated greedy filter (run_kalman_filter_scheduled with
- * selection_method='greedy', kf_workers.py:826-957), per filter in one launch.  Streams:
+ * selection_method='greedy', kf_workers.py:826-957), per filter.  By default two passes: the
+ * windows and picks from the event times and types (the greedy pick's gains differ only in R,
+ * so the constants decide it), then the picked events, with the gains checked on the covariance
+ * wherever both sensor classes were queued; a filter where they disagree (a NaN covariance, a
+ * rounding tie) is rerun by the fused kernel.  The handle keeps a [T][B] pick workspace.  Streams:
  * t device [T][B] absolute event times (double), etype device [T][B] (KF_EVENT_GPS|IMU, NONE =
  * padding at the end), payload device [T][9][B].  prev_time device [B]: time of the state in the
  * handle.  Events within 1/f of the last processed one are queued; the first event past the

@@ -52,6 +52,9 @@ struct kf_batch {
     // reference models: the caller's noise constants on the device when they differ from the
     // reference's (kf_params.ref_*), else nullptr and the kernels built on the reference's literals
     kfmi::RefConsts* kc;
+    double gps_r0, imu_r0;   // R_gps[0], R_imu[0]: which sensor the greedy scheduler picks
+    void* sched_ws;          // kf_run_scheduled's two passes: picks [T][B] u32, flags [B] (grown on demand)
+    size_t sched_ws_bytes;
 };
 
 namespace {
@@ -292,8 +295,8 @@ int kf_set_option(kf_batch* h, int option, int64_t value) {
         case KF_OPT_PREDICT:
         case KF_OPT_STREAM:
         case KF_OPT_STREAM_FINAL:
-        case KF_OPT_SEARCH_PM:
-        case KF_OPT_SCHED_KERNEL: ok = value == 0 || value == 1; break;
+        case KF_OPT_SEARCH_PM: ok = value == 0 || value == 1; break;
+        case KF_OPT_SCHED_KERNEL: ok = value >= 0 && value <= 2; break;
         case KF_OPT_CV_KERNEL: ok = value == 0 || value == 1 || value == 2 || value == 4 || value == 8; break;
         case KF_OPT_BLOCKS_PER_CU: ok = value == 0 || (value >= 2 && value <= 8); break;
         case KF_OPT_EVENTS_KERNEL: ok = value >= 0 && value <= 3; break;
@@ -408,6 +411,8 @@ int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_pa
     h->device = dev;
     if (params) h->params = *params;
     else kf_default_params(model, &h->params);
+    h->gps_r0 = h->params.ref_r_gps[0];
+    h->imu_r0 = h->params.ref_r_imu[0];
     h->r_diag = true;
     for (int i = 0; i < h->m; ++i)
         for (int j = 0; j < h->m; ++j)
@@ -477,6 +482,7 @@ int kf_free(kf_batch* h) {
     if (h->pend_u) (void)hipFree(h->pend_u);
     if (h->pend_done) (void)hipEventDestroy(h->pend_done);
     if (h->kc) (void)hipFree(h->kc);
+    if (h->sched_ws) (void)hipFree(h->sched_ws);
     delete h;
     return KF_OK;
 }
@@ -1212,6 +1218,25 @@ int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, 
     a.sel_time = sel_time;
     a.n_sel = n_sel;
     a.regs = opt(h, KF_OPT_SCHED_KERNEL) == 1;
+    a.fused = opt(h, KF_OPT_SCHED_KERNEL) != 0;
+    // the greedy pick when both sensor classes are queued: the larger R gives the larger
+    // posterior trace (launch_ref15_scheduled; checked on the covariance by the apply pass)
+    a.gps_wins = h->gps_r0 > h->imu_r0 ? 1 : h->gps_r0 < h->imu_r0 ? 0 : -1;
+    if (!a.fused && T > 0 && n_sel && sel_time) {
+        const size_t need = align256(sizeof(uint32_t) * size_t(T) * size_t(h->B)) + align256(sizeof(int32_t) * size_t(h->B));
+        if (h->sched_ws_bytes < need) {
+            if (h->sched_ws) (void)hipFree(h->sched_ws);
+            h->sched_ws = nullptr;
+            h->sched_ws_bytes = 0;
+            if (hipMalloc(&h->sched_ws, need) == hipSuccess) h->sched_ws_bytes = need;
+            else (void)hipGetLastError();  // no workspace: the fused kernel runs
+        }
+        if (h->sched_ws) {
+            a.picks = static_cast<uint32_t*>(h->sched_ws);
+            a.flags = reinterpret_cast<int32_t*>(static_cast<char*>(h->sched_ws) +
+                                                 align256(sizeof(uint32_t) * size_t(T) * size_t(h->B)));
+        }
+    }
     hipError_t e = kfmi::launch_ref15_scheduled(h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_run_scheduled");
 }

@@ -274,6 +274,15 @@ struct Ref15SchedArgs {
     int32_t* n_sel;          // [B]
     bool regs;               // the register-input kernel even where the LDS one is legal (KF_OPT_SCHED_KERNEL)
     const RefConsts* kc;     // the handle's noise constants, or nullptr (the reference's)
+    // two-pass run (launch_ref15_scheduled): a pick pass (windows, queue, greedy rule from the
+    // constants; no covariance) writes picks[s][f] = code << 24 | event index and sel_time, an
+    // apply pass runs the picked events (checking the greedy rule on the covariance wherever
+    // both sensor classes were queued), and the fused kernel reruns any filter flagged there
+    uint32_t* picks;         // [T][B] workspace
+    int32_t* flags;          // [B] workspace: 1 = rerun this filter (the rule and the gains disagreed)
+    const int32_t* only;     // fused kernel: only the filters with only[f] != 0 (nullptr = all)
+    int gps_wins;            // both classes queued: 1 the GPS fix wins, 0 the other event, -1 a tie
+    bool fused;              // the fused kernels (KF_OPT_SCHED_KERNEL 1 / 2) instead of the two passes
 };
 
 enum class Op { Run, Predict, Update, Step, Reset };  // Step: predict + update (kf_capi's deferral)

@@ -2479,6 +2479,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED
     const Ref15SchedArgs a) {
     const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (f >= a.B) return;
+    if (a.only && !a.only[f]) return;  // the two-pass run's fallback: flagged filters only
     const int64_t B = a.B;
     const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
     const uint32_t rb = uint32_t(B) * uint32_t(sizeof(T));
@@ -2571,6 +2572,238 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED
     a.status[f] = L.st;
 }
 
+
+// ------------------------------------------------------------------------------------
+// Two-pass scheduled filter.  The greedy pick (kf_workers.py:195-213) compares two posterior
+// traces tr(P) - |P e_0|^2 / (P_00 + R) whose only difference is R: R_gps[0] for a fix, R_imu[0]
+// for any other event.  Wherever the covariance is finite the pick is therefore decided by the
+// constants alone — the larger R gives the larger trace — so the windows, the queue and the
+// picks need no covariance at all.  Pass 1 (ref15_pick_kernel) runs them from the event times
+// and types only (registers for a handful of scalars, 8 waves per SIMD) and writes each pick as
+// code << 24 | event index (code: event type, both-classes-queued bit, fix-first bit) with its
+// time.  Pass 2 (ref15_apply_kernel) runs the picked events as the fused kernel's apply does,
+// the picked payload rows gathered HBM -> LDS by DMA one pick ahead, and at every pick made with
+// both classes queued it evaluates the two gains on the covariance, as the fused kernel does: if
+// the greedy rule disagrees (a NaN covariance, a rounding tie) the filter is flagged and left
+// untouched, and the fused kernel reruns exactly those filters.  Outputs are the fused kernel's.
+// ------------------------------------------------------------------------------------
+constexpr int kPickBoth = 0x10, kPickGpsFirst = 0x20;
+
+// payload element i of this lane in the apply pass's image ([9][W / 4][64] dwords: the gather
+// moves 4 B per lane and instruction), read from LDS where the update uses it
+template <typename T>
+struct LdsGathered {
+    const uint32_t* img;  // image base + lane
+    __device__ __forceinline__ T operator[](int i) const {
+        if constexpr (sizeof(T) == 8) {
+            const v2u u = {img[(2 * i) * 64], img[(2 * i + 1) * 64]};
+            return __builtin_bit_cast(T, u);
+        } else {
+            return __builtin_bit_cast(T, img[i * 64]);
+        }
+    }
+};
+
+#ifndef KF_PICK_CHUNK
+#define KF_PICK_CHUNK 8
+#endif
+// events per LDS image of the pick pass: its lanes hold a few scalars, so the LDS, not the
+// registers, sets its waves per SIMD (8 events: 4 workgroups of 4 waves per CU)
+constexpr int kPickChunk = KF_PICK_CHUNK;
+constexpr int kPickImg = kPickChunk * 512 + kPickChunk * 64;
+__global__ __launch_bounds__(kBlock) void ref15_pick_kernel(const Ref15SchedArgs a) {
+    constexpr int kSchedChunk = kPickChunk, kSchedImg = kPickImg;  // the fused kernel's staging, resized
+    __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * 2 * kSchedImg];
+    const int lane = int(threadIdx.x & 63);
+    const int wave = wave_uniform(int(threadIdx.x >> 6));
+    const int64_t f0 = int64_t(blockIdx.x) * kBlock + int64_t(wave) * 64;
+    if (f0 >= a.B) return;  // whole waves (B % 64 == 0)
+    const int64_t f = f0 + lane;
+    const int64_t B = a.B;
+    unsigned char* const img0 = lds + wave * 2 * kSchedImg;
+    double prev = a.prev_time[f];
+    const double period = 1.0 / (a.freq ? a.freq[f] : a.freq_all);  // kf_workers.py:880
+    int q_len = 0, nsel = 0, qi0 = -1, qi1 = -1, qt0 = 0, qt1 = 0;
+    double qtime0 = 0.0, qtime1 = 0.0;
+    waitcnt<vmcnt_imm(0)>();
+    const uint32_t voff_t = uint32_t(lane >> 5) * uint32_t(B) * 8u + uint32_t(lane & 31) * 16u;
+    const uint32_t voff_e = uint32_t(lane >> 2) * uint32_t(B) + uint32_t(lane & 3) * 16u;
+    auto issue = [&](int c, unsigned char* img) {
+        const int r0 = c * kSchedChunk;
+        const int nr = a.T - r0 < kSchedChunk ? a.T - r0 : kSchedChunk;
+#pragma unroll
+        for (int k = 0; k < kSchedChunk / 2; ++k) {
+            if (2 * k >= nr) break;  // wave-uniform
+            const char* tb = reinterpret_cast<const char*>(a.t) + (int64_t(r0 + 2 * k) * B + f0) * 8;
+            const uint32_t span = 2 * k + 1 < nr ? uint32_t(B) * 8u + 512u : 512u;
+            lds_dma16(bytes_rsrc(tb, span), img + k * 1024, voff_t, 0);
+        }
+        const char* eb = reinterpret_cast<const char*>(a.etype) + int64_t(r0) * B + f0;
+        lds_dma16(bytes_rsrc(eb, uint32_t(nr - 1) * uint32_t(B) + 64u), img + kSchedChunk * 512, voff_e, 0);
+    };
+    const int nch = (a.T + kSchedChunk - 1) / kSchedChunk;
+    if (nch > 0) issue(0, img0);
+    for (int c = 0; c < nch; ++c) {
+        waitcnt<0>();
+        unsigned char* const img = img0 + (c & 1) * kSchedImg;
+        if (c + 1 < nch) issue(c + 1, img0 + ((c + 1) & 1) * kSchedImg);
+        const double* ti_img = reinterpret_cast<const double*>(img) + lane;
+        const unsigned char* ty_img = img + kSchedChunk * 512 + lane;
+        const int r0 = c * kSchedChunk;
+        const int nr = a.T - r0 < kSchedChunk ? a.T - r0 : kSchedChunk;
+#pragma unroll 1
+        for (int d = 0; d < nr; ++d) {
+            const int ty = int(ty_img[d * 64]);
+            const double ti = ti_img[d * 64];
+            const int i = r0 + d;
+            if (ty == 255) continue;  // padding of a ragged stream
+            const bool gps = ty == kGps;
+            const bool window = ti - prev < period;  // SchedLane::event, kf_workers.py:870-957
+            if (window || q_len == 0) {
+                if (gps && qi0 < 0) {
+                    qi0 = i;
+                    qt0 = ty;
+                    qtime0 = ti;
+                }
+                if (!gps && qi1 < 0) {
+                    qi1 = i;
+                    qt1 = ty;
+                    qtime1 = ti;
+                }
+                ++q_len;
+                if (window) continue;
+            }
+            const bool both = qi0 >= 0 && qi1 >= 0;
+            const bool gps_first = qi0 >= 0 && (qi1 < 0 || qi0 < qi1);
+            const bool pick0 = both ? (a.gps_wins > 0 ? true : a.gps_wins == 0 ? false : gps_first) : qi0 >= 0;
+            const int sel = pick0 ? qi0 : qi1;
+            const double tsel = pick0 ? qtime0 : qtime1;
+            const int code = (pick0 ? qt0 : qt1) | (both ? kPickBoth : 0) | (gps_first ? kPickGpsFirst : 0);
+            a.picks[int64_t(nsel) * B + f] = (uint32_t(code) << 24) | uint32_t(sel);
+            if (a.sel_time) a.sel_time[int64_t(nsel) * B + f] = tsel;
+            ++nsel;
+            prev = tsel;
+            q_len = 0;
+            qi0 = qi1 = -1;
+        }
+    }
+    if (a.n_sel) a.n_sel[f] = nsel;
+    a.flags[f] = 0;
+}
+
+template <typename T, bool CUSTOM>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void ref15_apply_kernel(
+    const Ref15SchedArgs a) {
+    constexpr int W = int(sizeof(T));
+    constexpr int NPW = W / 4;            // dwords per payload value
+    constexpr int PAY = 9 * NPW * 256;    // image: payload [9][NPW][64] dwords, then the pick times
+    constexpr int TM_OFF = PAY, IMG = TM_OFF + 512;
+    constexpr int PK = 256;               // a row of picks: 64 u32, three slots (rows q .. q + 2)
+    constexpr int NST = 7;                // traj (6 rows), logdet; absent ones dropped by offset
+    __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * (2 * IMG + 3 * PK)];
+    const int lane = int(threadIdx.x & 63);
+    const int wave = wave_uniform(int(threadIdx.x >> 6));
+    const int64_t f0 = int64_t(blockIdx.x) * kBlock + int64_t(wave) * 64;
+    if (f0 >= a.B) return;  // whole waves (B % 64 == 0)
+    const int64_t f = f0 + lane;
+    const int64_t B = a.B;
+    unsigned char* const img0 = lds + wave * (2 * IMG + 3 * PK);
+    unsigned char* const pk0 = img0 + 2 * IMG;
+    const uint32_t off = uint32_t(f) * uint32_t(W);
+    const uint32_t rb = uint32_t(B) * uint32_t(W);
+    Ref15<T, CUSTOM> s;
+    s.kc = a.kc;
+    s.load(a.x, a.P, rb, off);
+    int32_t st = a.status[f];
+    const int nsel = a.n_sel[f];
+    double prev = a.prev_time[f];
+    int S = nsel;  // the wave's longest pick list
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        const int o = __shfl_xor(S, sh, 64);
+        S = o > S ? o : S;
+    }
+    S = wave_uniform(S);
+    const auto r_tr = span_rsrc(a.traj, 0, rb, uint32_t(S) * 6u);
+    const auto r_ld = span_rsrc(a.logdet, 0, rb, uint32_t(S));
+    waitcnt<vmcnt_imm(0)>();
+    // pick s of this lane: its event's payload rows gathered per lane (the picked rows of a
+    // wave may lie anywhere in [T][9][B]: 64-bit addresses), its time by one wave DMA; a lane
+    // past its list reads row 0 (every lane issues every DMA, so the waits can be counted)
+    auto issue = [&](int sidx, uint32_t pick, unsigned char* img) {
+        const uint32_t ev = pick & 0xFFFFFFu;
+        const int64_t row = (sidx < nsel && ev < uint32_t(a.T)) ? int64_t(ev) : 0;
+        const char* src = reinterpret_cast<const char*>(a.payload) + (row * 9 * B + f) * W;
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+#pragma unroll
+            for (int h = 0; h < NPW; ++h)
+                __builtin_amdgcn_global_load_lds(src + int64_t(i) * B * W + h * 4,
+                                                 (__attribute__((address_space(3))) void*)(img + (i * NPW + h) * 256), 4,
+                                                 0, 0);
+        const char* tb = reinterpret_cast<const char*>(a.sel_time) + (int64_t(sidx) * B + f0) * 8;
+        if (lane < 32) lds_dma16(bytes_rsrc(tb, 512u), img + TM_OFF, uint32_t(lane) * 16u, 0);
+    };
+    // the picks reach LDS by DMA two rows ahead (a register load in the loop made the compiler
+    // drain every store at the back edge to wait for it)
+    auto issue_picks = [&](int r) {
+        const char* pb = reinterpret_cast<const char*>(a.picks) + (int64_t(r) * B + f0) * 4;
+        if (lane < 16) lds_dma16(bytes_rsrc(pb, 256u), pk0 + (r % 3) * PK, uint32_t(lane) * 16u, 0);
+    };
+    auto pick_row = [&](int r) { return reinterpret_cast<const uint32_t*>(pk0 + (r % 3) * PK)[lane]; };
+    if (S > 0) {
+        issue_picks(0);
+        if (S > 1) issue_picks(1);
+        waitcnt<vmcnt_imm(0)>();
+        issue(0, pick_row(0), img0);
+        waitcnt<vmcnt_imm(0)>();  // the first image (no stores yet)
+    }
+    bool bad = false;
+    for (int q = 0; q < S; ++q) {
+        unsigned char* const img = img0 + (q & 1) * IMG;
+        // image q and pick row q + 1 are older than event q - 1's NST stores
+        if (q > 0) waitcnt<vmcnt_imm(NST)>();
+        const double tq = reinterpret_cast<const double*>(img + TM_OFF)[lane];
+        const uint32_t pick_c = pick_row(q);
+        if (q + 1 < S) {
+            issue(q + 1, pick_row(q + 1), img0 + ((q + 1) & 1) * IMG);
+            if (q + 2 < S) issue_picks(q + 2);  // into the slot row q - 1 held
+        }
+        const bool live = q < nsel;
+        const int code = int(pick_c >> 24);
+        const int type = code & 7;
+        if (live && !bad && (code & kPickBoth)) {
+            // the greedy rule on this covariance (SchedLane::event): the pick pass's choice must
+            // be the first candidate with the largest gain
+            const T g0 = first_row_gain(s, kGps), g1 = first_row_gain(s, kImu);
+            const bool v0 = g0 == g0, v1 = g1 == g1;
+            const bool gps_first = (code & kPickGpsFirst) != 0;
+            bool pick0;
+            if (v0 && v1) pick0 = g0 > g1 ? true : (g1 > g0 ? false : gps_first);
+            else if (v0 != v1) pick0 = v0;
+            else pick0 = gps_first;
+            bad = pick0 != (type == kGps);
+        }
+        if (live && !bad) {
+            const LdsGathered<T> pay{reinterpret_cast<const uint32_t*>(img) + lane};  // read where used
+            bool ok = true;
+            s.template event<false>(type, T(tq - prev), pay, false, T(0), ok);
+            if (!ok) {
+                st = kNotSpd;
+                s.fill_nan();
+            }
+            prev = tq;
+        }
+        const uint32_t vo = live ? off : kDropOffset;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) stv(r_tr, (uint32_t(q) * 6u + uint32_t(k)) * rb + vo, s.x[k]);
+        stv(r_ld, uint32_t(q) * rb + vo, s.logdet());
+    }
+    a.flags[f] = bad ? 1 : 0;
+    if (bad) return;  // the fused kernel reruns this filter from the handle's state
+    s.store(a.x, a.P, rb, off);
+    a.status[f] = st;
+}
 }  // namespace
 
 // kernel<..., CUSTOM> for a launch: the reference's constants (kc == nullptr) or the handle's
@@ -2596,10 +2829,29 @@ hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t str
 
 hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream) {
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-    // the LDS variant's descriptors: whole waves, and a chunk's row spans within 32-bit ranges
+    // the LDS variants' descriptors: whole waves, and a chunk's row spans within 32-bit ranges
     const bool lds = a.B % 64 == 0 && uint64_t(a.B) * 8 * 2 < (uint64_t(1) << 32) &&
                      reinterpret_cast<uintptr_t>(a.t) % 16 == 0 && reinterpret_cast<uintptr_t>(a.etype) % 16 == 0 &&
                      uint64_t(a.B) * kSchedChunk < (uint64_t(1) << 32) && !a.regs;
+    // two passes where legal (the host gives them workspace); the pick codes hold 24-bit indices
+    // and the apply pass's record spans 32-bit byte ranges
+    const bool two = lds && !a.fused && a.picks && a.flags && a.n_sel && a.sel_time && a.T < (1 << 24) &&
+                     uint64_t(a.T) * 6u * uint64_t(a.B) * (f64 ? 8u : 4u) < (uint64_t(1) << 32) &&
+                     reinterpret_cast<uintptr_t>(a.sel_time) % 16 == 0;
+    if (two) {
+        ref15_pick_kernel<<<grid, kBlock, 0, stream>>>(a);
+        KF_CUSTOM_DISPATCH(a.kc, {
+            if (f64) ref15_apply_kernel<double, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+            else ref15_apply_kernel<float, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+        });
+        Ref15SchedArgs b = a;  // the flagged filters (usually none: every lane leaves at once)
+        b.only = a.flags;
+        KF_CUSTOM_DISPATCH(a.kc, {
+            if (f64) ref15_sched_kernel<double, CUSTOM><<<grid, kBlock, 0, stream>>>(b);
+            else ref15_sched_kernel<float, CUSTOM><<<grid, kBlock, 0, stream>>>(b);
+        });
+        return hipGetLastError();
+    }
     KF_CUSTOM_DISPATCH(a.kc, {
         if (lds) {
             if (f64) ref15_sched_lds_kernel<double, CUSTOM><<<grid, kBlock, 0, stream>>>(a);

@@ -96,8 +96,17 @@ def test_scheduler_facade(golden_dir):
         q = [('a', 'IMU'), ('b', 'GPS'), ('c', 'IMU'), ('d', 'GPS')]
         want = ref_kf.greedy_schedule([(0, s, 0.0, None) for _, s in q], S)
         assert sch.greedy_schedule(q, S, Rm, Hm) == want
+    # a caller's diagonal R is scored with its own constants (kf_workers.py:112-185 takes any
+    # R); one that couples the axes is not (the engine's chains are independent)
+    S0 = g['sched_sigma'][0]
+    want = np.trace(ref_kf.scheduler_cov_matrix([1], S0, Rm['GPS'] * 2, Hm['GPS']))
+    assert _rel(sch.gain(('x', 'GPS'), S0, {'GPS': Rm['GPS'] * 2}, Hm), want) <= 1e-6
+    Rc = Rm['GPS'].astype(float)
+    Rc[0, 1] = Rc[1, 0] = 0.5
     with pytest.raises(ValueError):
-        sch.gain(('x', 'GPS'), g['sched_sigma'][0], {'GPS': Rm['GPS'] * 2}, Hm)
+        sch.gain(('x', 'GPS'), S0, {'GPS': Rc}, Hm)
+    with pytest.raises(ValueError):
+        sch.gain(('x', 'GPS'), S0, {'GPS': Rm['GPS']}, {'GPS': np.eye(15)[3:6]})
 
 
 def test_combo_worker_with_class_args(golden_dir):
@@ -112,7 +121,17 @@ def test_combo_worker_with_class_args(golden_dir):
     res = kfw.evaluate_combo_chunk_worker(chunk, g['x0'], g['P0'], class_args, float(g['prev_time']),
                                           float(g['target_end']))
     assert _rel([v for r in res for v in r[5]], g['logdet_flat']) <= 1e-6
-    bad = dict(class_args, get_gps_measurement_noise_covariance_matrix=lambda: np.diag([1, 1, 1]))
+    # other diagonal constants run with those constants (the oracle worker with the same K) ...
+    other = dict(class_args, get_gps_measurement_noise_covariance_matrix=lambda: np.diag([1, 1, 1]))
+    res = kfw.evaluate_combo_chunk_worker(chunk, g['x0'], g['P0'], other, float(g['prev_time']),
+                                          float(g['target_end']))
+    K = dict(q=np.diag(ref_kf.Q_ref15(1.0)), r_imu=np.diag(ref_kf.R_imu15()), r_gps=np.ones(3),
+             p0=np.diag(ref_kf.P0_REF15))
+    want = ref_kf.evaluate_combo_chunk(chunk, g['x0'], g['P0'], float(g['prev_time']), float(g['target_end']), K=K)
+    assert _rel([v for r in res for v in r[5]], [v for r in want for v in r[5]]) <= 1e-6
+    # ... a coupled one is refused before any GPU work
+    bad = dict(class_args, get_gps_measurement_noise_covariance_matrix=lambda: np.array(
+        [[3.0, 1.0, 0.0], [1.0, 3.0, 0.0], [0.0, 0.0, 3.0]]))
     with pytest.raises(ValueError):
         kfw.evaluate_combo_chunk_worker(chunk, g['x0'], g['P0'], bad, 0.0, 1.0)
 
