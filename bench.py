@@ -732,12 +732,18 @@ def sched_workload(cfg, args, rank, world, dev):
     # sel_time 8 written; per filter: state (15 + 27) x 8 loaded and stored, prev / freq read,
     # status read + written, n_sel written
     nbytes = B * T * 9 + n_selected * (72 + 64) + B * (2 * 42 * 8 + 8 + 8 + 8 + 4)
+    mode = kf.get_option('sched_kernel')
+    if B % 64:
+        kernel = 'ref15_sched_kernel'
+    elif mode == 0:  # two passes (kf.h KF_OPT_SCHED_KERNEL)
+        kernel = 'ref15_pick_kernel + ref15_apply_kernel (+ ref15_sched_kernel over flagged filters)'
+    else:
+        kernel = 'ref15_sched_lds_kernel' if mode == 2 else 'ref15_sched_kernel'
     return dict(step=step, units=B * T, bytes=nbytes, bytes_per_unit=nbytes / (B * T),
-                kernel='ref15_sched_lds_kernel' if B % 64 == 0 else 'ref15_sched_kernel', traffic=None, cpu=cpu,
-                gather=None, kf=kf,
+                kernel=kernel, traffic=None, cpu=cpu, gather=None, kf=kf,
                 roofline_note=f'{n_selected / (B * T):.3f} of the examined events are selected and applied (a '
-                              f'full 15-state event each, its payload gathered per lane); latency / issue-bound at '
-                              f'2 waves per SIMD',
+                              f'full 15-state event each, its payload gathered per lane); latency / issue-bound: '
+                              f'the time is the launch sequence on the handle\'s stream',
                 desc=f'SURVEY 8f row 3: rate-decimated greedy scheduled filter (kf_workers.py:826-957), reference '
                      f'15-state model, f64, B={B} filters/GPU, T={T} events at 200 Hz (GPS every {k}th), '
                      f'processing rates {cfg["rates"][0]}..{cfg["rates"][-1]} Hz across the batch (64 filters per rate)',

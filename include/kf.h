@@ -132,6 +132,9 @@ const char* kf_version(void);
  *   KF_OPT_SEARCH_PM      kf_search_combos' parent-major kernel: 0 = parent in LDS, 1 = registers
  *   KF_OPT_SCHED_KERNEL   kf_run_scheduled: 0 = auto (the two-pass run where legal), 1 = the fused
  *                         register-input kernel, 2 = the fused LDS-input kernel
+ *   KF_OPT_SCHED_GROUP    kf_run_scheduled's two passes: waves per workgroup, 0 = 4, 1 or 4
+ *                         (one-wave groups free their slot when their wave's pick list ends;
+ *                         measured slower)
  * KF_EINVAL for an unknown option or an out-of-range value. */
 #define KF_OPT_PREDICT        1
 #define KF_OPT_CV_KERNEL      2
@@ -144,7 +147,8 @@ const char* kf_version(void);
 #define KF_OPT_SEARCH_KERNEL  9
 #define KF_OPT_SEARCH_PM      10
 #define KF_OPT_SCHED_KERNEL   11
-#define KF_OPT_COUNT          12
+#define KF_OPT_SCHED_GROUP    12
+#define KF_OPT_COUNT          13
 int kf_set_option(kf_batch* handle, int option, int64_t value);
 int kf_get_option(const kf_batch* handle, int option, int64_t* value);
 

@@ -297,6 +297,7 @@ int kf_set_option(kf_batch* h, int option, int64_t value) {
         case KF_OPT_STREAM_FINAL:
         case KF_OPT_SEARCH_PM: ok = value == 0 || value == 1; break;
         case KF_OPT_SCHED_KERNEL: ok = value >= 0 && value <= 2; break;
+        case KF_OPT_SCHED_GROUP: ok = value == 0 || value == 1 || value == 4; break;
         case KF_OPT_CV_KERNEL: ok = value == 0 || value == 1 || value == 2 || value == 4 || value == 8; break;
         case KF_OPT_BLOCKS_PER_CU: ok = value == 0 || (value >= 2 && value <= 8); break;
         case KF_OPT_EVENTS_KERNEL: ok = value >= 0 && value <= 3; break;
@@ -1219,6 +1220,7 @@ int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, 
     a.n_sel = n_sel;
     a.regs = opt(h, KF_OPT_SCHED_KERNEL) == 1;
     a.fused = opt(h, KF_OPT_SCHED_KERNEL) != 0;
+    a.group_waves = opt(h, KF_OPT_SCHED_GROUP) == 1 ? 1 : 4;
     // the greedy pick when both sensor classes are queued: the larger R gives the larger
     // posterior trace (launch_ref15_scheduled; checked on the covariance by the apply pass)
     a.gps_wins = h->gps_r0 > h->imu_r0 ? 1 : h->gps_r0 < h->imu_r0 ? 0 : -1;

@@ -2607,16 +2607,21 @@ struct LdsGathered {
 #ifndef KF_PICK_CHUNK
 #define KF_PICK_CHUNK 8
 #endif
+#ifndef KF_APPLY_PROBE
+#define KF_APPLY_PROBE 0  // 1 / 2: gather-cost probes for in-process A/B builds (tools/ab_inproc.py)
+#endif
 // events per LDS image of the pick pass: its lanes hold a few scalars, so the LDS, not the
 // registers, sets its waves per SIMD (8 events: 4 workgroups of 4 waves per CU)
 constexpr int kPickChunk = KF_PICK_CHUNK;
 constexpr int kPickImg = kPickChunk * 512 + kPickChunk * 64;
-__global__ __launch_bounds__(kBlock) void ref15_pick_kernel(const Ref15SchedArgs a) {
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void ref15_pick_kernel(const Ref15SchedArgs a) {
     constexpr int kSchedChunk = kPickChunk, kSchedImg = kPickImg;  // the fused kernel's staging, resized
-    __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * 2 * kSchedImg];
+    static_assert(kSchedChunk % 2 == 0 && kSchedChunk <= 16, "t rows move in pairs; etype rows 4 lanes each");
+    __shared__ __attribute__((aligned(16))) unsigned char lds[WAVES * 2 * kSchedImg];
     const int lane = int(threadIdx.x & 63);
-    const int wave = wave_uniform(int(threadIdx.x >> 6));
-    const int64_t f0 = int64_t(blockIdx.x) * kBlock + int64_t(wave) * 64;
+    const int wave = WAVES == 1 ? 0 : wave_uniform(int(threadIdx.x >> 6));
+    const int64_t f0 = int64_t(blockIdx.x) * (WAVES * 64) + int64_t(wave) * 64;
     if (f0 >= a.B) return;  // whole waves (B % 64 == 0)
     const int64_t f = f0 + lane;
     const int64_t B = a.B;
@@ -2638,8 +2643,11 @@ __global__ __launch_bounds__(kBlock) void ref15_pick_kernel(const Ref15SchedArgs
             const uint32_t span = 2 * k + 1 < nr ? uint32_t(B) * 8u + 512u : 512u;
             lds_dma16(bytes_rsrc(tb, span), img + k * 1024, voff_t, 0);
         }
+        // 4 lanes per etype row: the lanes past this chunk's rows would write zeros (their rows
+        // are out of the descriptor's range) beyond the image
         const char* eb = reinterpret_cast<const char*>(a.etype) + int64_t(r0) * B + f0;
-        lds_dma16(bytes_rsrc(eb, uint32_t(nr - 1) * uint32_t(B) + 64u), img + kSchedChunk * 512, voff_e, 0);
+        if (lane < 4 * kSchedChunk)
+            lds_dma16(bytes_rsrc(eb, uint32_t(nr - 1) * uint32_t(B) + 64u), img + kSchedChunk * 512, voff_e, 0);
     };
     const int nch = (a.T + kSchedChunk - 1) / kSchedChunk;
     if (nch > 0) issue(0, img0);
@@ -2691,8 +2699,8 @@ __global__ __launch_bounds__(kBlock) void ref15_pick_kernel(const Ref15SchedArgs
     a.flags[f] = 0;
 }
 
-template <typename T, bool CUSTOM>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void ref15_apply_kernel(
+template <typename T, bool CUSTOM, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void ref15_apply_kernel(
     const Ref15SchedArgs a) {
     constexpr int W = int(sizeof(T));
     constexpr int NPW = W / 4;            // dwords per payload value
@@ -2700,10 +2708,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     constexpr int TM_OFF = PAY, IMG = TM_OFF + 512;
     constexpr int PK = 256;               // a row of picks: 64 u32, three slots (rows q .. q + 2)
     constexpr int NST = 7;                // traj (6 rows), logdet; absent ones dropped by offset
-    __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * (2 * IMG + 3 * PK)];
+    __shared__ __attribute__((aligned(16))) unsigned char lds[WAVES * (2 * IMG + 3 * PK)];
     const int lane = int(threadIdx.x & 63);
-    const int wave = wave_uniform(int(threadIdx.x >> 6));
-    const int64_t f0 = int64_t(blockIdx.x) * kBlock + int64_t(wave) * 64;
+    const int wave = WAVES == 1 ? 0 : wave_uniform(int(threadIdx.x >> 6));
+    const int64_t f0 = int64_t(blockIdx.x) * (WAVES * 64) + int64_t(wave) * 64;
     if (f0 >= a.B) return;  // whole waves (B % 64 == 0)
     const int64_t f = f0 + lane;
     const int64_t B = a.B;
@@ -2724,18 +2732,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
         S = o > S ? o : S;
     }
     S = wave_uniform(S);
-    const auto r_tr = span_rsrc(a.traj, 0, rb, uint32_t(S) * 6u);
-    const auto r_ld = span_rsrc(a.logdet, 0, rb, uint32_t(S));
     waitcnt<vmcnt_imm(0)>();
     // pick s of this lane: its event's payload rows gathered per lane (the picked rows of a
     // wave may lie anywhere in [T][9][B]: 64-bit addresses), its time by one wave DMA; a lane
     // past its list reads row 0 (every lane issues every DMA, so the waits can be counted)
     auto issue = [&](int sidx, uint32_t pick, unsigned char* img) {
         const uint32_t ev = pick & 0xFFFFFFu;
+#if KF_APPLY_PROBE == 1  // timing probe (wrong results): every lane gathers lane 0's row
+        const int64_t row = __shfl((sidx < nsel && ev < uint32_t(a.T)) ? int(ev) : 0, 0, 64);
+#else
         const int64_t row = (sidx < nsel && ev < uint32_t(a.T)) ? int64_t(ev) : 0;
+#endif
         const char* src = reinterpret_cast<const char*>(a.payload) + (row * 9 * B + f) * W;
 #pragma unroll
         for (int i = 0; i < 9; ++i)
+#if KF_APPLY_PROBE == 2  // timing probe (wrong results): no payload gather
+            if (sidx < 0)
+#endif
 #pragma unroll
             for (int h = 0; h < NPW; ++h)
                 __builtin_amdgcn_global_load_lds(src + int64_t(i) * B * W + h * 4,
@@ -2794,10 +2807,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
             }
             prev = tq;
         }
+        // a record's descriptor per pick (the records of the whole run exceed 32-bit offsets)
         const uint32_t vo = live ? off : kDropOffset;
+        const auto r_tr = span_rsrc(a.traj, int64_t(q) * 6, rb, 6u);
 #pragma unroll
-        for (int k = 0; k < 6; ++k) stv(r_tr, (uint32_t(q) * 6u + uint32_t(k)) * rb + vo, s.x[k]);
-        stv(r_ld, uint32_t(q) * rb + vo, s.logdet());
+        for (int k = 0; k < 6; ++k) stv(r_tr, uint32_t(k) * rb + vo, s.x[k]);
+        stv(span_rsrc(a.logdet, q, rb, 1u), vo, s.logdet());
     }
     a.flags[f] = bad ? 1 : 0;
     if (bad) return;  // the fused kernel reruns this filter from the handle's state
@@ -2834,16 +2849,27 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
                      reinterpret_cast<uintptr_t>(a.t) % 16 == 0 && reinterpret_cast<uintptr_t>(a.etype) % 16 == 0 &&
                      uint64_t(a.B) * kSchedChunk < (uint64_t(1) << 32) && !a.regs;
     // two passes where legal (the host gives them workspace); the pick codes hold 24-bit indices
-    // and the apply pass's record spans 32-bit byte ranges
+    // and the apply pass's record of one pick spans a 32-bit byte range
     const bool two = lds && !a.fused && a.picks && a.flags && a.n_sel && a.sel_time && a.T < (1 << 24) &&
-                     uint64_t(a.T) * 6u * uint64_t(a.B) * (f64 ? 8u : 4u) < (uint64_t(1) << 32) &&
+                     uint64_t(a.B) * 6u * (f64 ? 8u : 4u) < (uint64_t(1) << 32) &&
                      reinterpret_cast<uintptr_t>(a.sel_time) % 16 == 0;
     if (two) {
-        ref15_pick_kernel<<<grid, kBlock, 0, stream>>>(a);
-        KF_CUSTOM_DISPATCH(a.kc, {
-            if (f64) ref15_apply_kernel<double, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
-            else ref15_apply_kernel<float, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
-        });
+        // four-wave groups (KF_OPT_SCHED_GROUP): one-wave groups, which free their slot when their
+        // wave's pick list ends, measured slower on the bench row (5.51 vs 5.07 ms apply)
+        const dim3 g1(static_cast<unsigned>(a.B / 64)), g4(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
+        if (a.group_waves == 4) {
+            ref15_pick_kernel<4><<<g4, 256, 0, stream>>>(a);
+            KF_CUSTOM_DISPATCH(a.kc, {
+                if (f64) ref15_apply_kernel<double, CUSTOM, 4><<<g4, 256, 0, stream>>>(a);
+                else ref15_apply_kernel<float, CUSTOM, 4><<<g4, 256, 0, stream>>>(a);
+            });
+        } else {
+            ref15_pick_kernel<1><<<g1, 64, 0, stream>>>(a);
+            KF_CUSTOM_DISPATCH(a.kc, {
+                if (f64) ref15_apply_kernel<double, CUSTOM, 1><<<g1, 64, 0, stream>>>(a);
+                else ref15_apply_kernel<float, CUSTOM, 1><<<g1, 64, 0, stream>>>(a);
+            });
+        }
         Ref15SchedArgs b = a;  // the flagged filters (usually none: every lane leaves at once)
         b.only = a.flags;
         KF_CUSTOM_DISPATCH(a.kc, {

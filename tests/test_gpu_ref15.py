@@ -479,6 +479,58 @@ def test_scheduled_random_streams_vs_oracle(seed, B):
         assert _rel(ld[:n, f], rl[1:]) <= TOL, f
 
 
+def _sched_streams(rng, B, T):
+    """Random scheduled-filter inputs as test_scheduled_random_streams_vs_oracle builds them."""
+    t0 = 1697739278.761565
+    rates = rng.choice([10, 20, 35, 50, 75, 120, 160, 400], B).astype(np.float64)
+    etype = np.where(rng.random((T, B)) < 0.15, 0, 1).astype(np.uint8)
+    tt = t0 + np.cumsum(rng.uniform(0.003, 0.007, (T, B)), axis=0)
+    pay = rng.normal(0, 1, (T, 9, B))
+    pay[:, 0:3] *= 0.05
+    pay[:, 6:9] *= 0.3
+    pay[:, 0:3] = np.where((etype == 0)[:, None, :], pay[:, 0:3] * 60, pay[:, 0:3])
+    lens = rng.integers(T // 2, T + 1, B)
+    for f in range(B):
+        etype[lens[f]:, f] = 255
+    return t0, rates, etype, tt, pay
+
+
+@pytest.mark.parametrize('r_gps', [None, 0.0, 400.0])
+def test_sched_two_pass_matches_fused_kernels(r_gps):
+    """KF_OPT_SCHED_KERNEL: the two-pass path (pick pass + apply pass, mispicks rerun by the fused
+    kernel; one- and four-wave groups, KF_OPT_SCHED_GROUP) equals the fused LDS and register kernels, with the reference constants, with
+    R_gps[0] == R_imu[0] (a tie: the pick pass cannot decide and every gain comparison is left to
+    the covariance, so rounding sends filters down the fallback) and with R_gps > R_imu (GPS
+    wins).  Same arithmetic in every kernel: 1e-12."""
+    rng = np.random.default_rng(31)
+    B, T = 192, 96
+    t0, rates, etype, tt, pay = _sched_streams(rng, B, T)
+    ref = ref15.ModelConsts('ref15')
+    if r_gps is None:
+        params = None
+    else:
+        rg = np.full(3, r_gps if r_gps else ref.r_imu[0])
+        params = ref15.ModelConsts('ref15', r_gps=rg).params()
+    out = {}
+    arms = {'auto': {}, 'group1': {'sched_group': 'wave'}, 'fused': {'sched_kernel': 'fused'},
+            'regs': {'sched_kernel': 'regs'}}
+    for kern, opts in arms.items():
+        kf = kfmi.BatchedKF('ref15', B, 'f64', params=params, options=opts)
+        res = kf.run_scheduled(tt, etype, pay, np.full(B, t0), rates)
+        out[kern] = [v.cpu().numpy() for v in res]
+        kf.close()
+    tr, ld, stt, ns = out['auto']
+    assert ns.min() > 0
+    for kern in ('group1', 'fused', 'regs'):
+        t2, l2, s2, n2 = out[kern]
+        np.testing.assert_array_equal(ns, n2, err_msg=kern)
+        for f in range(B):  # rows past n_sel are not written
+            n = int(ns[f])
+            np.testing.assert_array_equal(stt[:n, f], s2[:n, f], err_msg=kern)
+            np.testing.assert_allclose(tr[:n, :, f], t2[:n, :, f], rtol=1e-12, atol=1e-12, err_msg=kern)
+            np.testing.assert_allclose(ld[:n, f], l2[:n, f], rtol=1e-12, atol=1e-12, err_msg=kern)
+
+
 def test_score_candidates_random_batch():
     """kf_score_candidates over a batch of random block-diagonal covariances vs the oracle's
     Scheduler.cov_matrix trace (first row and full)."""

@@ -31,22 +31,27 @@ def main():
     out_dir, cfgs = sys.argv[1], sys.argv[2:]
     res = {'note': ' '.join(__doc__.split('\n\n')[2].split())}
     for c in cfgs:
-        kern = {'ref15': 'ref_events', 'sched': 'ref15_sched', '1': 'ref_chain_kernel'}.get(c, 'cv_block_kernel')
         d = os.path.join(out_dir, f'cfg{c}')
-        vals = {}
-        for ctr in COUNTERS:
-            v = pick(per_kernel(d, ctr), kern)
-            vals[ctr] = sum(v) / len(v)
         rec = bench_line(os.path.join(out_dir, f'cfg{c}.log'))
-        ms = rec['roofline']['kernel_ms']
         units = rec['value'] * rec['ms_per_step'] * 1e-3        # filter-steps (events) per launch
         wave_steps = units / 64
-        res[f'config{c}'] = dict(
-            counters_per_launch=vals, kernel_ms=ms, launches_profiled=len(v),
-            valu_per_wave_step=vals['SQ_INSTS_VALU'] / wave_steps,
-            valu_issue_frac=vals['SQ_INSTS_VALU'] * CYC / (ms * 1e-3 * CLK * SIMDS),
-            wave_cycles_waiting_frac=vals['SQ_WAIT_ANY'] / vals['SQ_WAVE_CYCLES'],
-            wave_cycles_issue_stall_frac=vals['SQ_WAIT_INST_ANY'] / vals['SQ_WAVE_CYCLES'])
+        if c == 'sched' and 'apply' in rec['roofline']['kernel']:
+            # the two passes, each timed by its own GRBM_GUI_ACTIVE (GPU busy cycles in the dispatch)
+            kerns = {'apply': 'ref15_apply_kernel', 'pick': 'ref15_pick_kernel'}
+        else:
+            kerns = {'': {'ref15': 'ref_events', 'sched': 'ref15_sched', '1': 'ref_chain_kernel'}.get(c, 'cv_block_kernel')}
+        for tag, kern in kerns.items():
+            vals = {}
+            for ctr in COUNTERS:
+                v = pick(per_kernel(d, ctr), kern)
+                vals[ctr] = sum(v) / len(v)
+            ms = rec['roofline']['kernel_ms'] if len(kerns) == 1 else vals['GRBM_GUI_ACTIVE'] / CLK * 1e3
+            res[f'config{c}' + (f'_{tag}' if tag else '')] = dict(
+                kernel=kern, counters_per_launch=vals, kernel_ms=ms, launches_profiled=len(v),
+                valu_per_wave_step=vals['SQ_INSTS_VALU'] / wave_steps,
+                valu_issue_frac=vals['SQ_INSTS_VALU'] * CYC / (ms * 1e-3 * CLK * SIMDS),
+                wave_cycles_waiting_frac=vals['SQ_WAIT_ANY'] / vals['SQ_WAVE_CYCLES'],
+                wave_cycles_issue_stall_frac=vals['SQ_WAIT_INST_ANY'] / vals['SQ_WAVE_CYCLES'])
     with open(os.path.join(out_dir, 'pmc_valu.json'), 'w') as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
