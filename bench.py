@@ -735,8 +735,10 @@ def sched_workload(cfg, args, rank, world, dev):
     mode = kf.get_option('sched_kernel')
     if B % 64:
         kernel = 'ref15_sched_kernel'
-    elif mode == 0:  # two passes (kf.h KF_OPT_SCHED_KERNEL)
+    elif mode in (0, 3):  # two passes (kf.h KF_OPT_SCHED_KERNEL)
         kernel = 'ref15_pick_kernel + ref15_apply_kernel (+ ref15_sched_kernel over flagged filters)'
+    elif mode == 4:
+        kernel = 'ref15_apply_kernel<pick phase> (+ ref15_sched_kernel over flagged filters)'
     else:
         kernel = 'ref15_sched_lds_kernel' if mode == 2 else 'ref15_sched_kernel'
     return dict(step=step, units=B * T, bytes=nbytes, bytes_per_unit=nbytes / (B * T),

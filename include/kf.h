@@ -130,8 +130,10 @@ const char* kf_version(void);
  *   KF_OPT_START_THREADS  kf_run_stream: threads per block of the start kernel; 0 = 256
  *   KF_OPT_SEARCH_KERNEL  kf_search_combos: 0 = per level, 1 = child-major, 2 = parent-major
  *   KF_OPT_SEARCH_PM      kf_search_combos' parent-major kernel: 0 = parent in LDS, 1 = registers
- *   KF_OPT_SCHED_KERNEL   kf_run_scheduled: 0 = auto (the two-pass run where legal), 1 = the fused
- *                         register-input kernel, 2 = the fused LDS-input kernel
+ *   KF_OPT_SCHED_KERNEL   kf_run_scheduled: 0 = auto (the two passes where legal, as 3), 1 = the
+ *                         fused register-input kernel, 2 = the fused LDS-input kernel, 3 = the
+ *                         pick and apply passes as two launches, 4 = as the two phases of one
+ *                         launch
  *   KF_OPT_SCHED_GROUP    kf_run_scheduled's two passes: waves per workgroup, 0 = 4, 1 or 4
  *                         (one-wave groups free their slot when their wave's pick list ends;
  *                         measured slower)

@@ -296,7 +296,7 @@ int kf_set_option(kf_batch* h, int option, int64_t value) {
         case KF_OPT_STREAM:
         case KF_OPT_STREAM_FINAL:
         case KF_OPT_SEARCH_PM: ok = value == 0 || value == 1; break;
-        case KF_OPT_SCHED_KERNEL: ok = value >= 0 && value <= 2; break;
+        case KF_OPT_SCHED_KERNEL: ok = value >= 0 && value <= 4; break;
         case KF_OPT_SCHED_GROUP: ok = value == 0 || value == 1 || value == 4; break;
         case KF_OPT_CV_KERNEL: ok = value == 0 || value == 1 || value == 2 || value == 4 || value == 8; break;
         case KF_OPT_BLOCKS_PER_CU: ok = value == 0 || (value >= 2 && value <= 8); break;
@@ -1218,8 +1218,12 @@ int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, 
     a.logdet = logdet;
     a.sel_time = sel_time;
     a.n_sel = n_sel;
-    a.regs = opt(h, KF_OPT_SCHED_KERNEL) == 1;
-    a.fused = opt(h, KF_OPT_SCHED_KERNEL) != 0;
+    // KF_OPT_SCHED_KERNEL: 1 / 2 the fused register / LDS kernels, 3 the two passes as two
+    // launches, 4 as the phases of one launch; 0 the library's choice
+    const int64_t sk = opt(h, KF_OPT_SCHED_KERNEL);
+    a.regs = sk == 1;
+    a.fused = sk == 1 || sk == 2;
+    a.one_launch = sk == 4;
     a.group_waves = opt(h, KF_OPT_SCHED_GROUP) == 1 ? 1 : 4;
     // the greedy pick when both sensor classes are queued: the larger R gives the larger
     // posterior trace (launch_ref15_scheduled; checked on the covariance by the apply pass)

@@ -284,6 +284,7 @@ struct Ref15SchedArgs {
     int gps_wins;            // both classes queued: 1 the GPS fix wins, 0 the other event, -1 a tie
     bool fused;              // the fused kernels (KF_OPT_SCHED_KERNEL 1 / 2) instead of the two passes
     int group_waves;         // the two passes' waves per workgroup (KF_OPT_SCHED_GROUP: 1 or 4)
+    bool one_launch;         // the two passes as the phases of one kernel (KF_OPT_SCHED_KERNEL 4)
 };
 
 enum class Op { Run, Predict, Update, Step, Reset };  // Step: predict + update (kf_capi's deferral)

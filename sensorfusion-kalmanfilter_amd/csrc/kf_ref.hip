@@ -421,6 +421,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
 // straddles B) and 9 * B * W < 2^32; the host falls back to ref_events_kernel otherwise.
 // ------------------------------------------------------------------------------------
 constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
+constexpr int lgkmcnt0_imm = 15 | (7 << 4) | (0 << 8) | (3 << 14);  // LDS reads drained, vmcnt untouched
 
 // payload element i of this lane, read from the wave's LDS image where the update uses it
 template <typename T>
@@ -2589,43 +2590,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED
 // ------------------------------------------------------------------------------------
 constexpr int kPickBoth = 0x10, kPickGpsFirst = 0x20;
 
-// payload element i of this lane in the apply pass's image ([9][W / 4][64] dwords: the gather
-// moves 4 B per lane and instruction), read from LDS where the update uses it
+// payload element i of this lane in the apply pass's image: [9][64] slots of GB bytes per lane,
+// read from LDS where the update uses it
 template <typename T>
 struct LdsGathered {
-    const uint32_t* img;  // image base + lane
-    __device__ __forceinline__ T operator[](int i) const {
-        if constexpr (sizeof(T) == 8) {
-            const v2u u = {img[(2 * i) * 64], img[(2 * i + 1) * 64]};
-            return __builtin_bit_cast(T, u);
-        } else {
-            return __builtin_bit_cast(T, img[i * 64]);
-        }
-    }
+    const unsigned char* img;  // image base + this lane's slot + its value's offset in the slot
+    static constexpr int kSlot = sizeof(T) == 8 ? 16 : 4;
+    __device__ __forceinline__ T operator[](int i) const { return *reinterpret_cast<const T*>(img + i * 64 * kSlot); }
 };
 
 #ifndef KF_PICK_CHUNK
 #define KF_PICK_CHUNK 8
 #endif
 #ifndef KF_APPLY_PROBE
-#define KF_APPLY_PROBE 0  // 1 / 2: gather-cost probes for in-process A/B builds (tools/ab_inproc.py)
+#define KF_APPLY_PROBE 0  // 1 / 2 / 3: apply-pass timing probes for in-process A/B builds (tools/ab_inproc.py)
 #endif
 // events per LDS image of the pick pass: its lanes hold a few scalars, so the LDS, not the
 // registers, sets its waves per SIMD (8 events: 4 workgroups of 4 waves per CU)
 constexpr int kPickChunk = KF_PICK_CHUNK;
 constexpr int kPickImg = kPickChunk * 512 + kPickChunk * 64;
-template <int WAVES>
-__global__ __launch_bounds__(WAVES * 64) void ref15_pick_kernel(const Ref15SchedArgs a) {
+// The pick pass of one wave (filters f0 .. f0 + 63) with its two staging images at img0
+// (2 * kPickImg bytes); returns this lane's pick count.  Every store is issued on return.
+__device__ __forceinline__ int pick_phase(const Ref15SchedArgs& a, int lane, int64_t f0, unsigned char* img0) {
     constexpr int kSchedChunk = kPickChunk, kSchedImg = kPickImg;  // the fused kernel's staging, resized
     static_assert(kSchedChunk % 2 == 0 && kSchedChunk <= 16, "t rows move in pairs; etype rows 4 lanes each");
-    __shared__ __attribute__((aligned(16))) unsigned char lds[WAVES * 2 * kSchedImg];
-    const int lane = int(threadIdx.x & 63);
-    const int wave = WAVES == 1 ? 0 : wave_uniform(int(threadIdx.x >> 6));
-    const int64_t f0 = int64_t(blockIdx.x) * (WAVES * 64) + int64_t(wave) * 64;
-    if (f0 >= a.B) return;  // whole waves (B % 64 == 0)
     const int64_t f = f0 + lane;
     const int64_t B = a.B;
-    unsigned char* const img0 = lds + wave * 2 * kSchedImg;
     double prev = a.prev_time[f];
     const double period = 1.0 / (a.freq ? a.freq[f] : a.freq_all);  // kf_workers.py:880
     int q_len = 0, nsel = 0, qi0 = -1, qi1 = -1, qt0 = 0, qt1 = 0;
@@ -2697,33 +2687,59 @@ __global__ __launch_bounds__(WAVES * 64) void ref15_pick_kernel(const Ref15Sched
     }
     if (a.n_sel) a.n_sel[f] = nsel;
     a.flags[f] = 0;
+    return nsel;
 }
 
-template <typename T, bool CUSTOM, int WAVES>
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void ref15_pick_kernel(const Ref15SchedArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[WAVES * 2 * kPickImg];
+    const int lane = int(threadIdx.x & 63);
+    const int wave = WAVES == 1 ? 0 : wave_uniform(int(threadIdx.x >> 6));
+    const int64_t f0 = int64_t(blockIdx.x) * (WAVES * 64) + int64_t(wave) * 64;
+    if (f0 >= a.B) return;  // whole waves (B % 64 == 0)
+    (void)pick_phase(a, lane, f0, lds + wave * 2 * kPickImg);
+}
+
+// PICK: the wave runs its pick pass first (one launch for both passes: a wave's streaming pick
+// phase overlaps the other waves' compute-bound apply phases)
+template <typename T, bool CUSTOM, int WAVES, bool PICK>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void ref15_apply_kernel(
     const Ref15SchedArgs a) {
     constexpr int W = int(sizeof(T));
-    constexpr int NPW = W / 4;            // dwords per payload value
-    constexpr int PAY = 9 * NPW * 256;    // image: payload [9][NPW][64] dwords, then the pick times
-    constexpr int TM_OFF = PAY, IMG = TM_OFF + 512;
-    constexpr int PK = 256;               // a row of picks: 64 u32, three slots (rows q .. q + 2)
-    constexpr int NST = 7;                // traj (6 rows), logdet; absent ones dropped by offset
-    __shared__ __attribute__((aligned(16))) unsigned char lds[WAVES * (2 * IMG + 3 * PK)];
+    // The picked payload is gathered per lane: the picks of a wave's lanes lie on different rows,
+    // so every gather instruction touches up to 64 cache lines and the address unit, not HBM,
+    // bounds the pass.  f64 moves 16 B per lane (the aligned pair holding the lane's value: one
+    // instruction per value instead of two dword ones), f32 4 B.  One payload image per wave:
+    // the next pick's gather is issued once this event's update has read the image, and waited
+    // for after the next predict.
+    constexpr int GB = LdsGathered<T>::kSlot;
+    constexpr int PAY = 9 * 64 * GB;       // payload image [9][64] slots
+    constexpr int TM = PAY;                // pick times, two rows (q & 1)
+    constexpr int PK = TM + 2 * 512;       // picks, three rows (q % 3), 64 u32 each
+    constexpr int APPLY_LDS = PK + 3 * 256;
+    constexpr int WAVE_LDS = PICK && 2 * kPickImg > APPLY_LDS ? 2 * kPickImg : APPLY_LDS;  // the pick phase's images alias
+    constexpr int NST = 7;                 // traj (6 rows), logdet; absent ones dropped by offset
+    __shared__ __attribute__((aligned(16))) unsigned char lds[WAVES * WAVE_LDS];
     const int lane = int(threadIdx.x & 63);
     const int wave = WAVES == 1 ? 0 : wave_uniform(int(threadIdx.x >> 6));
     const int64_t f0 = int64_t(blockIdx.x) * (WAVES * 64) + int64_t(wave) * 64;
     if (f0 >= a.B) return;  // whole waves (B % 64 == 0)
     const int64_t f = f0 + lane;
     const int64_t B = a.B;
-    unsigned char* const img0 = lds + wave * (2 * IMG + 3 * PK);
-    unsigned char* const pk0 = img0 + 2 * IMG;
+    unsigned char* const base = lds + wave * WAVE_LDS;
     const uint32_t off = uint32_t(f) * uint32_t(W);
     const uint32_t rb = uint32_t(B) * uint32_t(W);
+    int nsel;
+    if constexpr (PICK) {
+        nsel = pick_phase(a, lane, f0, base);
+        waitcnt<vmcnt_imm(0)>();  // its picks are read back below (this wave's own rows)
+    } else {
+        nsel = a.n_sel[f];
+    }
     Ref15<T, CUSTOM> s;
     s.kc = a.kc;
     s.load(a.x, a.P, rb, off);
     int32_t st = a.status[f];
-    const int nsel = a.n_sel[f];
     double prev = a.prev_time[f];
     int S = nsel;  // the wave's longest pick list
 #pragma unroll
@@ -2733,58 +2749,65 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     }
     S = wave_uniform(S);
     waitcnt<vmcnt_imm(0)>();
-    // pick s of this lane: its event's payload rows gathered per lane (the picked rows of a
-    // wave may lie anywhere in [T][9][B]: 64-bit addresses), its time by one wave DMA; a lane
-    // past its list reads row 0 (every lane issues every DMA, so the waits can be counted)
-    auto issue = [&](int sidx, uint32_t pick, unsigned char* img) {
+    // pick r's payload (9 VMEM): a lane past its list reads row 0.  Device pass only: the 16-B
+    // form of the builtin is a gfx950 one, and the host pass would drop the kernel's stub.
+    auto gather = [&](int r, uint32_t pick) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const int64_t col = W == 8 ? (f & ~int64_t(1)) : f;  // f64: the 16-B-aligned pair
         const uint32_t ev = pick & 0xFFFFFFu;
 #if KF_APPLY_PROBE == 1  // timing probe (wrong results): every lane gathers lane 0's row
-        const int64_t row = __shfl((sidx < nsel && ev < uint32_t(a.T)) ? int(ev) : 0, 0, 64);
+        const int64_t row = __shfl((r < nsel && ev < uint32_t(a.T)) ? int(ev) : 0, 0, 64);
 #else
-        const int64_t row = (sidx < nsel && ev < uint32_t(a.T)) ? int64_t(ev) : 0;
+        const int64_t row = (r < nsel && ev < uint32_t(a.T)) ? int64_t(ev) : 0;
 #endif
-        const char* src = reinterpret_cast<const char*>(a.payload) + (row * 9 * B + f) * W;
+        const char* src = reinterpret_cast<const char*>(a.payload) + (row * 9 * B + col) * W;
 #pragma unroll
         for (int i = 0; i < 9; ++i)
 #if KF_APPLY_PROBE == 2  // timing probe (wrong results): no payload gather
-            if (sidx < 0)
+            if (r < 0)
 #endif
-#pragma unroll
-            for (int h = 0; h < NPW; ++h)
-                __builtin_amdgcn_global_load_lds(src + int64_t(i) * B * W + h * 4,
-                                                 (__attribute__((address_space(3))) void*)(img + (i * NPW + h) * 256), 4,
-                                                 0, 0);
-        const char* tb = reinterpret_cast<const char*>(a.sel_time) + (int64_t(sidx) * B + f0) * 8;
-        if (lane < 32) lds_dma16(bytes_rsrc(tb, 512u), img + TM_OFF, uint32_t(lane) * 16u, 0);
+                __builtin_amdgcn_global_load_lds(src + int64_t(i) * B * W,
+                                                 (__attribute__((address_space(3))) void*)(base + i * 64 * GB),
+                                                 LdsGathered<T>::kSlot, 0, 0);
+#else
+        (void)r;
+        (void)pick;
+#endif
     };
-    // the picks reach LDS by DMA two rows ahead (a register load in the loop made the compiler
-    // drain every store at the back edge to wait for it)
+    // pick r's time / row r of the picks (1 VMEM each, issued by every wave: past the list a
+    // zero-length descriptor, so the waits below can be counted)
+    auto issue_time = [&](int r) {
+        const char* tb = reinterpret_cast<const char*>(a.sel_time) + (int64_t(r) * B + f0) * 8;
+        if (lane < 32) lds_dma16(bytes_rsrc(tb, r < S ? 512u : 0u), base + TM + (r & 1) * 512, uint32_t(lane) * 16u, 0);
+    };
     auto issue_picks = [&](int r) {
         const char* pb = reinterpret_cast<const char*>(a.picks) + (int64_t(r) * B + f0) * 4;
-        if (lane < 16) lds_dma16(bytes_rsrc(pb, 256u), pk0 + (r % 3) * PK, uint32_t(lane) * 16u, 0);
+        if (lane < 16) lds_dma16(bytes_rsrc(pb, r < S ? 256u : 0u), base + PK + (r % 3) * 256, uint32_t(lane) * 16u, 0);
     };
-    auto pick_row = [&](int r) { return reinterpret_cast<const uint32_t*>(pk0 + (r % 3) * PK)[lane]; };
+    auto pick_row = [&](int r) { return reinterpret_cast<const uint32_t*>(base + PK + (r % 3) * 256)[lane]; };
+    const LdsGathered<T> pay{base + lane * GB + (W == 8 ? (lane & 1) * 8 : 0)};  // read where used
     if (S > 0) {
         issue_picks(0);
-        if (S > 1) issue_picks(1);
+        issue_picks(1);
+        issue_time(0);
         waitcnt<vmcnt_imm(0)>();
-        issue(0, pick_row(0), img0);
-        waitcnt<vmcnt_imm(0)>();  // the first image (no stores yet)
+        gather(0, pick_row(0));
     }
     bool bad = false;
     for (int q = 0; q < S; ++q) {
-        unsigned char* const img = img0 + (q & 1) * IMG;
-        // image q and pick row q + 1 are older than event q - 1's NST stores
-        if (q > 0) waitcnt<vmcnt_imm(NST)>();
-        const double tq = reinterpret_cast<const double*>(img + TM_OFF)[lane];
+        // time q and pick row q: older than pick row q + 1, gather q (9) and event q - 1's stores
+        if (q > 0) waitcnt<vmcnt_imm(1 + 9 + NST)>();
+        const double tq = reinterpret_cast<const double*>(base + TM + (q & 1) * 512)[lane];
         const uint32_t pick_c = pick_row(q);
-        if (q + 1 < S) {
-            issue(q + 1, pick_row(q + 1), img0 + ((q + 1) & 1) * IMG);
-            if (q + 2 < S) issue_picks(q + 2);  // into the slot row q - 1 held
-        }
+        issue_time(q + 1);
+        issue_picks(q + 2);  // into the slot row q - 1 held
         const bool live = q < nsel;
         const int code = int(pick_c >> 24);
+#if KF_APPLY_PROBE == 3  // timing probe (wrong results): lane 0's event type for the wave
+        const int type = __shfl(code & 7, 0, 64);
+#else
         const int type = code & 7;
+#endif
         if (live && !bad && (code & kPickBoth)) {
             // the greedy rule on this covariance (SchedLane::event): the pick pass's choice must
             // be the first candidate with the largest gain
@@ -2795,18 +2818,38 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
             if (v0 && v1) pick0 = g0 > g1 ? true : (g1 > g0 ? false : gps_first);
             else if (v0 != v1) pick0 = v0;
             else pick0 = gps_first;
+#if KF_APPLY_PROBE == 3
+            bad = false && pick0;
+#else
             bad = pick0 != (type == kGps);
+#endif
         }
-        if (live && !bad) {
-            const LdsGathered<T> pay{reinterpret_cast<const uint32_t*>(img) + lane};  // read where used
-            bool ok = true;
-            s.template event<false>(type, T(tq - prev), pay, false, T(0), ok);
+        const bool run = live && !bad;
+        const T dt = T(tq - prev);
+        if (run) s.predict(dt);  // Chains::event, split around the payload wait
+        // gather q: older than event q - 1's stores, time q + 1 and pick row q + 2
+        if (q > 0) waitcnt<vmcnt_imm(NST + 2)>();
+        else waitcnt<vmcnt_imm(2)>();
+        if (run && (type == kGps || type == kImu)) {
+            bool ok;
+            if (type == kGps) {
+                const T z[3] = {pay[0], pay[1], pay[2]};  // (easting, northing, altitude)
+                ok = s.template update_gps<false>(z);
+            } else {
+                ok = s.template update_imu<false>(pay, dt);
+            }
             if (!ok) {
                 st = kNotSpd;
                 s.fill_nan();
             }
-            prev = tq;
         }
+        if (run) prev = tq;
+        // the image's reads are done: gather q + 1 into it (its pick row landed before gather q;
+        // reading the payload into registers first, to issue the gather before the update, cost
+        // 10 spilled registers and measured 5.98 vs 5.45 ms)
+        __builtin_amdgcn_s_waitcnt(lgkmcnt0_imm);
+        asm volatile("" ::: "memory");
+        if (q + 1 < S) gather(q + 1, pick_row(q + 1));
         // a record's descriptor per pick (the records of the whole run exceed 32-bit offsets)
         const uint32_t vo = live ? off : kDropOffset;
         const auto r_tr = span_rsrc(a.traj, int64_t(q) * 6, rb, 6u);
@@ -2852,22 +2895,28 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
     // and the apply pass's record of one pick spans a 32-bit byte range
     const bool two = lds && !a.fused && a.picks && a.flags && a.n_sel && a.sel_time && a.T < (1 << 24) &&
                      uint64_t(a.B) * 6u * (f64 ? 8u : 4u) < (uint64_t(1) << 32) &&
-                     reinterpret_cast<uintptr_t>(a.sel_time) % 16 == 0;
+                     reinterpret_cast<uintptr_t>(a.sel_time) % 16 == 0 &&
+                     (!f64 || reinterpret_cast<uintptr_t>(a.payload) % 16 == 0);
     if (two) {
         // four-wave groups (KF_OPT_SCHED_GROUP): one-wave groups, which free their slot when their
         // wave's pick list ends, measured slower on the bench row (5.51 vs 5.07 ms apply)
         const dim3 g1(static_cast<unsigned>(a.B / 64)), g4(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-        if (a.group_waves == 4) {
+        if (a.one_launch) {
+            KF_CUSTOM_DISPATCH(a.kc, {
+                if (f64) ref15_apply_kernel<double, CUSTOM, 4, true><<<g4, 256, 0, stream>>>(a);
+                else ref15_apply_kernel<float, CUSTOM, 4, true><<<g4, 256, 0, stream>>>(a);
+            });
+        } else if (a.group_waves == 4) {
             ref15_pick_kernel<4><<<g4, 256, 0, stream>>>(a);
             KF_CUSTOM_DISPATCH(a.kc, {
-                if (f64) ref15_apply_kernel<double, CUSTOM, 4><<<g4, 256, 0, stream>>>(a);
-                else ref15_apply_kernel<float, CUSTOM, 4><<<g4, 256, 0, stream>>>(a);
+                if (f64) ref15_apply_kernel<double, CUSTOM, 4, false><<<g4, 256, 0, stream>>>(a);
+                else ref15_apply_kernel<float, CUSTOM, 4, false><<<g4, 256, 0, stream>>>(a);
             });
         } else {
             ref15_pick_kernel<1><<<g1, 64, 0, stream>>>(a);
             KF_CUSTOM_DISPATCH(a.kc, {
-                if (f64) ref15_apply_kernel<double, CUSTOM, 1><<<g1, 64, 0, stream>>>(a);
-                else ref15_apply_kernel<float, CUSTOM, 1><<<g1, 64, 0, stream>>>(a);
+                if (f64) ref15_apply_kernel<double, CUSTOM, 1, false><<<g1, 64, 0, stream>>>(a);
+                else ref15_apply_kernel<float, CUSTOM, 1, false><<<g1, 64, 0, stream>>>(a);
             });
         }
         Ref15SchedArgs b = a;  // the flagged filters (usually none: every lane leaves at once)

@@ -512,8 +512,8 @@ def test_sched_two_pass_matches_fused_kernels(r_gps):
         rg = np.full(3, r_gps if r_gps else ref.r_imu[0])
         params = ref15.ModelConsts('ref15', r_gps=rg).params()
     out = {}
-    arms = {'auto': {}, 'group1': {'sched_group': 'wave'}, 'fused': {'sched_kernel': 'fused'},
-            'regs': {'sched_kernel': 'regs'}}
+    arms = {'auto': {}, 'group1': {'sched_group': 'wave'}, 'one_launch': {'sched_kernel': 'one_launch'},
+            'fused': {'sched_kernel': 'fused'}, 'regs': {'sched_kernel': 'regs'}}
     for kern, opts in arms.items():
         kf = kfmi.BatchedKF('ref15', B, 'f64', params=params, options=opts)
         res = kf.run_scheduled(tt, etype, pay, np.full(B, t0), rates)
@@ -521,7 +521,7 @@ def test_sched_two_pass_matches_fused_kernels(r_gps):
         kf.close()
     tr, ld, stt, ns = out['auto']
     assert ns.min() > 0
-    for kern in ('group1', 'fused', 'regs'):
+    for kern in ('group1', 'one_launch', 'fused', 'regs'):
         t2, l2, s2, n2 = out[kern]
         np.testing.assert_array_equal(ns, n2, err_msg=kern)
         for f in range(B):  # rows past n_sel are not written

@@ -77,6 +77,27 @@ def main():
                 'traffic_over_algorithmic': (fetch * read_scale + write * write_scale) / alg,
                 'launches_profiled': len(f), 'note': f'per search: the sum over its {nl} level launches'}
             continue
+        if c == 'sched':
+            # the two passes per launch, each against its own bytes; the algorithmic total is the
+            # bench line's (it depends on the picks: n_selected)
+            rec = None
+            with open(os.path.join(out_dir, 'cfgsched_FETCH_SIZE.log')) as fh:
+                for line in fh:
+                    if line.startswith('{"metric"'):
+                        rec = json.loads(line)
+            tot = 0.0
+            for tag, kern in (('apply', 'ref15_apply_kernel'), ('pick', 'ref15_pick_kernel')):
+                f = pick(per_kernel(os.path.join(out_dir, 'cfgsched_FETCH_SIZE'), 'FETCH_SIZE'), kern)
+                w = pick(per_kernel(os.path.join(out_dir, 'cfgsched_WRITE_SIZE'), 'WRITE_SIZE'), kern)
+                fetch, write = 1024 * sum(f) / len(f), 1024 * sum(w) / len(w)
+                res[f'configsched_{tag}'] = {'kernel': kern, 'fetch_bytes_raw': fetch, 'write_bytes_raw': write,
+                                             'bytes_per_launch': fetch * read_scale + write * write_scale,
+                                             'launches_profiled': len(f)}
+                tot += fetch * read_scale + write * write_scale
+            alg = rec['roofline']['algorithmic_bytes_per_launch']
+            res['configsched'] = {'bytes_per_launch': tot, 'algorithmic_bytes_per_launch': alg,
+                                  'traffic_over_algorithmic': tot / alg, 'note': 'pick + apply passes'}
+            continue
         kern = 'ref_events' if c == 'ref15' else 'cv_block_kernel'
         f = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE'), kern)
         w = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE'), kern)

@@ -27,6 +27,18 @@ def bench_line(path):
     return rec
 
 
+def kernel_trace_ms(out_dir, c, kern):
+    """Average duration (ms) of the kernel matching `kern` in pmc_valu.sh's kernel-trace pass."""
+    import csv
+    import glob
+    for f in glob.glob(os.path.join(out_dir, f'kt{c}', '**', '*kernel_stats.csv'), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if kern in r['Name']:
+                    return float(r['AverageNs']) * 1e-6
+    raise SystemExit(f'no kernel-trace row for {kern!r} under {out_dir}/kt{c}')
+
+
 def main():
     out_dir, cfgs = sys.argv[1], sys.argv[2:]
     res = {'note': ' '.join(__doc__.split('\n\n')[2].split())}
@@ -45,7 +57,7 @@ def main():
             for ctr in COUNTERS:
                 v = pick(per_kernel(d, ctr), kern)
                 vals[ctr] = sum(v) / len(v)
-            ms = rec['roofline']['kernel_ms'] if len(kerns) == 1 else vals['GRBM_GUI_ACTIVE'] / CLK * 1e3
+            ms = rec['roofline']['kernel_ms'] if len(kerns) == 1 else kernel_trace_ms(out_dir, c, kern)
             res[f'config{c}' + (f'_{tag}' if tag else '')] = dict(
                 kernel=kern, counters_per_launch=vals, kernel_ms=ms, launches_profiled=len(v),
                 valu_per_wave_step=vals['SQ_INSTS_VALU'] / wave_steps,
