@@ -20,10 +20,10 @@ _ONE_THREAD = ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS')
 def _worker(job):
     from oracle import ref_kf
     kind, sh, seconds = job
-    units, t0 = 0, time.perf_counter()
+    units, tic = 0, time.perf_counter()
     nf = sh['n']
     f = 0
-    while f < nf and time.perf_counter() - t0 < seconds:
+    while f < nf and time.perf_counter() - tic < seconds:
         if kind == 'cv':
             model = ref_kf.CVModel(sh['d'], r_full=sh.get('R'))
             T = sh['u'].shape[0]
@@ -64,7 +64,7 @@ def _worker(job):
         else:
             raise ValueError(kind)
         f += 1
-    return units, time.perf_counter() - t0, f
+    return units, time.perf_counter() - tic, f
 
 
 def _warm(_):

@@ -305,3 +305,13 @@ def test_numpy_pool_runs_the_reference_loop_on_all_workers():
     assert out['cores'] == 2 and out['filters'] == 2 * nf and out['units'] == 2 * nf * T
     assert out['value'] > 0
     assert numpy_pool.split(10, 3) == [(0, 4), (4, 7), (7, 10)]
+    # the scheduled kind (its streams carry their own t0: the worker's clock must not be it)
+    T, nf, t0 = 40, 3, 1697739278.761565
+    et = np.ones((T, nf), np.uint8)
+    et[9::10] = 0
+    sched = [dict(et=et, t=t0 + 0.005 * np.arange(1, T + 1)[:, None] + np.zeros((1, nf)),
+                  pay=rng.normal(0, 0.1, (T, 9, nf)), freq=np.array([20.0, 50.0, 120.0]), t0=t0, n=nf)
+             for _ in range(2)]
+    out = numpy_pool.run('sched', sched, seconds=30.0)
+    assert out['filters'] == 2 * nf and out['units'] == 2 * nf * T
+    assert 0 < out['seconds'] < 30 and out['value'] > 0
