@@ -137,6 +137,9 @@ const char* kf_version(void);
  *   KF_OPT_SCHED_GROUP    kf_run_scheduled's two passes: waves per workgroup, 0 = 4, 1 or 4
  *                         (one-wave groups free their slot when their wave's pick list ends;
  *                         measured slower)
+ *   KF_OPT_SCHED_ORDER    kf_run_scheduled's two launches: 0 = the apply pass runs the waves
+ *                         heaviest first (their longest pick lists, sorted on the device),
+ *                         1 = in batch order
  * KF_EINVAL for an unknown option or an out-of-range value. */
 #define KF_OPT_PREDICT        1
 #define KF_OPT_CV_KERNEL      2
@@ -150,7 +153,8 @@ const char* kf_version(void);
 #define KF_OPT_SEARCH_PM      10
 #define KF_OPT_SCHED_KERNEL   11
 #define KF_OPT_SCHED_GROUP    12
-#define KF_OPT_COUNT          13
+#define KF_OPT_SCHED_ORDER    13
+#define KF_OPT_COUNT          14
 int kf_set_option(kf_batch* handle, int option, int64_t value);
 int kf_get_option(const kf_batch* handle, int option, int64_t* value);
 

@@ -298,6 +298,7 @@ int kf_set_option(kf_batch* h, int option, int64_t value) {
         case KF_OPT_SEARCH_PM: ok = value == 0 || value == 1; break;
         case KF_OPT_SCHED_KERNEL: ok = value >= 0 && value <= 4; break;
         case KF_OPT_SCHED_GROUP: ok = value == 0 || value == 1 || value == 4; break;
+        case KF_OPT_SCHED_ORDER: ok = value == 0 || value == 1; break;
         case KF_OPT_CV_KERNEL: ok = value == 0 || value == 1 || value == 2 || value == 4 || value == 8; break;
         case KF_OPT_BLOCKS_PER_CU: ok = value == 0 || (value >= 2 && value <= 8); break;
         case KF_OPT_EVENTS_KERNEL: ok = value >= 0 && value <= 3; break;
@@ -1229,7 +1230,19 @@ int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, 
     // posterior trace (launch_ref15_scheduled; checked on the covariance by the apply pass)
     a.gps_wins = h->gps_r0 > h->imu_r0 ? 1 : h->gps_r0 < h->imu_r0 ? 0 : -1;
     if (!a.fused && T > 0 && n_sel && sel_time) {
-        const size_t need = align256(sizeof(uint32_t) * size_t(T) * size_t(h->B)) + align256(sizeof(int32_t) * size_t(h->B));
+        // picks [T][B] | flags [B] | with B % 64 == 0 and KF_OPT_SCHED_ORDER 0: the waves' keys, ids,
+        // sorted keys, order [B / 64] and the sort's scratch
+        const size_t picks_b = align256(sizeof(uint32_t) * size_t(T) * size_t(h->B));
+        const size_t flags_b = align256(sizeof(int32_t) * size_t(h->B));
+        const int nw = h->B % 64 == 0 && opt(h, KF_OPT_SCHED_ORDER) == 0 ? int(h->B / 64) : 0;
+        size_t sort_b = 0;
+        if (nw && kfmi::sort_pairs_desc_u32(nullptr, &sort_b, nullptr, nullptr, nullptr, nullptr, nw, 31, nullptr) !=
+                      hipSuccess) {
+            (void)hipGetLastError();
+            sort_b = 0;
+        }
+        const size_t wave_b = nw && sort_b ? 4 * align256(sizeof(uint32_t) * size_t(nw)) + align256(sort_b) : 0;
+        const size_t need = picks_b + flags_b + wave_b;
         if (h->sched_ws_bytes < need) {
             if (h->sched_ws) (void)hipFree(h->sched_ws);
             h->sched_ws = nullptr;
@@ -1238,9 +1251,19 @@ int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, 
             else (void)hipGetLastError();  // no workspace: the fused kernel runs
         }
         if (h->sched_ws) {
-            a.picks = static_cast<uint32_t*>(h->sched_ws);
-            a.flags = reinterpret_cast<int32_t*>(static_cast<char*>(h->sched_ws) +
-                                                 align256(sizeof(uint32_t) * size_t(T) * size_t(h->B)));
+            char* w = static_cast<char*>(h->sched_ws);
+            a.picks = reinterpret_cast<uint32_t*>(w);
+            a.flags = reinterpret_cast<int32_t*>(w + picks_b);
+            if (wave_b) {
+                const size_t wb = align256(sizeof(uint32_t) * size_t(nw));
+                char* k = w + picks_b + flags_b;
+                a.wave_key = reinterpret_cast<uint32_t*>(k);
+                a.wave_id = reinterpret_cast<uint32_t*>(k + wb);
+                a.wave_key_sorted = reinterpret_cast<uint32_t*>(k + 2 * wb);
+                a.order = reinterpret_cast<uint32_t*>(k + 3 * wb);
+                a.sort_tmp = k + 4 * wb;
+                a.sort_tmp_bytes = sort_b;
+            }
         }
     }
     hipError_t e = kfmi::launch_ref15_scheduled(h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));

@@ -25,6 +25,12 @@
 #include "kf_internal.h"
 
 namespace kfmi {
+hipError_t sort_pairs_desc_u32(void* tmp, size_t* tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                               const uint32_t* vals_in, uint32_t* vals_out, int n, int bits, hipStream_t stream) {
+    return hipcub::DeviceRadixSort::SortPairsDescending(tmp, *tmp_bytes, keys_in, keys_out, vals_in, vals_out, n, 0,
+                                                        bits, stream);
+}
+
 namespace {
 
 constexpr int kIngBlock = 256;

@@ -285,6 +285,15 @@ struct Ref15SchedArgs {
     bool fused;              // the fused kernels (KF_OPT_SCHED_KERNEL 1 / 2) instead of the two passes
     int group_waves;         // the two passes' waves per workgroup (KF_OPT_SCHED_GROUP: 1 or 4)
     bool one_launch;         // the two passes as the phases of one kernel (KF_OPT_SCHED_KERNEL 4)
+    // heaviest waves first (KF_OPT_SCHED_ORDER 0): the pick pass writes each wave's longest pick
+    // list (wave_key) and its index (wave_id); a descending radix sort gives `order`, the apply
+    // pass's wave sequence.  All nullptr: batch order.
+    uint32_t* wave_key;      // [B / 64]
+    uint32_t* wave_id;       // [B / 64]
+    uint32_t* wave_key_sorted;
+    uint32_t* order;         // [B / 64]
+    void* sort_tmp;
+    size_t sort_tmp_bytes;
 };
 
 enum class Op { Run, Predict, Update, Step, Reset };  // Step: predict + update (kf_capi's deferral)
@@ -310,6 +319,10 @@ hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t st
 hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream);
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream);
 hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream);
+// descending stable radix sort of n (key, value) pairs on the key's low `bits` bits (kf_ingest.hip,
+// hipCUB); tmp == nullptr: *tmp_bytes = the scratch it needs
+hipError_t sort_pairs_desc_u32(void* tmp, size_t* tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                               const uint32_t* vals_in, uint32_t* vals_out, int n, int bits, hipStream_t stream);
 
 constexpr int kBlock = 256;  // 4 wave64 per workgroup
 

@@ -2697,7 +2697,19 @@ __global__ __launch_bounds__(WAVES * 64) void ref15_pick_kernel(const Ref15Sched
     const int wave = WAVES == 1 ? 0 : wave_uniform(int(threadIdx.x >> 6));
     const int64_t f0 = int64_t(blockIdx.x) * (WAVES * 64) + int64_t(wave) * 64;
     if (f0 >= a.B) return;  // whole waves (B % 64 == 0)
-    (void)pick_phase(a, lane, f0, lds + wave * 2 * kPickImg);
+    const int nsel = pick_phase(a, lane, f0, lds + wave * 2 * kPickImg);
+    if (a.wave_key) {  // the wave's longest pick list, for the apply pass's heaviest-first order
+        int S = nsel;
+#pragma unroll
+        for (int sh = 32; sh >= 1; sh >>= 1) {
+            const int o = __shfl_xor(S, sh, 64);
+            S = o > S ? o : S;
+        }
+        if (lane == 0) {
+            a.wave_key[f0 >> 6] = uint32_t(S);
+            a.wave_id[f0 >> 6] = uint32_t(f0 >> 6);
+        }
+    }
 }
 
 // PICK: the wave runs its pick pass first (one launch for both passes: a wave's streaming pick
@@ -2722,8 +2734,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     __shared__ __attribute__((aligned(16))) unsigned char lds[WAVES * WAVE_LDS];
     const int lane = int(threadIdx.x & 63);
     const int wave = WAVES == 1 ? 0 : wave_uniform(int(threadIdx.x >> 6));
-    const int64_t f0 = int64_t(blockIdx.x) * (WAVES * 64) + int64_t(wave) * 64;
-    if (f0 >= a.B) return;  // whole waves (B % 64 == 0)
+    const int64_t slot = int64_t(blockIdx.x) * WAVES + wave;  // the wave's place in the launch
+    if (slot * 64 >= a.B) return;  // whole waves (B % 64 == 0)
+    // heaviest waves first where the pick pass sorted them (their list lengths differ by rate,
+    // and the longest started last set the launch's tail)
+    const int64_t f0 = (!PICK && a.order ? int64_t(wave_uniform(int(a.order[slot]))) : slot) * 64;
     const int64_t f = f0 + lane;
     const int64_t B = a.B;
     unsigned char* const base = lds + wave * WAVE_LDS;
@@ -2906,17 +2921,25 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
                 if (f64) ref15_apply_kernel<double, CUSTOM, 4, true><<<g4, 256, 0, stream>>>(a);
                 else ref15_apply_kernel<float, CUSTOM, 4, true><<<g4, 256, 0, stream>>>(a);
             });
-        } else if (a.group_waves == 4) {
-            ref15_pick_kernel<4><<<g4, 256, 0, stream>>>(a);
-            KF_CUSTOM_DISPATCH(a.kc, {
-                if (f64) ref15_apply_kernel<double, CUSTOM, 4, false><<<g4, 256, 0, stream>>>(a);
-                else ref15_apply_kernel<float, CUSTOM, 4, false><<<g4, 256, 0, stream>>>(a);
-            });
         } else {
-            ref15_pick_kernel<1><<<g1, 64, 0, stream>>>(a);
+            if (a.group_waves == 4) ref15_pick_kernel<4><<<g4, 256, 0, stream>>>(a);
+            else ref15_pick_kernel<1><<<g1, 64, 0, stream>>>(a);
+            if (a.order) {  // the waves by their longest pick list, descending (stable)
+                int bits = 1;
+                while ((1 << bits) <= a.T && bits < 31) ++bits;
+                size_t tb = a.sort_tmp_bytes;
+                const hipError_t e = sort_pairs_desc_u32(a.sort_tmp, &tb, a.wave_key, a.wave_key_sorted, a.wave_id,
+                                                         a.order, static_cast<int>(a.B / 64), bits, stream);
+                if (e != hipSuccess) return e;
+            }
             KF_CUSTOM_DISPATCH(a.kc, {
-                if (f64) ref15_apply_kernel<double, CUSTOM, 1, false><<<g1, 64, 0, stream>>>(a);
-                else ref15_apply_kernel<float, CUSTOM, 1, false><<<g1, 64, 0, stream>>>(a);
+                if (a.group_waves == 4) {
+                    if (f64) ref15_apply_kernel<double, CUSTOM, 4, false><<<g4, 256, 0, stream>>>(a);
+                    else ref15_apply_kernel<float, CUSTOM, 4, false><<<g4, 256, 0, stream>>>(a);
+                } else {
+                    if (f64) ref15_apply_kernel<double, CUSTOM, 1, false><<<g1, 64, 0, stream>>>(a);
+                    else ref15_apply_kernel<float, CUSTOM, 1, false><<<g1, 64, 0, stream>>>(a);
+                }
             });
         }
         Ref15SchedArgs b = a;  // the flagged filters (usually none: every lane leaves at once)

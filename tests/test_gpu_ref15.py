@@ -498,7 +498,8 @@ def _sched_streams(rng, B, T):
 @pytest.mark.parametrize('r_gps', [None, 0.0, 400.0])
 def test_sched_two_pass_matches_fused_kernels(r_gps):
     """KF_OPT_SCHED_KERNEL: the two-pass path (pick pass + apply pass, mispicks rerun by the fused
-    kernel; one- and four-wave groups, KF_OPT_SCHED_GROUP) equals the fused LDS and register kernels, with the reference constants, with
+    kernel; one- and four-wave groups, KF_OPT_SCHED_GROUP; heaviest-first or batch wave order,
+    KF_OPT_SCHED_ORDER) equals the fused LDS and register kernels, with the reference constants, with
     R_gps[0] == R_imu[0] (a tie: the pick pass cannot decide and every gain comparison is left to
     the covariance, so rounding sends filters down the fallback) and with R_gps > R_imu (GPS
     wins).  Same arithmetic in every kernel: 1e-12."""
@@ -513,7 +514,8 @@ def test_sched_two_pass_matches_fused_kernels(r_gps):
         params = ref15.ModelConsts('ref15', r_gps=rg).params()
     out = {}
     arms = {'auto': {}, 'group1': {'sched_group': 'wave'}, 'one_launch': {'sched_kernel': 'one_launch'},
-            'fused': {'sched_kernel': 'fused'}, 'regs': {'sched_kernel': 'regs'}}
+            'batch_order': {'sched_order': 'batch'}, 'fused': {'sched_kernel': 'fused'},
+            'regs': {'sched_kernel': 'regs'}}
     for kern, opts in arms.items():
         kf = kfmi.BatchedKF('ref15', B, 'f64', params=params, options=opts)
         res = kf.run_scheduled(tt, etype, pay, np.full(B, t0), rates)
@@ -521,7 +523,7 @@ def test_sched_two_pass_matches_fused_kernels(r_gps):
         kf.close()
     tr, ld, stt, ns = out['auto']
     assert ns.min() > 0
-    for kern in ('group1', 'one_launch', 'fused', 'regs'):
+    for kern in ('group1', 'one_launch', 'batch_order', 'fused', 'regs'):
         t2, l2, s2, n2 = out[kern]
         np.testing.assert_array_equal(ns, n2, err_msg=kern)
         for f in range(B):  # rows past n_sel are not written
