@@ -1243,14 +1243,16 @@ int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, 
         }
         const size_t wave_b = nw && sort_b ? 4 * align256(sizeof(uint32_t) * size_t(nw)) + align256(sort_b) : 0;
         const size_t need = picks_b + flags_b + wave_b;
-        if (h->sched_ws_bytes < need) {
+        // no allocation inside a graph capture (hipMalloc / hipFree are not capturable): a
+        // workspace too small for this T leaves the fused kernel to run
+        if (h->sched_ws_bytes < need && !capturing(static_cast<hipStream_t>(stream))) {
             if (h->sched_ws) (void)hipFree(h->sched_ws);
             h->sched_ws = nullptr;
             h->sched_ws_bytes = 0;
             if (hipMalloc(&h->sched_ws, need) == hipSuccess) h->sched_ws_bytes = need;
             else (void)hipGetLastError();  // no workspace: the fused kernel runs
         }
-        if (h->sched_ws) {
+        if (h->sched_ws && h->sched_ws_bytes >= need) {
             char* w = static_cast<char*>(h->sched_ws);
             a.picks = reinterpret_cast<uint32_t*>(w);
             a.flags = reinterpret_cast<int32_t*>(w + picks_b);

@@ -533,6 +533,58 @@ def test_sched_two_pass_matches_fused_kernels(r_gps):
             np.testing.assert_allclose(ld[:n, f], l2[:n, f], rtol=1e-12, atol=1e-12, err_msg=kern)
 
 
+@pytest.mark.parametrize('warm', [True, False])
+def test_scheduled_replays_as_a_hip_graph(warm):
+    """kf_run_scheduled captured into a hipGraph.  Warm: an eager call sized the two-pass
+    workspace first, and the replay gives that call's outputs bitwise (pick pass, wave sort,
+    apply pass, fallback).  Cold: no workspace can be allocated inside the capture, so the fused
+    kernel runs, and the replay equals an eager two-pass run at 1e-12 (the kernels' agreement)."""
+    rng = np.random.default_rng(41)
+    B, T = 128, 80
+    t0, rates, etype, tt, pay = _sched_streams(rng, B, T)
+    dev = torch.device('cuda', 0)
+    ttd, etd, payd = (torch.as_tensor(v, device=dev) for v in (tt, etype, pay))
+    prev, frd = torch.full((B,), t0, dtype=torch.float64, device=dev), torch.as_tensor(rates, device=dev)
+    x0 = torch.zeros(15, B, dtype=torch.float64, device=dev)
+    P0b = torch.as_tensor(np.repeat(ref15.to_blocks(ref_kf.P0_REF15)[:, None], B, axis=1), device=dev)
+    outs = (torch.empty(T, 6, B, dtype=torch.float64, device=dev), torch.empty(T, B, dtype=torch.float64, device=dev),
+            torch.empty(T, B, dtype=torch.float64, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+
+    def run(kf):
+        kf.set_state(x0, P0b)
+        for o, r in zip(outs, kf.run_scheduled(ttd, etd, payd, prev, frd)):
+            o.copy_(r)
+
+    ref_kf_ = kfmi.BatchedKF('ref15', B, 'f64')
+    run(ref_kf_)
+    torch.cuda.synchronize()
+    eager = [o.cpu().numpy().copy() for o in outs]
+    ref_kf_.close()
+    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    if warm:
+        run(kf)
+        torch.cuda.synchronize()
+    for o in outs:
+        o.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        run(kf)
+    g.replay()
+    torch.cuda.synchronize()
+    got = [o.cpu().numpy() for o in outs]
+    kf.close()
+    np.testing.assert_array_equal(got[3], eager[3])
+    for f in range(B):
+        n = int(eager[3][f])
+        np.testing.assert_array_equal(got[2][:n, f], eager[2][:n, f])
+        if warm:
+            np.testing.assert_array_equal(got[0][:n, :, f], eager[0][:n, :, f])
+            np.testing.assert_array_equal(got[1][:n, f], eager[1][:n, f])
+        else:
+            np.testing.assert_allclose(got[0][:n, :, f], eager[0][:n, :, f], rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(got[1][:n, f], eager[1][:n, f], rtol=1e-12, atol=1e-12)
+
+
 def test_score_candidates_random_batch():
     """kf_score_candidates over a batch of random block-diagonal covariances vs the oracle's
     Scheduler.cov_matrix trace (first row and full)."""
