@@ -495,8 +495,8 @@ def _sched_streams(rng, B, T):
     return t0, rates, etype, tt, pay
 
 
-@pytest.mark.parametrize('r_gps', [None, 0.0, 400.0])
-def test_sched_two_pass_matches_fused_kernels(r_gps):
+@pytest.mark.parametrize('r_gps,dtype', [(None, 'f64'), (0.0, 'f64'), (400.0, 'f64'), (None, 'f32')])
+def test_sched_two_pass_matches_fused_kernels(r_gps, dtype):
     """KF_OPT_SCHED_KERNEL: the two-pass path (pick pass + apply pass, mispicks rerun by the fused
     kernel; one- and four-wave groups, KF_OPT_SCHED_GROUP; heaviest-first or batch wave order,
     KF_OPT_SCHED_ORDER) equals the fused LDS and register kernels, with the reference constants, with
@@ -517,20 +517,21 @@ def test_sched_two_pass_matches_fused_kernels(r_gps):
             'batch_order': {'sched_order': 'batch'}, 'fused': {'sched_kernel': 'fused'},
             'regs': {'sched_kernel': 'regs'}}
     for kern, opts in arms.items():
-        kf = kfmi.BatchedKF('ref15', B, 'f64', params=params, options=opts)
-        res = kf.run_scheduled(tt, etype, pay, np.full(B, t0), rates)
+        kf = kfmi.BatchedKF('ref15', B, dtype, params=params, options=opts)
+        res = kf.run_scheduled(tt, etype, pay.astype(np.float32) if dtype == 'f32' else pay, np.full(B, t0), rates)
         out[kern] = [v.cpu().numpy() for v in res]
         kf.close()
     tr, ld, stt, ns = out['auto']
     assert ns.min() > 0
+    tol = 1e-12 if dtype == 'f64' else 1e-5  # f32: the same operations, the fp32 event's rounding
     for kern in ('group1', 'one_launch', 'batch_order', 'fused', 'regs'):
         t2, l2, s2, n2 = out[kern]
         np.testing.assert_array_equal(ns, n2, err_msg=kern)
         for f in range(B):  # rows past n_sel are not written
             n = int(ns[f])
             np.testing.assert_array_equal(stt[:n, f], s2[:n, f], err_msg=kern)
-            np.testing.assert_allclose(tr[:n, :, f], t2[:n, :, f], rtol=1e-12, atol=1e-12, err_msg=kern)
-            np.testing.assert_allclose(ld[:n, f], l2[:n, f], rtol=1e-12, atol=1e-12, err_msg=kern)
+            np.testing.assert_allclose(tr[:n, :, f], t2[:n, :, f], rtol=tol, atol=tol, err_msg=kern)
+            np.testing.assert_allclose(ld[:n, f], l2[:n, f], rtol=tol, atol=tol, err_msg=kern)
 
 
 @pytest.mark.parametrize('warm', [True, False])
