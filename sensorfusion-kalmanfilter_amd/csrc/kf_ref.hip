@@ -2712,6 +2712,26 @@ __global__ __launch_bounds__(WAVES * 64) void ref15_pick_kernel(const Ref15Sched
     }
 }
 
+// The one-launch run's wave order: its picks do not exist before the launch, so each wave is
+// keyed by its highest processing frequency, which sets its pick count (bit patterns of
+// positive floats sort as their values).
+__global__ __launch_bounds__(kBlock) void ref15_rate_key_kernel(const Ref15SchedArgs a) {
+    const int lane = int(threadIdx.x & 63);
+    const int64_t f0 = int64_t(blockIdx.x) * kBlock + int64_t(threadIdx.x >> 6) * 64;
+    if (f0 >= a.B) return;  // whole waves (B % 64 == 0)
+    float fr = float(a.freq[f0 + lane]);
+    fr = fr > 0.0f ? fr : 0.0f;  // NaN and non-positive rates sort last
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        const float o = __shfl_xor(fr, sh, 64);
+        fr = o > fr ? o : fr;
+    }
+    if (lane == 0) {
+        a.wave_key[f0 >> 6] = __float_as_uint(fr);
+        a.wave_id[f0 >> 6] = uint32_t(f0 >> 6);
+    }
+}
+
 // PICK: the wave runs its pick pass first (one launch for both passes: a wave's streaming pick
 // phase overlaps the other waves' compute-bound apply phases)
 template <typename T, bool CUSTOM, int WAVES, bool PICK>
@@ -2738,7 +2758,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     if (slot * 64 >= a.B) return;  // whole waves (B % 64 == 0)
     // heaviest waves first where the pick pass sorted them (their list lengths differ by rate,
     // and the longest started last set the launch's tail)
-    const int64_t f0 = (!PICK && a.order ? int64_t(wave_uniform(int(a.order[slot]))) : slot) * 64;
+    const int64_t f0 = (a.order ? int64_t(wave_uniform(int(a.order[slot]))) : slot) * 64;
     const int64_t f = f0 + lane;
     const int64_t B = a.B;
     unsigned char* const base = lds + wave * WAVE_LDS;
@@ -2917,9 +2937,19 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
         // wave's pick list ends, measured slower on the bench row (5.51 vs 5.07 ms apply)
         const dim3 g1(static_cast<unsigned>(a.B / 64)), g4(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
         if (a.one_launch) {
-            KF_CUSTOM_DISPATCH(a.kc, {
-                if (f64) ref15_apply_kernel<double, CUSTOM, 4, true><<<g4, 256, 0, stream>>>(a);
-                else ref15_apply_kernel<float, CUSTOM, 4, true><<<g4, 256, 0, stream>>>(a);
+            Ref15SchedArgs c = a;  // heaviest first by rate where the filters have their own rates
+            c.order = nullptr;
+            if (a.order && a.freq) {
+                ref15_rate_key_kernel<<<g4, 256, 0, stream>>>(a);
+                size_t tb = a.sort_tmp_bytes;
+                const hipError_t e = sort_pairs_desc_u32(a.sort_tmp, &tb, a.wave_key, a.wave_key_sorted, a.wave_id,
+                                                         a.order, static_cast<int>(a.B / 64), 32, stream);
+                if (e != hipSuccess) return e;
+                c.order = a.order;
+            }
+            KF_CUSTOM_DISPATCH(c.kc, {
+                if (f64) ref15_apply_kernel<double, CUSTOM, 4, true><<<g4, 256, 0, stream>>>(c);
+                else ref15_apply_kernel<float, CUSTOM, 4, true><<<g4, 256, 0, stream>>>(c);
             });
         } else {
             if (a.group_waves == 4) ref15_pick_kernel<4><<<g4, 256, 0, stream>>>(a);
