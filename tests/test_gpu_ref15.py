@@ -495,8 +495,9 @@ def _sched_streams(rng, B, T):
     return t0, rates, etype, tt, pay
 
 
-@pytest.mark.parametrize('r_gps,dtype', [(None, 'f64'), (0.0, 'f64'), (400.0, 'f64'), (None, 'f32')])
-def test_sched_two_pass_matches_fused_kernels(r_gps, dtype):
+@pytest.mark.parametrize('r_gps,dtype,nan', [(None, 'f64', False), (0.0, 'f64', False), (400.0, 'f64', False),
+                                             (None, 'f32', False), (None, 'f64', True)])
+def test_sched_two_pass_matches_fused_kernels(r_gps, dtype, nan):
     """KF_OPT_SCHED_KERNEL: the two-pass path (pick pass + apply pass, mispicks rerun by the fused
     kernel; one- and four-wave groups, KF_OPT_SCHED_GROUP; heaviest-first or batch wave order,
     KF_OPT_SCHED_ORDER) equals the fused LDS and register kernels, with the reference constants, with
@@ -506,6 +507,10 @@ def test_sched_two_pass_matches_fused_kernels(r_gps, dtype):
     rng = np.random.default_rng(31)
     B, T = 192, 96
     t0, rates, etype, tt, pay = _sched_streams(rng, B, T)
+    if nan:  # a NaN sample poisons its filter (KF_ENOTSPD, NaN outputs; the gains then leave the
+        # greedy rule to the queue order, which the apply pass checks against the pick pass)
+        for f in (3, 70, 131):
+            pay[20:50, :, f] = np.nan  # 30 events: longer than any window, so one is picked
     ref = ref15.ModelConsts('ref15')
     if r_gps is None:
         params = None
@@ -519,14 +524,16 @@ def test_sched_two_pass_matches_fused_kernels(r_gps, dtype):
     for kern, opts in arms.items():
         kf = kfmi.BatchedKF('ref15', B, dtype, params=params, options=opts)
         res = kf.run_scheduled(tt, etype, pay.astype(np.float32) if dtype == 'f32' else pay, np.full(B, t0), rates)
-        out[kern] = [v.cpu().numpy() for v in res]
+        out[kern] = [v.cpu().numpy() for v in res] + [kf.status().cpu().numpy()]
         kf.close()
-    tr, ld, stt, ns = out['auto']
+    tr, ld, stt, ns, st = out['auto']
     assert ns.min() > 0
+    assert (st != 0).sum() == (3 if nan else 0)
     tol = 1e-12 if dtype == 'f64' else 1e-5  # f32: the same operations, the fp32 event's rounding
     for kern in ('group1', 'one_launch', 'batch_order', 'fused', 'regs'):
-        t2, l2, s2, n2 = out[kern]
+        t2, l2, s2, n2, st2 = out[kern]
         np.testing.assert_array_equal(ns, n2, err_msg=kern)
+        np.testing.assert_array_equal(st, st2, err_msg=kern)
         for f in range(B):  # rows past n_sel are not written
             n = int(ns[f])
             np.testing.assert_array_equal(stt[:n, f], s2[:n, f], err_msg=kern)
