@@ -371,7 +371,10 @@ int kf_score_rows(kf_batch* handle, int n_cand, const int32_t* types, const uint
  * windows and picks from the event times and types (the greedy pick's gains differ only in R,
  * so the constants decide it), then the picked events, with the gains checked on the covariance
  * wherever both sensor classes were queued; a filter where they disagree (a NaN covariance, a
- * rounding tie) is rerun by the fused kernel.  The handle keeps a [T][B] pick workspace.  Streams:
+ * rounding tie) is rerun by the fused kernel.  The handle keeps a [T][B] pick workspace, grown
+ * on demand; inside a graph capture it is never allocated, so a capture before any eager call of
+ * that T runs the fused kernel (same outputs to rounding).  The apply pass runs the waves with
+ * the longest pick lists first (KF_OPT_SCHED_ORDER).  Streams:
  * t device [T][B] absolute event times (double), etype device [T][B] (KF_EVENT_GPS|IMU, NONE =
  * padding at the end), payload device [T][9][B].  prev_time device [B]: time of the state in the
  * handle.  Events within 1/f of the last processed one are queued; the first event past the
