@@ -507,8 +507,7 @@ def test_sched_two_pass_matches_fused_kernels(r_gps, dtype, nan):
     rng = np.random.default_rng(31)
     B, T = 192, 96
     t0, rates, etype, tt, pay = _sched_streams(rng, B, T)
-    if nan:  # a NaN sample poisons its filter (KF_ENOTSPD, NaN outputs; the gains then leave the
-        # greedy rule to the queue order, which the apply pass checks against the pick pass)
+    if nan:  # a NaN sample poisons its filter's state (the covariance never reads it)
         for f in (3, 70, 131):
             pay[20:50, :, f] = np.nan  # 30 events: longer than any window, so one is picked
     ref = ref15.ModelConsts('ref15')
@@ -528,7 +527,9 @@ def test_sched_two_pass_matches_fused_kernels(r_gps, dtype, nan):
         kf.close()
     tr, ld, stt, ns, st = out['auto']
     assert ns.min() > 0
-    assert (st != 0).sum() == (3 if nan else 0)
+    assert (st != 0).sum() == 0  # a NaN measurement leaves P (and so S) intact: NaN states only
+    for f in ((3, 70, 131) if nan else ()):
+        assert np.isnan(tr[:ns[f], :, f]).any(), f
     tol = 1e-12 if dtype == 'f64' else 1e-5  # f32: the same operations, the fp32 event's rounding
     for kern in ('group1', 'one_launch', 'batch_order', 'fused', 'regs'):
         t2, l2, s2, n2, st2 = out[kern]
