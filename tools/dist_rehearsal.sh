@@ -21,3 +21,11 @@ for cfg in 3 ref15; do
     [ $rc -eq 0 ] || { tail -30 "$OUT/c${cfg}_n$n.log"; exit $rc; }
   done
 done
+# the self-launching form (the BENCH command's own: no launcher; bench.py starts its ranks as
+# a child torch.distributed.run and relays rank 0's line)
+timeout -k 10 300 python bench.py --gpus 2 --steps 3 --warmup 1 --config 3 --batch 262144 \
+  --dist-backend gloo --gather-traj-every 8 > "$OUT/self_launch_n2.log" 2>&1
+rc=$?
+echo "self-launch config 3 n=2 rc=$rc" | tee -a "$OUT/steps.txt"
+grep '^{"metric"' "$OUT/self_launch_n2.log" | tail -1 >> "$OUT/lines.jsonl" || true
+[ $rc -eq 0 ] || { tail -30 "$OUT/self_launch_n2.log"; exit $rc; }
