@@ -98,7 +98,7 @@ def main():
             res['configsched'] = {'bytes_per_launch': tot, 'algorithmic_bytes_per_launch': alg,
                                   'traffic_over_algorithmic': tot / alg, 'note': 'pick + apply passes'}
             continue
-        kern = 'ref_events' if c == 'ref15' else 'cv_block_kernel'
+        kern = {'ref15': 'ref_events', '3gen': 'cv_run_kernel'}.get(c, 'cv_block_kernel')
         f = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE'), kern)
         w = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE'), kern)
         fetch = 1024 * sum(f) / len(f)

@@ -51,7 +51,8 @@ def main():
             # the two passes, each timed by its own GRBM_GUI_ACTIVE (GPU busy cycles in the dispatch)
             kerns = {'apply': 'ref15_apply_kernel', 'pick': 'ref15_pick_kernel'}
         else:
-            kerns = {'': {'ref15': 'ref_events', 'sched': 'ref15_sched', '1': 'ref_chain_kernel'}.get(c, 'cv_block_kernel')}
+            kerns = {'': {'ref15': 'ref_events', 'sched': 'ref15_sched', '1': 'ref_chain_kernel',
+                          '3gen': 'cv_run_kernel'}.get(c, 'cv_block_kernel')}
         for tag, kern in kerns.items():
             vals = {}
             for ctr in COUNTERS:
