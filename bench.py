@@ -372,9 +372,11 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
     d = 2 if cfg['model'] == 'cv2' else 3
     bytes_launch, bytes_step = algorithmic_bytes(cfg)
     kernel = 'cv_block_kernel' if block_kernel_in_use(cfg) else 'cv_run_kernel'
+    # the committed PMC summaries hold each row's default kernel (the 3gen row's is the general one)
+    pmc = kernel == ('cv_run_kernel' if cfg.get('coupled') else 'cv_block_kernel')
     return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_step, kernel=kernel,
-                traffic=load_traffic(cfg_id) if kernel == 'cv_block_kernel' else None, cpu=cpu,
-                valu=load_valu(cfg_id) if kernel == 'cv_block_kernel' else None,
+                traffic=load_traffic(cfg_id) if pmc else None, cpu=cpu,
+                valu=load_valu(cfg_id) if pmc else None,
                 gather=gather_payload, kf=kf, pcie=pcie, probe=probe, per_step=per_step, update_every=k,
                 desc=f"BASELINE config {cfg_id}: {cfg['model']} ({2 * d}-state/{d}-meas), {cfg['dtype']}, "
                      f"B={B} filters/GPU, T={T}, dt={dt}, GPS update every {k} step(s)",
@@ -742,7 +744,9 @@ def sched_workload(cfg, args, rank, world, dev):
     else:
         kernel = 'ref15_sched_lds_kernel' if mode == 2 else 'ref15_sched_kernel'
     return dict(step=step, units=B * T, bytes=nbytes, bytes_per_unit=nbytes / (B * T),
-                kernel=kernel, traffic=None, cpu=cpu, gather=None, kf=kf,
+                kernel=kernel, traffic=load_traffic('sched') if mode in (0, 3) and B % 64 == 0 else None,
+                valu=load_valu('sched') if mode in (0, 3) and B % 64 == 0 else None,
+                cpu=cpu, gather=None, kf=kf,
                 roofline_note=f'{n_selected / (B * T):.3f} of the examined events are selected and applied (a '
                               f'full 15-state event each, its payload gathered per lane); latency / issue-bound: '
                               f'the time is the launch sequence on the handle\'s stream',
