@@ -171,7 +171,9 @@ __device__ __forceinline__ T logdet_ldl(const T (&P)[N * (N + 1) / 2]) {
 // NV > 1: NV state vectors share the covariance (filters that differ only in their state, as
 // kf_run_stream's map variants do): S, K and P+ are computed once, every x_v[v] is updated with
 // the same K, each term in the same order as the single-state update.
-template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2, bool POISON = true, int NV = 1>
+// JOSEPH = false: the reference models' own form P+ = (I-KH)P = P - K G^T (kf_workers.py:711,
+// hw5_2.py:372), upper triangle only: the same rows without the E K^T term.
+template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2, bool POISON = true, int NV = 1, bool JOSEPH = true>
 __device__ __forceinline__ bool sel_update_nv(T (&xv)[NV][N], T (&P)[N * (N + 1) / 2], const T (&zv)[NV][M],
                                               const T (&R)[M * (M + 1) / 2]) {
     constexpr int MT = M * (M + 1) / 2;
@@ -250,20 +252,24 @@ __device__ __forceinline__ bool sel_update_nv(T (&xv)[NV][N], T (&P)[N * (N + 1)
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         T E[M];
+        if constexpr (JOSEPH) {
 #pragma unroll
-        for (int a = 0; a < M; ++a) {
-            T e = -P[tri<N>(i, a)];
+            for (int a = 0; a < M; ++a) {
+                T e = -P[tri<N>(i, a)];
 #pragma unroll
-            for (int b = 0; b < M; ++b) e = fmaT(K[i][b], S[tri<M>(b, a)], e);
-            E[a] = e;
+                for (int b = 0; b < M; ++b) e = fmaT(K[i][b], S[tri<M>(b, a)], e);
+                E[a] = e;
+            }
         }
 #pragma unroll
         for (int j = i; j < N; ++j) {
             T s = P[tri<N>(i, j)];
 #pragma unroll
             for (int b = 0; b < M; ++b) s = fmaT(-K[i][b], P[tri<N>(b, j)], s);
+            if constexpr (JOSEPH) {
 #pragma unroll
-            for (int a = 0; a < M; ++a) s = fmaT(E[a], K[j][a], s);
+                for (int a = 0; a < M; ++a) s = fmaT(E[a], K[j][a], s);
+            }
             if (i < M)
                 top[i][j] = s;
             else
@@ -277,7 +283,7 @@ __device__ __forceinline__ bool sel_update_nv(T (&xv)[NV][N], T (&P)[N * (N + 1)
     return ok;
 }
 
-template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2, bool POISON = true>
+template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2, bool POISON = true, bool JOSEPH = true>
 __device__ __forceinline__ bool sel_update(T (&x)[N], T (&P)[N * (N + 1) / 2], const T (&z)[M],
                                            const T (&R)[M * (M + 1) / 2]) {
     T xv[1][N], zv[1][M];
@@ -285,7 +291,7 @@ __device__ __forceinline__ bool sel_update(T (&x)[N], T (&P)[N * (N + 1) / 2], c
     for (int i = 0; i < N; ++i) xv[0][i] = x[i];
 #pragma unroll
     for (int a = 0; a < M; ++a) zv[0][a] = z[a];
-    const bool ok = sel_update_nv<N, M, DIAG_R, T, NEWTON, POISON, 1>(xv, P, zv, R);
+    const bool ok = sel_update_nv<N, M, DIAG_R, T, NEWTON, POISON, 1, JOSEPH>(xv, P, zv, R);
 #pragma unroll
     for (int i = 0; i < N; ++i) x[i] = xv[0][i];
     return ok;

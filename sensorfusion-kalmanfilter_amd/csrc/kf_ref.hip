@@ -33,6 +33,15 @@ using namespace dev;
 constexpr int kGps = 0, kImu = 1;  // KF_EVENT_GPS / KF_EVENT_IMU; 2 = predict only, 255 = none
 // Newton steps on the update's pivot reciprocals (see sel_update)
 constexpr int kRefNewton = 1;
+// Covariance update of the reference models.  fp64 takes the reference's own form
+// P = (I - K H) P (kf_workers.py:711, hw5_2.py:372) over the packed upper triangle; fp32 keeps
+// Joseph's, which the fp32 parity gate needs (the simple form drifts there).
+// KF_REF_JOSEPH_F64=1 builds fp64 with Joseph too (the A/B arm).
+#ifndef KF_REF_JOSEPH_F64
+#define KF_REF_JOSEPH_F64 0
+#endif
+template <typename T>
+constexpr bool kRefJoseph = sizeof(T) == 4 || KF_REF_JOSEPH_F64 != 0;
 
 
 // Noise constants shared by both reference models (kf_workers.py:519-544, 581-614;
@@ -205,7 +214,7 @@ struct Chains {
             T xb[3];
             get_pva(c, xb);
             const T zb[1] = {z[c]};
-            ok = sel_update<3, 1, true, T, kRefNewton, POISON>(xb, pva[c], zb, R) && ok;
+            ok = sel_update<3, 1, true, T, kRefNewton, POISON, kRefJoseph<T>>(xb, pva[c], zb, R) && ok;
             put_pva(c, xb);
         }
         return ok;
@@ -228,7 +237,7 @@ struct Chains {
             const T V = fmaT(a, dt, xb[1]);   // V = x_v + a dt
             const T X = fmaT(V, dt, xb[0]);   // X = x_p + V dt
             const T zb[3] = {X, V, a};
-            ok = sel_update<3, 3, true, T, kRefNewton, POISON>(xb, pva[c], zb, Rp) && ok;
+            ok = sel_update<3, 3, true, T, kRefNewton, POISON, kRefJoseph<T>>(xb, pva[c], zb, Rp) && ok;
             put_pva(c, xb);
         }
 #pragma unroll
@@ -238,7 +247,7 @@ struct Chains {
             T xa[2];
             get_aw(c, xa);
             const T za[2] = {imu[M::imu_att(c)], imu[M::imu_rate(c)]};
-            ok = sel_update<2, 2, true, T, kRefNewton, POISON>(xa, aw[c], za, Ra) && ok;
+            ok = sel_update<2, 2, true, T, kRefNewton, POISON, kRefJoseph<T>>(xa, aw[c], za, Ra) && ok;
             put_aw(c, xa);
         }
         return ok;
@@ -786,7 +795,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
 #pragma unroll
                         for (int v = 0; v < NV; ++v) zb[v][0] = va;
                         const T R[1] = {Rgps};
-                        ok = sel_update_nv<3, 1, true, T, kRefNewton, true, NV>(x, P, zb, R);
+                        ok = sel_update_nv<3, 1, true, T, kRefNewton, true, NV, kRefJoseph<T>>(x, P, zb, R);
                     }
                 } else {
                     T zb[NV][3];
@@ -798,7 +807,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
                         zb[v][1] = pva ? V : vb;
                         zb[v][2] = pva ? vb : T(0);
                     }
-                    ok = sel_update_nv<3, 3, true, T, kRefNewton, true, NV>(x, P, zb, Rimu);
+                    ok = sel_update_nv<3, 3, true, T, kRefNewton, true, NV, kRefJoseph<T>>(x, P, zb, Rimu);
                     if (!pva) {  // reset the inert state
 #pragma unroll
                         for (int v = 0; v < NV; ++v) x[v][2] = T(0);
@@ -1993,13 +2002,13 @@ __device__ __forceinline__ void search_pva(const SearchEvent& v, int ch, T (&Pb)
     C15::template chain_predict<3>(xb, Pb, dt, qpva);
     if (v.type == kGps) {
         const T zb[1] = {T(v.e[2 + ch])};
-        ok = sel_update<3, 1, true, T, kRefNewton, true>(xb, Pb, zb, Rg) && ok;
+        ok = sel_update<3, 1, true, T, kRefNewton, true, kRefJoseph<T>>(xb, Pb, zb, Rg) && ok;
     } else {
         const T acc = T(v.e[2 + M15::imu_acc(ch)]);
         const T V = fmaT(acc, dt, xb[1]);
         const T X = fmaT(V, dt, xb[0]);
         const T zb[3] = {X, V, acc};
-        ok = sel_update<3, 3, true, T, kRefNewton, true>(xb, Pb, zb, Rp) && ok;
+        ok = sel_update<3, 3, true, T, kRefNewton, true, kRefJoseph<T>>(xb, Pb, zb, Rp) && ok;
     }
 }
 
@@ -2013,7 +2022,7 @@ __device__ __forceinline__ void search_aw(const SearchEvent& v, int ch, T (&Pa)[
     C15::template chain_predict<2>(xa, Pa, T(v.dt), qaw);
     if (v.type != kGps) {  // a GPS fix updates the pva chains only
         const T za[2] = {T(v.e[2 + M15::imu_att(ch)]), T(v.e[2 + M15::imu_rate(ch)])};
-        ok = sel_update<2, 2, true, T, kRefNewton, true>(xa, Pa, za, Ra) && ok;
+        ok = sel_update<2, 2, true, T, kRefNewton, true, kRefJoseph<T>>(xa, Pa, za, Ra) && ok;
     }
 }
 
@@ -2074,13 +2083,17 @@ struct SearchScore {
 // The parent's covariance as search_child reads it: from registers, or from a lane's LDS column
 // (the parent-major kernel's LDS variant, which frees the registers that hold it across the
 // loop over children).
+// kChainFence: a scheduling barrier after each chain, so the compiler does not hoist the next
+// chains' LDS reads over this one's arithmetic (which spilled the 3-wave LDS variant)
 template <typename T>
 struct ParRegs {
+    static constexpr bool kChainFence = false;
     const T* P;
     __device__ __forceinline__ T operator()(int i) const { return P[i]; }
 };
 template <typename T>
 struct ParLds {
+    static constexpr bool kChainFence = true;
     const T* col;  // row i at col[i * 64]
     __device__ __forceinline__ T operator()(int i) const { return col[i * 64]; }
 };
@@ -2113,6 +2126,7 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
             search_pva<T, CUSTOM>(vg, ch, Pb, sg.ok, a.kc);
             sg.add_pva(vg, Pb, ch);
         }
+        if constexpr (PS::kChainFence) __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int ch = 0; ch < M15::NA; ++ch) {
@@ -2129,6 +2143,7 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
             search_aw<T, CUSTOM>(vg, ch, Pa, sg.ok, a.kc);
             sg.add_aw(vg, Pa, ch);
         }
+        if constexpr (PS::kChainFence) __builtin_amdgcn_sched_barrier(0);
     }
     T fmax;
     const T run = ss.finish(vs, par.run, fmax);
@@ -2288,7 +2303,7 @@ __device__ __forceinline__ Ref15<T, CUSTOM> posterior(const Ref15<T, CUSTOM>& s0
         T q[3], Rp[6], rg;
         pva_noise<CUSTOM, M15>(s0.kc, 0, q, Rp, rg);
         const T R[1] = {type == kGps ? rg : Rp[0]};
-        sel_update<3, 1, true, T, kRefNewton>(xb, c.pva[0], z, R);
+        sel_update<3, 1, true, T, kRefNewton, true, kRefJoseph<T>>(xb, c.pva[0], z, R);
     } else if (type == kGps) {
         const T z[3] = {T(0), T(0), T(0)};
         c.update_gps(z);
@@ -2367,7 +2382,7 @@ __device__ __forceinline__ T first_row_gain(const Ref15<T, CUSTOM>& s, int type)
     T q[3], Rp[6], rg;
     pva_noise<CUSTOM, M15>(s.kc, 0, q, Rp, rg);
     const T R[1] = {type == kGps ? rg : Rp[0]};
-    sel_update<3, 1, true, T, kRefNewton>(xb, p, z, R);
+    sel_update<3, 1, true, T, kRefNewton, true, kRefJoseph<T>>(xb, p, z, R);
     T tr = p[0] + p[3] + p[5];
 #pragma unroll
     for (int i = 1; i < 3; ++i) tr += s.pva[i][0] + s.pva[i][3] + s.pva[i][5];
