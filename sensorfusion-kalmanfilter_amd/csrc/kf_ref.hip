@@ -2617,6 +2617,9 @@ struct LdsGathered {
 #ifndef KF_PICK_CHUNK
 #define KF_PICK_CHUNK 8
 #endif
+#ifndef KF_APPLY_IMAGES
+#define KF_APPLY_IMAGES 1  // payload images per wave of the two-pass apply (2: two-wave groups)
+#endif
 #ifndef KF_APPLY_PROBE
 #define KF_APPLY_PROBE 0  // 1 / 2 / 3: apply-pass timing probes for in-process A/B builds (tools/ab_inproc.py)
 #endif
@@ -2759,9 +2762,13 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     // instruction per value instead of two dword ones), f32 4 B.  One payload image per wave:
     // the next pick's gather is issued once this event's update has read the image, and waited
     // for after the next predict.
+    // NIMG = 2: two payload images, pick q + 1's gather issued before event q's predict (a whole
+    // event of cover instead of one predict), at the LDS cost of fewer waves per CU
+    constexpr int NIMG = PICK ? 1 : KF_APPLY_IMAGES;
+    static_assert(NIMG == 1 || NIMG == 2, "payload images");
     constexpr int GB = LdsGathered<T>::kSlot;
     constexpr int PAY = 9 * 64 * GB;       // payload image [9][64] slots
-    constexpr int TM = PAY;                // pick times, two rows (q & 1)
+    constexpr int TM = NIMG * PAY;         // pick times, two rows (q & 1)
     constexpr int PK = TM + 2 * 512;       // picks, three rows (q % 3), 64 u32 each
     constexpr int APPLY_LDS = PK + 3 * 256;
     constexpr int WAVE_LDS = PICK && 2 * kPickImg > APPLY_LDS ? 2 * kPickImg : APPLY_LDS;  // the pick phase's images alias
@@ -2817,7 +2824,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
             if (r < 0)
 #endif
                 __builtin_amdgcn_global_load_lds(src + int64_t(i) * B * W,
-                                                 (__attribute__((address_space(3))) void*)(base + i * 64 * GB),
+                                                 (__attribute__((address_space(3))) void*)(base + (r & (NIMG - 1)) * PAY + i * 64 * GB),
                                                  LdsGathered<T>::kSlot, 0, 0);
 #else
         (void)r;
@@ -2835,7 +2842,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
         if (lane < 16) lds_dma16(bytes_rsrc(pb, r < S ? 256u : 0u), base + PK + (r % 3) * 256, uint32_t(lane) * 16u, 0);
     };
     auto pick_row = [&](int r) { return reinterpret_cast<const uint32_t*>(base + PK + (r % 3) * 256)[lane]; };
-    const LdsGathered<T> pay{base + lane * GB + (W == 8 ? (lane & 1) * 8 : 0)};  // read where used
+    const unsigned char* const pay0 = base + lane * GB + (W == 8 ? (lane & 1) * 8 : 0);  // read where used
     if (S > 0) {
         issue_picks(0);
         issue_picks(1);
@@ -2845,8 +2852,18 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     }
     bool bad = false;
     for (int q = 0; q < S; ++q) {
-        // time q and pick row q: older than pick row q + 1, gather q (9) and event q - 1's stores
-        if (q > 0) waitcnt<vmcnt_imm(1 + 9 + NST)>();
+        const LdsGathered<T> pay{pay0 + (q & (NIMG - 1)) * PAY};
+        if constexpr (NIMG == 1) {
+            // time q and pick row q: older than pick row q + 1, gather q (9) and event q - 1's stores
+            if (q > 0) waitcnt<vmcnt_imm(1 + 9 + NST)>();
+        } else {
+            // time q, pick row q + 1 and gather q: older than event q - 1's stores
+            if (q > 0) waitcnt<vmcnt_imm(NST)>();
+            // the other image was last read by event q - 1's update
+            __builtin_amdgcn_s_waitcnt(lgkmcnt0_imm);
+            asm volatile("" ::: "memory");
+            if (q + 1 < S) gather(q + 1, pick_row(q + 1));
+        }
         const double tq = reinterpret_cast<const double*>(base + TM + (q & 1) * 512)[lane];
         const uint32_t pick_c = pick_row(q);
         issue_time(q + 1);
@@ -2877,9 +2894,15 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
         const bool run = live && !bad;
         const T dt = T(tq - prev);
         if (run) s.predict(dt);  // Chains::event, split around the payload wait
-        // gather q: older than event q - 1's stores, time q + 1 and pick row q + 2
-        if (q > 0) waitcnt<vmcnt_imm(NST + 2)>();
-        else waitcnt<vmcnt_imm(2)>();
+        if constexpr (NIMG == 1) {
+            // gather q: older than event q - 1's stores, time q + 1 and pick row q + 2
+            if (q > 0) waitcnt<vmcnt_imm(NST + 2)>();
+            else waitcnt<vmcnt_imm(2)>();
+        } else if (q == 0) {
+            // gather 0: older than gather 1 (when there is one), time 1 and pick row 2
+            if (S > 1) waitcnt<vmcnt_imm(9 + 2)>();
+            else waitcnt<vmcnt_imm(2)>();
+        }
         if (run && (type == kGps || type == kImu)) {
             bool ok;
             if (type == kGps) {
@@ -2897,9 +2920,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
         // the image's reads are done: gather q + 1 into it (its pick row landed before gather q;
         // reading the payload into registers first, to issue the gather before the update, cost
         // 10 spilled registers and measured 5.98 vs 5.45 ms)
-        __builtin_amdgcn_s_waitcnt(lgkmcnt0_imm);
-        asm volatile("" ::: "memory");
-        if (q + 1 < S) gather(q + 1, pick_row(q + 1));
+        if constexpr (NIMG == 1) {
+            __builtin_amdgcn_s_waitcnt(lgkmcnt0_imm);
+            asm volatile("" ::: "memory");
+            if (q + 1 < S) gather(q + 1, pick_row(q + 1));
+        }
         // a record's descriptor per pick (the records of the whole run exceed 32-bit offsets)
         const uint32_t vo = live ? off : kDropOffset;
         const auto r_tr = span_rsrc(a.traj, int64_t(q) * 6, rb, 6u);
@@ -2978,7 +3003,11 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
                 if (e != hipSuccess) return e;
             }
             KF_CUSTOM_DISPATCH(a.kc, {
-                if (a.group_waves == 4) {
+                if (a.group_waves == 4 && KF_APPLY_IMAGES == 2) {  // two images: 8 waves per CU in LDS
+                    const dim3 g2(static_cast<unsigned>((a.B + 127) / 128));
+                    if (f64) ref15_apply_kernel<double, CUSTOM, 2, false><<<g2, 128, 0, stream>>>(a);
+                    else ref15_apply_kernel<float, CUSTOM, 2, false><<<g2, 128, 0, stream>>>(a);
+                } else if (a.group_waves == 4) {
                     if (f64) ref15_apply_kernel<double, CUSTOM, 4, false><<<g4, 256, 0, stream>>>(a);
                     else ref15_apply_kernel<float, CUSTOM, 4, false><<<g4, 256, 0, stream>>>(a);
                 } else {
