@@ -173,7 +173,11 @@ __device__ __forceinline__ T logdet_ldl(const T (&P)[N * (N + 1) / 2]) {
 // the same K, each term in the same order as the single-state update.
 // JOSEPH = false: the reference models' own form P+ = (I-KH)P = P - K G^T (kf_workers.py:711,
 // hw5_2.py:372), upper triangle only: the same rows without the E K^T term.
-template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2, bool POISON = true, int NV = 1, bool JOSEPH = true>
+// GAIN_R (H = I, M == N, diagonal R): P+ = K R.  I - K = (S - P) S^-1 = R S^-1, so
+// (I - K)P = R S^-1 P, the transpose of P S^-1 R = K R, and the product is symmetric: one multiply
+// per entry and no cancellation (P - K P subtracts nearly equal terms where P >> R).
+template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2, bool POISON = true, int NV = 1, bool JOSEPH = true,
+          bool GAIN_R = false>
 __device__ __forceinline__ bool sel_update_nv(T (&xv)[NV][N], T (&P)[N * (N + 1) / 2], const T (&zv)[NV][M],
                                               const T (&R)[M * (M + 1) / 2]) {
     constexpr int MT = M * (M + 1) / 2;
@@ -242,6 +246,13 @@ __device__ __forceinline__ bool sel_update_nv(T (&xv)[NV][N], T (&P)[N * (N + 1)
             xv[v][i] = s;
         }
     }
+    if constexpr (GAIN_R && M == N && DIAG_R) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+#pragma unroll
+            for (int j = i; j < N; ++j) P[tri<N>(i, j)] = K[i][j] * R[tri<M>(j, j)];
+        return ok;
+    }
     // Joseph: P+ = (I-KH) P (I-KH)^T + K R K^T = (P - K G^T) + E K^T with G = P H^T and
     // E = K S - G, an identity for ANY K (E is the residual of the gain equation K S = G,
     // so an error dK in the gain enters P+ only as dK S dK^T).  Upper triangle only, row
@@ -283,7 +294,8 @@ __device__ __forceinline__ bool sel_update_nv(T (&xv)[NV][N], T (&P)[N * (N + 1)
     return ok;
 }
 
-template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2, bool POISON = true, bool JOSEPH = true>
+template <int N, int M, bool DIAG_R, typename T, int NEWTON = 2, bool POISON = true, bool JOSEPH = true,
+          bool GAIN_R = false>
 __device__ __forceinline__ bool sel_update(T (&x)[N], T (&P)[N * (N + 1) / 2], const T (&z)[M],
                                            const T (&R)[M * (M + 1) / 2]) {
     T xv[1][N], zv[1][M];
@@ -291,7 +303,7 @@ __device__ __forceinline__ bool sel_update(T (&x)[N], T (&P)[N * (N + 1) / 2], c
     for (int i = 0; i < N; ++i) xv[0][i] = x[i];
 #pragma unroll
     for (int a = 0; a < M; ++a) zv[0][a] = z[a];
-    const bool ok = sel_update_nv<N, M, DIAG_R, T, NEWTON, POISON, 1, JOSEPH>(xv, P, zv, R);
+    const bool ok = sel_update_nv<N, M, DIAG_R, T, NEWTON, POISON, 1, JOSEPH, GAIN_R>(xv, P, zv, R);
 #pragma unroll
     for (int i = 0; i < N; ++i) x[i] = xv[0][i];
     return ok;

@@ -42,6 +42,13 @@ constexpr int kRefNewton = 1;
 #endif
 template <typename T>
 constexpr bool kRefJoseph = sizeof(T) == 4 || KF_REF_JOSEPH_F64 != 0;
+// The IMU pseudo-measurement's H = I chain updates take P = K R (sel_update_nv's GAIN_R: the
+// same value as (I - K)P, without its cancellation), in both precisions; KF_REF_GAIN_R=0 builds
+// the A/B arm without it.
+#ifndef KF_REF_GAIN_R
+#define KF_REF_GAIN_R 1
+#endif
+constexpr bool kRefGainR = KF_REF_GAIN_R != 0;
 
 
 // Noise constants shared by both reference models (kf_workers.py:519-544, 581-614;
@@ -214,7 +221,7 @@ struct Chains {
             T xb[3];
             get_pva(c, xb);
             const T zb[1] = {z[c]};
-            ok = sel_update<3, 1, true, T, kRefNewton, POISON, kRefJoseph<T>>(xb, pva[c], zb, R) && ok;
+            ok = sel_update<3, 1, true, T, kRefNewton, POISON, kRefJoseph<T>, kRefGainR>(xb, pva[c], zb, R) && ok;
             put_pva(c, xb);
         }
         return ok;
@@ -237,7 +244,7 @@ struct Chains {
             const T V = fmaT(a, dt, xb[1]);   // V = x_v + a dt
             const T X = fmaT(V, dt, xb[0]);   // X = x_p + V dt
             const T zb[3] = {X, V, a};
-            ok = sel_update<3, 3, true, T, kRefNewton, POISON, kRefJoseph<T>>(xb, pva[c], zb, Rp) && ok;
+            ok = sel_update<3, 3, true, T, kRefNewton, POISON, kRefJoseph<T>, kRefGainR>(xb, pva[c], zb, Rp) && ok;
             put_pva(c, xb);
         }
 #pragma unroll
@@ -247,7 +254,7 @@ struct Chains {
             T xa[2];
             get_aw(c, xa);
             const T za[2] = {imu[M::imu_att(c)], imu[M::imu_rate(c)]};
-            ok = sel_update<2, 2, true, T, kRefNewton, POISON, kRefJoseph<T>>(xa, aw[c], za, Ra) && ok;
+            ok = sel_update<2, 2, true, T, kRefNewton, POISON, kRefJoseph<T>, kRefGainR>(xa, aw[c], za, Ra) && ok;
             put_aw(c, xa);
         }
         return ok;
@@ -795,7 +802,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
 #pragma unroll
                         for (int v = 0; v < NV; ++v) zb[v][0] = va;
                         const T R[1] = {Rgps};
-                        ok = sel_update_nv<3, 1, true, T, kRefNewton, true, NV, kRefJoseph<T>>(x, P, zb, R);
+                        ok = sel_update_nv<3, 1, true, T, kRefNewton, true, NV, kRefJoseph<T>, kRefGainR>(x, P, zb, R);
                     }
                 } else {
                     T zb[NV][3];
@@ -807,7 +814,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
                         zb[v][1] = pva ? V : vb;
                         zb[v][2] = pva ? vb : T(0);
                     }
-                    ok = sel_update_nv<3, 3, true, T, kRefNewton, true, NV, kRefJoseph<T>>(x, P, zb, Rimu);
+                    ok = sel_update_nv<3, 3, true, T, kRefNewton, true, NV, kRefJoseph<T>, kRefGainR>(x, P, zb, Rimu);
                     if (!pva) {  // reset the inert state
 #pragma unroll
                         for (int v = 0; v < NV; ++v) x[v][2] = T(0);
@@ -2002,13 +2009,13 @@ __device__ __forceinline__ void search_pva(const SearchEvent& v, int ch, T (&Pb)
     C15::template chain_predict<3>(xb, Pb, dt, qpva);
     if (v.type == kGps) {
         const T zb[1] = {T(v.e[2 + ch])};
-        ok = sel_update<3, 1, true, T, kRefNewton, true, kRefJoseph<T>>(xb, Pb, zb, Rg) && ok;
+        ok = sel_update<3, 1, true, T, kRefNewton, true, kRefJoseph<T>, kRefGainR>(xb, Pb, zb, Rg) && ok;
     } else {
         const T acc = T(v.e[2 + M15::imu_acc(ch)]);
         const T V = fmaT(acc, dt, xb[1]);
         const T X = fmaT(V, dt, xb[0]);
         const T zb[3] = {X, V, acc};
-        ok = sel_update<3, 3, true, T, kRefNewton, true, kRefJoseph<T>>(xb, Pb, zb, Rp) && ok;
+        ok = sel_update<3, 3, true, T, kRefNewton, true, kRefJoseph<T>, kRefGainR>(xb, Pb, zb, Rp) && ok;
     }
 }
 
@@ -2022,7 +2029,7 @@ __device__ __forceinline__ void search_aw(const SearchEvent& v, int ch, T (&Pa)[
     C15::template chain_predict<2>(xa, Pa, T(v.dt), qaw);
     if (v.type != kGps) {  // a GPS fix updates the pva chains only
         const T za[2] = {T(v.e[2 + M15::imu_att(ch)]), T(v.e[2 + M15::imu_rate(ch)])};
-        ok = sel_update<2, 2, true, T, kRefNewton, true, kRefJoseph<T>>(xa, Pa, za, Ra) && ok;
+        ok = sel_update<2, 2, true, T, kRefNewton, true, kRefJoseph<T>, kRefGainR>(xa, Pa, za, Ra) && ok;
     }
 }
 
@@ -2303,7 +2310,7 @@ __device__ __forceinline__ Ref15<T, CUSTOM> posterior(const Ref15<T, CUSTOM>& s0
         T q[3], Rp[6], rg;
         pva_noise<CUSTOM, M15>(s0.kc, 0, q, Rp, rg);
         const T R[1] = {type == kGps ? rg : Rp[0]};
-        sel_update<3, 1, true, T, kRefNewton, true, kRefJoseph<T>>(xb, c.pva[0], z, R);
+        sel_update<3, 1, true, T, kRefNewton, true, kRefJoseph<T>, kRefGainR>(xb, c.pva[0], z, R);
     } else if (type == kGps) {
         const T z[3] = {T(0), T(0), T(0)};
         c.update_gps(z);
@@ -2382,7 +2389,7 @@ __device__ __forceinline__ T first_row_gain(const Ref15<T, CUSTOM>& s, int type)
     T q[3], Rp[6], rg;
     pva_noise<CUSTOM, M15>(s.kc, 0, q, Rp, rg);
     const T R[1] = {type == kGps ? rg : Rp[0]};
-    sel_update<3, 1, true, T, kRefNewton, true, kRefJoseph<T>>(xb, p, z, R);
+    sel_update<3, 1, true, T, kRefNewton, true, kRefJoseph<T>, kRefGainR>(xb, p, z, R);
     T tr = p[0] + p[3] + p[5];
 #pragma unroll
     for (int i = 1; i < 3; ++i) tr += s.pva[i][0] + s.pva[i][3] + s.pva[i][5];
