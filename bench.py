@@ -695,15 +695,27 @@ def sched_workload(cfg, args, rank, world, dev):
     rb = max(1, int(getattr(args, 'rate_block', 64) or 64))
     freq = rates[(torch.arange(B, device=dev) // rb) % len(cfg['rates'])].contiguous()
     prev = torch.full((B,), t0, dtype=torch.float64, device=dev)
+    # the payload as one 80-B record per event (kf_run_scheduled_rec, the default) or as the
+    # [T][9][B] rows of kf_run_scheduled (--sched-payload rows): same events, same outputs
+    rows = getattr(args, 'sched_payload', 'records') == 'rows'
+    recs = None
+    if not rows:
+        recs = torch.zeros(T, B, 10, dtype=torch.float64, device=dev)
+        recs[:, :, :9] = pay.transpose(1, 2)
     traj = kf.empty(T, 6, B)
     logdet = kf.empty(T, B)
     sel_time = torch.empty(T, B, dtype=torch.float64, device=dev)
     n_sel = torch.empty(B, dtype=torch.int32, device=dev)
 
     def step():
-        _lib.check(_lib.lib().kf_run_scheduled(kf.handle, T, _ptr(tt), _ptr(etype), _ptr(pay), _ptr(prev), _ptr(freq),
-                                                0.0, _ptr(traj), _ptr(logdet), _ptr(sel_time), _ptr(n_sel),
-                                                kf._stream()))
+        if rows:
+            _lib.check(_lib.lib().kf_run_scheduled(kf.handle, T, _ptr(tt), _ptr(etype), _ptr(pay), _ptr(prev),
+                                                    _ptr(freq), 0.0, _ptr(traj), _ptr(logdet), _ptr(sel_time),
+                                                    _ptr(n_sel), kf._stream()))
+        else:
+            _lib.check(_lib.lib().kf_run_scheduled_rec(kf.handle, T, _ptr(tt), _ptr(etype), _ptr(recs), 10,
+                                                        _ptr(prev), _ptr(freq), 0.0, _ptr(traj), _ptr(logdet),
+                                                        _ptr(sel_time), _ptr(n_sel), kf._stream()))
 
     step()
     torch.cuda.synchronize(dev)
@@ -752,8 +764,11 @@ def sched_workload(cfg, args, rank, world, dev):
                               f'the time is the launch sequence on the handle\'s stream',
                 desc=f'SURVEY 8f row 3: rate-decimated greedy scheduled filter (kf_workers.py:826-957), reference '
                      f'15-state model, f64, B={B} filters/GPU, T={T} events at 200 Hz (GPS every {k}th), '
-                     f'processing rates {cfg["rates"][0]}..{cfg["rates"][-1]} Hz across the batch (64 filters per rate)',
-                extra={'filters_per_gpu': B, 'events_per_launch': T, 'selected_events': n_selected})
+                     f'processing rates {cfg["rates"][0]}..{cfg["rates"][-1]} Hz across the batch (64 filters per rate), '
+                     + ('payload [T][9][B] rows (kf_run_scheduled)' if rows else
+                        'payload [T][B][10] records (kf_run_scheduled_rec)'),
+                extra={'filters_per_gpu': B, 'events_per_launch': T, 'selected_events': n_selected,
+                       'payload': 'rows' if rows else 'records'})
 
 
 def bf_workload(cfg, args, rank, world, dev):
@@ -928,6 +943,8 @@ def main():
                     help='cv configs, N=1: also time the per-step predict()/update() call shape')
     ap.add_argument('--rate-block', type=int, default=64,
                     help='config sched: consecutive filters sharing a processing rate (1 = per-lane rates)')
+    ap.add_argument('--sched-payload', choices=['records', 'rows'], default='records',
+                    help='config sched: the payload as [T][B][10] records (kf_run_scheduled_rec) or [T][9][B] rows')
     ap.add_argument('--graph', action='store_true',
                     help='config 1: replay the step as a hipGraph (measured no faster than eager launches)')
     ap.add_argument('--ablate', choices=['none', 'no-traj', 'no-logdet', 'no-traj-no-logdet'], default='none',

@@ -387,6 +387,17 @@ int kf_run_scheduled(kf_batch* handle, int T, const double* t, const uint8_t* et
                      const double* prev_time, const double* freq, double freq_all, void* traj, void* logdet,
                      double* sel_time, int32_t* n_sel, void* stream);
 
+/* kf_run_scheduled with the payload as one record per event: records device [T][B][rec_len], the
+ * 9 values of kf_run_scheduled's payload at rec[0..8] (rec[9..] unread: the reference keeps each
+ * event's sensor values together, sdata of its (index, type, time, sdata) tuples,
+ * kf_workers.py:870, 910).  rec_len >= 9 with rec_len * element size a multiple of 16 bytes
+ * (f64: 10, f32: 12) and records 16-byte aligned, else KF_EINVAL.  The picked events' values are
+ * then one contiguous span per filter instead of nine rows B elements apart, which is what the
+ * apply pass gathers.  Same outputs as kf_run_scheduled, bit for bit. */
+int kf_run_scheduled_rec(kf_batch* handle, int T, const double* t, const uint8_t* etype, const void* records,
+                         int rec_len, const double* prev_time, const double* freq, double freq_all, void* traj,
+                         void* logdet, double* sel_time, int32_t* n_sel, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Ingest: CSV logs -> one merged event stream in HBM (the reference's load_data,
  * gps_to_modified_utm, compute_imu_biases, unbias_imu_data, combine_sensor_data;

@@ -1193,15 +1193,26 @@ int kf_score_rows(kf_batch* h, int n_cand, const int32_t* types, const uint32_t*
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_score_rows");
 }
 
-int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, const void* payload,
-                     const double* prev_time, const double* freq, double freq_all, void* traj, void* logdet,
-                     double* sel_time, int32_t* n_sel, void* stream) {
+}  // extern "C"
+
+namespace {
+// kf_run_scheduled (rec = 0: payload rows [T][9][B]) and kf_run_scheduled_rec (rec elements per
+// record, [T][B][rec])
+int run_scheduled(const char* fn, kf_batch* h, int T, const double* t, const uint8_t* etype, const void* payload,
+                  int rec, const double* prev_time, const double* freq, double freq_all, void* traj, void* logdet,
+                  double* sel_time, int32_t* n_sel, void* stream) {
     if (int rc = check_handle(h)) return rc;
-    if (!is_ref15(h)) return fail(KF_EINVAL, "kf_run_scheduled: needs a KF_MODEL_REF15 handle");
-    if (T < 0) return fail(KF_EINVAL, "kf_run_scheduled: T = %d < 0", T);
-    if (!freq && !(freq_all > 0.0)) return fail(KF_EINVAL, "kf_run_scheduled: processing frequency must be > 0");
+    if (!is_ref15(h)) return fail(KF_EINVAL, "%s: needs a KF_MODEL_REF15 handle", fn);
+    if (T < 0) return fail(KF_EINVAL, "%s: T = %d < 0", fn, T);
+    if (!freq && !(freq_all > 0.0)) return fail(KF_EINVAL, "%s: processing frequency must be > 0", fn);
+    const int esz = h->dtype == KF_F64 ? 8 : 4;
+    if (rec && (rec < 9 || (rec * esz) % 16 != 0))
+        return fail(KF_EINVAL, "%s: rec_len = %d: need >= 9 elements and a multiple of 16 bytes (%d-byte elements)",
+                    fn, rec, esz);
+    if (rec && reinterpret_cast<uintptr_t>(payload) % 16 != 0)
+        return fail(KF_EINVAL, "%s: the records must be 16-byte aligned", fn);
     if (h->B == 0) return KF_OK;
-    if (!t || !etype || !payload || !prev_time) return fail(KF_EINVAL, "kf_run_scheduled: null input stream");
+    if (!t || !etype || !payload || !prev_time) return fail(KF_EINVAL, "%s: null input stream", fn);
     kfmi::Ref15SchedArgs a{};
     a.B = h->B;
     a.kc = h->kc;
@@ -1209,6 +1220,7 @@ int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, 
     a.t = t;
     a.etype = etype;
     a.payload = payload;
+    a.pay_rec = rec;
     a.prev_time = prev_time;
     a.freq = freq;
     a.freq_all = freq_all;
@@ -1269,7 +1281,25 @@ int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, 
         }
     }
     hipError_t e = kfmi::launch_ref15_scheduled(h->dtype == KF_F64, a, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? KF_OK : hip_fail(e, "kf_run_scheduled");
+    return e == hipSuccess ? KF_OK : hip_fail(e, fn);
+}
+}  // namespace
+
+extern "C" {
+
+int kf_run_scheduled(kf_batch* h, int T, const double* t, const uint8_t* etype, const void* payload,
+                     const double* prev_time, const double* freq, double freq_all, void* traj, void* logdet,
+                     double* sel_time, int32_t* n_sel, void* stream) {
+    return run_scheduled("kf_run_scheduled", h, T, t, etype, payload, 0, prev_time, freq, freq_all, traj, logdet,
+                         sel_time, n_sel, stream);
+}
+
+int kf_run_scheduled_rec(kf_batch* h, int T, const double* t, const uint8_t* etype, const void* records,
+                         int rec_len, const double* prev_time, const double* freq, double freq_all, void* traj,
+                         void* logdet, double* sel_time, int32_t* n_sel, void* stream) {
+    if (rec_len <= 0) return fail(KF_EINVAL, "kf_run_scheduled_rec: rec_len = %d", rec_len);
+    return run_scheduled("kf_run_scheduled_rec", h, T, t, etype, records, rec_len, prev_time, freq, freq_all, traj,
+                         logdet, sel_time, n_sel, stream);
 }
 
 }  // extern "C"

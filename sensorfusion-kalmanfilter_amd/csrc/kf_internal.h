@@ -261,7 +261,8 @@ struct Ref15SchedArgs {
     int T;
     const double* t;         // [T][B] absolute event times (fp64)
     const uint8_t* etype;    // [T][B]
-    const void* payload;     // [T][9][B]
+    const void* payload;     // [T][9][B], or [T][B][pay_rec] records
+    int pay_rec;             // 0: payload rows [T][9][B]; else elements per record (kf_run_scheduled_rec)
     const double* prev_time; // [B] time of the state in the handle
     const double* freq;      // [B] processing frequency per filter, or nullptr
     double freq_all;         // used when freq == nullptr

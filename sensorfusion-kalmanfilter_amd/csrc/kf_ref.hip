@@ -2472,9 +2472,12 @@ struct SchedLane {
         T pay[9];
         // the selected event differs per lane: plain 64-bit addressing (a buffer descriptor per
         // lane would be a waterfall loop)
-        const T* ps = static_cast<const T*>(a.payload) + int64_t(sel) * 9 * B + f;
+        // [T][9][B] rows, or [T][B][pay_rec] records (kf_run_scheduled_rec)
+        const T* ps = static_cast<const T*>(a.payload) +
+                      (a.pay_rec ? (int64_t(sel) * B + f) * a.pay_rec : int64_t(sel) * 9 * B + f);
+        const int64_t pstep = a.pay_rec ? 1 : B;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) pay[k] = ps[int64_t(k) * B];
+        for (int k = 0; k < 9; ++k) pay[k] = ps[int64_t(k) * pstep];
         bool ok = true;
         s.template event<false>(tsel_type, T(tsel - prev), pay, false, T(0), ok);
         if (!ok) {
@@ -2612,13 +2615,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED
 // ------------------------------------------------------------------------------------
 constexpr int kPickBoth = 0x10, kPickGpsFirst = 0x20;
 
-// payload element i of this lane in the apply pass's image: [9][64] slots of GB bytes per lane,
-// read from LDS where the update uses it
-template <typename T>
+// payload element i of this lane in the apply pass's image, read from LDS where the update uses
+// it.  Rows ([T][9][B]): [9][64] slots of kSlot bytes per lane.  Records ([T][B][rec],
+// REC): the first 9 values of the lane's record as 16-B chunks, [chunk][64][16 B].
+template <typename T, bool REC = false>
 struct LdsGathered {
-    const unsigned char* img;  // image base + this lane's slot + its value's offset in the slot
-    static constexpr int kSlot = sizeof(T) == 8 ? 16 : 4;
-    __device__ __forceinline__ T operator[](int i) const { return *reinterpret_cast<const T*>(img + i * 64 * kSlot); }
+    const unsigned char* img;  // image base + this lane's slot (+ its value's offset in the slot)
+    static constexpr int kSlot = REC || sizeof(T) == 8 ? 16 : 4;
+    static constexpr int kChunks = (9 * int(sizeof(T)) + 15) / 16;  // REC: 16-B chunks per record
+    __device__ __forceinline__ T operator[](int i) const {
+        constexpr int W = int(sizeof(T));
+        if constexpr (REC) return *reinterpret_cast<const T*>(img + ((i * W) >> 4) * 1024 + ((i * W) & 15));
+        else return *reinterpret_cast<const T*>(img + i * 64 * kSlot);
+    }
 };
 
 #ifndef KF_PICK_CHUNK
@@ -2626,6 +2635,9 @@ struct LdsGathered {
 #endif
 #ifndef KF_APPLY_IMAGES
 #define KF_APPLY_IMAGES 1  // payload images per wave of the two-pass apply (2: two-wave groups)
+#endif
+#ifndef KF_REC_IMAGES
+#define KF_REC_IMAGES 1  // payload images per wave of the apply pass over payload records (2: A/B)
 #endif
 #ifndef KF_APPLY_PROBE
 #define KF_APPLY_PROBE 0  // 1 / 2 / 3: apply-pass timing probes for in-process A/B builds (tools/ab_inproc.py)
@@ -2759,7 +2771,9 @@ __global__ __launch_bounds__(kBlock) void ref15_rate_key_kernel(const Ref15Sched
 
 // PICK: the wave runs its pick pass first (one launch for both passes: a wave's streaming pick
 // phase overlaps the other waves' compute-bound apply phases)
-template <typename T, bool CUSTOM, int WAVES, bool PICK>
+// REC: the payload is [T][B][pay_rec] records (kf_run_scheduled_rec): a lane's 9 values are one
+// contiguous 72-B (f64) span, gathered as 16-B chunks, instead of 9 rows B elements apart
+template <typename T, bool CUSTOM, int WAVES, bool PICK, bool REC = false>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void ref15_apply_kernel(
     const Ref15SchedArgs a) {
     constexpr int W = int(sizeof(T));
@@ -2771,10 +2785,13 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     // for after the next predict.
     // NIMG = 2: two payload images, pick q + 1's gather issued before event q's predict (a whole
     // event of cover instead of one predict), at the LDS cost of fewer waves per CU
-    constexpr int NIMG = PICK ? 1 : KF_APPLY_IMAGES;
+    // (records: 5-KB images, so two fit 12 waves per CU, KF_REC_IMAGES=2: measured no faster)
+    constexpr int NIMG = PICK ? 1 : REC ? KF_REC_IMAGES : KF_APPLY_IMAGES;
     static_assert(NIMG == 1 || NIMG == 2, "payload images");
-    constexpr int GB = LdsGathered<T>::kSlot;
-    constexpr int PAY = 9 * 64 * GB;       // payload image [9][64] slots
+    using Gathered = LdsGathered<T, REC>;
+    constexpr int GB = Gathered::kSlot;
+    constexpr int PAY = REC ? Gathered::kChunks * 1024 : 9 * 64 * GB;  // payload image
+    constexpr int NG = REC ? Gathered::kChunks : 9;                     // gather instructions per pick
     constexpr int TM = NIMG * PAY;         // pick times, two rows (q & 1)
     constexpr int PK = TM + 2 * 512;       // picks, three rows (q % 3), 64 u32 each
     constexpr int APPLY_LDS = PK + 3 * 256;
@@ -2813,7 +2830,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     }
     S = wave_uniform(S);
     waitcnt<vmcnt_imm(0)>();
-    // pick r's payload (9 VMEM): a lane past its list reads row 0.  Device pass only: the 16-B
+    // pick r's payload (NG VMEM): a lane past its list reads row 0.  Device pass only: the 16-B
     // form of the builtin is a gfx950 one, and the host pass would drop the kernel's stub.
     auto gather = [&](int r, uint32_t pick) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -2824,15 +2841,24 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
 #else
         const int64_t row = (r < nsel && ev < uint32_t(a.T)) ? int64_t(ev) : 0;
 #endif
-        const char* src = reinterpret_cast<const char*>(a.payload) + (row * 9 * B + col) * W;
+        if constexpr (REC) {  // the record's first kChunks 16-B chunks (within pay_rec * W bytes)
+            const char* src = reinterpret_cast<const char*>(a.payload) + (row * B + f) * int64_t(a.pay_rec) * W;
 #pragma unroll
-        for (int i = 0; i < 9; ++i)
+            for (int c = 0; c < Gathered::kChunks; ++c)
+                __builtin_amdgcn_global_load_lds(src + c * 16,
+                                                 (__attribute__((address_space(3))) void*)(base + (r & (NIMG - 1)) * PAY + c * 1024),
+                                                 16, 0, 0);
+        } else {
+            const char* src = reinterpret_cast<const char*>(a.payload) + (row * 9 * B + col) * W;
+#pragma unroll
+            for (int i = 0; i < 9; ++i)
 #if KF_APPLY_PROBE == 2  // timing probe (wrong results): no payload gather
-            if (r < 0)
+                if (r < 0)
 #endif
-                __builtin_amdgcn_global_load_lds(src + int64_t(i) * B * W,
-                                                 (__attribute__((address_space(3))) void*)(base + (r & (NIMG - 1)) * PAY + i * 64 * GB),
-                                                 LdsGathered<T>::kSlot, 0, 0);
+                    __builtin_amdgcn_global_load_lds(src + int64_t(i) * B * W,
+                                                     (__attribute__((address_space(3))) void*)(base + (r & (NIMG - 1)) * PAY + i * 64 * GB),
+                                                     Gathered::kSlot, 0, 0);
+        }
 #else
         (void)r;
         (void)pick;
@@ -2849,7 +2875,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
         if (lane < 16) lds_dma16(bytes_rsrc(pb, r < S ? 256u : 0u), base + PK + (r % 3) * 256, uint32_t(lane) * 16u, 0);
     };
     auto pick_row = [&](int r) { return reinterpret_cast<const uint32_t*>(base + PK + (r % 3) * 256)[lane]; };
-    const unsigned char* const pay0 = base + lane * GB + (W == 8 ? (lane & 1) * 8 : 0);  // read where used
+    const unsigned char* const pay0 = base + lane * GB + (!REC && W == 8 ? (lane & 1) * 8 : 0);  // read where used
     if (S > 0) {
         issue_picks(0);
         issue_picks(1);
@@ -2859,10 +2885,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     }
     bool bad = false;
     for (int q = 0; q < S; ++q) {
-        const LdsGathered<T> pay{pay0 + (q & (NIMG - 1)) * PAY};
+        const Gathered pay{pay0 + (q & (NIMG - 1)) * PAY};
         if constexpr (NIMG == 1) {
-            // time q and pick row q: older than pick row q + 1, gather q (9) and event q - 1's stores
-            if (q > 0) waitcnt<vmcnt_imm(1 + 9 + NST)>();
+            // time q and pick row q: older than pick row q + 1, gather q (NG) and event q - 1's stores
+            if (q > 0) waitcnt<vmcnt_imm(1 + NG + NST)>();
         } else {
             // time q, pick row q + 1 and gather q: older than event q - 1's stores
             if (q > 0) waitcnt<vmcnt_imm(NST)>();
@@ -2907,7 +2933,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
             else waitcnt<vmcnt_imm(2)>();
         } else if (q == 0) {
             // gather 0: older than gather 1 (when there is one), time 1 and pick row 2
-            if (S > 1) waitcnt<vmcnt_imm(9 + 2)>();
+            if (S > 1) waitcnt<vmcnt_imm(NG + 2)>();
             else waitcnt<vmcnt_imm(2)>();
         }
         if (run && (type == kGps || type == kImu)) {
@@ -2978,12 +3004,13 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
     const bool two = lds && !a.fused && a.picks && a.flags && a.n_sel && a.sel_time && a.T < (1 << 24) &&
                      uint64_t(a.B) * 6u * (f64 ? 8u : 4u) < (uint64_t(1) << 32) &&
                      reinterpret_cast<uintptr_t>(a.sel_time) % 16 == 0 &&
-                     (!f64 || reinterpret_cast<uintptr_t>(a.payload) % 16 == 0);
+                     ((!f64 && !a.pay_rec) || reinterpret_cast<uintptr_t>(a.payload) % 16 == 0) &&
+                     (!a.pay_rec || (a.pay_rec * (f64 ? 8 : 4)) % 16 == 0);
     if (two) {
         // four-wave groups (KF_OPT_SCHED_GROUP): one-wave groups, which free their slot when their
         // wave's pick list ends, measured slower on the bench row (5.51 vs 5.07 ms apply)
         const dim3 g1(static_cast<unsigned>(a.B / 64)), g4(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-        if (a.one_launch) {
+        if (a.one_launch && !a.pay_rec) {  // records: the two launches
             Ref15SchedArgs c = a;  // heaviest first by rate where the filters have their own rates
             c.order = nullptr;
             if (a.order && a.freq) {
@@ -3010,11 +3037,18 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
                 if (e != hipSuccess) return e;
             }
             KF_CUSTOM_DISPATCH(a.kc, {
-                if (a.group_waves == 4 && KF_APPLY_IMAGES == 2) {  // two images: 8 waves per CU in LDS
+                if (a.pay_rec) {  // payload records (kf_run_scheduled_rec): four-wave groups
+                    if (f64) ref15_apply_kernel<double, CUSTOM, 4, false, true><<<g4, 256, 0, stream>>>(a);
+                    else ref15_apply_kernel<float, CUSTOM, 4, false, true><<<g4, 256, 0, stream>>>(a);
+                } else
+#if KF_APPLY_IMAGES == 2
+                if (a.group_waves == 4) {  // two images: 8 waves per CU in LDS
                     const dim3 g2(static_cast<unsigned>((a.B + 127) / 128));
                     if (f64) ref15_apply_kernel<double, CUSTOM, 2, false><<<g2, 128, 0, stream>>>(a);
                     else ref15_apply_kernel<float, CUSTOM, 2, false><<<g2, 128, 0, stream>>>(a);
-                } else if (a.group_waves == 4) {
+                } else
+#endif
+                if (a.group_waves == 4) {
                     if (f64) ref15_apply_kernel<double, CUSTOM, 4, false><<<g4, 256, 0, stream>>>(a);
                     else ref15_apply_kernel<float, CUSTOM, 4, false><<<g4, 256, 0, stream>>>(a);
                 } else {

@@ -468,17 +468,20 @@ class BatchedKF:
                                        mk.ctypes.data_as(ctypes.c_void_p), _ptr(out), _ptr(post), self._stream()))
         return (out, post) if posterior else out
 
-    def run_scheduled(self, t, etype, payload, prev_time, freq):
+    def run_scheduled(self, t, etype, payload, prev_time, freq, records=False):
         """KF_MODEL_REF15 rate-decimated greedy filter (kf_run_scheduled).  t [T, B] float64
-        absolute times, etype [T, B] uint8, payload [T, 9, B], prev_time [B] float64, freq scalar
-        or [B] float64 (a sampling sweep in one launch).  Returns (traj [T, 6, B], logdet [T, B],
-        sel_time [T, B], n_sel [B]) with the first n_sel[f] rows of filter f valid."""
+        absolute times, etype [T, B] uint8, payload [T, 9, B] — or, with records=True, one record
+        per event [T, B, rec] (rec >= 9, rec * element size a multiple of 16 B: kf_run_scheduled_rec)
+        — prev_time [B] float64, freq scalar or [B] float64 (a sampling sweep in one launch).
+        Returns (traj [T, 6, B], logdet [T, B], sel_time [T, B], n_sel [B]) with the first n_sel[f]
+        rows of filter f valid."""
         if self.model != 'ref15':
             raise ValueError('run_scheduled needs a ref15 handle')
         T = int(t.shape[0])
         td = self._dev(t, (T, self.batch), 't', torch.float64)
         et = self._dev(etype, (T, self.batch), 'etype', torch.uint8)
-        pay = self._dev(payload, (T, 9, self.batch), 'payload')
+        rec = int(payload.shape[2]) if records else 0
+        pay = self._dev(payload, (T, self.batch, rec) if records else (T, 9, self.batch), 'payload')
         pv = self._dev(prev_time, (self.batch,), 'prev_time', torch.float64)
         fr = None
         if np.ndim(freq) != 0:
@@ -487,9 +490,14 @@ class BatchedKF:
         ld = self.empty(max(T, 1), self.batch)
         stt = torch.empty(max(T, 1), self.batch, dtype=torch.float64, device=self.device)
         ns = torch.empty(self.batch, dtype=torch.int32, device=self.device)
-        check(_lib.lib().kf_run_scheduled(self.handle, T, _ptr(td), _ptr(et), _ptr(pay), _ptr(pv), _ptr(fr),
-                                          float(freq) if fr is None else 0.0, _ptr(tr), _ptr(ld), _ptr(stt),
-                                          _ptr(ns), self._stream()))
+        fa = float(freq) if fr is None else 0.0
+        if records:
+            check(_lib.lib().kf_run_scheduled_rec(self.handle, T, _ptr(td), _ptr(et), _ptr(pay), rec, _ptr(pv),
+                                                  _ptr(fr), fa, _ptr(tr), _ptr(ld), _ptr(stt), _ptr(ns),
+                                                  self._stream()))
+        else:
+            check(_lib.lib().kf_run_scheduled(self.handle, T, _ptr(td), _ptr(et), _ptr(pay), _ptr(pv), _ptr(fr),
+                                              fa, _ptr(tr), _ptr(ld), _ptr(stt), _ptr(ns), self._stream()))
         return tr, ld, stt, ns
 
     # -- synthetic streams -----------------------------------------------

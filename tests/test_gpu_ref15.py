@@ -520,11 +520,27 @@ def test_sched_two_pass_matches_fused_kernels(r_gps, dtype, nan):
     arms = {'auto': {}, 'group1': {'sched_group': 'wave'}, 'one_launch': {'sched_kernel': 'one_launch'},
             'batch_order': {'sched_order': 'batch'}, 'fused': {'sched_kernel': 'fused'},
             'regs': {'sched_kernel': 'regs'}}
-    for kern, opts in arms.items():
+    # the same runs with the payload as one record per event (kf_run_scheduled_rec)
+    rec_arms = {'rec_' + k: v for k, v in arms.items() if k != 'batch_order'}
+    payt = pay.astype(np.float32) if dtype == 'f32' else pay
+    recs = _sched_records(payt, 10 if dtype == 'f64' else 12)
+    for kern, opts in {**arms, **rec_arms}.items():
         kf = kfmi.BatchedKF('ref15', B, dtype, params=params, options=opts)
-        res = kf.run_scheduled(tt, etype, pay.astype(np.float32) if dtype == 'f32' else pay, np.full(B, t0), rates)
+        if kern.startswith('rec_'):
+            res = kf.run_scheduled(tt, etype, recs, np.full(B, t0), rates, records=True)
+        else:
+            res = kf.run_scheduled(tt, etype, payt, np.full(B, t0), rates)
         out[kern] = [v.cpu().numpy() for v in res] + [kf.status().cpu().numpy()]
         kf.close()
+    for kern in rec_arms:  # the records change only where the values are read from: bitwise
+        for a, b in zip(out[kern[4:]], out[kern]):
+            if a.ndim == 1:
+                np.testing.assert_array_equal(a, b, err_msg=kern)
+        ns0 = out[kern[4:]][3]
+        for f in range(B):
+            n = int(ns0[f])
+            for a, b in zip(out[kern[4:]][:3], out[kern][:3]):
+                np.testing.assert_array_equal(a[:n, ..., f], b[:n, ..., f], err_msg=kern)
     tr, ld, stt, ns, st = out['auto']
     assert ns.min() > 0
     assert (st != 0).sum() == 0  # a NaN measurement leaves P (and so S) intact: NaN states only
@@ -540,6 +556,35 @@ def test_sched_two_pass_matches_fused_kernels(r_gps, dtype, nan):
             np.testing.assert_array_equal(stt[:n, f], s2[:n, f], err_msg=kern)
             np.testing.assert_allclose(tr[:n, :, f], t2[:n, :, f], rtol=tol, atol=tol, err_msg=kern)
             np.testing.assert_allclose(ld[:n, f], l2[:n, f], rtol=tol, atol=tol, err_msg=kern)
+
+
+def _sched_records(pay, rec):
+    """[T, 9, B] payload rows -> [T, B, rec] records (kf_run_scheduled_rec), the pad slots NaN
+    (never read)."""
+    T, _, B = pay.shape
+    r = np.full((T, B, rec), np.nan, dtype=pay.dtype)
+    k = min(rec, 9)  # (a too-short record for the rejection test)
+    r[:, :, :k] = pay.transpose(0, 2, 1)[:, :, :k]
+    return r
+
+
+def test_sched_records_reject_bad_layouts():
+    """kf_run_scheduled_rec: a record shorter than 9 values, one whose byte length is not a
+    multiple of 16, and records that are not 16-byte aligned are KF_EINVAL."""
+    rng = np.random.default_rng(5)
+    B, T = 64, 16
+    t0, rates, etype, tt, pay = _sched_streams(rng, B, T)
+    dev = torch.device('cuda', 0)
+    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    for rec in (8, 9, 11):
+        with pytest.raises(kfmi.KFError, match='rec_len'):
+            kf.run_scheduled(tt, etype, _sched_records(pay, rec), np.full(B, t0), rates, records=True)
+    buf = torch.zeros(T * B * 10 + 1, dtype=torch.float64, device=dev)
+    mis = buf[1:].view(T, B, 10)  # 8 bytes past a 16-byte boundary
+    mis.copy_(torch.as_tensor(_sched_records(pay, 10), device=dev))
+    with pytest.raises(kfmi.KFError, match='aligned'):
+        kf.run_scheduled(tt, etype, mis, np.full(B, t0), rates, records=True)
+    kf.close()
 
 
 @pytest.mark.parametrize('warm', [True, False])
