@@ -695,12 +695,13 @@ def sched_workload(cfg, args, rank, world, dev):
     rb = max(1, int(getattr(args, 'rate_block', 64) or 64))
     freq = rates[(torch.arange(B, device=dev) // rb) % len(cfg['rates'])].contiguous()
     prev = torch.full((B,), t0, dtype=torch.float64, device=dev)
-    # the payload as one 80-B record per event (kf_run_scheduled_rec, the default) or as the
+    # the payload as one 96-B record per event (kf_run_scheduled_rec, the default) or as the
     # [T][9][B] rows of kf_run_scheduled (--sched-payload rows): same events, same outputs
     rows = getattr(args, 'sched_payload', 'records') == 'rows'
+    rec = int(getattr(args, 'sched_rec', 12) or 12)
     recs = None
     if not rows:
-        recs = torch.zeros(T, B, 10, dtype=torch.float64, device=dev)
+        recs = torch.zeros(T, B, rec, dtype=torch.float64, device=dev)
         recs[:, :, :9] = pay.transpose(1, 2)
     traj = kf.empty(T, 6, B)
     logdet = kf.empty(T, B)
@@ -713,7 +714,7 @@ def sched_workload(cfg, args, rank, world, dev):
                                                     _ptr(freq), 0.0, _ptr(traj), _ptr(logdet), _ptr(sel_time),
                                                     _ptr(n_sel), kf._stream()))
         else:
-            _lib.check(_lib.lib().kf_run_scheduled_rec(kf.handle, T, _ptr(tt), _ptr(etype), _ptr(recs), 10,
+            _lib.check(_lib.lib().kf_run_scheduled_rec(kf.handle, T, _ptr(tt), _ptr(etype), _ptr(recs), rec,
                                                         _ptr(prev), _ptr(freq), 0.0, _ptr(traj), _ptr(logdet),
                                                         _ptr(sel_time), _ptr(n_sel), kf._stream()))
 
@@ -766,9 +767,9 @@ def sched_workload(cfg, args, rank, world, dev):
                      f'15-state model, f64, B={B} filters/GPU, T={T} events at 200 Hz (GPS every {k}th), '
                      f'processing rates {cfg["rates"][0]}..{cfg["rates"][-1]} Hz across the batch (64 filters per rate), '
                      + ('payload [T][9][B] rows (kf_run_scheduled)' if rows else
-                        'payload [T][B][10] records (kf_run_scheduled_rec)'),
+                        f'payload [T][B][{rec}] records (kf_run_scheduled_rec)'),
                 extra={'filters_per_gpu': B, 'events_per_launch': T, 'selected_events': n_selected,
-                       'payload': 'rows' if rows else 'records'})
+                       'payload': 'rows' if rows else f'records of {rec}'})
 
 
 def bf_workload(cfg, args, rank, world, dev):
@@ -945,6 +946,9 @@ def main():
                     help='config sched: consecutive filters sharing a processing rate (1 = per-lane rates)')
     ap.add_argument('--sched-payload', choices=['records', 'rows'], default='records',
                     help='config sched: the payload as [T][B][10] records (kf_run_scheduled_rec) or [T][9][B] rows')
+    ap.add_argument('--sched-rec', type=int, default=12,
+                    help='config sched, records: doubles per record (>= 10, even; 12 = 96-B records on 32-B '
+                         'boundaries, the fastest measured)')
     ap.add_argument('--graph', action='store_true',
                     help='config 1: replay the step as a hipGraph (measured no faster than eager launches)')
     ap.add_argument('--ablate', choices=['none', 'no-traj', 'no-logdet', 'no-traj-no-logdet'], default='none',

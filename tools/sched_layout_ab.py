@@ -1,7 +1,7 @@
 """In-process A/B of the sched row's payload layout: [T][9][B] rows (kf_run_scheduled) against
-[T][B][10] records (kf_run_scheduled_rec), on one set of streams, alternating launches.
+[T][B][N] records (kf_run_scheduled_rec), on one set of streams, alternating launches.
 
-    python tools/sched_layout_ab.py [--rounds 6] [--launches 10] [--rate-block 64]
+    python tools/sched_layout_ab.py [--arms rows,rec10,rec12] [--rounds 6] [--launches 10] [--rate-block 64]
 """
 import argparse
 import json
@@ -18,6 +18,7 @@ def main():
     ap.add_argument('--rounds', type=int, default=6)
     ap.add_argument('--launches', type=int, default=10)
     ap.add_argument('--rate-block', type=int, default=64)
+    ap.add_argument('--arms', default='rows,rec10', help='rows and/or recN (N doubles per record)')
     args = ap.parse_args()
     import torch
     import bench
@@ -26,9 +27,10 @@ def main():
     cfg = dict(bench.CONFIGS['sched'])
     cfg['opts'] = {}
     arms = {}
-    for lay in ('rows', 'records'):
+    for lay in args.arms.split(','):
         ns = argparse.Namespace(ablate='none', gpus=1, no_cpu_baseline=True, rate_block=args.rate_block,
-                                sched_payload=lay)
+                                sched_payload='rows' if lay == 'rows' else 'records',
+                                sched_rec=0 if lay == 'rows' else int(lay[3:]))
         arms[lay] = bench.sched_workload(cfg, ns, 0, 1, dev)
     for lay, w in arms.items():
         w['step']()
