@@ -172,7 +172,7 @@ __device__ __forceinline__ T logdet_ldl(const T (&P)[N * (N + 1) / 2]) {
 // kf_run_stream's map variants do): S, K and P+ are computed once, every x_v[v] is updated with
 // the same K, each term in the same order as the single-state update.
 // JOSEPH = false: the reference models' own form P+ = (I-KH)P = P - K G^T (kf_workers.py:711,
-// hw5_2.py:372), upper triangle only: the same rows without the E K^T term.
+// hw5_2.py:358, 376), upper triangle only: the same rows without the E K^T term.
 // GAIN_R (H = I, M == N, diagonal R): P+ = K R.  I - K = (S - P) S^-1 = R S^-1, so
 // (I - K)P = R S^-1 P, the transpose of P S^-1 R = K R, and the product is symmetric: one multiply
 // per entry and no cancellation (P - K P subtracts nearly equal terms where P >> R).

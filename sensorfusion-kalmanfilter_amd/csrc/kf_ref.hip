@@ -34,7 +34,7 @@ constexpr int kGps = 0, kImu = 1;  // KF_EVENT_GPS / KF_EVENT_IMU; 2 = predict o
 // Newton steps on the update's pivot reciprocals (see sel_update)
 constexpr int kRefNewton = 1;
 // Covariance update of the reference models.  fp64 takes the reference's own form
-// P = (I - K H) P (kf_workers.py:711, hw5_2.py:372) over the packed upper triangle; fp32 keeps
+// P = (I - K H) P (kf_workers.py:711, hw5_2.py:358, 376) over the packed upper triangle; fp32 keeps
 // Joseph's, which the fp32 parity gate needs (the simple form drifts there).
 // KF_REF_JOSEPH_F64=1 builds fp64 with Joseph too (the A/B arm).
 #ifndef KF_REF_JOSEPH_F64
