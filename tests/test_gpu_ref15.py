@@ -2,8 +2,9 @@
 (tests/golden/ref15_*.npz) and the CPU oracle — needs an MI355X.
 
 Tolerance (north_star): 1e-6 relative for fp64 (states normalised by max(|x|, 1), logdets by
-max(|logdet|, 1)); the engine uses the Joseph form and LDL^T solves where the reference uses
-(I-KH)P and np.linalg.inv, so agreement is ~1e-10, not bitwise.
+max(|logdet|, 1)); the engine solves by LDL^T where the reference uses np.linalg.inv, and forms
+(I-KH)P per chain (P = KR for the IMU's H = I chains; Joseph for the fp32 GPS fix), so agreement
+is ~1e-10, not bitwise.
 """
 import math
 import os
@@ -766,7 +767,8 @@ def test_ref15_bench_size_sampled():
 
 def test_sched_bench_size_sampled():
     """The sched bench workload at its full size (2^20 filters x 256 events, 64 filters per rate,
-    the LDS-staged kernel), 24 filters spread over the batch against the oracle's greedy driver."""
+    the two passes), 24 filters spread over the batch against the oracle's greedy driver; the
+    bench's payload records give every output bitwise."""
     dev = torch.device('cuda', 0)
     B, T, k = 1 << 20, 256, 20
     rates_all = (10, 20, 30, 40, 50, 60, 70, 80, 90, 100, 110, 120)
@@ -783,7 +785,21 @@ def test_sched_bench_size_sampled():
     rates = torch.tensor(rates_all, dtype=torch.float64, device=dev)
     freq = rates[(torch.arange(B, device=dev) // 64) % len(rates_all)].contiguous()
     kf = kfmi.BatchedKF('ref15', B, 'f64')
-    tr, ld, stt, ns = kf.run_scheduled(tt, etype, pay, torch.full((B,), t0, dtype=torch.float64, device=dev), freq)
+    prev = torch.full((B,), t0, dtype=torch.float64, device=dev)
+    # the bench's layout: 12-double records (kf_run_scheduled_rec), every output bitwise the rows'
+    recs = torch.zeros(T, B, 12, dtype=torch.float64, device=dev)
+    recs[:, :, :9] = pay.transpose(1, 2)
+    rec_out = kf.run_scheduled(tt, etype, recs, prev, freq, records=True)
+    del recs
+    kf.close()
+    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    tr, ld, stt, ns = kf.run_scheduled(tt, etype, pay, prev, freq)
+    assert torch.equal(ns, rec_out[3])
+    live = torch.arange(T, device=dev)[:, None] < ns[None, :].long()  # rows past n_sel are not written
+    for a, b in zip((tr, ld, stt), rec_out[:3]):
+        m = live[:, None, :] if a.dim() == 3 else live
+        assert torch.equal(torch.where(m, a, 0.0), torch.where(m, b, 0.0))
+    del rec_out
     idx = torch.linspace(0, B - 1, 24).long().to(dev)
     tr, ld, stt, ns = (v[..., idx].cpu().numpy() for v in (tr, ld, stt, ns))
     et, ts, pa, fr = (v[..., idx].cpu().numpy() for v in (etype, tt, pay, freq))
