@@ -1206,7 +1206,7 @@ int run_scheduled(const char* fn, kf_batch* h, int T, const double* t, const uin
     if (T < 0) return fail(KF_EINVAL, "%s: T = %d < 0", fn, T);
     if (!freq && !(freq_all > 0.0)) return fail(KF_EINVAL, "%s: processing frequency must be > 0", fn);
     const int esz = h->dtype == KF_F64 ? 8 : 4;
-    if (rec && (rec < 9 || (rec * esz) % 16 != 0))
+    if (rec && (rec < 9 || (int64_t(rec) * esz) % 16 != 0))
         return fail(KF_EINVAL, "%s: rec_len = %d: need >= 9 elements and a multiple of 16 bytes (%d-byte elements)",
                     fn, rec, esz);
     if (rec && reinterpret_cast<uintptr_t>(payload) % 16 != 0)

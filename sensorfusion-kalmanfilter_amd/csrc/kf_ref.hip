@@ -3005,7 +3005,7 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
                      uint64_t(a.B) * 6u * (f64 ? 8u : 4u) < (uint64_t(1) << 32) &&
                      reinterpret_cast<uintptr_t>(a.sel_time) % 16 == 0 &&
                      ((!f64 && !a.pay_rec) || reinterpret_cast<uintptr_t>(a.payload) % 16 == 0) &&
-                     (!a.pay_rec || (a.pay_rec * (f64 ? 8 : 4)) % 16 == 0);
+                     (!a.pay_rec || (int64_t(a.pay_rec) * (f64 ? 8 : 4)) % 16 == 0);
     if (two) {
         // four-wave groups (KF_OPT_SCHED_GROUP): one-wave groups, which free their slot when their
         // wave's pick list ends, measured slower on the bench row (5.51 vs 5.07 ms apply)
