@@ -761,8 +761,9 @@ def sched_workload(cfg, args, rank, world, dev):
                 valu=load_valu('sched') if mode in (0, 3) and B % 64 == 0 else None,
                 cpu=cpu, gather=None, kf=kf,
                 roofline_note=f'{n_selected / (B * T):.3f} of the examined events are selected and applied (a '
-                              f'full 15-state event each, its payload gathered per lane); latency / issue-bound: '
-                              f'the time is the launch sequence on the handle\'s stream',
+                              f'full 15-state event each, its payload gathered per lane); the two passes move '
+                              f'their actual HBM traffic (traffic, PMC: the gathers fetch whole 32-B sectors) at '
+                              f'the HBM\'s practical rate, so frac understates them by traffic / algorithmic',
                 desc=f'SURVEY 8f row 3: rate-decimated greedy scheduled filter (kf_workers.py:826-957), reference '
                      f'15-state model, f64, B={B} filters/GPU, T={T} events at 200 Hz (GPS every {k}th), '
                      f'processing rates {cfg["rates"][0]}..{cfg["rates"][-1]} Hz across the batch (64 filters per rate), '
