@@ -11,6 +11,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/kf.h"
 #include "kf_internal.h"
@@ -28,6 +29,12 @@ struct kf_batch {
     void* P;          // [n(n+1)/2][B]
     int32_t* status;  // [B]
     void* ws;         // KF_MODEL_REF15: device workspace for kf_eval_combos (events, binomials, init)
+    // what ws holds (the binomials from kf_alloc on; the events and init of the last upload, whose
+    // copy ws_evt marks on ws_stream): a search or evaluation over the same inputs uploads nothing
+    std::vector<double> ws_events, ws_init;
+    int ws_n;
+    hipEvent_t ws_evt;
+    hipStream_t ws_stream;
     void* search_ws;  // KF_MODEL_REF15: kf_search_combos level buffers (grown on demand)
     size_t search_ws_bytes;
     bool r_diag;      // BASELINE models: R has no off-diagonal entry
@@ -109,14 +116,33 @@ const uint64_t* binom_table() {
     return binom;
 }
 
-// Upload the combination search's inputs (events, binomials, root state) to the handle's workspace.
+bool capturing(hipStream_t st);
+
+// Upload the combination search's inputs (events, root state) to the handle's workspace (the
+// binomials went there at kf_alloc).  Inputs equal, bit for bit, to the last upload are already
+// there: nothing is copied, and a call on another stream waits for that upload's copy.  Inside
+// a graph capture the inputs are always copied (the capture holds its own copy nodes).
 int upload_combo_inputs(kf_batch* h, int n_events, const double* events, const double* init, hipStream_t st,
                         const char* what) {
     char* ws = static_cast<char*>(h->ws);
-    hipError_t e = hipMemcpyAsync(ws, events, sizeof(double) * 11 * n_events, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(ws + kWsEvents, binom_table(), kWsBinom, hipMemcpyHostToDevice, st);
+    const size_t ne = size_t(11) * size_t(n_events);
+    const bool cap = capturing(st);
+    if (!cap && h->ws_n == n_events && std::memcmp(h->ws_events.data(), events, sizeof(double) * ne) == 0 &&
+        std::memcmp(h->ws_init.data(), init, kWsInit) == 0) {
+        const hipError_t e = h->ws_stream == st ? hipSuccess : hipStreamWaitEvent(st, h->ws_evt, 0);
+        return e == hipSuccess ? KF_OK : hip_fail(e, what);
+    }
+    h->ws_n = -1;  // until this upload is queued
+    hipError_t e = hipMemcpyAsync(ws, events, sizeof(double) * ne, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(ws + kWsEvents + kWsBinom, init, kWsInit, hipMemcpyHostToDevice, st);
-    return e == hipSuccess ? KF_OK : hip_fail(e, what);
+    if (e != hipSuccess) return hip_fail(e, what);
+    if (!cap && hipEventRecord(h->ws_evt, st) == hipSuccess) {
+        h->ws_events.assign(events, events + ne);
+        h->ws_init.assign(init, init + kWsInit / sizeof(double));
+        h->ws_n = n_events;
+        h->ws_stream = st;
+    }
+    return KF_OK;
 }
 
 // kf_search_combos kernel per level: child-major (one wave per parent block and child event)
@@ -439,7 +465,11 @@ int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_pa
         kf_free(h);
         return fail(KF_ENOMEM, "hipMalloc of the control copy of %zu filters failed", nb);
     }
-    if (model == KF_MODEL_REF15 && hipMalloc(&h->ws, kWsEvents + kWsBinom + kWsInit) != hipSuccess) {
+    h->ws_n = -1;
+    if (model == KF_MODEL_REF15 &&
+        (hipMalloc(&h->ws, kWsEvents + kWsBinom + kWsInit) != hipSuccess ||
+         hipMemcpy(static_cast<char*>(h->ws) + kWsEvents, binom_table(), kWsBinom, hipMemcpyHostToDevice) != hipSuccess ||
+         hipEventCreateWithFlags(&h->ws_evt, hipEventDisableTiming) != hipSuccess)) {
         (void)hipGetLastError();
         kf_free(h);
         return fail(KF_ENOMEM, "hipMalloc of the combination workspace failed");
@@ -478,6 +508,7 @@ int kf_free(kf_batch* h) {
     if (h->P) (void)hipFree(h->P);
     if (h->status) (void)hipFree(h->status);
     if (h->ws) (void)hipFree(h->ws);
+    if (h->ws_evt) (void)hipEventDestroy(h->ws_evt);
     if (h->search_ws) (void)hipFree(h->search_ws);
     if (h->flag) (void)hipFree(h->flag);
     if (h->stream_ws) (void)hipFree(h->stream_ws);

@@ -150,6 +150,49 @@ def test_search_subset_max_equals_eval_combos(golden_dir, dtype, kernel):
     assert worst <= (1e-12 if dtype == 'f64' else 1e-6), (worst, exact, total)
 
 
+def test_combo_inputs_reused_and_refreshed(golden_dir):
+    """The handle keeps the last uploaded candidates and root on the device: a call with other
+    inputs uploads them, a call with the same ones reuses them, also from another stream (which
+    then waits for that upload), and kf_eval_combos shares the workspace.  Every result equals a
+    fresh handle's, bit for bit."""
+    n = 10
+    cand, ev, init, t0, target = _search_case(golden_dir, n)
+    ev2 = ev.copy()
+    ev2[[2, 5]] = ev2[[5, 2]]  # two candidates out of time order: other subsets skip a negative dt
+    init2 = init.copy()
+    init2[15] *= 1.5  # another root covariance
+
+    def search(kf, e, i):
+        _, _, _, sm = kf.search_combos(e, i, t0, target, threshold=-1e30, exhaustive=True, subset_max=True)
+        return sm.cpu().numpy()
+
+    def evals(kf, e, i):
+        return kf.eval_combos(e, i, t0, target, 3, logdets=False)[0].cpu().numpy()
+
+    fresh = {}
+    for key, (e, i) in {'a': (ev, init), 'b': (ev2, init), 'c': (ev, init2)}.items():
+        kf = kfmi.BatchedKF('ref15', 1, 'f64')
+        fresh[key] = search(kf, e, i)
+        kf.close()
+    assert not np.array_equal(fresh['a'][1:], fresh['b'][1:]) and not np.array_equal(fresh['a'][1:], fresh['c'][1:])
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    for key, (e, i) in (('a', (ev, init)), ('a', (ev, init)), ('b', (ev2, init)), ('c', (ev, init2)), ('a', (ev, init))):
+        np.testing.assert_array_equal(search(kf, e, i), fresh[key], err_msg=key)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        got = search(kf, ev, init)
+    np.testing.assert_array_equal(got, fresh['a'])
+    kf.close()
+    # kf_eval_combos over the same workspace, interleaved with searches
+    kc = kfmi.BatchedKF('ref15', math.comb(n, 3), 'f64')
+    e_a, e_b = evals(kc, ev, init), evals(kc, ev2, init)
+    np.testing.assert_array_equal(evals(kc, ev, init), e_a)
+    kc.close()
+    kc = kfmi.BatchedKF('ref15', math.comb(n, 3), 'f64')
+    np.testing.assert_array_equal(evals(kc, ev2, init), e_b)
+    kc.close()
+
+
 @pytest.mark.parametrize('kernel', ['cm', 'pm'])
 @pytest.mark.parametrize('n,k_max', [(1, 1), (2, 2), (3, 3), (4, 4), (9, 3), (9, 8), (9, 9)])
 def test_search_small_and_cut_levels(golden_dir, n, k_max, kernel):
