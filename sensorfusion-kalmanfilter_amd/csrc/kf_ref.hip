@@ -2778,9 +2778,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     const Ref15SchedArgs a) {
     constexpr int W = int(sizeof(T));
     // The picked payload is gathered per lane: the picks of a wave's lanes lie on different rows,
-    // so every gather instruction touches up to 64 cache lines and the address unit, not HBM,
-    // bounds the pass.  f64 moves 16 B per lane (the aligned pair holding the lane's value: one
-    // instruction per value instead of two dword ones), f32 4 B.  One payload image per wave:
+    // so with the [T][9][B] rows every gather instruction touches up to 64 cache lines and the
+    // address unit, not HBM, bounds the pass.  f64 moves 16 B per lane (the aligned pair holding
+    // the lane's value: one instruction per value instead of two dword ones), f32 4 B.  With
+    // records (REC) a pick is 5 (f64) / 3 (f32) 16-B chunks of one span, and the pass moves its
+    // bytes at the HBM's rate.  One payload image per wave:
     // the next pick's gather is issued once this event's update has read the image, and waited
     // for after the next predict.
     // NIMG = 2: two payload images, pick q + 1's gather issued before event q's predict (a whole
