@@ -40,6 +40,16 @@ def test_binding_arity_matches_header_prototypes():
         assert len(_lib.SIGNATURES[name][1]) == n, (name, params)
 
 
+def test_integration_guide_binds_every_header_function():
+    """INTEGRATION.md's reference-side ctypes stubs cover every entry point include/kf.h
+    declares (the maintainer's binding stays in step with the header)."""
+    import re
+    guide = open(os.path.join(os.path.dirname(_lib.HEADER), '..', 'INTEGRATION.md')).read()
+    documented = set(re.findall(r'lib\.(kf_\w+)\.(?:argtypes|restype)', guide))
+    missing = sorted(set(_lib.header_functions()) - documented)
+    assert not missing, f'INTEGRATION.md has no ctypes stub for {missing}'
+
+
 def test_header_constants_match_binding():
     text = open(_lib.HEADER).read()
     for name in ('KF_OK', 'KF_EINVAL', 'KF_EHIP', 'KF_ENOTSPD', 'KF_ENODEV', 'KF_ENOMEM',
