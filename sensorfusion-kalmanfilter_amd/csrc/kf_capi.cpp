@@ -33,6 +33,7 @@ struct kf_batch {
     // copy ws_evt marks on ws_stream): a search or evaluation over the same inputs uploads nothing
     std::vector<double> ws_events, ws_init;
     int ws_n;
+    bool ws_captured;  // an upload was captured into a graph: its replays rewrite ws, so never skip
     hipEvent_t ws_evt;
     hipStream_t ws_stream;
     void* search_ws;  // KF_MODEL_REF15: kf_search_combos level buffers (grown on demand)
@@ -120,14 +121,17 @@ bool capturing(hipStream_t st);
 
 // Upload the combination search's inputs (events, root state) to the handle's workspace (the
 // binomials went there at kf_alloc).  Inputs equal, bit for bit, to the last upload are already
-// there: nothing is copied, and a call on another stream waits for that upload's copy.  Inside
-// a graph capture the inputs are always copied (the capture holds its own copy nodes).
+// there: nothing is copied, and a call on another stream waits for that upload's copy.  A call
+// inside a graph capture copies (HIP refuses to capture a copy from pageable host memory, so
+// such a capture fails today; were it to succeed, its replays would rewrite the workspace
+// behind the cache, so from then on every call copies).
 int upload_combo_inputs(kf_batch* h, int n_events, const double* events, const double* init, hipStream_t st,
                         const char* what) {
     char* ws = static_cast<char*>(h->ws);
     const size_t ne = size_t(11) * size_t(n_events);
     const bool cap = capturing(st);
-    if (!cap && h->ws_n == n_events && std::memcmp(h->ws_events.data(), events, sizeof(double) * ne) == 0 &&
+    if (cap) h->ws_captured = true;
+    if (!h->ws_captured && h->ws_n == n_events && std::memcmp(h->ws_events.data(), events, sizeof(double) * ne) == 0 &&
         std::memcmp(h->ws_init.data(), init, kWsInit) == 0) {
         const hipError_t e = h->ws_stream == st ? hipSuccess : hipStreamWaitEvent(st, h->ws_evt, 0);
         return e == hipSuccess ? KF_OK : hip_fail(e, what);
