@@ -133,7 +133,7 @@ const char* kf_version(void);
  *   KF_OPT_SCHED_KERNEL   kf_run_scheduled: 0 = auto (the two passes where legal, as 3), 1 = the
  *                         fused register-input kernel, 2 = the fused LDS-input kernel, 3 = the
  *                         pick and apply passes as two launches, 4 = as the two phases of one
- *                         launch (kf_run_scheduled_rec: as 3)
+ *                         launch
  *   KF_OPT_SCHED_GROUP    kf_run_scheduled's two passes: waves per workgroup, 0 = 4, 1 or 4
  *                         (one-wave groups free their slot when their wave's pick list ends;
  *                         measured slower; kf_run_scheduled_rec's apply pass: 4)

@@ -3012,7 +3012,7 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
         // four-wave groups (KF_OPT_SCHED_GROUP): one-wave groups, which free their slot when their
         // wave's pick list ends, measured slower on the bench row (5.51 vs 5.07 ms apply)
         const dim3 g1(static_cast<unsigned>(a.B / 64)), g4(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-        if (a.one_launch && !a.pay_rec) {  // records: the two launches
+        if (a.one_launch) {
             Ref15SchedArgs c = a;  // heaviest first by rate where the filters have their own rates
             c.order = nullptr;
             if (a.order && a.freq) {
@@ -3024,8 +3024,13 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
                 c.order = a.order;
             }
             KF_CUSTOM_DISPATCH(c.kc, {
-                if (f64) ref15_apply_kernel<double, CUSTOM, 4, true><<<g4, 256, 0, stream>>>(c);
-                else ref15_apply_kernel<float, CUSTOM, 4, true><<<g4, 256, 0, stream>>>(c);
+                if (c.pay_rec) {
+                    if (f64) ref15_apply_kernel<double, CUSTOM, 4, true, true><<<g4, 256, 0, stream>>>(c);
+                    else ref15_apply_kernel<float, CUSTOM, 4, true, true><<<g4, 256, 0, stream>>>(c);
+                } else {
+                    if (f64) ref15_apply_kernel<double, CUSTOM, 4, true><<<g4, 256, 0, stream>>>(c);
+                    else ref15_apply_kernel<float, CUSTOM, 4, true><<<g4, 256, 0, stream>>>(c);
+                }
             });
         } else {
             if (a.group_waves == 4) ref15_pick_kernel<4><<<g4, 256, 0, stream>>>(a);
