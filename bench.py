@@ -383,16 +383,12 @@ def cv_workload(cfg_id, cfg, args, rank, world, dev):
                 extra={'filters_per_gpu': B, 'time_steps_per_launch': T, 'update_every': k})
 
 
-def ref15_workload(cfg, args, rank, world, dev):
-    """The reference's 15-state model on 200 Hz IMU + 10 Hz GPS event streams (every k-th event a
-    GPS fix), one stream per filter, synthetic (torch RNG on the device; the reference's
-    imu_data.csv is absent)."""
-    import kfmi
-    from kfmi import _lib
-    from kfmi.engine import _ptr
-    B, T, dt, k = cfg['B'], cfg['T'], cfg['dt'], cfg['k']
-    kf = kfmi.BatchedKF('ref15', B, cfg['dtype'], device=dev.index, options=cfg.get('opts'))
-    g = torch.Generator(device=dev).manual_seed(SEED + rank)
+def ref15_streams(B, T, dt, k, seed, dev, dtype=torch.float64):
+    """The ref15 rows' event streams (also the bench-size parity tests'): every k-th event a GPS
+    fix, the others 200 Hz IMU samples, dt fixed; torch's Philox draws on the device.  Returns
+    etype [T, B] u8, dt [T, B] f64, payload [T, 9, B] in ``dtype`` (fp32: the f64 draws rounded
+    once)."""
+    g = torch.Generator(device=dev).manual_seed(seed)
     etype = torch.ones(T, B, dtype=torch.uint8, device=dev)
     etype[k - 1::k] = 0
     dts = torch.full((T, B), dt, dtype=torch.float64, device=dev)
@@ -402,7 +398,69 @@ def ref15_workload(cfg, args, rank, world, dev):
     pay[:, 6:9] *= 0.3    # accelerations
     gps = (etype == 0)[:, None, :]
     pay[:, 0:3] = torch.where(gps, pay[:, 0:3] * 60.0, pay[:, 0:3])  # GPS fixes within ~3 m
-    pay = pay.to(kf.torch_dtype)  # the fp32 row: the same draws rounded once
+    return etype, dts, pay.to(dtype)
+
+
+SCHED_T0 = 1697739278.761565
+
+
+def sched_streams(B, T, dt, k, rates, rate_block, seed, dev):
+    """The sched row's streams (also its bench-size parity test's): 200 Hz events with +-0.5 ms
+    jitter per filter and event, every k-th a GPS fix; one processing rate per ``rate_block``
+    consecutive filters.  Returns t [T, B], etype [T, B], payload [T, 9, B], freq [B], prev [B]."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    t0 = SCHED_T0
+    etype = torch.ones(T, B, dtype=torch.uint8, device=dev)
+    etype[k - 1::k] = 0
+    tt = (t0 + dt * torch.arange(1, T + 1, dtype=torch.float64, device=dev)[:, None]
+          + 5e-4 * (torch.rand(T, B, dtype=torch.float64, device=dev, generator=g) - 0.5))
+    pay = torch.randn(T, 9, B, dtype=torch.float64, device=dev, generator=g)
+    pay[:, 0:3] *= 0.05
+    pay[:, 3:6] *= 0.01
+    pay[:, 6:9] *= 0.3
+    gps = (etype == 0)[:, None, :]
+    pay[:, 0:3] = torch.where(gps, pay[:, 0:3] * 60.0, pay[:, 0:3])
+    rates = torch.tensor(rates, dtype=torch.float64, device=dev)
+    freq = rates[(torch.arange(B, device=dev) // max(1, rate_block)) % len(rates)].contiguous()
+    prev = torch.full((B,), t0, dtype=torch.float64, device=dev)
+    return tt, etype, pay, freq, prev
+
+
+BF_T0 = 1697739552.3362827
+
+
+def bf_events(n, seed=SEED):
+    """The bf row's n candidate events after a warm start (also its parity test's): 200 Hz IMU
+    samples with a GPS fix every 20th, a block-diagonal warm-start covariance of the shape the
+    reference's own runs produce.  Returns (ev [n, 11] (t, type, payload), init (x, blocks), Pw,
+    t0, t_end)."""
+    from kfmi import ref15 as r15
+    rng = np.random.default_rng(seed)
+    t0 = BF_T0
+    ev = np.zeros((n, 11))
+    ev[:, 0] = t0 + 0.005 * np.arange(1, n + 1)
+    ev[:, 1] = 1
+    ev[::20, 1] = 0          # GPS fixes among the IMU samples (10 Hz vs 200 Hz)
+    ev[:, 2:5] = rng.normal(0, 0.05, (n, 3))
+    ev[:, 5:8] = rng.normal(0, 0.01, (n, 3))
+    ev[:, 8:11] = rng.normal(0, 0.3, (n, 3))
+    gps = ev[:, 1] == 0
+    ev[gps, 2:5] = rng.normal(0, 3, (int(gps.sum()), 3))
+    Pw = np.diag([0.9, 0.9, 0.9, 0.02, 0.02, 0.02, 0.5, 0.5, 0.5, 0.05, 0.05, 0.05, 20.0, 20.0, 20.0])
+    init = np.concatenate([np.zeros(15), r15.to_blocks(Pw)])
+    return ev, init, Pw, t0, t0 + 0.005 * (n + 1)
+
+
+def ref15_workload(cfg, args, rank, world, dev):
+    """The reference's 15-state model on 200 Hz IMU + 10 Hz GPS event streams (every k-th event a
+    GPS fix), one stream per filter, synthetic (torch RNG on the device; the reference's
+    imu_data.csv is absent)."""
+    import kfmi
+    from kfmi import _lib
+    from kfmi.engine import _ptr
+    B, T, dt, k = cfg['B'], cfg['T'], cfg['dt'], cfg['k']
+    kf = kfmi.BatchedKF('ref15', B, cfg['dtype'], device=dev.index, options=cfg.get('opts'))
+    etype, dts, pay = ref15_streams(B, T, dt, k, SEED + rank, dev, kf.torch_dtype)
     traj = kf.empty(T, 6, B)
     logdet = kf.empty(T, B)
 
@@ -675,26 +733,12 @@ def sched_workload(cfg, args, rank, world, dev):
     from kfmi.engine import _ptr
     B, T, dt, k = cfg['B'], cfg['T'], cfg['dt'], cfg['k']
     kf = kfmi.BatchedKF('ref15', B, 'f64', device=dev.index, options=cfg.get('opts'))
-    g = torch.Generator(device=dev).manual_seed(SEED + rank)
-    t0 = 1697739278.761565
-    etype = torch.ones(T, B, dtype=torch.uint8, device=dev)
-    etype[k - 1::k] = 0
-    # 200 Hz with +-0.5 ms jitter per filter and event
-    tt = (t0 + dt * torch.arange(1, T + 1, dtype=torch.float64, device=dev)[:, None]
-          + 5e-4 * (torch.rand(T, B, dtype=torch.float64, device=dev, generator=g) - 0.5))
-    pay = torch.randn(T, 9, B, dtype=torch.float64, device=dev, generator=g)
-    pay[:, 0:3] *= 0.05
-    pay[:, 3:6] *= 0.01
-    pay[:, 6:9] *= 0.3
-    gps = (etype == 0)[:, None, :]
-    pay[:, 0:3] = torch.where(gps, pay[:, 0:3] * 60.0, pay[:, 0:3])
-    rates = torch.tensor(cfg['rates'], dtype=torch.float64, device=dev)
+    t0 = SCHED_T0
     # one rate per 64 consecutive filters (a wave): the sweep's filters batched by rate, so the
     # lanes of a wave reach their processing windows together (the jitter aside);
     # --rate-block 1 gives every lane of a wave its own rate (the divergent case)
     rb = max(1, int(getattr(args, 'rate_block', 64) or 64))
-    freq = rates[(torch.arange(B, device=dev) // rb) % len(cfg['rates'])].contiguous()
-    prev = torch.full((B,), t0, dtype=torch.float64, device=dev)
+    tt, etype, pay, freq, prev = sched_streams(B, T, dt, k, cfg['rates'], rb, SEED + rank, dev)
     # the payload as one 96-B record per event (kf_run_scheduled_rec, the default) or as the
     # [T][9][B] rows of kf_run_scheduled (--sched-payload rows): same events, same outputs
     rows = getattr(args, 'sched_payload', 'records') == 'rows'
@@ -778,28 +822,13 @@ def bf_workload(cfg, args, rank, world, dev):
     k-subset, k = 1..n, of n candidate events after a warm start, through kf_eval_combos.  Each
     rank runs the whole search (weak scaling: the same search per GPU)."""
     import kfmi
-    from kfmi import ref15 as r15
     n, chunk = cfg['n'], cfg['chunk']
-    rng = np.random.default_rng(SEED)
-    t0 = 1697739552.3362827
-    ev = np.zeros((n, 11))
-    ev[:, 0] = t0 + 0.005 * np.arange(1, n + 1)
-    ev[:, 1] = 1
-    ev[::20, 1] = 0          # GPS fixes among the IMU samples (10 Hz vs 200 Hz)
-    ev[:, 2:5] = rng.normal(0, 0.05, (n, 3))
-    ev[:, 5:8] = rng.normal(0, 0.01, (n, 3))
-    ev[:, 8:11] = rng.normal(0, 0.3, (n, 3))
-    gps = ev[:, 1] == 0
-    ev[gps, 2:5] = rng.normal(0, 3, (int(gps.sum()), 3))
-    # a warm-start covariance of the shape the reference's own runs produce (block-diagonal)
-    Pw = np.diag([0.9, 0.9, 0.9, 0.02, 0.02, 0.02, 0.5, 0.5, 0.5, 0.05, 0.05, 0.05, 20.0, 20.0, 20.0])
-    init = np.concatenate([np.zeros(15), r15.to_blocks(Pw)])
+    ev, init, Pw, t0, t_end = bf_events(n)
     width = min(chunk, max(math.comb(n, k) for k in range(1, n + 1)))
     kf = kfmi.BatchedKF('ref15', width, 'f64', device=dev.index)
     total_combos = 2 ** n - 1
     total_steps = sum(math.comb(n, k) * (k + 1) for k in range(1, n + 1))
     launches = [(k, off) for k in range(1, n + 1) for off in range(0, math.comb(n, k), width)]
-    t_end = t0 + 0.005 * (n + 1)
     search = cfg['search']
     if search:
         kf.close()

@@ -16,13 +16,28 @@
  * driven by Python time loops (kf_workers.py:623-728, 22-97).  Each entry point below
  * names the reference code it replaces.  The per-step math is
  *     x = F x + G u;  P = F P F^T + Q;  K = P H^T (H P H^T + R)^-1;
- *     x += K (z - H x);  P = (I - K H) P (I - K H)^T + K R K^T   (Joseph form)
- * with S^-1 from an in-lane LDL^T factorisation and logdet(P) from an LDL^T of P.
+ *     x += K (z - H x);  then the covariance update, whose form depends on the model:
+ *   - KF_MODEL_CV2 / CV3 (both dtypes): Joseph's form
+ *         P = (I - K H) P (I - K H)^T + K R K^T   (north_star);
+ *   - KF_MODEL_REF15 / REF8, fp64: the reference's own P = (I - K H) P (kf_workers.py:711,
+ *     hw5_2.py:358, 376); a build with -DKF_REF_JOSEPH_F64=1 takes Joseph's form instead;
+ *   - KF_MODEL_REF15 / REF8, fp32: Joseph's form (the simple form drifts in fp32);
+ *   - the IMU pseudo-measurement's H = I chain updates of REF15 / REF8, both dtypes: P = K R,
+ *     which equals (I - K H) P exactly when H = I and R is diagonal; a build
+ *     with -DKF_REF_GAIN_R=0 takes the dtype's form above instead.
+ * S^-1 comes from an in-lane LDL^T factorisation and logdet(P) from an LDL^T of P (block
+ * determinants for the reference models).
  *
  * All functions return KF_OK (0) or a negative KF_E* code; kf_last_error() then
  * describes the failure (thread-local).  Launching entry points are asynchronous on
- * the given hipStream_t (NULL = the null stream) and never synchronise, allocate or
- * free, so they can be captured into a hipGraph.
+ * the given hipStream_t (NULL = the null stream) and never synchronise, so they can be
+ * captured into a hipGraph.  Workspaces: kf_search_combos, kf_run_stream and
+ * kf_run_scheduled(_rec) keep a device workspace in the handle, allocated by the first call
+ * that needs it and grown (hipMalloc; hipFree synchronises the device) only by a call that
+ * needs more than every earlier one; every other launch allocates nothing.  Run such a call
+ * once eagerly before capturing it: inside a capture nothing is allocated (kf_run_scheduled
+ * then takes its fused kernel, the other two return KF_EINVAL).  A workspace a capture used
+ * is never freed before kf_free, so a graph stays valid after a later, larger eager call.
  *
  * Threading: distinct handles may be used from different threads at once; one handle is used
  * by one thread at a time.  That includes the calls that only read it (kf_get_state,

@@ -296,3 +296,111 @@ void cpu_ref15_events(int64_t B, int T, const uint8_t* etype, const double* dt, 
         }
     }
 }
+
+/* Scheduler.gain (kf_workers.py:174-185) with cov_matrix(S = [1]) (kf_workers.py:112-147, the
+ * device='cpu' branch): trace(Sigma - ((Sigma h^T) inv(r + h (Sigma h^T)) h) Sigma) for the
+ * first measurement row h of the sensor's H (a unit row: H_gps and H_imu both start with e_0)
+ * and its noise r = R[0][0].  The trace is summed in index order (the reference's np.trace may
+ * pair terms; the gains only rank candidates, they are not outputs). */
+static double sched_gain(const double* P, double r) {
+    double h[15] = {0}, Ph[15], hPh, Si, KhP[225];
+    h[0] = 1.0;
+    matmul_bt(15, 15, 1, P, h, Ph);            /* Sigma h^T */
+    matmul(1, 15, 1, h, Ph, &hPh);             /* h (Sigma h^T) */
+    const double S = r + hPh;
+    if (!inv(1, &S, &Si)) return NAN;
+    double K[15], Kh[225];
+    for (int i = 0; i < 15; ++i) K[i] = Ph[i] * Si;
+    matmul(15, 1, 15, K, h, Kh);
+    matmul(15, 15, 15, Kh, P, KhP);
+    double tr = 0.0;
+    for (int i = 0; i < 15; ++i) tr += P[i * 15 + i] - KhP[i * 15 + i];
+    return tr;
+}
+
+/* run_kalman_filter_scheduled, greedy arm, warm start (kf_workers.py:826-957): per filter, the
+ * events of column f of t [T][B], etype [T][B] (0 GPS, 1 IMU), payload [T][9][B] follow the
+ * warm-start event (time prev0[f], state x0[0:6][f] (NULL: zeros), covariance P0).  An event
+ * within 1/freq[f] of the last processed time is queued; the next one past the window picks
+ * the first queued candidate of largest gain (Scheduler.greedy_schedule :195-213; an empty queue
+ * takes the triggering event itself, otherwise it is dropped), then one predict over the
+ * accumulated dt and one update on the pick.  Outputs per pick j < n_sel[f]: sel_time [T][B],
+ * traj [T][6][B] (x[0:6]), logdet [T][B].  Filters [f0, f1). */
+void cpu_ref15_sched(int64_t B, int T, const double* t, const uint8_t* etype, const double* payload,
+                     const double* prev0, const double* freq, const double* x0, const double* P0, double* sel_time,
+                     double* traj, double* logdet_out, int32_t* n_sel, int64_t f0, int64_t f1, int nthreads) {
+    static const double rimu[5] = {50.0, 0.05, 10.0, 0.1, 100.0};
+    double Hg[3 * 15] = {0}, Rg[9] = {0}, Hi[225] = {0}, Ri[225] = {0};
+    for (int i = 0; i < 3; ++i) {
+        Hg[i * 15 + i] = 1.0;
+        Rg[i * 3 + i] = 3.0;
+    }
+    for (int i = 0; i < 15; ++i) {
+        Hi[i * 15 + i] = 1.0;
+        Ri[i * 15 + i] = rimu[i / 3];
+    }
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 16)
+    for (int64_t f = f0; f < f1; ++f) {
+        double x[15] = {0}, P[225], F[225], Q[225];
+        if (x0)
+            for (int i = 0; i < 6; ++i) x[i] = x0[i * B + f];
+        memcpy(P, P0, sizeof(P));
+        double prev = prev0[f];
+        const double win = 1.0 / freq[f];
+        int q0 = 0, nq = 0, ns = 0;              /* the queue is the events [q0, q0 + nq) */
+        for (int i = 0; i < T; ++i) {
+            const double ti = t[(int64_t)i * B + f];
+            if (ti - prev < win) {
+                if (nq == 0) q0 = i;
+                ++nq;
+                continue;
+            }
+            if (nq == 0) {
+                q0 = i;
+                nq = 1;
+            }
+            int sel = -1;
+            double best = -INFINITY;
+            for (int q = q0; q < q0 + nq; ++q) {
+                const int ty = etype[(int64_t)q * B + f];
+                const double g = sched_gain(P, ty == 0 ? Rg[0] : Ri[0]);
+                if (g > best) {
+                    best = g;
+                    sel = q;
+                }
+            }
+            if (sel < 0) sel = q0;
+            nq = 0;
+            const double st = t[(int64_t)sel * B + f];
+            const double h = st - prev;
+            const int ty = etype[(int64_t)sel * B + f];
+            const double* p = payload + (int64_t)sel * 9 * B + f;
+            F15(h, F);
+            Q15(h, Q);
+            predict(15, F, Q, NULL, x, P);
+            if (ty == 0) {
+                const double Z[3] = {p[0], p[B], p[2 * B]};
+                update(15, 3, Hg, Rg, Z, x, P);
+            } else {
+                double Z[15];
+                for (int c = 0; c < 3; ++c) {
+                    const double a = p[(6 + c) * B];
+                    const double V = x[6 + c] + a * h;
+                    Z[c] = x[c] + V * h;
+                    Z[3 + c] = p[c * B];
+                    Z[6 + c] = V;
+                    Z[9 + c] = p[(3 + c) * B];
+                    Z[12 + c] = a;
+                }
+                update(15, 15, Hi, Ri, Z, x, P);
+            }
+            if (sel_time) sel_time[(int64_t)ns * B + f] = st;
+            if (traj)
+                for (int c = 0; c < 6; ++c) traj[((int64_t)ns * 6 + c) * B + f] = x[c];
+            if (logdet_out) logdet_out[(int64_t)ns * B + f] = logdet(15, P);
+            ++ns;
+            prev = st;
+        }
+        if (n_sel) n_sel[f] = ns;
+    }
+}

@@ -28,6 +28,8 @@ def lib():
         L.cpu_cv_run.restype = None
         L.cpu_ref15_events.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32]
         L.cpu_ref15_events.restype = None
+        L.cpu_ref15_sched.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32]
+        L.cpu_ref15_sched.restype = None
         _lib = L
     return _lib
 
@@ -80,3 +82,19 @@ def ref15_events(etype, dt, payload, x0, P0, filters=None, nthreads=None, record
     lib().cpu_ref15_events(B, T, _p(etype), _p(dt), _p(payload), _p(x0), _p(P0), _p(traj), _p(ld), f0, f1,
                            nthreads or threads())
     return traj, ld
+
+
+def ref15_sched(t, etype, payload, prev0, freq, P0, x0=None, filters=None, nthreads=None):
+    """The greedy scheduled driver (kf_workers.py:826-957, warm start): t [T, B], etype [T, B] u8,
+    payload [T, 9, B], prev0 [B], freq [B], P0 15x15, x0 [6, B] or None (zeros).  Returns
+    (sel_time [T, B], traj [T, 6, B], logdet [T, B], n_sel [B]); rows j >= n_sel[f] stay zero."""
+    t, etype, payload = _c(t), _c(etype, np.uint8), _c(payload)
+    prev0, freq, P0 = _c(prev0), _c(freq), _c(P0)
+    x0 = None if x0 is None else _c(x0)
+    T, B = etype.shape
+    f0, f1 = filters or (0, B)
+    st, traj, ld = np.zeros((T, B)), np.zeros((T, 6, B)), np.zeros((T, B))
+    ns = np.zeros(B, np.int32)
+    lib().cpu_ref15_sched(B, T, _p(t), _p(etype), _p(payload), _p(prev0), _p(freq), _p(x0), _p(P0), _p(st),
+                          _p(traj), _p(ld), _p(ns), f0, f1, nthreads or threads())
+    return st, traj, ld, ns

@@ -63,6 +63,10 @@ struct kf_batch {
     double gps_r0, imu_r0;   // R_gps[0], R_imu[0]: which sensor the greedy scheduler picks
     void* sched_ws;          // kf_run_scheduled's two passes: picks [T][B] u32, flags [B] (grown on demand)
     size_t sched_ws_bytes;
+    // a graph capture baked the address of this workspace in: its replays write it, so it is
+    // never freed before kf_free (a larger one replaces it and it moves to `retired`)
+    bool search_ws_graph, stream_ws_graph, sched_ws_graph;
+    std::vector<void*> retired;
 };
 
 namespace {
@@ -118,6 +122,30 @@ const uint64_t* binom_table() {
 }
 
 bool capturing(hipStream_t st);
+
+// Grow a per-handle device workspace to at least `need` bytes (the grown-on-demand buffers
+// search_ws / stream_ws / sched_ws).  Growing allocates, and hipFree synchronises the device, so
+// it happens only on the first call of a kind and on a call that needs more than any before it
+// (kf.h: "Workspaces").  A buffer that a graph capture used stays alive until kf_free, since the
+// graph's replays still write it; inside a capture nothing is allocated (returns false).
+bool grow_ws(kf_batch* h, void** buf, size_t* bytes, bool* graph, size_t need, hipStream_t st) {
+    if (*bytes >= need) return true;
+    if (capturing(st)) return false;
+    if (*buf) {
+        if (*graph) h->retired.push_back(*buf);
+        else (void)hipFree(*buf);
+    }
+    *buf = nullptr;
+    *bytes = 0;
+    *graph = false;
+    if (hipMalloc(buf, need) != hipSuccess) {
+        (void)hipGetLastError();
+        *buf = nullptr;
+        return false;
+    }
+    *bytes = need;
+    return true;
+}
 
 // Upload the combination search's inputs (events, root state) to the handle's workspace (the
 // binomials went there at kf_alloc).  Inputs equal, bit for bit, to the last upload are already
@@ -520,6 +548,7 @@ int kf_free(kf_batch* h) {
     if (h->pend_done) (void)hipEventDestroy(h->pend_done);
     if (h->kc) (void)hipFree(h->kc);
     if (h->sched_ws) (void)hipFree(h->sched_ws);
+    for (void* p : h->retired) (void)hipFree(p);
     delete h;
     return KF_OK;
 }
@@ -867,16 +896,12 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     const size_t need = 256 + 2 * bank1 + bank4 + 2 * align256(sizeof(double) * 12 * nch * C) +
                         align256(sizeof(double) * 15 * nch * ntiles) + align256(sizeof(double) * n * C) + lft_bytes +
                         rec_bytes;
-    if (h->stream_ws_bytes < need) {
-        if (h->stream_ws) (void)hipFree(h->stream_ws);
-        h->stream_ws = nullptr;
-        h->stream_ws_bytes = 0;
-        if (hipMalloc(&h->stream_ws, need) != hipSuccess) {
-            (void)hipGetLastError();
-            return fail(KF_EHIP, "kf_run_stream: cannot allocate %zu bytes of chunk banks", need);
-        }
-        h->stream_ws_bytes = need;
-    }
+    if (!grow_ws(h, &h->stream_ws, &h->stream_ws_bytes, &h->stream_ws_graph, need, static_cast<hipStream_t>(stream)))
+        return capturing(static_cast<hipStream_t>(stream))
+                   ? fail(KF_EINVAL, "kf_run_stream: the chunk banks (%zu bytes) must be sized by an eager call "
+                                     "before a graph capture", need)
+                   : fail(KF_EHIP, "kf_run_stream: cannot allocate %zu bytes of chunk banks", need);
+    if (capturing(static_cast<hipStream_t>(stream))) h->stream_ws_graph = true;
     char* p = static_cast<char*>(h->stream_ws);
     kfmi::StreamArgs sa{};
     sa.C = C;
@@ -1098,17 +1123,12 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
     const size_t head = 4096;  // best[65], n_acc[65]
     const size_t level = widest ? static_cast<size_t>(kfmi::search_level_bytes(widest, esz)) : 0;
     const size_t need = head + 2 * level;
-    if (h->search_ws_bytes < need) {
-        if (h->search_ws) (void)hipFree(h->search_ws);
-        h->search_ws = nullptr;
-        h->search_ws_bytes = 0;
-        if (hipMalloc(&h->search_ws, need) != hipSuccess) {
-            (void)hipGetLastError();
-            return fail(KF_ENOMEM, "kf_search_combos: hipMalloc of %zu bytes of level buffers failed", need);
-        }
-        h->search_ws_bytes = need;
-    }
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (!grow_ws(h, &h->search_ws, &h->search_ws_bytes, &h->search_ws_graph, need, st))
+        return capturing(st) ? fail(KF_EINVAL, "kf_search_combos: the level buffers (%zu bytes) must be sized by an "
+                                               "eager call before a graph capture", need)
+                             : fail(KF_ENOMEM, "kf_search_combos: hipMalloc of %zu bytes of level buffers failed", need);
+    if (capturing(st)) h->search_ws_graph = true;
     if (int rc = upload_combo_inputs(h, n_events, events, init, st, "kf_search_combos: upload")) return rc;
     char* ws = static_cast<char*>(h->ws);
     char* sw = static_cast<char*>(h->search_ws);
@@ -1283,7 +1303,7 @@ int run_scheduled(const char* fn, kf_batch* h, int T, const double* t, const uin
         const size_t flags_b = align256(sizeof(int32_t) * size_t(h->B));
         const int nw = h->B % 64 == 0 && opt(h, KF_OPT_SCHED_ORDER) == 0 ? int(h->B / 64) : 0;
         size_t sort_b = 0;
-        if (nw && kfmi::sort_pairs_desc_u32(nullptr, &sort_b, nullptr, nullptr, nullptr, nullptr, nw, 31, nullptr) !=
+        if (nw && kfmi::sort_pairs_desc_u32(nullptr, &sort_b, nullptr, nullptr, nullptr, nullptr, nw, 32, nullptr) !=
                       hipSuccess) {
             (void)hipGetLastError();
             sort_b = 0;
@@ -1291,15 +1311,9 @@ int run_scheduled(const char* fn, kf_batch* h, int T, const double* t, const uin
         const size_t wave_b = nw && sort_b ? 4 * align256(sizeof(uint32_t) * size_t(nw)) + align256(sort_b) : 0;
         const size_t need = picks_b + flags_b + wave_b;
         // no allocation inside a graph capture (hipMalloc / hipFree are not capturable): a
-        // workspace too small for this T leaves the fused kernel to run
-        if (h->sched_ws_bytes < need && !capturing(static_cast<hipStream_t>(stream))) {
-            if (h->sched_ws) (void)hipFree(h->sched_ws);
-            h->sched_ws = nullptr;
-            h->sched_ws_bytes = 0;
-            if (hipMalloc(&h->sched_ws, need) == hipSuccess) h->sched_ws_bytes = need;
-            else (void)hipGetLastError();  // no workspace: the fused kernel runs
-        }
-        if (h->sched_ws && h->sched_ws_bytes >= need) {
+        // workspace too small for this T (or none at all) leaves the fused kernel to run
+        if (grow_ws(h, &h->sched_ws, &h->sched_ws_bytes, &h->sched_ws_graph, need, static_cast<hipStream_t>(stream))) {
+            if (capturing(static_cast<hipStream_t>(stream))) h->sched_ws_graph = true;
             char* w = static_cast<char*>(h->sched_ws);
             a.picks = reinterpret_cast<uint32_t*>(w);
             a.flags = reinterpret_cast<int32_t*>(w + picks_b);

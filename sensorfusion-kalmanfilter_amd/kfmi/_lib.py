@@ -136,12 +136,18 @@ def header_functions(path=HEADER):
 
 def source_hash():
     """SHA-256 (16 hex) of the sources in this tree that libkfmi.so is built from, in the
-    Makefile's order (HASHED): csrc/*.cpp, *.h, *.hip sorted by name, then include/kf.h."""
+    Makefile's order (HASHED): csrc/*.cpp, *.h, *.hip sorted by name, then include/kf.h.  None
+    when the sources are not here (an installed package): the library's origin is then unknown."""
     files = sorted(p for ext in ('cpp', 'h', 'hip') for p in glob.glob(os.path.join(CSRC, '*.' + ext)))
+    if not files or not os.path.exists(HEADER):
+        return None
     h = hashlib.sha256()
-    for p in files + [HEADER]:
-        with open(p, 'rb') as f:
-            h.update(f.read())
+    try:
+        for p in files + [HEADER]:
+            with open(p, 'rb') as f:
+                h.update(f.read())
+    except OSError:
+        return None
     return h.hexdigest()[:16]
 
 
@@ -167,11 +173,15 @@ def lib():
         fn = getattr(handle, name)
         fn.restype = res
         fn.argtypes = args
-    built, tree = library_hash(handle), source_hash()
-    if built != tree and os.environ.get('KFMI_ALLOW_FOREIGN_LIB') != '1':
-        raise KFError(KF_ENODEV, f'{LIB_PATH} was built from sources {built}, this tree is {tree}: rebuild '
-                                 f'(make -C sensorfusion-kalmanfilter_amd); KFMI_ALLOW_FOREIGN_LIB=1 loads it '
-                                 f'anyway (A/B of another revision only)')
+    if os.environ.get('KFMI_ALLOW_FOREIGN_LIB') != '1':
+        built, tree = library_hash(handle), source_hash()
+        if tree is None:
+            raise KFError(KF_ENODEV, f'{LIB_PATH}: the sources it must match (csrc/, include/kf.h) are not in '
+                                     f'this tree; KFMI_ALLOW_FOREIGN_LIB=1 loads it unchecked')
+        if built != tree:
+            raise KFError(KF_ENODEV, f'{LIB_PATH} was built from sources {built}, this tree is {tree}: rebuild '
+                                     f'(make -C sensorfusion-kalmanfilter_amd); KFMI_ALLOW_FOREIGN_LIB=1 loads it '
+                                     f'anyway (A/B of another revision only)')
     _lib = handle
     return _lib
 

@@ -57,3 +57,26 @@ def test_bench_world_mismatch_exits_nonzero():
     p = _run(['--gpus', '2', '--launch-check'], {'WORLD_SIZE': '1', 'RANK': '0', 'LOCAL_RANK': '0'})
     assert p.returncode != 0
     assert 'WORLD_SIZE=1' in p.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('config', ['3', 'ref15'])
+def test_bench_two_ranks_on_the_gpu(config):
+    """`python bench.py --gpus 2` end to end on the GPU box, started as a fresh child process:
+    two ranks (gloo: they share the box's one GPU; the 8-GPU node's run is RCCL), each owning
+    its shard of filters, max-over-ranks timing, and the final all-gather of the final states,
+    last log-dets and the decimated trajectory, which every rank checks bitwise against its own
+    shard (bench.py's N > 1 path; replaces the reference's Pool(30) fan-out,
+    kf_workers.py:1320-1346)."""
+    cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--dist-backend', 'gloo', '--config', config,
+           '--batch', '65536', '--steps', '2', '--warmup', '1', '--no-cpu-baseline']
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec['n_gpus'] == rec['ranks_seen'] == 2
+    assert rec['failed_filters'] == 0 and rec['value'] > 0
+    ag = rec['allgather']
+    assert ag['checked'].startswith('bitwise') and ag['traj_steps'] > 0
+    assert ag['bytes_gathered'] == 2 * ag['bytes_per_rank'] > 0

@@ -126,3 +126,19 @@ def test_library_does_not_read_the_environment():
     import glob
     for p in glob.glob(os.path.join(os.path.dirname(_lib.HEADER), '..', 'sensorfusion-kalmanfilter_amd', 'csrc', '*')):
         assert 'getenv' not in open(p).read(), p
+
+
+def test_loader_without_sources_raises_kferror(monkeypatch, tmp_path):
+    """Loaded from a tree without its sources (an installed package), the hash gate reports the
+    origin unknown as KFError, not a raw FileNotFoundError; KFMI_ALLOW_FOREIGN_LIB=1 skips it
+    before any source file is read."""
+    monkeypatch.setattr(_lib, 'CSRC', str(tmp_path / 'no_csrc'))
+    monkeypatch.setattr(_lib, 'HEADER', str(tmp_path / 'no_kf.h'))
+    monkeypatch.setattr(_lib, '_lib', None)
+    assert _lib.source_hash() is None
+    monkeypatch.delenv('KFMI_ALLOW_FOREIGN_LIB', raising=False)
+    with pytest.raises(_lib.KFError):
+        _lib.lib()
+    monkeypatch.setattr(_lib, '_lib', None)
+    monkeypatch.setenv('KFMI_ALLOW_FOREIGN_LIB', '1')
+    assert _lib.lib() is not None

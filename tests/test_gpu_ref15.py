@@ -683,6 +683,50 @@ def test_scheduled_replays_as_a_hip_graph(warm):
             np.testing.assert_allclose(got[1][:n, f], eager[1][:n, f], rtol=1e-12, atol=1e-12)
 
 
+def test_scheduled_graph_survives_a_larger_eager_call():
+    """A captured kf_run_scheduled keeps its workspace: an eager call with a longer stream on the
+    same handle grows the workspace without freeing the one the graph writes, and a
+    replay after it still gives the first call's outputs bitwise."""
+    rng = np.random.default_rng(43)
+    B, T = 128, 80
+    t0, rates, etype, tt, pay = _sched_streams(rng, B, 3 * T)
+    dev = torch.device('cuda', 0)
+    ttd, etd, payd = (torch.as_tensor(v, device=dev) for v in (tt, etype, pay))
+    prev, frd = torch.full((B,), t0, dtype=torch.float64, device=dev), torch.as_tensor(rates, device=dev)
+    x0 = torch.zeros(15, B, dtype=torch.float64, device=dev)
+    P0b = torch.as_tensor(np.repeat(ref15.to_blocks(ref_kf.P0_REF15)[:, None], B, axis=1), device=dev)
+    outs = (torch.empty(T, 6, B, dtype=torch.float64, device=dev), torch.empty(T, B, dtype=torch.float64, device=dev),
+            torch.empty(T, B, dtype=torch.float64, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+
+    def run(kf, n):
+        kf.set_state(x0, P0b)
+        res = kf.run_scheduled(ttd[:n], etd[:n], payd[:n], prev, frd)
+        if n == T:
+            for o, r in zip(outs, res):
+                o.copy_(r)
+
+    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    run(kf, T)
+    torch.cuda.synchronize()
+    eager = [o.cpu().numpy().copy() for o in outs]
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        run(kf, T)
+    run(kf, 3 * T)           # grows the workspace: the captured one must stay alive
+    torch.cuda.synchronize()
+    for o in outs:
+        o.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    got = [o.cpu().numpy() for o in outs]
+    kf.close()
+    np.testing.assert_array_equal(got[3], eager[3])
+    live = np.arange(T)[:, None] < eager[3][None, :]
+    for a, b in zip(got[:3], eager[:3]):
+        m = live[:, None, :] if a.ndim == 3 else live
+        np.testing.assert_array_equal(np.where(m, a, 0.0), np.where(m, b, 0.0))
+
+
 def test_score_candidates_random_batch():
     """kf_score_candidates over a batch of random block-diagonal covariances vs the oracle's
     Scheduler.cov_matrix trace (first row and full)."""
@@ -769,96 +813,5 @@ def test_search_full_size_sampled_vs_per_subset():
         assert np.max(np.abs(got - mx) / np.maximum(np.abs(mx), 1.0)) <= 1e-12, k
 
 
-def test_ref15_bench_size_sampled():
-    """The ref15 bench workload at its full size (2^20 filters x 256 events, GPS every 20th,
-    the LDS-staged kernel), 48 filters spread over the batch against the oracle's step15 loop."""
-    import bench
-    dev = torch.device('cuda', 0)
-    cfg = dict(bench.CONFIGS['ref15'])
-    B, T, k, dt = cfg['B'], cfg['T'], cfg['k'], cfg['dt']
-    g = torch.Generator(device=dev).manual_seed(7)
-    etype = torch.ones(T, B, dtype=torch.uint8, device=dev)
-    etype[k - 1::k] = 0
-    dts = torch.full((T, B), dt, dtype=torch.float64, device=dev)
-    pay = torch.randn(T, 9, B, dtype=torch.float64, device=dev, generator=g)
-    pay[:, 0:3] *= 0.05
-    pay[:, 3:6] *= 0.01
-    pay[:, 6:9] *= 0.3
-    pay[:, 0:3] = torch.where((etype == 0)[:, None, :], pay[:, 0:3] * 60.0, pay[:, 0:3])
-    kf = kfmi.BatchedKF('ref15', B, 'f64')
-    tr, ld, _, _ = kf.run_events(etype, dts, pay)
-    idx = torch.linspace(0, B - 1, 48).long().to(dev)
-    tr = tr[:, :, idx].cpu().numpy()
-    ld = ld[:, idx].cpu().numpy()
-    et, pa = etype[:, idx].cpu().numpy(), pay[:, :, idx].cpu().numpy()
-    assert int((kf.status() != 0).sum()) == 0
-    kf.close()
-    worst = 0.0
-    for j in range(idx.numel()):
-        x, P = np.zeros(15), ref_kf.P0_REF15.copy()
-        for t in range(T):
-            if et[t, j] == 0:
-                sd = {'easting': pa[t, 0, j], 'northing': pa[t, 1, j], 'altitude': pa[t, 2, j]}
-                x, P = ref_kf.step15(x, P, 'GPS', sd, dt)
-            else:
-                x, P = ref_kf.step15(x, P, 'IMU', ['t', *pa[t, :, j]], dt)
-            lr = np.linalg.slogdet(P)[1]
-            worst = max(worst, float(np.max(np.abs(tr[t, :, j] - x[:6]) / np.maximum(np.abs(x[:6]), 1.0))),
-                        abs(ld[t, j] - lr) / max(1.0, abs(lr)))
-    assert worst <= TOL, worst
-
-
-def test_sched_bench_size_sampled():
-    """The sched bench workload at its full size (2^20 filters x 256 events, 64 filters per rate,
-    the two passes), 24 filters spread over the batch against the oracle's greedy driver; the
-    bench's payload records give every output bitwise."""
-    dev = torch.device('cuda', 0)
-    B, T, k = 1 << 20, 256, 20
-    rates_all = (10, 20, 30, 40, 50, 60, 70, 80, 90, 100, 110, 120)
-    g = torch.Generator(device=dev).manual_seed(9)
-    t0 = 1697739278.761565
-    etype = torch.ones(T, B, dtype=torch.uint8, device=dev)
-    etype[k - 1::k] = 0
-    tt = (t0 + 0.005 * torch.arange(1, T + 1, dtype=torch.float64, device=dev)[:, None]
-          + 5e-4 * (torch.rand(T, B, dtype=torch.float64, device=dev, generator=g) - 0.5))
-    pay = torch.randn(T, 9, B, dtype=torch.float64, device=dev, generator=g)
-    pay[:, 0:3] *= 0.05
-    pay[:, 6:9] *= 0.3
-    pay[:, 0:3] = torch.where((etype == 0)[:, None, :], pay[:, 0:3] * 60.0, pay[:, 0:3])
-    rates = torch.tensor(rates_all, dtype=torch.float64, device=dev)
-    freq = rates[(torch.arange(B, device=dev) // 64) % len(rates_all)].contiguous()
-    kf = kfmi.BatchedKF('ref15', B, 'f64')
-    prev = torch.full((B,), t0, dtype=torch.float64, device=dev)
-    # the bench's layout: 12-double records (kf_run_scheduled_rec), every output bitwise the rows'
-    recs = torch.zeros(T, B, 12, dtype=torch.float64, device=dev)
-    recs[:, :, :9] = pay.transpose(1, 2)
-    rec_out = kf.run_scheduled(tt, etype, recs, prev, freq, records=True)
-    del recs
-    kf.close()
-    kf = kfmi.BatchedKF('ref15', B, 'f64')
-    tr, ld, stt, ns = kf.run_scheduled(tt, etype, pay, prev, freq)
-    assert torch.equal(ns, rec_out[3])
-    live = torch.arange(T, device=dev)[:, None] < ns[None, :].long()  # rows past n_sel are not written
-    for a, b in zip((tr, ld, stt), rec_out[:3]):
-        m = live[:, None, :] if a.dim() == 3 else live
-        assert torch.equal(torch.where(m, a, 0.0), torch.where(m, b, 0.0))
-    del rec_out
-    idx = torch.linspace(0, B - 1, 24).long().to(dev)
-    tr, ld, stt, ns = (v[..., idx].cpu().numpy() for v in (tr, ld, stt, ns))
-    et, ts, pa, fr = (v[..., idx].cpu().numpy() for v in (etype, tt, pay, freq))
-    kf.close()
-    for j in range(idx.numel()):
-        ev = [(0, 'GPS', t0, {'easting': 0.0, 'northing': 0.0, 'altitude': 0.0})]  # skipped (warm start)
-        for i in range(T):
-            if et[i, j] == 0:
-                ev.append((i + 1, 'GPS', ts[i, j], {'easting': pa[i, 0, j], 'northing': pa[i, 1, j],
-                                                    'altitude': pa[i, 2, j]}))
-            else:
-                ev.append((i + 1, 'IMU', ts[i, j], ['t', *pa[i, :, j]]))
-        rs, rl, _ = ref_kf.run_kalman_filter_scheduled(ev, 0, len(ev), ref_kf.P0_REF15.copy(),
-                                                       (t0, 0, 0, 0, 0, 0, 0), 'greedy', float(fr[j]))
-        n = int(ns[j])
-        assert n == len(rs) - 1, j
-        assert _rel(stt[:n, j], [r[0] for r in rs[1:]]) <= 1e-12, j
-        assert _rel(tr[:n, :, j], np.array([r[1:7] for r in rs[1:]])) <= TOL, j
-        assert _rel(ld[:n, j], rl[1:]) <= TOL, j
+# The ref15 / ref15f32 / sched rows at their bench sizes against the oracle (>= 4096 filters plus
+# the wave and batch edges): tests/test_gpu_bench_parity.py

@@ -315,3 +315,74 @@ def test_numpy_pool_runs_the_reference_loop_on_all_workers():
     out = numpy_pool.run('sched', sched, seconds=30.0)
     assert out['filters'] == 2 * nf and out['units'] == 2 * nf * T
     assert 0 < out['seconds'] < 30 and out['value'] > 0
+
+
+def _events_to_columns(events):
+    """Event tuples -> one filter's columns: t [T, 1], etype [T, 1], payload [T, 9, 1]."""
+    T = len(events)
+    t, et, pay = np.zeros((T, 1)), np.zeros((T, 1), np.uint8), np.zeros((T, 9, 1))
+    for i, (_, s, ti, sd) in enumerate(events):
+        t[i, 0] = ti
+        if s == 'GPS':
+            pay[i, 0:3, 0] = sd['easting'], sd['northing'], sd['altitude']
+        else:
+            et[i, 0] = 1
+            pay[i, :, 0] = sd[1:]
+    return t, et, pay
+
+
+@pytest.mark.parametrize('f', [20, 50, 120])
+def test_c_ref15_sched_vs_goldens(golden_dir, cpu_kf, f):
+    """oracle/cpu_kf.c's greedy scheduled driver reproduces the reference's own
+    run_kalman_filter_scheduled outputs (ref15_scheduled.npz): the cold start as a warm start
+    from the first fix (kf_workers.py:866-880), and the reference's warm-start window."""
+    g = _load(golden_dir, 'ref15_scheduled.npz')
+    events = unpack_events(g)
+    first = next(i for i, e in enumerate(events) if e[1] == 'GPS')
+    sd = events[first][3]
+    x0 = np.array([[sd['easting']], [sd['northing']], [sd['altitude']], [0.0], [0.0], [0.0]])
+    t, et, pay = _events_to_columns(events[first + 1:])
+    st, tr, ld, ns = cpu_kf.ref15_sched(t, et, pay, [events[first][2]], [float(f)], ref_kf.P0_REF15, x0=x0)
+    want = g[f'greedy{f}_states']
+    n = int(ns[0])
+    assert n == len(want) - 1
+    assert _rel(st[:n, 0], want[1:, 0]) == 0.0
+    assert _rel(tr[:n, :, 0], want[1:, 1:7]) < 1e-10
+    assert _rel(ld[:n, 0], g[f'greedy{f}_logdets'][1:]) < 1e-10
+    if f == 120:
+        s0 = tuple(g['warm_init_state'])
+        t, et, pay = _events_to_columns(events[61:180])
+        st, tr, ld, ns = cpu_kf.ref15_sched(t, et, pay, [s0[0]], [100.0], g['warm_init_P'],
+                                            x0=np.array(s0[1:7])[:, None])
+        want = g['warm_states']
+        n = int(ns[0])
+        assert n == len(want) - 1
+        assert _rel(tr[:n, :, 0], want[1:, 1:7]) < 1e-10
+        assert _rel(ld[:n, 0], g['warm_logdets'][1:]) < 1e-10
+
+
+def test_c_ref15_sched_vs_numpy_oracle(cpu_kf):
+    """Random jittered streams, per-filter rates (window edges, empty-queue triggers, fixes and
+    IMU samples queued together): every pick, time, state and log-det of the C driver equals
+    the NumPy restatement's (oracle/ref_kf.run_kalman_filter_scheduled, greedy)."""
+    rng = np.random.default_rng(11)
+    B, T, t0 = 12, 120, 1697739278.761565
+    et = (rng.random((T, B)) > 0.12).astype(np.uint8)
+    t = t0 + np.cumsum(rng.uniform(0.001, 0.02, (T, B)), axis=0)
+    pay = rng.normal(0, 1, (T, 9, B)) * np.array([20, 20, 20, .05, .05, .05, .5, .5, .5])[None, :, None]
+    freq = rng.choice([5.0, 20.0, 50.0, 120.0, 400.0], B)
+    x0 = rng.normal(0, 3, (6, B))
+    st, tr, ld, ns = cpu_kf.ref15_sched(t, et, pay, np.full(B, t0), freq, ref_kf.P0_REF15, x0=x0, nthreads=2)
+    for f in range(B):
+        ev = [(0, 'GPS', t0, {'easting': 0.0, 'northing': 0.0, 'altitude': 0.0})]
+        for i in range(T):
+            ev.append((i + 1, 'GPS', t[i, f], {'easting': pay[i, 0, f], 'northing': pay[i, 1, f],
+                                                'altitude': pay[i, 2, f]}) if et[i, f] == 0
+                      else (i + 1, 'IMU', t[i, f], ['t', *pay[i, :, f]]))
+        rs, rl, _ = ref_kf.run_kalman_filter_scheduled(ev, 0, len(ev), ref_kf.P0_REF15.copy(),
+                                                       (t0, *x0[:, f]), 'greedy', float(freq[f]))
+        n = int(ns[f])
+        assert n == len(rs) - 1 and n > 3, f
+        assert _rel(st[:n, f], [r[0] for r in rs[1:]]) == 0.0
+        assert _rel(tr[:n, :, f], np.array([r[1:7] for r in rs[1:]])) < 1e-10
+        assert _rel(ld[:n, f], rl[1:]) < 1e-10
