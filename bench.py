@@ -16,7 +16,9 @@ start, like the reference's windowed runs, kf_workers.py:2316-2323) over the sam
 Configs (BASELINE.json / SURVEY.md §8d); per GPU (weak scaling: each rank owns B filters):
     1  the reference's own case: ONE filter over a whole drive log — 15-state model,
        run_kalman_filter_full over ~638k merged GPS+IMU events (synthetic log with the shape of
-       gps_data.csv + the 200 Hz IMU log: CSV -> kf_ingest -> kf_events_dt + kf_run_events)
+       gps_data.csv + the 200 Hz IMU log: CSV -> kf_ingest -> kf_events_dt + kf_run_stream)
+    1ref8  the same log through hw5_2's 8-state filter (hw5_2.py:313-380; the small-state model
+       BASELINE config 1 names), one filter
     2  cv2 (4-state/2-meas)  fp32  B=65,536     T=1024 dt=0.1  update every step
     3  cv3 (6-state/3-meas)  fp64  B=1,048,576  T=256  dt=0.1  update every step   [default]
     4  cv3 (6-state/3-meas)  fp32  B=1,048,576  T=256  dt=0.1  update every step   (x8 GPUs)
@@ -56,6 +58,10 @@ CONFIGS = {
               parallel=True),
     '1seq': dict(model='ref15', dtype='f64', B=1, n_gps=30758, n_gps_nan_lead=2735, n_gps_nan=8887, n_imu=616322,
                  parallel=False),
+    # the same log through hw5_2's 8-state planar filter (hw5_2.py:313-380), the model the BASELINE
+    # 4-state config restricts: x0 = 0, the first fix at dt = 0, no dt < 0 guard, 2-D fixes
+    '1ref8': dict(model='ref8', dtype='f64', B=1, n_gps=30758, n_gps_nan_lead=2735, n_gps_nan=8887, n_imu=616322,
+                  parallel=True),
     '2': dict(model='cv2', dtype='f32', B=65536, T=1024, dt=0.1, k=1),
     '3': dict(model='cv3', dtype='f64', B=1048576, T=256, dt=0.1, k=1),
     '4': dict(model='cv3', dtype='f32', B=1048576, T=256, dt=0.1, k=1),
@@ -587,25 +593,30 @@ def synth_log(cfg, root, seed=SEED):
 
 
 def log_workload(cfg, args, rank, world, dev):
-    """BASELINE config 1: run_kalman_filter_full (kf_workers.py:623-728) over a whole drive log
-    with ONE filter — the reference's own use.  Ingest runs once, outside the timed region
-    (reported separately); a step is the device dt pass + one kf_run_events over every event."""
+    """BASELINE config 1: ONE filter over a whole drive log — the reference's own use.  With
+    model ref15 it is run_kalman_filter_full (kf_workers.py:623-728: x0 = the first fix, which is
+    processed again at dt = 0, dt < 0 events skipped); with ref8 (--config 1ref8) hw5_2's
+    run_kalman_filter (hw5_2.py:313-380: x0 = 0, fixes without altitude, no dt < 0 guard).
+    Ingest runs once, outside the timed region (reported separately); a step is the device dt
+    pass + one kf_run_stream (or kf_run_events_seq) over every event."""
     import tempfile
     import kfmi
     from kfmi import _lib, ingest
     from kfmi.engine import _ptr
+    ref8 = cfg['model'] == 'ref8'
+    n_state, width = (8, 3) if ref8 else (15, 6)
     root = tempfile.mkdtemp(prefix='kfmi_log_')
     gp, ip = synth_log(cfg, root)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     gcols, icols = ingest.read_csv(gp, 4), ingest.read_csv(ip, 11)
     t1 = time.perf_counter()
-    stream = ingest.ingest_arrays(gcols, icols, device=dev.index)
+    stream = ingest.ingest_arrays(gcols, icols, with_altitude=not ref8, device=dev.index)
     torch.cuda.synchronize(dev)
     t2 = time.perf_counter()
     # the first call also loads the library's code objects and warms torch's allocator: the
     # ingest itself is the second call's time (both reported)
-    stream = ingest.ingest_arrays(gcols, icols, device=dev.index)
+    stream = ingest.ingest_arrays(gcols, icols, with_altitude=not ref8, device=dev.index)
     torch.cuda.synchronize(dev)
     t3 = time.perf_counter()
     N = len(stream)
@@ -614,12 +625,14 @@ def log_workload(cfg, args, rank, world, dev):
     t_ev = stream.t[first:].contiguous()
     e_ev = stream.etype[first:].contiguous()
     pay = stream.payload[first:].contiguous()
-    x0 = torch.zeros(15, 1, dtype=torch.float64, device=dev)
-    x0[0:3, 0] = pay[0, 0:3]
-    kf = kfmi.BatchedKF('ref15', 1, 'f64', device=dev.index, options=cfg.get('opts'))
+    x0 = torch.zeros(n_state, 1, dtype=torch.float64, device=dev)
+    if not ref8:
+        x0[0:3, 0] = pay[0, 0:3]      # kf_workers.py:655-659 (hw5_2 starts from 0, hw5_2.py:316)
+    rule = _lib.KF_DT_RAW if ref8 else _lib.KF_DT_FULL
+    kf = kfmi.BatchedKF(cfg['model'], 1, 'f64', device=dev.index, options=cfg.get('opts'))
     dt = torch.empty(T, dtype=torch.float64, device=dev)
     et = torch.empty(T, dtype=torch.uint8, device=dev)
-    traj = kf.empty(T, 6, 1)
+    traj = kf.empty(T, width, 1)
     logdet = kf.empty(T, 1)
     prev0 = float(t_ev[0])
 
@@ -629,8 +642,7 @@ def log_workload(cfg, args, rank, world, dev):
     def launches():
         L = _lib.lib()  # looked up per step: tools/ab_inproc.py swaps libraries between launches
         kf.reset(x0)
-        _lib.check(L.kf_events_dt(T, _ptr(t_ev), _ptr(e_ev), prev0, _lib.KF_DT_FULL, _ptr(dt), _ptr(et),
-                                  kf._stream()))
+        _lib.check(L.kf_events_dt(T, _ptr(t_ev), _ptr(e_ev), prev0, rule, _ptr(dt), _ptr(et), kf._stream()))
         if cfg['parallel']:
             # time-parallel (kf_run_stream): chunks of the log as filters, checked on the device
             _lib.check(L.kf_run_stream(kf.handle, T, _ptr(et), _ptr(dt), _ptr(pay), _ptr(traj), None, _ptr(logdet),
@@ -660,67 +672,72 @@ def log_workload(cfg, args, rank, world, dev):
 
     def cpu():
         """One filter cannot use more than one core: the reference's dense event step restated in
-        C (oracle/cpu_kf.c) over the whole log from the first fix (run_kalman_filter_full's dt
-        rule applied on the host), 1 thread; plus the NumPy reference loop
-        (oracle/ref_kf.run_kalman_filter_full) over the first events, 1 core, ~3 s."""
+        C (oracle/cpu_kf.c) over the whole log from the first fix (the driver's dt rule applied
+        on the host), 1 thread; plus the NumPy reference loop (oracle/ref_kf.
+        run_kalman_filter_full / run_kalman_filter_8state) over the first events, 1 core, ~3 s."""
         from oracle import cpu_kf, ref_kf
         from kfmi.kf_workers import EventList
         h = stream.host()
         t_h, e_h, p_h = h['t'][first:], h['etype'][first:].copy(), h['payload'][first:]
         prev = np.r_[t_h[0], t_h[:-1]]
         d_h = t_h - prev
-        e_h[d_h < 0] = 255                                    # kf_workers.py:683-685
-        x0h = np.zeros((15, 1))
-        x0h[0:3, 0] = p_h[0, 0:3]
+        if not ref8:
+            e_h[d_h < 0] = 255                                # kf_workers.py:683-685
+        x0h = x0.cpu().numpy()
         n_c = min(T, 1 << 20)
+        port = cpu_kf.ref8_events if ref8 else cpu_kf.ref15_events
         ts = time.perf_counter()
-        cpu_kf.ref15_events(e_h[:n_c, None], d_h[:n_c, None], p_h[:n_c, :, None], x0h, ref_kf.P0_REF15,
-                            nthreads=1)
+        port(e_h[:n_c, None], d_h[:n_c, None], p_h[:n_c, :, None], x0h, ref_kf.P0_REF8 if ref8 else ref_kf.P0_REF15,
+             nthreads=1)
         el = time.perf_counter() - ts
         ev = EventList(stream)
         n = 2000
         while True:
             lst = ev[first:first + n]
             t1 = time.perf_counter()
-            st, _, _, _ = ref_kf.run_kalman_filter_full(lst, 0, n)
+            if ref8:
+                st, _ = ref_kf.run_kalman_filter_8state(lst)
+            else:
+                st, _, _, _ = ref_kf.run_kalman_filter_full(lst, 0, n)
             el_np = time.perf_counter() - t1
             if el_np > 3.0 or n >= T:
                 break
             n = min(T, n * 4)
+        driver = 'hw5_2.run_kalman_filter' if ref8 else 'run_kalman_filter_full'
+        np_fn = 'run_kalman_filter_8state' if ref8 else 'run_kalman_filter_full'
         return {'value': n_c / el, 'unit': 'KF events/s', 'cores': 1, 'kind': 'port',
-                'sample': f'run_kalman_filter_full over {n_c} events of this log (from the first fix) through '
-                          f'oracle/cpu_kf.c (the reference step, dense 15x15, C -O3), 1 thread (one filter), '
-                          f'{host_cpu()}', 'seconds': round(el, 2),
+                'sample': f'{driver} over {n_c} events of this log (from the first fix) through '
+                          f'oracle/cpu_kf.c (the reference step, dense {n_state}x{n_state}, C -O3), 1 thread (one '
+                          f'filter), {host_cpu()}', 'seconds': round(el, 2),
                 'numpy_reference_loop': {'value': (len(st) - 1) / el_np, 'cores': 1,
-                                         'sample': f'{len(st) - 1} events, oracle/ref_kf.run_kalman_filter_full, '
+                                         'sample': f'{len(st) - 1} events, oracle/ref_kf.{np_fn}, '
                                                    f'NumPy {np.__version__}'}}
 
-    per_event = 1 + 8 + 8 + 72 + 1 + 8 + 48 + 8   # dt pass (t, etype in; dt, etype out) + filter (in/out)
+    # dt pass (t, etype in; dt, etype out) + filter (etype, dt, payload in; traj, logdet out)
+    per_event = 1 + 8 + 8 + 72 + 1 + 8 + 8 * width + 8
+    model_desc = (f'hw5_2.run_kalman_filter (hw5_2.py:313-380), the 8-state planar model' if ref8 else
+                  'run_kalman_filter_full (kf_workers.py:623-728), the 15-state model')
+    desc = (f'BASELINE config 1: ONE filter, {model_desc}, over a whole drive log, {N} merged events '
+            f'({stream.n_fixes} fixes + {stream.n_imu} IMU at 200 Hz), f64; ')
+    extra = {'events': N, 'events_filtered': T, 'csv_parse_ms': (t1 - t0) * 1e3, 'kf_ingest_ms': (t3 - t2) * 1e3,
+             'kf_ingest_first_call_ms': (t2 - t1) * 1e3, 'filters': 1, 'model': cfg['model']}
     if cfg['parallel']:
         return dict(step=step, units=T, bytes=per_event * T, bytes_per_unit=per_event,
-                    kernel='ref_chain_kernel<f64,M15,stream> (warm-up, map and record passes) + stream_* kernels',
+                    kernel=f'ref_chain_kernel<f64,{"M8" if ref8 else "M15"},stream> (map pass) + stream_* kernels',
                     traffic=None, cpu=cpu, gather=None, kf=kf,
                     roofline_note='latency / issue-bound: the map pass runs its chunk length of events in '
                                   'sequence (one wave per SIMD), the covariance starts walk their windows of maps; '
                                   'the fraction is not the figure of merit',
-                    desc=f'BASELINE config 1: ONE 15-state filter (run_kalman_filter_full, kf_workers.py:623-728) '
-                         f'over a whole drive log, {N} merged events ({stream.n_fixes} fixes + {stream.n_imu} IMU '
-                         f'at 200 Hz), f64; time-parallel (kf_run_stream: chunks of the log as filters, '
-                         f'covariance warm-up + affine state maps composed on the device, checked, sequential '
-                         f"fallback); synthetic log with the reference log's shape",
-                    extra={'events': N, 'events_filtered': T, 'csv_parse_ms': (t1 - t0) * 1e3,
-                           'kf_ingest_ms': (t3 - t2) * 1e3, 'kf_ingest_first_call_ms': (t2 - t1) * 1e3, 'filters': 1,
-                           'stream_check': stream_check,
-                           'launch': 'hipGraph replay of the step' if getattr(args, 'graph', False) else 'eager'})
+                    desc=desc + 'time-parallel (kf_run_stream: chunks of the log as filters, covariance warm-up + '
+                                'affine state maps composed on the device, checked, sequential fallback); synthetic '
+                                "log with the reference log's shape",
+                    extra=dict(extra, stream_check=stream_check,
+                               launch='hipGraph replay of the step' if getattr(args, 'graph', False) else 'eager'))
     return dict(step=step, units=T, bytes=per_event * T, bytes_per_unit=per_event, kernel='ref_chain_kernel',
                 traffic=None, cpu=cpu, gather=None, kf=kf,
                 roofline_note='one filter: one wave whose per-event dependency chain bounds the rate (8 lanes, '
                               'one per axis chain); HBM is idle, so the fraction is not the figure of merit',
-                desc=f'BASELINE config 1: ONE 15-state filter (run_kalman_filter_full, kf_workers.py:623-728) over a '
-                     f'whole drive log, {N} merged events ({stream.n_fixes} fixes + {stream.n_imu} IMU at 200 Hz), '
-                     f'f64; synthetic log with the reference log\'s shape',
-                extra={'events': N, 'events_filtered': T, 'csv_parse_ms': (t1 - t0) * 1e3,
-                       'kf_ingest_ms': (t3 - t2) * 1e3, 'kf_ingest_first_call_ms': (t2 - t1) * 1e3, 'filters': 1})
+                desc=desc + "synthetic log with the reference log's shape", extra=extra)
 
 
 def sched_workload(cfg, args, rank, world, dev):
@@ -1037,7 +1054,7 @@ def main():
     for o in args.opt:
         name, _, val = o.partition('=')
         cfg['opts'][name] = int(val) if val.lstrip('-').isdigit() else val
-    if args.config in ('1', '1seq'):
+    if args.config in ('1', '1seq', '1ref8'):
         w = log_workload(cfg, args, rank, world, dev)
     elif args.config in ('ref15', 'ref15f32'):
         w = ref15_workload(cfg, args, rank, world, dev)

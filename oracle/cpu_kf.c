@@ -404,3 +404,67 @@ void cpu_ref15_sched(int64_t B, int T, const double* t, const uint8_t* etype, co
         if (n_sel) n_sel[f] = ns;
     }
 }
+
+/* hw5_2.py's 8-state planar model [x, y, theta, vx, vy, theta_dot, ax, ay] (hw5_2.py:219-304):
+ * F(dt) :219-231, Q(dt) = diag(5, 5, 0.05, 1, 1, 0.1, 2, 2) dt :233-251, a GPS fix updates
+ * (x, y) with R = 3 I2 (:258-264, 280-284, 341-349), an IMU sample the whole state with H = I8,
+ * R = diag(50, 50, 0.05, 10, 10, 0.1, 100, 100) through the pseudo-measurement built from the
+ * predicted state (:352-366). */
+static void F8(double dt, double* F) {
+    memset(F, 0, sizeof(double) * 64);
+    for (int i = 0; i < 8; ++i) F[i * 8 + i] = 1.0;
+    F[0 * 8 + 3] = dt;
+    F[0 * 8 + 6] = 0.5 * dt * dt;
+    F[1 * 8 + 4] = dt;
+    F[1 * 8 + 7] = 0.5 * dt * dt;
+    F[2 * 8 + 5] = dt;
+    F[3 * 8 + 6] = dt;
+    F[4 * 8 + 7] = dt;
+}
+
+/* events as cpu_ref15_events (payload [T][9][B]: GPS e, n, alt; IMU roll, pitch, yaw, wx, wy,
+ * wz, ax, ay, az); x0 [8][B]; P0 8x8; traj [T][3][B] (x, y, theta), logdet [T][B] optional. */
+void cpu_ref8_events(int64_t B, int T, const uint8_t* etype, const double* dt, const double* payload,
+                     const double* x0, const double* P0, double* traj, double* logdet_out, int64_t f0, int64_t f1,
+                     int nthreads) {
+    static const double q8[8] = {5.0, 5.0, 0.05, 1.0, 1.0, 0.1, 2.0, 2.0};
+    static const double r8[8] = {50.0, 50.0, 0.05, 10.0, 10.0, 0.1, 100.0, 100.0};
+    double Hg[2 * 8] = {0}, Rg[4] = {0}, Hi[64] = {0}, Ri[64] = {0};
+    for (int i = 0; i < 2; ++i) {
+        Hg[i * 8 + i] = 1.0;
+        Rg[i * 2 + i] = 3.0;
+    }
+    for (int i = 0; i < 8; ++i) {
+        Hi[i * 8 + i] = 1.0;
+        Ri[i * 8 + i] = r8[i];
+    }
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+    for (int64_t f = f0; f < f1; ++f) {
+        double x[8], P[64], F[64], Q[64];
+        for (int i = 0; i < 8; ++i) x[i] = x0[i * B + f];
+        memcpy(P, P0, sizeof(P));
+        for (int t = 0; t < T; ++t) {
+            const int ty = etype[(int64_t)t * B + f];
+            const double h = dt[(int64_t)t * B + f];
+            const double* p = payload + (int64_t)t * 9 * B + f;
+            if (ty != 255) {
+                F8(h, F);
+                memset(Q, 0, sizeof(Q));
+                for (int i = 0; i < 8; ++i) Q[i * 8 + i] = q8[i] * h;
+                predict(8, F, Q, NULL, x, P);
+                if (ty == 0) {
+                    const double Z[2] = {p[0], p[B]};
+                    update(8, 2, Hg, Rg, Z, x, P);
+                } else if (ty == 1) {
+                    const double ax = p[6 * B], ay = p[7 * B];
+                    const double Vx = x[3] + ax * h, Vy = x[4] + ay * h;
+                    const double Z[8] = {x[0] + Vx * h, x[1] + Vy * h, p[2 * B], Vx, Vy, p[5 * B], ax, ay};
+                    update(8, 8, Hi, Ri, Z, x, P);
+                }
+            }
+            if (traj)
+                for (int i = 0; i < 3; ++i) traj[((int64_t)t * 3 + i) * B + f] = x[i];
+            if (logdet_out) logdet_out[(int64_t)t * B + f] = logdet(8, P);
+        }
+    }
+}

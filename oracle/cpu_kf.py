@@ -30,6 +30,8 @@ def lib():
         L.cpu_ref15_events.restype = None
         L.cpu_ref15_sched.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32]
         L.cpu_ref15_sched.restype = None
+        L.cpu_ref8_events.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32]
+        L.cpu_ref8_events.restype = None
         _lib = L
     return _lib
 
@@ -81,6 +83,19 @@ def ref15_events(etype, dt, payload, x0, P0, filters=None, nthreads=None, record
     ld = np.zeros((T, B)) if records else None
     lib().cpu_ref15_events(B, T, _p(etype), _p(dt), _p(payload), _p(x0), _p(P0), _p(traj), _p(ld), f0, f1,
                            nthreads or threads())
+    return traj, ld
+
+
+def ref8_events(etype, dt, payload, x0, P0, filters=None, nthreads=None, records=True):
+    """hw5_2.py's 8-state model on event streams (cpu_ref8_events): etype [T, B] u8, dt [T, B],
+    payload [T, 9, B], x0 [8, B], P0 8x8.  Returns (traj [T, 3, B] (x, y, theta), logdet [T, B])."""
+    etype, dt, payload, x0, P0 = _c(etype, np.uint8), _c(dt), _c(payload), _c(x0), _c(P0)
+    T, B = etype.shape
+    f0, f1 = filters or (0, B)
+    traj = np.zeros((T, 3, B)) if records else None
+    ld = np.zeros((T, B)) if records else None
+    lib().cpu_ref8_events(B, T, _p(etype), _p(dt), _p(payload), _p(x0), _p(P0), _p(traj), _p(ld), f0, f1,
+                          nthreads or threads())
     return traj, ld
 
 

@@ -141,7 +141,7 @@ def _unrank_lex(n, k, ranks):
 
 def test_bf_full_size_subset_maxima_vs_oracle():
     """The bf row (n = 25 candidates, all 2^25 - 1 subsets, the shared-prefix search, exhaustive):
-    every subset of sizes 1-4 and 23-25 and 4096 spread subsets of every other size, plus each
+    every subset of sizes 1-4 and 21-25 and 4096 spread subsets of every other size, plus each
     size's first and last subset, scored as the oracle's per-subset worker scores them."""
     n = bench.CONFIGS['bf']['n']
     ev, init, Pw, t0, t_end = bench.bf_events(n)
@@ -211,32 +211,39 @@ def test_bf_full_size_winner_vs_oracle():
     kf.close()
 
 
-def test_config1_whole_log_vs_oracle(tmp_path):
+@pytest.mark.parametrize('config', ['1', '1ref8'])
+def test_config1_whole_log_vs_oracle(tmp_path, config):
     """BASELINE config 1 at its full size: the bench's synthetic drive log (30,758 GPS rows,
-    616,322 IMU rows), ingested on the device, dt by kf_events_dt, run_kalman_filter_full as ONE
-    filter through kf_run_stream (the time-parallel route the bench times); against the oracle's
-    own ingest of the same CSVs (oracle/ref_ingest) and the reference's dense step in C on one
+    616,322 IMU rows), ingested on the device, dt by kf_events_dt, ONE filter through
+    kf_run_stream (the time-parallel route the bench times) — run_kalman_filter_full's 15-state
+    filter (config 1) or hw5_2.run_kalman_filter's 8-state one (1ref8); against the oracle's own
+    ingest of the same CSVs (oracle/ref_ingest) and the reference's dense step in C on one
     filter, every one of the ~583k events."""
     dev = torch.device('cuda', 0)
-    cfg = bench.CONFIGS['1']
+    cfg = bench.CONFIGS[config]
+    ref8 = cfg['model'] == 'ref8'
+    n_state, width = (8, 3) if ref8 else (15, 6)
     gp, ip = bench.synth_log(cfg, str(tmp_path))
-    stream = ingest.ingest_arrays(ingest.read_csv(gp, 4), ingest.read_csv(ip, 11), device=0)
+    stream = ingest.ingest_arrays(ingest.read_csv(gp, 4), ingest.read_csv(ip, 11), with_altitude=not ref8, device=0)
     first = int(torch.nonzero(stream.etype == _lib.KF_EVENT_GPS)[0, 0])
     T = len(stream) - first
     t_ev, e_ev, pay = (v[first:].contiguous() for v in (stream.t, stream.etype, stream.payload))
-    x0 = torch.zeros(15, 1, dtype=torch.float64, device=dev)
-    x0[0:3, 0] = pay[0, 0:3]
-    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    x0 = torch.zeros(n_state, 1, dtype=torch.float64, device=dev)
+    if not ref8:
+        x0[0:3, 0] = pay[0, 0:3]
+    kf = kfmi.BatchedKF(cfg['model'], 1, 'f64')
     kf.reset(x0)
-    dt, et = ingest.events_dt(t_ev, float(t_ev[0]), _lib.KF_DT_FULL, e_ev)
+    dt, et = ingest.events_dt(t_ev, float(t_ev[0]), _lib.KF_DT_RAW if ref8 else _lib.KF_DT_FULL, e_ev)
     tr, ld, _, _ = kf.run_stream(et, dt, pay)
     chk = kf.stream_check()
     kf.close()
     assert chk['ok'] and chk['chunks'] > 1000, chk
+    assert tr.shape == (T, width, 1)
     tr, ld = tr.cpu().numpy(), ld.cpu().numpy()
-    # the oracle: the reference's ingest restated, then run_kalman_filter_full's loop
-    # (kf_workers.py:655-686: start at the first fix, processed again at dt = 0; dt < 0 skipped)
-    events, _, _ = ref_ingest.ingest(gp, ip)
+    # the oracle: the reference's ingest restated, then the driver's loop from the first fix
+    # (kf_workers.py:655-686 / hw5_2.py:332-340: the fix processed at dt = 0; the full driver
+    # skips a dt < 0 event, hw5_2 predicts over it)
+    events, _, _ = ref_ingest.ingest(gp, ip, with_altitude=not ref8)
     f0 = next(i for i, e in enumerate(events) if e[1] == 'GPS')
     events = events[f0:]
     assert len(events) == T
@@ -244,13 +251,18 @@ def test_config1_whole_log_vs_oracle(tmp_path):
     eh = np.array([0 if e[1] == 'GPS' else 1 for e in events], np.uint8)
     ph = np.zeros((T, 9))
     g = eh == 0
-    ph[g, 0:3] = [[e[3]['easting'], e[3]['northing'], e[3]['altitude']] for e in events if e[1] == 'GPS']
+    ph[g, 0:2] = [[e[3]['easting'], e[3]['northing']] for e in events if e[1] == 'GPS']
+    if not ref8:
+        ph[g, 2] = [e[3]['altitude'] for e in events if e[1] == 'GPS']
     ph[~g] = [e[3][1:10] for e in events if e[1] == 'IMU']
     np.testing.assert_array_equal(eh, e_ev.cpu().numpy())
     dh = th - np.r_[th[0], th[:-1]]
-    eh[dh < 0] = 255
-    xh = np.zeros((15, 1))
-    xh[0:3, 0] = ph[0, 0:3]
-    rt, rl = cpu_kf.ref15_events(eh[:, None], dh[:, None], ph[:, :, None], xh, ref_kf.P0_REF15, nthreads=1)
+    xh = np.zeros((n_state, 1))
+    if ref8:
+        rt, rl = cpu_kf.ref8_events(eh[:, None], dh[:, None], ph[:, :, None], xh, ref_kf.P0_REF8, nthreads=1)
+    else:
+        eh[dh < 0] = 255
+        xh[0:3, 0] = ph[0, 0:3]
+        rt, rl = cpu_kf.ref15_events(eh[:, None], dh[:, None], ph[:, :, None], xh, ref_kf.P0_REF15, nthreads=1)
     ex, el = parity(tr, ld, rt, rl)
     assert ex <= F64_TOL and el <= F64_TOL, (ex, el)

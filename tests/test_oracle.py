@@ -386,3 +386,32 @@ def test_c_ref15_sched_vs_numpy_oracle(cpu_kf):
         assert _rel(st[:n, f], [r[0] for r in rs[1:]]) == 0.0
         assert _rel(tr[:n, :, f], np.array([r[1:7] for r in rs[1:]])) < 1e-10
         assert _rel(ld[:n, f], rl[1:]) < 1e-10
+
+
+def ref8_columns(events):
+    """hw5_2.run_kalman_filter's stream (hw5_2.py:332-379) as one filter's columns: events from
+    the first GPS fix on (that fix at dt = 0), dt = t - previous t with no dt < 0 guard."""
+    first = next(i for i, e in enumerate(events) if e[1] == 'GPS')
+    ev = events[first:]
+    t, et, pay = _events_to_columns([(i, s, ti, sd) for (i, s, ti, sd) in ev])
+    dt = t - np.r_[t[:1], t[:-1]]
+    return et, dt, pay
+
+
+@pytest.mark.parametrize('prefix', ['', 'ooo_'])
+def test_c_ref8_events_vs_goldens(golden_dir, cpu_kf, prefix):
+    """oracle/cpu_kf.c's 8-state model reproduces the reference's hw5_2.run_kalman_filter
+    (ref8_full.npz, in-order and out-of-order streams) and the NumPy restatement's log-dets."""
+    g = _load(golden_dir, 'ref8_full.npz')
+    events = unpack_events(g, prefix)
+    et, dt, pay = ref8_columns(events)
+    tr, ld = cpu_kf.ref8_events(et, dt, pay, np.zeros((8, 1)), ref_kf.P0_REF8)
+    want = g[prefix + 'states']
+    assert tr.shape[0] == len(want) - 1
+    assert _rel(tr[:, :, 0], want[1:]) < 1e-10
+    x, P = np.zeros(8), ref_kf.P0_REF8.copy()
+    for i in range(len(et)):
+        s = 'GPS' if et[i, 0] == 0 else 'IMU'
+        sd = {'easting': pay[i, 0, 0], 'northing': pay[i, 1, 0]} if s == 'GPS' else ['t', *pay[i, :, 0]]
+        x, P = ref_kf.step8(x, P, s, sd, dt[i, 0])
+        assert abs(ld[i, 0] - np.linalg.slogdet(P)[1]) < 1e-10 * max(1.0, abs(np.linalg.slogdet(P)[1]))
