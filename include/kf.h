@@ -415,6 +415,23 @@ int kf_run_scheduled_rec(kf_batch* handle, int T, const double* t, const uint8_t
                          int rec_len, const double* prev_time, const double* freq, double freq_all, void* traj,
                          void* logdet, double* sel_time, int32_t* n_sel, void* stream);
 
+/* The random arm (run_kalman_filter_scheduled with selection_method='random', kf_workers.py:
+ * 826-957, Scheduler.random_schedule :188-193): the same windows and outputs as kf_run_scheduled,
+ * the pick drawn as np.random.choice(len(queue)) draws it from NumPy's global legacy RandomState —
+ * randint(0, n): no draw for n = 1, else 32-bit generator outputs masked to the smallest
+ * 2^k - 1 >= n - 1 until one is <= n - 1.  The windows follow the picks (each one opens at the
+ * picked event's time), so the draws happen on the device, in the reference's order, from
+ * words device [n_words][B] u32: column f holds the raw 32-bit outputs filter f consumes in
+ * order (for the reference's one filter, the next n_words outputs of np.random's MT19937:
+ * RandomState.randint(0, 2**32, n, dtype=uint32) on a copy of its state).  words_used device
+ * [B] int32: the outputs each filter took (the caller advances its generator by that many), or
+ * -1 if its column ran out (its outputs stop at the last completed pick; retry with more).
+ * payload: [T][9][B] rows (rec_len 0) or [T][B][rec_len] records as kf_run_scheduled_rec. */
+int kf_run_scheduled_random(kf_batch* handle, int T, const double* t, const uint8_t* etype, const void* payload,
+                            int rec_len, const double* prev_time, const double* freq, double freq_all,
+                            const uint32_t* words, int n_words, int32_t* words_used, void* traj, void* logdet,
+                            double* sel_time, int32_t* n_sel, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Ingest: CSV logs -> one merged event stream in HBM (the reference's load_data,
  * gps_to_modified_utm, compute_imu_biases, unbias_imu_data, combine_sensor_data;

@@ -1255,7 +1255,8 @@ namespace {
 // record, [T][B][rec])
 int run_scheduled(const char* fn, kf_batch* h, int T, const double* t, const uint8_t* etype, const void* payload,
                   int rec, const double* prev_time, const double* freq, double freq_all, void* traj, void* logdet,
-                  double* sel_time, int32_t* n_sel, void* stream) {
+                  double* sel_time, int32_t* n_sel, void* stream, const uint32_t* words = nullptr, int n_words = 0,
+                  int32_t* words_used = nullptr) {
     if (int rc = check_handle(h)) return rc;
     if (!is_ref15(h)) return fail(KF_EINVAL, "%s: needs a KF_MODEL_REF15 handle", fn);
     if (T < 0) return fail(KF_EINVAL, "%s: T = %d < 0", fn, T);
@@ -1268,7 +1269,12 @@ int run_scheduled(const char* fn, kf_batch* h, int T, const double* t, const uin
         return fail(KF_EINVAL, "%s: the records must be 16-byte aligned", fn);
     if (h->B == 0) return KF_OK;
     if (!t || !etype || !payload || !prev_time) return fail(KF_EINVAL, "%s: null input stream", fn);
+    if (words && (n_words < 0 || !words_used))
+        return fail(KF_EINVAL, "%s: n_words = %d, words_used %s", fn, n_words, words_used ? "set" : "null");
     kfmi::Ref15SchedArgs a{};
+    a.words = words;
+    a.n_words = words ? n_words : 0;
+    a.words_used = words_used;
     a.B = h->B;
     a.kc = h->kc;
     a.T = T;
@@ -1291,7 +1297,7 @@ int run_scheduled(const char* fn, kf_batch* h, int T, const double* t, const uin
     const int64_t sk = opt(h, KF_OPT_SCHED_KERNEL);
     a.regs = sk == 1;
     a.fused = sk == 1 || sk == 2;
-    a.one_launch = sk == 4;
+    a.one_launch = sk == 4 && !words;
     a.group_waves = opt(h, KF_OPT_SCHED_GROUP) == 1 ? 1 : 4;
     // the greedy pick when both sensor classes are queued: the larger R gives the larger
     // posterior trace (launch_ref15_scheduled; checked on the covariance by the apply pass)
@@ -1349,6 +1355,16 @@ int kf_run_scheduled_rec(kf_batch* h, int T, const double* t, const uint8_t* ety
     if (rec_len <= 0) return fail(KF_EINVAL, "kf_run_scheduled_rec: rec_len = %d", rec_len);
     return run_scheduled("kf_run_scheduled_rec", h, T, t, etype, records, rec_len, prev_time, freq, freq_all, traj,
                          logdet, sel_time, n_sel, stream);
+}
+
+int kf_run_scheduled_random(kf_batch* h, int T, const double* t, const uint8_t* etype, const void* payload,
+                            int rec_len, const double* prev_time, const double* freq, double freq_all,
+                            const uint32_t* words, int n_words, int32_t* words_used, void* traj, void* logdet,
+                            double* sel_time, int32_t* n_sel, void* stream) {
+    if (rec_len < 0) return fail(KF_EINVAL, "kf_run_scheduled_random: rec_len = %d", rec_len);
+    if (!words) return fail(KF_EINVAL, "kf_run_scheduled_random: null words");
+    return run_scheduled("kf_run_scheduled_random", h, T, t, etype, payload, rec_len, prev_time, freq, freq_all, traj,
+                         logdet, sel_time, n_sel, stream, words, n_words, words_used);
 }
 
 }  // extern "C"

@@ -295,6 +295,13 @@ struct Ref15SchedArgs {
     uint32_t* order;         // [B / 64]
     void* sort_tmp;
     size_t sort_tmp_bytes;
+    // random selection (Scheduler.random_schedule, kf_workers.py:188-193; kf_run_scheduled_random):
+    // filter f draws np.random.choice(len(queue)) from its column of raw 32-bit generator outputs
+    // words[n_words][B] (NumPy's legacy masked rejection) and records how many it consumed in
+    // words_used[f] (-1: the column ran out).  nullptr: the greedy pick.
+    const uint32_t* words;
+    int n_words;
+    int32_t* words_used;
 };
 
 enum class Op { Run, Predict, Update, Step, Reset };  // Step: predict + update (kf_capi's deferral)

@@ -2416,6 +2416,34 @@ __global__ __launch_bounds__(kBlock) void ref15_score_kernel(const Ref15ScoreArg
     }
 }
 
+// Scheduler.random_schedule (kf_workers.py:188-193) is np.random.choice(len(queue)) on NumPy's
+// global legacy RandomState: randint(0, n) by masked rejection on 32-bit MT19937 outputs (n = 1
+// takes no output; otherwise mask = the smallest 2^k - 1 >= n - 1, outputs & mask until one is
+// <= n - 1).  The caller hands each filter its column of the generator's raw outputs
+// (words[n_words][B]); wp counts the ones taken.  Returns the draw, or -1 when the column ran out.
+__device__ __forceinline__ int legacy_choice(const uint32_t* words, int n_words, int64_t B, int64_t f, int& wp, int n) {
+    const uint32_t rng = uint32_t(n - 1);
+    if (rng == 0) return 0;
+    uint32_t mask = rng;
+    mask |= mask >> 1;
+    mask |= mask >> 2;
+    mask |= mask >> 4;
+    mask |= mask >> 8;
+    mask |= mask >> 16;
+    while (wp < n_words) {
+        const uint32_t v = words[int64_t(wp++) * B + f] & mask;
+        if (v <= rng) return int(v);
+    }
+    return -1;
+}
+
+// the r-th queued event of a queue that began at event `first`: every event from there on that is
+// not padding was queued (a trigger ends the queue; an empty queue's trigger is its only event)
+__device__ __forceinline__ int queued_event(const uint8_t* etype, int64_t B, int64_t f, int first, int r) {
+    for (int ev = first;; ++ev)
+        if (etype[int64_t(ev) * B + f] != 255 && r-- == 0) return ev;
+}
+
 // The greedy pick needs no scan of the queue: a candidate's gain depends only on its sensor
 // type and the current covariance, so the first candidate with the largest gain is the first
 // queued GPS fix or the first queued other event (ties: whichever came first; a NaN gain is
@@ -2433,14 +2461,16 @@ struct SchedLane {
     // scratch memory)
     int qi0 = -1, qi1 = -1, qt0 = 0, qt1 = 0;
     double qtime0 = 0.0, qtime1 = 0.0;
+    int q_first = 0, wp = 0;  // random selection: the queue's first event, generator outputs taken (-1: ran out)
 
     // event i (type ty at time ti) of filter f (kf_workers.py:870-957)
     __device__ __forceinline__ void event(const Ref15SchedArgs& a, int64_t f, int i, int ty, double ti) {
-        if (ty == 255) return;  // padding of a ragged stream
+        if (ty == 255 || wp < 0) return;  // padding of a ragged stream; a random run out of draws
         const int64_t B = a.B;
         const bool gps = ty == kGps;
         const bool window = ti - prev < period;  // still inside the window: queue it
         if (window || q_len == 0) {  // a trigger with an empty queue is its own candidate
+            if (q_len == 0) q_first = i;
             if (gps && qi0 < 0) {
                 qi0 = i;
                 qt0 = ty;
@@ -2457,16 +2487,26 @@ struct SchedLane {
         // greedy_schedule (kf_workers.py:195-213); with one class queued its first event is
         // the pick whatever the gain (a NaN gain leaves the queue's first, the same event)
         bool pick0 = qi0 >= 0;
-        if (qi0 >= 0 && qi1 >= 0) {
+        if (qi0 >= 0 && qi1 >= 0 && !a.words) {
             const T g0 = first_row_gain(s, kGps), g1 = first_row_gain(s, kImu);
             const bool v0 = g0 == g0, v1 = g1 == g1;
             if (v0 && v1) pick0 = g0 > g1 ? true : (g1 > g0 ? false : qi0 < qi1);
             else if (v0 != v1) pick0 = v0;
             else pick0 = qi0 < qi1;  // the queue's first
         }
-        const int sel = pick0 ? qi0 : qi1;
-        const double tsel = pick0 ? qtime0 : qtime1;
-        const int tsel_type = pick0 ? qt0 : qt1;
+        int sel = pick0 ? qi0 : qi1;
+        double tsel = pick0 ? qtime0 : qtime1;
+        int tsel_type = pick0 ? qt0 : qt1;
+        if (a.words) {  // random_schedule: any queued event, drawn as the reference draws it
+            const int r = legacy_choice(a.words, a.n_words, B, f, wp, q_len);
+            if (r < 0) {
+                wp = -1;
+                return;
+            }
+            sel = queued_event(a.etype, B, f, q_first, r);
+            tsel = a.t[int64_t(sel) * B + f];
+            tsel_type = a.etype[int64_t(sel) * B + f];
+        }
         q_len = 0;
         qi0 = qi1 = -1;
         T pay[9];
@@ -2527,6 +2567,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED
         L.event(a, f, i, ty, ti);
     }
     if (a.n_sel) a.n_sel[f] = L.nsel;
+    if (a.words_used) a.words_used[f] = L.wp;
     L.s.store(a.x, a.P, rb, off);
     a.status[f] = L.st;
 }
@@ -2594,6 +2635,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KF_SCHED
         for (int d = 0; d < nr; ++d) L.event(a, f, r0 + d, int(ty_img[d * 64]), ti_img[d * 64]);
     }
     if (a.n_sel) a.n_sel[f] = L.nsel;
+    if (a.words_used) a.words_used[f] = L.wp;
     L.s.store(a.x, a.P, rb, off);
     a.status[f] = L.st;
 }
@@ -2648,6 +2690,9 @@ constexpr int kPickChunk = KF_PICK_CHUNK;
 constexpr int kPickImg = kPickChunk * 512 + kPickChunk * 64;
 // The pick pass of one wave (filters f0 .. f0 + 63) with its two staging images at img0
 // (2 * kPickImg bytes); returns this lane's pick count.  Every store is issued on return.
+// RND: random_schedule's pick (a.words) instead of the greedy rule's; picks carry no
+// both-classes bit, so the apply pass checks nothing and flags no filter.
+template <bool RND = false>
 __device__ __forceinline__ int pick_phase(const Ref15SchedArgs& a, int lane, int64_t f0, unsigned char* img0) {
     constexpr int kSchedChunk = kPickChunk, kSchedImg = kPickImg;  // the fused kernel's staging, resized
     static_assert(kSchedChunk % 2 == 0 && kSchedChunk <= 16, "t rows move in pairs; etype rows 4 lanes each");
@@ -2657,6 +2702,7 @@ __device__ __forceinline__ int pick_phase(const Ref15SchedArgs& a, int lane, int
     const double period = 1.0 / (a.freq ? a.freq[f] : a.freq_all);  // kf_workers.py:880
     int q_len = 0, nsel = 0, qi0 = -1, qi1 = -1, qt0 = 0, qt1 = 0;
     double qtime0 = 0.0, qtime1 = 0.0;
+    int q_first = 0, wp = 0;  // RND: the queue's first event, generator outputs taken (-1: ran out)
     waitcnt<vmcnt_imm(0)>();
     const uint32_t voff_t = uint32_t(lane >> 5) * uint32_t(B) * 8u + uint32_t(lane & 31) * 16u;
     const uint32_t voff_e = uint32_t(lane >> 2) * uint32_t(B) + uint32_t(lane & 3) * 16u;
@@ -2691,10 +2737,11 @@ __device__ __forceinline__ int pick_phase(const Ref15SchedArgs& a, int lane, int
             const int ty = int(ty_img[d * 64]);
             const double ti = ti_img[d * 64];
             const int i = r0 + d;
-            if (ty == 255) continue;  // padding of a ragged stream
+            if (ty == 255 || (RND && wp < 0)) continue;  // padding of a ragged stream; out of draws
             const bool gps = ty == kGps;
             const bool window = ti - prev < period;  // SchedLane::event, kf_workers.py:870-957
             if (window || q_len == 0) {
+                if (RND && q_len == 0) q_first = i;
                 if (gps && qi0 < 0) {
                     qi0 = i;
                     qt0 = ty;
@@ -2711,9 +2758,19 @@ __device__ __forceinline__ int pick_phase(const Ref15SchedArgs& a, int lane, int
             const bool both = qi0 >= 0 && qi1 >= 0;
             const bool gps_first = qi0 >= 0 && (qi1 < 0 || qi0 < qi1);
             const bool pick0 = both ? (a.gps_wins > 0 ? true : a.gps_wins == 0 ? false : gps_first) : qi0 >= 0;
-            const int sel = pick0 ? qi0 : qi1;
-            const double tsel = pick0 ? qtime0 : qtime1;
-            const int code = (pick0 ? qt0 : qt1) | (both ? kPickBoth : 0) | (gps_first ? kPickGpsFirst : 0);
+            int sel = pick0 ? qi0 : qi1;
+            double tsel = pick0 ? qtime0 : qtime1;
+            int code = (pick0 ? qt0 : qt1) | (both ? kPickBoth : 0) | (gps_first ? kPickGpsFirst : 0);
+            if constexpr (RND) {
+                const int r = legacy_choice(a.words, a.n_words, B, f, wp, q_len);
+                if (r < 0) {
+                    wp = -1;
+                    continue;
+                }
+                sel = queued_event(a.etype, B, f, q_first, r);
+                tsel = a.t[int64_t(sel) * B + f];
+                code = a.etype[int64_t(sel) * B + f];
+            }
             a.picks[int64_t(nsel) * B + f] = (uint32_t(code) << 24) | uint32_t(sel);
             if (a.sel_time) a.sel_time[int64_t(nsel) * B + f] = tsel;
             ++nsel;
@@ -2723,18 +2780,19 @@ __device__ __forceinline__ int pick_phase(const Ref15SchedArgs& a, int lane, int
         }
     }
     if (a.n_sel) a.n_sel[f] = nsel;
+    if (RND && a.words_used) a.words_used[f] = wp;
     a.flags[f] = 0;
     return nsel;
 }
 
-template <int WAVES>
+template <int WAVES, bool RND = false>
 __global__ __launch_bounds__(WAVES * 64) void ref15_pick_kernel(const Ref15SchedArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[WAVES * 2 * kPickImg];
     const int lane = int(threadIdx.x & 63);
     const int wave = WAVES == 1 ? 0 : wave_uniform(int(threadIdx.x >> 6));
     const int64_t f0 = int64_t(blockIdx.x) * (WAVES * 64) + int64_t(wave) * 64;
     if (f0 >= a.B) return;  // whole waves (B % 64 == 0)
-    const int nsel = pick_phase(a, lane, f0, lds + wave * 2 * kPickImg);
+    const int nsel = pick_phase<RND>(a, lane, f0, lds + wave * 2 * kPickImg);
     if (a.wave_key) {  // the wave's longest pick list, for the apply pass's heaviest-first order
         int S = nsel;
 #pragma unroll
@@ -3012,7 +3070,8 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
         // four-wave groups (KF_OPT_SCHED_GROUP): one-wave groups, which free their slot when their
         // wave's pick list ends, measured slower on the bench row (5.51 vs 5.07 ms apply)
         const dim3 g1(static_cast<unsigned>(a.B / 64)), g4(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
-        if (a.one_launch) {
+        const bool rnd = a.words != nullptr;
+        if (a.one_launch && !rnd) {
             Ref15SchedArgs c = a;  // heaviest first by rate where the filters have their own rates
             c.order = nullptr;
             if (a.order && a.freq) {
@@ -3033,7 +3092,8 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
                 }
             });
         } else {
-            if (a.group_waves == 4) ref15_pick_kernel<4><<<g4, 256, 0, stream>>>(a);
+            if (rnd) ref15_pick_kernel<4, true><<<g4, 256, 0, stream>>>(a);
+            else if (a.group_waves == 4) ref15_pick_kernel<4><<<g4, 256, 0, stream>>>(a);
             else ref15_pick_kernel<1><<<g1, 64, 0, stream>>>(a);
             if (a.order) {  // the waves by their longest pick list, descending (stable)
                 int bits = 1;
@@ -3064,6 +3124,7 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
                 }
             });
         }
+        if (rnd) return hipGetLastError();  // random picks are never checked, so none is flagged
         Ref15SchedArgs b = a;  // the flagged filters (usually none: every lane leaves at once)
         b.only = a.flags;
         KF_CUSTOM_DISPATCH(a.kc, {

@@ -500,6 +500,39 @@ class BatchedKF:
                                               fa, _ptr(tr), _ptr(ld), _ptr(stt), _ptr(ns), self._stream()))
         return tr, ld, stt, ns
 
+    def run_scheduled_random(self, t, etype, payload, prev_time, freq, words, records=False):
+        """KF_MODEL_REF15 random-selection scheduled filter (kf_run_scheduled_random): the
+        windows of run_scheduled, each pick np.random.choice(len(queue)) drawn on the device from
+        ``words`` [n_words, B] uint32 — column f the raw 32-bit generator outputs filter f
+        consumes, in order (see kfmi.ref15.legacy_words).  Returns (traj, logdet, sel_time, n_sel,
+        words_used [B] int32: outputs taken, -1 if a column ran out)."""
+        if self.model != 'ref15':
+            raise ValueError('run_scheduled_random needs a ref15 handle')
+        T = int(t.shape[0])
+        td = self._dev(t, (T, self.batch), 't', torch.float64)
+        et = self._dev(etype, (T, self.batch), 'etype', torch.uint8)
+        rec = int(payload.shape[2]) if records else 0
+        pay = self._dev(payload, (T, self.batch, rec) if records else (T, 9, self.batch), 'payload')
+        pv = self._dev(prev_time, (self.batch,), 'prev_time', torch.float64)
+        W = int(words.shape[0])
+        if isinstance(words, np.ndarray):
+            words = np.ascontiguousarray(words, np.uint32).view(np.int32)
+        elif words.dtype == torch.uint32:
+            words = words.view(torch.int32)
+        wd = self._dev(words, (W, self.batch), 'words', torch.int32)  # the bits of the uint32 outputs
+        fr = None
+        if np.ndim(freq) != 0:
+            fr = self._dev(freq, (self.batch,), 'freq', torch.float64)
+        tr = self.empty(max(T, 1), 6, self.batch)
+        ld = self.empty(max(T, 1), self.batch)
+        stt = torch.empty(max(T, 1), self.batch, dtype=torch.float64, device=self.device)
+        ns = torch.empty(self.batch, dtype=torch.int32, device=self.device)
+        used = torch.empty(self.batch, dtype=torch.int32, device=self.device)
+        check(_lib.lib().kf_run_scheduled_random(self.handle, T, _ptr(td), _ptr(et), _ptr(pay), rec, _ptr(pv), _ptr(fr),
+                                                 float(freq) if fr is None else 0.0, _ptr(wd), W, _ptr(used),
+                                                 _ptr(tr), _ptr(ld), _ptr(stt), _ptr(ns), self._stream()))
+        return tr, ld, stt, ns, used
+
     # -- synthetic streams (SURVEY.md §8d) -----------------------------------------------
     def synth(self, T, dt, update_every=1, seed=20251015, filter_offset=0):
         """Deterministic synthetic (x0 [n,B], u [T,c,B], z [U,m,B]) generated on the GPU."""

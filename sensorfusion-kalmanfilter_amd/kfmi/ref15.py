@@ -761,13 +761,21 @@ def _stream_arrays(cands, B=1):
     return t, et, pay
 
 
+def legacy_words(n):
+    """The next n raw 32-bit outputs of NumPy's global legacy generator (np.random's
+    MT19937), without advancing it: what kf_run_scheduled_random draws np.random.choice from."""
+    rs = np.random.RandomState()
+    rs.set_state(np.random.get_state())
+    return rs.randint(0, 1 << 32, size=n, dtype=np.uint32)
+
+
 def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt=None, initial_state=None,
                                 selection_method=None, processing_frequency=None, print_output=False,
                                 dtype='f64', device=0, consts=None):
     """kf_workers.py:826-957 on the GPU.  'greedy': windowing, Scheduler scoring and the filter
-    all run in kf_run_scheduled; 'random': the pick is np.random.choice over the queue, drawn
-    from the global NumPy RNG in the same order as the reference (the windows do not depend on
-    the filter state), and the selected events run in kf_run_events.  Returns (states,
+    all run in kf_run_scheduled; 'random': the same in kf_run_scheduled_random, each pick
+    np.random.choice over the queue drawn on the device from the global NumPy generator's outputs
+    in the reference's order (the generator advances by the outputs drawn).  Returns (states,
     logdets, P)."""
     if selection_method not in ('random', 'greedy'):
         print("Invalid selection_method. Choose either 'random' or 'greedy'.")
@@ -794,22 +802,30 @@ def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt
         states = [(prev0, *x0[:6])] + [(stt[i, 0], *tr[i, :, 0]) for i in range(n)]
         logdets = [float(ld0)] + [float(v) for v in ld[:n, 0]]
     else:
-        selected, queue, prev = [], [], prev0
-        for ev in cands:
-            if ev[2] - prev < 1 / f:
-                queue.append(ev)
-                continue
-            if not queue:
-                queue.append(ev)
-            sel = queue[np.random.choice(len(queue))]
-            queue = []
-            selected.append((GPS if sel[1] == 'GPS' else IMU, sel[2] - prev, event_payload(sel[1], sel[3]), sel[2]))
-            prev = sel[2]
-        tr, ld, _, x, Pb, st = _run_streams([[s[:3] for s in selected]], x0[None], to_blocks(P)[None], dtype, device,
-                                            consts=consts)
-        states = [(prev0, *tr[0, :, 0])] + [(s[3], *tr[i + 1, :, 0]) for i, s in enumerate(selected)]
-        logdets = [float(v) for v in ld[:len(selected) + 1, 0]]
-        Pf = from_blocks(Pb[:, 0])
+        # random_schedule (kf_workers.py:188-193): each window's np.random.choice is drawn on the
+        # device from the global generator's next outputs, in the reference's order (the windows
+        # follow the picks); the global generator then advances by the outputs the run took
+        kf = BatchedKF('ref15', 1, dtype, device=device, params=_params(consts))
+        npd = np.float64 if dtype == 'f64' else np.float32
+        t, et, pay = _stream_arrays(cands)
+        n_words = 2 * len(cands) + 64
+        while True:
+            kf.set_state(x0[:, None].astype(npd), to_blocks(P)[:, None].astype(npd))
+            tr, ld, stt, ns, used = kf.run_scheduled_random(t, et, pay.astype(npd), np.array([prev0]), f,
+                                                            legacy_words(n_words)[:, None])
+            taken = int(used[0])
+            if taken >= 0:
+                break
+            n_words *= 4  # the column ran out (rejections beyond 2 outputs per window): draw again
+        np.random.randint(0, 1 << 32, size=taken, dtype=np.uint32)
+        ld0 = _run_streams([[]], x0[None], to_blocks(P)[None], dtype, device, consts=consts)[1][0, 0]
+        n = int(ns[0])
+        tr, ld, stt = tr.double().cpu().numpy(), ld.double().cpu().numpy(), stt.cpu().numpy()
+        _, Pb = kf.state()
+        Pf = from_blocks(Pb[:, 0].double().cpu().numpy())
+        kf.close()
+        states = [(prev0, *x0[:6])] + [(stt[i, 0], *tr[i, :, 0]) for i in range(n)]
+        logdets = [float(ld0)] + [float(v) for v in ld[:n, 0]]
     if print_output:
         print(f'{selection_method.capitalize()} Scheduled Kalman Filter (GPU): processed {len(states) - 1} measurements')
     return states, logdets, Pf

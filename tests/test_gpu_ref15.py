@@ -523,6 +523,63 @@ def test_scheduled_random_streams_vs_oracle(seed, B):
         assert _rel(ld[:n, f], rl[1:]) <= TOL, f
 
 
+@pytest.mark.parametrize('B,records', [(48, False), (128, False), (128, True)])
+def test_scheduled_random_vs_oracle(B, records):
+    """kf_run_scheduled_random (the random arm, kf_workers.py:826-957 with random_schedule
+    :188-193) over random ragged streams with per-lane rates: each filter draws from its own
+    column of generator outputs, and against the oracle's random driver drawing from a
+    RandomState with the same seed it picks the same events (times bitwise) with the same states
+    and log-dets, and reports exactly the outputs the oracle consumed.  B = 48: the fused kernel;
+    B = 128: the pick and apply passes (payload rows and records).  A column too short for its
+    filter's draws reports -1."""
+    rng = np.random.default_rng(60 + B + records)
+    T = 120
+    t0, rates, etype, tt, pay = _sched_streams(rng, B, T)
+    W = 2 * T + 64
+    words = np.stack([np.random.RandomState(1000 + f).randint(0, 1 << 32, size=W, dtype=np.uint32)
+                      for f in range(B)], axis=1)
+    x0 = np.zeros((15, B))
+    x0[0:6] = rng.normal(0, 2, (6, B))
+    Pblk = np.repeat(ref15.to_blocks(ref_kf.P0_REF15)[:, None], B, axis=1)
+    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    kf.set_state(x0, Pblk)
+    payload = _sched_records(pay, 12) if records else pay
+    tr, ld, stt, ns, used = (v.cpu().numpy() for v in kf.run_scheduled_random(tt, etype, payload, np.full(B, t0),
+                                                                               rates, words, records=records))
+    kf.close()
+    for f in range(B):
+        ev = [(0, 'GPS', t0, {'easting': 0.0, 'northing': 0.0, 'altitude': 0.0})]  # skipped (warm start)
+        for i in range(T):
+            if etype[i, f] == 255:
+                break
+            ev.append((i + 1, 'GPS', tt[i, f], {'easting': pay[i, 0, f], 'northing': pay[i, 1, f],
+                                                'altitude': pay[i, 2, f]}) if etype[i, f] == 0
+                      else (i + 1, 'IMU', tt[i, f], ['t', *pay[i, :, f]]))
+        gen = np.random.RandomState(1000 + f)
+        rs, rl, _ = ref_kf.run_kalman_filter_scheduled(ev, 0, len(ev), ref_kf.P0_REF15.copy(), (t0, *x0[0:6, f]),
+                                                       'random', rates[f], rng_choice=gen.choice)
+        after = gen.random_sample()
+        check = np.random.RandomState(1000 + f)
+        check.randint(0, 1 << 32, size=int(used[f]), dtype=np.uint32)
+        assert check.random_sample() == after, f     # the outputs taken are the ones the oracle drew
+        n = int(ns[f])
+        assert n == len(rs) - 1, f
+        if n == 0:
+            continue
+        np.testing.assert_array_equal(stt[:n, f], [r[0] for r in rs[1:]])
+        assert _rel(tr[:n, :, f], np.array([r[1:7] for r in rs[1:]])) <= TOL, f
+        assert _rel(ld[:n, f], rl[1:]) <= TOL, f
+    # too few outputs: the filter stops at its last completed pick and reports -1
+    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    kf.set_state(x0, Pblk)
+    out = kf.run_scheduled_random(tt, etype, payload, np.full(B, t0), rates, words[:3], records=records)
+    kf.close()
+    u3, n3 = out[4].cpu().numpy(), out[3].cpu().numpy()
+    short = used > 3
+    assert short.any() and (u3[short] == -1).all() and (u3[~short] == used[~short]).all()
+    assert (n3[short] <= ns[short]).all() and (n3[~short] == ns[~short]).all()
+
+
 def _sched_streams(rng, B, T):
     """Random scheduled-filter inputs as test_scheduled_random_streams_vs_oracle builds them."""
     t0 = 1697739278.761565

@@ -159,3 +159,45 @@ def test_class_args_worker_checks_formulas():
           'get_imu_measurement_noise_covariance_matrix': lambda: np.diag(np.arange(1.0, 16.0))}
     c = kw._consts_of(ok)
     np.testing.assert_array_equal(c.r_imu, np.arange(1.0, 16.0))
+
+
+def legacy_choice_emulation(words, lens):
+    """What kf_run_scheduled_random's legacy_choice does (kf_ref.hip), in Python: per window of
+    n queued events, no output for n = 1, else outputs & (smallest 2^k - 1 >= n - 1) until one is
+    <= n - 1.  Returns (draws, outputs taken)."""
+    wp, out = 0, []
+    for n in lens:
+        rng = int(n) - 1
+        if rng == 0:
+            out.append(0)
+            continue
+        mask = rng
+        for sh in (1, 2, 4, 8, 16):
+            mask |= mask >> sh
+        while True:
+            v = int(words[wp]) & mask
+            wp += 1
+            if v <= rng:
+                out.append(v)
+                break
+    return out, wp
+
+
+def test_device_draws_reproduce_np_random_choice():
+    """The random scheduled filter draws np.random.choice(len(queue)) on the device from the
+    global generator's raw outputs (kfmi.ref15.legacy_words, read without advancing it); the
+    masked rejection gives the reference's draws exactly (kf_workers.py:188-193), including queues
+    of one (no draw) and sizes past 2^16, and advancing the generator by the outputs taken leaves
+    it where the reference's calls leave it."""
+    rng = np.random.default_rng(3)
+    lens = np.r_[rng.integers(1, 300, 5000), [1, 1, 2, 65537, 3, 1 << 20, 1]]
+    np.random.seed(77)
+    words = ref15.legacy_words(3 * len(lens))
+    got, taken = legacy_choice_emulation(words, lens)
+    want = [np.random.choice(int(n)) for n in lens]
+    after = np.random.random()
+    assert got == want
+    np.random.seed(77)
+    np.testing.assert_array_equal(ref15.legacy_words(3 * len(lens)), words)   # reading does not advance
+    np.random.randint(0, 1 << 32, size=taken, dtype=np.uint32)
+    assert np.random.random() == after
