@@ -726,18 +726,36 @@ def scheduler_gain(covariances, types=('GPS', 'IMU'), full=False, dtype='f64', d
     return out
 
 
+def _host_stream(events):
+    """The host arrays behind an event list that views an ingested stream (kfmi.kf_workers
+    .EventList over kf_ingest's output), or None for a plain list of tuples."""
+    h = getattr(events, 'h', None)
+    return h if isinstance(h, dict) and {'t', 'etype', 'payload'} <= set(h) else None
+
+
 def _scheduled_window_events(events, start_idx, end_idx, initial_pt, initial_state, consts=None):
-    """Start state and candidate list exactly as run_kalman_filter_scheduled sets them up
-    (kf_workers.py:828-877).  Returns (x0, P, prev_time, candidates) or None."""
+    """Start state and candidate events exactly as run_kalman_filter_scheduled sets them up
+    (kf_workers.py:828-877).  Returns (x0, P, prev_time, candidates) or None; candidates is the
+    list of event tuples, or for an event list over an ingested stream the (lo, hi) index range
+    of the candidates in its arrays (no per-event Python)."""
     if start_idx is None or start_idx < 0:
         start_idx = 0
     if end_idx is None or end_idx > len(events):
         end_idx = len(events)
     x0 = np.zeros(15)
+    h = _host_stream(events)
     if initial_state is not None:
         P = np.asarray(initial_pt, np.float64)
         x0[0:6] = initial_state[1:7]
         start_off, prev = start_idx, initial_state[0]
+    elif h is not None:
+        P = _p0(consts)
+        fixes = np.nonzero(h['etype'][start_idx:end_idx] == GPS)[0]
+        if not len(fixes):
+            return None
+        start_off = start_idx + int(fixes[0])
+        x0[0:3] = h['payload'][start_off, 0:3]
+        prev = float(h['t'][start_off])
     else:
         P = _p0(consts)
         cs = _cold_start(events, start_idx, end_idx)
@@ -746,10 +764,26 @@ def _scheduled_window_events(events, start_idx, end_idx, initial_pt, initial_sta
         x0, prev, start_off = cs
     if end_idx == -1:
         end_idx = len(events)
+    if h is not None:
+        return x0, P, prev, (start_off + 1, max(start_off + 1, end_idx))
     return x0, P, prev, list(events[start_off + 1:end_idx])
 
 
-def _stream_arrays(cands, B=1):
+def _stream_arrays(cands, B=1, events=None):
+    """Candidate events as one filter's streams repeated over B columns: t [T, B], etype [T, B],
+    payload [T, 9, B] (T >= 1: an empty window is one padding event).  cands: event tuples, or
+    an index range into the ingested arrays of ``events`` (_scheduled_window_events)."""
+    if isinstance(cands, tuple):
+        h = _host_stream(events)
+        lo, hi = cands
+        T = hi - lo
+        t = np.zeros((max(T, 1), B))
+        et = np.full((max(T, 1), B), NONE, np.uint8)
+        pay = np.zeros((max(T, 1), 9, B))
+        t[:T] = h['t'][lo:hi, None]
+        et[:T] = h['etype'][lo:hi, None]
+        pay[:T] = h['payload'][lo:hi, :, None]
+        return t, et, pay, T
     T = len(cands)
     t = np.zeros((max(T, 1), B))
     et = np.full((max(T, 1), B), NONE, np.uint8)
@@ -758,7 +792,7 @@ def _stream_arrays(cands, B=1):
         t[i, :] = ti
         et[i, :] = GPS if stype == 'GPS' else IMU
         pay[i, :, :] = np.asarray(event_payload(stype, sdata))[:, None]
-    return t, et, pay
+    return t, et, pay, T
 
 
 def legacy_words(n):
@@ -789,9 +823,8 @@ def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt
         kf = BatchedKF('ref15', 1, dtype, device=device, params=_params(consts))
         npd = np.float64 if dtype == 'f64' else np.float32
         kf.set_state(x0[:, None].astype(npd), to_blocks(P)[:, None].astype(npd))
-        t, et, pay = _stream_arrays(cands)
-        tr, ld, stt, ns = kf.run_scheduled(t[:len(cands) or 1], et[:len(cands) or 1], pay.astype(npd)[:len(cands) or 1],
-                                           np.array([prev0]), f)
+        t, et, pay, _ = _stream_arrays(cands, events=events)
+        tr, ld, stt, ns = kf.run_scheduled(t, et, pay.astype(npd), np.array([prev0]), f)
         # the handle's initial logdet comes from a zero-event pass of the same kernels
         ld0 = _run_streams([[]], x0[None], to_blocks(P)[None], dtype, device, consts=consts)[1][0, 0]
         n = int(ns[0])
@@ -807,8 +840,8 @@ def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt
         # follow the picks); the global generator then advances by the outputs the run took
         kf = BatchedKF('ref15', 1, dtype, device=device, params=_params(consts))
         npd = np.float64 if dtype == 'f64' else np.float32
-        t, et, pay = _stream_arrays(cands)
-        n_words = 2 * len(cands) + 64
+        t, et, pay, n_cand = _stream_arrays(cands, events=events)
+        n_words = 2 * n_cand + 64
         while True:
             kf.set_state(x0[:, None].astype(npd), to_blocks(P)[:, None].astype(npd))
             tr, ld, stt, ns, used = kf.run_scheduled_random(t, et, pay.astype(npd), np.array([prev0]), f,
@@ -845,7 +878,7 @@ def sampling_sweep(events, frequencies, start_idx=None, end_idx=None, initial_pt
     npd = np.float64 if dtype == 'f64' else np.float32
     kf = BatchedKF('ref15', B, dtype, device=device, params=_params(consts))
     kf.set_state(np.repeat(x0[:, None], B, 1).astype(npd), np.repeat(to_blocks(P)[:, None], B, 1).astype(npd))
-    t, et, pay = _stream_arrays(cands, B)
+    t, et, pay, _ = _stream_arrays(cands, B, events=events)
     tr, ld, stt, ns = kf.run_scheduled(t, et, pay.astype(npd), np.full(B, prev0), freqs)
     ld0 = _run_streams([[]], x0[None], to_blocks(P)[None], dtype, device, consts=consts)[1][0, 0]
     tr, ld, stt, ns = tr.double().cpu().numpy(), ld.double().cpu().numpy(), stt.cpu().numpy(), ns.cpu().numpy()

@@ -152,3 +152,30 @@ def test_hw5_2_sequence(csvs):
     assert np.array(st).shape == np.array(rs).shape
     assert _rel(st, rs) <= 1e-6
     assert abs(sf.quaternion_to_euler(0.0, 0.0, 0.0, 1.0)[2]) == 0.0
+
+
+@pytest.mark.parametrize('method', ['greedy', 'random'])
+def test_scheduled_driver_on_the_ingested_list(csvs, method):
+    """run_kalman_filter_scheduled on the façade's event list over the ingested stream (its
+    windows read straight from the stream's arrays, no per-event tuples): cold start and a
+    warm-start window, against the oracle's driver over the oracle's own ingest, with np.random
+    seeded alike for the random arm; the global generator ends where the reference leaves it."""
+    sf = kfw.KF_SensorFusion(*csvs)
+    sf.load_data()
+    sf.gps_to_modified_utm()
+    bw, ba, _ = sf.compute_imu_biases(sf.gps_data, sf.imu_data)
+    sf.unbias_imu_data(bw, ba)
+    sf.combine_sensor_data()
+    sf.set_processing_frequency(50)
+    events, _, _ = ref_ingest.ingest(*csvs)
+    P = ref_kf.P0_REF15 * 0.01
+    for args in ((None, None, None, None), (400, 1500, P, (float(events[399][2]), 1.0, 2.0, 0.5, 0.0, 0.0, 0.1))):
+        np.random.seed(11)
+        st, ld, Pf = sf.run_kalman_filter_scheduled(*args, selection_method=method)
+        after = np.random.random()
+        np.random.seed(11)
+        rs, rl, rP = ref_kf.run_kalman_filter_scheduled(events, *args, method, 50.0)
+        assert np.random.random() == after
+        assert len(st) == len(rs) > 10
+        np.testing.assert_array_equal([s[0] for s in st], [r[0] for r in rs])
+        assert _rel(st, rs) <= 1e-6 and _rel(ld, rl) <= 1e-6 and _rel(Pf, rP) <= 1e-6
