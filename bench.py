@@ -764,6 +764,8 @@ def sched_workload(cfg, args, rank, world, dev):
     if not rows:
         recs = torch.zeros(T, B, rec, dtype=torch.float64, device=dev)
         recs[:, :, :9] = pay.transpose(1, 2)
+        if rec >= 10:
+            recs[:, :, 9] = tt  # the event's time (read with --opt sched_rec_time=on)
     traj = kf.empty(T, 6, B)
     logdet = kf.empty(T, B)
     sel_time = torch.empty(T, B, dtype=torch.float64, device=dev)

@@ -155,6 +155,11 @@ const char* kf_version(void);
  *   KF_OPT_SCHED_ORDER    kf_run_scheduled's two launches: 0 = the apply pass runs the waves
  *                         heaviest first (their longest pick lists, sorted on the device),
  *                         1 = in batch order
+ *   KF_OPT_SCHED_REC_TIME kf_run_scheduled_rec / _random over f64 records of rec_len >= 10:
+ *                         0 = rec[9..] unread; 1 = rec[9] holds the event's time (t[i][f]) and
+ *                         the apply pass takes each pick's time from the record it gathers
+ *                         anyway (the pick pass then writes no sel_time row of its own: the apply
+ *                         pass writes it, coalesced)
  * KF_EINVAL for an unknown option or an out-of-range value. */
 #define KF_OPT_PREDICT        1
 #define KF_OPT_CV_KERNEL      2
@@ -169,7 +174,8 @@ const char* kf_version(void);
 #define KF_OPT_SCHED_KERNEL   11
 #define KF_OPT_SCHED_GROUP    12
 #define KF_OPT_SCHED_ORDER    13
-#define KF_OPT_COUNT          14
+#define KF_OPT_SCHED_REC_TIME 14
+#define KF_OPT_COUNT          15
 int kf_set_option(kf_batch* handle, int option, int64_t value);
 int kf_get_option(const kf_batch* handle, int option, int64_t* value);
 

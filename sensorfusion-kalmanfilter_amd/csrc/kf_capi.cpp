@@ -356,7 +356,8 @@ int kf_set_option(kf_batch* h, int option, int64_t value) {
         case KF_OPT_SEARCH_PM: ok = value == 0 || value == 1; break;
         case KF_OPT_SCHED_KERNEL: ok = value >= 0 && value <= 4; break;
         case KF_OPT_SCHED_GROUP: ok = value == 0 || value == 1 || value == 4; break;
-        case KF_OPT_SCHED_ORDER: ok = value == 0 || value == 1; break;
+        case KF_OPT_SCHED_ORDER:
+        case KF_OPT_SCHED_REC_TIME: ok = value == 0 || value == 1; break;
         case KF_OPT_CV_KERNEL: ok = value == 0 || value == 1 || value == 2 || value == 4 || value == 8; break;
         case KF_OPT_BLOCKS_PER_CU: ok = value == 0 || (value >= 2 && value <= 8); break;
         case KF_OPT_EVENTS_KERNEL: ok = value >= 0 && value <= 3; break;
@@ -1298,6 +1299,9 @@ int run_scheduled(const char* fn, kf_batch* h, int T, const double* t, const uin
     a.regs = sk == 1;
     a.fused = sk == 1 || sk == 2;
     a.one_launch = sk == 4 && !words;
+    // the event's time at rec[9] of f64 records (KF_OPT_SCHED_REC_TIME): the apply pass reads it
+    // from the record it gathers, and writes sel_time itself
+    a.rec_time = opt(h, KF_OPT_SCHED_REC_TIME) == 1 && rec >= 10 && h->dtype == KF_F64;
     a.group_waves = opt(h, KF_OPT_SCHED_GROUP) == 1 ? 1 : 4;
     // the greedy pick when both sensor classes are queued: the larger R gives the larger
     // posterior trace (launch_ref15_scheduled; checked on the covariance by the apply pass)

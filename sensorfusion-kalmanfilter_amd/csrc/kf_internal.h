@@ -302,6 +302,9 @@ struct Ref15SchedArgs {
     const uint32_t* words;
     int n_words;
     int32_t* words_used;
+    // f64 records whose element 9 is the event's time (KF_OPT_SCHED_REC_TIME): the two passes
+    // take each pick's time from its gathered record (the pick pass writes no sel_time)
+    bool rec_time;
 };
 
 enum class Op { Run, Predict, Update, Step, Reset };  // Step: predict + update (kf_capi's deferral)

@@ -2772,7 +2772,7 @@ __device__ __forceinline__ int pick_phase(const Ref15SchedArgs& a, int lane, int
                 code = a.etype[int64_t(sel) * B + f];
             }
             a.picks[int64_t(nsel) * B + f] = (uint32_t(code) << 24) | uint32_t(sel);
-            if (a.sel_time) a.sel_time[int64_t(nsel) * B + f] = tsel;
+            if (a.sel_time && !a.rec_time) a.sel_time[int64_t(nsel) * B + f] = tsel;  // rec_time: the apply pass writes it
             ++nsel;
             prev = tsel;
             q_len = 0;
@@ -2831,9 +2831,14 @@ __global__ __launch_bounds__(kBlock) void ref15_rate_key_kernel(const Ref15Sched
 // phase overlaps the other waves' compute-bound apply phases)
 // REC: the payload is [T][B][pay_rec] records (kf_run_scheduled_rec): a lane's 9 values are one
 // contiguous 72-B (f64) span, gathered as 16-B chunks, instead of 9 rows B elements apart
-template <typename T, bool CUSTOM, int WAVES, bool PICK, bool REC = false>
+// RT: f64 records carry the event's time at rec[9] (KF_OPT_SCHED_REC_TIME): each pick's time
+// comes with its gathered record (the 16-B chunk holding payload[8] already spans it) instead of
+// a sel_time row read, and this pass writes sel_time; two payload images, so pick q + 1's record
+// (and time) is in flight through event q
+template <typename T, bool CUSTOM, int WAVES, bool PICK, bool REC = false, bool RT = false>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3))) void ref15_apply_kernel(
     const Ref15SchedArgs a) {
+    static_assert(!RT || (REC && sizeof(T) == 8 && !PICK), "record time: f64 records, two launches");
     constexpr int W = int(sizeof(T));
     // The picked payload is gathered per lane: the picks of a wave's lanes lie on different rows,
     // so with the [T][9][B] rows every gather instruction touches up to 64 cache lines and the
@@ -2846,7 +2851,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     // NIMG = 2: two payload images, pick q + 1's gather issued before event q's predict (a whole
     // event of cover instead of one predict), at the LDS cost of fewer waves per CU
     // (records: 5-KB images, so two fit 12 waves per CU, KF_REC_IMAGES=2: measured no faster)
-    constexpr int NIMG = PICK ? 1 : REC ? KF_REC_IMAGES : KF_APPLY_IMAGES;
+    constexpr int NIMG = RT ? 2 : PICK ? 1 : REC ? KF_REC_IMAGES : KF_APPLY_IMAGES;
     static_assert(NIMG == 1 || NIMG == 2, "payload images");
     using Gathered = LdsGathered<T, REC>;
     constexpr int GB = Gathered::kSlot;
@@ -2856,7 +2861,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     constexpr int PK = TM + 2 * 512;       // picks, three rows (q % 3), 64 u32 each
     constexpr int APPLY_LDS = PK + 3 * 256;
     constexpr int WAVE_LDS = PICK && 2 * kPickImg > APPLY_LDS ? 2 * kPickImg : APPLY_LDS;  // the pick phase's images alias
-    constexpr int NST = 7;                 // traj (6 rows), logdet; absent ones dropped by offset
+    constexpr int NST = RT ? 8 : 7;        // traj (6 rows), logdet (RT: sel_time); absent ones dropped by offset
     __shared__ __attribute__((aligned(16))) unsigned char lds[WAVES * WAVE_LDS];
     const int lane = int(threadIdx.x & 63);
     const int wave = WAVES == 1 ? 0 : wave_uniform(int(threadIdx.x >> 6));
@@ -2939,7 +2944,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     if (S > 0) {
         issue_picks(0);
         issue_picks(1);
-        issue_time(0);
+        if constexpr (!RT) issue_time(0);
         waitcnt<vmcnt_imm(0)>();
         gather(0, pick_row(0));
     }
@@ -2956,10 +2961,17 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
             __builtin_amdgcn_s_waitcnt(lgkmcnt0_imm);
             asm volatile("" ::: "memory");
             if (q + 1 < S) gather(q + 1, pick_row(q + 1));
+            // RT: the time is in record q (gather 0 is older than gather 1, when there is one)
+            if (RT && q == 0) {
+                if (S > 1) waitcnt<vmcnt_imm(NG)>();
+                else waitcnt<vmcnt_imm(0)>();
+            }
         }
-        const double tq = reinterpret_cast<const double*>(base + TM + (q & 1) * 512)[lane];
+        double tq;
+        if constexpr (RT) tq = pay[9];
+        else tq = reinterpret_cast<const double*>(base + TM + (q & 1) * 512)[lane];
         const uint32_t pick_c = pick_row(q);
-        issue_time(q + 1);
+        if constexpr (!RT) issue_time(q + 1);
         issue_picks(q + 2);  // into the slot row q - 1 held
         const bool live = q < nsel;
         const int code = int(pick_c >> 24);
@@ -2991,7 +3003,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
             // gather q: older than event q - 1's stores, time q + 1 and pick row q + 2
             if (q > 0) waitcnt<vmcnt_imm(NST + 2)>();
             else waitcnt<vmcnt_imm(2)>();
-        } else if (q == 0) {
+        } else if (!RT && q == 0) {
             // gather 0: older than gather 1 (when there is one), time 1 and pick row 2
             if (S > 1) waitcnt<vmcnt_imm(NG + 2)>();
             else waitcnt<vmcnt_imm(2)>();
@@ -3024,6 +3036,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
 #pragma unroll
         for (int k = 0; k < 6; ++k) stv(r_tr, uint32_t(k) * rb + vo, s.x[k]);
         stv(span_rsrc(a.logdet, q, rb, 1u), vo, s.logdet());
+        if constexpr (RT) stv(span_rsrc(a.sel_time, q, rb, 1u), vo, tq);
     }
     a.flags[f] = bad ? 1 : 0;
     if (bad) return;  // the fused kernel reruns this filter from the handle's state
@@ -3074,6 +3087,7 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
         if (a.one_launch && !rnd) {
             Ref15SchedArgs c = a;  // heaviest first by rate where the filters have their own rates
             c.order = nullptr;
+            c.rec_time = false;    // its pick phase's sel_time rows are its apply phase's times
             if (a.order && a.freq) {
                 ref15_rate_key_kernel<<<g4, 256, 0, stream>>>(a);
                 size_t tb = a.sort_tmp_bytes;
@@ -3105,7 +3119,8 @@ hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t
             }
             KF_CUSTOM_DISPATCH(a.kc, {
                 if (a.pay_rec) {  // payload records (kf_run_scheduled_rec): four-wave groups
-                    if (f64) ref15_apply_kernel<double, CUSTOM, 4, false, true><<<g4, 256, 0, stream>>>(a);
+                    if (f64 && a.rec_time) ref15_apply_kernel<double, CUSTOM, 4, false, true, true><<<g4, 256, 0, stream>>>(a);
+                    else if (f64) ref15_apply_kernel<double, CUSTOM, 4, false, true><<<g4, 256, 0, stream>>>(a);
                     else ref15_apply_kernel<float, CUSTOM, 4, false, true><<<g4, 256, 0, stream>>>(a);
                 } else
 #if KF_APPLY_IMAGES == 2

@@ -42,6 +42,7 @@ OPTIONS = {
     'sched_kernel': (_lib.KF_OPT_SCHED_KERNEL, {'auto': 0, 'regs': 1, 'fused': 2, 'two_pass': 3, 'one_launch': 4}),
     'sched_group': (_lib.KF_OPT_SCHED_GROUP, {'auto': 0, 'wave': 1, 'block': 4}),
     'sched_order': (_lib.KF_OPT_SCHED_ORDER, {'auto': 0, 'heaviest_first': 0, 'batch': 1}),
+    'sched_rec_time': (_lib.KF_OPT_SCHED_REC_TIME, {'auto': 0, 'off': 0, 'on': 1}),
 }
 
 

@@ -523,7 +523,7 @@ def test_scheduled_random_streams_vs_oracle(seed, B):
         assert _rel(ld[:n, f], rl[1:]) <= TOL, f
 
 
-@pytest.mark.parametrize('B,records', [(48, False), (128, False), (128, True)])
+@pytest.mark.parametrize('B,records', [(48, False), (128, False), (128, True), (128, 'time')])
 def test_scheduled_random_vs_oracle(B, records):
     """kf_run_scheduled_random (the random arm, kf_workers.py:826-957 with random_schedule
     :188-193) over random ragged streams with per-lane rates: each filter draws from its own
@@ -541,9 +541,13 @@ def test_scheduled_random_vs_oracle(B, records):
     x0 = np.zeros((15, B))
     x0[0:6] = rng.normal(0, 2, (6, B))
     Pblk = np.repeat(ref15.to_blocks(ref_kf.P0_REF15)[:, None], B, axis=1)
-    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    opts = {'sched_rec_time': 'on'} if records == 'time' else None   # rec[9] = the event's time
+    kf = kfmi.BatchedKF('ref15', B, 'f64', options=opts)
     kf.set_state(x0, Pblk)
     payload = _sched_records(pay, 12) if records else pay
+    if records == 'time':
+        payload[:, :, 9] = tt
+    records = bool(records)
     tr, ld, stt, ns, used = (v.cpu().numpy() for v in kf.run_scheduled_random(tt, etype, payload, np.full(B, t0),
                                                                                rates, words, records=records))
     kf.close()
@@ -570,7 +574,7 @@ def test_scheduled_random_vs_oracle(B, records):
         assert _rel(tr[:n, :, f], np.array([r[1:7] for r in rs[1:]])) <= TOL, f
         assert _rel(ld[:n, f], rl[1:]) <= TOL, f
     # too few outputs: the filter stops at its last completed pick and reports -1
-    kf = kfmi.BatchedKF('ref15', B, 'f64')
+    kf = kfmi.BatchedKF('ref15', B, 'f64', options=opts)
     kf.set_state(x0, Pblk)
     out = kf.run_scheduled_random(tt, etype, payload, np.full(B, t0), rates, words[:3], records=records)
     kf.close()
@@ -625,22 +629,31 @@ def test_sched_two_pass_matches_fused_kernels(r_gps, dtype, nan):
     rec_arms = {'rec_' + k: v for k, v in arms.items() if k != 'batch_order'}
     payt = pay.astype(np.float32) if dtype == 'f32' else pay
     recs = _sched_records(payt, 10 if dtype == 'f64' else 12)
+    # f64 records carrying the event's time at rec[9] (KF_OPT_SCHED_REC_TIME): the apply pass
+    # takes each pick's time from its record and writes sel_time itself
+    recs_t = None
+    if dtype == 'f64':
+        recs_t = _sched_records(payt, 12)
+        recs_t[:, :, 9] = tt
+        rec_arms.update({'rect_' + k: dict(v, sched_rec_time='on') for k, v in arms.items() if k != 'batch_order'})
     for kern, opts in {**arms, **rec_arms}.items():
         kf = kfmi.BatchedKF('ref15', B, dtype, params=params, options=opts)
-        if kern.startswith('rec_'):
-            res = kf.run_scheduled(tt, etype, recs, np.full(B, t0), rates, records=True)
+        if kern.startswith('rec'):
+            res = kf.run_scheduled(tt, etype, recs_t if kern.startswith('rect_') else recs, np.full(B, t0), rates,
+                                   records=True)
         else:
             res = kf.run_scheduled(tt, etype, payt, np.full(B, t0), rates)
         out[kern] = [v.cpu().numpy() for v in res] + [kf.status().cpu().numpy()]
         kf.close()
     for kern in rec_arms:  # the records change only where the values are read from: bitwise
-        for a, b in zip(out[kern[4:]], out[kern]):
+        base = kern.split('_', 1)[1]
+        for a, b in zip(out[base], out[kern]):
             if a.ndim == 1:
                 np.testing.assert_array_equal(a, b, err_msg=kern)
-        ns0 = out[kern[4:]][3]
+        ns0 = out[base][3]
         for f in range(B):
             n = int(ns0[f])
-            for a, b in zip(out[kern[4:]][:3], out[kern][:3]):
+            for a, b in zip(out[base][:3], out[kern][:3]):
                 np.testing.assert_array_equal(a[:n, ..., f], b[:n, ..., f], err_msg=kern)
     tr, ld, stt, ns, st = out['auto']
     assert ns.min() > 0
