@@ -532,7 +532,7 @@ def test_scheduled_random_vs_oracle(B, records):
     and log-dets, and reports exactly the outputs the oracle consumed.  B = 48: the fused kernel;
     B = 128: the pick and apply passes (payload rows and records).  A column too short for its
     filter's draws reports -1."""
-    rng = np.random.default_rng(60 + B + records)
+    rng = np.random.default_rng(60 + B + {False: 0, True: 1, 'time': 2}[records])
     T = 120
     t0, rates, etype, tt, pay = _sched_streams(rng, B, T)
     W = 2 * T + 64
