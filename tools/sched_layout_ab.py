@@ -1,7 +1,10 @@
 """In-process A/B of the sched row's payload layout: [T][9][B] rows (kf_run_scheduled) against
 [T][B][N] records (kf_run_scheduled_rec), on one set of streams, alternating launches.
 
-    python tools/sched_layout_ab.py [--arms rows,rec10,rec12] [--rounds 6] [--launches 10] [--rate-block 64]
+    python tools/sched_layout_ab.py [--arms rows,rec10,rec12,rec12t] [--rounds 6] [--launches 10] [--rate-block 64]
+
+recNt: N-double records whose rec[9] holds the event time, read by the apply pass
+(KF_OPT_SCHED_REC_TIME = 1).
 """
 import argparse
 import json
@@ -24,13 +27,13 @@ def main():
     import bench
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
-    cfg = dict(bench.CONFIGS['sched'])
-    cfg['opts'] = {}
     arms = {}
     for lay in args.arms.split(','):
+        cfg = dict(bench.CONFIGS['sched'])
+        cfg['opts'] = {'sched_rec_time': 1} if lay.endswith('t') else {}
         ns = argparse.Namespace(ablate='none', gpus=1, no_cpu_baseline=True, rate_block=args.rate_block,
                                 sched_payload='rows' if lay == 'rows' else 'records',
-                                sched_rec=0 if lay == 'rows' else int(lay[3:]))
+                                sched_rec=0 if lay == 'rows' else int(lay[3:].rstrip('t')))
         arms[lay] = bench.sched_workload(cfg, ns, 0, 1, dev)
     for lay, w in arms.items():
         w['step']()
