@@ -895,7 +895,7 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     const size_t rec_bytes = map_records ? align256(size_t(4 * vstride) * ntraj * w) + align256(sizeof(double) * n) : 0;
     const int64_t ntiles = (C + kfmi::kStreamScanTile - 1) / kfmi::kStreamScanTile;
     const size_t need = 256 + 2 * bank1 + bank4 + 2 * align256(sizeof(double) * 12 * nch * C) +
-                        align256(sizeof(double) * 15 * nch * ntiles) + align256(sizeof(double) * n * C) + lft_bytes +
+                        align256(sizeof(double) * 12 * nch * ntiles) + align256(sizeof(double) * n * C) + lft_bytes +
                         rec_bytes;
     if (!grow_ws(h, &h->stream_ws, &h->stream_ws_bytes, &h->stream_ws_graph, need, static_cast<hipStream_t>(stream)))
         return capturing(static_cast<hipStream_t>(stream))
@@ -932,8 +932,7 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     sa.pref = reinterpret_cast<double*>(p);
     p += align256(sizeof(double) * 12 * nch * C);
     sa.tiles = reinterpret_cast<double*>(p);
-    sa.tstart = sa.tiles + 12 * nch * ntiles;
-    p += align256(sizeof(double) * 15 * nch * ntiles);
+    p += align256(sizeof(double) * 12 * nch * ntiles);
     sa.starts = reinterpret_cast<double*>(p);
     p += align256(sizeof(double) * n * C);
     if (lft) {
@@ -1016,14 +1015,15 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
         // every variant's trajectory); the trajectories are then the affine maps' values at the
         // true chunk starts
         if (e == hipSuccess) e = chain(C, sa.mx, sa.mP, sa.mst, L, 0, true, traj ? traj4 : nullptr, 4, 4);
-        // the maps composed into the chunk starts, and the verdict
-        for (int ph = kfmi::kStreamPhaseScanTiles; ph <= kfmi::kStreamPhaseStarts && e == hipSuccess; ++ph)
-            e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
+        // the maps composed into the chunk starts (the tile scan, then the starts kernel, which
+        // composes the tile products itself), and the verdict
+        for (int ph : {kfmi::kStreamPhaseScanTiles, kfmi::kStreamPhaseStarts})
+            if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
         if (e == hipSuccess && traj) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseRecords, sa, st);
     } else {
         if (e == hipSuccess) e = chain(C, sa.mx, sa.mP, sa.mst, L, 0, false, nullptr, 1, 4);
-        for (int ph = kfmi::kStreamPhaseScanTiles; ph <= kfmi::kStreamPhaseStarts && e == hipSuccess; ++ph)
-            e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
+        for (int ph : {kfmi::kStreamPhaseScanTiles, kfmi::kStreamPhaseStarts})
+            if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
         if (e == hipSuccess) e = chain(C, sa.fx, sa.fP, sa.fst, L, 0, true);
         if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseFinish, sa, st);
     }

@@ -1194,41 +1194,33 @@ __global__ __launch_bounds__(kScanTile) void stream_scan_tiles_kernel(const Stre
     }
 }
 
-// phase 3: one block per chain
+// phase 4: grid (tiles, chains).  Each block first composes the products of the tiles before
+// its own (the scan's top phase, which was a launch of its own: every block redoes its prefix,
+// ntiles maps of 12 doubles, in rounds of kScanTile) into its tile start; the block of the last
+// tile also runs through its own product: the stream's end state.
 template <typename T, class M>
-__global__ __launch_bounds__(kScanTile) void stream_scan_top_kernel(const StreamArgs a) {
+__global__ __launch_bounds__(kScanTile) void stream_starts_kernel(const StreamArgs a) {
     constexpr int NCH = M::NP + M::NA;
     __shared__ double pre[12][kScanTile];
     __shared__ double carry[3];
     const int tid = int(threadIdx.x);
-    const int ch = int(blockIdx.x);
+    const int ch = int(blockIdx.y);
     const int ns = ch < M::NP ? 3 : 2;
-    const int64_t ntiles = (a.C + kScanTile - 1) / kScanTile;
+    const int64_t tile = blockIdx.x, c = tile * kScanTile + tid;
+    const int64_t ntiles = gridDim.x;
     if (tid < 3) carry[tid] = tid < ns ? double(static_cast<const T*>(a.hx)[chain_state<M>(ch, tid)]) : 0.0;
-    for (int64_t r0 = 0; r0 < ntiles; r0 += kScanTile) {
+    for (int64_t r0 = 0; r0 < tile; r0 += kScanTile) {
         const int64_t t = r0 + tid;
         double v[12];
-        if (t < ntiles) {
+        if (t < tile) {
 #pragma unroll
             for (int e = 0; e < 12; ++e) v[e] = a.tiles[(t * NCH + ch) * 12 + e];
         } else {
             affine_identity(v);
         }
-        __syncthreads();  // the previous round's readers of pre / carry are done
+        __syncthreads();  // carry written (the previous round / the init), pre free
         block_scan_affine(v, pre, tid);
-        double x[3] = {carry[0], carry[1], carry[2]};
-        if (tid > 0) {
-            double e1[12];
-#pragma unroll
-            for (int e = 0; e < 12; ++e) e1[e] = pre[e][tid - 1];
-            apply_map(x, e1);
-        }
-        if (t < ntiles) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) a.tstart[(t * NCH + ch) * 3 + k] = x[k];
-        }
-        __syncthreads();  // every thread has read carry
-        if (tid == kScanTile - 1) {  // past the round (identity maps past the last tile)
+        if (tid == kScanTile - 1) {  // the round's product (identity maps past `tile`)
             double xe[3] = {carry[0], carry[1], carry[2]};
             apply_map(xe, v);
 #pragma unroll
@@ -1236,31 +1228,23 @@ __global__ __launch_bounds__(kScanTile) void stream_scan_top_kernel(const Stream
         }
     }
     __syncthreads();
-    if (tid == 0 && a.xend) {  // the stream's end state
-        bool fin = true;
+    bool fin = true;
+    if (a.xend && tile == ntiles - 1 && tid == 0) {  // the stream's end state
+        double xe[3] = {carry[0], carry[1], carry[2]}, tp[12];
+#pragma unroll
+        for (int e = 0; e < 12; ++e) tp[e] = a.tiles[(tile * NCH + ch) * 12 + e];
+        apply_map(xe, tp);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             if (k >= ns) continue;
-            a.xend[chain_state<M>(ch, k)] = carry[k];
-            fin = fin && (carry[k] - carry[k] == 0.0);
+            // read by the verdict's block (maybe on another XCD): a device-scope atomic
+            atomicExch(reinterpret_cast<unsigned long long*>(&a.xend[chain_state<M>(ch, k)]),
+                       static_cast<unsigned long long>(__double_as_longlong(xe[k])));
+            fin = fin && (xe[k] - xe[k] == 0.0);
         }
-        if (!fin) atomicOr(&a.check->bad, kStreamBadStart);
     }
-}
-
-// phase 4: grid (tiles, chains)
-template <typename T, class M>
-__global__ __launch_bounds__(kScanTile) void stream_starts_kernel(const StreamArgs a) {
-    constexpr int NCH = M::NP + M::NA;
-    const int tid = int(threadIdx.x);
-    const int ch = int(blockIdx.y);
-    const int ns = ch < M::NP ? 3 : 2;
-    const int64_t tile = blockIdx.x, c = tile * kScanTile + tid;
-    bool fin = true;
     if (c < a.C) {
-        double x[3], e1[12];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) x[k] = a.tstart[(tile * NCH + ch) * 3 + k];
+        double x[3] = {carry[0], carry[1], carry[2]}, e1[12];
 #pragma unroll
         for (int e = 0; e < 12; ++e) e1[e] = a.pref[(c * NCH + ch) * 12 + e];
         apply_map(x, e1);
@@ -1302,7 +1286,9 @@ __global__ __launch_bounds__(kScanTile) void stream_starts_kernel(const StreamAr
     k->ok = ok ? 1 : 0;
     if (ok) {
         const int64_t col = a.C - 1, B4 = 4 * a.C;  // the last chunk's end covariance
-        for (int i = 0; i < M::N; ++i) static_cast<T*>(a.hx)[i] = T(a.xend[i]);
+        for (int i = 0; i < M::N; ++i)  // written by the last tile's block (a device-scope atomic)
+            static_cast<T*>(a.hx)[i] = T(__longlong_as_double(static_cast<long long>(
+                atomicOr(reinterpret_cast<unsigned long long*>(&a.xend[i]), 0ull))));
         for (int r = 0; r < M::NBLK; ++r) static_cast<T*>(a.hP)[r] = static_cast<const T*>(a.mP)[r * B4 + col];
         a.hstatus[0] = 0;
     }
@@ -3224,7 +3210,6 @@ void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
             stream_scan_tiles_kernel<T, M><<<g, kScanTile, 0, stream>>>(a);
             break;
         }
-        case kStreamPhaseScanTop: stream_scan_top_kernel<T, M><<<NCH, kScanTile, 0, stream>>>(a); break;
         case kStreamPhaseStarts: {
             const dim3 g(unsigned((a.C + kScanTile - 1) / kScanTile), NCH);
             stream_starts_kernel<T, M><<<g, kScanTile, 0, stream>>>(a);
