@@ -1390,24 +1390,33 @@ __device__ __forceinline__ void lft_event(double (&v)[6], int type, double dt, b
     }
 }
 
+// kLftHalves lanes per (chunk piece, chain), each carrying 6 / kLftHalves columns of the 6x6
+// product: the columns are independent, so the split doubles the waves of this latency-bound
+// pass (0.75 wave per SIMD at 8192 chunks with all six columns in one lane) at the cost of
+// paying an event's type / dt handling twice
+#ifndef KF_LFT_HALVES
+#define KF_LFT_HALVES 2
+#endif
+constexpr int kLftHalves = KF_LFT_HALVES;
+static_assert(6 % kLftHalves == 0, "columns per lane");
 template <typename T, class M, bool CUSTOM>
 __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArgs a) {
     constexpr int NCH = M::NP + M::NA;
-    // one lane per (chunk piece, chain), carrying all six columns of the 6x6 product: an event's
-    // type / dt handling is paid once for the six columns (the round-1 kernel ran one column per
-    // lane of an 8-lane group, two lanes idle)
-    const int64_t grp = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (grp >= a.C * a.np * NCH) return;
+    constexpr int NJ = 6 / kLftHalves;  // columns per lane
+    const int64_t gl = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (gl >= a.C * a.np * NCH * kLftHalves) return;
+    const int64_t grp = gl / kLftHalves;  // (chunk * np + piece) * NCH + chain
+    const int j0 = int(gl % kLftHalves) * NJ;
     const int64_t cp = grp / NCH;  // chunk * np + piece
     const int ch = int(grp % NCH);
     const bool pva = ch < M::NP;
     double q[3], si[3], sg;
     chain_noise<M, CUSTOM>(ch, q, si, sg, a.kc);
-    double v[6][6];  // v[j] = column j
+    double v[NJ][6];  // v[j] = column j0 + j
 #pragma unroll
-    for (int j = 0; j < 6; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int i = 0; i < 6; ++i) v[j][i] = i == j ? 1.0 : 0.0;
+        for (int i = 0; i < 6; ++i) v[j][i] = i == j0 + j ? 1.0 : 0.0;
     const int64_t c = cp / a.np, piece = cp % a.np;
     const int64_t cend = (c + 1) * a.L < a.S ? (c + 1) * a.L : a.S;
     const int64_t e0 = c * a.L + piece * a.lp, e1 = e0 + a.lp < cend ? e0 + a.lp : cend;
@@ -1436,18 +1445,21 @@ __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArg
 #pragma unroll
         for (int k = 0; k < kB; ++k)
 #pragma unroll
-            for (int j = 0; j < 6; ++j) lft_event<M>(v[j], ty[k], dv[k], pva, q, si, sg);
+            for (int j = 0; j < NJ; ++j) lft_event<M>(v[j], ty[k], dv[k], pva, q, si, sg);
         if (((e - e0) & 15) == kB) {  // every 16 events: rescale by a power of two (the max)
+            // of all six columns: the lanes of one product exchange their maxima (adjacent lanes)
             double mx = 0.0;
 #pragma unroll
-            for (int j = 0; j < 6; ++j)
+            for (int j = 0; j < NJ; ++j)
 #pragma unroll
                 for (int i = 0; i < 6; ++i) mx = fmax(mx, fabs(v[j][i]));
+#pragma unroll
+            for (int sh = 1; sh < kLftHalves; sh <<= 1) mx = fmax(mx, __shfl_xor(mx, sh, 64));
             int ex;
             (void)frexp(mx, &ex);
             const double sc = ldexp(1.0, -ex);
 #pragma unroll
-            for (int j = 0; j < 6; ++j)
+            for (int j = 0; j < NJ; ++j)
 #pragma unroll
                 for (int i = 0; i < 6; ++i) v[j][i] *= sc;
         }
@@ -1456,7 +1468,7 @@ __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArg
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
-        for (int j = 0; j < 6; ++j) o[i * 6 + j] = v[j][i];
+        for (int j = 0; j < NJ; ++j) o[i * 6 + j0 + j] = v[j][i];
 }
 
 // a chain's block of the block-packed covariance as a full 3x3 (the inert state: variance 1)
@@ -3216,8 +3228,8 @@ void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
             break;
         }
         case kStreamPhaseLftMaps:
-            if (a.kc) stream_lft_maps_kernel<T, M, true><<<grid(a.C * a.np * NCH), kBlock, 0, stream>>>(a);
-            else stream_lft_maps_kernel<T, M, false><<<grid(a.C * a.np * NCH), kBlock, 0, stream>>>(a);
+            if (a.kc) stream_lft_maps_kernel<T, M, true><<<grid(a.C * a.np * NCH * kLftHalves), kBlock, 0, stream>>>(a);
+            else stream_lft_maps_kernel<T, M, false><<<grid(a.C * a.np * NCH * kLftHalves), kBlock, 0, stream>>>(a);
             break;
         case kStreamPhaseLftStart: {
             const int64_t bc = a.g > 0 ? a.G : kBlock;
