@@ -145,6 +145,8 @@ const char* kf_version(void);
  *   KF_OPT_START_THREADS  kf_run_stream: threads per block of the start kernel; 0 = 256
  *   KF_OPT_SEARCH_KERNEL  kf_search_combos: 0 = per level, 1 = child-major, 2 = parent-major
  *   KF_OPT_SEARCH_PM      kf_search_combos' parent-major kernel: 0 = parent in LDS, 1 = registers
+ *   KF_OPT_SEARCH_HEAD    kf_search_combos: 0 = the first levels (sizes whose subsets need few event
+ *                         steps in all) in one launch, one lane per subset; 1 = level by level
  *   KF_OPT_SCHED_KERNEL   kf_run_scheduled: 0 = auto (the two passes where legal, as 3), 1 = the
  *                         fused register-input kernel, 2 = the fused LDS-input kernel, 3 = the
  *                         pick and apply passes as two launches, 4 = as the two phases of one
@@ -175,7 +177,8 @@ const char* kf_version(void);
 #define KF_OPT_SCHED_GROUP    12
 #define KF_OPT_SCHED_ORDER    13
 #define KF_OPT_SCHED_REC_TIME 14
-#define KF_OPT_COUNT          15
+#define KF_OPT_SEARCH_HEAD    15
+#define KF_OPT_COUNT          16
 int kf_set_option(kf_batch* handle, int option, int64_t value);
 int kf_get_option(const kf_batch* handle, int option, int64_t* value);
 

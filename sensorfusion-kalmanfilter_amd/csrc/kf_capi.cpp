@@ -100,6 +100,9 @@ constexpr size_t kWsBinom = sizeof(uint64_t) * (kMaxComboEvents + 1) * (kMaxComb
 constexpr size_t kWsInit = sizeof(double) * 42;
 // levels with at most this many parents run child-major (see search_child_major)
 constexpr uint64_t kSearchChildMajorParents = 200000;
+// the search's head launch covers the sizes whose subsets' event steps from the root add up to at
+// most this many (n = 25: sizes 1 .. 5, 323,775 steps for 68,405 subsets)
+constexpr uint64_t kSearchHeadSteps = 400000;
 
 int64_t opt(const kf_batch* h, int o) { return h->opt[o]; }
 
@@ -353,7 +356,8 @@ int kf_set_option(kf_batch* h, int option, int64_t value) {
         case KF_OPT_PREDICT:
         case KF_OPT_STREAM:
         case KF_OPT_STREAM_FINAL:
-        case KF_OPT_SEARCH_PM: ok = value == 0 || value == 1; break;
+        case KF_OPT_SEARCH_PM:
+        case KF_OPT_SEARCH_HEAD: ok = value == 0 || value == 1; break;
         case KF_OPT_SCHED_KERNEL: ok = value >= 0 && value <= 4; break;
         case KF_OPT_SCHED_GROUP: ok = value == 0 || value == 1 || value == 4; break;
         case KF_OPT_SCHED_ORDER:
@@ -1140,7 +1144,55 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
     char* lv[2] = {sw + head, sw + head + level};
     uint64_t best[kMaxComboEvents + 1] = {}, acc[kMaxComboEvents + 1] = {};
     int found = 0, last = 0;
-    for (int k = 1; k <= kf_max; ++k) {
+    // the head: levels 1 .. K in one launch, one lane per subset (launch_ref15_search_head), K the
+    // largest size whose subsets' event steps from the root (sum_k k C(n, k)) stay within
+    // kSearchHeadSteps, at least 2 and below kf_max (level K + 1 reads its stored nodes)
+    int K = 0;
+    if (opt(h, KF_OPT_SEARCH_HEAD) == 0 && n >= 5) {
+        uint64_t steps = 0;
+        for (int k = 1; k <= n - 2 && k < kf_max; ++k) {
+            steps += uint64_t(k) * C(n, k);
+            if (steps > kSearchHeadSteps) break;
+            K = k;
+        }
+        if (K < 2) K = 0;
+    }
+    int k_first = 1;
+    if (K) {
+        kfmi::Ref15SearchArgs a{};
+        a.kc = h->kc;
+        a.n_events = n;
+        a.k = K;
+        a.shift = n_fixed;
+        a.k_base = k_base;
+        a.root_mask = fixed_mask;
+        a.ev_all = reinterpret_cast<const double*>(ws);
+        for (int k = 1; k <= K; ++k) a.n_child += C(n, k);
+        a.ev = reinterpret_cast<const double*>(ws) + 11 * n_fixed;
+        a.binom = reinterpret_cast<const uint64_t*>(ws + kWsEvents);
+        a.binom_host = binom;
+        a.init = reinterpret_cast<const double*>(ws + kWsEvents + kWsBinom);
+        a.prev_time = prev_time;
+        a.target_end = target_end;
+        a.threshold = threshold;
+        a.child = lv[K & 1];
+        a.best = d_best;
+        a.n_acc = d_acc;
+        a.subset_max = subset_max;
+        a.tail = 1;
+        e = kfmi::launch_ref15_search_head(h->dtype == KF_F64, a, st);
+        if (e != hipSuccess) return hip_fail(e, "kf_search_combos: head launch");
+        last = k_base + K;
+        k_first = K + 1;
+        if (!exhaustive) {  // any acceptable subset of sizes k_base .. k_base + K ends the search
+            e = hipMemcpyAsync(&best[k_base], &d_best[k_base], sizeof(uint64_t) * (K + 1), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return hip_fail(e, "kf_search_combos: head result");
+            for (int k = k_base; k <= last; ++k)
+                if (best[k]) k_first = kf_max + 1;
+        }
+    }
+    for (int k = k_first; k <= kf_max; ++k) {
         kfmi::Ref15SearchArgs a{};
         a.kc = h->kc;
         a.n_events = n;

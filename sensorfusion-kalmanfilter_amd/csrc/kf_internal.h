@@ -327,6 +327,8 @@ hipError_t launch_ref_reset(int model, bool f64, const RefArgs& a, hipStream_t s
 hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream);
 // child_major: one wave per (parent block, child event) instead of one lane per parent
 hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream);
+// levels 1 .. a.k of a search in one launch (one lane per subset of at most a.k free events)
+hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStream_t stream);
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream);
 hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream);
 // descending stable radix sort of n (key, value) pairs on the key's low `bits` bits (kf_ingest.hip,

@@ -2229,6 +2229,127 @@ ref15_search_pm_kernel(const Ref15SearchArgs a) {
     if (a.tail) search_publish(a, a.k + 1, best1, cnt1);
 }
 
+// The head of the search: levels 1 .. K (a.k = K) in ONE launch, one lane per subset of at most
+// K free candidates — lanes in (size, colex rank) order — each run from the root through its
+// events in index order with the level kernels' per-chain operations, so every score and every
+// stored node is the level search's, bit for bit.  It replaces K launches whose first few hold a
+// few dozen to a few thousand subsets each and sit at a launch-and-one-event floor of ~10 us
+// (DESIGN.md §3).  Level K's subsets whose largest candidate is <= n - 3 are stored as level
+// K + 1's parents; one whose largest is n - 2 also scores its child with n - 1 (the tail).
+// a.n_child = sum_{k <= K} C(n, k).  Every lane stays to the end (the publish reductions read
+// every lane).
+template <typename T, bool CUSTOM>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void ref15_search_head_kernel(
+    const Ref15SearchArgs a) {
+    const int n = a.n_events, K = a.k;
+    const uint64_t* C = a.binom;
+    auto binom = [&](int x, int y) -> uint64_t { return C[x * (kMaxEvents + 1) + y]; };
+    const uint64_t g = uint64_t(blockIdx.x) * 64 + threadIdx.x;
+    const bool live = g < a.n_child;
+    int k = 1;
+    uint64_t r = live ? g : 0;
+    while (k < K && r >= binom(n, k)) {
+        r -= binom(n, k);
+        ++k;
+    }
+    // colex unranking: rank r = sum_i C(c_i, i) over the sorted members c_1 < ... < c_k
+    uint64_t sub = 0;
+    {
+        uint64_t rr = r;
+        int c = n - 1;
+        for (int i = k; i >= 1; --i) {
+            while (binom(c, i) > rr) --c;
+            rr -= binom(c, i);
+            sub |= uint64_t(1) << c;
+            --c;
+        }
+    }
+    uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0;
+    SearchNode<T, CUSTOM> nd;
+    {
+        uint64_t rb = 0, rc = 0;  // a fixed root is itself one of the subsets searched (lane 0 scores it)
+        const bool eval = a.root_mask != 0 && g == 0;
+        const T f = nd.root(a, eval);
+        if (eval) search_score(a, a.root_mask, f, rb, rc);
+        search_publish(a, 0, rb, rc);
+    }
+    T fmax = nd.run;
+#pragma unroll 1
+    for (uint64_t m = sub; m; m &= m - 1) {
+        const int j = __builtin_ctzll(m);
+        SearchEvent vs = search_event(a, j, nd.prev);
+        vs.final_predict = vs.final_predict && (m & (m - 1)) == 0;  // only the subset itself is scored
+        SearchScore<T, CUSTOM> ss;
+        ss.kc = a.kc;
+#pragma unroll
+        for (int ch = 0; ch < M15::NP; ++ch) {
+            T Pb[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) Pb[i] = nd.P[6 * ch + i];
+            search_pva<T, CUSTOM>(vs, ch, Pb, ss.ok, a.kc);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) nd.P[6 * ch + i] = Pb[i];
+            ss.add_pva(vs, Pb, ch);
+        }
+#pragma unroll
+        for (int ch = 0; ch < M15::NA; ++ch) {
+            T Pa[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) Pa[i] = nd.P[6 * M15::NP + 3 * ch + i];
+            search_aw<T, CUSTOM>(vs, ch, Pa, ss.ok, a.kc);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) nd.P[6 * M15::NP + 3 * ch + i] = Pa[i];
+            ss.add_aw(vs, Pa, ch);
+        }
+        nd.run = ss.finish(vs, nd.run, fmax);
+        nd.prev = vs.prev;
+        nd.mask |= uint64_t(1) << (j + a.shift);
+    }
+    const int top = sub ? 63 - __builtin_clzll(sub) : -1;
+    if (live) {
+        search_score(a, nd.mask, fmax, best, cnt);
+        if (k == K && a.child && top <= n - 3) {  // level K + 1's parent, at its colex rank
+            char* cb = level_block<T>(a.child, r);
+            const uint32_t cl = uint32_t(r) & 63u;
+#pragma unroll
+            for (int i = 0; i < 27; ++i) *level_row<T>(cb, cl, i) = nd.P[i];
+            *level_row<T>(cb, cl, 27) = nd.run;
+            *level_tail<T>(cb, cl, 0) = nd.prev;
+            *level_tail<T>(cb, cl, 1) = __builtin_bit_cast(double, nd.mask);
+        }
+        if (k == K && a.tail && top == n - 2) {  // its only child, plus event n - 1 (size K + 1)
+            const SearchEvent vg = search_event(a, n - 1, nd.prev);
+            SearchScore<T, CUSTOM> sg;
+            sg.kc = a.kc;
+#pragma unroll
+            for (int ch = 0; ch < M15::NP; ++ch) {
+                T Pb[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) Pb[i] = nd.P[6 * ch + i];
+                search_pva<T, CUSTOM>(vg, ch, Pb, sg.ok, a.kc);
+                sg.add_pva(vg, Pb, ch);
+            }
+#pragma unroll
+            for (int ch = 0; ch < M15::NA; ++ch) {
+                T Pa[3];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) Pa[i] = nd.P[6 * M15::NP + 3 * ch + i];
+                search_aw<T, CUSTOM>(vg, ch, Pa, sg.ok, a.kc);
+                sg.add_aw(vg, Pa, ch);
+            }
+            T gmax;
+            (void)sg.finish(vg, nd.run, gmax);
+            search_score(a, nd.mask | (uint64_t(1) << (n - 1 + a.shift)), gmax, best1, cnt1);
+        }
+    }
+    // per size: a wave holds lanes of at most a few consecutive sizes
+#pragma unroll 1
+    for (int kk = 1; kk <= K; ++kk)
+        if (__builtin_amdgcn_ballot_w64(live && k == kk) != 0)
+            search_publish(a, kk, k == kk ? best : 0, k == kk ? cnt : 0);
+    if (a.tail) search_publish(a, K + 1, best1, cnt1);
+}
+
 // Child-major: one wave per (parent block of 64, child event) work item, one child per lane,
 // so no lane walks a long list of children (the narrow levels, where few parents have many
 // children each).  Items are ordered by parent block, then j, and dealt to the XCDs in
@@ -3290,6 +3411,18 @@ hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t st
     return hipGetLastError();
 }
 
+
+hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStream_t stream) {
+    if (a.n_events > kMaxEvents || a.n_events < 3 || a.k < 1 || a.k > a.n_events - 2 || a.n_child == 0 ||
+        a.n_child >= (1ull << 31))
+        return hipErrorInvalidValue;
+    const dim3 grid(unsigned((a.n_child + 63) / 64));
+    KF_CUSTOM_DISPATCH(a.kc, {
+        if (f64) ref15_search_head_kernel<double, CUSTOM><<<grid, 64, 0, stream>>>(a);
+        else ref15_search_head_kernel<float, CUSTOM><<<grid, 64, 0, stream>>>(a);
+    });
+    return hipGetLastError();
+}
 
 hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream) {
     // node offsets are 32-bit byte offsets (buffer voffset)

@@ -52,7 +52,8 @@ KF_OPT_SCHED_KERNEL = 11
 KF_OPT_SCHED_GROUP = 12
 KF_OPT_SCHED_ORDER = 13
 KF_OPT_SCHED_REC_TIME = 14
-KF_OPT_COUNT = 15
+KF_OPT_SEARCH_HEAD = 15
+KF_OPT_COUNT = 16
 
 _ERRNAMES = {KF_EINVAL: 'KF_EINVAL', KF_EHIP: 'KF_EHIP', KF_ENOTSPD: 'KF_ENOTSPD',
              KF_ENODEV: 'KF_ENODEV', KF_ENOMEM: 'KF_ENOMEM'}

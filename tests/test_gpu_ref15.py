@@ -119,15 +119,17 @@ def _search_case(golden_dir, n, swap=True):
     return cand, ev, init, st[-1][0], target
 
 
+@pytest.mark.parametrize('head', ['on', 'off'])
 @pytest.mark.parametrize('kernel', ['cm', 'pm'])
 @pytest.mark.parametrize('dtype', ['f64', 'f32'])
-def test_search_subset_max_equals_eval_combos(golden_dir, dtype, kernel):
+def test_search_subset_max_equals_eval_combos(golden_dir, dtype, kernel, head):
     """kf_search_combos (one event step per subset, from the stored prefix) gives every subset the
     max log-det the per-subset kernel gives (same operations in the same order), with either
-    search kernel (child-major / parent-major levels)."""
+    search kernel (child-major / parent-major levels), with the first levels in the one-launch
+    head (KF_OPT_SEARCH_HEAD) or level by level."""
     n = 12
     cand, ev, init, t0, target = _search_case(golden_dir, n)
-    kf = kfmi.BatchedKF('ref15', 1, dtype, options={'search_kernel': kernel})
+    kf = kfmi.BatchedKF('ref15', 1, dtype, options={'search_kernel': kernel, 'search_head': head})
     kfound, win, acc, sm = kf.search_combos(ev, init, t0, target, threshold=-1e30, exhaustive=True, subset_max=True)
     kf.close()
     assert kfound == 0 and win is None and int(acc.sum()) == 0
@@ -193,14 +195,15 @@ def test_combo_inputs_reused_and_refreshed(golden_dir):
     kc.close()
 
 
+@pytest.mark.parametrize('head', ['on', 'off'])
 @pytest.mark.parametrize('kernel', ['cm', 'pm'])
-@pytest.mark.parametrize('n,k_max', [(1, 1), (2, 2), (3, 3), (4, 4), (9, 3), (9, 8), (9, 9)])
-def test_search_small_and_cut_levels(golden_dir, n, k_max, kernel):
+@pytest.mark.parametrize('n,k_max', [(1, 1), (2, 2), (3, 3), (4, 4), (5, 5), (9, 3), (9, 8), (9, 9)])
+def test_search_small_and_cut_levels(golden_dir, n, k_max, kernel, head):
     """Edge cases of the stored levels: with n <= 3 some levels have no stored parents (scored
     whole by the previous launch's tail); with k_max < n no subset larger than k_max is scored
     (the tail stops at k_max).  Every subset up to k_max gets the per-subset kernel's score."""
     cand, ev, init, t0, target = _search_case(golden_dir, n, swap=n > 6)
-    kf = kfmi.BatchedKF('ref15', 1, 'f64', options={'search_kernel': kernel})
+    kf = kfmi.BatchedKF('ref15', 1, 'f64', options={'search_kernel': kernel, 'search_head': head})
     kfound, win, acc, sm = kf.search_combos(ev, init, t0, target, threshold=-1e30, k_max=k_max, exhaustive=True,
                                             subset_max=True)
     kf.close()
@@ -218,15 +221,16 @@ def test_search_small_and_cut_levels(golden_dir, n, k_max, kernel):
         assert np.max(np.abs(got - mx) / np.maximum(np.abs(mx), 1.0)) <= 1e-12, k
 
 
+@pytest.mark.parametrize('head', ['on', 'off'])
 @pytest.mark.parametrize('kernel', ['cm', 'pm'])
 @pytest.mark.parametrize('q', [0.0, 0.01, 0.3, 0.9])
-def test_search_winner_matches_per_subset_search(golden_dir, q, kernel):
+def test_search_winner_matches_per_subset_search(golden_dir, q, kernel, head):
     """The search's winner and per-size accepted counts at thresholds across the distribution of
     subset scores equal the per-subset kernel's (first acceptable subset in itertools order of
     the smallest size)."""
     n = 11
     cand, ev, init, t0, target = _search_case(golden_dir, n)
-    kf = kfmi.BatchedKF('ref15', 1, 'f64', options={'search_kernel': kernel})
+    kf = kfmi.BatchedKF('ref15', 1, 'f64', options={'search_kernel': kernel, 'search_head': head})
     _, _, _, sm = kf.search_combos(ev, init, t0, target, threshold=-1e30, exhaustive=True, subset_max=True)
     vals = np.sort(sm.cpu().numpy()[1:])
     thr = float(vals[int(q * (len(vals) - 1))]) + (1e-9 if q > 0 else -1.0)
@@ -247,6 +251,32 @@ def test_search_winner_matches_per_subset_search(golden_dir, q, kernel):
     assert (kfound, win) == (want_k, want_combo)
     if q == 0.0:
         assert kfound == 0
+
+
+@pytest.mark.parametrize('n_fixed,fixed_mask', [(0, 0), (3, 0b101)])
+def test_search_head_equals_level_search(golden_dir, n_fixed, fixed_mask):
+    """The one-launch head (levels 1 .. K, one lane per subset from the root) and the level-by-level
+    search give every subset the same max log-det, bit for bit, the same acceptance counts per
+    size and the same winner, exhaustive and not, also on a class of a sharded search (fixed
+    candidates); n = 18 (the head covers sizes 1 .. 7 there, the level kernels the rest)."""
+    n = 18
+    cand, ev, init, t0, target = _search_case(golden_dir, n)
+    out = {}
+    for head in ('on', 'off'):
+        kf = kfmi.BatchedKF('ref15', 1, 'f64', options={'search_head': head})
+        _, _, _, sm = kf.search_combos(ev, init, t0, target, -1e30, exhaustive=True, subset_max=True,
+                                       n_fixed=n_fixed, fixed_mask=fixed_mask)
+        sm = sm.cpu().numpy()
+        vals = np.sort(sm[np.isfinite(sm)])
+        thr = float(vals[len(vals) // 50]) + 1e-9
+        ex = kf.search_combos(ev, init, t0, target, thr, exhaustive=True, n_fixed=n_fixed, fixed_mask=fixed_mask)
+        first = kf.search_combos(ev, init, t0, target, thr, exhaustive=False, n_fixed=n_fixed, fixed_mask=fixed_mask)
+        kf.close()
+        out[head] = (sm, ex, first)
+    a, b = out['on'], out['off']
+    np.testing.assert_array_equal(a[0], b[0])
+    assert a[1][:2] == b[1][:2] and a[2][:2] == b[2][:2] and a[1][0] > 0
+    np.testing.assert_array_equal(a[1][2], b[1][2])
 
 
 @pytest.mark.parametrize('w', [1, 3])
