@@ -441,6 +441,17 @@ int kf_run_scheduled_random(kf_batch* handle, int T, const double* t, const uint
                             const uint32_t* words, int n_words, int32_t* words_used, void* traj, void* logdet,
                             double* sel_time, int32_t* n_sel, void* stream);
 
+/* The random arm's picks alone: the same windows and draws as kf_run_scheduled_random (they need
+ * no filter state), no filter run.  pick device [T][B] int32: the picked events' indices (the
+ * first n_sel[f] rows of filter f), sel_time [T][B] their times, words_used as above.  Run the
+ * picked events through kf_run_events (dt = sel_time[s] - sel_time[s - 1], the first from
+ * prev_time): for ONE filter over a long log that is kf_run_events' time-parallel route, which
+ * is what kfmi.ref15.run_kalman_filter_scheduled does for the reference's one filter.  Any
+ * model's handle (only its batch size is used). */
+int kf_sched_random_picks(kf_batch* handle, int T, const double* t, const uint8_t* etype, const double* prev_time,
+                          const double* freq, double freq_all, const uint32_t* words, int n_words, int32_t* words_used,
+                          int32_t* pick, double* sel_time, int32_t* n_sel, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Ingest: CSV logs -> one merged event stream in HBM (the reference's load_data,
  * gps_to_modified_utm, compute_imu_biases, unbias_imu_data, combine_sensor_data;

@@ -1413,6 +1413,32 @@ int kf_run_scheduled_rec(kf_batch* h, int T, const double* t, const uint8_t* ety
                          logdet, sel_time, n_sel, stream);
 }
 
+int kf_sched_random_picks(kf_batch* h, int T, const double* t, const uint8_t* etype, const double* prev_time,
+                          const double* freq, double freq_all, const uint32_t* words, int n_words, int32_t* words_used,
+                          int32_t* pick, double* sel_time, int32_t* n_sel, void* stream) {
+    if (int rc = check_handle(h)) return rc;
+    if (T < 0) return fail(KF_EINVAL, "kf_sched_random_picks: T = %d < 0", T);
+    if (!freq && !(freq_all > 0.0)) return fail(KF_EINVAL, "kf_sched_random_picks: processing frequency must be > 0");
+    if (h->B == 0) return KF_OK;
+    if (!t || !etype || !prev_time || !words || n_words < 0 || !words_used || !pick || !sel_time || !n_sel)
+        return fail(KF_EINVAL, "kf_sched_random_picks: null stream or output");
+    kfmi::Ref15SchedArgs a{};
+    a.B = h->B;
+    a.T = T;
+    a.t = t;
+    a.etype = etype;
+    a.prev_time = prev_time;
+    a.freq = freq;
+    a.freq_all = freq_all;
+    a.sel_time = sel_time;
+    a.n_sel = n_sel;
+    a.words = words;
+    a.n_words = n_words;
+    a.words_used = words_used;
+    hipError_t e = kfmi::launch_ref15_random_picks(a, pick, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? KF_OK : hip_fail(e, "kf_sched_random_picks");
+}
+
 int kf_run_scheduled_random(kf_batch* h, int T, const double* t, const uint8_t* etype, const void* payload,
                             int rec_len, const double* prev_time, const double* freq, double freq_all,
                             const uint32_t* words, int n_words, int32_t* words_used, void* traj, void* logdet,

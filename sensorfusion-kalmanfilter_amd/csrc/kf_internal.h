@@ -331,6 +331,8 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
 hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStream_t stream);
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream);
 hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream);
+// random_schedule's picks only (a.words): pick [T][B] event indices, a.sel_time, a.n_sel, a.words_used
+hipError_t launch_ref15_random_picks(const Ref15SchedArgs& a, int32_t* pick, hipStream_t stream);
 // descending stable radix sort of n (key, value) pairs on the key's low `bits` bits (kf_ingest.hip,
 // hipCUB); tmp == nullptr: *tmp_bytes = the scratch it needs
 hipError_t sort_pairs_desc_u32(void* tmp, size_t* tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,

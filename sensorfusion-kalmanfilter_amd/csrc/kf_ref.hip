@@ -2655,6 +2655,73 @@ struct SchedLane {
     }
 };
 
+// random_schedule's picks alone (kf_sched_random_picks): the windows and the draws need only the
+// event times and types (the windows open at the picked events' times, the draws consume the
+// filter's generator outputs), so a lane per filter walks its stream with no filter arithmetic
+// and writes the picked event indices and times; the caller runs the picked events through the
+// event engine (for one filter over a long log: kf_run_events' time-parallel route).  Event
+// types and times ride an 8-deep register ring; the generator outputs a 4-deep one.
+template <int D>
+__device__ __forceinline__ void ring_shift(int (&ty)[D], double (&tt)[D]) {
+#pragma unroll
+    for (int k = 0; k + 1 < D; ++k) {
+        ty[k] = ty[k + 1];
+        tt[k] = tt[k + 1];
+    }
+}
+__global__ __launch_bounds__(kBlock) void ref15_random_picks_kernel(const Ref15SchedArgs a, int32_t* pick) {
+    const int64_t f = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (f >= a.B) return;
+    const int64_t B = a.B;
+    constexpr int D = 8;
+    int ty[D];
+    double tt[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        ty[k] = k < a.T ? int(a.etype[int64_t(k) * B + f]) : 255;
+        tt[k] = k < a.T ? a.t[int64_t(k) * B + f] : 0.0;
+    }
+    double prev = a.prev_time[f];
+    const double period = 1.0 / (a.freq ? a.freq[f] : a.freq_all);  // kf_workers.py:880
+    int q_len = 0, q_first = 0, nsel = 0, wp = 0;
+    bool q_gap = false;  // a padding event inside the queue: the r-th queued event needs a scan
+    for (int i = 0; i < a.T; ++i) {
+        const int ty0 = ty[0];
+        const double t0 = tt[0];
+        ring_shift(ty, tt);
+        const int nx = i + D;
+        ty[D - 1] = nx < a.T ? int(a.etype[int64_t(nx) * B + f]) : 255;
+        tt[D - 1] = nx < a.T ? a.t[int64_t(nx) * B + f] : 0.0;
+        if (ty0 == 255) {  // padding: never queued (a queue it falls inside is no longer contiguous)
+            q_gap = q_gap || q_len > 0;
+            continue;
+        }
+        const bool window = t0 - prev < period;
+        if (window || q_len == 0) {
+            if (q_len == 0) {
+                q_first = i;
+                q_gap = false;
+            }
+            ++q_len;
+            if (window) continue;
+        }
+        const int r = legacy_choice(a.words, a.n_words, B, f, wp, q_len);
+        if (r < 0) {
+            wp = -1;
+            break;
+        }
+        const int sel = q_gap ? queued_event(a.etype, B, f, q_first, r) : q_first + r;
+        const double ts = sel == i ? t0 : a.t[int64_t(sel) * B + f];
+        pick[int64_t(nsel) * B + f] = sel;
+        a.sel_time[int64_t(nsel) * B + f] = ts;
+        ++nsel;
+        prev = ts;
+        q_len = 0;
+    }
+    a.n_sel[f] = nsel;
+    a.words_used[f] = wp;
+}
+
 #ifndef KF_SCHED_WAVES
 #define KF_SCHED_WAVES 2
 #endif
@@ -3175,6 +3242,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
             __VA_ARGS__;                    \
         }                                   \
     } while (0)
+
+hipError_t launch_ref15_random_picks(const Ref15SchedArgs& a, int32_t* pick, hipStream_t stream) {
+    if (a.B <= 0 || a.T < 0 || !a.words || !a.words_used || !a.n_sel || !a.sel_time || !pick) return hipErrorInvalidValue;
+    ref15_random_picks_kernel<<<dim3(unsigned((a.B + kBlock - 1) / kBlock)), kBlock, 0, stream>>>(a, pick);
+    return hipGetLastError();
+}
 
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream) {
     const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));

@@ -120,6 +120,7 @@ SIGNATURES = {
     'kf_run_scheduled_rec': (_i, [_vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _d, _vp, _vp, _vp, _vp, _vp]),
     'kf_run_scheduled_random': (_i, [_vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _d, _vp, _i, _vp, _vp, _vp, _vp, _vp,
                                      _vp]),
+    'kf_sched_random_picks': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _d, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     'kf_csv_shape': (_i, [ctypes.c_char_p, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i)]),
     'kf_csv_read': (_i, [ctypes.c_char_p, _i, _i, _vp, _i64, _i64]),
     'kf_ingest': (_i, [_vp, _i64, _i64, _vp, _i64, _i64, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -535,6 +535,33 @@ class BatchedKF:
                                                  _ptr(tr), _ptr(ld), _ptr(stt), _ptr(ns), self._stream()))
         return tr, ld, stt, ns, used
 
+    def sched_random_picks(self, t, etype, prev_time, freq, words):
+        """The random arm's picks alone (kf_sched_random_picks): t [T, B], etype [T, B],
+        prev_time [B], freq scalar or [B], words [n_words, B] uint32.  Returns (pick [T, B] int32
+        event indices, sel_time [T, B], n_sel [B], words_used [B]); run the picked events with
+        run_events."""
+        T = int(t.shape[0])
+        td = self._dev(t, (T, self.batch), 't', torch.float64)
+        et = self._dev(etype, (T, self.batch), 'etype', torch.uint8)
+        pv = self._dev(prev_time, (self.batch,), 'prev_time', torch.float64)
+        W = int(words.shape[0])
+        if isinstance(words, np.ndarray):
+            words = np.ascontiguousarray(words, np.uint32).view(np.int32)
+        elif words.dtype == torch.uint32:
+            words = words.view(torch.int32)
+        wd = self._dev(words, (W, self.batch), 'words', torch.int32)
+        fr = None
+        if np.ndim(freq) != 0:
+            fr = self._dev(freq, (self.batch,), 'freq', torch.float64)
+        pick = torch.empty(max(T, 1), self.batch, dtype=torch.int32, device=self.device)
+        stt = torch.empty(max(T, 1), self.batch, dtype=torch.float64, device=self.device)
+        ns = torch.empty(self.batch, dtype=torch.int32, device=self.device)
+        used = torch.empty(self.batch, dtype=torch.int32, device=self.device)
+        check(_lib.lib().kf_sched_random_picks(self.handle, T, _ptr(td), _ptr(et), _ptr(pv), _ptr(fr),
+                                               float(freq) if fr is None else 0.0, _ptr(wd), W, _ptr(used),
+                                               _ptr(pick), _ptr(stt), _ptr(ns), self._stream()))
+        return pick, stt, ns, used
+
     # -- synthetic streams (SURVEY.md §8d) -----------------------------------------------
     def synth(self, T, dt, update_every=1, seed=20251015, filter_offset=0):
         """Deterministic synthetic (x0 [n,B], u [T,c,B], z [U,m,B]) generated on the GPU."""

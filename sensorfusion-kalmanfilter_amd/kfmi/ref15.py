@@ -838,27 +838,39 @@ def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt
         # random_schedule (kf_workers.py:188-193): each window's np.random.choice is drawn on the
         # device from the global generator's next outputs, in the reference's order (the windows
         # follow the picks); the global generator then advances by the outputs the run took
+        # the picks (windows + draws, kf_sched_random_picks: no filter state needed), then the
+        # picked events through the event engine, which runs one long filter parallel over time
         kf = BatchedKF('ref15', 1, dtype, device=device, params=_params(consts))
         npd = np.float64 if dtype == 'f64' else np.float32
         t, et, pay, n_cand = _stream_arrays(cands, events=events)
+        dev = kf.device
+        td, etd = torch.as_tensor(t, device=dev), torch.as_tensor(et, device=dev)
         n_words = 2 * n_cand + 64
         while True:
-            kf.set_state(x0[:, None].astype(npd), to_blocks(P)[:, None].astype(npd))
-            tr, ld, stt, ns, used = kf.run_scheduled_random(t, et, pay.astype(npd), np.array([prev0]), f,
-                                                            legacy_words(n_words)[:, None])
+            pick, stt, ns, used = kf.sched_random_picks(td, etd, np.array([prev0]), f,
+                                                        legacy_words(n_words)[:, None])
             taken = int(used[0])
             if taken >= 0:
                 break
             n_words *= 4  # the column ran out (rejections beyond 2 outputs per window): draw again
         np.random.randint(0, 1 << 32, size=taken, dtype=np.uint32)
-        ld0 = _run_streams([[]], x0[None], to_blocks(P)[None], dtype, device, consts=consts)[1][0, 0]
         n = int(ns[0])
-        tr, ld, stt = tr.double().cpu().numpy(), ld.double().cpu().numpy(), stt.cpu().numpy()
+        sel = pick[:n, 0].long()
+        st_d = stt[:n, 0]
+        prev_d = torch.cat([torch.tensor([prev0], dtype=torch.float64, device=dev), st_d[:-1]])
+        # a leading padding event: row 0 of the records holds the start state and its log-det
+        ev_t = torch.cat([torch.tensor([NONE], dtype=torch.uint8, device=dev), etd[sel, 0]])
+        ev_dt = torch.cat([torch.zeros(1, dtype=torch.float64, device=dev), st_d - prev_d])
+        paydev = torch.as_tensor(pay[:, :, 0].astype(npd), device=dev)
+        ev_p = torch.cat([torch.zeros(1, 9, dtype=paydev.dtype, device=dev), paydev[sel]])
+        kf.set_state(x0[:, None].astype(npd), to_blocks(P)[:, None].astype(npd))
+        tr, ld, _, _ = kf.run_events(ev_t[:, None], ev_dt[:, None], ev_p[:, :, None].contiguous())
+        tr, ld, stt = tr.double().cpu().numpy(), ld.double().cpu().numpy(), st_d.cpu().numpy()
         _, Pb = kf.state()
         Pf = from_blocks(Pb[:, 0].double().cpu().numpy())
         kf.close()
-        states = [(prev0, *x0[:6])] + [(stt[i, 0], *tr[i, :, 0]) for i in range(n)]
-        logdets = [float(ld0)] + [float(v) for v in ld[:n, 0]]
+        states = [(prev0, *x0[:6])] + [(stt[i], *tr[i + 1, :, 0]) for i in range(n)]
+        logdets = [float(v) for v in ld[:n + 1, 0]]
     if print_output:
         print(f'{selection_method.capitalize()} Scheduled Kalman Filter (GPU): processed {len(states) - 1} measurements')
     return states, logdets, Pf

@@ -580,7 +580,14 @@ def test_scheduled_random_vs_oracle(B, records):
     records = bool(records)
     tr, ld, stt, ns, used = (v.cpu().numpy() for v in kf.run_scheduled_random(tt, etype, payload, np.full(B, t0),
                                                                                rates, words, records=records))
+    # the picks alone (kf_sched_random_picks): the same events, times and generator outputs
+    pk, st2, ns2, used2 = (v.cpu().numpy() for v in kf.sched_random_picks(tt, etype, np.full(B, t0), rates, words))
     kf.close()
+    np.testing.assert_array_equal(ns2, ns)
+    np.testing.assert_array_equal(used2, used)
+    for f in range(B):
+        np.testing.assert_array_equal(st2[:ns[f], f], stt[:ns[f], f])
+        np.testing.assert_array_equal(st2[:ns[f], f], tt[pk[:ns[f], f], f])
     for f in range(B):
         ev = [(0, 'GPS', t0, {'easting': 0.0, 'northing': 0.0, 'altitude': 0.0})]  # skipped (warm start)
         for i in range(T):
