@@ -655,7 +655,7 @@ def log_workload(cfg, args, rank, world, dev):
                                        None, 0, 0.0, kf._stream()))
 
     def step():
-        """With --graph the step's launches (reset, dt pass, kf_run_stream's kernels: 10 in all)
+        """With --graph the step's launches (reset, dt pass, kf_run_stream's kernels: 9 in all)
         are captured into a hipGraph after the first, eager step and replayed: the C ABI launches
         never synchronise or allocate after their first call, so they capture as they are.
         Measured: 0.252 ms per step replayed vs 0.246 eager (profiles/r02_timeparallel/), so
