@@ -78,6 +78,27 @@ def main():
                        'path': 'kf_run_scheduled' if method == 'greedy' else 'kf_run_scheduled_random'}
         if method == 'random':
             rand = (st, ld)
+    # the same picks through the one-launch random kernel (kf_run_scheduled_random: windows, draws
+    # and the filter in one lane, the fused kernel for B = 1) instead of picks + the event engine
+    x0, P, prev0, cands = ref15._scheduled_window_events(sf.indexed_sensor_data, None, None, None, None)
+    t, et, pay, n_cand = ref15._stream_arrays(cands, events=sf.indexed_sensor_data)
+    import kfmi
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    words = ref15.legacy_words(2 * n_cand + 64)[:, None]
+    td, etd, payd = (torch.as_tensor(v, device=kf.device) for v in (t, et, pay))
+    fused = []
+    for r in range(args.reps + 1):
+        kf.set_state(x0[:, None], ref15.to_blocks(P)[:, None])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out_f = kf.run_scheduled_random(td, etd, payd, np.array([prev0]), args.freq, words)
+        torch.cuda.synchronize()
+        if r:
+            fused.append(time.perf_counter() - t0)
+    kf.close()
+    out['random_fused_kernel'] = {'seconds': min(fused), 'selected': int(out_f[3][0]),
+                                  'same_times': bool(np.array_equal(out_f[2][:int(out_f[3][0]), 0].cpu().numpy(),
+                                                                    np.array([s_[0] for s_ in rand[0][1:]])))}
     np.random.seed(5)
     t0 = time.perf_counter()
     hs, hl = host_loop_random(sf.indexed_sensor_data, args.freq)
