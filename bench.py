@@ -73,8 +73,10 @@ CONFIGS = {
     'ref15f32': dict(model='ref15', dtype='f32', B=1048576, T=256, dt=0.005, k=20),
     'bf': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=True),
     'bf_subsets': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=False),
+    # payload records carry the event time at rec[9] (KF_OPT_SCHED_REC_TIME; bench.py fills it):
+    # 4.52 vs 4.82 ms in-process (profiles/r04_ab1/ab_sched.log); --opt sched_rec_time=off reverts
     'sched': dict(model='ref15', dtype='f64', B=1048576, T=256, dt=0.005, k=20,
-                  rates=(10, 20, 30, 40, 50, 60, 70, 80, 90, 100, 110, 120)),
+                  rates=(10, 20, 30, 40, 50, 60, 70, 80, 90, 100, 110, 120), opts={'sched_rec_time': 1}),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 SEED = 20251015
@@ -910,19 +912,24 @@ def bf_workload(cfg, args, rank, world, dev):
                                                     f"{npl['cores']} processes, NumPy {np.__version__}")}
 
     if search:
-        from kfmi.ref15 import search_level_bytes
+        from kfmi.ref15 import search_head_size, search_launches, search_level_bytes
         # every stored node (the C(n-2, k) subsets of size k < n whose largest candidate is
-        # <= n - 3) is written once and read once as a parent
-        lvl = sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in range(1, n))
+        # <= n - 3) is written once and read once as a parent; the one-launch head (sizes 1 .. K)
+        # stores only its level K
+        K = search_head_size(n)
+        lvl = sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in range(max(K, 1), n))
         return dict(step=step, units=total_steps, bytes=2 * lvl, bytes_per_unit=2 * lvl / total_combos,
-                    kernel='ref15_search_pm_kernel+ref15_search_cm_kernel (the n-1 level launches of one search)', traffic=load_traffic('bf'), cpu=cpu, gather=None, kf=kf, combos=total_combos,
+                    kernel=f'ref15_search_head_kernel (sizes 1..{K}) + ref15_search_cm/pm_kernel (the '
+                           f'{search_launches(n)} launches of one search)', traffic=load_traffic('bf'), cpu=cpu,
+                    gather=None, kf=kf, combos=total_combos,
                     roofline_note='level-buffer bytes only (each stored prefix filter written and read once, the '
                                   'subsets holding candidate n-2 scored from registers); the search is fp64 issue / '
                                   'latency-bound: ~940 VALU instructions per subset (one event step, the final '
                                   'predict, two log-dets), profiles/r02_bf/',
                     desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '
                          f'all 2^{n}-1 subsets, reference 15-state model, f64, shared-prefix search '
-                         f'(kf_search_combos: one event step + final predict per subset, {n} level launches); '
+                         f'(kf_search_combos: one event step + final predict per subset, sizes 1..{K} in one '
+                         f'launch, then one launch per level: {search_launches(n)} launches); '
                          f'value counts the reference-equivalent steps (k events + final predict per k-subset)',
                     extra={'candidate_events': n, 'combinations': total_combos, 'levels': n})
     return dict(step=step, units=total_steps, bytes=None, bytes_per_unit=None, kernel='ref15_combo_kernel',
@@ -1052,7 +1059,7 @@ def main():
     cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg['B'] = args.batch
-    cfg['opts'] = {}
+    cfg['opts'] = dict(cfg.get('opts', {}))
     for o in args.opt:
         name, _, val = o.partition('=')
         cfg['opts'][name] = int(val) if val.lstrip('-').isdigit() else val

@@ -643,6 +643,34 @@ def search_level_bytes(nodes, dtype):
     return (nodes + 63) // 64 * 64 * (28 * w + 16)
 
 
+SEARCH_HEAD_STEPS = 400000  # kf_capi.cpp kSearchHeadSteps
+
+
+def search_head_size(n, k_max=None):
+    """The sizes 1 .. K kf_search_combos runs in its one-launch head (kf_capi.cpp: the largest K
+    <= n - 2, below k_max, whose subsets' event steps from the root sum_k k C(n, k) stay within
+    kSearchHeadSteps; 0 = no head, for n < 5 or K < 2).  Bookkeeping for the bench's bytes."""
+    k_max = n if k_max is None else k_max
+    if n < 5:
+        return 0
+    K, steps = 0, 0
+    for k in range(1, min(n - 2, k_max - 1) + 1):
+        steps += k * math.comb(n, k)
+        if steps > SEARCH_HEAD_STEPS:
+            break
+        K = k
+    return K if K >= 2 else 0
+
+
+def search_launches(n, k_max=None):
+    """Kernel launches of one kf_search_combos over n free candidates: the head (if any), then
+    every later level with stored parents (a level with none is scored by the previous tail)."""
+    k_max = n if k_max is None else k_max
+    K = search_head_size(n, k_max)
+    levels = [k for k in range(1, k_max + 1) if k == 1 or math.comb(n - 2, k - 1) > 0]
+    return (1 if K else 0) + sum(1 for k in levels if k > K)
+
+
 def search_levels(n, dtype='f64', mem_bytes=32 << 30):
     """Largest k_max for which kf_search_combos' level buffers (two of the widest stored level:
     the C(n - 2, k) subsets of size k < k_max whose largest candidate is <= n - 3) fit in

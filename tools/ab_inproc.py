@@ -47,6 +47,8 @@ def main():
         else:
             h = ctypes.CDLL(os.path.abspath(a))
             for name, (res, argt) in _lib.SIGNATURES.items():
+                if not hasattr(h, name):  # an older build: entry points added since are not called
+                    continue
                 fn = getattr(h, name)
                 fn.restype = res
                 fn.argtypes = argt

@@ -62,14 +62,15 @@ def main():
             wk = per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE')
             f = [v for k, vs in fk.items() if 'ref15_search' in k for v in vs]
             w = [v for k, vs in wk.items() if 'ref15_search' in k for v in vs]
-            from kfmi.ref15 import search_level_bytes
+            from kfmi.ref15 import search_head_size, search_launches, search_level_bytes
             import math
-            # launches per search: the levels with stored parents (level n is scored by the
-            # tail of level n - 1 and not launched)
-            nl = sum(1 for k in range(1, n + 1) if k == 1 or math.comb(n - 2, k - 1) > 0)
+            # launches per search: the head (sizes 1 .. K), then the levels with stored parents
+            # (level n is scored by the tail of level n - 1 and not launched)
+            nl = search_launches(n)
+            K = search_head_size(n)
             fetch = 1024 * sum(f) / (len(f) / nl)
             write = 1024 * sum(w) / (len(w) / nl)
-            alg = 2 * sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in range(1, n))
+            alg = 2 * sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in range(max(K, 1), n))
             res['configbf'] = {
                 'fetch_bytes_raw': fetch, 'write_bytes_raw': write,
                 'bytes_per_launch': fetch * read_scale + write * write_scale,
