@@ -757,6 +757,8 @@ def sched_workload(cfg, args, rank, world, dev):
     # lanes of a wave reach their processing windows together (the jitter aside);
     # --rate-block 1 gives every lane of a wave its own rate (the divergent case)
     rb = max(1, int(getattr(args, 'rate_block', 64) or 64))
+    if getattr(args, 'sched_rates', None):
+        cfg = dict(cfg, rates=tuple(float(x) for x in args.sched_rates.split(',')))
     tt, etype, pay, freq, prev = sched_streams(B, T, dt, k, cfg['rates'], rb, SEED + rank, dev)
     # the payload as one 96-B record per event (kf_run_scheduled_rec, the default) or as the
     # [T][9][B] rows of kf_run_scheduled (--sched-payload rows): same events, same outputs
@@ -835,6 +837,7 @@ def sched_workload(cfg, args, rank, world, dev):
                      + ('payload [T][9][B] rows (kf_run_scheduled)' if rows else
                         f'payload [T][B][{rec}] records (kf_run_scheduled_rec)'),
                 extra={'filters_per_gpu': B, 'events_per_launch': T, 'selected_events': n_selected,
+                       'rates_hz': list(cfg['rates']),
                        'payload': 'rows' if rows else f'records of {rec}'})
 
 
@@ -1005,6 +1008,10 @@ def main():
     ap.add_argument('--sched-rec', type=int, default=12,
                     help='config sched, records: doubles per record (>= 10, even; 12 = 96-B records on 32-B '
                          'boundaries, the fastest measured)')
+    ap.add_argument('--sched-rates', default=None,
+                    help='config sched, diagnostics: comma-separated processing rates (Hz) instead of the '
+                         "config's 10..120 sweep (e.g. only rates whose period is, or is not, a multiple of "
+                         "the 5-ms event spacing, where the event-time jitter splits a wave's windows)")
     ap.add_argument('--graph', action='store_true',
                     help='config 1: replay the step as a hipGraph (measured no faster than eager launches)')
     ap.add_argument('--ablate', choices=['none', 'no-traj', 'no-logdet', 'no-traj-no-logdet'], default='none',

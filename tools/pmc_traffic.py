@@ -6,7 +6,11 @@ usage: python tools/pmc_traffic.py OUTDIR CFG [CFG ...]   -> writes OUTDIR/pmc_t
 FETCH_SIZE / WRITE_SIZE are in KiB.  MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE is only
 calibrated for 16 B/lane streams (reads half the bytes there); other widths must be calibrated
 on a known byte count in the same access pattern.  The probe's soa_read (T*6*B*8 bytes read,
-8 B per lane) and soa_write (T*7*B*8 bytes written) provide that calibration here.
+8 B per lane) and soa_write (T*7*B*8 bytes written) provide that calibration here.  Where the
+RDSIZED pass ran (TCC_EA0_RDREQ_{32B,64B,128B}_sum: the L2's memory-side read requests by size),
+the fetched bytes are counted exactly as 32 n32 + 64 n64 + 128 n128 instead, whatever the access
+pattern (the calibration holds for streams of whole lines, not for per-lane gathers), and the
+FETCH_SIZE figure is kept beside it.
 """
 import csv
 import glob
@@ -34,6 +38,37 @@ def per_kernel(d, counter):
     return out
 
 
+SIZED = ('TCC_EA0_RDREQ_32B_sum', 'TCC_EA0_RDREQ_64B_sum', 'TCC_EA0_RDREQ_128B_sum', 'TCC_EA0_RDREQ_sum')
+
+
+def sized_fetch(out_dir, tag, match):
+    """(bytes per dispatch, requests of no size bucket per dispatch) of the kernels whose name
+    satisfies match, from the RDSIZED pass (None if it did not run); a list per dispatch."""
+    d = os.path.join(out_dir, f'{tag}_RDSIZED')
+    if not os.path.isdir(d):
+        return None
+    cols = {c: [v for k, vs in per_kernel(d, c).items() if match(k) for v in vs] for c in SIZED}
+    n = len(cols[SIZED[0]])
+    if not n or any(len(v) != n for v in cols.values()):
+        raise SystemExit(f'RDSIZED pass of {tag}: uneven dispatch counts {[len(v) for v in cols.values()]}')
+    by = [32 * a + 64 * b + 128 * c for a, b, c in zip(*(cols[x] for x in SIZED[:3]))]
+    other = [t - a - b - c for a, b, c, t in zip(*(cols[x] for x in SIZED))]
+    return by, other
+
+
+def fetch(out_dir, tag, match, fetch_kib, read_scale):
+    """Fetched bytes per dispatch (mean) and how they were counted: the sized requests where that
+    pass ran, else FETCH_SIZE (KiB) times the probe's calibration."""
+    sz = sized_fetch(out_dir, tag, match)
+    cal = 1024 * sum(fetch_kib) / len(fetch_kib) * read_scale
+    if sz is None:
+        return cal, {'fetch_source': 'FETCH_SIZE x calibration'}
+    by, other = sz
+    return sum(by) / len(by), {'fetch_source': 'TCC_EA0_RDREQ by size (32/64/128 B)',
+                               'fetch_bytes_calibrated': cal,
+                               'requests_of_no_size_bucket': sum(other) / len(other)}
+
+
 def pick(d, sub):
     vals = [v for k, v in d.items() if sub in k]
     if not vals:
@@ -54,29 +89,36 @@ def main():
     write_scale = known_write / (1024 * sum(wr) / len(wr))
     res = {'calibration': {'fetch_size_scale': read_scale, 'write_size_scale': write_scale,
                            'probe': 'tools/probes/bw_probe soa_read/soa_write, 8 B per lane, B=2^20, T=64'}}
+    sz = sized_fetch(out_dir, 'probe', lambda k: 'soa_read' in k)
+    if sz is not None:  # the sized count against the probe's known bytes
+        res['calibration']['sized_over_known_read'] = sum(sz[0]) / len(sz[0]) / known_read
     for c in cfgs:
         if c == 'bf':
-            # one search = its n level launches (ref15_search_{cm,pm}_kernel), summed
+            # one search = its level launches (ref15_search_*_kernel), summed
             n = CONFIGS['bf']['n']
+            is_search = lambda k: 'ref15_search' in k  # noqa: E731
             fk = per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE')
             wk = per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE')
-            f = [v for k, vs in fk.items() if 'ref15_search' in k for v in vs]
-            w = [v for k, vs in wk.items() if 'ref15_search' in k for v in vs]
+            f = [v for k, vs in fk.items() if is_search(k) for v in vs]
+            w = [v for k, vs in wk.items() if is_search(k) for v in vs]
             from kfmi.ref15 import search_head_size, search_launches, search_level_bytes
             import math
             # launches per search: the head (sizes 1 .. K), then the levels with stored parents
             # (level n is scored by the tail of level n - 1 and not launched)
             nl = search_launches(n)
             K = search_head_size(n)
-            fetch = 1024 * sum(f) / (len(f) / nl)
+            fb, info = fetch(out_dir, f'cfg{c}', is_search, f, read_scale)
+            fb *= nl
+            if 'fetch_bytes_calibrated' in info:
+                info['fetch_bytes_calibrated'] *= nl
             write = 1024 * sum(w) / (len(w) / nl)
             alg = 2 * sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in range(max(K, 1), n))
             res['configbf'] = {
-                'fetch_bytes_raw': fetch, 'write_bytes_raw': write,
-                'bytes_per_launch': fetch * read_scale + write * write_scale,
+                'fetch_bytes_raw': 1024 * sum(f) / (len(f) / nl), 'write_bytes_raw': write,
+                'bytes_per_launch': fb + write * write_scale,
                 'algorithmic_bytes_per_launch': alg,
-                'traffic_over_algorithmic': (fetch * read_scale + write * write_scale) / alg,
-                'launches_profiled': len(f), 'note': f'per search: the sum over its {nl} level launches'}
+                'traffic_over_algorithmic': (fb + write * write_scale) / alg,
+                'launches_profiled': len(f), 'note': f'per search: the sum over its {nl} level launches', **info}
             continue
         if c == 'sched':
             # the two passes per launch, each against its own bytes; the algorithmic total is the
@@ -90,11 +132,12 @@ def main():
             for tag, kern in (('apply', 'ref15_apply_kernel'), ('pick', 'ref15_pick_kernel')):
                 f = pick(per_kernel(os.path.join(out_dir, 'cfgsched_FETCH_SIZE'), 'FETCH_SIZE'), kern)
                 w = pick(per_kernel(os.path.join(out_dir, 'cfgsched_WRITE_SIZE'), 'WRITE_SIZE'), kern)
-                fetch, write = 1024 * sum(f) / len(f), 1024 * sum(w) / len(w)
-                res[f'configsched_{tag}'] = {'kernel': kern, 'fetch_bytes_raw': fetch, 'write_bytes_raw': write,
-                                             'bytes_per_launch': fetch * read_scale + write * write_scale,
-                                             'launches_profiled': len(f)}
-                tot += fetch * read_scale + write * write_scale
+                fb, info = fetch(out_dir, 'cfgsched', lambda k, kern=kern: kern in k, f, read_scale)
+                write = 1024 * sum(w) / len(w)
+                res[f'configsched_{tag}'] = {'kernel': kern, 'fetch_bytes_raw': 1024 * sum(f) / len(f),
+                                             'write_bytes_raw': write, 'bytes_per_launch': fb + write * write_scale,
+                                             'launches_profiled': len(f), **info}
+                tot += fb + write * write_scale
             alg = rec['roofline']['algorithmic_bytes_per_launch']
             res['configsched'] = {'bytes_per_launch': tot, 'algorithmic_bytes_per_launch': alg,
                                   'traffic_over_algorithmic': tot / alg, 'note': 'pick + apply passes'}
@@ -102,15 +145,15 @@ def main():
         kern = {'ref15': 'ref_events', '3gen': 'cv_run_kernel'}.get(c, 'cv_block_kernel')
         f = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE'), kern)
         w = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE'), kern)
-        fetch = 1024 * sum(f) / len(f)
+        fb, info = fetch(out_dir, f'cfg{c}', lambda k: kern in k, f, read_scale)
         write = 1024 * sum(w) / len(w)
         alg, _ = (ref15_algorithmic_bytes if c == 'ref15' else algorithmic_bytes)(CONFIGS[str(c)])
         res[f'config{c}'] = {
-            'fetch_bytes_raw': fetch, 'write_bytes_raw': write,
-            'bytes_per_launch': fetch * read_scale + write * write_scale,
+            'fetch_bytes_raw': 1024 * sum(f) / len(f), 'write_bytes_raw': write,
+            'bytes_per_launch': fb + write * write_scale,
             'algorithmic_bytes_per_launch': alg,
-            'traffic_over_algorithmic': (fetch * read_scale + write * write_scale) / alg,
-            'launches_profiled': len(f)}
+            'traffic_over_algorithmic': (fb + write * write_scale) / alg,
+            'launches_profiled': len(f), **info}
     with open(os.path.join(out_dir, 'pmc_traffic.json'), 'w') as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
