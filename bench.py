@@ -73,8 +73,9 @@ CONFIGS = {
     'ref15f32': dict(model='ref15', dtype='f32', B=1048576, T=256, dt=0.005, k=20),
     'bf': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=True),
     'bf_subsets': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=False),
-    # payload records carry the event time at rec[9] (KF_OPT_SCHED_REC_TIME; bench.py fills it):
-    # 4.52 vs 4.82 ms in-process (profiles/r04_ab1/ab_sched.log); --opt sched_rec_time=off reverts
+    # payload records of 10 doubles carry the event time at rec[9] (KF_OPT_SCHED_REC_TIME; bench.py
+    # fills it): 4.52 vs 4.82 ms in-process with 12-double records (profiles/r04_ab1/ab_sched.log),
+    # 4.18 vs 4.53 ms for 10 against 12 doubles (profiles/r04_pmc/sched_diag/ab.log)
     'sched': dict(model='ref15', dtype='f64', B=1048576, T=256, dt=0.005, k=20,
                   rates=(10, 20, 30, 40, 50, 60, 70, 80, 90, 100, 110, 120), opts={'sched_rec_time': 1}),
 }
@@ -760,10 +761,10 @@ def sched_workload(cfg, args, rank, world, dev):
     if getattr(args, 'sched_rates', None):
         cfg = dict(cfg, rates=tuple(float(x) for x in args.sched_rates.split(',')))
     tt, etype, pay, freq, prev = sched_streams(B, T, dt, k, cfg['rates'], rb, SEED + rank, dev)
-    # the payload as one 96-B record per event (kf_run_scheduled_rec, the default) or as the
-    # [T][9][B] rows of kf_run_scheduled (--sched-payload rows): same events, same outputs
+    # the payload as one 80-B record per event, its time at rec[9] (kf_run_scheduled_rec, the
+    # default), or as the [T][9][B] rows of kf_run_scheduled (--sched-payload rows): same outputs
     rows = getattr(args, 'sched_payload', 'records') == 'rows'
-    rec = int(getattr(args, 'sched_rec', 12) or 12)
+    rec = int(getattr(args, 'sched_rec', 10) or 10)
     recs = None
     if not rows:
         recs = torch.zeros(T, B, rec, dtype=torch.float64, device=dev)
@@ -815,6 +816,10 @@ def sched_workload(cfg, args, rank, world, dev):
     # status read + written, n_sel written
     nbytes = B * T * 9 + n_selected * (72 + 64) + B * (2 * 42 * 8 + 8 + 8 + 8 + 4)
     mode = kf.get_option('sched_kernel')
+    # the PMC figures (profiles/pmc_traffic.json, pmc_valu.json) are of the default row: two passes,
+    # 10-double records with their time, the config's rates 64 filters per rate
+    measured_shape = (mode in (0, 3) and B % 64 == 0 and not rows and rec == 10 and rb == 64
+                      and kf.get_option('sched_rec_time') == 1 and not getattr(args, 'sched_rates', None))
     if B % 64:
         kernel = 'ref15_sched_kernel'
     elif mode in (0, 3):  # two passes (kf.h KF_OPT_SCHED_KERNEL)
@@ -824,12 +829,12 @@ def sched_workload(cfg, args, rank, world, dev):
     else:
         kernel = 'ref15_sched_lds_kernel' if mode == 2 else 'ref15_sched_kernel'
     return dict(step=step, units=B * T, bytes=nbytes, bytes_per_unit=nbytes / (B * T),
-                kernel=kernel, traffic=load_traffic('sched') if mode in (0, 3) and B % 64 == 0 else None,
-                valu=load_valu('sched') if mode in (0, 3) and B % 64 == 0 else None,
+                kernel=kernel, traffic=load_traffic('sched') if measured_shape else None,
+                valu=load_valu('sched') if measured_shape else None,
                 cpu=cpu, gather=None, kf=kf,
                 roofline_note=f'{n_selected / (B * T):.3f} of the examined events are selected and applied (a '
                               f'full 15-state event each, its payload gathered per lane); the two passes move '
-                              f'their actual HBM traffic (traffic, PMC: the gathers fetch whole 32-B sectors) at '
+                              f'their actual HBM traffic (traffic, PMC: the gathers fetch whole 128-B lines) at '
                               f'the HBM\'s practical rate, so frac understates them by traffic / algorithmic',
                 desc=f'SURVEY 8f row 3: rate-decimated greedy scheduled filter (kf_workers.py:826-957), reference '
                      f'15-state model, f64, B={B} filters/GPU, T={T} events at 200 Hz (GPS every {k}th), '
@@ -1005,9 +1010,9 @@ def main():
                     help='config sched: consecutive filters sharing a processing rate (1 = per-lane rates)')
     ap.add_argument('--sched-payload', choices=['records', 'rows'], default='records',
                     help='config sched: the payload as [T][B][10] records (kf_run_scheduled_rec) or [T][9][B] rows')
-    ap.add_argument('--sched-rec', type=int, default=12,
-                    help='config sched, records: doubles per record (>= 10, even; 12 = 96-B records on 32-B '
-                         'boundaries, the fastest measured)')
+    ap.add_argument('--sched-rec', type=int, default=10,
+                    help='config sched, records: doubles per record (>= 10, even; 10 = the payload and the '
+                         'event time in 80 B, the fastest measured)')
     ap.add_argument('--sched-rates', default=None,
                     help='config sched, diagnostics: comma-separated processing rates (Hz) instead of the '
                          "config's 10..120 sweep (e.g. only rates whose period is, or is not, a multiple of "

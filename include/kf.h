@@ -417,9 +417,11 @@ int kf_run_scheduled(kf_batch* handle, int T, const double* t, const uint8_t* et
  * kf_workers.py:870, 910).  rec_len >= 9 with rec_len * element size a multiple of 16 bytes
  * (f64: 10, f32: 12) and records 16-byte aligned, else KF_EINVAL.  The picked events' values are
  * then one contiguous span per filter instead of nine rows B elements apart, which is what the
- * apply pass gathers; records on 32-byte boundaries (f64: rec_len 12, room for the
- * event's time, type and index) fetch the fewest memory sectors.  Same outputs as
- * kf_run_scheduled, bit for bit. */
+ * apply pass gathers.  The memory moves whole 128-byte lines (every read request
+ * of the apply pass measures 128 B), so the shortest record packs a wave's picks of one event
+ * into the fewest lines: f64 rec_len 10 with the event's time at rec[9] (KF_OPT_SCHED_REC_TIME),
+ * 80 B per pick where a wave's lanes pick the same event.  Same outputs as kf_run_scheduled, bit
+ * for bit. */
 int kf_run_scheduled_rec(kf_batch* handle, int T, const double* t, const uint8_t* etype, const void* records,
                          int rec_len, const double* prev_time, const double* freq, double freq_all, void* traj,
                          void* logdet, double* sel_time, int32_t* n_sel, void* stream);

@@ -78,15 +78,16 @@ def test_ref15_bench_size_vs_oracle(config):
 
 def test_sched_bench_size_vs_oracle():
     """The sched row (2^20 filters x 256 events, rates 10..120 Hz, the two passes over the
-    bench's 12-double payload records): the payload rows give every output bitwise, and 4096 +
-    edge filters match the oracle's greedy driver pick for pick."""
+    bench's 10-double payload records, each pick's time read from rec[9]): the payload rows give
+    every output bitwise, and 4096 + edge filters match the oracle's greedy driver pick for pick."""
     dev = torch.device('cuda', 0)
     cfg = bench.CONFIGS['sched']
     B, T, k, dt = cfg['B'], cfg['T'], cfg['k'], cfg['dt']
     tt, etype, pay, freq, prev = bench.sched_streams(B, T, dt, k, cfg['rates'], 64, bench.SEED, dev)
-    kf = kfmi.BatchedKF('ref15', B, 'f64')
-    recs = torch.zeros(T, B, 12, dtype=torch.float64, device=dev)
+    kf = kfmi.BatchedKF('ref15', B, 'f64', options=cfg['opts'])
+    recs = torch.zeros(T, B, 10, dtype=torch.float64, device=dev)
     recs[:, :, :9] = pay.transpose(1, 2)
+    recs[:, :, 9] = tt
     out = kf.run_scheduled(tt, etype, recs, prev, freq, records=True)
     del recs
     assert int((kf.status() != 0).sum()) == 0
