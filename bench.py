@@ -150,11 +150,15 @@ def host_cpu():
     return platform.processor() or platform.machine()
 
 
-def load_traffic(cfg_id):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
+def load_traffic(cfg_id, algorithmic=None):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py);
+    with ``algorithmic``, only if the summary was measured on a launch of those algorithmic bytes
+    (the same variant of the workload)."""
     try:
         with open(os.path.join(ROOT, 'profiles', 'pmc_traffic.json')) as f:
             rec = json.load(f).get(f'config{cfg_id}')
+        if rec and algorithmic is not None and rec.get('algorithmic_bytes_per_launch') != algorithmic:
+            return None
         return rec['bytes_per_launch'] if rec else None
     except (OSError, ValueError, KeyError):
         return None
@@ -920,26 +924,33 @@ def bf_workload(cfg, args, rank, world, dev):
                                                     f"{npl['cores']} processes, NumPy {np.__version__}")}
 
     if search:
-        from kfmi.ref15 import search_head_size, search_launches, search_level_bytes
+        from kfmi.ref15 import search_level_bytes
+        step()  # how the library runs this search (kf_search_info): axis-symmetric, head, launches
+        torch.cuda.synchronize(dev)
+        info = kf.search_info()
+        K, sym = info['head_sizes'], info['sym']
+        launches = info['level_launches'] + (1 if K else 0)
         # every stored node (the C(n-2, k) subsets of size k < n whose largest candidate is
         # <= n - 3) is written once and read once as a parent; the one-launch head (sizes 1 .. K)
         # stores only its level K
-        K = search_head_size(n)
-        lvl = sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in range(max(K, 1), n))
+        lvl = sum(search_level_bytes(math.comb(n - 2, k), 'f64', sym) for k in range(max(K, 1), n))
+        chains = ('axis-symmetric: one pva and one aw chain computed and stored for the three of each, '
+                  'KF_OPT_SEARCH_SYM' if sym else 'every chain')
         return dict(step=step, units=total_steps, bytes=2 * lvl, bytes_per_unit=2 * lvl / total_combos,
                     kernel=f'ref15_search_head_kernel (sizes 1..{K}) + ref15_search_cm/pm_kernel (the '
-                           f'{search_launches(n)} launches of one search)', traffic=load_traffic('bf'), cpu=cpu,
+                           f'{launches} launches of one search)',
+                    traffic=load_traffic('bf', 2 * lvl), cpu=cpu,
                     gather=None, kf=kf, combos=total_combos,
                     roofline_note='level-buffer bytes only (each stored prefix filter written and read once, the '
                                   'subsets holding candidate n-2 scored from registers); the search is fp64 issue / '
-                                  'latency-bound: ~940 VALU instructions per subset (one event step, the final '
-                                  'predict, two log-dets), profiles/r02_bf/',
+                                  'latency-bound (one event step, the final predict, two log-dets per subset; '
+                                  'DESIGN.md §3)',
                     desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '
                          f'all 2^{n}-1 subsets, reference 15-state model, f64, shared-prefix search '
                          f'(kf_search_combos: one event step + final predict per subset, sizes 1..{K} in one '
-                         f'launch, then one launch per level: {search_launches(n)} launches); '
+                         f'launch, then one launch per level: {launches} launches; {chains}); '
                          f'value counts the reference-equivalent steps (k events + final predict per k-subset)',
-                    extra={'candidate_events': n, 'combinations': total_combos, 'levels': n})
+                    extra={'candidate_events': n, 'combinations': total_combos, 'levels': n, 'search': info})
     return dict(step=step, units=total_steps, bytes=None, bytes_per_unit=None, kernel='ref15_combo_kernel',
                 traffic=None, cpu=cpu, gather=None, kf=kf, combos=total_combos,
                 desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '

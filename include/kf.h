@@ -147,6 +147,13 @@ const char* kf_version(void);
  *   KF_OPT_SEARCH_PM      kf_search_combos' parent-major kernel: 0 = parent in LDS, 1 = registers
  *   KF_OPT_SEARCH_HEAD    kf_search_combos: 0 = the first levels (sizes whose subsets need few event
  *                         steps in all) in one launch, one lane per subset; 1 = level by level
+ *   KF_OPT_SEARCH_SYM     kf_search_combos: 0 = where the handle's noise constants are the same on
+ *                         the three axes and so are the init covariance's blocks (bit for bit),
+ *                         the three pva chains carry one covariance, and so do the three aw
+ *                         chains: one of each is computed and stored (the every-chain search's
+ *                         results to rounding: its three compiled copies of a chain's arithmetic
+ *                         round alike in ~98 % of subsets, one ulp apart in the rest); 1 = every
+ *                         chain
  *   KF_OPT_SCHED_KERNEL   kf_run_scheduled: 0 = auto (the two passes where legal, as 3), 1 = the
  *                         fused register-input kernel, 2 = the fused LDS-input kernel, 3 = the
  *                         pick and apply passes as two launches, 4 = as the two phases of one
@@ -178,7 +185,8 @@ const char* kf_version(void);
 #define KF_OPT_SCHED_ORDER    13
 #define KF_OPT_SCHED_REC_TIME 14
 #define KF_OPT_SEARCH_HEAD    15
-#define KF_OPT_COUNT          16
+#define KF_OPT_SEARCH_SYM     16
+#define KF_OPT_COUNT          17
 int kf_set_option(kf_batch* handle, int option, int64_t value);
 int kf_get_option(const kf_batch* handle, int option, int64_t* value);
 
@@ -365,12 +373,18 @@ int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const d
  * subsets whose largest free candidate is <= n - 3 (a subset holding n - 1 has no extensions,
  * one holding n - 2 only the one adding n - 1, which is scored from registers); C(n - 2, k)
  * must stay below 2^28, and the handle's level buffers take 2 * C(n - 2, k) * (28 w + 16)
- * bytes at the widest stored level (w = 8 for f64, 4 for f32; n = free candidates).  The call
- * synchronises `stream`. */
+ * bytes at the widest stored level (w = 8 for f64, 4 for f32; n = free candidates; 10 w + 16
+ * for an axis-symmetric search, KF_OPT_SEARCH_SYM).  The call synchronises `stream`. */
 int kf_search_combos(kf_batch* handle, int n_events, const double* events, const double* init,
                      double prev_time, double target_end, double threshold, int k_max, int exhaustive,
                      int n_fixed, uint64_t fixed_mask, uint64_t* winner, int* k_found,
                      uint64_t* n_accepted, void* subset_max, void* stream);
+
+/* The last kf_search_combos on this handle: out[0] = 1 if it ran axis-symmetric
+ * (KF_OPT_SEARCH_SYM: one pva and one aw chain for the three of each), out[1] = the sizes its
+ * head launch covered (KF_OPT_SEARCH_HEAD; 0 = none), out[2] = its level launches after the
+ * head, out[3] = the bytes of one of its two level buffers.  All 0 before the first search. */
+int kf_search_info(const kf_batch* handle, int64_t* out);
 
 /* KF_MODEL_REF15 scheduler scoring: gain device [n_types][B] = trace of the posterior
  * covariance each candidate sensor type (types: host [n_types] KF_EVENT_GPS|KF_EVENT_IMU,

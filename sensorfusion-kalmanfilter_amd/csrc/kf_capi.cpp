@@ -67,6 +67,7 @@ struct kf_batch {
     // never freed before kf_free (a larger one replaces it and it moves to `retired`)
     bool search_ws_graph, stream_ws_graph, sched_ws_graph;
     std::vector<void*> retired;
+    int64_t search_info[4];  // the last kf_search_combos: sym, head sizes, level launches, level bytes
 };
 
 namespace {
@@ -358,6 +359,7 @@ int kf_set_option(kf_batch* h, int option, int64_t value) {
         case KF_OPT_STREAM_FINAL:
         case KF_OPT_SEARCH_PM:
         case KF_OPT_SEARCH_HEAD: ok = value == 0 || value == 1; break;
+        case KF_OPT_SEARCH_SYM: ok = value == 0 || value == 1; break;
         case KF_OPT_SCHED_KERNEL: ok = value >= 0 && value <= 4; break;
         case KF_OPT_SCHED_GROUP: ok = value == 0 || value == 1 || value == 4; break;
         case KF_OPT_SCHED_ORDER:
@@ -1094,6 +1096,27 @@ int kf_eval_combos(kf_batch* h, int n_events, const double* events, const double
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_eval_combos");
 }
 
+// kf_search_combos' axis-symmetric variant (Ref15SearchArgs::sym): the handle's noise constants are
+// the same on the three axes — pos / vel / acc and att / rate of axis c those of axis 0, R_gps[c]
+// R_gps[0] — and so are the blocks of the root covariance init[15 ..] (bit for bit), so every
+// covariance the search reaches has three equal pva blocks and three equal aw blocks
+static bool search_sym(const kf_batch* h, const double* init) {
+    if (opt(h, KF_OPT_SEARCH_SYM) == 1) return false;
+    const kf_params& p = h->params;
+    auto same = [](double a, double b) { return std::memcmp(&a, &b, sizeof a) == 0; };
+    const double* blk = init + 15;
+    for (int c = 1; c < 3; ++c) {
+        for (int s : {0, 6, 12, 3, 9})
+            if (!same(p.ref_q[s + c], p.ref_q[s]) || !same(p.ref_r_imu[s + c], p.ref_r_imu[s])) return false;
+        if (!same(p.ref_r_gps[c], p.ref_r_gps[0])) return false;
+        for (int i = 0; i < 6; ++i)
+            if (!same(blk[6 * c + i], blk[i])) return false;
+        for (int i = 0; i < 3; ++i)
+            if (!same(blk[18 + 3 * c + i], blk[18 + i])) return false;
+    }
+    return true;
+}
+
 int kf_search_combos(kf_batch* h, int n_events, const double* events, const double* init, double prev_time,
                      double target_end, double threshold, int k_max, int exhaustive, int n_fixed,
                      uint64_t fixed_mask, uint64_t* winner, int* k_found, uint64_t* n_accepted, void* subset_max,
@@ -1126,7 +1149,9 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
                         k, n - 2, k - 1, static_cast<unsigned long long>(C(n - 2, k - 1)));
     const int esz = static_cast<int>(elem(h));
     const size_t head = 4096;  // best[65], n_acc[65]
-    const size_t level = widest ? static_cast<size_t>(kfmi::search_level_bytes(widest, esz)) : 0;
+    const bool sym = search_sym(h, init);
+    const size_t level = widest ? static_cast<size_t>(kfmi::search_level_bytes(widest, esz, sym)) : 0;
+    int64_t launches = 0;
     const size_t need = head + 2 * level;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (!grow_ws(h, &h->search_ws, &h->search_ws_bytes, &h->search_ws_graph, need, st))
@@ -1180,6 +1205,7 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.n_acc = d_acc;
         a.subset_max = subset_max;
         a.tail = 1;
+        a.sym = sym;
         e = kfmi::launch_ref15_search_head(h->dtype == KF_F64, a, st);
         if (e != hipSuccess) return hip_fail(e, "kf_search_combos: head launch");
         last = k_base + K;
@@ -1216,11 +1242,13 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.n_acc = d_acc;
         a.subset_max = subset_max;
         a.tail = k < kf_max;
+        a.sym = sym;
         // a level without stored parents was scored whole by the previous launch's tail
         if (a.n_par) {
             a.pm_regs = opt(h, KF_OPT_SEARCH_PM) == 1;
             e = kfmi::launch_ref15_search(h->dtype == KF_F64, a, search_child_major(h, a.n_par), st);
             if (e != hipSuccess) return hip_fail(e, "kf_search_combos: level launch");
+            ++launches;
         }
         last = k_base + k;
         if (!exhaustive) {  // the reference stops at the first size with an acceptable subset
@@ -1238,10 +1266,21 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
     if (e != hipSuccess) return hip_fail(e, "kf_search_combos: results");
     for (int k = k_base > 0 ? k_base : 1; k <= last && !found; ++k)
         if (best[k]) found = k;
+    h->search_info[0] = sym;
+    h->search_info[1] = K;
+    h->search_info[2] = launches;
+    h->search_info[3] = static_cast<int64_t>(level);
     *k_found = found;
     *winner = found ? __builtin_bitreverse64(best[found]) : 0;
     if (n_accepted)
         for (int k = 0; k <= k_max; ++k) n_accepted[k] = k <= last ? acc[k] : 0;
+    return KF_OK;
+}
+
+int kf_search_info(const kf_batch* h, int64_t* out) {
+    if (int rc = check_handle(h)) return rc;
+    if (!out) return fail(KF_EINVAL, "kf_search_info: null output");
+    for (int i = 0; i < 4; ++i) out[i] = h->search_info[i];
     return KF_OK;
 }
 

@@ -195,7 +195,8 @@ struct Ref15ComboArgs {
 // ranks [C(j, k), C(j + 1, k)) and child rank = parent rank + C(j, k).  One lane per parent
 // evaluates all of its children.  Level buffer: node blocks of 64 nodes, block b =
 //   [28][64] T       block-packed P (27), running max log-det (NaN = failed filter); no state:
-//                    the max log-det depends on the covariance alone
+//                    the max log-det depends on the covariance alone (sym: [10][64], one pva
+//                    block, one aw block, the max)
 //   [64] double      time of the last applied event
 //   [64] uint64      subset bit mask
 struct Ref15SearchArgs {
@@ -228,13 +229,21 @@ struct Ref15SearchArgs {
     uint64_t gitem[66];
     uint64_t gblk[66];
     bool pm_regs;            // parent-major: the parent's covariance in registers, not LDS (KF_OPT_SEARCH_PM)
+    bool sym;                // axis-symmetric: the noise constants and the root's blocks are the same on
+                             // the three axes, so the three pva chains (and the three aw chains) carry
+                             // the same covariance; one of each is computed and stored
+                             // (KF_OPT_SEARCH_SYM)
     const RefConsts* kc;     // the handle's noise constants, or nullptr (the reference's)
 };
 
-constexpr int kSearchRows = 28;  // T rows of a search node
-__host__ __device__ constexpr uint64_t search_block_bytes(uint64_t elem) { return 64 * (kSearchRows * elem + 16); }
-__host__ __device__ inline uint64_t search_level_bytes(uint64_t nodes, uint64_t elem) {
-    return (nodes + 63) / 64 * search_block_bytes(elem);
+// T rows of a search node: the block-packed P (27) and the running max log-det; an axis-symmetric
+// search (Ref15SearchArgs::sym) keeps one pva block and one aw block (6 + 3) and the max
+__host__ __device__ constexpr int search_rows(bool sym) { return sym ? 10 : 28; }
+__host__ __device__ constexpr uint64_t search_block_bytes(uint64_t elem, bool sym = false) {
+    return 64 * (search_rows(sym) * elem + 16);
+}
+__host__ __device__ inline uint64_t search_level_bytes(uint64_t nodes, uint64_t elem, bool sym = false) {
+    return (nodes + 63) / 64 * search_block_bytes(elem, sym);
 }
 
 // Scheduler scoring (kf_workers.py:112-185): trace of the posterior covariance each candidate

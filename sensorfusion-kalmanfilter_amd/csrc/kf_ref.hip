@@ -1854,17 +1854,17 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }
 
 // Level buffers in node blocks of 64 (kf_internal.h): a wave's parents are one contiguous block.
-template <typename T>
+template <typename T, bool SYM = false>
 __device__ __forceinline__ char* level_block(const void* base, uint64_t c) {
-    return static_cast<char*>(const_cast<void*>(base)) + (c >> 6) * search_block_bytes(sizeof(T));
+    return static_cast<char*>(const_cast<void*>(base)) + (c >> 6) * search_block_bytes(sizeof(T), SYM);
 }
 template <typename T>
 __device__ __forceinline__ T* level_row(char* blk, uint32_t lane, int r) {
     return reinterpret_cast<T*>(blk + r * 64 * int(sizeof(T))) + lane;
 }
-template <typename T>
+template <typename T, bool SYM = false>
 __device__ __forceinline__ double* level_tail(char* blk, uint32_t lane, int q) {
-    return reinterpret_cast<double*>(blk + kSearchRows * 64 * int(sizeof(T)) + q * 512) + lane;
+    return reinterpret_cast<double*>(blk + search_rows(SYM) * 64 * int(sizeof(T)) + q * 512) + lane;
 }
 
 // Chains<T, M15>::logdet() accumulated one block at a time, in its order (pva chains, then aw
@@ -1896,9 +1896,16 @@ struct LogdetAcc {
 // depend on the measurements (nor, so, on the state): the state is not carried (kf_eval_combos
 // carries it for the per-combination API).  The updates see a constant zero state (search_pva,
 // search_aw), so their state half is dead code the compiler removes.
-template <typename T, bool CUSTOM>
+// SYM (Ref15SearchArgs::sym): the three pva chains, and the three aw chains, have the same
+// constants and the same start, so in exact arithmetic the same covariance; the node holds one of
+// each (rows 0..5 pva, 6..8 aw) and the search computes one of each, entering it into the
+// log-dets once per chain it stands for.  (The every-chain kernels' separately compiled copies
+// of a chain round alike in most subsets and one ulp apart in some.)
+template <typename T, bool CUSTOM, bool SYM = false>
 struct SearchNode {
-    T P[27];
+    static constexpr int NP = SYM ? 1 : M15::NP, NA = SYM ? 1 : M15::NA;
+    static constexpr int NR = 6 * NP + 3 * NA;  // covariance rows held (27, or 9)
+    T P[NR];
     T run;
     double prev;
     uint64_t mask;
@@ -1933,7 +1940,9 @@ struct SearchNode {
             prev = e[0];
         }
 #pragma unroll
-        for (int i = 0; i < 27; ++i) P[i] = r.blk(i);
+        for (int i = 0; i < 6 * NP; ++i) P[i] = r.blk(i);
+#pragma unroll
+        for (int i = 0; i < 3 * NA; ++i) P[6 * NP + i] = r.blk(6 * M15::NP + i);
         T fmax = run;
         if (eval && prev < a.target_end - 1e-8) {  // kf_workers.py:74-82
             r.predict(T(a.target_end - prev));
@@ -1943,13 +1952,23 @@ struct SearchNode {
         return fmax;
     }
     __device__ __forceinline__ void load(const void* level, uint64_t p) {
-        char* blk = level_block<T>(level, p);
+        char* blk = level_block<T, SYM>(level, p);
         const uint32_t lane = uint32_t(p) & 63u;
 #pragma unroll
-        for (int i = 0; i < 27; ++i) P[i] = *level_row<T>(blk, lane, i);
-        run = *level_row<T>(blk, lane, 27);
-        prev = *level_tail<T>(blk, lane, 0);
-        mask = __builtin_bit_cast(uint64_t, *level_tail<T>(blk, lane, 1));
+        for (int i = 0; i < NR; ++i) P[i] = *level_row<T>(blk, lane, i);
+        run = *level_row<T>(blk, lane, NR);
+        prev = *level_tail<T, SYM>(blk, lane, 0);
+        mask = __builtin_bit_cast(uint64_t, *level_tail<T, SYM>(blk, lane, 1));
+    }
+    // the node as level K + 1's parent at colex rank r (the head kernel)
+    __device__ __forceinline__ void store(void* level, uint64_t r) const {
+        char* cb = level_block<T, SYM>(level, r);
+        const uint32_t cl = uint32_t(r) & 63u;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) *level_row<T>(cb, cl, i) = P[i];
+        *level_row<T>(cb, cl, NR) = run;
+        *level_tail<T, SYM>(cb, cl, 0) = prev;
+        *level_tail<T, SYM>(cb, cl, 1) = __builtin_bit_cast(double, mask);
     }
     // largest free candidate in the subset (local index), -1 for the root
     __device__ __forceinline__ int max_event(int shift) const {
@@ -2039,27 +2058,33 @@ struct SearchScore {
     LogdetAcc<T> rec, fin;
     bool ok = true;
     const RefConsts* kc = nullptr;
-    __device__ __forceinline__ void add_pva(const SearchEvent& v, const T (&Pb)[6], int ch) {
+    // chains ch .. ch + reps - 1 all holding Pb (reps = 3: the axis-symmetric search's one pva
+    // chain standing for the three; their blocks enter the log-dets in the same order)
+    __device__ __forceinline__ void add_pva(const SearchEvent& v, const T (&Pb)[6], int ch, int reps = 1) {
         using C15 = Chains<T, M15>;
         T qpva[3], Rp[6], rg;
         pva_noise<CUSTOM, M15>(kc, ch, qpva, Rp, rg);
-        rec.add_pva(Pb, ch);
+#pragma unroll
+        for (int r = 0; r < reps; ++r) rec.add_pva(Pb, ch + r);
         T Pf[6], xf[3] = {T(0), T(0), T(0)};
 #pragma unroll
         for (int i = 0; i < 6; ++i) Pf[i] = Pb[i];
         if (v.final_predict) C15::template chain_predict<3>(xf, Pf, T(v.dte), qpva);
-        fin.add_pva(Pf, ch);
+#pragma unroll
+        for (int r = 0; r < reps; ++r) fin.add_pva(Pf, ch + r);
     }
-    __device__ __forceinline__ void add_aw(const SearchEvent& v, const T (&Pa)[3], int ch) {
+    __device__ __forceinline__ void add_aw(const SearchEvent& v, const T (&Pa)[3], int ch, int reps = 1) {
         using C15 = Chains<T, M15>;
         T qaw[2], Ra[3];
         aw_noise<CUSTOM, M15>(kc, ch, qaw, Ra);
-        rec.add_aw(Pa);
+#pragma unroll
+        for (int r = 0; r < reps; ++r) rec.add_aw(Pa);
         T Pf[3], xf[2] = {T(0), T(0)};
 #pragma unroll
         for (int i = 0; i < 3; ++i) Pf[i] = Pa[i];
         if (v.final_predict) C15::template chain_predict<2>(xf, Pf, T(v.dte), qaw);
-        fin.add_aw(Pf);
+#pragma unroll
+        for (int r = 0; r < reps; ++r) fin.add_aw(Pf);
     }
     // the running max log-det after the event (NaN for a failed filter, kf_eval_combos:
     // KF_ENOTSPD), and into fmax the subset's max log-det with the final predict
@@ -2103,21 +2128,23 @@ struct ParLds {
     __device__ __forceinline__ T operator()(int i) const { return col[i * 64]; }
 };
 
-template <typename T, bool CUSTOM, class PS>
-__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const SearchNode<T, CUSTOM>& par, const PS& pp, int j,
-                                             uint64_t c, uint64_t& best, uint64_t& cnt, uint64_t& best1,
+template <typename T, bool CUSTOM, bool SYM, class PS>
+__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const SearchNode<T, CUSTOM, SYM>& par, const PS& pp,
+                                             int j, uint64_t c, uint64_t& best, uint64_t& cnt, uint64_t& best1,
                                              uint64_t& cnt1) {
+    using Node = SearchNode<T, CUSTOM, SYM>;
+    constexpr int RP = SYM ? M15::NP : 1, RA = SYM ? M15::NA : 1;  // chains each computed one stands for
     const SearchEvent vs = search_event(a, j, par.prev);
     const bool store = a.child && j < a.n_events - 2;
     const bool tail = a.tail && j == a.n_events - 2;  // wave-uniform (j is)
     SearchEvent vg;
     if (tail) vg = search_event(a, j + 1, vs.prev);
-    char* cb = store ? level_block<T>(a.child, c) : nullptr;
+    char* cb = store ? level_block<T, SYM>(a.child, c) : nullptr;
     const uint32_t cl = uint32_t(c) & 63u;
     SearchScore<T, CUSTOM> ss, sg;
     ss.kc = sg.kc = a.kc;
 #pragma unroll
-    for (int ch = 0; ch < M15::NP; ++ch) {
+    for (int ch = 0; ch < Node::NP; ++ch) {
         T Pb[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) Pb[i] = pp(6 * ch + i);
@@ -2126,27 +2153,27 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
 #pragma unroll
             for (int i = 0; i < 6; ++i) *level_row<T>(cb, cl, 6 * ch + i) = Pb[i];
         }
-        ss.add_pva(vs, Pb, ch);
+        ss.add_pva(vs, Pb, ch, RP);
         if (tail) {
             search_pva<T, CUSTOM>(vg, ch, Pb, sg.ok, a.kc);
-            sg.add_pva(vg, Pb, ch);
+            sg.add_pva(vg, Pb, ch, RP);
         }
         if constexpr (PS::kChainFence) __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int ch = 0; ch < M15::NA; ++ch) {
+    for (int ch = 0; ch < Node::NA; ++ch) {
         T Pa[3];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) Pa[i] = pp(6 * M15::NP + 3 * ch + i);
+        for (int i = 0; i < 3; ++i) Pa[i] = pp(6 * Node::NP + 3 * ch + i);
         search_aw<T, CUSTOM>(vs, ch, Pa, ss.ok, a.kc);
         if (store) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, 6 * M15::NP + 3 * ch + i) = Pa[i];
+            for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, 6 * Node::NP + 3 * ch + i) = Pa[i];
         }
-        ss.add_aw(vs, Pa, ch);
+        ss.add_aw(vs, Pa, ch, RA);
         if (tail) {
             search_aw<T, CUSTOM>(vg, ch, Pa, sg.ok, a.kc);
-            sg.add_aw(vg, Pa, ch);
+            sg.add_aw(vg, Pa, ch, RA);
         }
         if constexpr (PS::kChainFence) __builtin_amdgcn_sched_barrier(0);
     }
@@ -2154,9 +2181,9 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
     const T run = ss.finish(vs, par.run, fmax);
     const uint64_t cmask = par.mask | (uint64_t(1) << (j + a.shift));
     if (store) {
-        *level_row<T>(cb, cl, 27) = run;
-        *level_tail<T>(cb, cl, 0) = vs.prev;
-        *level_tail<T>(cb, cl, 1) = __builtin_bit_cast(double, cmask);
+        *level_row<T>(cb, cl, Node::NR) = run;
+        *level_tail<T, SYM>(cb, cl, 0) = vs.prev;
+        *level_tail<T, SYM>(cb, cl, 1) = __builtin_bit_cast(double, cmask);
     }
     search_score(a, cmask, fmax, best, cnt);
     if (tail) {
@@ -2186,13 +2213,14 @@ __device__ __forceinline__ void search_publish(const Ref15SearchArgs& a, int k, 
 #endif
 // PLDS: the parent's covariance lives in LDS (one 64-lane block per workgroup, [27][64] T),
 // which fits the kernel in 3 waves per SIMD without spills; otherwise in registers.
-template <typename T, bool PLDS, bool CUSTOM>
+template <typename T, bool PLDS, bool CUSTOM, bool SYM>
 __global__ __launch_bounds__(PLDS ? 64 : kBlock) __attribute__((amdgpu_waves_per_eu(PLDS ? 3 : KF_SEARCH_PM_WAVES))) void
 ref15_search_pm_kernel(const Ref15SearchArgs a) {
     constexpr int NT = PLDS ? 64 : kBlock;
+    constexpr int NR = SearchNode<T, CUSTOM, SYM>::NR;
     const int64_t p = static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x;
     if (uint64_t(p) >= a.n_par) return;
-    SearchNode<T, CUSTOM> par;
+    SearchNode<T, CUSTOM, SYM> par;
     if (a.k == 1) {
         uint64_t rb = 0, rc = 0;  // a fixed root is itself one of the subsets searched
         const T f = par.root(a, a.root_mask != 0);
@@ -2205,24 +2233,24 @@ ref15_search_pm_kernel(const Ref15SearchArgs a) {
     const int j0 = wave_uniform(m) + 1;  // colex order: the first lane holds the smallest max
     uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0;
     if constexpr (PLDS) {
-        __shared__ T sP[27 * 64];
+        __shared__ T sP[NR * 64];
         T* col = sP + threadIdx.x;
 #pragma unroll
-        for (int i = 0; i < 27; ++i) col[i * 64] = par.P[i];  // read back by this lane only
+        for (int i = 0; i < NR; ++i) col[i * 64] = par.P[i];  // read back by this lane only
         const ParLds<T> pp{col};
 #pragma unroll 1
         for (int j = j0; j < a.n_events; ++j) {
             if (j <= m) continue;
-            search_child<T, CUSTOM>(a, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt, best1,
-                                    cnt1);
+            search_child<T, CUSTOM, SYM>(a, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt,
+                                         best1, cnt1);
         }
     } else {
         const ParRegs<T> pp{par.P};
 #pragma unroll 1
         for (int j = j0; j < a.n_events; ++j) {
             if (j <= m) continue;
-            search_child<T, CUSTOM>(a, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt, best1,
-                                    cnt1);
+            search_child<T, CUSTOM, SYM>(a, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt,
+                                         best1, cnt1);
         }
     }
     search_publish(a, a.k, best, cnt);
@@ -2238,9 +2266,11 @@ ref15_search_pm_kernel(const Ref15SearchArgs a) {
 // K + 1's parents; one whose largest is n - 2 also scores its child with n - 1 (the tail).
 // a.n_child = sum_{k <= K} C(n, k).  Every lane stays to the end (the publish reductions read
 // every lane).
-template <typename T, bool CUSTOM>
+template <typename T, bool CUSTOM, bool SYM>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void ref15_search_head_kernel(
     const Ref15SearchArgs a) {
+    using Node = SearchNode<T, CUSTOM, SYM>;
+    constexpr int RP = SYM ? M15::NP : 1, RA = SYM ? M15::NA : 1;
     const int n = a.n_events, K = a.k;
     const uint64_t* C = a.binom;
     auto binom = [&](int x, int y) -> uint64_t { return C[x * (kMaxEvents + 1) + y]; };
@@ -2265,7 +2295,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
         }
     }
     uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0;
-    SearchNode<T, CUSTOM> nd;
+    Node nd;
     {
         uint64_t rb = 0, rc = 0;  // a fixed root is itself one of the subsets searched (lane 0 scores it)
         const bool eval = a.root_mask != 0 && g == 0;
@@ -2282,24 +2312,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
         SearchScore<T, CUSTOM> ss;
         ss.kc = a.kc;
 #pragma unroll
-        for (int ch = 0; ch < M15::NP; ++ch) {
+        for (int ch = 0; ch < Node::NP; ++ch) {
             T Pb[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) Pb[i] = nd.P[6 * ch + i];
             search_pva<T, CUSTOM>(vs, ch, Pb, ss.ok, a.kc);
 #pragma unroll
             for (int i = 0; i < 6; ++i) nd.P[6 * ch + i] = Pb[i];
-            ss.add_pva(vs, Pb, ch);
+            ss.add_pva(vs, Pb, ch, RP);
         }
 #pragma unroll
-        for (int ch = 0; ch < M15::NA; ++ch) {
+        for (int ch = 0; ch < Node::NA; ++ch) {
             T Pa[3];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) Pa[i] = nd.P[6 * M15::NP + 3 * ch + i];
+            for (int i = 0; i < 3; ++i) Pa[i] = nd.P[6 * Node::NP + 3 * ch + i];
             search_aw<T, CUSTOM>(vs, ch, Pa, ss.ok, a.kc);
 #pragma unroll
-            for (int i = 0; i < 3; ++i) nd.P[6 * M15::NP + 3 * ch + i] = Pa[i];
-            ss.add_aw(vs, Pa, ch);
+            for (int i = 0; i < 3; ++i) nd.P[6 * Node::NP + 3 * ch + i] = Pa[i];
+            ss.add_aw(vs, Pa, ch, RA);
         }
         nd.run = ss.finish(vs, nd.run, fmax);
         nd.prev = vs.prev;
@@ -2308,34 +2338,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
     const int top = sub ? 63 - __builtin_clzll(sub) : -1;
     if (live) {
         search_score(a, nd.mask, fmax, best, cnt);
-        if (k == K && a.child && top <= n - 3) {  // level K + 1's parent, at its colex rank
-            char* cb = level_block<T>(a.child, r);
-            const uint32_t cl = uint32_t(r) & 63u;
-#pragma unroll
-            for (int i = 0; i < 27; ++i) *level_row<T>(cb, cl, i) = nd.P[i];
-            *level_row<T>(cb, cl, 27) = nd.run;
-            *level_tail<T>(cb, cl, 0) = nd.prev;
-            *level_tail<T>(cb, cl, 1) = __builtin_bit_cast(double, nd.mask);
-        }
+        if (k == K && a.child && top <= n - 3) nd.store(a.child, r);  // level K + 1's parent, at its colex rank
         if (k == K && a.tail && top == n - 2) {  // its only child, plus event n - 1 (size K + 1)
             const SearchEvent vg = search_event(a, n - 1, nd.prev);
             SearchScore<T, CUSTOM> sg;
             sg.kc = a.kc;
 #pragma unroll
-            for (int ch = 0; ch < M15::NP; ++ch) {
+            for (int ch = 0; ch < Node::NP; ++ch) {
                 T Pb[6];
 #pragma unroll
                 for (int i = 0; i < 6; ++i) Pb[i] = nd.P[6 * ch + i];
                 search_pva<T, CUSTOM>(vg, ch, Pb, sg.ok, a.kc);
-                sg.add_pva(vg, Pb, ch);
+                sg.add_pva(vg, Pb, ch, RP);
             }
 #pragma unroll
-            for (int ch = 0; ch < M15::NA; ++ch) {
+            for (int ch = 0; ch < Node::NA; ++ch) {
                 T Pa[3];
 #pragma unroll
-                for (int i = 0; i < 3; ++i) Pa[i] = nd.P[6 * M15::NP + 3 * ch + i];
+                for (int i = 0; i < 3; ++i) Pa[i] = nd.P[6 * Node::NP + 3 * ch + i];
                 search_aw<T, CUSTOM>(vg, ch, Pa, sg.ok, a.kc);
-                sg.add_aw(vg, Pa, ch);
+                sg.add_aw(vg, Pa, ch, RA);
             }
             T gmax;
             (void)sg.finish(vg, nd.run, gmax);
@@ -2356,7 +2378,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
 // contiguous ranges, so the items that read one parent block run back to back on one XCD and
 // re-read it from that XCD's L2.  Blocks are grouped by their first parent's largest event v
 // (non-decreasing in colex order); a block of group v has items j = v + 1 .. n - 1.
-template <typename T, bool CUSTOM>
+template <typename T, bool CUSTOM, bool SYM>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void ref15_search_cm_kernel(const Ref15SearchArgs a,
                                                                                                      uint64_t n_items) {
     const uint64_t per_xcd = (n_items + 7) / 8;
@@ -2385,7 +2407,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
     }
     const uint64_t p = blk * 64 + threadIdx.x;
     if (p >= a.n_par) return;
-    SearchNode<T, CUSTOM> par;
+    SearchNode<T, CUSTOM, SYM> par;
     if (k == 1) {
         uint64_t rb = 0, rc = 0;  // a fixed root is itself one of the subsets searched (item 0 scores it)
         const bool eval = a.root_mask != 0 && item == 0;
@@ -2397,7 +2419,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
     }
     uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0;
     if (par.max_event(a.shift) < j)
-        search_child<T, CUSTOM>(a, par, ParRegs<T>{par.P}, j, p + binom(j, k), best, cnt, best1, cnt1);
+        search_child<T, CUSTOM, SYM>(a, par, ParRegs<T>{par.P}, j, p + binom(j, k), best, cnt, best1, cnt1);
     search_publish(a, a.k, best, cnt);
     if (a.tail) search_publish(a, a.k + 1, best1, cnt1);
 }
@@ -3491,8 +3513,13 @@ hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStrea
         return hipErrorInvalidValue;
     const dim3 grid(unsigned((a.n_child + 63) / 64));
     KF_CUSTOM_DISPATCH(a.kc, {
-        if (f64) ref15_search_head_kernel<double, CUSTOM><<<grid, 64, 0, stream>>>(a);
-        else ref15_search_head_kernel<float, CUSTOM><<<grid, 64, 0, stream>>>(a);
+        if (a.sym) {
+            if (f64) ref15_search_head_kernel<double, CUSTOM, true><<<grid, 64, 0, stream>>>(a);
+            else ref15_search_head_kernel<float, CUSTOM, true><<<grid, 64, 0, stream>>>(a);
+        } else {
+            if (f64) ref15_search_head_kernel<double, CUSTOM, false><<<grid, 64, 0, stream>>>(a);
+            else ref15_search_head_kernel<float, CUSTOM, false><<<grid, 64, 0, stream>>>(a);
+        }
     });
     return hipGetLastError();
 }
@@ -3531,20 +3558,35 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
         const uint64_t waves = (items + 7) / 8 * 8;
         if (waves >= (1ull << 31)) return hipErrorInvalidValue;
         KF_CUSTOM_DISPATCH(a.kc, {
-            if (f64) ref15_search_cm_kernel<double, CUSTOM><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
-            else ref15_search_cm_kernel<float, CUSTOM><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
+            if (a.sym) {
+                if (f64) ref15_search_cm_kernel<double, CUSTOM, true><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
+                else ref15_search_cm_kernel<float, CUSTOM, true><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
+            } else {
+                if (f64) ref15_search_cm_kernel<double, CUSTOM, false><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
+                else ref15_search_cm_kernel<float, CUSTOM, false><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
+            }
         });
         return hipGetLastError();
     }
     KF_CUSTOM_DISPATCH(a.kc, {
         if (!a.pm_regs) {
             const dim3 grid(static_cast<unsigned>((a.n_par + 63) / 64));
-            if (f64) ref15_search_pm_kernel<double, true, CUSTOM><<<grid, 64, 0, stream>>>(a);
-            else ref15_search_pm_kernel<float, true, CUSTOM><<<grid, 64, 0, stream>>>(a);
+            if (a.sym) {
+                if (f64) ref15_search_pm_kernel<double, true, CUSTOM, true><<<grid, 64, 0, stream>>>(a);
+                else ref15_search_pm_kernel<float, true, CUSTOM, true><<<grid, 64, 0, stream>>>(a);
+            } else {
+                if (f64) ref15_search_pm_kernel<double, true, CUSTOM, false><<<grid, 64, 0, stream>>>(a);
+                else ref15_search_pm_kernel<float, true, CUSTOM, false><<<grid, 64, 0, stream>>>(a);
+            }
         } else {
             const dim3 grid(static_cast<unsigned>((a.n_par + kBlock - 1) / kBlock));
-            if (f64) ref15_search_pm_kernel<double, false, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
-            else ref15_search_pm_kernel<float, false, CUSTOM><<<grid, kBlock, 0, stream>>>(a);
+            if (a.sym) {
+                if (f64) ref15_search_pm_kernel<double, false, CUSTOM, true><<<grid, kBlock, 0, stream>>>(a);
+                else ref15_search_pm_kernel<float, false, CUSTOM, true><<<grid, kBlock, 0, stream>>>(a);
+            } else {
+                if (f64) ref15_search_pm_kernel<double, false, CUSTOM, false><<<grid, kBlock, 0, stream>>>(a);
+                else ref15_search_pm_kernel<float, false, CUSTOM, false><<<grid, kBlock, 0, stream>>>(a);
+            }
         }
     });
     return hipGetLastError();

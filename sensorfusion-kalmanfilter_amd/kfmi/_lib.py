@@ -53,7 +53,8 @@ KF_OPT_SCHED_GROUP = 12
 KF_OPT_SCHED_ORDER = 13
 KF_OPT_SCHED_REC_TIME = 14
 KF_OPT_SEARCH_HEAD = 15
-KF_OPT_COUNT = 16
+KF_OPT_SEARCH_SYM = 16
+KF_OPT_COUNT = 17
 
 _ERRNAMES = {KF_EINVAL: 'KF_EINVAL', KF_EHIP: 'KF_EHIP', KF_ENOTSPD: 'KF_ENOTSPD',
              KF_ENODEV: 'KF_ENODEV', KF_ENOMEM: 'KF_ENOMEM'}
@@ -114,6 +115,7 @@ SIGNATURES = {
     'kf_eval_combos': (_i, [_vp, _i, _vp, _vp, _d, _d, _i, ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     'kf_search_combos': (_i, [_vp, _i, _vp, _vp, _d, _d, _d, _i, _i, _i, ctypes.c_uint64,
                               ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_i), _vp, _vp, _vp]),
+    'kf_search_info': (_i, [_vp, _vp]),
     'kf_score_candidates': (_i, [_vp, _i, _vp, _i, _vp, _vp, _vp]),
     'kf_score_rows': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp]),
     'kf_run_scheduled': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _d, _vp, _vp, _vp, _vp, _vp]),

@@ -40,6 +40,7 @@ OPTIONS = {
     'search_kernel': (_lib.KF_OPT_SEARCH_KERNEL, {'auto': 0, 'cm': 1, 'pm': 2}),
     'search_pm': (_lib.KF_OPT_SEARCH_PM, {'auto': 0, 'lds': 0, 'regs': 1}),
     'search_head': (_lib.KF_OPT_SEARCH_HEAD, {'auto': 0, 'on': 0, 'off': 1}),
+    'search_sym': (_lib.KF_OPT_SEARCH_SYM, {'auto': 0, 'on': 0, 'off': 1}),
     'sched_kernel': (_lib.KF_OPT_SCHED_KERNEL, {'auto': 0, 'regs': 1, 'fused': 2, 'two_pass': 3, 'one_launch': 4}),
     'sched_group': (_lib.KF_OPT_SCHED_GROUP, {'auto': 0, 'wave': 1, 'block': 4}),
     'sched_order': (_lib.KF_OPT_SCHED_ORDER, {'auto': 0, 'heaviest_first': 0, 'batch': 1}),
@@ -438,6 +439,14 @@ class BatchedKF:
                                           self._stream()))
         combo = tuple(i for i in range(n) if (win.value >> i) & 1) if kf.value else None
         return kf.value, combo, acc, sm
+
+    def search_info(self):
+        """How the last search_combos ran (kf_search_info): axis-symmetric or not, the sizes its
+        head launch covered, its level launches after the head, the bytes of one level buffer."""
+        out = np.zeros(4, dtype=np.int64)
+        check(_lib.lib().kf_search_info(self.handle, out.ctypes.data_as(ctypes.c_void_p)))
+        return {'sym': bool(out[0]), 'head_sizes': int(out[1]), 'level_launches': int(out[2]),
+                'level_bytes': int(out[3])}
 
     def score_candidates(self, types, full=False, posterior=False):
         """KF_MODEL_REF15 scheduler scoring (kf_score_candidates): [len(types), B] traces of the

@@ -279,6 +279,106 @@ def test_search_head_equals_level_search(golden_dir, n_fixed, fixed_mask):
     np.testing.assert_array_equal(a[1][2], b[1][2])
 
 
+def _axis_symmetric(init):
+    """init with the x axis's covariance blocks copied to the y and z axes."""
+    out = np.array(init, dtype=np.float64)
+    b = out[15:]
+    for c in (1, 2):
+        b[6 * c:6 * c + 6] = b[0:6]
+        b[18 + 3 * c:18 + 3 * c + 3] = b[18:21]
+    return out
+
+
+def _symmetric_consts(seed):
+    """Caller constants that are the same on the three axes (one value per state group)."""
+    rng = np.random.default_rng(seed)
+    g = lambda lo, hi: np.repeat(rng.uniform(lo, hi, 5), 3)  # noqa: E731 (pos, att, vel, rate, acc)
+    return ref15.ModelConsts('ref15', q=g(0.01, 8.0), r_imu=g(0.02, 120.0), r_gps=np.full(3, rng.uniform(0.5, 9.0)),
+                             p0=g(20.0, 2e4))
+
+
+def _gap_threshold(vals, q):
+    """A threshold near quantile q of the finite scores, midway in a gap between two consecutive
+    ones of at least 1e-9 relative, so rounding-level differences cannot move a subset across it."""
+    v = np.unique(vals[np.isfinite(vals)])
+    i = int(q * (len(v) - 1))
+    while i + 1 < len(v) and v[i + 1] - v[i] <= 1e-9 * max(abs(v[i]), 1.0):
+        i += 1
+    return float(0.5 * (v[i] + v[i + 1]))
+
+
+@pytest.mark.parametrize('consts', ['reference', 'custom'])
+@pytest.mark.parametrize('kernel,pm', [('cm', 'auto'), ('pm', 'lds'), ('pm', 'regs')])
+@pytest.mark.parametrize('dtype', ['f64', 'f32'])
+def test_search_axis_symmetric_equals_every_chain(golden_dir, dtype, kernel, pm, consts):
+    """KF_OPT_SEARCH_SYM: with the same constants and root blocks on the three axes the search
+    computes and stores one pva and one aw chain for the three of each.  Every subset's max
+    log-det equals the every-chain search's to rounding (the three chains' copies of the same
+    arithmetic are compiled separately there, and round alike in ~98 % of subsets, one ulp
+    apart in the rest), and both equal the per-subset kernel's to 1e-12; the acceptance counts
+    and the winner (exhaustive and not) are the same, on each search kernel, with the head and
+    without, in both precisions."""
+    n = 14
+    cand, ev, init, t0, target = _search_case(golden_dir, n)
+    init = _axis_symmetric(init)
+    params = _symmetric_consts(5).params() if consts == 'custom' else None
+    tol = 1e-14 if dtype == 'f64' else 1e-6
+    out = {}
+    for sym in ('on', 'off'):
+        res = []
+        for head in ('on', 'off'):
+            kf = kfmi.BatchedKF('ref15', 1, dtype, params=params,
+                                options={'search_kernel': kernel, 'search_pm': pm, 'search_sym': sym, 'search_head': head})
+            _, _, _, sm = kf.search_combos(ev, init, t0, target, -1e30, exhaustive=True, subset_max=True)
+            info = kf.search_info()
+            sm = sm.double().cpu().numpy()
+            assert info['sym'] == (sym == 'on') and (info['head_sizes'] > 0) == (head == 'on'), info
+            res.append(sm)
+            kf.close()
+        out[sym] = res
+    ref = out['off'][0]
+    assert np.isnan(ref[0]) and np.isfinite(ref[1:]).all()
+    for sm in out['on'] + out['off'][1:]:
+        assert np.isnan(sm[0])
+        assert np.max(np.abs(sm[1:] - ref[1:]) / np.maximum(np.abs(ref[1:]), 1.0)) <= tol
+    for q in (0.02, 0.4):
+        thr = _gap_threshold(ref[1:], q)
+        got = {}
+        for sym in ('on', 'off'):
+            kf = kfmi.BatchedKF('ref15', 1, dtype, params=params,
+                                options={'search_kernel': kernel, 'search_pm': pm, 'search_sym': sym})
+            ex = kf.search_combos(ev, init, t0, target, thr, exhaustive=True)
+            first = kf.search_combos(ev, init, t0, target, thr, exhaustive=False)
+            kf.close()
+            got[sym] = (ex, first)
+        (ea, fa), (eb, fb) = got['on'], got['off']
+        assert ea[:2] == eb[:2] == fa[:2] == fb[:2] and ea[0] > 0, q
+        np.testing.assert_array_equal(ea[2], eb[2])
+
+
+def test_search_axis_symmetry_detected_exactly(golden_dir):
+    """The axis-symmetric search runs only where it is exact: the handle's constants the same on
+    the three axes and the root covariance's blocks equal bit for bit.  One ulp off in one block,
+    or one axis's constant changed, and the search runs every chain (and agrees with the oracle
+    as before)."""
+    n = 9
+    cand, ev, init, t0, target = _search_case(golden_dir, n)
+    sym_init = _axis_symmetric(init)
+    off_init = sym_init.copy()
+    off_init[15 + 6 + 2] = np.nextafter(off_init[15 + 6 + 2], np.inf)  # y axis, pva block entry (0, 2)
+    c = _symmetric_consts(6)
+    q = c.q.copy()
+    q[13] *= 1.5  # the y axis's acceleration noise
+    asym = ref15.ModelConsts('ref15', q=q, r_imu=c.r_imu, r_gps=c.r_gps, p0=c.p0)
+    cases = [(None, sym_init, True), (None, off_init, False), (c.params(), sym_init, True),
+             (asym.params(), sym_init, False)]
+    for params, ini, want in cases:
+        kf = kfmi.BatchedKF('ref15', 1, 'f64', params=params)
+        kf.search_combos(ev, ini, t0, target, -1e30, exhaustive=True)
+        assert kf.search_info()['sym'] == want
+        kf.close()
+
+
 @pytest.mark.parametrize('w', [1, 3])
 def test_search_classes_partition_the_search(golden_dir, w):
     """The per-GPU shards of kfmi.dist.brute_force_search: searches restricted to the subsets

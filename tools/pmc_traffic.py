@@ -113,6 +113,10 @@ def main():
                 info['fetch_bytes_calibrated'] *= nl
             write = 1024 * sum(w) / (len(w) / nl)
             alg = 2 * sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in range(max(K, 1), n))
+            with open(os.path.join(out_dir, 'cfgbf_FETCH_SIZE.log')) as fh:  # the bench line's own count
+                for line in fh:
+                    if line.startswith('{"metric"'):
+                        alg = json.loads(line)['roofline']['algorithmic_bytes_per_launch']
             res['configbf'] = {
                 'fetch_bytes_raw': 1024 * sum(f) / (len(f) / nl), 'write_bytes_raw': write,
                 'bytes_per_launch': fb + write * write_scale,
