@@ -939,7 +939,8 @@ def bf_workload(cfg, args, rank, world, dev):
         return dict(step=step, units=total_steps, bytes=2 * lvl, bytes_per_unit=2 * lvl / total_combos,
                     kernel=f'ref15_search_head_kernel (sizes 1..{K}) + ref15_search_cm/pm_kernel (the '
                            f'{launches} launches of one search)',
-                    traffic=load_traffic('bf', 2 * lvl), cpu=cpu,
+                    traffic=load_traffic('bf', 2 * lvl), valu=load_valu('bf') if load_traffic('bf', 2 * lvl) else None,
+                    cpu=cpu,
                     gather=None, kf=kf, combos=total_combos,
                     roofline_note='level-buffer bytes only (each stored prefix filter written and read once, the '
                                   'subsets holding candidate n-2 scored from registers); the search is fp64 issue / '

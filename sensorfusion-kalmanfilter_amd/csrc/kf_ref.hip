@@ -2211,10 +2211,14 @@ __device__ __forceinline__ void search_publish(const Ref15SearchArgs& a, int k, 
 #ifndef KF_SEARCH_PM_WAVES
 #define KF_SEARCH_PM_WAVES 2  // waves per SIMD of the register variant (its VGPR budget)
 #endif
+#ifndef KF_SEARCH_SYM_WAVES
+#define KF_SEARCH_SYM_WAVES 3  // waves per SIMD of the axis-symmetric search kernels (A/B builds)
+#endif
 // PLDS: the parent's covariance lives in LDS (one 64-lane block per workgroup, [27][64] T),
 // which fits the kernel in 3 waves per SIMD without spills; otherwise in registers.
 template <typename T, bool PLDS, bool CUSTOM, bool SYM>
-__global__ __launch_bounds__(PLDS ? 64 : kBlock) __attribute__((amdgpu_waves_per_eu(PLDS ? 3 : KF_SEARCH_PM_WAVES))) void
+__global__ __launch_bounds__(PLDS ? 64 : kBlock) __attribute__((
+    amdgpu_waves_per_eu(SYM ? KF_SEARCH_SYM_WAVES : PLDS ? 3 : KF_SEARCH_PM_WAVES))) void
 ref15_search_pm_kernel(const Ref15SearchArgs a) {
     constexpr int NT = PLDS ? 64 : kBlock;
     constexpr int NR = SearchNode<T, CUSTOM, SYM>::NR;
@@ -2267,7 +2271,7 @@ ref15_search_pm_kernel(const Ref15SearchArgs a) {
 // a.n_child = sum_{k <= K} C(n, k).  Every lane stays to the end (the publish reductions read
 // every lane).
 template <typename T, bool CUSTOM, bool SYM>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void ref15_search_head_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEARCH_SYM_WAVES : 3))) void ref15_search_head_kernel(
     const Ref15SearchArgs a) {
     using Node = SearchNode<T, CUSTOM, SYM>;
     constexpr int RP = SYM ? M15::NP : 1, RA = SYM ? M15::NA : 1;
@@ -2379,7 +2383,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void re
 // re-read it from that XCD's L2.  Blocks are grouped by their first parent's largest event v
 // (non-decreasing in colex order); a block of group v has items j = v + 1 .. n - 1.
 template <typename T, bool CUSTOM, bool SYM>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void ref15_search_cm_kernel(const Ref15SearchArgs a,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEARCH_SYM_WAVES : 3))) void ref15_search_cm_kernel(const Ref15SearchArgs a,
                                                                                                      uint64_t n_items) {
     const uint64_t per_xcd = (n_items + 7) / 8;
     const uint64_t item = uint64_t(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;

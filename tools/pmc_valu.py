@@ -39,12 +39,41 @@ def kernel_trace_ms(out_dir, c, kern):
     raise SystemExit(f'no kernel-trace row for {kern!r} under {out_dir}/kt{c}')
 
 
+def search_valu(out_dir, rec):
+    """bf: one search = its head and level launches (every ref15_search_* dispatch), counters and
+    kernel-trace durations summed per search; a unit is one subset."""
+    import csv
+    import glob
+    d = os.path.join(out_dir, 'cfgbf')
+    searches = len(pick(per_kernel(d, 'SQ_WAVES'), 'ref15_search_head'))
+    vals = {ctr: sum(v for k, vs in per_kernel(d, ctr).items() if 'ref15_search' in k for v in vs) / searches
+            for ctr in COUNTERS}
+    tot, heads = 0.0, 0
+    for f in glob.glob(os.path.join(out_dir, 'ktbf', '**', '*kernel_stats.csv'), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if 'ref15_search' in r['Name']:
+                    tot += float(r['TotalDurationNs'])
+                    heads += int(r['Calls']) if 'search_head' in r['Name'] else 0
+    ms = tot * 1e-6 / heads
+    wave_units = rec['config']['combinations'] / 64
+    return dict(kernel='ref15_search_head/cm/pm_kernel (one search)', counters_per_launch=vals, kernel_ms=ms,
+                launches_profiled=searches, valu_per_wave_step=vals['SQ_INSTS_VALU'] / wave_units,
+                valu_issue_frac=vals['SQ_INSTS_VALU'] * CYC / (ms * 1e-3 * CLK * SIMDS),
+                wave_cycles_waiting_frac=vals['SQ_WAIT_ANY'] / vals['SQ_WAVE_CYCLES'],
+                wave_cycles_issue_stall_frac=vals['SQ_WAIT_INST_ANY'] / vals['SQ_WAVE_CYCLES'],
+                unit='one subset (valu_per_wave_step: per 64 subsets)')
+
+
 def main():
     out_dir, cfgs = sys.argv[1], sys.argv[2:]
     res = {'note': ' '.join(__doc__.split('\n\n')[2].split())}
     for c in cfgs:
         d = os.path.join(out_dir, f'cfg{c}')
         rec = bench_line(os.path.join(out_dir, f'cfg{c}.log'))
+        if c == 'bf':
+            res['configbf'] = search_valu(out_dir, rec)
+            continue
         units = rec['value'] * rec['ms_per_step'] * 1e-3        # filter-steps (events) per launch
         wave_steps = units / 64
         if c == 'sched' and 'apply' in rec['roofline']['kernel']:
