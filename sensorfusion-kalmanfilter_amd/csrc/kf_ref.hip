@@ -1399,14 +1399,19 @@ __device__ __forceinline__ void lft_event(double (&v)[6], int type, double dt, b
 #endif
 constexpr int kLftHalves = KF_LFT_HALVES;
 static_assert(6 % kLftHalves == 0, "columns per lane");
+// lanes per product: a power of two for the max exchange (3 / 6 column lanes: one / two lanes
+// duplicate the last column and store nothing)
+constexpr int kLftStride = kLftHalves == 3 ? 4 : kLftHalves == 6 ? 8 : kLftHalves;
 template <typename T, class M, bool CUSTOM>
 __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArgs a) {
     constexpr int NCH = M::NP + M::NA;
     constexpr int NJ = 6 / kLftHalves;  // columns per lane
     const int64_t gl = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (gl >= a.C * a.np * NCH * kLftHalves) return;
-    const int64_t grp = gl / kLftHalves;  // (chunk * np + piece) * NCH + chain
-    const int j0 = int(gl % kLftHalves) * NJ;
+    if (gl >= a.C * a.np * NCH * kLftStride) return;  // whole products (kLftStride divides the wave)
+    const int64_t grp = gl / kLftStride;  // (chunk * np + piece) * NCH + chain
+    const int li = int(gl % kLftStride);
+    const bool own = li < kLftHalves;
+    const int j0 = (own ? li : kLftHalves - 1) * NJ;
     const int64_t cp = grp / NCH;  // chunk * np + piece
     const int ch = int(grp % NCH);
     const bool pva = ch < M::NP;
@@ -1454,7 +1459,7 @@ __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArg
 #pragma unroll
                 for (int i = 0; i < 6; ++i) mx = fmax(mx, fabs(v[j][i]));
 #pragma unroll
-            for (int sh = 1; sh < kLftHalves; sh <<= 1) mx = fmax(mx, __shfl_xor(mx, sh, 64));
+            for (int sh = 1; sh < kLftStride; sh <<= 1) mx = fmax(mx, __shfl_xor(mx, sh, 64));
             int ex;
             (void)frexp(mx, &ex);
             const double sc = ldexp(1.0, -ex);
@@ -1464,6 +1469,7 @@ __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArg
                 for (int i = 0; i < 6; ++i) v[j][i] *= sc;
         }
     }
+    if (!own) return;
     double* o = a.phi + grp * 36;
 #pragma unroll
     for (int i = 0; i < 6; ++i)
@@ -3448,8 +3454,8 @@ void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
             break;
         }
         case kStreamPhaseLftMaps:
-            if (a.kc) stream_lft_maps_kernel<T, M, true><<<grid(a.C * a.np * NCH * kLftHalves), kBlock, 0, stream>>>(a);
-            else stream_lft_maps_kernel<T, M, false><<<grid(a.C * a.np * NCH * kLftHalves), kBlock, 0, stream>>>(a);
+            if (a.kc) stream_lft_maps_kernel<T, M, true><<<grid(a.C * a.np * NCH * kLftStride), kBlock, 0, stream>>>(a);
+            else stream_lft_maps_kernel<T, M, false><<<grid(a.C * a.np * NCH * kLftStride), kBlock, 0, stream>>>(a);
             break;
         case kStreamPhaseLftStart: {
             const int64_t bc = a.g > 0 ? a.G : kBlock;
