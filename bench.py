@@ -935,7 +935,7 @@ def bf_workload(cfg, args, rank, world, dev):
         # stores only its level K
         lvl = sum(search_level_bytes(math.comb(n - 2, k), 'f64', sym) for k in range(max(K, 1), n))
         chains = ('axis-symmetric: one pva and one aw chain computed and stored for the three of each, '
-                  'KF_OPT_SEARCH_SYM' if sym else 'every chain')
+                  'KF_OPT_AXIS_SYM' if sym else 'every chain')
         return dict(step=step, units=total_steps, bytes=2 * lvl, bytes_per_unit=2 * lvl / total_combos,
                     kernel=f'ref15_search_head_kernel (sizes 1..{K}) + ref15_search_cm/pm_kernel (the '
                            f'{launches} launches of one search)',

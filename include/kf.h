@@ -147,13 +147,15 @@ const char* kf_version(void);
  *   KF_OPT_SEARCH_PM      kf_search_combos' parent-major kernel: 0 = parent in LDS, 1 = registers
  *   KF_OPT_SEARCH_HEAD    kf_search_combos: 0 = the first levels (sizes whose subsets need few event
  *                         steps in all) in one launch, one lane per subset; 1 = level by level
- *   KF_OPT_SEARCH_SYM     kf_search_combos: 0 = where the handle's noise constants are the same on
- *                         the three axes and so are the init covariance's blocks (bit for bit),
- *                         the three pva chains carry one covariance, and so do the three aw
- *                         chains: one of each is computed and stored (the every-chain search's
- *                         results to rounding: its three compiled copies of a chain's arithmetic
- *                         round alike in ~98 % of subsets, one ulp apart in the rest); 1 = every
- *                         chain
+ *   KF_OPT_AXIS_SYM       0 = where the handle's noise constants are the same on every axis
+ *                         (the reference's), work that depends on the constants alone is done
+ *                         once for the axes' identical chains: kf_run_stream's covariance maps
+ *                         (one pva and one aw chain's maps stand for all: the same numbers, bit
+ *                         for bit); kf_search_combos when the init covariance's axis blocks are
+ *                         also equal bit for bit (one pva and one aw chain computed and stored:
+ *                         the every-chain search's results to rounding, its three compiled
+ *                         copies of a chain's arithmetic rounding alike in ~98 % of subsets, one
+ *                         ulp apart in the rest); 1 = every chain
  *   KF_OPT_SCHED_KERNEL   kf_run_scheduled: 0 = auto (the two passes where legal, as 3), 1 = the
  *                         fused register-input kernel, 2 = the fused LDS-input kernel, 3 = the
  *                         pick and apply passes as two launches, 4 = as the two phases of one
@@ -185,7 +187,7 @@ const char* kf_version(void);
 #define KF_OPT_SCHED_ORDER    13
 #define KF_OPT_SCHED_REC_TIME 14
 #define KF_OPT_SEARCH_HEAD    15
-#define KF_OPT_SEARCH_SYM     16
+#define KF_OPT_AXIS_SYM       16
 #define KF_OPT_COUNT          17
 int kf_set_option(kf_batch* handle, int option, int64_t value);
 int kf_get_option(const kf_batch* handle, int option, int64_t* value);
@@ -374,14 +376,14 @@ int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const d
  * one holding n - 2 only the one adding n - 1, which is scored from registers); C(n - 2, k)
  * must stay below 2^28, and the handle's level buffers take 2 * C(n - 2, k) * (28 w + 16)
  * bytes at the widest stored level (w = 8 for f64, 4 for f32; n = free candidates; 10 w + 16
- * for an axis-symmetric search, KF_OPT_SEARCH_SYM).  The call synchronises `stream`. */
+ * for an axis-symmetric search, KF_OPT_AXIS_SYM).  The call synchronises `stream`. */
 int kf_search_combos(kf_batch* handle, int n_events, const double* events, const double* init,
                      double prev_time, double target_end, double threshold, int k_max, int exhaustive,
                      int n_fixed, uint64_t fixed_mask, uint64_t* winner, int* k_found,
                      uint64_t* n_accepted, void* subset_max, void* stream);
 
 /* The last kf_search_combos on this handle: out[0] = 1 if it ran axis-symmetric
- * (KF_OPT_SEARCH_SYM: one pva and one aw chain for the three of each), out[1] = the sizes its
+ * (KF_OPT_AXIS_SYM: one pva and one aw chain for the three of each), out[1] = the sizes its
  * head launch covered (KF_OPT_SEARCH_HEAD; 0 = none), out[2] = its level launches after the
  * head, out[3] = the bytes of one of its two level buffers.  All 0 before the first search. */
 int kf_search_info(const kf_batch* handle, int64_t* out);

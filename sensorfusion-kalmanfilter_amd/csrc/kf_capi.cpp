@@ -329,6 +329,49 @@ int flush_predict(kf_batch* h, void* stream, const char* what) {
     return note_pend_reader(h, stream, what);
 }
 
+// KF_OPT_AXIS_SYM: the handle's noise constants are the same on every axis, bit for bit — REF15:
+// pos / vel / acc and att / rate of axes 1 and 2 those of axis 0, and R_gps; REF8: x's and y's
+// (pos, vel, acc) chains (its heading chain is the only aw chain) — so work that depends on the
+// constants alone is the same for the axes' chains
+bool same_bits(double a, double b) { return std::memcmp(&a, &b, sizeof a) == 0; }
+
+bool axis_sym_consts(const kf_batch* h) {
+    if (opt(h, KF_OPT_AXIS_SYM) == 1) return false;
+    const kf_params& p = h->params;
+    auto same_state = [&](int s, int t) {
+        return same_bits(p.ref_q[s], p.ref_q[t]) && same_bits(p.ref_r_imu[s], p.ref_r_imu[t]);
+    };
+    if (h->model == KF_MODEL_REF15) {
+        for (int c = 1; c < 3; ++c) {
+            for (int s : {0, 6, 12, 3, 9})
+                if (!same_state(s + c, s)) return false;
+            if (!same_bits(p.ref_r_gps[c], p.ref_r_gps[0])) return false;
+        }
+        return true;
+    }
+    if (h->model == KF_MODEL_REF8) {
+        for (int s : {0, 3, 6})
+            if (!same_state(s + 1, s)) return false;
+        return same_bits(p.ref_r_gps[1], p.ref_r_gps[0]);
+    }
+    return false;
+}
+
+// kf_search_combos' axis-symmetric variant (Ref15SearchArgs::sym): axis-symmetric constants and
+// the root covariance's blocks init[15 ..] equal on the three axes (bit for bit), so every
+// covariance the search reaches has three equal pva blocks and three equal aw blocks
+bool search_sym(const kf_batch* h, const double* init) {
+    if (!axis_sym_consts(h)) return false;
+    const double* blk = init + 15;
+    for (int c = 1; c < 3; ++c) {
+        for (int i = 0; i < 6; ++i)
+            if (!same_bits(blk[6 * c + i], blk[i])) return false;
+        for (int i = 0; i < 3; ++i)
+            if (!same_bits(blk[18 + 3 * c + i], blk[18 + i])) return false;
+    }
+    return true;
+}
+
 }  // namespace
 
 namespace kfmi {
@@ -359,7 +402,7 @@ int kf_set_option(kf_batch* h, int option, int64_t value) {
         case KF_OPT_STREAM_FINAL:
         case KF_OPT_SEARCH_PM:
         case KF_OPT_SEARCH_HEAD: ok = value == 0 || value == 1; break;
-        case KF_OPT_SEARCH_SYM: ok = value == 0 || value == 1; break;
+        case KF_OPT_AXIS_SYM: ok = value == 0 || value == 1; break;
         case KF_OPT_SCHED_KERNEL: ok = value >= 0 && value <= 4; break;
         case KF_OPT_SCHED_GROUP: ok = value == 0 || value == 1 || value == 4; break;
         case KF_OPT_SCHED_ORDER:
@@ -918,6 +961,7 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     sa.tol_cov = h->dtype == KF_F64 ? 1e-12 : 1e-5;
     sa.start_threads = int(opt(h, KF_OPT_START_THREADS));
     sa.kc = h->kc;
+    sa.sym = axis_sym_consts(h);
     sa.hx = h->x;
     sa.hP = h->P;
     sa.hstatus = h->status;
@@ -1094,27 +1138,6 @@ int kf_eval_combos(kf_batch* h, int n_events, const double* events, const double
     a.n_records = n_records;
     hipError_t e = kfmi::launch_ref15_combos(h->dtype == KF_F64, a, st);
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_eval_combos");
-}
-
-// kf_search_combos' axis-symmetric variant (Ref15SearchArgs::sym): the handle's noise constants are
-// the same on the three axes — pos / vel / acc and att / rate of axis c those of axis 0, R_gps[c]
-// R_gps[0] — and so are the blocks of the root covariance init[15 ..] (bit for bit), so every
-// covariance the search reaches has three equal pva blocks and three equal aw blocks
-static bool search_sym(const kf_batch* h, const double* init) {
-    if (opt(h, KF_OPT_SEARCH_SYM) == 1) return false;
-    const kf_params& p = h->params;
-    auto same = [](double a, double b) { return std::memcmp(&a, &b, sizeof a) == 0; };
-    const double* blk = init + 15;
-    for (int c = 1; c < 3; ++c) {
-        for (int s : {0, 6, 12, 3, 9})
-            if (!same(p.ref_q[s + c], p.ref_q[s]) || !same(p.ref_r_imu[s + c], p.ref_r_imu[s])) return false;
-        if (!same(p.ref_r_gps[c], p.ref_r_gps[0])) return false;
-        for (int i = 0; i < 6; ++i)
-            if (!same(blk[6 * c + i], blk[i])) return false;
-        for (int i = 0; i < 3; ++i)
-            if (!same(blk[18 + 3 * c + i], blk[18 + i])) return false;
-    }
-    return true;
 }
 
 int kf_search_combos(kf_batch* h, int n_events, const double* events, const double* init, double prev_time,

@@ -144,6 +144,9 @@ struct StreamArgs {
     int64_t G;               // chunks per block of the start kernel (their windows' maps staged in LDS)
     int64_t g;               // chunks per thread of the start kernel; 0: no LDS, one chunk per thread
     int start_threads;       // threads per block of the start kernel (KF_OPT_START_THREADS); 0 = kBlock
+    int sym;                 // KF_OPT_AXIS_SYM: the constants are the same on every axis, so the
+                             // covariance maps of one pva and one aw chain (chains 0 and NP) stand
+                             // for every chain (lft_maps computes only those; lft_start reads them)
     const RefConsts* kc;     // the handle's noise constants, or nullptr (the reference's)
     // records from the map pass (no final pass): the map bank's trajectories per variant
     const void* traj4;       // [4][vstride][NTRAJ]
@@ -232,7 +235,7 @@ struct Ref15SearchArgs {
     bool sym;                // axis-symmetric: the noise constants and the root's blocks are the same on
                              // the three axes, so the three pva chains (and the three aw chains) carry
                              // the same covariance; one of each is computed and stored
-                             // (KF_OPT_SEARCH_SYM)
+                             // (KF_OPT_AXIS_SYM)
     const RefConsts* kc;     // the handle's noise constants, or nullptr (the reference's)
 };
 

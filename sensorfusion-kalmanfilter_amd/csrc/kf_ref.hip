@@ -1402,18 +1402,30 @@ static_assert(6 % kLftHalves == 0, "columns per lane");
 // lanes per product: a power of two for the max exchange (3 / 6 column lanes: one / two lanes
 // duplicate the last column and store nothing)
 constexpr int kLftStride = kLftHalves == 3 ? 4 : kLftHalves == 6 ? 8 : kLftHalves;
+// a.sym: the maps of chains 0 (pva) and NP (aw) only, which stand for every chain
+template <class M>
+__host__ __device__ constexpr int lft_map_chains(bool sym) {
+    return sym ? 1 + (M::NA > 0 ? 1 : 0) : M::NP + M::NA;
+}
+template <class M>
+__device__ __forceinline__ int lft_map_chain(bool sym, int ch) {  // whose maps chain ch uses
+    return sym ? (ch < M::NP ? 0 : M::NP) : ch;
+}
 template <typename T, class M, bool CUSTOM>
 __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArgs a) {
     constexpr int NCH = M::NP + M::NA;
     constexpr int NJ = 6 / kLftHalves;  // columns per lane
+    const int nmc = lft_map_chains<M>(a.sym != 0);
     const int64_t gl = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (gl >= a.C * a.np * NCH * kLftStride) return;  // whole products (kLftStride divides the wave)
-    const int64_t grp = gl / kLftStride;  // (chunk * np + piece) * NCH + chain
+    if (gl >= a.C * a.np * nmc * kLftStride) return;  // whole products (kLftStride divides the wave)
+    const int64_t gm = gl / kLftStride;  // (chunk * np + piece) * nmc + map chain
     const int li = int(gl % kLftStride);
     const bool own = li < kLftHalves;
     const int j0 = (own ? li : kLftHalves - 1) * NJ;
-    const int64_t cp = grp / NCH;  // chunk * np + piece
-    const int ch = int(grp % NCH);
+    const int64_t cp = gm / nmc;  // chunk * np + piece
+    const int cm = int(gm % nmc);
+    const int ch = a.sym ? (cm == 0 ? 0 : M::NP) : cm;
+    const int64_t grp = cp * NCH + ch;  // the map's slot
     const bool pva = ch < M::NP;
     double q[3], si[3], sg;
     chain_noise<M, CUSTOM>(ch, q, si, sg, a.kc);
@@ -1580,7 +1592,7 @@ __global__ __launch_bounds__(kBlock) void stream_lft_start_kernel(const StreamAr
         // 32-bit indices (a 64-bit division is a ~100-instruction sequence per element), 16 loads
         // in flight per thread (a load-store loop waited one memory latency per element)
         const uint32_t n = uint32_t(we > ws ? we - ws : 0) * uint32_t(a.np) * 36u;
-        const double* src = a.phi + (ws * a.np * NCH + ch) * 36;
+        const double* src = a.phi + (ws * a.np * NCH + lft_map_chain<M>(a.sym != 0, ch)) * 36;
         constexpr int kU = 16;
         const uint32_t nt = blockDim.x;
         for (uint32_t e0 = uint32_t(tid); e0 < n; e0 += kU * nt) {
@@ -1639,7 +1651,7 @@ __global__ __launch_bounds__(kBlock) void stream_lft_start_kernel(const StreamAr
 #pragma unroll
                 for (int e = 0; e < 36; ++e) m[e] = src[uint32_t(e) * nu];
             } else {
-                const double* src = a.phi + (u * NCH + ch) * 36;
+                const double* src = a.phi + (u * NCH + lft_map_chain<M>(a.sym != 0, ch)) * 36;
 #pragma unroll
                 for (int e = 0; e < 36; ++e) m[e] = src[e];
             }
@@ -3453,10 +3465,12 @@ void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
             stream_starts_kernel<T, M><<<g, kScanTile, 0, stream>>>(a);
             break;
         }
-        case kStreamPhaseLftMaps:
-            if (a.kc) stream_lft_maps_kernel<T, M, true><<<grid(a.C * a.np * NCH * kLftStride), kBlock, 0, stream>>>(a);
-            else stream_lft_maps_kernel<T, M, false><<<grid(a.C * a.np * NCH * kLftStride), kBlock, 0, stream>>>(a);
+        case kStreamPhaseLftMaps: {
+            const int64_t lanes = a.C * a.np * lft_map_chains<M>(a.sym != 0) * kLftStride;
+            if (a.kc) stream_lft_maps_kernel<T, M, true><<<grid(lanes), kBlock, 0, stream>>>(a);
+            else stream_lft_maps_kernel<T, M, false><<<grid(lanes), kBlock, 0, stream>>>(a);
             break;
+        }
         case kStreamPhaseLftStart: {
             const int64_t bc = a.g > 0 ? a.G : kBlock;
             // LDS variant: G / g threads walk, but the whole block stages the window maps (more

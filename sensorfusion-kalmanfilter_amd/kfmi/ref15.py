@@ -639,7 +639,7 @@ def brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype='f64', d
 
 def search_level_bytes(nodes, dtype, sym=False):
     """Device bytes of one kf_search_combos level buffer (node blocks of 64, kf_internal.h; an
-    axis-symmetric search's nodes hold 10 rows instead of 28, KF_OPT_SEARCH_SYM)."""
+    axis-symmetric search's nodes hold 10 rows instead of 28, KF_OPT_AXIS_SYM)."""
     w = 8 if dtype == 'f64' else 4
     return (nodes + 63) // 64 * 64 * ((10 if sym else 28) * w + 16)
 

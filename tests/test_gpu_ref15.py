@@ -311,7 +311,7 @@ def _gap_threshold(vals, q):
 @pytest.mark.parametrize('kernel,pm', [('cm', 'auto'), ('pm', 'lds'), ('pm', 'regs')])
 @pytest.mark.parametrize('dtype', ['f64', 'f32'])
 def test_search_axis_symmetric_equals_every_chain(golden_dir, dtype, kernel, pm, consts):
-    """KF_OPT_SEARCH_SYM: with the same constants and root blocks on the three axes the search
+    """KF_OPT_AXIS_SYM: with the same constants and root blocks on the three axes the search
     computes and stores one pva and one aw chain for the three of each.  Every subset's max
     log-det equals the every-chain search's to rounding (the three chains' copies of the same
     arithmetic are compiled separately there, and round alike in ~98 % of subsets, one ulp
@@ -328,7 +328,7 @@ def test_search_axis_symmetric_equals_every_chain(golden_dir, dtype, kernel, pm,
         res = []
         for head in ('on', 'off'):
             kf = kfmi.BatchedKF('ref15', 1, dtype, params=params,
-                                options={'search_kernel': kernel, 'search_pm': pm, 'search_sym': sym, 'search_head': head})
+                                options={'search_kernel': kernel, 'search_pm': pm, 'axis_sym': sym, 'search_head': head})
             _, _, _, sm = kf.search_combos(ev, init, t0, target, -1e30, exhaustive=True, subset_max=True)
             info = kf.search_info()
             sm = sm.double().cpu().numpy()
@@ -346,7 +346,7 @@ def test_search_axis_symmetric_equals_every_chain(golden_dir, dtype, kernel, pm,
         got = {}
         for sym in ('on', 'off'):
             kf = kfmi.BatchedKF('ref15', 1, dtype, params=params,
-                                options={'search_kernel': kernel, 'search_pm': pm, 'search_sym': sym})
+                                options={'search_kernel': kernel, 'search_pm': pm, 'axis_sym': sym})
             ex = kf.search_combos(ev, init, t0, target, thr, exhaustive=True)
             first = kf.search_combos(ev, init, t0, target, thr, exhaustive=False)
             kf.close()

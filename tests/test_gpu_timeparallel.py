@@ -166,6 +166,35 @@ def test_records_updated_cov_ref8(final_pass):
             assert _rel(a, b) <= 1e-9
 
 
+@pytest.mark.parametrize('model', ['ref15', 'ref8'])
+@pytest.mark.parametrize('dtype', ['f64', 'f32'])
+def test_axis_symmetric_maps_equal_every_chain(model, dtype):
+    """KF_OPT_AXIS_SYM: with the reference's constants (the same on every axis) the stream
+    computes the covariance maps of one pva and one aw chain for all; the maps of the others are
+    the same arithmetic on the same numbers, so every record, the final state and covariance and
+    the device check equal the every-chain run's bit for bit."""
+    T = 70000
+    et, dt, pay, x0 = _stream(T, seed=21, skips=10)
+    n = 15 if model == 'ref15' else 8
+    outs = []
+    for sym in ('on', 'off'):
+        kf = kfmi.BatchedKF(model, 1, dtype, options={'axis_sym': sym})
+        P0 = kf.state()[1].cpu().numpy()
+        xs = np.zeros((n, 1), P0.dtype)
+        xs[0:2, 0] = x0[0:2]
+        kf.set_state(xs, P0)
+        tr, ld, up, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None].astype(P0.dtype), updated=True,
+                                       cov=True)
+        chk = kf.stream_check()
+        assert chk['ok'] and chk['chunks'] > 1, chk
+        x, P = kf.state()
+        outs.append((tuple(v.cpu().numpy() for v in (tr, ld, up, cv, x, P)), chk['cov_gap']))
+        kf.close()
+    for a, b in zip(outs[0][0], outs[1][0]):
+        np.testing.assert_array_equal(a, b)
+    assert outs[0][1] == outs[1][1]
+
+
 def test_run_full_stream_parallel_matches_single_filter():
     """run_kalman_filter_full's device driver picks the chunked run for a long window; same
     outputs as parallel=False."""
