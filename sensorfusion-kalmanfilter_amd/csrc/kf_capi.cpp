@@ -1283,10 +1283,13 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
             if (best[lo] || best[last]) break;
         }
     }
-    e = hipMemcpyAsync(best, d_best, sizeof best, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(acc, d_acc, sizeof acc, hipMemcpyDeviceToHost, st);
+    // best[] and n_acc[] are adjacent on the device: one copy
+    uint64_t res[2 * (kMaxComboEvents + 1)];
+    e = hipMemcpyAsync(res, d_best, sizeof res, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(e, "kf_search_combos: results");
+    std::memcpy(best, res, sizeof best);
+    std::memcpy(acc, res + (kMaxComboEvents + 1), sizeof acc);
     for (int k = k_base > 0 ? k_base : 1; k <= last && !found; ++k)
         if (best[k]) found = k;
     h->search_info[0] = sym;

@@ -568,11 +568,25 @@ constexpr int kStreamDepth = KF_STREAM_DEPTH;  // its input ring in stream mode 
 #endif
 // the map pass's ring (4 state variants per lane): shallower, so the lane fits 2 waves per SIMD
 constexpr int kStreamVarDepth = KF_STREAM_VAR_DEPTH;
+#ifndef KF_STREAM_VAR_SPLIT
+#define KF_STREAM_VAR_SPLIT 0
+#endif
+// the map pass's four state variants as two per lane over two 8-lane groups per chunk (variants
+// 0, 1 and 2, 3): twice the waves, each lane's event a little shorter (the covariance work
+// repeated in both groups).  Measured slower on config 1, 0.2196 vs 0.2045 ms per log in-process
+// (profiles/r04_pmc/cfg1_diag/ab_split_sym_halves.log), so off; kept for A/B builds
+constexpr bool kStreamVarSplit = KF_STREAM_VAR_SPLIT != 0;
+// lanes per filter of ref_chain_kernel
+template <int NV>
+__host__ __device__ constexpr int chain_lanes() {
+    return NV == 4 && kStreamVarSplit ? 2 * 8 : 8;
+}
 
 // Sums / ORs over the 8-lane group with DPP (a VALU-latency lane exchange, no LDS round trip):
 // quad_perm [1,0,3,2] (xor 1), quad_perm [2,3,0,1] (xor 2), then row_half_mirror (lane i <-> 7-i
 // within each 8 lanes), which pairs the two quads.  Every lane of the group ends with the total.
 constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141;
+constexpr int kDppRowRor8 = 0x128;  // row_ror:8: lane l of a 16-lane row reads lane l +- 8
 
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
@@ -641,10 +655,13 @@ template <typename T, class M, bool STREAM, bool CUSTOM, int NV = 1>
 __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     static_assert(NV == 1 || STREAM, "state variants are a stream-mode feature");
     if (a.skip && *a.skip) return;  // the sequential fallback of a stream run that passed its checks
+    constexpr int LPF = chain_lanes<NV>();         // lanes per filter
+    constexpr int NL = LPF == 2 * kGroup ? 2 : NV;  // variants this lane holds
     const int64_t g = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    const int64_t f = g / kGroup;
-    if (f >= a.B) return;  // whole groups leave together (kGroup divides the wave)
+    const int64_t f = g / LPF;
+    if (f >= a.B) return;  // whole groups leave together (LPF divides the wave)
     const int c = static_cast<int>(g % kGroup);
+    const int vb = NL < NV ? int((g % LPF) / kGroup) * NL : 0;  // this lane's first variant
     const bool pva = c < M::NP;
     const bool live = c < M::NP + M::NA;
     const int ca = pva ? c : (live ? c - M::NP : 0);
@@ -686,19 +703,25 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
         if (pva) Rgps = T(kc->r_gps[ca]);
     }
 
-    T x[NV][3], P[6];
+    T x[NL][3], P[6];
+    T xs0[3];  // variant 0's start (the map pass's guess)
     {
         const auto rx = span_rsrc(a.x, 0, rbank, M::N), rp = span_rsrc(a.P, 0, rbank, M::NBLK);
 #pragma unroll
-        for (int v = 0; v < NV; ++v)
+        for (int v = 0; v < NL; ++v)
 #pragma unroll
-            for (int k = 0; k < 3; ++k) x[v][k] = ldv(rx, vx[k] == kDropOffset ? kDropOffset : vx[k] + uint32_t(v) * rb, T(0));
+            for (int k = 0; k < 3; ++k)
+                x[v][k] = ldv(rx, vx[k] == kDropOffset ? kDropOffset : vx[k] + uint32_t(vb + v) * rb, T(0));
 #pragma unroll
         for (int k = 0; k < 6; ++k) P[k] = pr[k] >= 0 ? ldv(rp, vp[k], T(0)) : T(k == 0 || k == 3 || k == 5 ? 1 : 0);
-    }
-    T xs0[3];  // variant 0's start (the map pass's guess)
+        if constexpr (NL < NV) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) xs0[k] = x[0][k];
+            for (int k = 0; k < 3; ++k) xs0[k] = ldv(rx, vx[k], T(0));
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) xs0[k] = x[0][k];
+        }
+    }
     // the map pass's seam check reads the next chunk's start covariance: loaded here, before
     // any of this lane's stores (a later load would wait for all of them, vmcnt being in order)
     double wnx[6] = {0, 0, 0, 0, 0, 0};
@@ -723,7 +746,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     // with s_nvar > 1, variant q's trajectory records go to rows [q * s_vstride, q * s_vstride +
     // S) (s_vstride >= S + chunk, so a padded chunk's rows past S stay inside its own variant),
     // and only variant 0 writes the others
-    const int var = STREAM ? int(f / a.s_nchunks) : 0;
+    const int var = STREAM ? int(f / a.s_nchunks) + vb : 0;
     const uint32_t trows = STREAM ? (a.s_nvar > 1 ? uint32_t(a.s_nvar) * uint32_t(a.s_vstride) : S) : 0u;
     const auto r_str = bytes_rsrc(a.traj, trows * uint32_t(M::NTRAJ * sizeof(T)));
     const auto r_scv = bytes_rsrc(a.cov, S * uint32_t(M::NBLK * sizeof(T)));
@@ -739,7 +762,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
                                                       uint32_t(sizeof(T))
                                                 : 0u;
     const uint32_t vstep_tr = uint32_t(a.s_vstride) * uint32_t(M::NTRAJ * sizeof(T));  // next variant's rows
-    const uint32_t m_ld = c == 0 && var == 0 ? 0u : kDropOffset;
+    const uint32_t m_ld = c == 0 && var == 0 ? 0u : kDropOffset;  // variant 0's group only
     uint32_t col_cv[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k)
@@ -770,7 +793,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
             const T c02 = pva ? T(0.5) * dt * dt : T(0);
             const T c12 = pva ? dt : T(0);
 #pragma unroll
-            for (int v = 0; v < NV; ++v) {
+            for (int v = 0; v < NL; ++v) {
                 const T xn0 = fmaT(c02, x[v][2], fmaT(dt, x[v][1], x[v][0]));
                 const T xn1 = fmaT(c12, x[v][2], x[v][1]);
                 x[v][0] = xn0;
@@ -798,26 +821,26 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
             if (applied) {
                 if (type == kGps) {
                     if (pva) {
-                        T zb[NV][1];
+                        T zb[NL][1];
 #pragma unroll
-                        for (int v = 0; v < NV; ++v) zb[v][0] = va;
+                        for (int v = 0; v < NL; ++v) zb[v][0] = va;
                         const T R[1] = {Rgps};
-                        ok = sel_update_nv<3, 1, true, T, kRefNewton, true, NV, kRefJoseph<T>, kRefGainR>(x, P, zb, R);
+                        ok = sel_update_nv<3, 1, true, T, kRefNewton, true, NL, kRefJoseph<T>, kRefGainR>(x, P, zb, R);
                     }
                 } else {
-                    T zb[NV][3];
+                    T zb[NL][3];
 #pragma unroll
-                    for (int v = 0; v < NV; ++v) {
+                    for (int v = 0; v < NL; ++v) {
                         const T V = fmaT(vb, dt, x[v][1]);
                         const T X = fmaT(V, dt, x[v][0]);
                         zb[v][0] = pva ? X : va;
                         zb[v][1] = pva ? V : vb;
                         zb[v][2] = pva ? vb : T(0);
                     }
-                    ok = sel_update_nv<3, 3, true, T, kRefNewton, true, NV, kRefJoseph<T>, kRefGainR>(x, P, zb, Rimu);
+                    ok = sel_update_nv<3, 3, true, T, kRefNewton, true, NL, kRefJoseph<T>, kRefGainR>(x, P, zb, Rimu);
                     if (!pva) {  // reset the inert state
 #pragma unroll
-                        for (int v = 0; v < NV; ++v) x[v][2] = T(0);
+                        for (int v = 0; v < NL; ++v) x[v][2] = T(0);
                         P[5] = T(1);
                     }
                 }
@@ -825,7 +848,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
             if (group_any(!ok)) {
                 st = kNotSpd;
 #pragma unroll
-                for (int v = 0; v < NV; ++v)
+                for (int v = 0; v < NL; ++v)
 #pragma unroll
                     for (int k = 0; k < 3; ++k) x[v][k] = quiet_nan<T>();
 #pragma unroll
@@ -835,7 +858,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
         if constexpr (STREAM) {
             const uint32_t ue = uint32_t(e0 + t);
 #pragma unroll
-            for (int v = 0; v < NV; ++v)
+            for (int v = 0; v < NL; ++v)
                 stv(r_str, (ue * uint32_t(M::NTRAJ * sizeof(T)) + col_tr + uint32_t(v) * vstep_tr) | m_tr, x[v][0]);
             // absent records: skipped by a wave-uniform branch (a store to a zero-length
             // descriptor is dropped, but it is still issued)
@@ -898,13 +921,16 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     {
         const auto rx = span_rsrc(a.x, 0, rbank, M::N), rp = span_rsrc(a.P, 0, rbank, M::NBLK);
 #pragma unroll
-        for (int v = 0; v < NV; ++v)
+        for (int v = 0; v < NL; ++v)
 #pragma unroll
-            for (int k = 0; k < 3; ++k) stv(rx, vx[k] == kDropOffset ? kDropOffset : vx[k] + uint32_t(v) * rb, x[v][k]);
+            for (int k = 0; k < 3; ++k)
+                stv(rx, vx[k] == kDropOffset ? kDropOffset : vx[k] + uint32_t(vb + v) * rb, x[v][k]);
+        if (vb == 0) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) stv(rp, vp[k], P[k]);
+            for (int k = 0; k < 6; ++k) stv(rp, vp[k], P[k]);
+        }
     }
-    if (c == 0) a.status[f] = st;
+    if (c == 0 && vb == 0) a.status[f] = st;
     if constexpr (NV == 4) {
         // the map pass's epilogue (kf_run_stream): this chunk's affine map per chain, x_end =
         // A x_start + b (fp64), A by differences of the variants (variant q + 1 started at the
@@ -914,18 +940,30 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
         constexpr int NCH = M::NP + M::NA;
         const int ns = pva ? 3 : 2;
         double crel = 0.0;
-        if (live && a.s_maps) {
+        // every variant's end state: with the split, variants 2, 3 come from the other group of
+        // 16 (DPP row_ror:8 pairs lane l with l + 8 within the row), every lane exchanging
+        double xe[4][3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+#pragma unroll
+            for (int v = 0; v < NL; ++v) xe[v][k] = double(x[v][k]);
+            if constexpr (NL < 4) {
+#pragma unroll
+                for (int v = 0; v < NL; ++v) xe[NL + v][k] = dpp_d<kDppRowRor8>(xe[v][k]);
+            }
+        }
+        if (live && a.s_maps && vb == 0) {
             double A[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, b[3] = {0, 0, 0};
             const double rdelta = 1.0 / a.s_delta;  // delta is a power of two: exact
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 if (k >= ns) continue;
-                const double e0v = double(x[0][k]);
+                const double e0v = xe[0][k];
                 double sacc = e0v;
 #pragma unroll
                 for (int qq = 0; qq < 3; ++qq) {
                     if (qq >= ns) continue;
-                    A[k][qq] = (double(x[qq + 1][k]) - e0v) * rdelta;
+                    A[k][qq] = (xe[qq + 1][k] - e0v) * rdelta;
                     sacc = __builtin_fma(-A[k][qq], double(xs0[qq]), sacc);
                 }
                 b[k] = sacc;
@@ -959,7 +997,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
             crel = fmax(crel, dpp_d<kDppHalfMirror>(crel));
             // a wave whose chunks all exist has every lane here (a partial last wave lost its
             // dead groups at the top, so it keeps one atomic per chunk)
-            const bool full = (g & ~int64_t(63)) / kGroup + 64 / kGroup <= a.B;  // wave-uniform
+            const bool full = (g & ~int64_t(63)) / LPF + 64 / LPF <= a.B;  // wave-uniform
             if (full) {
 #pragma unroll
                 for (int sh = kGroup; sh < 64; sh <<= 1) crel = fmax(crel, __shfl_xor(crel, sh, 64));
@@ -968,8 +1006,8 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
                 const bool any_bad = __builtin_amdgcn_ballot_w64(c == 0 && st != 0) != 0;
                 if (lane0 && any_bad) atomicOr(&a.s_check->bad, kStreamBadFilter);
             } else {
-                if (c == 0 && crel != 0.0) atomic_max_pos(&a.s_check->cov_gap, crel);
-                if (c == 0 && st != 0) atomicOr(&a.s_check->bad, kStreamBadFilter);
+                if (c == 0 && vb == 0 && crel != 0.0) atomic_max_pos(&a.s_check->cov_gap, crel);
+                if (c == 0 && vb == 0 && st != 0) atomicOr(&a.s_check->bad, kStreamBadFilter);
             }
         }
     }
@@ -1391,11 +1429,13 @@ __device__ __forceinline__ void lft_event(double (&v)[6], int type, double dt, b
 }
 
 // kLftHalves lanes per (chunk piece, chain), each carrying 6 / kLftHalves columns of the 6x6
-// product: the columns are independent, so the split doubles the waves of this latency-bound
+// product: the columns are independent, so the split multiplies the waves of this latency-bound
 // pass (0.75 wave per SIMD at 8192 chunks with all six columns in one lane) at the cost of
-// paying an event's type / dt handling twice
+// paying an event's type / dt handling in every lane.  Config 1 in-process, with the axis-
+// symmetric maps: 1 / 2 / 3 / 6 lanes 0.208 / 0.200 / 0.195 / 0.196 ms per log
+// (profiles/r04_pmc/cfg1_diag/ab_halves.log)
 #ifndef KF_LFT_HALVES
-#define KF_LFT_HALVES 2
+#define KF_LFT_HALVES 3
 #endif
 constexpr int kLftHalves = KF_LFT_HALVES;
 static_assert(6 % kLftHalves == 0, "columns per lane");
@@ -3413,9 +3453,13 @@ void ref_events_t(const RefArgs& a, hipStream_t stream, int variant) {
 }
 template <typename T, class M, bool CUSTOM>
 void ref_stream_t(const RefArgs& a, hipStream_t stream, int nv) {
-    const dim3 cgrid(static_cast<unsigned>((a.B * kGroup + kBlock - 1) / kBlock));
-    if (nv == 4) ref_chain_kernel<T, M, true, CUSTOM, 4><<<cgrid, kBlock, 0, stream>>>(a);
-    else ref_chain_kernel<T, M, true, CUSTOM><<<cgrid, kBlock, 0, stream>>>(a);
+    if (nv == 4) {
+        const dim3 vgrid(static_cast<unsigned>((a.B * chain_lanes<4>() + kBlock - 1) / kBlock));
+        ref_chain_kernel<T, M, true, CUSTOM, 4><<<vgrid, kBlock, 0, stream>>>(a);
+    } else {
+        const dim3 cgrid(static_cast<unsigned>((a.B * kGroup + kBlock - 1) / kBlock));
+        ref_chain_kernel<T, M, true, CUSTOM><<<cgrid, kBlock, 0, stream>>>(a);
+    }
 }
 }  // namespace
 
