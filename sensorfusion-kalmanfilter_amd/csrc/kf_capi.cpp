@@ -861,6 +861,11 @@ constexpr int64_t kStreamTargetChunks = 8192;
 constexpr int64_t kStreamMinChunk = 32;
 // piece maps (36 doubles) the start kernel stages in LDS per block: 64 KB
 constexpr int64_t kStreamStartLdsMaps = 65536 / (36 * 8);
+// chunks per start thread, at most: 2 of the 3 that fit measured 0.1937 vs 0.1951 ms per log
+// (config 1 in-process, profiles/r04_pmc/cfg1_diag/ab_start_g_chunks.log; 1: 0.1948)
+#ifndef KF_START_MAX_G
+#define KF_START_MAX_G 2
+#endif
 
 size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
 
@@ -1049,7 +1054,7 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
         // windows, (64 g + iters) * np of them, in 64 KB of LDS; g = 0: no LDS (one chunk per
         // thread, maps from global memory)
         const int64_t fit = kStreamStartLdsMaps / np - sa.iters;
-        sa.g = fit >= 64 ? std::min<int64_t>(fit / 64, 4) : 0;  // kStartMaxG
+        sa.g = fit >= 64 ? std::min<int64_t>(fit / 64, KF_START_MAX_G) : 0;  // <= kStartMaxG
         sa.G = 64 * sa.g;
         e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseLftMaps, sa, st);
         // the start kernel also zeroes the check and fills the warm-up bank (and, without event
