@@ -557,7 +557,7 @@ def ref15_workload(cfg, args, rank, world, dev):
 
     return dict(step=step, units=B * T, bytes=bytes_launch, bytes_per_unit=bytes_event, probe=probe,
                 kernel='ref_events_lds_kernel',
-                traffic=load_traffic('ref15') if cfg['dtype'] == 'f64' else None,
+                traffic=load_traffic('ref15' if cfg['dtype'] == 'f64' else 'ref15f32', bytes_launch),
                 valu=load_valu('ref15') if cfg['dtype'] == 'f64' else None, cpu=cpu, gather=gather_payload, kf=kf,
                 desc=f'SURVEY 8f row 2: reference 15-state model (kf_workers.py:493-614), {cfg["dtype"]}, B={B} filters/GPU, '
                      f'T={T} events (IMU 200 Hz, GPS fix every {k}th event), dt={dt}',

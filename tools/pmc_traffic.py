@@ -146,12 +146,12 @@ def main():
             res['configsched'] = {'bytes_per_launch': tot, 'algorithmic_bytes_per_launch': alg,
                                   'traffic_over_algorithmic': tot / alg, 'note': 'pick + apply passes'}
             continue
-        kern = {'ref15': 'ref_events', '3gen': 'cv_run_kernel'}.get(c, 'cv_block_kernel')
+        kern = {'ref15': 'ref_events', 'ref15f32': 'ref_events', '3gen': 'cv_run_kernel'}.get(c, 'cv_block_kernel')
         f = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE'), kern)
         w = pick(per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE'), kern)
         fb, info = fetch(out_dir, f'cfg{c}', lambda k: kern in k, f, read_scale)
         write = 1024 * sum(w) / len(w)
-        alg, _ = (ref15_algorithmic_bytes if c == 'ref15' else algorithmic_bytes)(CONFIGS[str(c)])
+        alg, _ = (ref15_algorithmic_bytes if c in ('ref15', 'ref15f32') else algorithmic_bytes)(CONFIGS[str(c)])
         res[f'config{c}'] = {
             'fetch_bytes_raw': 1024 * sum(f) / len(f), 'write_bytes_raw': write,
             'bytes_per_launch': fb + write * write_scale,
