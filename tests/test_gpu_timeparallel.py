@@ -166,9 +166,26 @@ def test_records_updated_cov_ref8(final_pass):
             assert _rel(a, b) <= 1e-9
 
 
+def _symmetric_params(model, seed):
+    """Caller constants that are the same on every axis (REF15: per state group; REF8: x and y)."""
+    rng = np.random.default_rng(seed)
+    if model == 'ref15':
+        g = lambda lo, hi: np.repeat(rng.uniform(lo, hi, 5), 3)  # noqa: E731 (pos, att, vel, rate, acc)
+        q, ri, p0 = g(0.01, 8.0), g(0.02, 120.0), g(20.0, 2e4)
+        rg = np.full(3, rng.uniform(0.5, 9.0))
+    else:
+        def g(lo, hi):  # [x, y, theta, vx, vy, theta_dot, ax, ay]
+            a, t, v, w, c = rng.uniform(lo, hi, 5)
+            return np.array([a, a, t, v, v, w, c, c])
+        q, ri, p0 = g(0.01, 8.0), g(0.02, 120.0), g(20.0, 2e4)
+        rg = np.full(2, rng.uniform(0.5, 9.0))
+    return ref15.ModelConsts(model, q=q, r_imu=ri, r_gps=rg, p0=p0).params()
+
+
+@pytest.mark.parametrize('consts', ['reference', 'custom'])
 @pytest.mark.parametrize('model', ['ref15', 'ref8'])
 @pytest.mark.parametrize('dtype', ['f64', 'f32'])
-def test_axis_symmetric_maps_equal_every_chain(model, dtype):
+def test_axis_symmetric_maps_equal_every_chain(model, dtype, consts):
     """KF_OPT_AXIS_SYM: with the reference's constants (the same on every axis) the stream
     computes the covariance maps of one pva and one aw chain for all; the maps of the others are
     the same arithmetic on the same numbers, so every record, the final state and covariance and
@@ -178,7 +195,8 @@ def test_axis_symmetric_maps_equal_every_chain(model, dtype):
     n = 15 if model == 'ref15' else 8
     outs = []
     for sym in ('on', 'off'):
-        kf = kfmi.BatchedKF(model, 1, dtype, options={'axis_sym': sym})
+        kf = kfmi.BatchedKF(model, 1, dtype, options={'axis_sym': sym},
+                            params=_symmetric_params(model, 17) if consts == 'custom' else None)
         P0 = kf.state()[1].cpu().numpy()
         xs = np.zeros((n, 1), P0.dtype)
         xs[0:2, 0] = x0[0:2]
