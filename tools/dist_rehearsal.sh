@@ -10,11 +10,13 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT"
-for cfg in 3 ref15; do
+for cfg in 3 ref15 sched bf 1; do
   for n in 2 4; do
+    [ "$n" = 4 ] && [ "$cfg" != 3 ] && [ "$cfg" != ref15 ] && continue  # the §8f rows and config 1 at N = 2
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
       --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --steps 3 --warmup 1 \
-      --config $cfg --batch 262144 --dist-backend gloo > "$OUT/c${cfg}_n$n.log" 2>&1
+      --config $cfg $([ "$cfg" = bf ] || [ "$cfg" = 1 ] || echo --batch 262144) --dist-backend gloo \
+      --no-cpu-baseline > "$OUT/c${cfg}_n$n.log" 2>&1
     rc=$?
     echo "config $cfg n=$n rc=$rc" | tee -a "$OUT/steps.txt"
     grep '^{"metric"' "$OUT/c${cfg}_n$n.log" | tail -1 >> "$OUT/lines.jsonl" || true
