@@ -568,6 +568,14 @@ constexpr int kStreamDepth = KF_STREAM_DEPTH;  // its input ring in stream mode 
 #endif
 // the map pass's ring (4 state variants per lane): shallower, so the lane fits 2 waves per SIMD
 constexpr int kStreamVarDepth = KF_STREAM_VAR_DEPTH;
+#ifndef KF_STREAM_LD_BATCH
+#define KF_STREAM_LD_BATCH 1
+#endif
+// the map pass's log-det records: the group's determinant product per event, kept by lane
+// (event mod 8) and logged every 8 events (one log per lane-8-events instead of per lane-event;
+// the pass is bound by its instruction issue).  0: every lane logs its chain every event and the
+// group sums the logs (the NV = 1 chain kernel's form)
+constexpr bool kStreamLdBatch = KF_STREAM_LD_BATCH != 0;
 #ifndef KF_STREAM_VAR_SPLIT
 #define KF_STREAM_VAR_SPLIT 0
 #endif
@@ -628,6 +636,31 @@ __device__ __forceinline__ T chain_log_det(const T (&P)[6]) {
     renorm(prod, ex);
     const T ld = log_mant(prod, ex);
     return ok ? ld : quiet_nan<T>();
+}
+
+// chain_log_det before its log: the determinant as a mantissa in [0.5, 1) (NaN unless the
+// block is positive definite) and a binary exponent
+template <typename T>
+__device__ __forceinline__ void chain_det_mant(const T (&P)[6], T& m, int& ex) {
+    T num = T(1), den = T(1);
+    bool ok = true;
+    det3_scaled<T>(P, num, den, ok);
+    m = num * rcp_nr<kRefNewton>(den);
+    ex = 0;
+    renorm(m, ex);
+    m = ok ? m : quiet_nan<T>();
+}
+
+// (mantissa, exponent) product over the 8-lane group, the same DPP pattern as group_sum: every
+// lane ends with the same bits (each step multiplies a pair in both orders, and x * y == y * x)
+template <typename T>
+__device__ __forceinline__ void group_prod(T& m, int& ex) {
+    m *= dpp_d<kDppXor1>(m);
+    ex += __builtin_amdgcn_mov_dpp(ex, kDppXor1, 0xF, 0xF, false);
+    m *= dpp_d<kDppXor2>(m);
+    ex += __builtin_amdgcn_mov_dpp(ex, kDppXor2, 0xF, 0xF, false);
+    m *= dpp_d<kDppHalfMirror>(m);
+    ex += __builtin_amdgcn_mov_dpp(ex, kDppHalfMirror, 0xF, 0xF, false);
 }
 
 // non-negative doubles (and +NaN) order as their bit patterns: atomic max via uint64
@@ -735,6 +768,9 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     }
     int32_t st = a.status[f];
     const bool need_ld = a.logdet != nullptr;
+    constexpr bool kLdBatch = STREAM && NV == 4 && kStreamLdBatch;
+    T bm = T(1);  // kLdBatch: the group's determinant product of event (t - t mod 8 + c)
+    int bex = 0;
 
     // stream mode: this filter's event t is stream event e0 + t; one descriptor per stream
     // (events outside [0, S) are skipped: dropped loads, NONE type, dropped records)
@@ -868,9 +904,31 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
                     stv(r_scv, (ue * uint32_t(M::NBLK * sizeof(T)) + col_cv[k]) | (col_cv[k] & kDropOffset), P[k]);
             }
             if (need_ld) {
-                const T ld = group_sum(live ? chain_log_det(P) : T(0));
-                st = (ld == ld) ? st : kNotSpd;
-                stv(r_sld, (ue * uint32_t(sizeof(T))) | m_ld, ld);
+                if constexpr (kLdBatch) {
+                    T m;
+                    int ex;
+                    chain_det_mant(P, m, ex);
+                    m = live ? m : T(1);
+                    ex = live ? ex : 0;
+                    group_prod(m, ex);
+                    const int slot = t & (kGroup - 1);
+                    if (c == slot) {
+                        bm = m;
+                        bex = ex;
+                    }
+                    if (slot == kGroup - 1 || t == a.T - 1) {  // wave-uniform: lane j logs event t - slot + j
+                        int e;
+                        const T ld = log_mant(frexp(bm, &e), bex + e);
+                        const bool mine = c <= slot;
+                        if (group_any(mine && !(ld == ld))) st = kNotSpd;
+                        const uint32_t uj = uint32_t(e0 + t - slot + c);
+                        stv(r_sld, (uj * uint32_t(sizeof(T))) | (mine && var == 0 ? 0u : kDropOffset), ld);
+                    }
+                } else {
+                    const T ld = group_sum(live ? chain_log_det(P) : T(0));
+                    st = (ld == ld) ? st : kNotSpd;
+                    stv(r_sld, (ue * uint32_t(sizeof(T))) | m_ld, ld);
+                }
             }
             if (a.updated) __builtin_amdgcn_raw_buffer_store_b8(applied ? uint8_t(1) : uint8_t(0), r_sup, ue | m_ld, 0, 0);
         } else {
