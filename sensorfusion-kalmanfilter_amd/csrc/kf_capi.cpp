@@ -946,7 +946,9 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     const int ntraj = h->model == KF_MODEL_REF15 ? 6 : 3;
     const int64_t vstride = T + L;
     const bool map_records = opt(h, KF_OPT_STREAM_FINAL) == 0 && uint64_t(4 * vstride) * ntraj * w < (uint64_t(1) << 31);
-    const size_t rec_bytes = map_records ? align256(size_t(4 * vstride) * ntraj * w) + align256(sizeof(double) * n) : 0;
+    const size_t rec_bytes = map_records ? align256(size_t(4 * vstride) * ntraj * w) + align256(sizeof(double) * n) +
+                                               align256(sizeof(double) * 4 * nch * C)
+                                         : 0;
     const int64_t ntiles = (C + kfmi::kStreamScanTile - 1) / kfmi::kStreamScanTile;
     const size_t need = 256 + 2 * bank1 + bank4 + 2 * align256(sizeof(double) * 12 * nch * C) +
                         align256(sizeof(double) * 12 * nch * ntiles) + align256(sizeof(double) * n * C) + lft_bytes +
@@ -999,6 +1001,8 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
         traj4 = p;
         p += align256(size_t(4 * vstride) * ntraj * w);
         sa.xend = reinterpret_cast<double*>(p);
+        p += align256(sizeof(double) * n);
+        sa.dtab = reinterpret_cast<double*>(p);  // the records' start offsets, [C][chains][4]
         sa.traj4 = traj4;
         sa.vstride = vstride;
         sa.traj = traj;

@@ -131,6 +131,7 @@ struct StreamArgs {
     double* pref;            // [C][chains][12]: the product of the chunk maps before c in c's tile
     double* tiles;           // [C / kScanTile][chains][12]: each tile's product
     double* starts;          // [N][C] the chunk starts (fp64)
+    double* dtab;            // [C][chains][4] (records from the map pass): start - guess per chain component
     StreamCheck* check;
     // covariance start by linear-fractional maps (kf_run_stream's default warm-up)
     const uint8_t* etype;    // the stream [S], dt [S]

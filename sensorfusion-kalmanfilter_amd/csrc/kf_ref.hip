@@ -576,6 +576,11 @@ constexpr int kStreamVarDepth = KF_STREAM_VAR_DEPTH;
 // the pass is bound by its instruction issue).  0: every lane logs its chain every event and the
 // group sums the logs (the NV = 1 chain kernel's form)
 constexpr bool kStreamLdBatch = KF_STREAM_LD_BATCH != 0;
+#ifndef KF_STREAM_RECORD_PAIRS
+#define KF_STREAM_RECORD_PAIRS 1
+#endif
+// the records from the map pass two entries per thread (stream_records2_kernel; 0: one each)
+constexpr bool kStreamRecordPairs = KF_STREAM_RECORD_PAIRS != 0;
 #ifndef KF_STREAM_VAR_SPLIT
 #define KF_STREAM_VAR_SPLIT 0
 #endif
@@ -1349,6 +1354,8 @@ __global__ __launch_bounds__(kScanTile) void stream_starts_kernel(const StreamAr
             if (k >= ns) continue;
             const int i = chain_state<M>(ch, k);
             a.starts[i * a.C + c] = x[k];
+            // the records' offsets, start - guess, in the records kernel's own arithmetic
+            if (a.dtab) a.dtab[(c * NCH + ch) * 4 + k] = x[k] - double(static_cast<const T*>(a.wx)[i * a.C + c]);
             fin = fin && (x[k] - x[k] == 0.0);  // NaN or inf fails
             if (!a.xend) static_cast<T*>(a.fx)[i * a.C + c] = T(x[k]);
         }
@@ -1411,15 +1418,79 @@ __global__ __launch_bounds__(kBlock) void stream_records_kernel(const StreamArgs
     const int ns = ch < M::NP ? 3 : 2;
     const double x0 = double(t4[g]);
     double acc = x0;
+    // start - guess of the chain's components: the starts kernel's table (two loads shared by
+    // the chunk's threads), or the starts and guess rows themselves
+    double d[3];
+    if (a.dtab) {
+        const double* dt = a.dtab + (c * NCH + ch) * 4;
+        const double2 d01 = *reinterpret_cast<const double2*>(dt);
+        d[0] = d01.x;
+        d[1] = d01.y;
+        d[2] = ns == 3 ? dt[2] : 0.0;
+    } else {
+#pragma unroll
+        for (int qq = 0; qq < 3; ++qq) {
+            const int idx = chain_state<M>(ch, qq);
+            d[qq] = qq < ns ? a.starts[idx * a.C + c] - double(wx[idx * a.C + c]) : 0.0;
+        }
+    }
 #pragma unroll
     for (int qq = 0; qq < 3; ++qq) {
         if (qq >= ns) continue;
         const double xq = double(t4[(qq + 1) * a.vstride * M::NTRAJ + g]);
-        const int idx = chain_state<M>(ch, qq);
-        const double d = a.starts[idx * a.C + c] - double(wx[idx * a.C + c]);
-        acc = __builtin_fma((xq - x0) * a.rdelta, d, acc);  // delta is a power of two: exact
+        acc = __builtin_fma((xq - x0) * a.rdelta, d[qq], acc);  // delta is a power of two: exact
     }
     static_cast<T*>(a.traj)[g] = T(acc);
+}
+
+// The same records two entries per thread (an even NTRAJ: entries 2j, 2j + 1 of one event):
+// one 2-wide load per variant row and one 2-wide store instead of two each, the start offsets
+// from the starts kernel's table.  Each entry's arithmetic is stream_records_kernel's.
+template <typename T, class M>
+__global__ __launch_bounds__(kBlock) void stream_records2_kernel(const StreamArgs a) {
+    static_assert(M::NTRAJ % 2 == 0, "pairs of one event's entries");
+    typedef T T2 __attribute__((ext_vector_type(2)));
+    constexpr int NCH = M::NP + M::NA;
+    const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;  // pair: entries 2p, 2p + 1
+    if (p >= a.S * (M::NTRAJ / 2)) return;
+    const uint32_t e = uint32_t(p) / uint32_t(M::NTRAJ / 2);
+    const int i0 = 2 * int(uint32_t(p) - e * uint32_t(M::NTRAJ / 2));
+    const int64_t c = e / uint32_t(a.L);
+    const T2* t4 = static_cast<const T2*>(a.traj4);
+    int ch[2] = {0, 0};
+#pragma unroll
+    for (int cc = 0; cc < NCH; ++cc) {
+        if (chain_state<M>(cc, 0) == i0) ch[0] = cc;
+        if (chain_state<M>(cc, 0) == i0 + 1) ch[1] = cc;
+    }
+    double d[2][3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const double* dt = a.dtab + (c * NCH + ch[h]) * 4;
+        const double2 d01 = *reinterpret_cast<const double2*>(dt);
+        d[h][0] = d01.x;
+        d[h][1] = d01.y;
+        d[h][2] = ch[h] < M::NP ? dt[2] : 0.0;
+    }
+    const T2 v0 = t4[p];
+    const double x0[2] = {double(v0.x), double(v0.y)};
+    double acc[2] = {x0[0], x0[1]};
+    const bool any3 = ch[0] < M::NP || ch[1] < M::NP;  // a third variant row is needed
+#pragma unroll
+    for (int qq = 0; qq < 3; ++qq) {
+        if (qq == 2 && !any3) continue;
+        const T2 vq = t4[(qq + 1) * a.vstride * (M::NTRAJ / 2) + p];
+        const double xq[2] = {double(vq.x), double(vq.y)};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int ns = ch[h] < M::NP ? 3 : 2;
+            if (qq < ns) acc[h] = __builtin_fma((xq[h] - x0[h]) * a.rdelta, d[h][qq], acc[h]);
+        }
+    }
+    T2 out;
+    out.x = T(acc[0]);
+    out.y = T(acc[1]);
+    static_cast<T2*>(a.traj)[p] = out;
 }
 
 // ------------------------------------------------------------------------------------
@@ -3588,7 +3659,16 @@ void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
             break;
         }
         case 5: stream_finish_kernel<T, M><<<1, 1024, 0, stream>>>(a); break;
-        case kStreamPhaseRecords: stream_records_kernel<T, M><<<grid(a.S * M::NTRAJ), kBlock, 0, stream>>>(a); break;
+        case kStreamPhaseRecords:
+            if constexpr (M::NTRAJ % 2 == 0 && kStreamRecordPairs) {
+                // (a caller's trajectory that is not aligned to a pair takes the one-entry kernel)
+                if (a.dtab && reinterpret_cast<uintptr_t>(a.traj) % (2 * sizeof(T)) == 0) {
+                    stream_records2_kernel<T, M><<<grid(a.S * (M::NTRAJ / 2)), kBlock, 0, stream>>>(a);
+                    break;
+                }
+            }
+            stream_records_kernel<T, M><<<grid(a.S * M::NTRAJ), kBlock, 0, stream>>>(a);
+            break;
         default: break;
     }
 }
