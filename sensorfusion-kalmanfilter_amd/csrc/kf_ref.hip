@@ -1384,15 +1384,27 @@ __global__ __launch_bounds__(kScanTile) void stream_starts_kernel(const StreamAr
     asm volatile("" ::: "memory");  // the verdict's reads stay after the count
     const int bad = atomicOr(&k->bad, 0);
     const double cov_gap = __longlong_as_double(atomicOr(reinterpret_cast<unsigned long long*>(&k->cov_gap), 0ull));
-    k->state_gap = bad & kStreamBadStart ? __builtin_inf() : __builtin_nan("");
     const bool ok = bad == 0 && cov_gap <= a.tol_cov;
+    // every read issued before the first store: a read after a store that may alias it waits
+    // for the store, which made the 42 reads below round trips one after another
+    const int64_t col = a.C - 1, B4 = 4 * a.C;  // the last chunk's end covariance
+    double xv[M::N];
+    T pv[M::NBLK];
+    if (ok) {
+#pragma unroll
+        for (int i = 0; i < M::N; ++i)  // written by the last tile's block (a device-scope atomic)
+            xv[i] = __longlong_as_double(
+                static_cast<long long>(atomicOr(reinterpret_cast<unsigned long long*>(&a.xend[i]), 0ull)));
+#pragma unroll
+        for (int r = 0; r < M::NBLK; ++r) pv[r] = static_cast<const T*>(a.mP)[r * B4 + col];
+    }
+    k->state_gap = bad & kStreamBadStart ? __builtin_inf() : __builtin_nan("");
     k->ok = ok ? 1 : 0;
     if (ok) {
-        const int64_t col = a.C - 1, B4 = 4 * a.C;  // the last chunk's end covariance
-        for (int i = 0; i < M::N; ++i)  // written by the last tile's block (a device-scope atomic)
-            static_cast<T*>(a.hx)[i] = T(__longlong_as_double(static_cast<long long>(
-                atomicOr(reinterpret_cast<unsigned long long*>(&a.xend[i]), 0ull))));
-        for (int r = 0; r < M::NBLK; ++r) static_cast<T*>(a.hP)[r] = static_cast<const T*>(a.mP)[r * B4 + col];
+#pragma unroll
+        for (int i = 0; i < M::N; ++i) static_cast<T*>(a.hx)[i] = T(xv[i]);
+#pragma unroll
+        for (int r = 0; r < M::NBLK; ++r) static_cast<T*>(a.hP)[r] = pv[r];
         a.hstatus[0] = 0;
     }
 }
