@@ -1618,21 +1618,27 @@ __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArg
     const int64_t c = cp / a.np, piece = cp % a.np;
     const int64_t cend = (c + 1) * a.L < a.S ? (c + 1) * a.L : a.S;
     const int64_t e0 = c * a.L + piece * a.lp, e1 = e0 + a.lp < cend ? e0 + a.lp : cend;
-    // events in batches of 8, the next batch's type and dt loaded while this one computes
+    // events in batches of 8, the next batch's type and dt loaded while this one computes.  The
+    // loads are unconditional buffer loads (past the stream they return 0) and the batch's range
+    // test is applied where the values are used: loads under a per-lane condition were branched
+    // around, and the branches' join waited for every load in flight (vmcnt 0), the batch just
+    // issued included
     constexpr int kB = 8;
-    int tyn[kB];
+    const auto r_et = bytes_rsrc(a.etype, uint32_t(a.S));
+    const auto r_dt = bytes_rsrc(a.dt, uint32_t(a.S) * 8u);
+    uint32_t tyn[kB];
     double dvn[kB];
     auto fetch = [&](int64_t e) {
 #pragma unroll
         for (int k = 0; k < kB; ++k) {
-            const bool in = e + k < e1;
-            tyn[k] = in ? int(a.etype[e + k]) : 255;
-            dvn[k] = in ? a.dt[e + k] : 0.0;
+            const uint32_t ue = uint32_t(e + k);
+            tyn[k] = __builtin_amdgcn_raw_buffer_load_b8(r_et, ue, 0, 0);
+            dvn[k] = ldv(r_dt, ue * 8u, 0.0);
         }
     };
     fetch(e0);
     for (int64_t e = e0; e < e1; e += kB) {
-        int ty[kB];
+        uint32_t ty[kB];
         double dv[kB];
 #pragma unroll
         for (int k = 0; k < kB; ++k) {
@@ -1641,9 +1647,13 @@ __global__ __launch_bounds__(kBlock) void stream_lft_maps_kernel(const StreamArg
         }
         fetch(e + kB);
 #pragma unroll
-        for (int k = 0; k < kB; ++k)
+        for (int k = 0; k < kB; ++k) {
+            const bool in = e + k < e1;
+            const int tk = in ? int(ty[k]) : 255;
+            const double dk = in ? dv[k] : 0.0;
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) lft_event<M>(v[j], ty[k], dv[k], pva, q, si, sg);
+            for (int j = 0; j < NJ; ++j) lft_event<M>(v[j], tk, dk, pva, q, si, sg);
+        }
         if (((e - e0) & 15) == kB) {  // every 16 events: rescale by a power of two (the max)
             // of all six columns: the lanes of one product exchange their maxima (adjacent lanes)
             double mx = 0.0;
