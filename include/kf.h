@@ -527,13 +527,22 @@ int kf_quat_to_euler(int64_t n, const double* q, int64_t ld, double* out, void* 
  *   KF_DT_MONOTONE  adaptive / no-update drivers and the combination worker (:1012-1016,
  *                   :1113-1116, :38-40): a skipped event does not move the previous time
  *   KF_DT_RAW       run_kalman_filter / hw5_2 (:763-767, hw5_2.py:331-336): no guard
- * t/etype_in/dt/etype_out device [n]; prev0 = the time of the state the run starts from;
- * etype_in NULL = all KF_EVENT_IMU; etype_out may be NULL. */
+ * t/etype_in/dt/etype_out device [n]; prev0 = the time of the state the run starts from, or
+ * NaN for a driver with no previous time yet, whose first event gets dt 0 (hw5_2.py:401, 407;
+ * FULL and RAW only); etype_in NULL = all KF_EVENT_IMU; etype_out may be NULL. */
 #define KF_DT_FULL     0
 #define KF_DT_MONOTONE 1
 #define KF_DT_RAW      2
 int kf_events_dt(int64_t n, const double* t, const uint8_t* etype_in, double prev0, int rule, double* dt,
                  uint8_t* etype_out, void* stream);
+
+/* The events of one type out of a merged stream, in stream order: hw5_2.run_dead_reckoning_for_IMU
+ * walks the IMU events alone, skipping every fix (hw5_2.py:402-404).  etype device [n], t device
+ * [n], payload device [n][9] (kf_ingest's layout); writes the K kept events' t_out [K],
+ * payload_out [K][9] and src_out [K] (their stream positions), each of which may be NULL, with
+ * capacity n, and *n_kept = K (host).  Synchronous (the count is returned). */
+int kf_events_select(int64_t n, const uint8_t* etype, const double* t, const double* payload, int keep_type,
+                     double* t_out, double* payload_out, int32_t* src_out, int64_t* n_kept, void* stream);
 
 #ifdef __cplusplus
 }

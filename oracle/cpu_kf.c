@@ -468,3 +468,46 @@ void cpu_ref8_events(int64_t B, int T, const uint8_t* etype, const double* dt, c
         }
     }
 }
+
+/* hw5_2.run_dead_reckoning_for_IMU (hw5_2.py:382-436) over one merged stream as kf_ingest lays
+ * it out (etype [N] 0 = GPS / 1 = IMU, t [N], payload [N][9] row-major): only the IMU events
+ * are filtered (:403-404), dt runs from the previous IMU event with the first at 0 (:401, 407,
+ * no dt < 0 guard), x0 = 0, P0 = diag(1000, 1000, 100, 100, 100, 100, 1000, 1000) (:385-395),
+ * and each event predicts then applies the H = I8 pseudo-measurement (:410-431).  Writes one
+ * (x, y, theta) row per IMU event into traj [K][3] and its log-det into logdet [K] (either may
+ * be NULL) and returns K. */
+int64_t cpu_ref8_dead_reckoning(int64_t N, const uint8_t* etype, const double* t, const double* payload,
+                                double* traj, double* logdet_out) {
+    static const double q8[8] = {5.0, 5.0, 0.05, 1.0, 1.0, 0.1, 2.0, 2.0};
+    static const double r8[8] = {50.0, 50.0, 0.05, 10.0, 10.0, 0.1, 100.0, 100.0};
+    static const double p08[8] = {1000.0, 1000.0, 100.0, 100.0, 100.0, 100.0, 1000.0, 1000.0};
+    double Hi[64] = {0}, Ri[64] = {0}, x[8] = {0}, P[64] = {0}, F[64], Q[64];
+    for (int i = 0; i < 8; ++i) {
+        Hi[i * 8 + i] = 1.0;
+        Ri[i * 8 + i] = r8[i];
+        P[i * 8 + i] = p08[i];
+    }
+    int64_t k = 0;
+    int have_prev = 0;
+    double prev = 0.0;
+    for (int64_t e = 0; e < N; ++e) {
+        if (etype[e] != 1) continue;
+        const double h = have_prev ? t[e] - prev : 0.0;
+        const double* p = payload + e * 9;
+        F8(h, F);
+        memset(Q, 0, sizeof(Q));
+        for (int i = 0; i < 8; ++i) Q[i * 8 + i] = q8[i] * h;
+        predict(8, F, Q, NULL, x, P);
+        const double ax = p[6], ay = p[7];
+        const double Vx = x[3] + ax * h, Vy = x[4] + ay * h;
+        const double Z[8] = {x[0] + Vx * h, x[1] + Vy * h, p[2], Vx, Vy, p[5], ax, ay};
+        update(8, 8, Hi, Ri, Z, x, P);
+        if (traj)
+            for (int i = 0; i < 3; ++i) traj[k * 3 + i] = x[i];
+        if (logdet_out) logdet_out[k] = logdet(8, P);
+        ++k;
+        prev = t[e];
+        have_prev = 1;
+    }
+    return k;
+}

@@ -32,6 +32,8 @@ def lib():
         L.cpu_ref15_sched.restype = None
         L.cpu_ref8_events.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32]
         L.cpu_ref8_events.restype = None
+        L.cpu_ref8_dead_reckoning.argtypes = [i64, vp, vp, vp, vp, vp]
+        L.cpu_ref8_dead_reckoning.restype = i64
         _lib = L
     return _lib
 
@@ -96,6 +98,19 @@ def ref8_events(etype, dt, payload, x0, P0, filters=None, nthreads=None, records
     ld = np.zeros((T, B)) if records else None
     lib().cpu_ref8_events(B, T, _p(etype), _p(dt), _p(payload), _p(x0), _p(P0), _p(traj), _p(ld), f0, f1,
                           nthreads or threads())
+    return traj, ld
+
+
+def ref8_dead_reckoning(etype, t, payload):
+    """hw5_2.run_dead_reckoning_for_IMU (cpu_ref8_dead_reckoning) over one merged stream:
+    etype [N] u8 (0 GPS, 1 IMU), t [N], payload [N, 9].  Returns (traj [K, 3] (x, y, theta),
+    logdet [K]) for the K IMU events."""
+    etype, t, payload = _c(etype, np.uint8), _c(t), _c(payload)
+    N = etype.shape[0]
+    K = int(np.count_nonzero(etype == 1))
+    traj, ld = np.zeros((K, 3)), np.zeros(K)
+    k = lib().cpu_ref8_dead_reckoning(N, _p(etype), _p(t), _p(payload), _p(traj), _p(ld))
+    assert k == K
     return traj, ld
 
 

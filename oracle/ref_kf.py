@@ -510,6 +510,26 @@ def run_kalman_filter_8state(events):
     return states, Pt
 
 
+def run_dead_reckoning_8state(events):
+    """hw5_2.py:382-436 (run_dead_reckoning_for_IMU): the 8-state filter over the IMU events
+    alone — GPS events neither predict nor move the previous time (:403-404), the first IMU
+    event has dt 0 (:401, 407), x0 = 0 and P0 as :385-395, every IMU event predicts and applies
+    the H = I8 pseudo-measurement (:410-431), one (x, y, theta) per IMU event and no initial
+    record (:399, 433)."""
+    xt = np.array([0, 0, 0, 0, 0, 0, 0, 0])
+    Pt = P0_REF8.astype(np.int64)
+    states = []
+    prev = None
+    for (_, stype, t, sdata) in events:
+        if stype != 'IMU':
+            continue
+        dt = t - prev if prev is not None else 0
+        xt, Pt = step8(xt, Pt, 'IMU', sdata, dt)
+        states.append((xt[0], xt[1], xt[2]))
+        prev = t
+    return states, Pt
+
+
 # --------------------------------------------------------------------------------------
 # Batched constant-velocity filters (the BASELINE configs), reference op order
 # --------------------------------------------------------------------------------------

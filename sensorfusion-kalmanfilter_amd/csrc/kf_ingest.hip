@@ -250,8 +250,10 @@ __global__ __launch_bounds__(kIngBlock) void dt_kernel(int64_t n, const double* 
     double p;
     if (rule == 1)
         p = prev[i];
+    else if (i == 0)
+        p = prev0 != prev0 ? t[0] : prev0;  // NaN: no previous time yet, dt 0 (hw5_2.py:401, 407)
     else
-        p = i == 0 ? prev0 : t[i - 1];
+        p = t[i - 1];
     const double d = t[i] - p;
     const uint8_t e = et_in ? et_in[i] : uint8_t(KF_EVENT_IMU);
     dt[i] = d;
@@ -262,6 +264,28 @@ __global__ __launch_bounds__(kIngBlock) void euler_kernel(int64_t n, const doubl
     const int64_t i = int64_t(blockIdx.x) * kIngBlock + threadIdx.x;
     if (i >= n) return;
     quat_to_euler(q[i], q[ld + i], q[2 * ld + i], q[3 * ld + i], out[i], out[n + i], out[2 * n + i]);
+}
+
+// kf_events_select: the kept events' positions come from hipCUB's DeviceSelect over the event
+// indices; this gathers their time, payload row and position.
+struct IsType {
+    const uint8_t* etype;
+    uint8_t type;
+    __device__ __forceinline__ bool operator()(int32_t i) const { return etype[i] == type; }
+};
+
+__global__ __launch_bounds__(kIngBlock) void select_gather_kernel(int64_t k, const int32_t* idx, const double* t,
+                                                                   const double* payload, double* t_out,
+                                                                   double* payload_out, int32_t* src_out) {
+    const int64_t j = int64_t(blockIdx.x) * kIngBlock + threadIdx.x;
+    if (j >= k) return;
+    const int64_t i = idx[j];
+    if (t_out) t_out[j] = t[i];
+    if (src_out) src_out[j] = static_cast<int32_t>(i);
+    if (payload_out) {
+#pragma unroll
+        for (int c = 0; c < 9; ++c) payload_out[j * 9 + c] = payload[i * 9 + c];
+    }
 }
 
 struct MaxOp {
@@ -445,6 +469,8 @@ int kf_events_dt(int64_t n, const double* t, const uint8_t* etype_in, double pre
                  uint8_t* etype_out, void* stream) {
     if (n < 0) return set_error(KF_EINVAL, "kf_events_dt: n = %lld", (long long)n);
     if (rule < KF_DT_FULL || rule > KF_DT_RAW) return set_error(KF_EINVAL, "kf_events_dt: unknown rule %d", rule);
+    if (rule == KF_DT_MONOTONE && prev0 != prev0)
+        return set_error(KF_EINVAL, "kf_events_dt: KF_DT_MONOTONE needs a previous time (prev0 is NaN)");
     if (n == 0) return KF_OK;
     if (!t || !dt) return set_error(KF_EINVAL, "kf_events_dt: null t/dt");
     if (n >= (int64_t(1) << 31)) return set_error(KF_EINVAL, "kf_events_dt: more than 2^31 events");
@@ -466,6 +492,43 @@ int kf_events_dt(int64_t n, const double* t, const uint8_t* etype_in, double pre
     dt_kernel<<<grid(n), kIngBlock, 0, st>>>(n, t, prev, etype_in, prev0, rule, dt, etype_out);
     KF_TRY(hipGetLastError(), "kf_events_dt");
     if (ws.p) KF_TRY(hipStreamSynchronize(st), "kf_events_dt sync");  // before the workspace goes
+    return KF_OK;
+}
+
+int kf_events_select(int64_t n, const uint8_t* etype, const double* t, const double* payload, int keep_type,
+                     double* t_out, double* payload_out, int32_t* src_out, int64_t* n_kept, void* stream) {
+    if (n < 0 || !n_kept) return set_error(KF_EINVAL, "kf_events_select: n = %lld, n_kept %p", (long long)n,
+                                           static_cast<void*>(n_kept));
+    if (keep_type < 0 || keep_type > 255) return set_error(KF_EINVAL, "kf_events_select: event type %d", keep_type);
+    if (n >= (int64_t(1) << 31)) return set_error(KF_EINVAL, "kf_events_select: more than 2^31 events");
+    *n_kept = 0;
+    if (n == 0) return KF_OK;
+    if (!etype || (t_out && !t) || (payload_out && !payload))
+        return set_error(KF_EINVAL, "kf_events_select: null etype, or an output without its input");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const IsType pred{etype, static_cast<uint8_t>(keep_type)};
+    hipcub::CountingInputIterator<int32_t> rows(0);
+    size_t tmp = 0;
+    KF_TRY(hipcub::DeviceSelect::If(nullptr, tmp, rows, (int32_t*)nullptr, (int32_t*)nullptr, static_cast<int>(n),
+                                    pred, st),
+           "kf_events_select sizing");
+    const size_t ib = (4 * size_t(n) + 255) & ~size_t(255);
+    DevBuf ws;
+    KF_TRY(hipMalloc(&ws.p, ib + 256 + tmp), "kf_events_select workspace");
+    int32_t* idx = static_cast<int32_t*>(ws.p);
+    int32_t* count = reinterpret_cast<int32_t*>(static_cast<char*>(ws.p) + ib);
+    KF_TRY(hipcub::DeviceSelect::If(static_cast<char*>(ws.p) + ib + 256, tmp, rows, idx, count, static_cast<int>(n),
+                                    pred, st),
+           "kf_events_select");
+    int32_t k = 0;
+    KF_TRY(hipMemcpyAsync(&k, count, 4, hipMemcpyDeviceToHost, st), "kf_events_select readback");
+    KF_TRY(hipStreamSynchronize(st), "kf_events_select sync");
+    if (k && (t_out || payload_out || src_out)) {
+        select_gather_kernel<<<grid(k), kIngBlock, 0, st>>>(k, idx, t, payload, t_out, payload_out, src_out);
+        KF_TRY(hipGetLastError(), "kf_events_select gather");
+        KF_TRY(hipStreamSynchronize(st), "kf_events_select sync");  // before the workspace goes
+    }
+    *n_kept = k;
     return KF_OK;
 }
 

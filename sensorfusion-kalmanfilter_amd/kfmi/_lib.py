@@ -129,6 +129,7 @@ SIGNATURES = {
                        ctypes.POINTER(kf_ingest_info), _vp]),
     'kf_quat_to_euler': (_i, [_i64, _vp, _i64, _vp, _vp]),
     'kf_events_dt': (_i, [_i64, _vp, _vp, _d, _i, _vp, _vp, _vp]),
+    'kf_events_select': (_i, [_i64, _vp, _vp, _vp, _i, _vp, _vp, _vp, ctypes.POINTER(_i64), _vp]),
 }
 
 _lib = None

@@ -109,14 +109,18 @@ class KF_SensorFusion:
     def run_kalman_filter(self):
         """hw5_2.py:313-380: [(x, y, theta), ...], with the constants of this object's getters
         (a subclass may replace them with diagonal ones) and ``self.P0``."""
+        return ref8.run_kalman_filter(self.indexed_sensor_data, self.dtype, self.device, consts=self._consts())
+
+    def _consts(self):
         from .ref15 import ModelConsts
-        c = ModelConsts.from_matrices('ref8', F=self.get_state_transition_matrix,
-                                      Q=self.get_process_noise_covariance_matrix,
-                                      H_gps=self.get_gps_observation_matrix(), H_imu=self.get_imu_observation_matrix(),
-                                      R_gps=self.get_gps_measurement_noise_covariance_matrix(),
-                                      R_imu=self.get_imu_measurement_noise_covariance_matrix(),
-                                      P0=getattr(self, 'P0', None))
-        return ref8.run_kalman_filter(self.indexed_sensor_data, self.dtype, self.device, consts=c)
+        return ModelConsts.from_matrices('ref8', F=self.get_state_transition_matrix,
+                                         Q=self.get_process_noise_covariance_matrix,
+                                         H_gps=self.get_gps_observation_matrix(), H_imu=self.get_imu_observation_matrix(),
+                                         R_gps=self.get_gps_measurement_noise_covariance_matrix(),
+                                         R_imu=self.get_imu_measurement_noise_covariance_matrix(),
+                                         P0=getattr(self, 'P0', None))
 
     def run_dead_reckoning_for_IMU(self):
-        raise NotImplementedError('hw5_2.run_dead_reckoning_for_IMU is a plotting aid, out of scope')
+        """hw5_2.py:382-436: [(x, y, theta), ...] per IMU event of indexed_sensor_data (fixes
+        skipped, first dt 0, x0 = 0), the IMU events compacted and filtered on the GPU."""
+        return ref8.run_dead_reckoning(self.indexed_sensor_data, self.dtype, self.device, consts=self._consts())

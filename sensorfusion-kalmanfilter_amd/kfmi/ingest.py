@@ -179,9 +179,27 @@ def quaternion_to_euler(q, device=0):
     return out
 
 
+def select_events(stream, etype):
+    """The events of one type of an EventStream, in stream order (kf_events_select): returns
+    device (t [K], payload [K, 9], src [K] int32 stream positions)."""
+    n = len(stream)
+    dev = stream.t.device
+    t = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+    pay = torch.empty(max(n, 1), 9, dtype=torch.float64, device=dev)
+    src = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    k = ctypes.c_int64(0)
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    with torch.cuda.device(dev):
+        check(_lib.lib().kf_events_select(n, _ptr(stream.etype.contiguous()), _ptr(stream.t.contiguous()),
+                                          _ptr(stream.payload.contiguous()), int(etype), _ptr(t), _ptr(pay),
+                                          _ptr(src), ctypes.byref(k), st))
+    return t[:k.value], pay[:k.value], src[:k.value]
+
+
 def events_dt(t, prev0, rule, etype=None):
     """Per-event dt of a driver over a stream slice (kf_events_dt); returns (dt, etype_out) with
-    skipped events marked KF_EVENT_NONE.  rule: _lib.KF_DT_FULL / KF_DT_MONOTONE / KF_DT_RAW."""
+    skipped events marked KF_EVENT_NONE.  rule: _lib.KF_DT_FULL / KF_DT_MONOTONE / KF_DT_RAW.
+    prev0 NaN (FULL / RAW): no previous time yet, the first event gets dt 0."""
     n = int(t.shape[0])
     tc = t.contiguous()
     ec = None if etype is None else etype.contiguous()

@@ -18,7 +18,8 @@ Fixtures written (inputs and the reference's outputs, nothing else):
   ref15_scheduled.npz   run_kalman_filter_scheduled (826-957), Scheduler.gain/cov_matrix (112-185)
   ref15_drivers.npz run_kalman_filter (kf_workers.py:738-824, states + per-step covariances)
                     and run_no_update_kalman_filter (1060-1160), cold and warm
-  ref8_full.npz     hw5_2.run_kalman_filter (hw5_2.py:313-380), in-order and out-of-order streams
+  ref8_full.npz     hw5_2.run_kalman_filter (hw5_2.py:313-380) and run_dead_reckoning_for_IMU
+                    (382-436), in-order and out-of-order streams
   ingest.npz        load_data_from_csv / gps_to_modified_utm / compute_imu_biases /
                     unbias_imu_data / combine_sensor_data (kf_workers.py:290-385) and
                     hw5_2.gps_to_utm (hw5_2.py:29-54) on synthetic GPS and IMU CSVs in the
@@ -295,12 +296,16 @@ def ref8_full(h5):
     st = sf.run_kalman_filter()
     out = pack_events(events)
     out.update(states=np.array(st, dtype=np.float64))
+    # run_dead_reckoning_for_IMU (hw5_2.py:382-436) over the same list: IMU events only (the
+    # leading ones before the first fix included), x0 = 0, first dt 0, no initial record
+    out.update(dr_states=np.array(sf.run_dead_reckoning_for_IMU(), dtype=np.float64))
     # an out-of-order stream: hw5_2 has no dt < 0 guard, it predicts over the negative dt
     ev2 = synth_events(seed=18, seconds=0.8, out_of_order=True)
     sf.indexed_sensor_data = ev2
     st2 = sf.run_kalman_filter()
     out.update({'ooo_' + k: v for k, v in pack_events(ev2).items()})
     out.update(ooo_states=np.array(st2, dtype=np.float64))
+    out.update(ooo_dr_states=np.array(sf.run_dead_reckoning_for_IMU(), dtype=np.float64))
     np.savez_compressed(os.path.join(OUT, 'ref8_full.npz'), **out)
     print('ref8_full:', len(events), 'events')
 

@@ -151,6 +151,12 @@ def test_hw5_2_sequence(csvs):
     rs, _ = ref_kf.run_kalman_filter_8state(events)
     assert np.array(st).shape == np.array(rs).shape
     assert _rel(st, rs) <= 1e-6
+    # hw5_2.py:540: run_dead_reckoning_for_IMU over the same list (the rest of __main__, :543-546,
+    # plots these two outputs)
+    dr = sf.run_dead_reckoning_for_IMU()
+    rdr, _ = ref_kf.run_dead_reckoning_8state(events)
+    assert len(dr) == len(rdr) == sum(e[1] == 'IMU' for e in events)
+    assert _rel(dr, rdr) <= 1e-6
     assert abs(sf.quaternion_to_euler(0.0, 0.0, 0.0, 1.0)[2]) == 0.0
 
 

@@ -1,0 +1,107 @@
+"""hw5_2.run_dead_reckoning_for_IMU (hw5_2.py:382-436) on the GPU — needs an MI355X.
+
+The 8-state filter over the IMU events alone (fixes skipped, first dt 0, x0 = 0), against the
+reference's own outputs (tests/golden/ref8_full.npz: in-order and out-of-order streams) through
+both routes of kfmi.ref8.run_dead_reckoning — the reference's event list (host-built stream, one
+kf_run_events launch) and an EventStream (kf_events_select + kf_events_dt on the device) — and,
+over the bench's whole synthetic drive log (616,322 IMU rows, the time-parallel kf_run_stream
+route), against the C oracle's walk of the oracle's own ingest (oracle/cpu_kf.c
+cpu_ref8_dead_reckoning, pinned to the goldens by test_oracle.py).  Tolerance: 1e-6 relative
+(north_star, fp64).
+"""
+import numpy as np
+import pytest
+import torch
+
+import bench
+from golden_events import unpack_events
+from kfmi import _lib, ingest, ref8
+from oracle import cpu_kf, ref_ingest, ref_kf
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1.0))) if a.size else 0.0
+
+
+def _stream_from_golden(g, prefix):
+    """An EventStream holding a golden's merged events (as kf_ingest lays them out)."""
+    et = np.asarray(g[prefix + 'ev_type'], np.uint8)
+    t = np.asarray(g[prefix + 'ev_t'], np.float64)
+    pay = np.zeros((len(t), 9))
+    pay[et == 0, 0:3] = g[prefix + 'ev_gps'][et == 0]
+    pay[et == 1] = g[prefix + 'ev_imu'][et == 1]
+    d = torch.device('cuda', 0)
+    n = len(t)
+    return ingest.EventStream(torch.from_numpy(et).to(d), torch.from_numpy(t).to(d), torch.from_numpy(pay).to(d),
+                              torch.arange(n, dtype=torch.int32, device=d), torch.zeros(n, dtype=torch.int8, device=d),
+                              torch.zeros(n, dtype=torch.uint8, device=d), 0, np.zeros(3), np.zeros(3), np.zeros(2),
+                              int((et == 0).sum()), int((et == 1).sum()), True)
+
+
+@pytest.mark.parametrize('prefix', ['', 'ooo_'])
+def test_dead_reckoning_vs_reference_golden(golden_dir, prefix):
+    g = np.load(f'{golden_dir}/ref8_full.npz')
+    want = g[prefix + 'dr_states']
+    events = unpack_events(g, prefix)
+    st = ref8.run_dead_reckoning(events)
+    assert np.array(st).shape == want.shape
+    assert _rel(st, want) <= 1e-6
+    st2, P2 = ref8.run_dead_reckoning(_stream_from_golden(g, prefix), return_covariance=True)
+    assert np.array(st2).shape == want.shape
+    assert _rel(st2, want) <= 1e-6
+    _, rP = ref_kf.run_dead_reckoning_8state(events)
+    assert _rel(P2, rP) <= 1e-6
+
+
+def test_dead_reckoning_select_and_dt():
+    """kf_events_select keeps one type in stream order; kf_events_dt with prev0 = NaN gives the
+    first event dt 0 (hw5_2.py:401, 407) and the rest raw differences (no guard)."""
+    rng = np.random.default_rng(3)
+    n = 100_003
+    et = rng.choice([0, 1, 1, 1], n).astype(np.uint8)
+    t = np.cumsum(rng.uniform(0.0, 0.01, n)) + 1.7e9
+    t[500], t[501] = t[501], t[500]
+    pay = rng.normal(size=(n, 9))
+    d = torch.device('cuda', 0)
+    s = ingest.EventStream(torch.from_numpy(et).to(d), torch.from_numpy(t).to(d), torch.from_numpy(pay).to(d),
+                           torch.arange(n, dtype=torch.int32, device=d), torch.zeros(n, dtype=torch.int8, device=d),
+                           torch.zeros(n, dtype=torch.uint8, device=d), 0, np.zeros(3), np.zeros(3), np.zeros(2),
+                           int((et == 0).sum()), int((et == 1).sum()), True)
+    for ty in (0, 1, 7):
+        ts, ps, src = ingest.select_events(s, ty)
+        k = np.nonzero(et == ty)[0]
+        np.testing.assert_array_equal(src.cpu().numpy(), k)
+        np.testing.assert_array_equal(ts.cpu().numpy(), t[k])
+        np.testing.assert_array_equal(ps.cpu().numpy(), pay[k])
+    ts, _, _ = ingest.select_events(s, 1)
+    dt, eo = ingest.events_dt(ts, float('nan'), _lib.KF_DT_RAW)
+    th = t[et == 1]
+    np.testing.assert_array_equal(dt.cpu().numpy(), np.r_[0.0, np.diff(th)])
+    assert (eo.cpu().numpy() == _lib.KF_EVENT_IMU).all()
+    with pytest.raises(_lib.KFError):
+        ingest.events_dt(ts, float('nan'), _lib.KF_DT_MONOTONE)
+
+
+def test_dead_reckoning_whole_log_vs_oracle(tmp_path):
+    """The bench's whole synthetic drive log (config 1ref8's CSVs: 30,758 GPS rows, 616,322 IMU
+    rows) ingested on the device as hw5_2 does (no altitude), dead-reckoned through the
+    time-parallel route, against the C oracle's walk of the oracle's own ingest, every IMU
+    event."""
+    cfg = bench.CONFIGS['1ref8']
+    gp, ip = bench.synth_log(cfg, str(tmp_path))
+    stream = ingest.ingest_arrays(ingest.read_csv(gp, 4), ingest.read_csv(ip, 11), with_altitude=False, device=0)
+    st, P = ref8.run_dead_reckoning(stream, return_covariance=True)
+    chk = dict(ref8.dead_reckoning_check)
+    assert chk['ok'] and chk['chunks'] > 1000, chk
+    assert len(st) == stream.n_imu == cfg['n_imu']
+    events, _, _ = ref_ingest.ingest(gp, ip, with_altitude=False)
+    et = np.array([0 if e[1] == 'GPS' else 1 for e in events], np.uint8)
+    th = np.array([e[2] for e in events])
+    ph = np.zeros((len(events), 9))
+    ph[et == 1] = [e[3][1:10] for e in events if e[1] == 'IMU']
+    rt, _ = cpu_kf.ref8_dead_reckoning(et, th, ph)
+    assert rt.shape == (len(st), 3)
+    assert _rel(st, rt) <= 1e-6

@@ -87,6 +87,18 @@ def test_ref8_full(golden_dir):
     assert _rel(st, g['ooo_states']) < RTOL
 
 
+@pytest.mark.parametrize('prefix', ['', 'ooo_'])
+def test_ref8_dead_reckoning(golden_dir, prefix):
+    """hw5_2.run_dead_reckoning_for_IMU (hw5_2.py:382-436): the restatement against the
+    reference's own output, in-order and out-of-order (a negative IMU-to-IMU dt) streams."""
+    g = _load(golden_dir, 'ref8_full.npz')
+    events = unpack_events(g, prefix)
+    st, _ = ref_kf.run_dead_reckoning_8state(events)
+    want = g[prefix + 'dr_states']
+    assert len(st) == len(want) == sum(e[1] == 'IMU' for e in events)
+    assert _rel(st, want) < RTOL
+
+
 def test_ref15_run_kalman_filter_simple(golden_dir):
     g = _load(golden_dir, 'ref15_drivers.npz')
     events = unpack_events(g)
@@ -415,3 +427,26 @@ def test_c_ref8_events_vs_goldens(golden_dir, cpu_kf, prefix):
         sd = {'easting': pay[i, 0, 0], 'northing': pay[i, 1, 0]} if s == 'GPS' else ['t', *pay[i, :, 0]]
         x, P = ref_kf.step8(x, P, s, sd, dt[i, 0])
         assert abs(ld[i, 0] - np.linalg.slogdet(P)[1]) < 1e-10 * max(1.0, abs(np.linalg.slogdet(P)[1]))
+
+
+@pytest.mark.parametrize('prefix', ['', 'ooo_'])
+def test_c_ref8_dead_reckoning_vs_goldens(golden_dir, cpu_kf, prefix):
+    """oracle/cpu_kf.c's dead-reckoning walk (cpu_ref8_dead_reckoning) over the merged stream
+    reproduces the reference's hw5_2.run_dead_reckoning_for_IMU (ref8_full.npz) and the NumPy
+    restatement's log-dets."""
+    g = _load(golden_dir, 'ref8_full.npz')
+    events = unpack_events(g, prefix)
+    t, et, pay = _events_to_columns(events)
+    tr, ld = cpu_kf.ref8_dead_reckoning(et[:, 0], t[:, 0], pay[:, :, 0])
+    want = g[prefix + 'dr_states']
+    assert tr.shape == want.shape
+    assert _rel(tr, want) < 1e-10
+    x, P, prev, k = np.zeros(8), ref_kf.P0_REF8.copy(), None, 0
+    for (_, s, ti, sd) in events:
+        if s != 'IMU':
+            continue
+        x, P = ref_kf.step8(x, P, 'IMU', sd, ti - prev if prev is not None else 0.0)
+        prev = ti
+        assert abs(ld[k] - np.linalg.slogdet(P)[1]) < 1e-10 * max(1.0, abs(np.linalg.slogdet(P)[1]))
+        k += 1
+    assert k == len(ld)
