@@ -780,6 +780,14 @@ def sched_workload(cfg, args, rank, world, dev):
     sel_time = torch.empty(T, B, dtype=torch.float64, device=dev)
     n_sel = torch.empty(B, dtype=torch.int32, device=dev)
 
+    def gather_payload():
+        """N > 1: each rank's final states, each filter's last selected log-det and the
+        per-selection trajectory rows (rows past a filter's n_sel are its own unwritten rows:
+        the bitwise check compares a shard with itself)."""
+        x, _ = kf.state()
+        last = (n_sel.long() - 1).clamp(min=0)
+        return x, logdet.gather(0, last[None, :])[0], traj
+
     def step():
         if rows:
             _lib.check(_lib.lib().kf_run_scheduled(kf.handle, T, _ptr(tt), _ptr(etype), _ptr(pay), _ptr(prev),
@@ -835,7 +843,7 @@ def sched_workload(cfg, args, rank, world, dev):
     return dict(step=step, units=B * T, bytes=nbytes, bytes_per_unit=nbytes / (B * T),
                 kernel=kernel, traffic=load_traffic('sched') if measured_shape else None,
                 valu=load_valu('sched') if measured_shape else None,
-                cpu=cpu, gather=None, kf=kf,
+                cpu=cpu, gather=gather_payload, kf=kf,
                 roofline_note=f'{n_selected / (B * T):.3f} of the examined events are selected and applied (a '
                               f'full 15-state event each, its payload gathered per lane); the two passes move '
                               f'their actual HBM traffic (traffic, PMC: the gathers fetch whole 128-B lines) at '
@@ -923,6 +931,45 @@ def bf_workload(cfg, args, rank, world, dev):
                                                     f"evaluate_combo_chunk (kf_workers.py:22-97) in a spawn Pool of "
                                                     f"{npl['cores']} processes, NumPy {np.__version__}")}
 
+    def dist_check():
+        """N > 1, after the timed region: the search sharded by subset class across the ranks
+        (kfmi.dist.search_winner, the reduction brute_force_search uses: MIN of the first
+        accepted size, MAX of the bit-reversed winner mask; acceptance counts summed), at a
+        threshold that accepts 2 % of the subsets, against rank 0's own one-rank search of the
+        same candidates.  Replaces the reference's Pool(30) fan-out (kf_workers.py:1320-1346)."""
+        import torch.distributed as tdist
+        from kfmi import dist as kdist
+        thr = torch.tensor([float('-inf')], dtype=torch.float64)
+        if rank == 0:
+            _, _, _, sm = kf.search_combos(ev, init, t0, t_end, -1e30, exhaustive=True, subset_max=True)
+            vals = torch.sort(sm[torch.isfinite(sm)]).values
+            thr[0] = float(vals[len(vals) // 50]) + 1e-9
+            del sm, vals
+        thr = thr.to(kdist._tdev())
+        tdist.all_reduce(thr, op=tdist.ReduceOp.MAX)
+        thr = float(thr.item())
+        w = kdist.search_classes(n, world)
+        acc = np.zeros(n + 1, dtype=np.int64)
+
+        def search_class(n_fixed, fixed_mask):
+            k, idx, a, _ = kf.search_combos(ev, init, t0, t_end, thr, k_max=n, exhaustive=True, n_fixed=n_fixed,
+                                            fixed_mask=fixed_mask)
+            acc[:] += a.astype(np.int64)
+            return k, idx
+        won = kdist.search_winner(search_class, n, w)
+        total = kdist.sum_counts(acc)
+        out = {'threshold': thr, 'classes': 1 << w, 'k_found': won[0] if won else 0,
+               'winner': list(won[1]) if won else None, 'accepted_per_size': [int(v) for v in total]}
+        if rank == 0:
+            k1, idx1, acc1, _ = kf.search_combos(ev, init, t0, t_end, thr, exhaustive=True)
+            out['one_rank'] = {'k_found': k1, 'winner': list(idx1) if idx1 else None,
+                               'accepted_per_size': [int(v) for v in acc1]}
+            out['one_rank_equal'] = (out['k_found'] == k1 and out['winner'] == out['one_rank']['winner']
+                                     and out['accepted_per_size'] == out['one_rank']['accepted_per_size'])
+            if not out['one_rank_equal']:
+                raise SystemExit(f'the {world}-rank search disagrees with the one-rank search: {out}')
+        return out
+
     if search:
         from kfmi.ref15 import search_level_bytes
         step()  # how the library runs this search (kf_search_info): axis-symmetric, head, launches
@@ -941,7 +988,7 @@ def bf_workload(cfg, args, rank, world, dev):
                            f'{launches} launches of one search)',
                     traffic=load_traffic('bf', 2 * lvl), valu=load_valu('bf') if load_traffic('bf', 2 * lvl) else None,
                     cpu=cpu,
-                    gather=None, kf=kf, combos=total_combos,
+                    gather=None, dist_check=dist_check, kf=kf, combos=total_combos,
                     roofline_note='level-buffer bytes only (each stored prefix filter written and read once, the '
                                   'subsets holding candidate n-2 scored from registers); the search is fp64 issue / '
                                   'latency-bound (one event step, the final predict, two log-dets per subset; '
@@ -1121,7 +1168,7 @@ def main():
 
     kf = w['kf']
     bad = int((kf.status() != 0).sum().item()) if not args.config.startswith('bf') else 0
-    gather_ms = gather_info = None
+    gather_ms = gather_info = dist_info = None
     if dist:
         from kfmi import dist as kdist
         elapsed, kern_ms, bad = kdist.max_over_ranks([elapsed, kern_ms, bad], dev)
@@ -1153,6 +1200,8 @@ def main():
                            'bytes_gathered': res['bytes_per_rank'] * world,
                            'checked': 'bitwise: every rank finds its shard at its global offset'}
             del res
+        if w.get('dist_check') is not None:
+            dist_info = w['dist_check']()
 
     if rank == 0:
         rec = {
@@ -1211,6 +1260,8 @@ def main():
         if gather_ms is not None:
             rec['allgather_ms'] = gather_ms
             rec['allgather'] = gather_info
+        if dist_info is not None:
+            rec['dist_search'] = dist_info
         rec['cpu_baseline'] = w['cpu']() if (world == 1 and not args.no_cpu_baseline) else None
         if args.pcie and world == 1 and w.get('pcie'):
             rec['pcie_inclusive'] = w['pcie']()

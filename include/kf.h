@@ -37,7 +37,9 @@
  * needs more than every earlier one; every other launch allocates nothing.  Run such a call
  * once eagerly before capturing it: inside a capture nothing is allocated (kf_run_scheduled
  * then takes its fused kernel, the other two return KF_EINVAL).  A workspace a capture used
- * is never freed before kf_free, so a graph stays valid after a later, larger eager call.
+ * is never freed before kf_free, so a graph stays valid after a later, larger eager call: each
+ * such growth keeps the smaller buffer (retired) until kf_free or kf_release_retired, so a
+ * handle that alternates captures with ever-larger eager calls holds all of them.
  *
  * Threading: distinct handles may be used from different threads at once; one handle is used
  * by one thread at a time.  That includes the calls that only read it (kf_get_state,
@@ -214,6 +216,12 @@ int kf_init(int device);
 int kf_alloc(kf_batch** handle, int model, int64_t batch, int dtype, const kf_params* params);
 int kf_free(kf_batch* handle);
 
+/* Free the workspaces a graph capture used that larger eager calls have since replaced (see
+ * "Workspaces" above); *bytes_freed (nullable) = their size.  Call it only once every graph
+ * captured from this handle's calls is destroyed: their replays would write freed memory.
+ * The workspaces in use stay.  Synchronises the device (hipFree). */
+int kf_release_retired(kf_batch* handle, int64_t* bytes_freed);
+
 /* Dimensions of a handle (any pointer may be NULL).  For KF_MODEL_REF15: n = 15, m = 3 (GPS),
  * c = 0, and the covariance has 27 block-packed rows instead of n(n+1)/2 (KF_MODEL_REF8: n = 8,
  * m = 2, c = 0, 15 rows). */
@@ -369,9 +377,11 @@ int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const d
  * n_fixed / fixed_mask: search only the subsets whose intersection with candidates
  * 0 .. n_fixed - 1 is fixed_mask (0 / 0 = every subset; one class per GPU shards the search
  * evenly, kfmi.dist), k_max counting the fixed candidates,
- * n_accepted host [k_max + 1] (nullable) accepted subsets per size.  subset_max: device [2^n]
- * of the handle's dtype (n_events <= 30, nullable) receives every evaluated subset's max
- * log-determinant (NaN for a failed filter), indexed by mask.  Level k stores the C(n - 2, k)
+ * n_accepted host [k_max + 1] (nullable) accepted subsets per size (0 past *k_found when not
+ * `exhaustive`).  subset_max: device [2^n] of the handle's dtype (n_events <= 30, nullable)
+ * receives every evaluated subset's max log-determinant (NaN for a failed filter), indexed by
+ * mask; not `exhaustive`, the sizes past *k_found that the one-launch head scored are written
+ * too (KF_OPT_SEARCH_HEAD; the level-by-level search leaves them untouched).  Level k stores the C(n - 2, k)
  * subsets whose largest free candidate is <= n - 3 (a subset holding n - 1 has no extensions,
  * one holding n - 2 only the one adding n - 1, which is scored from registers); C(n - 2, k)
  * must stay below 2^28, and the handle's level buffers take 2 * C(n - 2, k) * (28 w + 16)

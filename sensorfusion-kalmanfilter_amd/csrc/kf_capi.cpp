@@ -66,7 +66,7 @@ struct kf_batch {
     // a graph capture baked the address of this workspace in: its replays write it, so it is
     // never freed before kf_free (a larger one replaces it and it moves to `retired`)
     bool search_ws_graph, stream_ws_graph, sched_ws_graph;
-    std::vector<void*> retired;
+    std::vector<std::pair<void*, size_t>> retired;
     int64_t search_info[4];  // the last kf_search_combos: sym, head sizes, level launches, level bytes
 };
 
@@ -136,7 +136,7 @@ bool grow_ws(kf_batch* h, void** buf, size_t* bytes, bool* graph, size_t need, h
     if (*bytes >= need) return true;
     if (capturing(st)) return false;
     if (*buf) {
-        if (*graph) h->retired.push_back(*buf);
+        if (*graph) h->retired.emplace_back(*buf, *bytes);
         else (void)hipFree(*buf);
     }
     *buf = nullptr;
@@ -598,8 +598,20 @@ int kf_free(kf_batch* h) {
     if (h->pend_done) (void)hipEventDestroy(h->pend_done);
     if (h->kc) (void)hipFree(h->kc);
     if (h->sched_ws) (void)hipFree(h->sched_ws);
-    for (void* p : h->retired) (void)hipFree(p);
+    for (auto& r : h->retired) (void)hipFree(r.first);
     delete h;
+    return KF_OK;
+}
+
+int kf_release_retired(kf_batch* h, int64_t* bytes_freed) {
+    if (int rc = check_handle(h)) return rc;
+    int64_t freed = 0;
+    for (auto& r : h->retired) {
+        (void)hipFree(r.first);
+        freed += static_cast<int64_t>(r.second);
+    }
+    h->retired.clear();
+    if (bytes_freed) *bytes_freed = freed;
     return KF_OK;
 }
 
@@ -950,9 +962,12 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
                                                align256(sizeof(double) * 4 * nch * C)
                                          : 0;
     const int64_t ntiles = (C + kfmi::kStreamScanTile - 1) / kfmi::kStreamScanTile;
+    // more tiles than one scan round: the top kernel writes the tile starts (kf_ref.hip phase 3)
+    const bool top = ntiles > kfmi::kStreamScanTile;
+    const size_t top_bytes = top ? align256(sizeof(double) * 3 * nch * ntiles) : 0;
     const size_t need = 256 + 2 * bank1 + bank4 + 2 * align256(sizeof(double) * 12 * nch * C) +
                         align256(sizeof(double) * 12 * nch * ntiles) + align256(sizeof(double) * n * C) + lft_bytes +
-                        rec_bytes;
+                        rec_bytes + top_bytes;
     if (!grow_ws(h, &h->stream_ws, &h->stream_ws_bytes, &h->stream_ws_graph, need, static_cast<hipStream_t>(stream)))
         return capturing(static_cast<hipStream_t>(stream))
                    ? fail(KF_EINVAL, "kf_run_stream: the chunk banks (%zu bytes) must be sized by an eager call "
@@ -992,6 +1007,10 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     p += align256(sizeof(double) * 12 * nch * ntiles);
     sa.starts = reinterpret_cast<double*>(p);
     p += align256(sizeof(double) * n * C);
+    if (top) {
+        sa.tstart = reinterpret_cast<double*>(p);
+        p += top_bytes;
+    }
     if (lft) {
         sa.phi = reinterpret_cast<double*>(p);
         p += align256(sizeof(double) * 36 * nch * C * np);
@@ -1076,13 +1095,15 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
         if (e == hipSuccess) e = chain(C, sa.mx, sa.mP, sa.mst, L, 0, true, traj ? traj4 : nullptr, 4, 4);
         // the maps composed into the chunk starts (the tile scan, then the starts kernel, which
         // composes the tile products itself), and the verdict
-        for (int ph : {kfmi::kStreamPhaseScanTiles, kfmi::kStreamPhaseStarts})
-            if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
+        for (int ph : {kfmi::kStreamPhaseScanTiles, kfmi::kStreamPhaseTop, kfmi::kStreamPhaseStarts})
+            if (e == hipSuccess && (ph != kfmi::kStreamPhaseTop || top))
+                e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
         if (e == hipSuccess && traj) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseRecords, sa, st);
     } else {
         if (e == hipSuccess) e = chain(C, sa.mx, sa.mP, sa.mst, L, 0, false, nullptr, 1, 4);
-        for (int ph : {kfmi::kStreamPhaseScanTiles, kfmi::kStreamPhaseStarts})
-            if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
+        for (int ph : {kfmi::kStreamPhaseScanTiles, kfmi::kStreamPhaseTop, kfmi::kStreamPhaseStarts})
+            if (e == hipSuccess && (ph != kfmi::kStreamPhaseTop || top))
+                e = kfmi::launch_stream_phase(h->model, f64, ph, sa, st);
         if (e == hipSuccess) e = chain(C, sa.fx, sa.fP, sa.fst, L, 0, true);
         if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseFinish, sa, st);
     }
@@ -1307,8 +1328,11 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
     h->search_info[3] = static_cast<int64_t>(level);
     *k_found = found;
     *winner = found ? __builtin_bitreverse64(best[found]) : 0;
+    // without `exhaustive` the search ends at the first accepted size: the one-launch head may
+    // have counted larger sizes too, which the level-by-level search never reaches
+    const int reported = !exhaustive && found ? found : last;
     if (n_accepted)
-        for (int k = 0; k <= k_max; ++k) n_accepted[k] = k <= last ? acc[k] : 0;
+        for (int k = 0; k <= k_max; ++k) n_accepted[k] = k <= reported ? acc[k] : 0;
     return KF_OK;
 }
 

@@ -130,6 +130,8 @@ struct StreamArgs {
     double* maps;            // [C][chains][12]: per chunk and chain, A (3x3) and b of x_end = A x_start + b
     double* pref;            // [C][chains][12]: the product of the chunk maps before c in c's tile
     double* tiles;           // [C / kScanTile][chains][12]: each tile's product
+    double* tstart;          // [C / kScanTile][chains][3]: each tile's start (phase 3), or nullptr
+                             // (one scan round of tiles: the starts kernel composes its prefix)
     double* starts;          // [N][C] the chunk starts (fp64)
     double* dtab;            // [C][chains][4] (records from the map pass): start - guess per chain component
     StreamCheck* check;
@@ -167,7 +169,7 @@ constexpr int kStreamPhaseLftMaps = 6, kStreamPhaseLftStart = 7;
 // check->bad bits: a chunk filter failed / a chunk start or the end state is not finite
 constexpr int kStreamBadFilter = 1, kStreamBadStart = 2;
 // records from the map pass: phase 8 = trajectories from the variants and the chunk starts
-constexpr int kStreamPhaseScanTiles = 2, kStreamPhaseStarts = 4, kStreamPhaseFinish = 5,
+constexpr int kStreamPhaseScanTiles = 2, kStreamPhaseTop = 3, kStreamPhaseStarts = 4, kStreamPhaseFinish = 5,
               kStreamPhaseRecords = 8;
 constexpr int64_t kStreamScanTile = 256;  // chunks per scan tile (kScanTile in kf_ref.hip)
 

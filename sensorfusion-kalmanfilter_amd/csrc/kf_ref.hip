@@ -1295,10 +1295,57 @@ __global__ __launch_bounds__(kScanTile) void stream_scan_tiles_kernel(const Stre
     }
 }
 
+// phase 3 (only when there are more tiles than one scan round holds): grid (1, chains).  The
+// scan's top phase as a launch of its own: rounds of kScanTile tile products, each scanned and
+// applied to the carried state, give every tile's start state in a.tstart.  Below that size
+// the starts kernel composes its own prefix (one round per block, no launch).
+template <typename T, class M>
+__global__ __launch_bounds__(kScanTile) void stream_top_kernel(const StreamArgs a) {
+    constexpr int NCH = M::NP + M::NA;
+    __shared__ double pre[12][kScanTile];
+    __shared__ double carry[3];
+    const int tid = int(threadIdx.x);
+    const int ch = int(blockIdx.y);
+    const int ns = ch < M::NP ? 3 : 2;
+    const int64_t ntiles = (a.C + kScanTile - 1) / kScanTile;
+    if (tid < 3) carry[tid] = tid < ns ? double(static_cast<const T*>(a.hx)[chain_state<M>(ch, tid)]) : 0.0;
+    for (int64_t r0 = 0; r0 < ntiles; r0 += kScanTile) {
+        const int64_t t = r0 + tid;
+        double v[12];
+        if (t < ntiles) {
+#pragma unroll
+            for (int e = 0; e < 12; ++e) v[e] = a.tiles[(t * NCH + ch) * 12 + e];
+        } else {
+            affine_identity(v);
+        }
+        __syncthreads();  // carry written (the previous round / the init), pre free
+        block_scan_affine(v, pre, tid);
+        if (t < ntiles) {  // tile t's start: the round's carry through the tiles before t
+            double x[3] = {carry[0], carry[1], carry[2]};
+            if (tid > 0) {
+                double e1[12];
+#pragma unroll
+                for (int e = 0; e < 12; ++e) e1[e] = pre[e][tid - 1];
+                apply_map(x, e1);
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) a.tstart[(t * NCH + ch) * 3 + k] = x[k];
+        }
+        __syncthreads();  // every thread has read carry and pre
+        if (tid == kScanTile - 1) {  // the round's product (identity maps past the last tile)
+            double xe[3] = {carry[0], carry[1], carry[2]};
+            apply_map(xe, v);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) carry[k] = xe[k];
+        }
+    }
+}
+
 // phase 4: grid (tiles, chains).  Each block first composes the products of the tiles before
-// its own (the scan's top phase, which was a launch of its own: every block redoes its prefix,
-// ntiles maps of 12 doubles, in rounds of kScanTile) into its tile start; the block of the last
-// tile also runs through its own product: the stream's end state.
+// its own into its tile start — at most one round of kScanTile tiles; with more tiles the top
+// kernel (phase 3) has written every tile start to a.tstart, since redoing the prefix per block
+// would cost O(ntiles^2) — and the block of the last tile also runs through its own
+// product: the stream's end state.
 template <typename T, class M>
 __global__ __launch_bounds__(kScanTile) void stream_starts_kernel(const StreamArgs a) {
     constexpr int NCH = M::NP + M::NA;
@@ -1309,8 +1356,12 @@ __global__ __launch_bounds__(kScanTile) void stream_starts_kernel(const StreamAr
     const int ns = ch < M::NP ? 3 : 2;
     const int64_t tile = blockIdx.x, c = tile * kScanTile + tid;
     const int64_t ntiles = gridDim.x;
-    if (tid < 3) carry[tid] = tid < ns ? double(static_cast<const T*>(a.hx)[chain_state<M>(ch, tid)]) : 0.0;
-    for (int64_t r0 = 0; r0 < tile; r0 += kScanTile) {
+    if (a.tstart) {
+        if (tid < 3) carry[tid] = tid < ns ? a.tstart[(tile * NCH + ch) * 3 + tid] : 0.0;
+    } else if (tid < 3) {
+        carry[tid] = tid < ns ? double(static_cast<const T*>(a.hx)[chain_state<M>(ch, tid)]) : 0.0;
+    }
+    for (int64_t r0 = 0; !a.tstart && r0 < tile; r0 += kScanTile) {
         const int64_t t = r0 + tid;
         double v[12];
         if (t < tile) {
@@ -3655,6 +3706,9 @@ void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
             stream_scan_tiles_kernel<T, M><<<g, kScanTile, 0, stream>>>(a);
             break;
         }
+        case kStreamPhaseTop:
+            stream_top_kernel<T, M><<<dim3(1, NCH), kScanTile, 0, stream>>>(a);
+            break;
         case kStreamPhaseStarts: {
             const dim3 g(unsigned((a.C + kScanTile - 1) / kScanTile), NCH);
             stream_starts_kernel<T, M><<<g, kScanTile, 0, stream>>>(a);

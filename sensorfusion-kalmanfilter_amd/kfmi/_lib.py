@@ -98,6 +98,7 @@ SIGNATURES = {
     'kf_init': (_i, [_i]),
     'kf_alloc': (_i, [ctypes.POINTER(_vp), _i, _i64, _i, ctypes.POINTER(kf_params)]),
     'kf_free': (_i, [_vp]),
+    'kf_release_retired': (_i, [_vp, ctypes.POINTER(_i64)]),
     'kf_dims': (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),
                      ctypes.POINTER(_i64), ctypes.POINTER(_i)]),
     'kf_reset': (_i, [_vp, _vp, _vp]),

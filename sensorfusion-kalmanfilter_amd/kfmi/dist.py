@@ -157,19 +157,35 @@ def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, init
         def finish(k, idx):
             return ref15.brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device,
                                             indices=idx, consts=consts)
-    backend = dist.get_backend(group)
-    tdev = torch.device('cuda', torch.cuda.current_device()) if backend == 'nccl' else torch.device('cpu')
     try:
-        k_r, key_r = _NONE, 0  # this rank: smallest accepted size, and its max bit-reversed mask
-        for c in range(rank, 1 << w, world):
-            k, idx = search_class(w, c)
-            if k and idx is not None:
-                key = _bitrev64(sum(1 << i for i in idx))
-                if k < k_r or (k == k_r and key > key_r):
-                    k_r, key_r = k, key
+        won = search_winner(search_class, n, w, group)
     finally:
         if kf is not None:
             kf.close()
+    return None if won is None else finish(*won)
+
+
+def _tdev(group=None):
+    import torch.distributed as dist
+    return torch.device('cuda', torch.cuda.current_device()) if dist.get_backend(group) == 'nccl' else torch.device('cpu')
+
+
+def search_winner(search_class, n, w, group=None):
+    """The cross-rank half of ``brute_force_search``: this rank searches its classes c = rank,
+    rank + world, ... of the 2^w (``search_class(w, c) -> (k, indices or None)``), keeping the
+    smallest accepted size and, at it, the first subset in itertools.combinations order; two
+    all-reduces (MIN of the size, then MAX of the bit-reversed mask as two 32-bit halves) give
+    every rank the global winner (k, indices), or None when no class accepted a subset."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    tdev = _tdev(group)
+    k_r, key_r = _NONE, 0  # this rank: smallest accepted size, and its max bit-reversed mask
+    for c in range(rank, 1 << w, world):
+        k, idx = search_class(w, c)
+        if k and idx is not None:
+            key = _bitrev64(sum(1 << i for i in idx))
+            if k < k_r or (k == k_r and key > key_r):
+                k_r, key_r = k, key
     t = torch.tensor([k_r], dtype=torch.int64, device=tdev)
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     k_min = int(t.item())
@@ -182,7 +198,16 @@ def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, init
                       dtype=torch.int64, device=tdev)
     dist.all_reduce(lo, op=dist.ReduceOp.MAX, group=group)
     mask = _bitrev64((int(hi.item()) << 32) | int(lo.item()))
-    return finish(k_min, tuple(i for i in range(n) if (mask >> i) & 1))
+    return k_min, tuple(i for i in range(n) if (mask >> i) & 1)
+
+
+def sum_counts(counts, group=None):
+    """Element-wise sum over the ranks of a per-size count array (uint64 values < 2^63)."""
+    import numpy as np
+    import torch.distributed as dist
+    t = torch.as_tensor(np.asarray(counts, dtype=np.int64), device=_tdev(group))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t.cpu().numpy()
 
 
 def _bitrev64(v):

@@ -103,6 +103,14 @@ class BatchedKF:
             _lib.lib().kf_free(self._h)
             self._h = None
 
+    def release_retired(self):
+        """Free the workspaces earlier graph captures used and larger eager calls replaced
+        (kf_release_retired); only once every graph captured from this handle is destroyed.
+        Returns the bytes freed."""
+        out = ctypes.c_int64(0)
+        check(_lib.lib().kf_release_retired(self.handle, ctypes.byref(out)))
+        return out.value
+
     def __del__(self):
         try:
             self.close()

@@ -834,12 +834,13 @@ def legacy_words(n):
 
 def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt=None, initial_state=None,
                                 selection_method=None, processing_frequency=None, print_output=False,
-                                dtype='f64', device=0, consts=None):
+                                dtype='f64', device=0, consts=None, parallel=True):
     """kf_workers.py:826-957 on the GPU.  'greedy': windowing, Scheduler scoring and the filter
     all run in kf_run_scheduled; 'random': the same in kf_run_scheduled_random, each pick
     np.random.choice over the queue drawn on the device from the global NumPy generator's outputs
     in the reference's order (the generator advances by the outputs drawn).  Returns (states,
-    logdets, P)."""
+    logdets, P).  parallel=False: the random arm's picked events run as the single filter even
+    where kf_run_events would take the time-parallel route (a long log; tests)."""
     if selection_method not in ('random', 'greedy'):
         print("Invalid selection_method. Choose either 'random' or 'greedy'.")
         return None
@@ -893,7 +894,8 @@ def run_kalman_filter_scheduled(events, start_idx=None, end_idx=None, initial_pt
         paydev = torch.as_tensor(pay[:, :, 0].astype(npd), device=dev)
         ev_p = torch.cat([torch.zeros(1, 9, dtype=paydev.dtype, device=dev), paydev[sel]])
         kf.set_state(x0[:, None].astype(npd), to_blocks(P)[:, None].astype(npd))
-        tr, ld, _, _ = kf.run_events(ev_t[:, None], ev_dt[:, None], ev_p[:, :, None].contiguous())
+        tr, ld, _, _ = kf.run_events(ev_t[:, None], ev_dt[:, None], ev_p[:, :, None].contiguous(),
+                                     sequential=not parallel)
         tr, ld, stt = tr.double().cpu().numpy(), ld.double().cpu().numpy(), st_d.cpu().numpy()
         _, Pb = kf.state()
         Pf = from_blocks(Pb[:, 0].double().cpu().numpy())

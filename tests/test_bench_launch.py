@@ -60,14 +60,16 @@ def test_bench_world_mismatch_exits_nonzero():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('config', ['3', 'ref15'])
+@pytest.mark.parametrize('config', ['3', 'ref15', 'sched', 'bf'])
 def test_bench_two_ranks_on_the_gpu(config):
     """`python bench.py --gpus 2` end to end on the GPU box, started as a fresh child process:
     two ranks (gloo: they share the box's one GPU; the 8-GPU node's run is RCCL), each owning
     its shard of filters, max-over-ranks timing, and the final all-gather of the final states,
     last log-dets and the decimated trajectory, which every rank checks bitwise against its own
     shard (bench.py's N > 1 path; replaces the reference's Pool(30) fan-out,
-    kf_workers.py:1320-1346)."""
+    kf_workers.py:1320-1346).  bf: the brute-force search sharded by subset class across the two
+    ranks with its cross-rank reductions (kfmi.dist.search_winner / sum_counts) gives rank 0's
+    one-rank winner and acceptance counts."""
     cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--dist-backend', 'gloo', '--config', config,
            '--batch', '65536', '--steps', '2', '--warmup', '1', '--no-cpu-baseline']
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
@@ -77,6 +79,12 @@ def test_bench_two_ranks_on_the_gpu(config):
     rec = json.loads(lines[0])
     assert rec['n_gpus'] == rec['ranks_seen'] == 2
     assert rec['failed_filters'] == 0 and rec['value'] > 0
+    if config == 'bf':
+        ds = rec['dist_search']
+        assert ds['one_rank_equal'] and ds['k_found'] > 0 and ds['classes'] >= 2
+        assert ds['winner'] == ds['one_rank']['winner'] and ds['accepted_per_size'] == ds['one_rank']['accepted_per_size']
+        assert sum(ds['accepted_per_size']) > 0
+        return
     ag = rec['allgather']
     assert ag['checked'].startswith('bitwise') and ag['traj_steps'] > 0
     assert ag['bytes_gathered'] == 2 * ag['bytes_per_rank'] > 0

@@ -277,6 +277,9 @@ def test_search_head_equals_level_search(golden_dir, n_fixed, fixed_mask):
     np.testing.assert_array_equal(a[0], b[0])
     assert a[1][:2] == b[1][:2] and a[2][:2] == b[2][:2] and a[1][0] > 0
     np.testing.assert_array_equal(a[1][2], b[1][2])
+    # not exhaustive: the counts stop at the first accepted size whichever way the levels ran
+    np.testing.assert_array_equal(a[2][2], b[2][2])
+    assert a[2][0] > 0 and not a[2][2][a[2][0] + 1:].any()
 
 
 def _axis_symmetric(init):
@@ -926,6 +929,11 @@ def test_scheduled_graph_survives_a_larger_eager_call():
     g.replay()
     torch.cuda.synchronize()
     got = [o.cpu().numpy() for o in outs]
+    # the graph is destroyed: its workspace can go (kf_release_retired), once
+    del g
+    assert kf.release_retired() > 0 and kf.release_retired() == 0
+    run(kf, 3 * T)           # the grown workspace is still the handle's
+    torch.cuda.synchronize()
     kf.close()
     np.testing.assert_array_equal(got[3], eager[3])
     live = np.arange(T)[:, None] < eager[3][None, :]
@@ -1022,3 +1030,27 @@ def test_search_full_size_sampled_vs_per_subset():
 
 # The ref15 / ref15f32 / sched rows at their bench sizes against the oracle (>= 4096 filters plus
 # the wave and batch edges): tests/test_gpu_bench_parity.py
+
+
+def test_scheduled_random_long_log_stream_route(tmp_path):
+    """The random arm over a whole drive log (the config-1 CSVs, 50 Hz: ~146k picks, beyond
+    kf_run_events' one-filter time-parallel threshold of 65,536 events, so its leading padding
+    event goes through kf_run_stream): with np.random seeded alike the picks are the
+    same, the states and log-dets equal the single filter's over the same picked events
+    (parallel=False) at roundoff, and the global generator ends at the same place."""
+    import bench
+    from kfmi import ingest
+    from kfmi.kf_workers import EventList
+    gp, ip = bench.synth_log(bench.CONFIGS['1'], str(tmp_path))
+    stream = ingest.ingest_arrays(ingest.read_csv(gp, 4), ingest.read_csv(ip, 11), device=0)
+    ev = EventList(stream)
+    out = []
+    for par in (True, False):
+        np.random.seed(3)
+        st, ld, P = ref15.run_kalman_filter_scheduled(ev, None, None, None, None, 'random', 50.0, parallel=par)
+        out.append((np.array(st), np.array(ld), P, np.random.random()))
+    (s1, l1, P1, r1), (s2, l2, P2, r2) = out
+    assert len(s1) == len(s2) > 65536 + 1 and r1 == r2
+    np.testing.assert_array_equal(s1[:, 0], s2[:, 0])        # the picked times
+    rel = lambda a, b: float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1.0)))  # noqa: E731
+    assert rel(s1[:, 1:], s2[:, 1:]) <= 1e-9 and rel(l1, l2) <= 1e-9 and rel(P1, P2) <= 1e-9

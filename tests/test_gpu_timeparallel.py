@@ -271,6 +271,20 @@ def test_many_chunks_multi_round_scan():
         assert _rel(a, b) <= 1e-9
 
 
+def test_many_tiles_top_scan():
+    """Far more chunks than one scan round of tiles (2.2M events in chunks of 8: 275,000 chunks,
+    1,075 tiles, five rounds of the top kernel, kf_ref.hip phase 3, instead of every starts block
+    redoing its prefix): records, final state and covariance equal the single filter's."""
+    et, dt, pay, x0 = _stream(2_200_000, seed=31, skips=40)
+    seq = _sequential(et, dt, pay, x0)
+    par = _parallel(et, dt, pay, x0, chunk=8)
+    chk = ref15.parallel_check
+    assert chk['ok'] and chk['chunks'] > 256 * 1024, chk
+    for a, b in zip(par, seq):
+        assert a.shape == b.shape
+        assert _rel(a, b) <= 1e-9
+
+
 def test_stream_run_replays_as_a_hip_graph():
     """kf_run_stream's launches (after a first eager call has sized the workspace) capture into a
     hipGraph as they are — no host synchronisation or allocation — and the replay gives the
