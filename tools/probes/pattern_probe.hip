@@ -70,6 +70,82 @@ __global__ __launch_bounds__(256) void pattern_kernel(const void* u, const void*
         if (t + j < T_) step(t + j, buf[j]);
 }
 
+// Round 5 candidate: pattern_kernel with its stores phase-separated from its
+// loads per wave — each step's six trajectory values and log-det are held in registers for HOLD
+// steps and stored as one burst of HOLD * 7 row stores, so a wave alternates runs of loads with
+// runs of stores instead of interleaving them every step.  Same loads, same rows, same bytes.
+template <int D, typename T, int DEPTH, int HOLD>
+__global__ __launch_bounds__(256) void pattern_burst_kernel(const void* u, const void* z, void* traj, void* logdet,
+                                                            int64_t B, int T_, int k_upd) {
+    constexpr int N = 2 * D;
+    static_assert(DEPTH % HOLD == 0, "bursts end at ring boundaries");
+    const int64_t f = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (f >= B) return;
+    const uint32_t off = uint32_t(f) * uint32_t(sizeof(T));
+    const uint32_t rb = uint32_t(B) * uint32_t(sizeof(T));
+    const int U = T_ / k_upd;
+    int ld_upd_step = k_upd - 1;
+    int ld_s = 0;
+    const uint32_t rb_z = U > 0 ? rb : 0u;
+    auto load_in = [&](int t, ProbeIn<D, T>& in) {
+        const int tc = t < T_ ? t : T_ - 1;
+        if (tc > ld_upd_step) {
+            ld_upd_step += k_upd;
+            ++ld_s;
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) in.u[i] = ldb_stream(u, int64_t(tc) * D + i, rb, off, T(0));
+        int s = ld_s < U ? ld_s : U - 1;
+        s = s > 0 ? s : 0;
+        const uint32_t rbz = tc == ld_upd_step ? rb_z : 0u;
+#pragma unroll
+        for (int i = 0; i < D; ++i) in.z[i] = ldb_stream(z, int64_t(s) * D + i, rbz, off, T(0));
+    };
+    T acc = T(0);
+    T held[HOLD][N + 1];
+    auto step = [&](int j, const ProbeIn<D, T>& in) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) acc += in.u[i] + in.z[i];
+#pragma unroll
+        for (int i = 0; i < N; ++i) held[j % HOLD][i] = acc + T(i);
+        held[j % HOLD][N] = acc;
+    };
+    auto burst = [&](int t0, int n) {
+#pragma unroll
+        for (int h = 0; h < HOLD; ++h) {
+            if (h >= n) break;
+#pragma unroll
+            for (int i = 0; i < N; ++i) stb_rec(traj, int64_t(t0 + h) * N + i, rb, off, held[h][i]);
+            stb_rec(logdet, t0 + h, rb, off, held[h][N]);
+        }
+    };
+    ProbeIn<D, T> buf[DEPTH];
+#pragma unroll
+    for (int j = 0; j < DEPTH - 1; ++j) load_in(j, buf[j]);
+    __builtin_amdgcn_s_waitcnt(0);
+    int t = 0;
+    for (; t + DEPTH <= T_; t += DEPTH) {
+#pragma unroll
+        for (int j = 0; j < DEPTH; ++j) {
+            load_in(t + j + DEPTH - 1, buf[(j + DEPTH - 1) % DEPTH]);
+            step(j, buf[j]);
+            if (j % HOLD == HOLD - 1) burst(t + j - (HOLD - 1), HOLD);
+        }
+    }
+    int h = 0;
+#pragma unroll
+    for (int j = 0; j < DEPTH - 1; ++j)
+        if (t + j < T_) {
+            step(j, buf[j]);
+            ++h;
+            if (h == HOLD) {
+                burst(t + j - (HOLD - 1), HOLD);
+                h = 0;
+            }
+        }
+    if (h) burst(T_ - h, h);
+}
+
 // ref_events_lds_kernel's memory instructions (kf_ref.hip): the state rows loaded once and
 // stored once, each event's payload / dt / type moved HBM -> LDS by buffer_load ... lds into
 // one of two per-wave images while the previous event is consumed, the same counted waits, and
@@ -254,6 +330,30 @@ extern "C" int kfprobe_pattern(int axes, int f64, const void* u, const void* z, 
     else e = f64 ? launch<2, double>(u, z, traj, logdet, B, T, update_every, st)
                  : launch<2, float>(u, z, traj, logdet, B, T, update_every, st);
     return int(e);
+}
+
+// pattern_burst_kernel (cv3 / cv2 buffers as kfprobe_pattern; hold = 1, 2, 4 or 8 steps per
+// store burst; hold 1 is pattern_kernel's interleaving).
+extern "C" int kfprobe_pattern_burst(int axes, int f64, const void* u, const void* z, void* traj, void* logdet,
+                                     int64_t B, int T, int update_every, int hold, void* stream) {
+    if ((axes != 2 && axes != 3) || B <= 0 || T <= 0 || update_every < 1 || B * 8 >= (int64_t(1) << 31))
+        return int(hipErrorInvalidValue);
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const dim3 g(unsigned((B + 255) / 256));
+#define KF_BURST(H)                                                                                            \
+    if (hold == H) {                                                                                           \
+        if (axes == 3 && f64) pattern_burst_kernel<3, double, 8, H><<<g, 256, 0, st>>>(u, z, traj, logdet, B, T, update_every); \
+        else if (axes == 3) pattern_burst_kernel<3, float, 8, H><<<g, 256, 0, st>>>(u, z, traj, logdet, B, T, update_every);   \
+        else if (f64) pattern_burst_kernel<2, double, 8, H><<<g, 256, 0, st>>>(u, z, traj, logdet, B, T, update_every);        \
+        else pattern_burst_kernel<2, float, 8, H><<<g, 256, 0, st>>>(u, z, traj, logdet, B, T, update_every);                  \
+        return int(hipGetLastError());                                                                         \
+    }
+    KF_BURST(1)
+    KF_BURST(2)
+    KF_BURST(4)
+    KF_BURST(8)
+#undef KF_BURST
+    return int(hipErrorInvalidValue);
 }
 
 // etype [T][B] u8, dt [T][B] f64, payload [T][9][B], x [15][B], P [27][B], traj [T][6][B],
