@@ -1253,6 +1253,7 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.prev_time = prev_time;
         a.target_end = target_end;
         a.threshold = threshold;
+        kfmi::set_search_band(a, h->dtype == KF_F64);
         a.child = lv[K & 1];
         a.best = d_best;
         a.n_acc = d_acc;
@@ -1289,6 +1290,7 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.prev_time = prev_time;
         a.target_end = target_end;
         a.threshold = threshold;
+        kfmi::set_search_band(a, h->dtype == KF_F64);
         a.par = k > 1 ? lv[(k - 1) & 1] : nullptr;
         a.child = k < kf_max ? lv[k & 1] : nullptr;
         a.best = d_best;

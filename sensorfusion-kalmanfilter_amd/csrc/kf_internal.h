@@ -200,9 +200,10 @@ struct Ref15ComboArgs {
 // k - 1's stored states.  Levels are in colex order: the subsets whose largest event is j hold
 // ranks [C(j, k), C(j + 1, k)) and child rank = parent rank + C(j, k).  One lane per parent
 // evaluates all of its children.  Level buffer: node blocks of 64 nodes, block b =
-//   [28][64] T       block-packed P (27), running max log-det (NaN = failed filter); no state:
-//                    the max log-det depends on the covariance alone (sym: [10][64], one pva
-//                    block, one aw block, the max)
+//   [28][64] T       block-packed P (27), the running max log-det's determinant: its mantissa
+//                    (NaN = failed filter); no state: the max log-det depends on the covariance
+//                    alone (sym: [10][64], one pva block, one aw block, the mantissa)
+//   [64] int32       the running max's binary exponent
 //   [64] double      time of the last applied event
 //   [64] uint64      subset bit mask
 struct Ref15SearchArgs {
@@ -221,6 +222,10 @@ struct Ref15SearchArgs {
     double prev_time;        // root time
     double target_end;
     double threshold;        // acceptance: max log-det < threshold (kf_workers.py:1353)
+    // the same test on the max's determinant (set_search_band): accepted below 2^lo_e lo_m,
+    // rejected above 2^hi_e hi_m, the log decides in between; mode 1 / 2: accept all / none
+    double band_lo_m, band_hi_m;
+    int band_lo_e, band_hi_e, band_mode;
     const void* par;         // level k - 1 buffer (unused for k = 1)
     void* child;             // level k buffer, or nullptr when level k is not stored
     uint64_t* best;          // device [65]: per subset size, max over accepted subsets of bitrev(mask)
@@ -242,11 +247,12 @@ struct Ref15SearchArgs {
     const RefConsts* kc;     // the handle's noise constants, or nullptr (the reference's)
 };
 
-// T rows of a search node: the block-packed P (27) and the running max log-det; an axis-symmetric
-// search (Ref15SearchArgs::sym) keeps one pva block and one aw block (6 + 3) and the max
+// T rows of a search node: the block-packed P (27) and the running max's mantissa; an
+// axis-symmetric search (Ref15SearchArgs::sym) keeps one pva block and one aw block (6 + 3) and
+// the mantissa; then 4 B of exponent, 8 B of time and 8 B of mask per node
 __host__ __device__ constexpr int search_rows(bool sym) { return sym ? 10 : 28; }
 __host__ __device__ constexpr uint64_t search_block_bytes(uint64_t elem, bool sym = false) {
-    return 64 * (search_rows(sym) * elem + 16);
+    return 64 * (search_rows(sym) * elem + 20);
 }
 __host__ __device__ inline uint64_t search_level_bytes(uint64_t nodes, uint64_t elem, bool sym = false) {
     return (nodes + 63) / 64 * search_block_bytes(elem, sym);
@@ -342,6 +348,8 @@ hipError_t launch_ref_reset(int model, bool f64, const RefArgs& a, hipStream_t s
 hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t stream);
 // child_major: one wave per (parent block, child event) instead of one lane per parent
 hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream);
+// the acceptance band of a search's threshold (Ref15SearchArgs::band_*), for its dtype
+void set_search_band(Ref15SearchArgs& a, bool f64);
 // levels 1 .. a.k of a search in one launch (one lane per subset of at most a.k free events)
 hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStream_t stream);
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream);

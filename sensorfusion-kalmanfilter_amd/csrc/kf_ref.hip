@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 
@@ -264,9 +265,17 @@ struct Chains {
     // the blocks' determinants, division-free per block (det3_scaled / det2) and one reciprocal
     // for the pva pivots; fp32 renormalises after every block (three pva blocks reach 1e48).
     __device__ __forceinline__ T logdet() const {
+        int ex;
+        const T prod = det_mant(ex);
+        const T ld = log_mant(prod, ex);
+        return prod == prod ? ld : quiet_nan<T>();
+    }
+    // the same determinant before its log: mantissa in [0.5, 1) (NaN unless positive definite)
+    // times 2^ex
+    __device__ __forceinline__ T det_mant(int& ex) const {
         constexpr bool kNarrow = sizeof(T) == 4;
         T num = T(1), den = T(1);
-        int ex = 0;
+        ex = 0;
         bool ok = true;
 #pragma unroll
         for (int c = 0; c < M::NP; ++c) {
@@ -280,8 +289,7 @@ struct Chains {
         }
         T prod = num * rcp_nr<kRefNewton>(den);
         renorm(prod, ex);
-        const T ld = log_mant(prod, ex);
-        return ok ? ld : quiet_nan<T>();
+        return ok ? prod : quiet_nan<T>();
     }
 
     __device__ __forceinline__ void reset_cov() {
@@ -2122,10 +2130,67 @@ template <typename T>
 __device__ __forceinline__ T* level_row(char* blk, uint32_t lane, int r) {
     return reinterpret_cast<T*>(blk + r * 64 * int(sizeof(T))) + lane;
 }
+// the running max's binary exponent (int32 per node, after the T rows)
+template <typename T, bool SYM = false>
+__device__ __forceinline__ int32_t* level_exp(char* blk, uint32_t lane) {
+    return reinterpret_cast<int32_t*>(blk + search_rows(SYM) * 64 * int(sizeof(T))) + lane;
+}
 template <typename T, bool SYM = false>
 __device__ __forceinline__ double* level_tail(char* blk, uint32_t lane, int q) {
-    return reinterpret_cast<double*>(blk + search_rows(SYM) * 64 * int(sizeof(T)) + q * 512) + lane;
+    return reinterpret_cast<double*>(blk + search_rows(SYM) * 64 * int(sizeof(T)) + 256 + q * 512) + lane;
 }
+
+// A positive determinant as (mantissa in [0.5, 1), binary exponent); a failed filter's has a NaN
+// mantissa.  The search carries each subset's running max this way and compares determinants,
+// not their logs (log is monotone): one log per scored subset where its max log-det is an
+// output (subset_max), none where only the acceptance test reads it (DetBand), instead of a log
+// per record and per final predict.
+// A NaN determinant carries the exponent that makes the comparisons below treat it as the log
+// domain's `ld > run ? ld : run` treats a NaN: kNanLoses on a failed record or final predict
+// (it never wins a max), kNanWins on a failed running max (nothing beats it: it stays NaN).
+constexpr int kNanLoses = -2147483647 - 1, kNanWins = 2147483647;
+template <typename T>
+struct DetV {
+    T m;
+    int e;
+    __device__ __forceinline__ bool valid() const { return m == m; }
+    // this > o (by exponent, then mantissa: both normalised)
+    __device__ __forceinline__ bool gt(const DetV& o) const { return e > o.e || (e == o.e && m > o.m); }
+    __device__ __forceinline__ T log() const { return valid() ? log_mant(m, e) : quiet_nan<T>(); }
+    __device__ __forceinline__ void fail() {
+        m = quiet_nan<T>();
+        e = kNanWins;
+    }
+};
+
+// `d.gt(r) ? d : r`, the exponent blended with a mask (a select of two loaded members is folded
+// into a load from a select of their addresses, which keeps the search node in scratch memory)
+template <typename T>
+__device__ __forceinline__ DetV<T> dmax(const DetV<T>& d, const DetV<T>& r) {
+    const bool g = d.gt(r);
+    const int mk = -int(g);
+    return DetV<T>{g ? d.m : r.m, (d.e & mk) | (r.e & ~mk)};
+}
+
+// The acceptance test max(log_det) < R_threshold (kf_workers.py:1353) on a determinant: below
+// lo it holds and above hi it fails for any log the kernels could compute (lo, hi = exp(thr) (1
+// -+ eps), eps far above log_mant's and exp's rounding; set_search_band computes them on the
+// host); in between the log decides, as `log < T(thr)` exactly.
+template <typename T>
+struct DetBand {
+    DetV<T> lo, hi;
+    int mode;  // 0: the band; 1: accept every valid determinant; 2: accept none
+    T thr;
+    __device__ __forceinline__ explicit DetBand(const Ref15SearchArgs& a)
+        : lo{T(a.band_lo_m), a.band_lo_e}, hi{T(a.band_hi_m), a.band_hi_e}, mode(a.band_mode), thr(T(a.threshold)) {}
+    // d: a subset's max (valid, or NaN with kNanWins, which lies above hi)
+    __device__ __forceinline__ bool accept(const DetV<T>& d) const {
+        if (mode != 0) return mode == 1 && d.valid();
+        if (lo.gt(d)) return true;
+        if (d.gt(hi)) return false;
+        return log_mant(d.m, d.e) < thr;
+    }
+};
 
 // Chains<T, M15>::logdet() accumulated one block at a time, in its order (pva chains, then aw
 // chains) with its renormalisations, so the value is the same.
@@ -2148,10 +2213,17 @@ struct LogdetAcc {
         const T ld = log_mant(prod, ex);
         return ok ? ld : quiet_nan<T>();
     }
+    // the determinant itself (Chains::det_mant's value): no log
+    __device__ __forceinline__ DetV<T> det() {
+        T prod = num * rcp_nr<kRefNewton>(den);
+        renorm(prod, ex);
+        return DetV<T>{ok ? prod : quiet_nan<T>(), ok ? ex : kNanLoses};
+    }
 };
 
 // A stored node of the search: the covariance after a subset's events, its running max
-// log-det, the time of its last applied event and its subset mask.  The search scores a subset
+// determinant (DetV: the max log-det before its log), the time of its last applied event and its
+// subset mask.  The search scores a subset
 // by its max log-det alone, which depends on the covariance alone, and the covariance does not
 // depend on the measurements (nor, so, on the state): the state is not carried (kf_eval_combos
 // carries it for the per-combination API).  The updates see a constant zero state (search_pva,
@@ -2166,7 +2238,7 @@ struct SearchNode {
     static constexpr int NP = SYM ? 1 : M15::NP, NA = SYM ? 1 : M15::NA;
     static constexpr int NR = 6 * NP + 3 * NA;  // covariance rows held (27, or 9)
     T P[NR];
-    T run;
+    DetV<T> run;
     double prev;
     uint64_t mask;
 
@@ -2174,14 +2246,15 @@ struct SearchNode {
     // initial filter in index order as the worker applies a combination's events
     // (kf_workers.py:36-71); record 0 is the logdet of the initial covariance (:32).  With
     // `eval`, the root subset itself is also scored (its max log-det with the final predict).
-    __device__ __forceinline__ T root(const Ref15SearchArgs& a, bool eval) {
+    __device__ __forceinline__ DetV<T> root(const Ref15SearchArgs& a, bool eval) {
         Ref15<T, CUSTOM> r;
         r.kc = a.kc;
 #pragma unroll
         for (int i = 0; i < 15; ++i) r.x[i] = T(a.init[i]);
 #pragma unroll
         for (int i = 0; i < 27; ++i) r.blk(i) = T(a.init[15 + i]);
-        run = r.logdet();
+        run.m = r.det_mant(run.e);
+        if (!run.valid()) run.fail();
         prev = a.prev_time;
         mask = a.root_mask;
         const T no_gate = T(0);
@@ -2194,20 +2267,24 @@ struct SearchNode {
             for (int i = 0; i < 9; ++i) pay[i] = T(e[2 + i]);
             bool ok = true;
             r.event(int(e[1]), T(dtd), pay, false, no_gate, ok);
-            const T ld = r.logdet();
-            run = ld > run ? ld : run;
-            run = ok ? run : quiet_nan<T>();
+            DetV<T> d;
+            d.m = r.det_mant(d.e);
+            d.e = d.valid() ? d.e : kNanLoses;
+            run = dmax(d, run);
+            if (!ok) run.fail();
             prev = e[0];
         }
 #pragma unroll
         for (int i = 0; i < 6 * NP; ++i) P[i] = r.blk(i);
 #pragma unroll
         for (int i = 0; i < 3 * NA; ++i) P[6 * NP + i] = r.blk(6 * M15::NP + i);
-        T fmax = run;
+        DetV<T> fmax = run;
         if (eval && prev < a.target_end - 1e-8) {  // kf_workers.py:74-82
             r.predict(T(a.target_end - prev));
-            const T ld = r.logdet();
-            fmax = ld > run ? ld : run;
+            DetV<T> d;
+            d.m = r.det_mant(d.e);
+            d.e = d.valid() ? d.e : kNanLoses;
+            fmax = dmax(d, run);
         }
         return fmax;
     }
@@ -2216,7 +2293,8 @@ struct SearchNode {
         const uint32_t lane = uint32_t(p) & 63u;
 #pragma unroll
         for (int i = 0; i < NR; ++i) P[i] = *level_row<T>(blk, lane, i);
-        run = *level_row<T>(blk, lane, NR);
+        run.m = *level_row<T>(blk, lane, NR);
+        run.e = *level_exp<T, SYM>(blk, lane);
         prev = *level_tail<T, SYM>(blk, lane, 0);
         mask = __builtin_bit_cast(uint64_t, *level_tail<T, SYM>(blk, lane, 1));
     }
@@ -2226,7 +2304,8 @@ struct SearchNode {
         const uint32_t cl = uint32_t(r) & 63u;
 #pragma unroll
         for (int i = 0; i < NR; ++i) *level_row<T>(cb, cl, i) = P[i];
-        *level_row<T>(cb, cl, NR) = run;
+        *level_row<T>(cb, cl, NR) = run.m;
+        *level_exp<T, SYM>(cb, cl) = run.e;
         *level_tail<T, SYM>(cb, cl, 0) = prev;
         *level_tail<T, SYM>(cb, cl, 1) = __builtin_bit_cast(double, mask);
     }
@@ -2237,12 +2316,20 @@ struct SearchNode {
     }
 };
 
-// a scored subset: every max log-det to subset_max, the acceptance test into (best, cnt)
+// a scored subset: every max log-det to subset_max (its one log), the acceptance test into
+// (best, cnt) — on the determinant (DetBand) when no log was taken
 template <typename T>
-__device__ __forceinline__ void search_score(const Ref15SearchArgs& a, uint64_t mask, T fmax, uint64_t& best,
-                                             uint64_t& cnt) {
-    if (a.subset_max) static_cast<T*>(a.subset_max)[mask] = fmax;
-    if (fmax < T(a.threshold)) {  // max(log_det) < R_threshold (kf_workers.py:1353); NaN never passes
+__device__ __forceinline__ void search_score(const Ref15SearchArgs& a, const DetBand<T>& band, uint64_t mask,
+                                             const DetV<T>& fmax, uint64_t& best, uint64_t& cnt) {
+    bool acc;
+    if (a.subset_max) {
+        const T ld = fmax.log();
+        static_cast<T*>(a.subset_max)[mask] = ld;
+        acc = ld < band.thr;
+    } else {
+        acc = band.accept(fmax);
+    }
+    if (acc) {  // max(log_det) < R_threshold (kf_workers.py:1353); NaN never passes
         const uint64_t key = __builtin_bitreverse64(mask);  // larger key = earlier in itertools order
         best = key > best ? key : best;
         ++cnt;
@@ -2346,19 +2433,20 @@ struct SearchScore {
 #pragma unroll
         for (int r = 0; r < reps; ++r) fin.add_aw(Pf);
     }
-    // the running max log-det after the event (NaN for a failed filter, kf_eval_combos:
-    // KF_ENOTSPD), and into fmax the subset's max log-det with the final predict
-    __device__ __forceinline__ T finish(const SearchEvent& v, T run_in, T& fmax) {
-        T run = run_in;
+    // the running max determinant after the event (NaN for a failed filter, kf_eval_combos:
+    // KF_ENOTSPD), and into fmax the subset's max with the final predict — the max log-dets'
+    // determinants, no log taken
+    __device__ __forceinline__ DetV<T> finish(const SearchEvent& v, const DetV<T>& run_in, DetV<T>& fmax) {
+        DetV<T> run = run_in;
         if (v.step) {
-            const T ld = rec.finish();
-            run = ld > run_in ? ld : run_in;
-            run = ok ? run : quiet_nan<T>();
+            const DetV<T> d = rec.det();
+            run = dmax(d, run_in);
+            if (!ok) run.fail();
         }
         fmax = run;
         if (v.final_predict) {
-            const T ld = fin.finish();
-            fmax = ld > run ? ld : run;
+            const DetV<T> d = fin.det();
+            fmax = dmax(d, run);
         }
         return run;
     }
@@ -2389,9 +2477,9 @@ struct ParLds {
 };
 
 template <typename T, bool CUSTOM, bool SYM, class PS>
-__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const SearchNode<T, CUSTOM, SYM>& par, const PS& pp,
-                                             int j, uint64_t c, uint64_t& best, uint64_t& cnt, uint64_t& best1,
-                                             uint64_t& cnt1) {
+__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const DetBand<T>& band,
+                                             const SearchNode<T, CUSTOM, SYM>& par, const PS& pp, int j, uint64_t c,
+                                             uint64_t& best, uint64_t& cnt, uint64_t& best1, uint64_t& cnt1) {
     using Node = SearchNode<T, CUSTOM, SYM>;
     constexpr int RP = SYM ? M15::NP : 1, RA = SYM ? M15::NA : 1;  // chains each computed one stands for
     const SearchEvent vs = search_event(a, j, par.prev);
@@ -2437,19 +2525,20 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Sea
         }
         if constexpr (PS::kChainFence) __builtin_amdgcn_sched_barrier(0);
     }
-    T fmax;
-    const T run = ss.finish(vs, par.run, fmax);
+    DetV<T> fmax;
+    const DetV<T> run = ss.finish(vs, par.run, fmax);
     const uint64_t cmask = par.mask | (uint64_t(1) << (j + a.shift));
     if (store) {
-        *level_row<T>(cb, cl, Node::NR) = run;
+        *level_row<T>(cb, cl, Node::NR) = run.m;
+        *level_exp<T, SYM>(cb, cl) = run.e;
         *level_tail<T, SYM>(cb, cl, 0) = vs.prev;
         *level_tail<T, SYM>(cb, cl, 1) = __builtin_bit_cast(double, cmask);
     }
-    search_score(a, cmask, fmax, best, cnt);
+    search_score(a, band, cmask, fmax, best, cnt);
     if (tail) {
-        T gmax;
+        DetV<T> gmax;
         (void)sg.finish(vg, run, gmax);
-        search_score(a, cmask | (uint64_t(1) << (j + 1 + a.shift)), gmax, best1, cnt1);
+        search_score(a, band, cmask | (uint64_t(1) << (j + 1 + a.shift)), gmax, best1, cnt1);
     }
 }
 
@@ -2484,11 +2573,12 @@ ref15_search_pm_kernel(const Ref15SearchArgs a) {
     constexpr int NR = SearchNode<T, CUSTOM, SYM>::NR;
     const int64_t p = static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x;
     if (uint64_t(p) >= a.n_par) return;
+    const DetBand<T> band(a);
     SearchNode<T, CUSTOM, SYM> par;
     if (a.k == 1) {
         uint64_t rb = 0, rc = 0;  // a fixed root is itself one of the subsets searched
-        const T f = par.root(a, a.root_mask != 0);
-        if (a.root_mask) search_score(a, a.root_mask, f, rb, rc);
+        const DetV<T> f = par.root(a, a.root_mask != 0);
+        if (a.root_mask) search_score(a, band, a.root_mask, f, rb, rc);
         search_publish(a, 0, rb, rc);
     } else {
         par.load(a.par, uint64_t(p));
@@ -2505,16 +2595,16 @@ ref15_search_pm_kernel(const Ref15SearchArgs a) {
 #pragma unroll 1
         for (int j = j0; j < a.n_events; ++j) {
             if (j <= m) continue;
-            search_child<T, CUSTOM, SYM>(a, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt,
-                                         best1, cnt1);
+            search_child<T, CUSTOM, SYM>(a, band, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best,
+                                         cnt, best1, cnt1);
         }
     } else {
         const ParRegs<T> pp{par.P};
 #pragma unroll 1
         for (int j = j0; j < a.n_events; ++j) {
             if (j <= m) continue;
-            search_child<T, CUSTOM, SYM>(a, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best, cnt,
-                                         best1, cnt1);
+            search_child<T, CUSTOM, SYM>(a, band, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best,
+                                         cnt, best1, cnt1);
         }
     }
     search_publish(a, a.k, best, cnt);
@@ -2559,15 +2649,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEA
         }
     }
     uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0;
+    const DetBand<T> band(a);
     Node nd;
     {
         uint64_t rb = 0, rc = 0;  // a fixed root is itself one of the subsets searched (lane 0 scores it)
         const bool eval = a.root_mask != 0 && g == 0;
-        const T f = nd.root(a, eval);
-        if (eval) search_score(a, a.root_mask, f, rb, rc);
+        const DetV<T> f = nd.root(a, eval);
+        if (eval) search_score(a, band, a.root_mask, f, rb, rc);
         search_publish(a, 0, rb, rc);
     }
-    T fmax = nd.run;
+    DetV<T> fmax = nd.run;
 #pragma unroll 1
     for (uint64_t m = sub; m; m &= m - 1) {
         const int j = __builtin_ctzll(m);
@@ -2601,7 +2692,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEA
     }
     const int top = sub ? 63 - __builtin_clzll(sub) : -1;
     if (live) {
-        search_score(a, nd.mask, fmax, best, cnt);
+        search_score(a, band, nd.mask, fmax, best, cnt);
         if (k == K && a.child && top <= n - 3) nd.store(a.child, r);  // level K + 1's parent, at its colex rank
         if (k == K && a.tail && top == n - 2) {  // its only child, plus event n - 1 (size K + 1)
             const SearchEvent vg = search_event(a, n - 1, nd.prev);
@@ -2623,9 +2714,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEA
                 search_aw<T, CUSTOM>(vg, ch, Pa, sg.ok, a.kc);
                 sg.add_aw(vg, Pa, ch, RA);
             }
-            T gmax;
+            DetV<T> gmax;
             (void)sg.finish(vg, nd.run, gmax);
-            search_score(a, nd.mask | (uint64_t(1) << (n - 1 + a.shift)), gmax, best1, cnt1);
+            search_score(a, band, nd.mask | (uint64_t(1) << (n - 1 + a.shift)), gmax, best1, cnt1);
         }
     }
     // per size: a wave holds lanes of at most a few consecutive sizes
@@ -2671,19 +2762,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEA
     }
     const uint64_t p = blk * 64 + threadIdx.x;
     if (p >= a.n_par) return;
+    const DetBand<T> band(a);
     SearchNode<T, CUSTOM, SYM> par;
     if (k == 1) {
         uint64_t rb = 0, rc = 0;  // a fixed root is itself one of the subsets searched (item 0 scores it)
         const bool eval = a.root_mask != 0 && item == 0;
-        const T f = par.root(a, eval);
-        if (eval) search_score(a, a.root_mask, f, rb, rc);
+        const DetV<T> f = par.root(a, eval);
+        if (eval) search_score(a, band, a.root_mask, f, rb, rc);
         search_publish(a, 0, rb, rc);
     } else {
         par.load(a.par, p);
     }
     uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0;
     if (par.max_event(a.shift) < j)
-        search_child<T, CUSTOM, SYM>(a, par, ParRegs<T>{par.P}, j, p + binom(j, k), best, cnt, best1, cnt1);
+        search_child<T, CUSTOM, SYM>(a, band, par, ParRegs<T>{par.P}, j, p + binom(j, k), best, cnt, best1, cnt1);
     search_publish(a, a.k, best, cnt);
     if (a.tail) search_publish(a, a.k + 1, best1, cnt1);
 }
@@ -3788,6 +3880,26 @@ hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t st
     return hipGetLastError();
 }
 
+
+void set_search_band(Ref15SearchArgs& a, bool f64) {
+    // the threshold as the kernels compare it (T(threshold)); (mantissa, exponent) pairs whose
+    // mantissa T's rounding keeps far inside eps (a mantissa rounded up to 1 only makes the
+    // kernels' (e, m) comparisons conservative)
+    const double t = f64 ? a.threshold : double(float(a.threshold));
+    a.band_mode = t == t ? (t > 1e4 ? 1 : (t < -1e4 ? 2 : 0)) : 2;
+    a.band_lo_m = a.band_hi_m = 1.0;
+    a.band_lo_e = a.band_hi_e = 0;
+    if (a.band_mode != 0) return;
+    const double eps = f64 ? 1e-10 : 1e-4;
+    const double q = t * 1.4426950408889634074;  // thr / ln 2: e^thr = 2^fl * 2^(q - fl)
+    const double fl = std::floor(q);
+    const double mm = std::exp2(q - fl);
+    int e1, e2;
+    a.band_lo_m = std::frexp(mm * (1.0 - eps), &e1);
+    a.band_hi_m = std::frexp(mm * (1.0 + eps), &e2);
+    a.band_lo_e = int(fl) + e1;
+    a.band_hi_e = int(fl) + e2;
+}
 
 hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStream_t stream) {
     if (a.n_events > kMaxEvents || a.n_events < 3 || a.k < 1 || a.k > a.n_events - 2 || a.n_child == 0 ||

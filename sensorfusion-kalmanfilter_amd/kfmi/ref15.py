@@ -639,9 +639,10 @@ def brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype='f64', d
 
 def search_level_bytes(nodes, dtype, sym=False):
     """Device bytes of one kf_search_combos level buffer (node blocks of 64, kf_internal.h; an
-    axis-symmetric search's nodes hold 10 rows instead of 28, KF_OPT_AXIS_SYM)."""
+    axis-symmetric search's nodes hold 10 rows instead of 28, KF_OPT_AXIS_SYM; then the running
+    max's exponent, the time and the mask: 20 B)."""
     w = 8 if dtype == 'f64' else 4
-    return (nodes + 63) // 64 * 64 * ((10 if sym else 28) * w + 16)
+    return (nodes + 63) // 64 * 64 * ((10 if sym else 28) * w + 20)
 
 
 SEARCH_HEAD_STEPS = 400000  # kf_capi.cpp kSearchHeadSteps
