@@ -2174,8 +2174,8 @@ __device__ __forceinline__ DetV<T> dmax(const DetV<T>& d, const DetV<T>& r) {
 
 // The acceptance test max(log_det) < R_threshold (kf_workers.py:1353) on a determinant: below
 // lo it holds and above hi it fails for any log the kernels could compute (lo, hi = exp(thr) (1
-// -+ eps), eps far above log_mant's and exp's rounding; set_search_band computes them on the
-// host); in between the log decides, as `log < T(thr)` exactly.
+// -+ eps), eps far above log_mant's and exp's rounding near thr; set_search_band computes them
+// on the host); in between the log decides, as `log < T(thr)` exactly.
 template <typename T>
 struct DetBand {
     DetV<T> lo, hi;
@@ -3885,12 +3885,16 @@ void set_search_band(Ref15SearchArgs& a, bool f64) {
     // the threshold as the kernels compare it (T(threshold)); (mantissa, exponent) pairs whose
     // mantissa T's rounding keeps far inside eps (a mantissa rounded up to 1 only makes the
     // kernels' (e, m) comparisons conservative)
+    // |log det| of a 15 x 15 SPD matrix stays below 15 * 745 (every pivot is a finite double, a
+    // float's log below 15 * 104): beyond 1e5 the test accepts every valid determinant, or none
     const double t = f64 ? a.threshold : double(float(a.threshold));
-    a.band_mode = t == t ? (t > 1e4 ? 1 : (t < -1e4 ? 2 : 0)) : 2;
+    a.band_mode = t == t ? (t > 1e5 ? 1 : (t < -1e5 ? 2 : 0)) : 2;
     a.band_lo_m = a.band_hi_m = 1.0;
     a.band_lo_e = a.band_hi_e = 0;
     if (a.band_mode != 0) return;
-    const double eps = f64 ? 1e-10 : 1e-4;
+    // the band's half-width in log units: above the log's absolute rounding near t (a few ulps of
+    // t in T) and this exp2's (q - fl carries q's rounding, 1e-16 |t|)
+    const double eps = f64 ? std::fmax(1e-10, std::fabs(t) * 1e-14) : std::fmax(1e-4, std::fabs(t) * 1e-6);
     const double q = t * 1.4426950408889634074;  // thr / ln 2: e^thr = 2^fl * 2^(q - fl)
     const double fl = std::floor(q);
     const double mm = std::exp2(q - fl);

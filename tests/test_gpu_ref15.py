@@ -152,6 +152,38 @@ def test_search_subset_max_equals_eval_combos(golden_dir, dtype, kernel, head):
     assert worst <= (1e-12 if dtype == 'f64' else 1e-6), (worst, exact, total)
 
 
+@pytest.mark.parametrize('dtype', ['f64', 'f32'])
+def test_search_acceptance_on_determinants_is_the_logs(golden_dir, dtype):
+    """Without subset_max the search tests max(log_det) < R_threshold on determinants (a band
+    around exp(threshold), the log taken only inside it).  At thresholds equal to subsets' own
+    max log-dets, one ulp either side of them, and far outside every max, the per-size
+    acceptance counts and the winner equal the ones the logs give (counted on the host from the
+    same search's subset_max)."""
+    n = 12
+    cand, ev, init, t0, target = _search_case(golden_dir, n)
+    kf = kfmi.BatchedKF('ref15', 1, dtype)
+    _, _, _, sm = kf.search_combos(ev, init, t0, target, -1e30, exhaustive=True, subset_max=True)
+    sm = sm.cpu().numpy()
+    size = np.array([bin(m).count('1') for m in range(1 << n)])
+    vals = np.sort(sm[np.isfinite(sm)])
+    npt = np.float64 if dtype == 'f64' else np.float32
+    picks = [vals[0], vals[len(vals) // 3], vals[len(vals) // 2], vals[-1]]
+    thresholds = [float(np.nextafter(npt(v), npt(d))) for v in picks for d in (-np.inf, np.inf)]
+    thresholds += [float(v) for v in picks] + [float(vals[0]) - 50.0, float(vals[-1]) + 50.0, 2e5, -2e5]
+    for thr in thresholds:
+        k, win, acc, _ = kf.search_combos(ev, init, t0, target, thr, exhaustive=True)
+        ok = sm < npt(thr)           # NaN never passes
+        want = [int(np.sum(ok & (size == s))) for s in range(n + 1)]
+        assert [int(a) for a in acc] == want, thr
+        first = next((s for s in range(1, n + 1) if want[s]), 0)
+        assert k == first, thr
+        if first:
+            masks = [m for m in range(1 << n) if size[m] == first and ok[m]]
+            lex = min(tuple(i for i in range(n) if (m >> i) & 1) for m in masks)
+            assert win == lex, thr
+    kf.close()
+
+
 def test_combo_inputs_reused_and_refreshed(golden_dir):
     """The handle keeps the last uploaded candidates and root on the device: a call with other
     inputs uploads them, a call with the same ones reuses them, also from another stream (which
