@@ -273,3 +273,60 @@ def test_gloo_world2_brute_force_search(golden_dir, thr):
         spans = sorted((lo, hi) for r in (0, 1) for (kk, lo, hi) in res[r][1] if kk == k)
         assert spans[0][0] == 0 and spans[-1][1] == comb(n, k)      # (a rank with no ranks skips)
         assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+def _winner_worker(rank, world, port, n, w, out_q):
+    """kfmi.dist.search_winner / sum_counts on synthetic class results: each class reports the
+    smallest size at which it accepts and its first accepted subset (itertools order), from one
+    random acceptance table shared by every rank; the reduction must give the global winner."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from itertools import combinations
+        rng = np.random.default_rng(77)
+        accept = {}
+        for k in range(1, n + 1):
+            for c in combinations(range(n), k):
+                accept[c] = rng.random() < 0.02 * k
+        counts = np.zeros(n + 1, np.int64)
+
+        def search_class(n_fixed, fixed_mask):
+            best = None
+            for k in range(1, n + 1):
+                for c in combinations(range(n), k):
+                    if sum(1 << i for i in c if i < n_fixed) != fixed_mask or not accept[c]:
+                        continue
+                    counts[k] += 1
+                    if best is None:
+                        best = (k, c)
+            return best if best else (0, None)
+        won = kdist.search_winner(search_class, n, w)
+        total = kdist.sum_counts(counts)
+        if rank == 0:
+            k1 = next(k for k in range(1, n + 1) if any(accept[c] for c in combinations(range(n), k)))
+            c1 = next(c for c in combinations(range(n), k1) if accept[c])
+            want = [0] + [sum(accept[c] for c in combinations(range(n), k)) for k in range(1, n + 1)]
+            out_q.put((won, (k1, c1), list(total), want))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_gloo_search_winner_and_counts(world):
+    """The cross-rank half of the sharded search (the bench's bf row at N > 1 runs it too):
+    classes dealt round-robin over the ranks, MIN of the first accepted size, MAX of the
+    bit-reversed mask, counts summed — the same winner and counts as one rank over every class."""
+    n = 9
+    w = kdist.search_classes(n, world)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_winner_worker, args=(r, world, port, n, w, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    assert [p.exitcode for p in procs] == [0] * world
+    won, want_won, total, want = q.get(timeout=10)
+    assert won == want_won
+    assert total == want
