@@ -62,6 +62,10 @@ CONFIGS = {
     # 4-state config restricts: x0 = 0, the first fix at dt = 0, no dt < 0 guard, 2-D fixes
     '1ref8': dict(model='ref8', dtype='f64', B=1, n_gps=30758, n_gps_nan_lead=2735, n_gps_nan=8887, n_imu=616322,
                   parallel=True),
+    # hw5_2's run_dead_reckoning_for_IMU (hw5_2.py:382-436) over the same log: the 8-state filter
+    # over the IMU events alone (the fixes compacted away on the device), x0 = 0, first dt 0
+    '1dr': dict(model='ref8', dtype='f64', B=1, n_gps=30758, n_gps_nan_lead=2735, n_gps_nan=8887, n_imu=616322,
+                parallel=True, dead_reckoning=True),
     '2': dict(model='cv2', dtype='f32', B=65536, T=1024, dt=0.1, k=1),
     '3': dict(model='cv3', dtype='f64', B=1048576, T=256, dt=0.1, k=1),
     '4': dict(model='cv3', dtype='f32', B=1048576, T=256, dt=0.1, k=1),
@@ -627,6 +631,8 @@ def log_workload(cfg, args, rank, world, dev):
     torch.cuda.synchronize(dev)
     t3 = time.perf_counter()
     N = len(stream)
+    if cfg.get('dead_reckoning'):
+        return dead_reckoning_workload(cfg, args, dev, stream, (t1 - t0, t2 - t1, t3 - t2))
     first = int(torch.nonzero(stream.etype == _lib.KF_EVENT_GPS)[0, 0])
     T = N - first
     t_ev = stream.t[first:].contiguous()
@@ -745,6 +751,92 @@ def log_workload(cfg, args, rank, world, dev):
                 roofline_note='one filter: one wave whose per-event dependency chain bounds the rate (8 lanes, '
                               'one per axis chain); HBM is idle, so the fraction is not the figure of merit',
                 desc=desc + "synthetic log with the reference log's shape", extra=extra)
+
+
+def dead_reckoning_workload(cfg, args, dev, stream, ingest_s):
+    """hw5_2.run_dead_reckoning_for_IMU (hw5_2.py:382-436) over a whole ingested drive log: a step
+    is the device compaction of the IMU events (kf_events_select: the driver skips every fix,
+    :403-404), their dt (kf_events_dt, KF_DT_RAW from no previous time: the first IMU event at dt
+    0, :401, 407) and one kf_run_stream of the 8-state filter from x0 = 0 over them (:410-433),
+    the trajectory (x, y, theta) recorded per IMU event."""
+    import ctypes
+    import kfmi
+    from kfmi import _lib
+    from kfmi.engine import _ptr
+    N = len(stream)
+    T = int(stream.n_imu)
+    kf = kfmi.BatchedKF('ref8', 1, 'f64', device=dev.index, options=cfg.get('opts'))
+    x0 = torch.zeros(8, 1, dtype=torch.float64, device=dev)
+    t_sel = torch.empty(N, dtype=torch.float64, device=dev)
+    p_sel = torch.empty(N, 9, dtype=torch.float64, device=dev)
+    dt = torch.empty(T, dtype=torch.float64, device=dev)
+    et = torch.empty(T, dtype=torch.uint8, device=dev)
+    traj = kf.empty(T, 3, 1)
+    et_in, t_in, p_in = stream.etype.contiguous(), stream.t.contiguous(), stream.payload.contiguous()
+    stream_check = {}
+
+    def step():
+        L = _lib.lib()
+        kf.reset(x0)
+        k = ctypes.c_int64(0)
+        _lib.check(L.kf_events_select(N, _ptr(et_in), _ptr(t_in), _ptr(p_in), _lib.KF_EVENT_IMU, _ptr(t_sel),
+                                      _ptr(p_sel), None, ctypes.byref(k), kf._stream()))
+        if k.value != T:
+            raise SystemExit(f'kf_events_select kept {k.value} IMU events, the stream holds {T}')
+        _lib.check(L.kf_events_dt(T, _ptr(t_sel), None, float('nan'), _lib.KF_DT_RAW, _ptr(dt), _ptr(et),
+                                  kf._stream()))
+        _lib.check(L.kf_run_stream(kf.handle, T, _ptr(et), _ptr(dt), _ptr(p_sel), _ptr(traj), None, None, None, 0, -1,
+                                   kf._stream()))
+        if not stream_check:  # first (warm-up) step: record the device checks (synchronises)
+            stream_check.update(kf.stream_check())
+
+    def cpu():
+        """The dead-reckoning walk restated in C (oracle/cpu_kf.c cpu_ref8_dead_reckoning: the
+        dense 8x8 step over the IMU events of the merged stream) over the whole log, 1 thread (one
+        filter); plus the NumPy restatement (oracle/ref_kf.run_dead_reckoning_8state) over the
+        first events, 1 core, ~3 s."""
+        from oracle import cpu_kf, ref_kf
+        from kfmi.kf_workers import EventList
+        h = stream.host()
+        ts = time.perf_counter()
+        cpu_kf.ref8_dead_reckoning(h['etype'], h['t'], h['payload'])
+        el = time.perf_counter() - ts
+        ev = EventList(stream)
+        n = 2000
+        while True:
+            lst = ev[:n]
+            t1 = time.perf_counter()
+            st, _ = ref_kf.run_dead_reckoning_8state(lst)
+            el_np = time.perf_counter() - t1
+            if el_np > 3.0 or n >= N:
+                break
+            n = min(N, n * 4)
+        return {'value': T / el, 'unit': 'KF events/s', 'cores': 1, 'kind': 'port',
+                'sample': f'hw5_2.run_dead_reckoning_for_IMU over the {T} IMU events of this log through '
+                          f'oracle/cpu_kf.c (the reference step, dense 8x8, C -O3), 1 thread (one filter), '
+                          f'{host_cpu()}', 'seconds': round(el, 2),
+                'numpy_reference_loop': {'value': len(st) / el_np, 'cores': 1,
+                                         'sample': f'{len(st)} IMU events, oracle/ref_kf.run_dead_reckoning_8state, '
+                                                   f'NumPy {np.__version__}'}}
+
+    # select (etype in, t + payload of the kept events out, their positions), dt pass (t in; dt,
+    # etype out), filter (etype, dt, payload in; trajectory out): bytes per IMU event
+    per_event = (N * 1 + T * (8 + 72 + 4)) / T + (8 + 8 + 1) + (1 + 8 + 72 + 8 * 3)
+    csv_s, ingest_first_s, ingest_s2 = ingest_s
+    return dict(step=step, units=T, bytes=per_event * T, bytes_per_unit=per_event,
+                kernel='kf_events_select + kf_events_dt + kf_run_stream (ref_chain_kernel<f64,M8,stream> map pass and '
+                       'stream_* kernels)',
+                traffic=None, cpu=cpu, gather=None, kf=kf,
+                roofline_note='latency / issue-bound like config 1 (the map pass runs its chunk length of events in '
+                              'sequence); the compaction\'s count is read back by the host once per step',
+                desc=f'hw5_2.run_dead_reckoning_for_IMU (hw5_2.py:382-436): ONE 8-state filter over the {T} IMU events '
+                     f'of a whole drive log ({N} merged events, {stream.n_fixes} fixes skipped), f64; IMU events '
+                     f'compacted on the device, time-parallel (kf_run_stream); synthetic log with the reference '
+                     f"log's shape",
+                extra={'events': N, 'events_filtered': T, 'csv_parse_ms': csv_s * 1e3,
+                       'kf_ingest_ms': ingest_s2 * 1e3, 'kf_ingest_first_call_ms': ingest_first_s * 1e3,
+                       'filters': 1, 'model': 'ref8', 'driver': 'run_dead_reckoning_for_IMU',
+                       'stream_check': stream_check})
 
 
 def sched_workload(cfg, args, rank, world, dev):
@@ -1134,7 +1226,7 @@ def main():
     for o in args.opt:
         name, _, val = o.partition('=')
         cfg['opts'][name] = int(val) if val.lstrip('-').isdigit() else val
-    if args.config in ('1', '1seq', '1ref8'):
+    if args.config in ('1', '1seq', '1ref8', '1dr'):
         w = log_workload(cfg, args, rank, world, dev)
     elif args.config in ('ref15', 'ref15f32'):
         w = ref15_workload(cfg, args, rank, world, dev)

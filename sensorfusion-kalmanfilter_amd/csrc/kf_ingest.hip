@@ -20,6 +20,8 @@
 #include <stdint.h>
 
 #include <hipcub/hipcub.hpp>
+#include <mutex>
+#include <vector>
 
 #include "../../include/kf.h"
 #include "kf_internal.h"
@@ -310,6 +312,20 @@ struct DevBuf {
 int hip_err(hipError_t e, const char* what) {
     return set_error(KF_EHIP, "%s: %s (%d)", what, hipGetErrorString(e), static_cast<int>(e));
 }
+
+// kf_events_select's scratch (the kept positions, the count, hipCUB's temporaries): one buffer
+// per device, grown on demand and kept for the process, so a call allocates nothing after the
+// first of its size (hipMalloc / hipFree would synchronise the device on every call).  The call
+// is synchronous and holds the lock throughout, so one buffer serves every stream.
+struct SelectScratch {
+    std::mutex mu;
+    std::vector<void*> buf;
+    std::vector<size_t> bytes;
+};
+SelectScratch& select_scratch() {
+    static SelectScratch s;
+    return s;
+}
 }  // namespace
 
 #define KF_TRY(expr, what)                          \
@@ -513,12 +529,26 @@ int kf_events_select(int64_t n, const uint8_t* etype, const double* t, const dou
                                     pred, st),
            "kf_events_select sizing");
     const size_t ib = (4 * size_t(n) + 255) & ~size_t(255);
-    DevBuf ws;
-    KF_TRY(hipMalloc(&ws.p, ib + 256 + tmp), "kf_events_select workspace");
-    int32_t* idx = static_cast<int32_t*>(ws.p);
-    int32_t* count = reinterpret_cast<int32_t*>(static_cast<char*>(ws.p) + ib);
-    KF_TRY(hipcub::DeviceSelect::If(static_cast<char*>(ws.p) + ib + 256, tmp, rows, idx, count, static_cast<int>(n),
-                                    pred, st),
+    const size_t need = ib + 256 + tmp;
+    int dev = 0;
+    KF_TRY(hipGetDevice(&dev), "kf_events_select device");
+    SelectScratch& sc = select_scratch();
+    std::lock_guard<std::mutex> lock(sc.mu);
+    if (sc.buf.size() <= size_t(dev)) {
+        sc.buf.resize(dev + 1, nullptr);
+        sc.bytes.resize(dev + 1, 0);
+    }
+    if (sc.bytes[dev] < need) {
+        if (sc.buf[dev]) (void)hipFree(sc.buf[dev]);
+        sc.buf[dev] = nullptr;
+        sc.bytes[dev] = 0;
+        KF_TRY(hipMalloc(&sc.buf[dev], need), "kf_events_select workspace");
+        sc.bytes[dev] = need;
+    }
+    char* const ws = static_cast<char*>(sc.buf[dev]);
+    int32_t* idx = reinterpret_cast<int32_t*>(ws);
+    int32_t* count = reinterpret_cast<int32_t*>(ws + ib);
+    KF_TRY(hipcub::DeviceSelect::If(ws + ib + 256, tmp, rows, idx, count, static_cast<int>(n), pred, st),
            "kf_events_select");
     int32_t k = 0;
     KF_TRY(hipMemcpyAsync(&k, count, 4, hipMemcpyDeviceToHost, st), "kf_events_select readback");
@@ -526,7 +556,7 @@ int kf_events_select(int64_t n, const uint8_t* etype, const double* t, const dou
     if (k && (t_out || payload_out || src_out)) {
         select_gather_kernel<<<grid(k), kIngBlock, 0, st>>>(k, idx, t, payload, t_out, payload_out, src_out);
         KF_TRY(hipGetLastError(), "kf_events_select gather");
-        KF_TRY(hipStreamSynchronize(st), "kf_events_select sync");  // before the workspace goes
+        KF_TRY(hipStreamSynchronize(st), "kf_events_select sync");  // before the scratch is reused
     }
     *n_kept = k;
     return KF_OK;

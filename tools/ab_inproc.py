@@ -60,7 +60,7 @@ def main():
         w = bench.ref15_workload(cfg, ns, 0, 1, dev)
     elif args.config in ('bf', 'bf_subsets'):
         w = bench.bf_workload(cfg, ns, 0, 1, dev)
-    elif args.config in ('1', '1ref8'):
+    elif args.config in ('1', '1ref8', '1dr'):
         w = bench.log_workload(cfg, ns, 0, 1, dev)
     elif args.config == 'sched':
         w = bench.sched_workload(cfg, ns, 0, 1, dev)
