@@ -2213,11 +2213,12 @@ struct LogdetAcc {
         const T ld = log_mant(prod, ex);
         return ok ? ld : quiet_nan<T>();
     }
-    // the determinant itself (Chains::det_mant's value): no log
+    // the determinant itself (Chains::det_mant's value): no log.  A product that underflowed to 0
+    // (log -inf) takes the lowest exponent, so it orders below every positive determinant.
     __device__ __forceinline__ DetV<T> det() {
         T prod = num * rcp_nr<kRefNewton>(den);
         renorm(prod, ex);
-        return DetV<T>{ok ? prod : quiet_nan<T>(), ok ? ex : kNanLoses};
+        return DetV<T>{ok ? prod : quiet_nan<T>(), ok && prod != T(0) ? ex : kNanLoses};
     }
 };
 
@@ -2255,6 +2256,7 @@ struct SearchNode {
         for (int i = 0; i < 27; ++i) r.blk(i) = T(a.init[15 + i]);
         run.m = r.det_mant(run.e);
         if (!run.valid()) run.fail();
+        if (run.m == T(0)) run.e = kNanLoses;
         prev = a.prev_time;
         mask = a.root_mask;
         const T no_gate = T(0);
@@ -2269,7 +2271,7 @@ struct SearchNode {
             r.event(int(e[1]), T(dtd), pay, false, no_gate, ok);
             DetV<T> d;
             d.m = r.det_mant(d.e);
-            d.e = d.valid() ? d.e : kNanLoses;
+            d.e = d.valid() && d.m != T(0) ? d.e : kNanLoses;
             run = dmax(d, run);
             if (!ok) run.fail();
             prev = e[0];
@@ -2283,7 +2285,7 @@ struct SearchNode {
             r.predict(T(a.target_end - prev));
             DetV<T> d;
             d.m = r.det_mant(d.e);
-            d.e = d.valid() ? d.e : kNanLoses;
+            d.e = d.valid() && d.m != T(0) ? d.e : kNanLoses;
             fmax = dmax(d, run);
         }
         return fmax;
