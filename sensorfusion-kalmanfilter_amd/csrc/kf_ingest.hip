@@ -276,17 +276,21 @@ struct IsType {
     __device__ __forceinline__ bool operator()(int32_t i) const { return etype[i] == type; }
 };
 
+// Thread o writes output double o of the [k][9] payload (row o / 9, column o % 9), so the stores
+// are contiguous and the loads follow the kept rows (runs of consecutive rows in a merged log);
+// threads o < k also write the time and position of kept event o.
 __global__ __launch_bounds__(kIngBlock) void select_gather_kernel(int64_t k, const int32_t* idx, const double* t,
                                                                    const double* payload, double* t_out,
                                                                    double* payload_out, int32_t* src_out) {
-    const int64_t j = int64_t(blockIdx.x) * kIngBlock + threadIdx.x;
-    if (j >= k) return;
-    const int64_t i = idx[j];
-    if (t_out) t_out[j] = t[i];
-    if (src_out) src_out[j] = static_cast<int32_t>(i);
-    if (payload_out) {
-#pragma unroll
-        for (int c = 0; c < 9; ++c) payload_out[j * 9 + c] = payload[i * 9 + c];
+    const int64_t o = int64_t(blockIdx.x) * kIngBlock + threadIdx.x;
+    if (o < k) {
+        const int64_t i = idx[o];
+        if (t_out) t_out[o] = t[i];
+        if (src_out) src_out[o] = static_cast<int32_t>(i);
+    }
+    if (payload_out && o < 9 * k) {
+        const int64_t j = o / 9;
+        payload_out[o] = payload[int64_t(idx[j]) * 9 + (o - 9 * j)];
     }
 }
 
@@ -554,7 +558,7 @@ int kf_events_select(int64_t n, const uint8_t* etype, const double* t, const dou
     KF_TRY(hipMemcpyAsync(&k, count, 4, hipMemcpyDeviceToHost, st), "kf_events_select readback");
     KF_TRY(hipStreamSynchronize(st), "kf_events_select sync");
     if (k && (t_out || payload_out || src_out)) {
-        select_gather_kernel<<<grid(k), kIngBlock, 0, st>>>(k, idx, t, payload, t_out, payload_out, src_out);
+        select_gather_kernel<<<grid(payload_out ? 9 * k : k), kIngBlock, 0, st>>>(k, idx, t, payload, t_out, payload_out, src_out);
         KF_TRY(hipGetLastError(), "kf_events_select gather");
         KF_TRY(hipStreamSynchronize(st), "kf_events_select sync");  // before the scratch is reused
     }
