@@ -36,7 +36,8 @@
  * that needs it and grown (hipMalloc; hipFree synchronises the device) only by a call that
  * needs more than every earlier one; every other launch allocates nothing.  Run such a call
  * once eagerly before capturing it: inside a capture nothing is allocated (kf_run_scheduled
- * then takes its fused kernel, the other two return KF_EINVAL).  A workspace a capture used
+ * then takes its fused kernel, kf_run_stream returns KF_EINVAL; kf_search_combos synchronises
+ * and is never captured).  A workspace a capture used
  * is never freed before kf_free, so a graph stays valid after a later, larger eager call: each
  * such growth keeps the smaller buffer (retired) until kf_free or kf_release_retired, so a
  * handle that alternates captures with ever-larger eager calls holds all of them.
@@ -384,9 +385,11 @@ int kf_eval_combos(kf_batch* handle, int n_events, const double* events, const d
  * too (KF_OPT_SEARCH_HEAD; the level-by-level search leaves them untouched).  Level k stores the C(n - 2, k)
  * subsets whose largest free candidate is <= n - 3 (a subset holding n - 1 has no extensions,
  * one holding n - 2 only the one adding n - 1, which is scored from registers); C(n - 2, k)
- * must stay below 2^28, and the handle's level buffers take 2 * C(n - 2, k) * (28 w + 16)
- * bytes at the widest stored level (w = 8 for f64, 4 for f32; n = free candidates; 10 w + 16
- * for an axis-symmetric search, KF_OPT_AXIS_SYM).  The call synchronises `stream`. */
+ * must stay below 2^28, and the handle's level buffers take 2 * C(n - 2, k) * (28 w + 20)
+ * bytes at the widest stored level (w = 8 for f64, 4 for f32; n = free candidates; 10 w + 20
+ * for an axis-symmetric search, KF_OPT_AXIS_SYM).  The call synchronises `stream` (its results
+ * return to the host through a mapped host buffer of the handle), so it cannot be captured into
+ * a hipGraph: inside a capture it returns KF_EINVAL. */
 int kf_search_combos(kf_batch* handle, int n_events, const double* events, const double* init,
                      double prev_time, double target_end, double threshold, int k_max, int exhaustive,
                      int n_fixed, uint64_t fixed_mask, uint64_t* winner, int* k_found,

@@ -68,6 +68,13 @@ struct kf_batch {
     bool search_ws_graph, stream_ws_graph, sched_ws_graph;
     std::vector<std::pair<void*, size_t>> retired;
     int64_t search_info[4];  // the last kf_search_combos: sym, head sizes, level launches, level bytes
+    // kf_search_combos' results: the finish kernel copies the device counters (best[], n_acc[])
+    // into this mapped, coherent host buffer and zeroes them, so the next search on the same
+    // stream starts without a clear and no result copy is staged through pageable memory
+    uint64_t* search_host;
+    uint64_t* search_host_dev;
+    bool search_ctr_zero;            // the counters are zero for a search queued on search_ctr_stream
+    hipStream_t search_ctr_stream;
 };
 
 namespace {
@@ -592,6 +599,7 @@ int kf_free(kf_batch* h) {
     if (h->ws) (void)hipFree(h->ws);
     if (h->ws_evt) (void)hipEventDestroy(h->ws_evt);
     if (h->search_ws) (void)hipFree(h->search_ws);
+    if (h->search_host) (void)hipHostFree(h->search_host);
     if (h->flag) (void)hipFree(h->flag);
     if (h->stream_ws) (void)hipFree(h->stream_ws);
     if (h->pend_u) (void)hipFree(h->pend_u);
@@ -1207,17 +1215,39 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
     int64_t launches = 0;
     const size_t need = head + 2 * level;
     hipStream_t st = static_cast<hipStream_t>(stream);
+    void* const ws_before = h->search_ws;
     if (!grow_ws(h, &h->search_ws, &h->search_ws_bytes, &h->search_ws_graph, need, st))
         return capturing(st) ? fail(KF_EINVAL, "kf_search_combos: the level buffers (%zu bytes) must be sized by an "
                                                "eager call before a graph capture", need)
                              : fail(KF_ENOMEM, "kf_search_combos: hipMalloc of %zu bytes of level buffers failed", need);
-    if (capturing(st)) h->search_ws_graph = true;
+    if (capturing(st))
+        return fail(KF_EINVAL, "kf_search_combos: not capturable (its results return to the host in the call)");
+    if (!h->search_host) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, sizeof(uint64_t) * 2 * (kMaxComboEvents + 1), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess) {
+            (void)hipGetLastError();
+            return fail(KF_ENOMEM, "kf_search_combos: hipHostMalloc of the result buffer failed");
+        }
+        void* pd = nullptr;
+        if (hipHostGetDevicePointer(&pd, p, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipHostFree(p);
+            return fail(KF_EHIP, "kf_search_combos: no device address for the result buffer");
+        }
+        h->search_host = static_cast<uint64_t*>(p);
+        h->search_host_dev = static_cast<uint64_t*>(pd);
+    }
     if (int rc = upload_combo_inputs(h, n_events, events, init, st, "kf_search_combos: upload")) return rc;
     char* ws = static_cast<char*>(h->ws);
     char* sw = static_cast<char*>(h->search_ws);
     uint64_t* d_best = reinterpret_cast<uint64_t*>(sw);
     uint64_t* d_acc = d_best + (kMaxComboEvents + 1);
-    hipError_t e = hipMemsetAsync(sw, 0, head, st);
+    // the counters: zeroed by the previous search's finish kernel when it ran on this stream in
+    // this workspace, otherwise cleared here; until this search's finish they are not known zero
+    const bool ctr_zero = h->search_ctr_zero && h->search_ctr_stream == st && h->search_ws == ws_before;
+    h->search_ctr_zero = false;
+    hipError_t e = ctr_zero ? hipSuccess : hipMemsetAsync(sw, 0, head, st);
     if (e != hipSuccess) return hip_fail(e, "kf_search_combos: clear");
     char* lv[2] = {sw + head, sw + head + level};
     uint64_t best[kMaxComboEvents + 1] = {}, acc[kMaxComboEvents + 1] = {};
@@ -1315,13 +1345,15 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
             if (best[lo] || best[last]) break;
         }
     }
-    // best[] and n_acc[] are adjacent on the device: one copy
-    uint64_t res[2 * (kMaxComboEvents + 1)];
-    e = hipMemcpyAsync(res, d_best, sizeof res, hipMemcpyDeviceToHost, st);
+    // best[] and n_acc[] are adjacent on the device: one kernel writes both to the host buffer
+    // and zeroes them for the next search
+    e = kfmi::launch_search_finish(d_best, h->search_host_dev, 2 * (kMaxComboEvents + 1), st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(e, "kf_search_combos: results");
-    std::memcpy(best, res, sizeof best);
-    std::memcpy(acc, res + (kMaxComboEvents + 1), sizeof acc);
+    h->search_ctr_zero = true;
+    h->search_ctr_stream = st;
+    std::memcpy(best, h->search_host, sizeof best);
+    std::memcpy(acc, h->search_host + (kMaxComboEvents + 1), sizeof acc);
     for (int k = k_base > 0 ? k_base : 1; k <= last && !found; ++k)
         if (best[k]) found = k;
     h->search_info[0] = sym;

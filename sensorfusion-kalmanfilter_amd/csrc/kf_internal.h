@@ -352,6 +352,9 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
 void set_search_band(Ref15SearchArgs& a, bool f64);
 // levels 1 .. a.k of a search in one launch (one lane per subset of at most a.k free events)
 hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStream_t stream);
+// the end of a search: counters[0 .. n) (n <= 256) copied to `host` (the device address of mapped
+// host memory) and zeroed
+hipError_t launch_search_finish(uint64_t* counters, uint64_t* host, int n, hipStream_t stream);
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream);
 hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream);
 // random_schedule's picks only (a.words): pick [T][B] event indices, a.sel_time, a.n_sel, a.words_used

@@ -3609,6 +3609,18 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     s.store(a.x, a.P, rb, off);
     a.status[f] = st;
 }
+
+// The end of kf_search_combos: its counters (best[], n_acc[]) go to the handle's mapped host
+// buffer (vector stores, made visible to the host before the kernel ends) and are zeroed for
+// the next search on the stream.
+__global__ __launch_bounds__(256) void search_finish_kernel(uint64_t* counters, uint64_t* host, int n) {
+    const int i = int(threadIdx.x);
+    if (i < n) {
+        host[i] = counters[i];
+        counters[i] = 0;
+    }
+    __threadfence_system();
+}
 }  // namespace
 
 // kernel<..., CUSTOM> for a launch: the reference's constants (kc == nullptr) or the handle's
@@ -3905,6 +3917,12 @@ void set_search_band(Ref15SearchArgs& a, bool f64) {
     a.band_hi_m = std::frexp(mm * (1.0 + eps), &e2);
     a.band_lo_e = int(fl) + e1;
     a.band_hi_e = int(fl) + e2;
+}
+
+hipError_t launch_search_finish(uint64_t* counters, uint64_t* host, int n, hipStream_t stream) {
+    if (n < 1 || n > 256) return hipErrorInvalidValue;
+    search_finish_kernel<<<1, 256, 0, stream>>>(counters, host, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStream_t stream) {

@@ -448,6 +448,44 @@ def test_search_classes_partition_the_search(golden_dir, w):
     kf.close()
 
 
+def test_search_counters_carry_across_calls_and_streams(golden_dir):
+    """The finish kernel hands each search's counters to the host and zeroes them for the next
+    search on its stream: repeated searches, one on another stream, a non-exhaustive one that
+    stops early and a refused call in between all report what a fresh handle reports; inside a
+    graph capture the call is refused before it queues anything."""
+    n = 11
+    _, ev, init, t0, target = _search_case(golden_dir, n)
+    fresh = kfmi.BatchedKF('ref15', 1, 'f64')
+    _, _, _, sm = fresh.search_combos(ev, init, t0, target, threshold=-1e30, exhaustive=True, subset_max=True)
+    thr = float(np.sort(sm.cpu().numpy()[1:])[600]) + 1e-9
+    want = fresh.search_combos(ev, init, t0, target, thr, exhaustive=True)
+    want_ne = fresh.search_combos(ev, init, t0, target, thr, exhaustive=False)
+    fresh.close()
+    assert want[0] > 0 and int(want[2].sum()) > 0
+
+    def same(got, ref):
+        assert got[:2] == ref[:2]
+        np.testing.assert_array_equal(got[2], ref[2])
+
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    side = torch.cuda.Stream()
+    for _ in range(3):
+        same(kf.search_combos(ev, init, t0, target, thr, exhaustive=True), want)
+    with torch.cuda.stream(side):
+        same(kf.search_combos(ev, init, t0, target, thr, exhaustive=True), want)
+    same(kf.search_combos(ev, init, t0, target, thr, exhaustive=False), want_ne)
+    with pytest.raises(kfmi.KFError):
+        kf.search_combos(ev, init, t0, target, thr, k_max=n + 1)
+    same(kf.search_combos(ev, init, t0, target, thr, exhaustive=True), want)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(kfmi.KFError, match='capturable'):
+        with torch.cuda.graph(g):
+            kf.search_combos(ev, init, t0, target, thr, exhaustive=True)
+    same(kf.search_combos(ev, init, t0, target, thr, exhaustive=True), want)
+    kf.close()
+
+
 def test_search_combos_rejects_bad_arguments():
     kf = kfmi.BatchedKF('ref15', 1, 'f64')
     ev = np.zeros((4, 11))
