@@ -56,6 +56,47 @@ def test_dead_reckoning_vs_reference_golden(golden_dir, prefix):
     assert _rel(P2, rP) <= 1e-6
 
 
+def _stream_of_list(events):
+    """An EventStream over a reference event list (fixes: easting, northing, altitude)."""
+    et = np.array([0 if e[1] == 'GPS' else 1 for e in events], np.uint8)
+    t = np.array([e[2] for e in events], np.float64)
+    pay = np.array([ref8.event_payload(e[1], e[3]) for e in events], np.float64).reshape(len(events), 9)
+    d = torch.device('cuda', 0)
+    n = len(t)
+    return ingest.EventStream(torch.from_numpy(et).to(d), torch.from_numpy(t).to(d), torch.from_numpy(pay).to(d),
+                              torch.arange(n, dtype=torch.int32, device=d), torch.zeros(n, dtype=torch.int8, device=d),
+                              torch.zeros(n, dtype=torch.uint8, device=d), 0, np.zeros(3), np.zeros(3), np.zeros(2),
+                              int((et == 0).sum()), int((et == 1).sum()), True)
+
+
+def test_dead_reckoning_edge_cases(golden_dir):
+    """Logs with no IMU event (no estimates, P0 back), a single IMU event (dt 0: one update from
+    P0), fixes before the first IMU event (they never move the previous time), through both
+    routes against the oracle's walk; and the golden log forced through the time-parallel route
+    (kf_run_stream at its shortest chunks) against the reference's outputs."""
+    g = np.load(f'{golden_dir}/ref8_full.npz')
+    events = unpack_events(g, '')
+    gps = [e for e in events if e[1] == 'GPS']
+    imu_idx = [i for i, e in enumerate(events) if e[1] == 'IMU']
+    first_imu = imu_idx[0]
+    cases = {
+        'gps_only': gps[:5],
+        'one_imu': [events[first_imu]],
+        'fixes_first': gps[:3] + [e for e in events if e[1] == 'IMU'][:7] + gps[3:5],
+    }
+    for name, ev in cases.items():
+        want, wP = ref_kf.run_dead_reckoning_8state(ev)
+        for route in (ev, _stream_of_list(ev)):
+            st, P = ref8.run_dead_reckoning(route, return_covariance=True)
+            assert len(st) == len(want), name
+            assert _rel(st, want) <= 1e-6, name
+            assert _rel(P, wP) <= 1e-6, name
+    want = g['dr_states']
+    st = ref8.run_dead_reckoning(_stream_from_golden(g, ''), parallel_min_events=1)
+    assert np.array(st).shape == want.shape
+    assert _rel(st, want) <= 1e-6
+
+
 def test_dead_reckoning_select_and_dt():
     """kf_events_select keeps one type in stream order; kf_events_dt with prev0 = NaN gives the
     first event dt 0 (hw5_2.py:401, 407) and the rest raw differences (no guard)."""
