@@ -1,4 +1,4 @@
-"""Multi-process (world_size 2, gloo, CPU) coverage of the filter-sharding path used by
+"""Multi-process (world_size 2, 3 and 8, gloo, CPU) coverage of the filter-sharding path used by
 bench.py on N GPUs: shard ranges, per-rank work on its own slice, and the final
 all-gather reassembly.  The per-shard compute here is the CPU oracle (test
 infrastructure); on the GPU box the same kfmi.dist code moves RCCL tensors."""
@@ -60,20 +60,22 @@ def _worker(rank, world, port, total, T, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('total', [10, 9])  # even and uneven shards
-def test_gloo_world2_shard_and_gather(total):
+# even and uneven shards at world 2; world 8 (config 4's rank count) with uneven shards and
+# one rank holding no filter
+@pytest.mark.parametrize('world,total', [(2, 10), (2, 9), (8, 21), (8, 7)])
+def test_gloo_shard_and_gather(world, total):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, total, 6, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, total, 6, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=180)
-    assert [p.exitcode for p in procs] == [0, 0]
+    assert [p.exitcode for p in procs] == [0] * world
     err, slow = q.get(timeout=10)
     assert err < 1e-12
-    assert slow == [1.5, 0.0]
+    assert slow == [world - 0.5, 0.0]
 
 
 def _traj_worker(rank, world, port, total, T, every, out_q):
@@ -311,7 +313,7 @@ def _winner_worker(rank, world, port, n, w, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world', [2, 3])
+@pytest.mark.parametrize('world', [2, 3, 8])
 def test_gloo_search_winner_and_counts(world):
     """The cross-rank half of the sharded search (the bench's bf row at N > 1 runs it too):
     classes dealt round-robin over the ranks, MIN of the first accepted size, MAX of the
