@@ -553,8 +553,8 @@ int kf_events_dt(int64_t n, const double* t, const uint8_t* etype_in, double pre
  * walks the IMU events alone, skipping every fix (hw5_2.py:402-404).  etype device [n], t device
  * [n], payload device [n][9] (kf_ingest's layout); writes the K kept events' t_out [K],
  * payload_out [K][9] and src_out [K] (their stream positions), each of which may be NULL, with
- * capacity n, and *n_kept = K (host).  Synchronous (the count is returned); its scratch is a
- * per-device buffer the library keeps, so calls after the first of a size allocate nothing. */
+ * capacity n, and *n_kept = K (host).  Synchronous (the count is returned); its scratch (block counts, a
+ * mapped host int) is per device, allocated by the first call, so later calls allocate nothing. */
 int kf_events_select(int64_t n, const uint8_t* etype, const double* t, const double* payload, int keep_type,
                      double* t_out, double* payload_out, int32_t* src_out, int64_t* n_kept, void* stream);
 

@@ -268,29 +268,99 @@ __global__ __launch_bounds__(kIngBlock) void euler_kernel(int64_t n, const doubl
     quat_to_euler(q[i], q[ld + i], q[2 * ld + i], q[3 * ld + i], out[i], out[n + i], out[2 * n + i]);
 }
 
-// kf_events_select: the kept events' positions come from hipCUB's DeviceSelect over the event
-// indices; this gathers their time, payload row and position.
-struct IsType {
-    const uint8_t* etype;
-    uint8_t type;
-    __device__ __forceinline__ bool operator()(int32_t i) const { return etype[i] == type; }
-};
+// kf_events_select in two passes over blocks of consecutive events (at most kSelBlocks blocks;
+// a block walks its range in tiles of kIngBlock x kSelItems events):
+//   select_count_kernel   each block's number of kept events -> counts[b];
+//   select_gather_kernel  each block sums the counts of the blocks before it (its output
+//                         offset), ranks its tiles' kept events with a block scan and writes their
+//                         time and position; the payload rows of a tile are then copied one
+//                         output double per thread (contiguous stores, loads along the kept rows).
+// The last block writes the total.  Keeps stream order, so the output is DeviceSelect's.
+constexpr int kSelItems = 2;
+constexpr int kSelTile = kIngBlock * kSelItems;
+constexpr int kSelBlocks = 2048;
 
-// Thread o writes output double o of the [k][9] payload (row o / 9, column o % 9), so the stores
-// are contiguous and the loads follow the kept rows (runs of consecutive rows in a merged log);
-// threads o < k also write the time and position of kept event o.
-__global__ __launch_bounds__(kIngBlock) void select_gather_kernel(int64_t k, const int32_t* idx, const double* t,
+__global__ __launch_bounds__(kIngBlock) void select_count_kernel(int64_t n, int64_t per_block, const uint8_t* etype,
+                                                                  uint8_t type, int32_t* counts) {
+    using Reduce = hipcub::BlockReduce<int, kIngBlock>;
+    __shared__ typename Reduce::TempStorage tmp;
+    const int64_t lo = int64_t(blockIdx.x) * per_block;
+    const int64_t hi = lo + per_block < n ? lo + per_block : n;
+    int c = 0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kIngBlock) c += etype[i] == type;
+    c = Reduce(tmp).Sum(c);
+    if (threadIdx.x == 0) counts[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(kIngBlock) void select_gather_kernel(int64_t n, int64_t per_block, const uint8_t* etype,
+                                                                   uint8_t type, const int32_t* counts, const double* t,
                                                                    const double* payload, double* t_out,
-                                                                   double* payload_out, int32_t* src_out) {
-    const int64_t o = int64_t(blockIdx.x) * kIngBlock + threadIdx.x;
-    if (o < k) {
-        const int64_t i = idx[o];
-        if (t_out) t_out[o] = t[i];
-        if (src_out) src_out[o] = static_cast<int32_t>(i);
+                                                                   double* payload_out, int32_t* src_out,
+                                                                   int32_t* n_kept) {
+    using Reduce = hipcub::BlockReduce<int, kIngBlock>;
+    using Scan = hipcub::BlockScan<int, kIngBlock>;
+    __shared__ union {
+        typename Reduce::TempStorage red;
+        typename Scan::TempStorage scan;
+    } tmp;
+    __shared__ int32_t rows[kSelTile];
+    __shared__ int tile_kept;
+    const int tid = int(threadIdx.x);
+    int before = 0;
+    for (int b = tid; b < int(blockIdx.x); b += kIngBlock) before += counts[b];
+    int64_t base = Reduce(tmp.red).Sum(before);
+    __shared__ int64_t base_sh;
+    if (tid == 0) base_sh = base;
+    __syncthreads();
+    base = base_sh;
+    const int64_t lo = int64_t(blockIdx.x) * per_block;
+    const int64_t hi = lo + per_block < n ? lo + per_block : n;
+    for (int64_t t0 = lo; t0 < hi; t0 += kSelTile) {
+        // thread tid ranks events t0 + tid * kSelItems + 0 .. kSelItems - 1
+        const int64_t e0 = t0 + int64_t(tid) * kSelItems;
+        bool keep[kSelItems];
+        int mine = 0;
+#pragma unroll
+        for (int k = 0; k < kSelItems; ++k) {
+            keep[k] = e0 + k < hi && etype[e0 + k] == type;
+            mine += keep[k];
+        }
+        int off, total;
+        __syncthreads();  // tmp and rows are free again
+        Scan(tmp.scan).ExclusiveSum(mine, off, total);
+#pragma unroll
+        for (int k = 0; k < kSelItems; ++k)
+            if (keep[k]) {
+                const int64_t o = base + off;
+                rows[off] = int32_t(e0 + k);
+                if (t_out) t_out[o] = t[e0 + k];
+                if (src_out) src_out[o] = int32_t(e0 + k);
+                ++off;
+            }
+        if (tid == 0) tile_kept = total;
+        __syncthreads();
+        const int kept = tile_kept;
+        if (payload_out)
+            for (int q0 = tid; q0 < 9 * kept; q0 += 4 * kIngBlock) {  // four loads in flight
+                double v[4];
+                int64_t dst[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int q = q0 + u * kIngBlock;
+                    const int qc = q < 9 * kept ? q : 9 * kept - 1;  // past the tile: reload its last value
+                    const int j = qc / 9;
+                    v[u] = payload[int64_t(rows[j]) * 9 + (qc - 9 * j)];
+                    dst[u] = q < 9 * kept ? (base + j) * 9 + (qc - 9 * j) : -1;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (dst[u] >= 0) payload_out[dst[u]] = v[u];
+            }
+        base += kept;
     }
-    if (payload_out && o < 9 * k) {
-        const int64_t j = o / 9;
-        payload_out[o] = payload[int64_t(idx[j]) * 9 + (o - 9 * j)];
+    if (blockIdx.x == gridDim.x - 1 && tid == 0) {
+        *n_kept = int32_t(base);  // mapped host memory
+        __threadfence_system();
     }
 }
 
@@ -323,8 +393,9 @@ int hip_err(hipError_t e, const char* what) {
 // is synchronous and holds the lock throughout, so one buffer serves every stream.
 struct SelectScratch {
     std::mutex mu;
-    std::vector<void*> buf;
-    std::vector<size_t> bytes;
+    std::vector<int32_t*> counts;    // per device: the count pass's [kSelBlocks] block counts
+    std::vector<int32_t*> kept;      // per device: mapped, coherent host int the gather pass fills
+    std::vector<int32_t*> kept_dev;  // its device address
 };
 SelectScratch& select_scratch() {
     static SelectScratch s;
@@ -526,42 +597,43 @@ int kf_events_select(int64_t n, const uint8_t* etype, const double* t, const dou
     if (!etype || (t_out && !t) || (payload_out && !payload))
         return set_error(KF_EINVAL, "kf_events_select: null etype, or an output without its input");
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const IsType pred{etype, static_cast<uint8_t>(keep_type)};
-    hipcub::CountingInputIterator<int32_t> rows(0);
-    size_t tmp = 0;
-    KF_TRY(hipcub::DeviceSelect::If(nullptr, tmp, rows, (int32_t*)nullptr, (int32_t*)nullptr, static_cast<int>(n),
-                                    pred, st),
-           "kf_events_select sizing");
-    const size_t ib = (4 * size_t(n) + 255) & ~size_t(255);
-    const size_t need = ib + 256 + tmp;
     int dev = 0;
     KF_TRY(hipGetDevice(&dev), "kf_events_select device");
     SelectScratch& sc = select_scratch();
-    std::lock_guard<std::mutex> lock(sc.mu);
-    if (sc.buf.size() <= size_t(dev)) {
-        sc.buf.resize(dev + 1, nullptr);
-        sc.bytes.resize(dev + 1, 0);
+    std::lock_guard<std::mutex> lock(sc.mu);  // held to the end: the scratch is reused by the next call
+    if (sc.counts.size() <= size_t(dev)) {
+        sc.counts.resize(dev + 1, nullptr);
+        sc.kept.resize(dev + 1, nullptr);
+        sc.kept_dev.resize(dev + 1, nullptr);
     }
-    if (sc.bytes[dev] < need) {
-        if (sc.buf[dev]) (void)hipFree(sc.buf[dev]);
-        sc.buf[dev] = nullptr;
-        sc.bytes[dev] = 0;
-        KF_TRY(hipMalloc(&sc.buf[dev], need), "kf_events_select workspace");
-        sc.bytes[dev] = need;
+    if (!sc.counts[dev]) {
+        void *c = nullptr, *p = nullptr, *pd = nullptr;
+        hipError_t e = hipMalloc(&c, sizeof(int32_t) * kSelBlocks);
+        if (e == hipSuccess) e = hipHostMalloc(&p, sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&pd, p, 0);
+        if (e != hipSuccess) {
+            if (c) (void)hipFree(c);
+            if (p) (void)hipHostFree(p);
+            return set_error(KF_EHIP, "kf_events_select workspace: %s", hipGetErrorString(e));
+        }
+        sc.counts[dev] = static_cast<int32_t*>(c);
+        sc.kept[dev] = static_cast<int32_t*>(p);
+        sc.kept_dev[dev] = static_cast<int32_t*>(pd);
     }
-    char* const ws = static_cast<char*>(sc.buf[dev]);
-    int32_t* idx = reinterpret_cast<int32_t*>(ws);
-    int32_t* count = reinterpret_cast<int32_t*>(ws + ib);
-    KF_TRY(hipcub::DeviceSelect::If(ws + ib + 256, tmp, rows, idx, count, static_cast<int>(n), pred, st),
-           "kf_events_select");
-    int32_t k = 0;
-    KF_TRY(hipMemcpyAsync(&k, count, 4, hipMemcpyDeviceToHost, st), "kf_events_select readback");
+    // blocks of a multiple of the tile, at most kSelBlocks of them, none empty
+    const int64_t tiles = (n + kSelTile - 1) / kSelTile;
+    const int64_t per_block = ((tiles + kSelBlocks - 1) / kSelBlocks) * kSelTile;
+    const unsigned blocks = static_cast<unsigned>((n + per_block - 1) / per_block);
+    const uint8_t ty = static_cast<uint8_t>(keep_type);
+    *sc.kept[dev] = -1;
+    select_count_kernel<<<blocks, kIngBlock, 0, st>>>(n, per_block, etype, ty, sc.counts[dev]);
+    KF_TRY(hipGetLastError(), "kf_events_select count");
+    select_gather_kernel<<<blocks, kIngBlock, 0, st>>>(n, per_block, etype, ty, sc.counts[dev], t, payload, t_out,
+                                                       payload_out, src_out, sc.kept_dev[dev]);
+    KF_TRY(hipGetLastError(), "kf_events_select gather");
     KF_TRY(hipStreamSynchronize(st), "kf_events_select sync");
-    if (k && (t_out || payload_out || src_out)) {
-        select_gather_kernel<<<grid(payload_out ? 9 * k : k), kIngBlock, 0, st>>>(k, idx, t, payload, t_out, payload_out, src_out);
-        KF_TRY(hipGetLastError(), "kf_events_select gather");
-        KF_TRY(hipStreamSynchronize(st), "kf_events_select sync");  // before the scratch is reused
-    }
+    const int32_t k = *sc.kept[dev];
+    if (k < 0 || k > n) return set_error(KF_EHIP, "kf_events_select: no count came back (%d)", k);
     *n_kept = k;
     return KF_OK;
 }

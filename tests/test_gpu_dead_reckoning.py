@@ -97,6 +97,41 @@ def test_dead_reckoning_edge_cases(golden_dir):
     assert _rel(st, want) <= 1e-6
 
 
+@pytest.mark.parametrize('n,p_keep', [(1, 1.0), (2047, 0.5), (2048, 1.0), (2049, 0.0), (4_500_001, 0.97)])
+def test_events_select_sizes(n, p_keep):
+    """kf_events_select over one tile and its edges, none and all kept, and more tiles than
+    blocks (several tiles per block): every kept event's time, payload row and position, in
+    order, through the raw C ABI with each output alone too."""
+    import ctypes
+    rng = np.random.default_rng(n)
+    et = np.where(rng.random(n) < p_keep, 1, 0).astype(np.uint8)
+    d = torch.device('cuda', 0)
+    et_d = torch.from_numpy(et).to(d)
+    t_d = torch.arange(n, dtype=torch.float64, device=d) * 0.5
+    pay_d = torch.arange(9 * n, dtype=torch.float64, device=d).reshape(n, 9)
+    k_want = np.nonzero(et == 1)[0]
+    lib = _lib.lib()
+    for outs in ('all', 't', 'payload', 'src'):
+        t_o = torch.full((max(len(k_want), 1),), -1.0, dtype=torch.float64, device=d)
+        p_o = torch.full((max(len(k_want), 1), 9), -1.0, dtype=torch.float64, device=d)
+        s_o = torch.full((max(len(k_want), 1),), -1, dtype=torch.int32, device=d)
+        kept = ctypes.c_int64(-1)
+        ptr = lambda x, name: ctypes.c_void_p(x.data_ptr()) if outs in ('all', name) else None  # noqa: E731
+        rc = lib.kf_events_select(n, ctypes.c_void_p(et_d.data_ptr()), ctypes.c_void_p(t_d.data_ptr()),
+                                  ctypes.c_void_p(pay_d.data_ptr()), 1, ptr(t_o, 't'), ptr(p_o, 'payload'),
+                                  ptr(s_o, 'src'), ctypes.byref(kept),
+                                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert rc == 0, _lib.last_error()
+        assert kept.value == len(k_want)
+        m = len(k_want)
+        if outs in ('all', 't'):
+            np.testing.assert_array_equal(t_o[:m].cpu().numpy(), k_want * 0.5)
+        if outs in ('all', 'payload'):
+            np.testing.assert_array_equal(p_o[:m].cpu().numpy(), (9 * k_want[:, None] + np.arange(9)).astype(float))
+        if outs in ('all', 'src'):
+            np.testing.assert_array_equal(s_o[:m].cpu().numpy(), k_want)
+
+
 def test_dead_reckoning_select_and_dt():
     """kf_events_select keeps one type in stream order; kf_events_dt with prev0 = NaN gives the
     first event dt 0 (hw5_2.py:401, 407) and the rest raw differences (no guard)."""
