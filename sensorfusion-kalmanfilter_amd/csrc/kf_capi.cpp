@@ -1295,13 +1295,16 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         last = k_base + K;
         k_first = K + 1;
         if (!exhaustive) {  // any acceptable subset of sizes k_base .. k_base + K ends the search
-            e = hipMemcpyAsync(&best[k_base], &d_best[k_base], sizeof(uint64_t) * (K + 1), hipMemcpyDeviceToHost, st);
+            e = kfmi::launch_search_finish(d_best, h->search_host_dev, kMaxComboEvents + 1, false, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);
             if (e != hipSuccess) return hip_fail(e, "kf_search_combos: head result");
             for (int k = k_base; k <= last; ++k)
-                if (best[k]) k_first = kf_max + 1;
+                if (h->search_host[k]) k_first = kf_max + 1;
         }
     }
+    // not exhaustive: the results are peeked after groups of 1, 1, 2, 4, ... level launches, and
+    // a launch queued past the first accepted size does nothing (Ref15SearchArgs::stop_best)
+    int peek_at = k_first, peek_step = 1;
     for (int k = k_first; k <= kf_max; ++k) {
         kfmi::Ref15SearchArgs a{};
         a.kc = h->kc;
@@ -1328,6 +1331,11 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.subset_max = subset_max;
         a.tail = k < kf_max;
         a.sym = sym;
+        if (!exhaustive && k > 1) {  // sizes k_base .. k_base + k - 1 are complete
+            a.stop_best = d_best;
+            a.stop_lo = k_base;
+            a.stop_hi = k_base + k - 1;
+        }
         // a level without stored parents was scored whole by the previous launch's tail
         if (a.n_par) {
             a.pm_regs = opt(h, KF_OPT_SEARCH_PM) == 1;
@@ -1336,18 +1344,22 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
             ++launches;
         }
         last = k_base + k;
-        if (!exhaustive) {  // the reference stops at the first size with an acceptable subset
-            // (the first launch also scores the fixed root itself, size k_base)
-            const int lo = k == 1 ? k_base : last;
-            e = hipMemcpyAsync(&best[lo], &d_best[lo], sizeof(uint64_t) * (last - lo + 1), hipMemcpyDeviceToHost, st);
+        if (!exhaustive && k == peek_at && k < kf_max) {
+            // the reference stops at the first size with an acceptable subset (the first launch
+            // also scores the fixed root itself, size k_base)
+            e = kfmi::launch_search_finish(d_best, h->search_host_dev, kMaxComboEvents + 1, false, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);
             if (e != hipSuccess) return hip_fail(e, "kf_search_combos: level result");
-            if (best[lo] || best[last]) break;
+            bool any = false;
+            for (int s2 = k_base; s2 <= last; ++s2) any = any || h->search_host[s2] != 0;
+            if (any) break;
+            peek_at = k + peek_step;
+            peek_step *= 2;
         }
     }
     // best[] and n_acc[] are adjacent on the device: one kernel writes both to the host buffer
     // and zeroes them for the next search
-    e = kfmi::launch_search_finish(d_best, h->search_host_dev, 2 * (kMaxComboEvents + 1), st);
+    e = kfmi::launch_search_finish(d_best, h->search_host_dev, 2 * (kMaxComboEvents + 1), true, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(e, "kf_search_combos: results");
     h->search_ctr_zero = true;

@@ -245,6 +245,11 @@ struct Ref15SearchArgs {
                              // the same covariance; one of each is computed and stored
                              // (KF_OPT_AXIS_SYM)
     const RefConsts* kc;     // the handle's noise constants, or nullptr (the reference's)
+    // a non-exhaustive search queues several levels between its result peeks: a level launch
+    // does nothing when an earlier launch accepted a subset of a size it completed
+    // (stop_best[stop_lo .. stop_hi] not all zero; stop_hi - stop_lo < 64; nullptr: no test)
+    const uint64_t* stop_best;
+    int stop_lo, stop_hi;
 };
 
 // T rows of a search node: the block-packed P (27) and the running max's mantissa; an
@@ -352,9 +357,9 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
 void set_search_band(Ref15SearchArgs& a, bool f64);
 // levels 1 .. a.k of a search in one launch (one lane per subset of at most a.k free events)
 hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStream_t stream);
-// the end of a search: counters[0 .. n) (n <= 256) copied to `host` (the device address of mapped
-// host memory) and zeroed
-hipError_t launch_search_finish(uint64_t* counters, uint64_t* host, int n, hipStream_t stream);
+// a search's counters[0 .. n) (n <= 256) copied to `host` (the device address of mapped host
+// memory), and zeroed with `zero` (the end of the search)
+hipError_t launch_search_finish(uint64_t* counters, uint64_t* host, int n, bool zero, hipStream_t stream);
 hipError_t launch_ref15_score(bool f64, const Ref15ScoreArgs& a, hipStream_t stream);
 hipError_t launch_ref15_scheduled(bool f64, const Ref15SchedArgs& a, hipStream_t stream);
 // random_schedule's picks only (a.words): pick [T][B] event indices, a.sel_time, a.n_sel, a.words_used

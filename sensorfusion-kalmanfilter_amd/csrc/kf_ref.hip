@@ -2562,6 +2562,16 @@ __device__ __forceinline__ void search_publish(const Ref15SearchArgs& a, int k, 
 #ifndef KF_SEARCH_PM_WAVES
 #define KF_SEARCH_PM_WAVES 2  // waves per SIMD of the register variant (its VGPR budget)
 #endif
+// Ref15SearchArgs::stop_best: lane i reads size stop_lo + i (vector loads: these counters were
+// written by earlier launches' atomics); the same answer in every wave of the grid.  Called
+// before any lane leaves the kernel.
+__device__ __forceinline__ bool search_stopped(const Ref15SearchArgs& a) {
+    if (!a.stop_best) return false;
+    const int s = a.stop_lo + int(threadIdx.x & 63u);
+    const uint64_t v = s <= a.stop_hi ? __atomic_load_n(a.stop_best + s, __ATOMIC_RELAXED) : 0;
+    return __any(v != 0);
+}
+
 #ifndef KF_SEARCH_SYM_WAVES
 #define KF_SEARCH_SYM_WAVES 3  // waves per SIMD of the axis-symmetric search kernels (A/B builds)
 #endif
@@ -2571,6 +2581,7 @@ template <typename T, bool PLDS, bool CUSTOM, bool SYM>
 __global__ __launch_bounds__(PLDS ? 64 : kBlock) __attribute__((
     amdgpu_waves_per_eu(SYM ? KF_SEARCH_SYM_WAVES : PLDS ? 3 : KF_SEARCH_PM_WAVES))) void
 ref15_search_pm_kernel(const Ref15SearchArgs a) {
+    if (search_stopped(a)) return;
     constexpr int NT = PLDS ? 64 : kBlock;
     constexpr int NR = SearchNode<T, CUSTOM, SYM>::NR;
     const int64_t p = static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x;
@@ -2738,6 +2749,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEA
 template <typename T, bool CUSTOM, bool SYM>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEARCH_SYM_WAVES : 3))) void ref15_search_cm_kernel(const Ref15SearchArgs a,
                                                                                                      uint64_t n_items) {
+    if (search_stopped(a)) return;
     const uint64_t per_xcd = (n_items + 7) / 8;
     const uint64_t item = uint64_t(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
     if (item >= n_items) return;
@@ -3610,14 +3622,14 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
     a.status[f] = st;
 }
 
-// The end of kf_search_combos: its counters (best[], n_acc[]) go to the handle's mapped host
-// buffer (vector stores, made visible to the host before the kernel ends) and are zeroed for
-// the next search on the stream.
-__global__ __launch_bounds__(256) void search_finish_kernel(uint64_t* counters, uint64_t* host, int n) {
+// kf_search_combos' counters (best[], n_acc[]) to the handle's mapped host buffer (vector
+// stores, made visible to the host before the kernel ends): after a level of a non-exhaustive
+// search (peek), and at the end, where they are also zeroed for the next search on the stream.
+__global__ __launch_bounds__(256) void search_finish_kernel(uint64_t* counters, uint64_t* host, int n, bool zero) {
     const int i = int(threadIdx.x);
     if (i < n) {
         host[i] = counters[i];
-        counters[i] = 0;
+        if (zero) counters[i] = 0;
     }
     __threadfence_system();
 }
@@ -3919,9 +3931,9 @@ void set_search_band(Ref15SearchArgs& a, bool f64) {
     a.band_hi_e = int(fl) + e2;
 }
 
-hipError_t launch_search_finish(uint64_t* counters, uint64_t* host, int n, hipStream_t stream) {
+hipError_t launch_search_finish(uint64_t* counters, uint64_t* host, int n, bool zero, hipStream_t stream) {
     if (n < 1 || n > 256) return hipErrorInvalidValue;
-    search_finish_kernel<<<1, 256, 0, stream>>>(counters, host, n);
+    search_finish_kernel<<<1, 256, 0, stream>>>(counters, host, n, zero);
     return hipGetLastError();
 }
 

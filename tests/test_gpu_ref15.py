@@ -448,6 +448,37 @@ def test_search_classes_partition_the_search(golden_dir, w):
     kf.close()
 
 
+@pytest.mark.parametrize('head', ['on', 'off'])
+def test_search_stops_at_the_first_accepted_size(golden_dir, head):
+    """Not exhaustive, levels are queued in groups between result peeks and a level queued past
+    the first accepted size does nothing: for thresholds whose first accepted size runs over
+    the sizes (and none), the size, the winner and the counts up to it equal the exhaustive
+    search's, and the counts past it are 0."""
+    n = 18
+    _, ev, init, t0, target = _search_case(golden_dir, n)
+    kf = kfmi.BatchedKF('ref15', 1, 'f64', options={'search_head': head})
+    _, _, _, sm = kf.search_combos(ev, init, t0, target, threshold=-1e30, exhaustive=True, subset_max=True)
+    sm = sm.cpu().numpy()
+    sizes = np.array([bin(m).count('1') for m in range(1 << n)])
+    seen = set()
+    for s in list(range(1, n + 1)) + [None]:
+        if s is None:
+            thr = -1e30
+        else:
+            m = float(np.min(sm[sizes == s]))
+            thr = m + abs(m) * 1e-9 + 1e-12
+        want = kf.search_combos(ev, init, t0, target, thr, exhaustive=True)
+        got = kf.search_combos(ev, init, t0, target, thr, exhaustive=False)
+        kfound = want[0]
+        seen.add(kfound)
+        assert got[:2] == want[:2], (s, got[:2], want[:2])
+        np.testing.assert_array_equal(got[2][:kfound + 1], want[2][:kfound + 1])
+        if kfound:
+            assert not got[2][kfound + 1:].any()
+    kf.close()
+    assert 0 in seen and len(seen) >= 4
+
+
 def test_search_counters_carry_across_calls_and_streams(golden_dir):
     """The finish kernel hands each search's counters to the host and zeroes them for the next
     search on its stream: repeated searches, one on another stream, a non-exhaustive one that

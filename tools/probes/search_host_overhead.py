@@ -47,6 +47,23 @@ def main():
         b.record(st)
         b.synchronize()
         out[f'stream_span_us_n{n}'] = a.elapsed_time(b) * 1e3 / 20
+    # a non-exhaustive search that stops at a middle size: one result peek per level
+    ev, init, _, t0, t_end = bench.bf_events(25)
+    _, _, _, sm = kf.search_combos(ev, init, t0, t_end, -1e30, exhaustive=True, subset_max=True)
+    sm = sm.cpu().numpy()
+    masks = np.arange(1 << 25, dtype=np.uint32)
+    sizes = np.zeros(1 << 25, np.uint8)
+    for b in range(25):
+        sizes += ((masks >> b) & 1).astype(np.uint8)
+    mins = [float(np.nanmin(sm[sizes == k])) for k in range(1, 26)]
+    for label, thr in (('none', -1e30), ('mid', None)):
+        if thr is None:  # just above the lowest score of the largest size <= 16 below every
+            # smaller size's lowest: the search stops there
+            s_mid = max(s for s in range(1, 17) if all(mins[k - 1] > mins[s - 1] for k in range(1, s)))
+            thr = mins[s_mid - 1] + abs(mins[s_mid - 1]) * 1e-12 + 1e-15
+        out[f'stops_at_size_{label}'] = kf.search_combos(ev, init, t0, t_end, thr)[0]
+        out[f'wall_us_n25_stop_{label}'] = per_call(lambda: kf.search_combos(ev, init, t0, t_end, thr), 20)
+    del sm, sizes, masks
     ev, init, _, t0, t_end = bench.bf_events(4)
     ev = np.ascontiguousarray(ev)
     init = np.ascontiguousarray(init)
