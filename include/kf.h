@@ -150,6 +150,9 @@ const char* kf_version(void);
  *   KF_OPT_SEARCH_PM      kf_search_combos' parent-major kernel: 0 = parent in LDS, 1 = registers
  *   KF_OPT_SEARCH_HEAD    kf_search_combos: 0 = the first levels (sizes whose subsets need few event
  *                         steps in all) in one launch, one lane per subset; 1 = level by level
+ *   KF_OPT_SEARCH_END     kf_search_combos: 0 = the last levels (sizes whose subsets need few event
+ *                         steps from a stored prefix) in one launch, one lane per subset from its
+ *                         stored prefix; 1 = level by level
  *   KF_OPT_AXIS_SYM       0 = where the handle's noise constants are the same on every axis
  *                         (the reference's), work that depends on the constants alone is done
  *                         once for the axes' identical chains: kf_run_stream's covariance maps
@@ -191,7 +194,8 @@ const char* kf_version(void);
 #define KF_OPT_SCHED_REC_TIME 14
 #define KF_OPT_SEARCH_HEAD    15
 #define KF_OPT_AXIS_SYM       16
-#define KF_OPT_COUNT          17
+#define KF_OPT_SEARCH_END     17
+#define KF_OPT_COUNT          18
 int kf_set_option(kf_batch* handle, int option, int64_t value);
 int kf_get_option(const kf_batch* handle, int option, int64_t* value);
 

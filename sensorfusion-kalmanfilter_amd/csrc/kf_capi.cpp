@@ -111,6 +111,9 @@ constexpr uint64_t kSearchChildMajorParents = 200000;
 // the search's head launch covers the sizes whose subsets' event steps from the root add up to at
 // most this many (n = 25: sizes 1 .. 5, 323,775 steps for 68,405 subsets)
 constexpr uint64_t kSearchHeadSteps = 400000;
+// the end launch covers the last sizes whose subsets' event steps from their stored prefixes add
+// up to at most this many (n = 25: sizes 20 .. 25 from level 19, 86,712 steps for 68,406 subsets)
+constexpr uint64_t kSearchEndSteps = 200000;
 
 int64_t opt(const kf_batch* h, int o) { return h->opt[o]; }
 
@@ -408,7 +411,8 @@ int kf_set_option(kf_batch* h, int option, int64_t value) {
         case KF_OPT_STREAM:
         case KF_OPT_STREAM_FINAL:
         case KF_OPT_SEARCH_PM:
-        case KF_OPT_SEARCH_HEAD: ok = value == 0 || value == 1; break;
+        case KF_OPT_SEARCH_HEAD:
+        case KF_OPT_SEARCH_END: ok = value == 0 || value == 1; break;
         case KF_OPT_AXIS_SYM: ok = value == 0 || value == 1; break;
         case KF_OPT_SCHED_KERNEL: ok = value >= 0 && value <= 4; break;
         case KF_OPT_SCHED_GROUP: ok = value == 0 || value == 1 || value == 4; break;
@@ -1302,6 +1306,23 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
                 if (h->search_host[k]) k_first = kf_max + 1;
         }
     }
+    // the end launch: sizes k_end0 .. kf_max in one launch, each subset from its stored
+    // (k_end0 - 1)-prefix (launch_ref15_search_end), k_end0 the smallest size whose subsets' steps
+    // from their prefixes (sum_{k >= k_end0} (k - k_end0 + 1) C(n, k)) stay within
+    // kSearchEndSteps, above level 1 and above the head (level k_end0 - 1 is stored by a launch
+    // before it), and replacing at least two level launches (levels k_end0 and k_end0 + 1 have
+    // stored parents: k_end0 <= n - 2)
+    // The end launch takes one wave per (extension, 64 prefixes), its extensions (the subsets of
+    // k_end0 - 1 .. n - 1 of at most kf_max - k_end0 + 1 members) listed in the kernel
+    // arguments: at most 63 of them (n - k_end0 + 1 <= 6).
+    int k_end0 = kf_max + 1;
+    if (opt(h, KF_OPT_SEARCH_END) == 0)
+        for (int k0 = std::min(kf_max - 1, n - 2); k0 >= 2 && k0 > k_first && n - k0 + 1 <= 6; --k0) {
+            uint64_t steps = 0;
+            for (int k = k0; k <= kf_max; ++k) steps += uint64_t(k - k0 + 1) * C(n, k);
+            if (steps > kSearchEndSteps) break;
+            k_end0 = k0;
+        }
     // not exhaustive: the results are peeked after groups of 1, 1, 2, 4, ... level launches, and
     // a launch queued past the first accepted size does nothing (Ref15SearchArgs::stop_best)
     int peek_at = k_first, peek_step = 1;
@@ -1335,6 +1356,37 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
             a.stop_best = d_best;
             a.stop_lo = k_base;
             a.stop_hi = k_base + k - 1;
+        }
+        if (k == k_end0) {  // the rest of the search in one launch
+            a.k_end = kf_max;
+            a.n_par = 0;
+            a.child = nullptr;
+            a.tail = 0;
+            // extensions E of k_end0 - 1 .. n - 1, by size, then colex; each with the stored
+            // prefixes below its smallest member (C(e, k - 1); C(n - 2, k - 1) for E = {n - 1})
+            const int lo_c = k - 1, span = n - lo_c;
+            a.n_groups = 0;
+            a.n_child = 0;
+            uint64_t waves = 0;
+            for (int m = 1; m <= kf_max - k + 1; ++m)
+                for (uint32_t bits = 1; bits < (1u << span); ++bits) {
+                    if (__builtin_popcount(bits) != m) continue;
+                    const uint64_t ext = uint64_t(bits) << lo_c;
+                    const int e = __builtin_ctzll(ext);
+                    const uint64_t pre = C(e == n - 1 ? n - 2 : e, k - 1);
+                    if (!pre) continue;
+                    a.gblk[a.n_groups] = ext;
+                    a.gitem[a.n_groups] = waves;
+                    ++a.n_groups;
+                    waves += (pre + 63) / 64;
+                    a.n_child += pre;
+                }
+            a.gitem[a.n_groups] = waves;
+            e = kfmi::launch_ref15_search_end(h->dtype == KF_F64, a, st);
+            if (e != hipSuccess) return hip_fail(e, "kf_search_combos: end launch");
+            ++launches;
+            last = k_base + kf_max;
+            break;
         }
         // a level without stored parents was scored whole by the previous launch's tail
         if (a.n_par) {

@@ -250,6 +250,7 @@ struct Ref15SearchArgs {
     // (stop_best[stop_lo .. stop_hi] not all zero; stop_hi - stop_lo < 64; nullptr: no test)
     const uint64_t* stop_best;
     int stop_lo, stop_hi;
+    int k_end;               // the end launch (launch_ref15_search_end): sizes k .. k_end
 };
 
 // T rows of a search node: the block-packed P (27) and the running max's mantissa; an
@@ -357,6 +358,8 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
 void set_search_band(Ref15SearchArgs& a, bool f64);
 // levels 1 .. a.k of a search in one launch (one lane per subset of at most a.k free events)
 hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStream_t stream);
+// levels a.k .. a.k_end of a search in one launch, each subset from its stored (a.k - 1)-prefix
+hipError_t launch_ref15_search_end(bool f64, const Ref15SearchArgs& a, hipStream_t stream);
 // a search's counters[0 .. n) (n <= 256) copied to `host` (the device address of mapped host
 // memory), and zeroed with `zero` (the end of the search)
 hipError_t launch_search_finish(uint64_t* counters, uint64_t* host, int n, bool zero, hipStream_t stream);

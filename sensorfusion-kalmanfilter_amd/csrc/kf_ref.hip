@@ -2633,14 +2633,32 @@ ref15_search_pm_kernel(const Ref15SearchArgs a) {
 // K + 1's parents; one whose largest is n - 2 also scores its child with n - 1 (the tail).
 // a.n_child = sum_{k <= K} C(n, k).  Every lane stays to the end (the publish reductions read
 // every lane).
+// The binomials C(x, y), x <= n, y <= ymax, of the one-lane-per-subset kernels (head, end) in
+// LDS: their colex unranking walks up to n candidates per lane, each step a binomial load that
+// the next step depends on, so each step waits an LDS latency instead of an L1/L2 one.
+// Dynamic LDS of search_binom_lds_bytes(n, ymax); every lane of the block calls it.
+__host__ __device__ constexpr size_t search_binom_lds_bytes(int n, int ymax) {
+    return sizeof(uint64_t) * size_t(n + 1) * size_t(ymax + 1);
+}
+__device__ __forceinline__ const uint64_t* search_binom_lds(const Ref15SearchArgs& a, int ymax) {
+    extern __shared__ uint64_t sbinom[];
+    const int n = a.n_events, w = ymax + 1, tot = (n + 1) * w;
+    for (int i = int(threadIdx.x); i < tot; i += int(blockDim.x)) {
+        const int x = i / w, y = i - x * w;
+        sbinom[i] = a.binom[x * (kMaxEvents + 1) + y];
+    }
+    __syncthreads();
+    return sbinom;
+}
+
 template <typename T, bool CUSTOM, bool SYM>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEARCH_SYM_WAVES : 3))) void ref15_search_head_kernel(
     const Ref15SearchArgs a) {
     using Node = SearchNode<T, CUSTOM, SYM>;
     constexpr int RP = SYM ? M15::NP : 1, RA = SYM ? M15::NA : 1;
     const int n = a.n_events, K = a.k;
-    const uint64_t* C = a.binom;
-    auto binom = [&](int x, int y) -> uint64_t { return C[x * (kMaxEvents + 1) + y]; };
+    const uint64_t* C = search_binom_lds(a, K + 1);  // C(n, k) for k <= K, C(c, i) for i <= K
+    auto binom = [&](int x, int y) -> uint64_t { return C[x * (K + 2) + y]; };
     const uint64_t g = uint64_t(blockIdx.x) * 64 + threadIdx.x;
     const bool live = g < a.n_child;
     int k = 1;
@@ -2738,6 +2756,78 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEA
         if (__builtin_amdgcn_ballot_w64(live && k == kk) != 0)
             search_publish(a, kk, k == kk ? best : 0, k == kk ? cnt : 0);
     if (a.tail) search_publish(a, K + 1, best1, cnt1);
+}
+
+// The end of the search, sizes a.k .. a.k_end (free sizes) in ONE launch, extension-major: a
+// subset S of size >= a.k is its (a.k - 1)-prefix P (its smallest members, a node of level
+// a.k - 1) plus its extension E (the rest).  For an extension E whose smallest member is e, the
+// prefixes are every (a.k - 1)-subset of 0 .. e - 1, which are level a.k - 1's colex ranks
+// 0 .. C(e, a.k - 1) - 1, all stored (their largest member is <= n - 3) except, for E = {n - 1},
+// the ranks from C(n - 2, a.k - 1) on, whose subsets level a.k - 1's tail scored.  So one wave
+// takes one extension and 64 consecutive prefixes: its node loads are one parent block, its
+// events and subset size are wave-uniform, and nothing is unranked.  Group i of the host's table
+// is extension gblk[i] (a mask of free candidates, ordered by size), its waves start at
+// gitem[i].  Every subset's score is the level search's, bit for bit (the level kernels' per-chain
+// operations from the same stored node).  It replaces the last levels' launches, which hold a few
+// thousand subsets or fewer and sit at the launch-and-one-event floor.
+template <typename T, bool CUSTOM, bool SYM>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEARCH_SYM_WAVES : 3))) void ref15_search_end_kernel(
+    const Ref15SearchArgs a) {
+    if (search_stopped(a)) return;
+    using Node = SearchNode<T, CUSTOM, SYM>;
+    constexpr int RP = SYM ? M15::NP : 1, RA = SYM ? M15::NA : 1;
+    const int n = a.n_events, K0 = a.k;
+    const uint64_t w = blockIdx.x;
+    int lo = 0, hi = a.n_groups - 1;  // the last group whose first wave is <= w
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.gitem[mid] <= w) lo = mid;
+        else hi = mid - 1;
+    }
+    const uint64_t ext = a.gblk[lo];
+    const int e = __builtin_ctzll(ext);
+    const int ex = e == n - 1 ? n - 2 : e;  // E = {n - 1}: the stored prefixes only
+    const uint64_t n_pre = a.binom[ex * (kMaxEvents + 1) + K0 - 1];
+    const uint64_t rp = (w - a.gitem[lo]) * 64 + threadIdx.x;
+    const bool live = rp < n_pre;
+    uint64_t best = 0, cnt = 0;
+    const DetBand<T> band(a);
+    Node nd;
+    nd.load(a.par, live ? rp : 0);  // a stored node either way (rank 0 is)
+    DetV<T> fmax = nd.run;
+#pragma unroll 1
+    for (uint64_t m = ext; m; m &= m - 1) {
+        const int j = __builtin_ctzll(m);
+        SearchEvent vs = search_event(a, j, nd.prev);
+        vs.final_predict = vs.final_predict && (m & (m - 1)) == 0;  // only the subset itself is scored
+        SearchScore<T, CUSTOM> ss;
+        ss.kc = a.kc;
+#pragma unroll
+        for (int ch = 0; ch < Node::NP; ++ch) {
+            T Pb[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) Pb[i] = nd.P[6 * ch + i];
+            search_pva<T, CUSTOM>(vs, ch, Pb, ss.ok, a.kc);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) nd.P[6 * ch + i] = Pb[i];
+            ss.add_pva(vs, Pb, ch, RP);
+        }
+#pragma unroll
+        for (int ch = 0; ch < Node::NA; ++ch) {
+            T Pa[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) Pa[i] = nd.P[6 * Node::NP + 3 * ch + i];
+            search_aw<T, CUSTOM>(vs, ch, Pa, ss.ok, a.kc);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) nd.P[6 * Node::NP + 3 * ch + i] = Pa[i];
+            ss.add_aw(vs, Pa, ch, RA);
+        }
+        nd.run = ss.finish(vs, nd.run, fmax);
+        nd.prev = vs.prev;
+        nd.mask |= uint64_t(1) << (j + a.shift);
+    }
+    if (live) search_score(a, band, nd.mask, fmax, best, cnt);
+    search_publish(a, K0 - 1 + __builtin_popcountll(ext), best, cnt);
 }
 
 // Child-major: one wave per (parent block of 64, child event) work item, one child per lane,
@@ -3937,18 +4027,37 @@ hipError_t launch_search_finish(uint64_t* counters, uint64_t* host, int n, bool 
     return hipGetLastError();
 }
 
+hipError_t launch_ref15_search_end(bool f64, const Ref15SearchArgs& a, hipStream_t stream) {
+    if (a.n_events > kMaxEvents || a.k < 2 || a.k_end < a.k || a.k_end > a.n_events || !a.par || a.n_groups < 1 ||
+        a.n_groups > 65 || a.gitem[a.n_groups] == 0 || a.gitem[a.n_groups] >= (1ull << 31))
+        return hipErrorInvalidValue;
+    // the extensions' table (group i: extension gblk[i], first wave gitem[i], then the total)
+    const dim3 grid(unsigned(a.gitem[a.n_groups]));
+    KF_CUSTOM_DISPATCH(a.kc, {
+        if (a.sym) {
+            if (f64) ref15_search_end_kernel<double, CUSTOM, true><<<grid, 64, 0, stream>>>(a);
+            else ref15_search_end_kernel<float, CUSTOM, true><<<grid, 64, 0, stream>>>(a);
+        } else {
+            if (f64) ref15_search_end_kernel<double, CUSTOM, false><<<grid, 64, 0, stream>>>(a);
+            else ref15_search_end_kernel<float, CUSTOM, false><<<grid, 64, 0, stream>>>(a);
+        }
+    });
+    return hipGetLastError();
+}
+
 hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStream_t stream) {
     if (a.n_events > kMaxEvents || a.n_events < 3 || a.k < 1 || a.k > a.n_events - 2 || a.n_child == 0 ||
         a.n_child >= (1ull << 31))
         return hipErrorInvalidValue;
     const dim3 grid(unsigned((a.n_child + 63) / 64));
+    const size_t lds = search_binom_lds_bytes(a.n_events, a.k + 1);
     KF_CUSTOM_DISPATCH(a.kc, {
         if (a.sym) {
-            if (f64) ref15_search_head_kernel<double, CUSTOM, true><<<grid, 64, 0, stream>>>(a);
-            else ref15_search_head_kernel<float, CUSTOM, true><<<grid, 64, 0, stream>>>(a);
+            if (f64) ref15_search_head_kernel<double, CUSTOM, true><<<grid, 64, lds, stream>>>(a);
+            else ref15_search_head_kernel<float, CUSTOM, true><<<grid, 64, lds, stream>>>(a);
         } else {
-            if (f64) ref15_search_head_kernel<double, CUSTOM, false><<<grid, 64, 0, stream>>>(a);
-            else ref15_search_head_kernel<float, CUSTOM, false><<<grid, 64, 0, stream>>>(a);
+            if (f64) ref15_search_head_kernel<double, CUSTOM, false><<<grid, 64, lds, stream>>>(a);
+            else ref15_search_head_kernel<float, CUSTOM, false><<<grid, 64, lds, stream>>>(a);
         }
     });
     return hipGetLastError();

@@ -314,6 +314,47 @@ def test_search_head_equals_level_search(golden_dir, n_fixed, fixed_mask):
     assert a[2][0] > 0 and not a[2][2][a[2][0] + 1:].any()
 
 
+@pytest.mark.parametrize('dtype,sym,n_fixed,fixed_mask', [('f64', False, 0, 0), ('f64', True, 0, 0),
+                                                          ('f64', True, 3, 0b101), ('f32', True, 0, 0),
+                                                          ('f32', False, 2, 0b10)])
+def test_search_end_equals_level_search(golden_dir, dtype, sym, n_fixed, fixed_mask):
+    """The end launch (the last sizes in one launch, each subset from its stored prefix) and the
+    level-by-level search give every subset the same max log-det, bit for bit, the same counts
+    per size and the same winner, exhaustive and not, with the head on; n = 18 (the end launch
+    covers sizes 11 .. 18 of the free candidates there), every-chain and axis-symmetric nodes,
+    f64 and f32, a whole search and a class of a sharded one."""
+    n = 18
+    cand, ev, init, t0, target = _search_case(golden_dir, n)
+    if sym:
+        init = _axis_symmetric(init)
+    out = {}
+    for end in ('on', 'off'):
+        kf = kfmi.BatchedKF('ref15', 1, dtype, options={'search_end': end})
+        _, _, _, sm = kf.search_combos(ev, init, t0, target, -1e30, exhaustive=True, subset_max=True,
+                                       n_fixed=n_fixed, fixed_mask=fixed_mask)
+        info = kf.search_info()
+        assert info['sym'] == sym
+        sm = sm.cpu().numpy()
+        res = [sm]
+        for q in (0.02, 0.6, 0.97):
+            thr = _gap_threshold(sm, q)
+            res.append(kf.search_combos(ev, init, t0, target, thr, exhaustive=True, n_fixed=n_fixed,
+                                        fixed_mask=fixed_mask))
+            res.append(kf.search_combos(ev, init, t0, target, thr, exhaustive=False, n_fixed=n_fixed,
+                                        fixed_mask=fixed_mask))
+        out[end] = (res, info['level_launches'])
+        kf.close()
+    a, b = out['on'][0], out['off'][0]
+    np.testing.assert_array_equal(a[0], b[0])
+    assert np.isfinite(a[0][1:]).sum() > 0
+    for x, y in zip(a[1:], b[1:]):
+        assert x[:2] == y[:2]
+        np.testing.assert_array_equal(x[2], y[2])
+    # fewer launches (in a class of 15 free candidates the head leaves a single level, which the
+    # end launch does not replace)
+    assert out['on'][1] <= out['off'][1] and (n_fixed > 0 or out['on'][1] < out['off'][1])
+
+
 def _axis_symmetric(init):
     """init with the x axis's covariance blocks copied to the y and z axes."""
     out = np.array(init, dtype=np.float64)
