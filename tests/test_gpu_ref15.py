@@ -355,6 +355,44 @@ def test_search_end_equals_level_search(golden_dir, dtype, sym, n_fixed, fixed_m
     assert out['on'][1] <= out['off'][1] and (n_fixed > 0 or out['on'][1] < out['off'][1])
 
 
+def test_search_end_random_shapes(golden_dir):
+    """The end launch against the level-by-level search over seeded shapes: n 6 .. 20, k_max
+    below n, head on and off, every-chain and axis-symmetric nodes, fixed candidates; every
+    subset's max log-det bit for bit and the counts per size."""
+    rng = np.random.default_rng(2025)
+    fused = 0
+    for case in range(14):
+        n = int(rng.integers(6, 21))
+        k_max = int(rng.integers(max(2, n - 4), n + 1))
+        head = ['on', 'off'][case % 2]
+        sym = bool(case % 3)
+        n_fixed = int(rng.integers(0, 3))
+        fixed_mask = int(rng.integers(0, 1 << n_fixed)) if n_fixed else 0
+        if k_max <= bin(fixed_mask).count('1'):
+            k_max = n
+        _, ev, init, t0, target = _search_case(golden_dir, n, swap=n > 6)
+        if sym:
+            init = _axis_symmetric(init)
+        got = {}
+        for end in ('on', 'off'):
+            kf = kfmi.BatchedKF('ref15', 1, 'f64', options={'search_end': end, 'search_head': head})
+            k, win, acc, sm = kf.search_combos(ev, init, t0, target, -1e30, k_max=k_max, exhaustive=True,
+                                               subset_max=True, n_fixed=n_fixed, fixed_mask=fixed_mask)
+            launches = kf.search_info()['level_launches']
+            sm = sm.cpu().numpy()
+            thr = _gap_threshold(sm, 0.3)
+            r2 = kf.search_combos(ev, init, t0, target, thr, k_max=k_max, exhaustive=True, n_fixed=n_fixed,
+                                  fixed_mask=fixed_mask)
+            kf.close()
+            got[end] = (sm, r2, launches)
+        shape = (n, k_max, head, sym, n_fixed, fixed_mask)
+        np.testing.assert_array_equal(got['on'][0], got['off'][0], err_msg=str(shape))
+        assert got['on'][1][:2] == got['off'][1][:2], shape
+        np.testing.assert_array_equal(got['on'][1][2], got['off'][1][2], err_msg=str(shape))
+        fused += got['on'][2] < got['off'][2]
+    assert fused >= 4  # the end launch ran in enough of the shapes
+
+
 def _axis_symmetric(init):
     """init with the x axis's covariance blocks copied to the y and z axes."""
     out = np.array(init, dtype=np.float64)
