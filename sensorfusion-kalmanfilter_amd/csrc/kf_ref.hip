@@ -2418,7 +2418,7 @@ struct SearchScore {
         T Pf[6], xf[3] = {T(0), T(0), T(0)};
 #pragma unroll
         for (int i = 0; i < 6; ++i) Pf[i] = Pb[i];
-        if (v.final_predict) C15::template chain_predict<3>(xf, Pf, T(v.dte), qpva);
+        C15::template chain_predict<3>(xf, Pf, T(v.dte), qpva);  // read by finish() only with v.final_predict
 #pragma unroll
         for (int r = 0; r < reps; ++r) fin.add_pva(Pf, ch + r);
     }
@@ -2431,7 +2431,7 @@ struct SearchScore {
         T Pf[3], xf[2] = {T(0), T(0)};
 #pragma unroll
         for (int i = 0; i < 3; ++i) Pf[i] = Pa[i];
-        if (v.final_predict) C15::template chain_predict<2>(xf, Pf, T(v.dte), qaw);
+        C15::template chain_predict<2>(xf, Pf, T(v.dte), qaw);  // read by finish() only with v.final_predict
 #pragma unroll
         for (int r = 0; r < reps; ++r) fin.add_aw(Pf);
     }
