@@ -314,22 +314,28 @@ def test_search_head_equals_level_search(golden_dir, n_fixed, fixed_mask):
     assert a[2][0] > 0 and not a[2][2][a[2][0] + 1:].any()
 
 
-@pytest.mark.parametrize('dtype,sym,n_fixed,fixed_mask', [('f64', False, 0, 0), ('f64', True, 0, 0),
-                                                          ('f64', True, 3, 0b101), ('f32', True, 0, 0),
-                                                          ('f32', False, 2, 0b10)])
-def test_search_end_equals_level_search(golden_dir, dtype, sym, n_fixed, fixed_mask):
+@pytest.mark.parametrize('dtype,sym,n_fixed,fixed_mask,consts', [('f64', False, 0, 0, 'reference'),
+                                                                 ('f64', True, 0, 0, 'reference'),
+                                                                 ('f64', True, 3, 0b101, 'reference'),
+                                                                 ('f32', True, 0, 0, 'reference'),
+                                                                 ('f32', False, 2, 0b10, 'reference'),
+                                                                 ('f64', True, 0, 0, 'custom'),
+                                                                 ('f32', False, 0, 0, 'custom')])
+def test_search_end_equals_level_search(golden_dir, dtype, sym, n_fixed, fixed_mask, consts):
     """The end launch (the last sizes in one launch, each subset from its stored prefix) and the
     level-by-level search give every subset the same max log-det, bit for bit, the same counts
     per size and the same winner, exhaustive and not, with the head on; n = 18 (the end launch
     covers sizes 11 .. 18 of the free candidates there), every-chain and axis-symmetric nodes,
-    f64 and f32, a whole search and a class of a sharded one."""
+    f64 and f32, the reference's constants and a caller's, a whole search and a class of a
+    sharded one."""
     n = 18
     cand, ev, init, t0, target = _search_case(golden_dir, n)
     if sym:
         init = _axis_symmetric(init)
+    params = _symmetric_consts(7).params() if consts == 'custom' else None
     out = {}
     for end in ('on', 'off'):
-        kf = kfmi.BatchedKF('ref15', 1, dtype, options={'search_end': end})
+        kf = kfmi.BatchedKF('ref15', 1, dtype, params=params, options={'search_end': end})
         _, _, _, sm = kf.search_combos(ev, init, t0, target, -1e30, exhaustive=True, subset_max=True,
                                        n_fixed=n_fixed, fixed_mask=fixed_mask)
         info = kf.search_info()
