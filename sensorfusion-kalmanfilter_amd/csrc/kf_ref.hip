@@ -1818,7 +1818,12 @@ __device__ __forceinline__ void lft_apply(double (&p)[3][3], const double (&m)[3
 // guesses, variant q + 1 with + delta on component q of every chain.  Thread 0 of block 0
 // zeroes the check.
 constexpr int kStartMaxG = 4;  // chunks per thread of the start kernel (their starts stay in registers)
-template <typename T, class M, bool LDS>
+// NU: the LDS maps' row pitch fixed at compile time (where the block's window maps fit it): a
+// walk's 36 reads of a map are then immediate offsets from one address, where a runtime pitch
+// cost an address add per element and the products of each chunk's rows (~120 of the ~290
+// instructions of a map application)
+constexpr int kStartNu = 192;
+template <typename T, class M, bool LDS, bool NU = false>
 __global__ __launch_bounds__(kBlock) void stream_lft_start_kernel(const StreamArgs a) {
     extern __shared__ double lmap[];  // [36][nu]: element e of the block's nu = (G + iters) * np window maps
     constexpr int NCH = M::NP + M::NA;
@@ -1836,7 +1841,7 @@ __global__ __launch_bounds__(kBlock) void stream_lft_start_kernel(const StreamAr
     const int64_t b0 = int64_t(blockIdx.x) * BC;
     const int64_t ws = b0 - a.iters > 0 ? b0 - a.iters : 0;  // first chunk whose maps the block reads
     // struct of arrays: at each step of the walks, consecutive threads read maps g apart
-    const uint32_t nu = uint32_t((BC + a.iters) * a.np);
+    const uint32_t nu = NU ? uint32_t(kStartNu) : uint32_t((BC + a.iters) * a.np);
     if constexpr (LDS) {
         const int64_t we = (b0 + BC < a.C ? b0 + BC : a.C) - 1;  // maps of chunks [ws, we)
         // 32-bit indices (a 64-bit division is a ~100-instruction sequence per element), 16 loads
@@ -3936,9 +3941,13 @@ void stream_phase(int phase, const StreamArgs& a, hipStream_t stream) {
             const unsigned want = a.start_threads > 0 ? unsigned(a.start_threads) : unsigned(kBlock);
             const unsigned threads = a.g > 0 ? (want > walkers && want <= unsigned(kBlock) ? want : walkers)
                                              : unsigned(kBlock);
-            const size_t lds = a.g > 0 ? size_t(a.G + a.iters) * a.np * 36 * sizeof(double) : 0;
+            const bool fixed = a.g > 0 && (a.G + a.iters) * a.np <= kStartNu;
+            const size_t lds = !(a.g > 0) ? 0
+                               : fixed    ? size_t(kStartNu) * 36 * sizeof(double)
+                                          : size_t(a.G + a.iters) * a.np * 36 * sizeof(double);
             const dim3 g(unsigned((a.C + bc - 1) / bc), NCH);
-            if (a.g > 0) stream_lft_start_kernel<T, M, true><<<g, threads, lds, stream>>>(a);
+            if (fixed) stream_lft_start_kernel<T, M, true, true><<<g, threads, lds, stream>>>(a);
+            else if (a.g > 0) stream_lft_start_kernel<T, M, true><<<g, threads, lds, stream>>>(a);
             else stream_lft_start_kernel<T, M, false><<<g, threads, 0, stream>>>(a);
             break;
         }
