@@ -1063,21 +1063,22 @@ def bf_workload(cfg, args, rank, world, dev):
         return out
 
     if search:
-        from kfmi.ref15 import search_level_bytes
+        from kfmi.ref15 import search_end_size, search_level_bytes, search_stored_levels
         step()  # how the library runs this search (kf_search_info): axis-symmetric, head, launches
         torch.cuda.synchronize(dev)
         info = kf.search_info()
         K, sym = info['head_sizes'], info['sym']
         launches = info['level_launches'] + (1 if K else 0)
-        # every stored node (the C(n-2, k) subsets of size k < n whose largest candidate is
-        # <= n - 3) is written once and read once as a parent; the one-launch head (sizes 1 .. K)
-        # stores only its level K
-        lvl = sum(search_level_bytes(math.comb(n - 2, k), 'f64', sym) for k in range(max(K, 1), n))
+        k_end = search_end_size(n)
+        # every stored node (the C(n-2, k) subsets of size k whose largest candidate is <= n - 3)
+        # is written once and read once as a parent; the one-launch head (sizes 1 .. K) stores only
+        # its level K, and the end launch (sizes k_end .. n) reads level k_end - 1 and stores none
+        lvl = sum(search_level_bytes(math.comb(n - 2, k), 'f64', sym) for k in search_stored_levels(n))
         chains = ('axis-symmetric: one pva and one aw chain computed and stored for the three of each, '
                   'KF_OPT_AXIS_SYM' if sym else 'every chain')
         return dict(step=step, units=total_steps, bytes=2 * lvl, bytes_per_unit=2 * lvl / total_combos,
-                    kernel=f'ref15_search_head_kernel (sizes 1..{K}) + ref15_search_cm/pm_kernel (the '
-                           f'{launches} launches of one search)',
+                    kernel=f'ref15_search_head_kernel (sizes 1..{K}) + ref15_search_cm/pm_kernel + '
+                           f'ref15_search_end_kernel (sizes {k_end}..{n}) (the {launches} launches of one search)',
                     traffic=load_traffic('bf', 2 * lvl), valu=load_valu('bf') if load_traffic('bf', 2 * lvl) else None,
                     cpu=cpu,
                     gather=None, dist_check=dist_check, kf=kf, combos=total_combos,
@@ -1088,7 +1089,8 @@ def bf_workload(cfg, args, rank, world, dev):
                     desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '
                          f'all 2^{n}-1 subsets, reference 15-state model, f64, shared-prefix search '
                          f'(kf_search_combos: one event step + final predict per subset, sizes 1..{K} in one '
-                         f'launch, then one launch per level: {launches} launches; {chains}); '
+                         f'launch, then one launch per level, sizes {k_end}..{n} in one: {launches} launches; '
+                         f'{chains}); '
                          f'value counts the reference-equivalent steps (k events + final predict per k-subset)',
                     extra={'candidate_events': n, 'combinations': total_combos, 'levels': n, 'search': info})
     return dict(step=step, units=total_steps, bytes=None, bytes_per_unit=None, kernel='ref15_combo_kernel',

@@ -646,6 +646,7 @@ def search_level_bytes(nodes, dtype, sym=False):
 
 
 SEARCH_HEAD_STEPS = 400000  # kf_capi.cpp kSearchHeadSteps
+SEARCH_END_STEPS = 200000   # kf_capi.cpp kSearchEndSteps
 
 
 def search_head_size(n, k_max=None):
@@ -664,13 +665,43 @@ def search_head_size(n, k_max=None):
     return K if K >= 2 else 0
 
 
+def search_end_size(n, k_max=None, head=True):
+    """The first size k_end0 of kf_search_combos' end launch (kf_capi.cpp: sizes k_end0 .. k_max
+    in one launch from level k_end0 - 1's stored nodes), k_max + 1 for none: the smallest k0 with
+    sum_{k >= k0} (k - k0 + 1) C(n, k) within kSearchEndSteps, 2 <= k0 <= min(k_max - 1, n - 2),
+    above the head's sizes, n - k0 + 1 <= 6.  Bookkeeping for the bench's bytes."""
+    k_max = n if k_max is None else k_max
+    K = search_head_size(n, k_max) if head else 0
+    k_first = K + 1 if K else 1
+    end = k_max + 1
+    k0 = min(k_max - 1, n - 2)
+    while k0 >= 2 and k0 > k_first and n - k0 + 1 <= 6:
+        if sum((k - k0 + 1) * math.comb(n, k) for k in range(k0, k_max + 1)) > SEARCH_END_STEPS:
+            break
+        end = k0
+        k0 -= 1
+    return end
+
+
 def search_launches(n, k_max=None):
-    """Kernel launches of one kf_search_combos over n free candidates: the head (if any), then
-    every later level with stored parents (a level with none is scored by the previous tail)."""
+    """Kernel launches of one kf_search_combos over n free candidates: the head (if any), every
+    later level with stored parents (a level with none is scored by the previous tail) up to the
+    end launch, and the end launch (if any)."""
     k_max = n if k_max is None else k_max
     K = search_head_size(n, k_max)
-    levels = [k for k in range(1, k_max + 1) if k == 1 or math.comb(n - 2, k - 1) > 0]
-    return (1 if K else 0) + sum(1 for k in levels if k > K)
+    end = search_end_size(n, k_max)
+    levels = [k for k in range(1, min(k_max, end - 1) + 1) if k == 1 or math.comb(n - 2, k - 1) > 0]
+    return (1 if K else 0) + sum(1 for k in levels if k > K) + (1 if end <= k_max else 0)
+
+
+def search_stored_levels(n, k_max=None):
+    """The levels whose nodes one kf_search_combos writes once and reads once as parents: from
+    the head's last size (or 1) up to the level before the end launch (which reads that level and
+    stores nothing), or to the last level with children."""
+    k_max = n if k_max is None else k_max
+    K = search_head_size(n, k_max)
+    end = search_end_size(n, k_max)
+    return list(range(max(K, 1), min(end, k_max)))
 
 
 def search_levels(n, dtype='f64', mem_bytes=32 << 30):

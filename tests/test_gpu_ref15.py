@@ -325,7 +325,7 @@ def test_search_end_equals_level_search(golden_dir, dtype, sym, n_fixed, fixed_m
     """The end launch (the last sizes in one launch, each subset from its stored prefix) and the
     level-by-level search give every subset the same max log-det, bit for bit, the same counts
     per size and the same winner, exhaustive and not, with the head on; n = 18 (the end launch
-    covers sizes 11 .. 18 of the free candidates there), every-chain and axis-symmetric nodes,
+    covers sizes 13 .. 18 of the free candidates there), every-chain and axis-symmetric nodes,
     f64 and f32, the reference's constants and a caller's, a whole search and a class of a
     sharded one."""
     n = 18

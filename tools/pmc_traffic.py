@@ -101,18 +101,17 @@ def main():
             wk = per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE')
             f = [v for k, vs in fk.items() if is_search(k) for v in vs]
             w = [v for k, vs in wk.items() if is_search(k) for v in vs]
-            from kfmi.ref15 import search_head_size, search_launches, search_level_bytes
+            from kfmi.ref15 import search_launches, search_level_bytes, search_stored_levels
             import math
-            # launches per search: the head (sizes 1 .. K), then the levels with stored parents
-            # (level n is scored by the tail of level n - 1 and not launched)
+            # launches per search: the head (sizes 1 .. K), the levels with stored parents up to
+            # the end launch, and the end launch
             nl = search_launches(n)
-            K = search_head_size(n)
             fb, info = fetch(out_dir, f'cfg{c}', is_search, f, read_scale)
             fb *= nl
             if 'fetch_bytes_calibrated' in info:
                 info['fetch_bytes_calibrated'] *= nl
             write = 1024 * sum(w) / (len(w) / nl)
-            alg = 2 * sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in range(max(K, 1), n))
+            alg = 2 * sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in search_stored_levels(n))
             with open(os.path.join(out_dir, 'cfgbf_FETCH_SIZE.log')) as fh:  # the bench line's own count
                 for line in fh:
                     if line.startswith('{"metric"'):
