@@ -361,6 +361,19 @@ def test_search_end_equals_level_search(golden_dir, dtype, sym, n_fixed, fixed_m
     assert out['on'][1] <= out['off'][1] and (n_fixed > 0 or out['on'][1] < out['off'][1])
 
 
+@pytest.mark.parametrize('n', [4, 5, 9, 12, 18, 25])
+def test_search_launch_bookkeeping(golden_dir, n):
+    """kfmi.ref15's mirror of the launch plan (the bench's bytes and the PMC reduction use it)
+    agrees with what kf_search_combos ran: the head's sizes and the launches of one search."""
+    _, ev, init, t0, target = _search_case(golden_dir, n, swap=n > 6)
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    kf.search_combos(ev, init, t0, target, -1e30, exhaustive=True)
+    info = kf.search_info()
+    kf.close()
+    assert info['head_sizes'] == ref15.search_head_size(n)
+    assert info['level_launches'] + (1 if info['head_sizes'] else 0) == ref15.search_launches(n)
+
+
 def test_search_end_random_shapes(golden_dir):
     """The end launch against the level-by-level search over seeded shapes: n 6 .. 20, k_max
     below n, head on and off, every-chain and axis-symmetric nodes, fixed candidates; every
