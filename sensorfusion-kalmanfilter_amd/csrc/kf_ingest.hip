@@ -391,15 +391,18 @@ int hip_err(hipError_t e, const char* what) {
 // per device, grown on demand and kept for the process, so a call allocates nothing after the
 // first of its size (hipMalloc / hipFree would synchronise the device on every call).  The call
 // is synchronous and holds the lock throughout, so one buffer serves every stream.
-struct SelectScratch {
+// kf_events_select's scratch, one slot per device (each with its own lock, held through the
+// call: the next call on that device reuses the buffers)
+constexpr int kSelMaxDevices = 64;
+struct SelectSlot {
     std::mutex mu;
-    std::vector<int32_t*> counts;    // per device: the count pass's [kSelBlocks] block counts
-    std::vector<int32_t*> kept;      // per device: mapped, coherent host int the gather pass fills
-    std::vector<int32_t*> kept_dev;  // its device address
+    int32_t* counts = nullptr;    // the count pass's [kSelBlocks] block counts
+    int32_t* kept = nullptr;      // mapped, coherent host int the gather pass fills
+    int32_t* kept_dev = nullptr;  // its device address
 };
-SelectScratch& select_scratch() {
-    static SelectScratch s;
-    return s;
+SelectSlot& select_slot(int dev) {
+    static SelectSlot slots[kSelMaxDevices];
+    return slots[dev];
 }
 }  // namespace
 
@@ -599,14 +602,10 @@ int kf_events_select(int64_t n, const uint8_t* etype, const double* t, const dou
     hipStream_t st = static_cast<hipStream_t>(stream);
     int dev = 0;
     KF_TRY(hipGetDevice(&dev), "kf_events_select device");
-    SelectScratch& sc = select_scratch();
+    if (dev < 0 || dev >= kSelMaxDevices) return set_error(KF_EINVAL, "kf_events_select: device %d", dev);
+    SelectSlot& sc = select_slot(dev);
     std::lock_guard<std::mutex> lock(sc.mu);  // held to the end: the scratch is reused by the next call
-    if (sc.counts.size() <= size_t(dev)) {
-        sc.counts.resize(dev + 1, nullptr);
-        sc.kept.resize(dev + 1, nullptr);
-        sc.kept_dev.resize(dev + 1, nullptr);
-    }
-    if (!sc.counts[dev]) {
+    if (!sc.counts) {
         void *c = nullptr, *p = nullptr, *pd = nullptr;
         hipError_t e = hipMalloc(&c, sizeof(int32_t) * kSelBlocks);
         if (e == hipSuccess) e = hipHostMalloc(&p, sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent);
@@ -616,23 +615,23 @@ int kf_events_select(int64_t n, const uint8_t* etype, const double* t, const dou
             if (p) (void)hipHostFree(p);
             return set_error(KF_EHIP, "kf_events_select workspace: %s", hipGetErrorString(e));
         }
-        sc.counts[dev] = static_cast<int32_t*>(c);
-        sc.kept[dev] = static_cast<int32_t*>(p);
-        sc.kept_dev[dev] = static_cast<int32_t*>(pd);
+        sc.counts = static_cast<int32_t*>(c);
+        sc.kept = static_cast<int32_t*>(p);
+        sc.kept_dev = static_cast<int32_t*>(pd);
     }
     // blocks of a multiple of the tile, at most kSelBlocks of them, none empty
     const int64_t tiles = (n + kSelTile - 1) / kSelTile;
     const int64_t per_block = ((tiles + kSelBlocks - 1) / kSelBlocks) * kSelTile;
     const unsigned blocks = static_cast<unsigned>((n + per_block - 1) / per_block);
     const uint8_t ty = static_cast<uint8_t>(keep_type);
-    *sc.kept[dev] = -1;
-    select_count_kernel<<<blocks, kIngBlock, 0, st>>>(n, per_block, etype, ty, sc.counts[dev]);
+    *sc.kept = -1;
+    select_count_kernel<<<blocks, kIngBlock, 0, st>>>(n, per_block, etype, ty, sc.counts);
     KF_TRY(hipGetLastError(), "kf_events_select count");
-    select_gather_kernel<<<blocks, kIngBlock, 0, st>>>(n, per_block, etype, ty, sc.counts[dev], t, payload, t_out,
-                                                       payload_out, src_out, sc.kept_dev[dev]);
+    select_gather_kernel<<<blocks, kIngBlock, 0, st>>>(n, per_block, etype, ty, sc.counts, t, payload, t_out,
+                                                       payload_out, src_out, sc.kept_dev);
     KF_TRY(hipGetLastError(), "kf_events_select gather");
     KF_TRY(hipStreamSynchronize(st), "kf_events_select sync");
-    const int32_t k = *sc.kept[dev];
+    const int32_t k = *sc.kept;
     if (k < 0 || k > n) return set_error(KF_EHIP, "kf_events_select: no count came back (%d)", k);
     *n_kept = k;
     return KF_OK;
