@@ -60,7 +60,7 @@ def test_bench_world_mismatch_exits_nonzero():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('config', ['3', 'ref15', 'sched', 'bf'])
+@pytest.mark.parametrize('config', ['3', '4', '2', '5', 'ref15', 'sched', 'bf'])
 def test_bench_two_ranks_on_the_gpu(config):
     """`python bench.py --gpus 2` end to end on the GPU box, started as a fresh child process:
     two ranks (gloo: they share the box's one GPU; the 8-GPU node's run is RCCL), each owning
