@@ -28,7 +28,10 @@ SURVEY.md §8f rows on the same engine (not BASELINE lines):
            IMU + 10 Hz GPS stream (kf_run_events)
     ref15f32  the same in fp32
     bf     the reference's brute-force search: every k-subset (k = 1..25) of n = 25 candidate
-           events (kf_workers.py:2311), 2^25 - 1 filters (kf_eval_combos)
+           events (kf_workers.py:2311), 2^25 - 1 subsets, one kf_search_combos call; value in
+           subsets/s.  N > 1: ONE search split by subset class over the ranks (strong scaling)
+    bf40   the same over the reference's n = 40 window (kf_workers_visualizing.py:2293, 2340),
+           2^40 - 1 subsets as 256 class searches (--steps 1 --warmup 1: ~20 s a search)
     sched  the rate-decimated greedy scheduled filter, B=1,048,576, rates 10..120 Hz
            (--rate-block 1: every lane its own rate)
 Rank 0 prints ONE JSON line.  --dist-backend gloo (rehearsal only) lets N ranks share one GPU
@@ -76,6 +79,9 @@ CONFIGS = {
     'ref15': dict(model='ref15', dtype='f64', B=1048576, T=256, dt=0.005, k=20),
     'ref15f32': dict(model='ref15', dtype='f32', B=1048576, T=256, dt=0.005, k=20),
     'bf': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=True),
+    # the reference's visualizing window (kf_workers_visualizing.py:2293, 2340): 2^40 - 1 subsets as
+    # class searches (ref15.search_class_width); one search takes seconds, hence the step counts
+    'bf40': dict(model='ref15', dtype='f64', n=40, chunk=1 << 22, search=True, steps=1, warmup=1),
     'bf_subsets': dict(model='ref15', dtype='f64', n=25, chunk=1 << 22, search=False),
     # payload records of 10 doubles carry the event time at rec[9] (KF_OPT_SCHED_REC_TIME; bench.py
     # fills it): 4.52 vs 4.82 ms in-process with 12-double records (profiles/r04_ab1/ab_sched.log),
@@ -819,16 +825,19 @@ def dead_reckoning_workload(cfg, args, dev, stream, ingest_s):
                                          'sample': f'{len(st)} IMU events, oracle/ref_kf.run_dead_reckoning_8state, '
                                                    f'NumPy {np.__version__}'}}
 
-    # select (etype in, t + payload of the kept events out, their positions), dt pass (t in; dt,
-    # etype out), filter (etype, dt, payload in; trajectory out): bytes per IMU event
-    per_event = (N * 1 + T * (8 + 72 + 4)) / T + (8 + 8 + 1) + (1 + 8 + 72 + 8 * 3)
+    # select (etype read by its count and its gather pass; t + payload of the kept events read and
+    # written; no positions: src_out is NULL), dt pass (t in; dt, etype out), filter (etype, dt,
+    # payload in; trajectory out): bytes per IMU event
+    per_event = (2 * N * 1) / T + 2 * (8 + 72) + (8 + 8 + 1) + (1 + 8 + 72 + 8 * 3)
     csv_s, ingest_first_s, ingest_s2 = ingest_s
     return dict(step=step, units=T, bytes=per_event * T, bytes_per_unit=per_event,
                 kernel='kf_events_select + kf_events_dt + kf_run_stream (ref_chain_kernel<f64,M8,stream> map pass and '
                        'stream_* kernels)',
                 traffic=None, cpu=cpu, gather=None, kf=kf,
                 roofline_note='latency / issue-bound like config 1 (the map pass runs its chunk length of events in '
-                              'sequence); the compaction\'s count is read back by the host once per step',
+                              'sequence); the compaction\'s count is read back by the host once per step; bytes: '
+                              'the select reads etype twice over the stream and reads + writes the kept events\' '
+                              't and payload (2 x 80 B), the dt pass 17 B, the filter 105 B per IMU event',
                 desc=f'hw5_2.run_dead_reckoning_for_IMU (hw5_2.py:382-436): ONE 8-state filter over the {T} IMU events '
                      f'of a whole drive log ({N} merged events, {stream.n_fixes} fixes skipped), f64; IMU events '
                      f'compacted on the device, time-parallel (kf_run_stream); synthetic log with the reference '
@@ -950,37 +959,53 @@ def sched_workload(cfg, args, rank, world, dev):
                        'payload': 'rows' if rows else f'records of {rec}'})
 
 
+VALU_PEAK = 1024 * 2.4e9 / 4   # wave64 VALU instructions/s: 1024 SIMDs, 4 cycles each, 2.4 GHz
+
+
+def bf_plan(n, world, sym, mem_bytes=32 << 30):
+    """The class split of the bf rows' search: one call (w = 0) when every size fits, otherwise
+    ref15.search_class_width; N > 1 at least 4 classes per rank (kfmi.dist.search_classes)."""
+    from kfmi import dist as kdist
+    from kfmi import ref15 as r15
+    return kdist.search_classes(n, world, 'f64', mem_bytes, sym) if world > 1 else \
+        r15.search_class_width(n, 'f64', mem_bytes, sym)
+
+
+def bf_level_bytes(n, w, sym):
+    """Level-buffer bytes of one class search of n - w free candidates: every stored node (the
+    C(m-2, k) subsets of size k whose largest free candidate is <= m - 3) written once and read
+    once as a parent; the one-launch head (sizes 1 .. K) stores only its level K, and the end
+    launch (sizes k_end .. m) reads level k_end - 1 and stores none."""
+    from kfmi.ref15 import search_level_bytes, search_stored_levels
+    m = n - w
+    return 2 * sum(search_level_bytes(math.comb(m - 2, k), 'f64', sym) for k in search_stored_levels(m))
+
+
 def bf_workload(cfg, args, rank, world, dev):
-    """Exhaustive brute-force search (kf_workers.py:1218-1392 without the early exit): every
-    k-subset, k = 1..n, of n candidate events after a warm start, through kf_eval_combos.  Each
-    rank runs the whole search (weak scaling: the same search per GPU)."""
+    """Exhaustive brute-force search (kf_workers.py:1218-1392 without the early exit: R_threshold
+    below every subset's score, the reference's longest search, :1391-1392): every k-subset,
+    k = 1..n, of n candidate events after a warm start.  search: the shared-prefix search
+    (kf_search_combos), one call or 2^w class calls; N > 1, ONE search split by class over the
+    ranks with search_winner's all-reduces in the timed step (strong scaling; replaces the
+    reference's Pool(30) fan-out, :1320-1346).  bf_subsets: one filter per subset
+    (kf_eval_combos), each rank the whole search.  value = subsets/s; the reference-equivalent
+    steps (k events + the final predict per k-subset) are a secondary key."""
     import kfmi
+    from kfmi import dist as kdist
+    from kfmi import ref15 as r15
     n, chunk = cfg['n'], cfg['chunk']
     ev, init, Pw, t0, t_end = bf_events(n)
-    width = min(chunk, max(math.comb(n, k) for k in range(1, n + 1)))
-    kf = kfmi.BatchedKF('ref15', width, 'f64', device=dev.index)
     total_combos = 2 ** n - 1
-    total_steps = sum(math.comb(n, k) * (k + 1) for k in range(1, n + 1))
-    launches = [(k, off) for k in range(1, n + 1) for off in range(0, math.comb(n, k), width)]
+    ref_steps = sum(math.comb(n, k) * (k + 1) for k in range(1, n + 1))
     search = cfg['search']
-    if search:
-        kf.close()
-        kf = kfmi.BatchedKF('ref15', 1, 'f64', device=dev.index, options=cfg.get('opts'))
-
-    def step():
-        if search:
-            # R_threshold below every subset's score: the reference's longest search (every
-            # size, kf_workers.py:1391-1392); one kf_search_combos call, levels 1..n
-            kf.search_combos(ev, init, t0, t_end, -1e30, exhaustive=True)
-            return
-        for k, off in launches:
-            kf.eval_combos(ev, init, t0, t_end, k, combo_offset=off, logdets=False)
 
     def cpu():
         """The reference worker's per-subset filter (kf_workers.py:22-97) restated in C
         (oracle/cpu_kf.c, dense 15x15): the 12-subsets of the candidates as event streams (k
         events + the final predict), OpenMP over subsets on this host's allotted cores, ~10 s;
-        plus the worker's NumPy loop (oracle/ref_kf.evaluate_combo_chunk) on 1 core, ~3 s."""
+        plus the worker's NumPy loop (oracle/ref_kf.evaluate_combo_chunk) on 1 core, ~3 s.
+        value = the worker's subsets/s at this search's mean subset (ref_steps / 2^n - 1 steps):
+        KF steps/s x (2^n - 1) / ref_steps."""
         from itertools import combinations, islice
         from oracle import cpu_kf, ref_kf
         nth = cpu_kf.threads()
@@ -1014,91 +1039,150 @@ def bf_workload(cfg, args, rank, world, dev):
         shards = [dict(cand=cand, k=kk, lo=r * per, n=per, x0=np.zeros(15), P0=Pw, t0=t0, t_end=t_end)
                   for r in range(nth)]
         npl = numpy_pool.run('bf', shards, seconds=3.0)
-        return {'value': done * (kk + 1) / el, 'unit': 'KF steps/s', 'combinations_per_s': done / el, 'cores': nth,
+        steps_s = done * (kk + 1) / el
+        per_subset = ref_steps / total_combos
+        return {'value': steps_s / per_subset, 'unit': 'subsets/s', 'kf_steps_per_s': steps_s,
+                'steps_per_subset': per_subset, 'combinations_per_s': done / el, 'cores': nth,
                 'kind': 'port', 'sample': f'{done} {kk}-subsets of the {n} candidates as event streams through '
                                           f'oracle/cpu_kf.c (the reference step, dense 15x15, C -O3 OpenMP) on '
-                                          f'{nth} threads, {host_cpu()}', 'seconds': round(el, 2),
+                                          f'{nth} threads, {host_cpu()}; value = its KF steps/s / {per_subset:.2f}, '
+                                          f'the reference worker\'s steps per subset of this search',
+                'seconds': round(el, 2),
                 'numpy_reference_loop': dict(npl, combinations_per_s=npl['value'] / (kk + 1),
+                                             subsets_per_s=npl['value'] / per_subset,
                                              sample=f"{npl['filters']} {kk}-subsets, oracle/ref_kf."
                                                     f"evaluate_combo_chunk (kf_workers.py:22-97) in a spawn Pool of "
                                                     f"{npl['cores']} processes, NumPy {np.__version__}")}
 
+    if not search:
+        width = min(chunk, max(math.comb(n, k) for k in range(1, n + 1)))
+        kf = kfmi.BatchedKF('ref15', width, 'f64', device=dev.index)
+        launches = [(k, off) for k in range(1, n + 1) for off in range(0, math.comb(n, k), width)]
+
+        def step():
+            for k, off in launches:
+                kf.eval_combos(ev, init, t0, t_end, k, combo_offset=off, logdets=False)
+        return dict(step=step, units=total_combos, unit='subsets/s', ref_steps=ref_steps, bytes=None,
+                    bytes_per_unit=None, kernel='ref15_combo_kernel', traffic=None, cpu=cpu, gather=None, kf=kf,
+                    combos=total_combos,
+                    desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '
+                         f'all 2^{n}-1 subsets, reference 15-state model, f64, {len(launches)} kf_eval_combos launches '
+                         f'(one filter per subset; each rank the whole search)',
+                    extra={'candidate_events': n, 'combinations': total_combos, 'launch_width': width})
+
+    kf = kfmi.BatchedKF('ref15', 1, 'f64', device=dev.index, options=cfg.get('opts'))
+    sym = kf.search_plan(init, n, k_max=1)['sym']
+    w = bf_plan(n, world, sym)
+    mine = kdist.rank_classes(w, rank, world) if world > 1 else r15.class_order(w)
+
+    def search_class(nf, c, k_max):
+        k, idx, _, _ = kf.search_combos(ev, init, t0, t_end, -1e30, k_max=k_max, exhaustive=True, n_fixed=nf,
+                                        fixed_mask=c)
+        return k, idx
+
+    def step():
+        # R_threshold below every subset's score: every size of every class (no early exit)
+        if world > 1:
+            kdist.search_winner(search_class, n, w, exhaustive=True)
+        elif w == 0:
+            kf.search_combos(ev, init, t0, t_end, -1e30, exhaustive=True)
+        else:
+            r15.class_search(search_class, n, w, mine, exhaustive=True)
+
     def dist_check():
-        """N > 1, after the timed region: the search sharded by subset class across the ranks
-        (kfmi.dist.search_winner, the reduction brute_force_search uses: MIN of the first
-        accepted size, MAX of the bit-reversed winner mask; acceptance counts summed), at a
-        threshold that accepts 2 % of the subsets, against rank 0's own one-rank search of the
-        same candidates.  Replaces the reference's Pool(30) fan-out (kf_workers.py:1320-1346)."""
+        """N > 1, after the timed region: the reference's search (not exhaustive: it stops at the
+        first accepted size, kf_workers.py:1325-1371) sharded by class across the ranks
+        (kfmi.dist.search_winner: MIN of the first accepted size, MAX of the bit-reversed winner
+        mask) against rank 0's own one-GPU search of the same candidates, at a threshold that
+        accepts no single event (the winner has two or more); n <= 25 also exhaustive, with
+        every size's acceptance count summed over the ranks."""
         import torch.distributed as tdist
-        from kfmi import dist as kdist
         thr = torch.tensor([float('-inf')], dtype=torch.float64)
         if rank == 0:
-            _, _, _, sm = kf.search_combos(ev, init, t0, t_end, -1e30, exhaustive=True, subset_max=True)
-            vals = torch.sort(sm[torch.isfinite(sm)]).values
-            thr[0] = float(vals[len(vals) // 50]) + 1e-9
-            del sm, vals
+            ones = kf_one.eval_combos(ev, init, t0, t_end, 1, logdets=False)[0][:n]
+            L0 = float(np.linalg.slogdet(Pw)[1])
+            thr[0] = (L0 + float(ones.min())) / 2
         thr = thr.to(kdist._tdev())
         tdist.all_reduce(thr, op=tdist.ReduceOp.MAX)
         thr = float(thr.item())
-        w = kdist.search_classes(n, world)
-        acc = np.zeros(n + 1, dtype=np.int64)
 
-        def search_class(n_fixed, fixed_mask):
-            k, idx, a, _ = kf.search_combos(ev, init, t0, t_end, thr, k_max=n, exhaustive=True, n_fixed=n_fixed,
-                                            fixed_mask=fixed_mask)
-            acc[:] += a.astype(np.int64)
+        def search_thr(nf, c, k_max, exhaustive=False, acc=None):
+            k, idx, a, _ = kf.search_combos(ev, init, t0, t_end, thr, k_max=k_max, exhaustive=exhaustive, n_fixed=nf,
+                                            fixed_mask=c)
+            if acc is not None:
+                acc[:len(a)] += a.astype(np.int64)
             return k, idx
-        won = kdist.search_winner(search_class, n, w)
-        total = kdist.sum_counts(acc)
+        won = kdist.search_winner(search_thr, n, w)
         out = {'threshold': thr, 'classes': 1 << w, 'k_found': won[0] if won else 0,
-               'winner': list(won[1]) if won else None, 'accepted_per_size': [int(v) for v in total]}
+               'winner': list(won[1]) if won else None}
+        acc_t = None
+        if n <= 25:
+            acc = np.zeros(n + 1, dtype=np.int64)
+            won_x = kdist.search_winner(lambda nf, c, k_max: search_thr(nf, c, k_max, True, acc), n, w,
+                                        exhaustive=True)
+            acc_t = [int(v) for v in kdist.sum_counts(acc)]
+            out['exhaustive'] = {'k_found': won_x[0] if won_x else 0, 'winner': list(won_x[1]) if won_x else None,
+                                 'accepted_per_size': acc_t}
         if rank == 0:
-            k1, idx1, acc1, _ = kf.search_combos(ev, init, t0, t_end, thr, exhaustive=True)
-            out['one_rank'] = {'k_found': k1, 'winner': list(idx1) if idx1 else None,
-                               'accepted_per_size': [int(v) for v in acc1]}
-            out['one_rank_equal'] = (out['k_found'] == k1 and out['winner'] == out['one_rank']['winner']
-                                     and out['accepted_per_size'] == out['one_rank']['accepted_per_size'])
-            if not out['one_rank_equal']:
+            w1 = r15.search_class_width(n, 'f64', 32 << 30, sym)
+            k1, idx1, acc1, _ = r15.search_combos_classed(kf, ev, init, t0, t_end, thr, w1)
+            out['one_rank'] = {'k_found': k1, 'winner': list(idx1) if idx1 else None, 'classes': 1 << w1}
+            ok = out['k_found'] == k1 and out['winner'] == out['one_rank']['winner']
+            if acc_t is not None:
+                kx, idxx, accx, _ = r15.search_combos_classed(kf, ev, init, t0, t_end, thr, w1, exhaustive=True)
+                out['one_rank']['accepted_per_size'] = [int(v) for v in accx]
+                ok = ok and acc_t == out['one_rank']['accepted_per_size'] and \
+                    out['exhaustive']['winner'] == (list(idxx) if idxx else None)
+            out['one_rank_equal'] = ok
+            if not ok:
                 raise SystemExit(f'the {world}-rank search disagrees with the one-rank search: {out}')
         return out
 
-    if search:
-        from kfmi.ref15 import search_end_size, search_level_bytes, search_stored_levels
-        step()  # how the library runs this search (kf_search_info): axis-symmetric, head, launches
-        torch.cuda.synchronize(dev)
-        info = kf.search_info()
-        K, sym = info['head_sizes'], info['sym']
-        launches = info['level_launches'] + (1 if K else 0)
-        k_end = search_end_size(n)
-        # every stored node (the C(n-2, k) subsets of size k whose largest candidate is <= n - 3)
-        # is written once and read once as a parent; the one-launch head (sizes 1 .. K) stores only
-        # its level K, and the end launch (sizes k_end .. n) reads level k_end - 1 and stores none
-        lvl = sum(search_level_bytes(math.comb(n - 2, k), 'f64', sym) for k in search_stored_levels(n))
-        chains = ('axis-symmetric: one pva and one aw chain computed and stored for the three of each, '
-                  'KF_OPT_AXIS_SYM' if sym else 'every chain')
-        return dict(step=step, units=total_steps, bytes=2 * lvl, bytes_per_unit=2 * lvl / total_combos,
-                    kernel=f'ref15_search_head_kernel (sizes 1..{K}) + ref15_search_cm/pm_kernel + '
-                           f'ref15_search_end_kernel (sizes {k_end}..{n}) (the {launches} launches of one search)',
-                    traffic=load_traffic('bf', 2 * lvl), valu=load_valu('bf') if load_traffic('bf', 2 * lvl) else None,
-                    cpu=cpu,
-                    gather=None, dist_check=dist_check, kf=kf, combos=total_combos,
-                    roofline_note='level-buffer bytes only (each stored prefix filter written and read once, the '
-                                  'subsets holding candidate n-2 scored from registers); the search is fp64 issue / '
-                                  'latency-bound (one event step, the final predict, two log-dets per subset; '
-                                  'DESIGN.md §3)',
-                    desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '
-                         f'all 2^{n}-1 subsets, reference 15-state model, f64, shared-prefix search '
-                         f'(kf_search_combos: one event step + final predict per subset, sizes 1..{K} in one '
-                         f'launch, then one launch per level, sizes {k_end}..{n} in one: {launches} launches; '
-                         f'{chains}); '
-                         f'value counts the reference-equivalent steps (k events + final predict per k-subset)',
-                    extra={'candidate_events': n, 'combinations': total_combos, 'levels': n, 'search': info})
-    return dict(step=step, units=total_steps, bytes=None, bytes_per_unit=None, kernel='ref15_combo_kernel',
-                traffic=None, cpu=cpu, gather=None, kf=kf, combos=total_combos,
-                desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events (kf_workers.py:2311), '
-                     f'all 2^{n}-1 subsets, reference 15-state model, f64, {len(launches)} kf_eval_combos launches '
-                     f'(one filter per subset)',
-                extra={'candidate_events': n, 'combinations': total_combos, 'launch_width': width})
+    kf_one = kfmi.BatchedKF('ref15', 64, 'f64', device=dev.index) if world > 1 else None  # scores of the 1-subsets
+    step()  # how the library runs this search (kf_search_info): axis-symmetric, head, launches (last class)
+    torch.cuda.synchronize(dev)
+    info = kf.search_info()
+    K, sym_ran = info['head_sizes'], info['sym']
+    assert sym_ran == sym, (sym_ran, sym)
+    m = n - w
+    launches = info['level_launches'] + (1 if K else 0)
+    k_end = r15.search_end_size(m)
+    classes_here = len(mine)
+    per_class = bf_level_bytes(n, w, sym)
+    lvl_bytes = per_class * classes_here
+    subsets_here = total_combos if world == 1 else sum(2 ** m for _ in mine) - (1 if 0 in mine else 0)
+    chains = ('axis-symmetric: one pva and one aw chain computed and stored for the three of each, '
+              'KF_OPT_AXIS_SYM' if sym else 'every chain')
+    cfg_id = 'bf' if n == 25 else f'bf{n}'
+    valu = load_valu(cfg_id)
+    valu_per_search = None
+    try:
+        with open(os.path.join(ROOT, 'profiles', 'pmc_valu.json')) as f:
+            rec = json.load(f).get(f'config{cfg_id}')
+        if rec and rec.get('classes', 1) == 1 << w:
+            valu_per_search = rec['counters_per_launch']['SQ_INSTS_VALU']
+    except (OSError, ValueError, KeyError):
+        pass
+    split = (f'{1 << w} classes of {m} free candidates (the subsets split by their intersection with candidates '
+             f'0..{w - 1}), {classes_here} on this rank, each a kf_search_combos call' if w else 'one kf_search_combos call')
+    return dict(step=step, units=total_combos, unit='subsets/s', ref_steps=ref_steps, strong=world > 1,
+                bytes=lvl_bytes, bytes_per_unit=lvl_bytes / subsets_here,
+                valu_per_launch=valu_per_search if world == 1 else None,
+                kernel=f'ref15_search_head_kernel (sizes 1..{K}) + ref15_search_cm/pm_kernel + '
+                       f'ref15_search_end_kernel (sizes {k_end}..{m}) ({launches} launches per class search)',
+                traffic=load_traffic(cfg_id, lvl_bytes), valu=valu if world == 1 else None,
+                cpu=cpu, gather=None, dist_check=dist_check if world > 1 else None, kf=kf, combos=total_combos,
+                roofline_note='fp64 VALU issue: wave64 VALU instructions of one search (rocprofv3 SQ_INSTS_VALU, '
+                              'profiles/pmc_valu.json) / its time, against 1024 SIMDs x 2.4 GHz / 4 cycles; the '
+                              'level buffers (each stored prefix filter written and read once) are the hbm entry',
+                desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events '
+                     f'({"kf_workers.py:2311" if n == 25 else "kf_workers_visualizing.py:2293, 2340"}), '
+                     f'all 2^{n}-1 subsets, reference 15-state model, f64, shared-prefix search (one event step + '
+                     f'final predict per subset, sizes 1..{K} in one launch, then one launch per level, sizes '
+                     f'{k_end}..{m} in one: {launches} launches per class search; {chains}); {split}; '
+                     f'value = subsets/s of ONE search' + (f' split over {world} ranks' if world > 1 else ''),
+                extra={'candidate_events': n, 'combinations': total_combos, 'levels': n, 'search': info,
+                       'classes': 1 << w, 'classes_this_rank': classes_here, 'free_candidates_per_class': m})
 
 
 def _free_port():
@@ -1151,8 +1235,8 @@ def launch_check(world, rank):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--steps', type=int, default=None, help='timed steps (default 20; bf40: 1)')
+    ap.add_argument('--warmup', type=int, default=None, help='untimed steps (default 10; bf40: 1)')
     ap.add_argument('--config', default='3', choices=sorted(CONFIGS))
     ap.add_argument('--batch', type=int, default=None, help='override filters per GPU')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -1222,6 +1306,8 @@ def main():
     dev = torch.device('cuda', local)
 
     cfg = dict(CONFIGS[args.config])
+    args.steps = cfg.get('steps', 20) if args.steps is None else args.steps
+    args.warmup = cfg.get('warmup', 10) if args.warmup is None else args.warmup
     if args.batch:
         cfg['B'] = args.batch
     cfg['opts'] = dict(cfg.get('opts', {}))
@@ -1234,7 +1320,7 @@ def main():
         w = ref15_workload(cfg, args, rank, world, dev)
     elif args.config == 'sched':
         w = sched_workload(cfg, args, rank, world, dev)
-    elif args.config in ('bf', 'bf_subsets'):
+    elif args.config in ('bf', 'bf40', 'bf_subsets'):
         w = bf_workload(cfg, args, rank, world, dev)
     else:
         w = cv_workload(args.config, cfg, args, rank, world, dev)
@@ -1297,24 +1383,45 @@ def main():
         if w.get('dist_check') is not None:
             dist_info = w['dist_check']()
 
+    # weak scaling: each rank its own units (filters); strong (the bf rows at N > 1): the ranks
+    # share one search, so the job's units are one search's
+    mult = 1 if w.get('strong') else world
     if rank == 0:
         rec = {
             'metric': 'KF predict+update steps/sec (batched filters)',
-            'value': world * w['units'] * args.steps / elapsed,
-            'unit': 'KF steps/s',
+            'value': mult * w['units'] * args.steps / elapsed,
+            'unit': w.get('unit', 'KF steps/s'),
             'n_gpus': world,
             'steps': args.steps,
             'warmup': args.warmup,
             'ms_per_step': elapsed / max(args.steps, 1) * 1e3,
             'higher_is_better': True,
-            'scaling': 'weak',
+            'scaling': 'strong' if w.get('strong') else 'weak',
             'vs_baseline': None,
             'dtype': cfg['dtype'],
             'data': 'synthetic (GPS+IMU streams per SURVEY.md §8d, generated on the GPU, resident in HBM)',
             'config': dict({'workload': w['desc'], 'parallelism': f'filter shards x{world} (no data-path collective)'},
                            **w['extra']),
         }
-        if w['bytes'] is not None:
+        if 'valu_per_launch' in w:
+            # the search rows: fp64 VALU issue is the roof, the level buffers' HBM
+            # bandwidth a secondary entry
+            hbm = w['bytes'] / (kern_ms * 1e-3) / 1e9
+            vp = w['valu_per_launch']
+            va = vp / (kern_ms * 1e-3) if vp else None
+            rec['hbm_gbs'] = hbm
+            rec['roofline'] = {'bound': 'valu', 'achieved': va, 'peak': VALU_PEAK, 'unit': 'wave-instr/s',
+                               'frac': va / VALU_PEAK if va else None, 'traffic': w['traffic'],
+                               'kernel': w['kernel'], 'kernel_ms': kern_ms, 'valu_instructions_per_launch': vp,
+                               'hbm': {'achieved': hbm, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                                       'frac': hbm / HBM_PEAK_GBS, 'algorithmic_bytes_per_launch': w['bytes'],
+                                       'algorithmic_bytes_per_subset': w['bytes_per_unit'],
+                                       'traffic': w['traffic']},
+                               'note': w['roofline_note'] + ('' if vp else '; no SQ_INSTS_VALU summary for this '
+                                                                          'split, achieved unmeasured')}
+            if w.get('valu'):
+                rec['roofline']['valu'] = w['valu']
+        elif w['bytes'] is not None:
             achieved = w['bytes'] / (kern_ms * 1e-3) / 1e9
             rec['hbm_gbs'] = achieved
             rec['roofline'] = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
@@ -1342,7 +1449,11 @@ def main():
             rec['predict_steps_per_s'] = rec['value']
             rec['update_steps_per_s'] = world * (w['units'] // w['update_every']) * args.steps / elapsed
         if 'combos' in w:
-            rec['combinations_per_s'] = world * w['combos'] * args.steps / elapsed
+            rec['combinations_per_s'] = mult * w['combos'] * args.steps / elapsed
+        if 'ref_steps' in w:
+            # the steps the reference's worker would run for the same subsets (k events + the final
+            # predict per k-subset, kf_workers.py:22-97): the search shares prefixes instead
+            rec['reference_equivalent_steps_per_s'] = mult * w['ref_steps'] * args.steps / elapsed
         rec['failed_filters'] = bad
         if args.ablate != 'none':
             rec['ablation'] = args.ablate + ' (diagnostic run: NOT the benchmark workload)'

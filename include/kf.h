@@ -399,6 +399,16 @@ int kf_search_combos(kf_batch* handle, int n_events, const double* events, const
                      int n_fixed, uint64_t fixed_mask, uint64_t* winner, int* k_found,
                      uint64_t* n_accepted, void* subset_max, void* stream);
 
+/* How kf_search_combos would run with these arguments, without running it (no device work):
+ * out[0] = 1 if axis-symmetric (KF_OPT_AXIS_SYM and init's axis blocks equal bit for bit),
+ * out[1] = the workspace bytes it needs (two buffers of the widest stored level plus 4 KiB),
+ * out[2] = the widest stored level's nodes, out[3] = the most stored parents of a level,
+ * out[4] = the first size over the 2^28-parent cap (0 = none; kf_search_combos refuses it).
+ * The host uses it to split a search too large for one call into classes (n_fixed /
+ * fixed_mask) run one after another (kfmi.ref15.search_combos_classed). */
+int kf_search_plan(const kf_batch* handle, int n_events, const double* init, int n_fixed, uint64_t fixed_mask,
+                   int k_max, int64_t* out);
+
 /* The last kf_search_combos on this handle: out[0] = 1 if it ran axis-symmetric
  * (KF_OPT_AXIS_SYM: one pva and one aw chain for the three of each), out[1] = the sizes its
  * head launch covered (KF_OPT_SEARCH_HEAD; 0 = none), out[2] = its level launches after the
@@ -557,8 +567,10 @@ int kf_events_dt(int64_t n, const double* t, const uint8_t* etype_in, double pre
  * walks the IMU events alone, skipping every fix (hw5_2.py:402-404).  etype device [n], t device
  * [n], payload device [n][9] (kf_ingest's layout); writes the K kept events' t_out [K],
  * payload_out [K][9] and src_out [K] (their stream positions), each of which may be NULL, with
- * capacity n, and *n_kept = K (host).  Synchronous (the count is returned); its scratch (block counts, a
- * mapped host int) is per device, allocated by the first call, so later calls allocate nothing. */
+ * capacity n, and *n_kept = K (host).  Synchronous (the count is returned): inside a hipGraph
+ * capture it returns KF_EINVAL before queuing anything.  Its scratch (block counts, a mapped host
+ * int) is per device, allocated by the first call, so later calls allocate nothing; `stream` must
+ * belong to the current device (KF_EINVAL otherwise). */
 int kf_events_select(int64_t n, const uint8_t* etype, const double* t, const double* payload, int keep_type,
                      double* t_out, double* payload_out, int32_t* src_out, int64_t* n_kept, void* stream);
 

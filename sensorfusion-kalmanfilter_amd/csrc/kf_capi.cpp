@@ -1182,42 +1182,90 @@ int kf_eval_combos(kf_batch* h, int n_events, const double* events, const double
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_eval_combos");
 }
 
+namespace {
+// kf_search_combos' shape for (n_events, n_fixed, fixed_mask, k_max): the free levels it
+// searches, whether it runs axis-symmetric, its widest stored level, the first level over the
+// parent cap (0 = none) and its workspace bytes.  Free levels 1 .. kf_max - 1 are stored, and
+// of each only the subsets whose largest free candidate is <= n - 3 (the colex ranks below
+// C(n - 2, k)): a subset holding candidate n - 1 has no children, and one holding n - 2 (but not
+// n - 1) has the single child that adds n - 1, which the launch creating it scores from
+// registers (Ref15SearchArgs::tail).
+struct SearchShape {
+    int n = 0, k_base = 0, kf_max = 0, over_cap = 0;
+    bool sym = false;
+    uint64_t widest = 0, max_par = 0;
+    size_t level = 0, need = 0;
+};
+constexpr size_t kSearchHeadBytes = 4096;  // best[65], n_acc[65]
+
+int search_shape(const kf_batch* h, int n_events, const double* init, int n_fixed, uint64_t fixed_mask, int k_max,
+                 const char* who, SearchShape* s) {
+    if (n_fixed < 0 || n_fixed >= n_events)
+        return fail(KF_EINVAL, "%s: n_fixed = %d outside [0, %d)", who, n_fixed, n_events);
+    if (n_fixed < 64 && (fixed_mask >> n_fixed) != 0)
+        return fail(KF_EINVAL, "%s: fixed_mask has bits at or above n_fixed = %d", who, n_fixed);
+    s->k_base = __builtin_popcountll(fixed_mask);
+    s->n = n_events - n_fixed;  // free candidates
+    if (k_max <= s->k_base || k_max > n_events)
+        return fail(KF_EINVAL, "%s: k_max = %d outside [%d, %d]", who, k_max, s->k_base + 1, n_events);
+    const int n = s->n;
+    s->kf_max = k_max - s->k_base < n ? k_max - s->k_base : n;  // free levels searched
+    const uint64_t* binom = binom_table();
+    auto C = [&](int a, int b) { return binom[a * (kMaxComboEvents + 1) + b]; };
+    for (int k = 1; k < s->kf_max; ++k) s->widest = n >= 2 && C(n - 2, k) > s->widest ? C(n - 2, k) : s->widest;
+    for (int k = 2; k <= s->kf_max && n >= 2; ++k) {
+        const uint64_t par = C(n - 2, k - 1);
+        s->max_par = par > s->max_par ? par : s->max_par;
+        if (!s->over_cap && par >= (1ull << 28)) s->over_cap = k;
+    }
+    s->sym = search_sym(h, init);
+    s->level = s->widest ? static_cast<size_t>(kfmi::search_level_bytes(s->widest, elem(h), s->sym)) : 0;
+    s->need = kSearchHeadBytes + 2 * s->level;
+    return KF_OK;
+}
+}  // namespace
+
+int kf_search_plan(const kf_batch* h, int n_events, const double* init, int n_fixed, uint64_t fixed_mask, int k_max,
+                   int64_t* out) {
+    if (int rc = check_handle(h)) return rc;
+    if (h->model != KF_MODEL_REF15) return fail(KF_EINVAL, "kf_search_plan: needs a KF_MODEL_REF15 handle");
+    if (n_events < 1 || n_events > kMaxComboEvents)
+        return fail(KF_EINVAL, "kf_search_plan: n_events = %d outside [1, %d]", n_events, kMaxComboEvents);
+    if (!init || !out) return fail(KF_EINVAL, "kf_search_plan: null init/out");
+    SearchShape s;
+    if (int rc = search_shape(h, n_events, init, n_fixed, fixed_mask, k_max, "kf_search_plan", &s)) return rc;
+    out[0] = s.sym;
+    out[1] = static_cast<int64_t>(s.need);
+    out[2] = static_cast<int64_t>(s.widest);
+    out[3] = static_cast<int64_t>(s.max_par);
+    out[4] = s.over_cap;
+    return KF_OK;
+}
+
 int kf_search_combos(kf_batch* h, int n_events, const double* events, const double* init, double prev_time,
                      double target_end, double threshold, int k_max, int exhaustive, int n_fixed,
                      uint64_t fixed_mask, uint64_t* winner, int* k_found, uint64_t* n_accepted, void* subset_max,
                      void* stream) {
     if (int rc = check_handle(h)) return rc;
     if (int rc = check_combo_inputs(h, n_events, events, init, "kf_search_combos")) return rc;
-    if (n_fixed < 0 || n_fixed >= n_events)
-        return fail(KF_EINVAL, "kf_search_combos: n_fixed = %d outside [0, %d)", n_fixed, n_events);
-    if (n_fixed < 64 && (fixed_mask >> n_fixed) != 0)
-        return fail(KF_EINVAL, "kf_search_combos: fixed_mask has bits at or above n_fixed = %d", n_fixed);
-    const int k_base = __builtin_popcountll(fixed_mask);
-    const int n = n_events - n_fixed;  // free candidates
-    if (k_max <= k_base || k_max > n_events)
-        return fail(KF_EINVAL, "kf_search_combos: k_max = %d outside [%d, %d]", k_max, k_base + 1, n_events);
+    SearchShape shape;
+    if (int rc = search_shape(h, n_events, init, n_fixed, fixed_mask, k_max, "kf_search_combos", &shape)) return rc;
+    const int k_base = shape.k_base, n = shape.n, kf_max = shape.kf_max;
     if (!winner || !k_found) return fail(KF_EINVAL, "kf_search_combos: null winner/k_found");
     if (subset_max && n_events > 30)
         return fail(KF_EINVAL, "kf_search_combos: subset_max needs n_events <= 30 (2^n entries)");
-    const int kf_max = k_max - k_base < n ? k_max - k_base : n;  // free levels searched
     const uint64_t* binom = binom_table();
     auto C = [&](int a, int b) { return binom[a * (kMaxComboEvents + 1) + b]; };
-    // Free levels 1 .. kf_max - 1 are stored, and of each only the subsets whose largest free
-    // candidate is <= n - 3 (the colex ranks below C(n - 2, k)): a subset holding candidate n - 1
-    // has no children, and one holding n - 2 (but not n - 1) has the single child that adds
-    // n - 1, which the launch creating it scores from registers (Ref15SearchArgs::tail).
-    uint64_t widest = 0;
-    for (int k = 1; k < kf_max; ++k) widest = n >= 2 && C(n - 2, k) > widest ? C(n - 2, k) : widest;
-    for (int k = 2; k <= kf_max; ++k)
-        if (n >= 2 && C(n - 2, k - 1) >= (1ull << 28))
-            return fail(KF_EINVAL, "kf_search_combos: level %d has C(%d, %d) = %llu parents (limit 2^28); lower k_max",
-                        k, n - 2, k - 1, static_cast<unsigned long long>(C(n - 2, k - 1)));
-    const int esz = static_cast<int>(elem(h));
-    const size_t head = 4096;  // best[65], n_acc[65]
-    const bool sym = search_sym(h, init);
-    const size_t level = widest ? static_cast<size_t>(kfmi::search_level_bytes(widest, esz, sym)) : 0;
+    if (shape.over_cap) {
+        const int k = shape.over_cap;
+        return fail(KF_EINVAL, "kf_search_combos: level %d has C(%d, %d) = %llu parents (limit 2^28); lower k_max",
+                    k, n - 2, k - 1, static_cast<unsigned long long>(C(n - 2, k - 1)));
+    }
+    const size_t head = kSearchHeadBytes;
+    const bool sym = shape.sym;
+    const size_t level = shape.level;
     int64_t launches = 0;
-    const size_t need = head + 2 * level;
+    const size_t need = shape.need;
     hipStream_t st = static_cast<hipStream_t>(stream);
     void* const ws_before = h->search_ws;
     if (!grow_ws(h, &h->search_ws, &h->search_ws_bytes, &h->search_ws_graph, need, st))

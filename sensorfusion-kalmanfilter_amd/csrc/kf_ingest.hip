@@ -387,12 +387,9 @@ int hip_err(hipError_t e, const char* what) {
     return set_error(KF_EHIP, "%s: %s (%d)", what, hipGetErrorString(e), static_cast<int>(e));
 }
 
-// kf_events_select's scratch (the kept positions, the count, hipCUB's temporaries): one buffer
-// per device, grown on demand and kept for the process, so a call allocates nothing after the
-// first of its size (hipMalloc / hipFree would synchronise the device on every call).  The call
-// is synchronous and holds the lock throughout, so one buffer serves every stream.
 // kf_events_select's scratch, one slot per device (each with its own lock, held through the
-// call: the next call on that device reuses the buffers)
+// call: the next call on that device reuses the buffers; hipMalloc / hipFree per call would
+// synchronise the device)
 constexpr int kSelMaxDevices = 64;
 struct SelectSlot {
     std::mutex mu;
@@ -600,8 +597,22 @@ int kf_events_select(int64_t n, const uint8_t* etype, const double* t, const dou
     if (!etype || (t_out && !t) || (payload_out && !payload))
         return set_error(KF_EINVAL, "kf_events_select: null etype, or an output without its input");
     hipStream_t st = static_cast<hipStream_t>(stream);
+    // the call synchronises the stream to return the count, so it cannot be captured: refuse
+    // before anything is queued into the caller's capture (kf_search_combos does the same)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    KF_TRY(hipStreamIsCapturing(st, &cap), "kf_events_select capture status");
+    if (cap != hipStreamCaptureStatusNone)
+        return set_error(KF_EINVAL, "kf_events_select: not capturable (the kept count returns to the host in the call)");
+    // the scratch belongs to the current device: the stream must be one of its streams
     int dev = 0;
     KF_TRY(hipGetDevice(&dev), "kf_events_select device");
+    if (st) {
+        int sdev = dev;
+        KF_TRY(hipStreamGetDevice(st, &sdev), "kf_events_select stream device");
+        if (sdev != dev)
+            return set_error(KF_EINVAL, "kf_events_select: the stream is on device %d, the current device is %d",
+                             sdev, dev);
+    }
     if (dev < 0 || dev >= kSelMaxDevices) return set_error(KF_EINVAL, "kf_events_select: device %d", dev);
     SelectSlot& sc = select_slot(dev);
     std::lock_guard<std::mutex> lock(sc.mu);  // held to the end: the scratch is reused by the next call

@@ -223,7 +223,8 @@ struct Ref15SearchArgs {
     double target_end;
     double threshold;        // acceptance: max log-det < threshold (kf_workers.py:1353)
     // the same test on the max's determinant (set_search_band): accepted below 2^lo_e lo_m,
-    // rejected above 2^hi_e hi_m, the log decides in between; mode 1 / 2: accept all / none
+    // rejected above 2^hi_e hi_m, the log decides in between; mode 1 / 2 / 3: accept all / a
+    // zero determinant only / none
     double band_lo_m, band_hi_m;
     int band_lo_e, band_hi_e, band_mode;
     const void* par;         // level k - 1 buffer (unused for k = 1)

@@ -2184,13 +2184,15 @@ __device__ __forceinline__ DetV<T> dmax(const DetV<T>& d, const DetV<T>& r) {
 template <typename T>
 struct DetBand {
     DetV<T> lo, hi;
-    int mode;  // 0: the band; 1: accept every valid determinant; 2: accept none
+    // 0: the band; 1: accept every valid determinant; 2: accept only a valid determinant that
+    // underflowed to 0 (log -inf, below any finite threshold); 3: accept none (-inf or NaN)
+    int mode;
     T thr;
     __device__ __forceinline__ explicit DetBand(const Ref15SearchArgs& a)
         : lo{T(a.band_lo_m), a.band_lo_e}, hi{T(a.band_hi_m), a.band_hi_e}, mode(a.band_mode), thr(T(a.threshold)) {}
     // d: a subset's max (valid, or NaN with kNanWins, which lies above hi)
     __device__ __forceinline__ bool accept(const DetV<T>& d) const {
-        if (mode != 0) return mode == 1 && d.valid();
+        if (mode != 0) return d.valid() && (mode == 1 || (mode == 2 && d.m == T(0)));
         if (lo.gt(d)) return true;
         if (d.gt(hi)) return false;
         return log_mant(d.m, d.e) < thr;
@@ -4011,9 +4013,10 @@ void set_search_band(Ref15SearchArgs& a, bool f64) {
     // mantissa T's rounding keeps far inside eps (a mantissa rounded up to 1 only makes the
     // kernels' (e, m) comparisons conservative)
     // |log det| of a 15 x 15 SPD matrix stays below 15 * 745 (every pivot is a finite double, a
-    // float's log below 15 * 104): beyond 1e5 the test accepts every valid determinant, or none
+    // float's log below 15 * 104): above 1e5 the test accepts every valid determinant; below
+    // -1e5 only one that underflowed to 0 (its log is -inf), and none at -inf or NaN
     const double t = f64 ? a.threshold : double(float(a.threshold));
-    a.band_mode = t == t ? (t > 1e5 ? 1 : (t < -1e5 ? 2 : 0)) : 2;
+    a.band_mode = t == t ? (t > 1e5 ? 1 : (t < -1e5 ? (t == -HUGE_VAL ? 3 : 2) : 0)) : 3;
     a.band_lo_m = a.band_hi_m = 1.0;
     a.band_lo_e = a.band_hi_e = 0;
     if (a.band_mode != 0) return;
@@ -4073,9 +4076,10 @@ hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStrea
 }
 
 hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream) {
-    // node offsets are 32-bit byte offsets (buffer voffset)
-    if (a.n_events > kMaxEvents || a.k < 1 || a.k > a.n_events || a.n_par == 0 || a.n_par >= (1ull << 28) ||
-        a.n_child >= (1ull << 28))
+    // the stored parents (kf_search_combos' cap); a level's children C(n, k) may be many more
+    // (n = 40, k = 10: 8.5e8): child ranks and node addresses are 64-bit, and only the children
+    // below C(n - 2, k) are stored
+    if (a.n_events > kMaxEvents || a.k < 1 || a.k > a.n_events || a.n_par == 0 || a.n_par >= (1ull << 28))
         return hipErrorInvalidValue;
     if (child_major) {
         // work items: per group v of parent blocks, blocks x (n - 1 - v) child events; group v

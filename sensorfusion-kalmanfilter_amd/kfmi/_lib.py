@@ -117,6 +117,7 @@ SIGNATURES = {
     'kf_eval_combos': (_i, [_vp, _i, _vp, _vp, _d, _d, _i, ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     'kf_search_combos': (_i, [_vp, _i, _vp, _vp, _d, _d, _d, _i, _i, _i, ctypes.c_uint64,
                               ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_i), _vp, _vp, _vp]),
+    'kf_search_plan': (_i, [_vp, _i, _vp, _i, ctypes.c_uint64, _i, _vp]),
     'kf_search_info': (_i, [_vp, _vp]),
     'kf_score_candidates': (_i, [_vp, _i, _vp, _i, _vp, _vp, _vp]),
     'kf_score_rows': (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp]),

@@ -105,14 +105,19 @@ def max_over_ranks(values, device, group=None):
 _NONE = (1 << 63) - 1
 
 
-def search_classes(n, world):
+def search_classes(n, world, dtype='f64', mem_bytes=32 << 30, sym=False):
     """Shard plan of the shared-prefix search over ``world`` ranks: the subsets are split by their
-    intersection with the first w candidates (2^w classes of 2^(n-w) subsets each), w the
-    smallest with 2^w >= 4 world (at most n - 1); class c goes to rank c % world.  Returns w."""
+    intersection with the first w candidates (2^w classes of 2^(n-w) subsets each), class c going
+    to rank c % world.  w = the larger of the rank rule (the smallest w with 2^w >= 4 world, at
+    most n - 1; 0 for one rank) and the memory rule (ref15.search_class_width: a class's every
+    size fits ``mem_bytes`` and the 2^28-parent cap), so no rank ever falls back to one filter
+    per subset.  Returns w."""
+    from . import ref15
     w = 0
-    while (1 << w) < 4 * world and w < n - 1:
-        w += 1
-    return w if world > 1 else 0
+    if world > 1:
+        while (1 << w) < 4 * world and w < n - 1:
+            w += 1
+    return max(w, ref15.search_class_width(n, dtype, mem_bytes, sym))
 
 
 def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, initial_pt=None, initial_state=None,
@@ -120,39 +125,37 @@ def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, init
                        finish=None, search_mem_bytes=32 << 30, consts=None):
     """run_brute_force_kalman_filter_no_sampling_min_usage sharded over the ranks of ``group``
     with the shared-prefix search (kf_search_combos): the subsets are split into 2^w classes by
-    their intersection with the first w candidates (``search_classes``); each rank searches its
-    classes, keeping per class the first size with an acceptable subset and its first such
-    subset in itertools order, and two all-reduces (MIN of the size, then MAX of the
-    bit-reversed subset mask at that size) pick the same winner as the single-GPU search.
-    Every rank returns the reference's result dict (or None).  Falls back to
-    ``brute_force_search_ranks`` when a class's levels would not fit in ``search_mem_bytes``.
+    their intersection with the first w candidates (``search_classes``: enough classes for the
+    ranks and small enough for one search call each); each rank searches its classes, keeping
+    the first size with an acceptable subset and its first such subset in itertools order, and
+    two all-reduces (MIN of the size, then MAX of the bit-reversed subset mask at that size) pick
+    the same winner as the single-GPU search.  Every rank returns the reference's result dict
+    (or None).  ``max_combos_in_memory`` is the reference's argument (unused: no per-subset batch).
 
-    ``search_class(n_fixed, fixed_mask) -> (k, indices or None)`` / ``finish(k, indices)``
+    ``search_class(n_fixed, fixed_mask, k_max) -> (k, indices or None)`` / ``finish(k, indices)``
     replace the GPU evaluation (tests drive the reduction logic with the CPU oracle on gloo).
     consts: a ref15.ModelConsts (the reference's constants by default)."""
-    import torch.distributed as dist
-
     from . import ref15
     if R_threshold is None:
         raise ValueError('R_threshold must be specified for brute force KF.')
-    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
     st = ref15.brute_force_setup(events, start_idx, end_idx, initial_pt, initial_state, consts)
     if st is None:
         return None
     cand, xt, Pt, prev_time, target_end, ev, init = st
     n = len(cand)
-    w = search_classes(n, world)
-    if search_class is None and ref15.search_levels(n - w, dtype, search_mem_bytes) < n - w:
-        return brute_force_search_ranks(events, start_idx, end_idx, R_threshold, initial_pt, initial_state,
-                                        max_combos_in_memory, dtype, device, group, consts=consts)
     kf = None
+    sym = False
     if search_class is None:
         kf = ref15.BatchedKF('ref15', 1, dtype, device=device, params=ref15._params(consts))
+        sym = kf.search_plan(init, n, k_max=1)['sym']
 
-        def search_class(n_fixed, fixed_mask):
-            k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=n,
+        def search_class(n_fixed, fixed_mask, k_max):
+            k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=k_max,
                                             n_fixed=n_fixed, fixed_mask=fixed_mask)
             return k, idx
+    w = search_classes(n, world, dtype, search_mem_bytes, sym)
     if finish is None:
         def finish(k, idx):
             return ref15.brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device,
@@ -170,22 +173,29 @@ def _tdev(group=None):
     return torch.device('cuda', torch.cuda.current_device()) if dist.get_backend(group) == 'nccl' else torch.device('cpu')
 
 
-def search_winner(search_class, n, w, group=None):
-    """The cross-rank half of ``brute_force_search``: this rank searches its classes c = rank,
-    rank + world, ... of the 2^w (``search_class(w, c) -> (k, indices or None)``), keeping the
-    smallest accepted size and, at it, the first subset in itertools.combinations order; two
-    all-reduces (MIN of the size, then MAX of the bit-reversed mask as two 32-bit halves) give
-    every rank the global winner (k, indices), or None when no class accepted a subset."""
+def rank_classes(w, rank, world):
+    """The classes rank searches: c = rank, rank + world, ... of the 2^w, fewest fixed members
+    first (ref15.class_order)."""
+    from . import ref15
+    return [c for c in ref15.class_order(w) if c % world == rank]
+
+
+def search_winner(search_class, n, w, group=None, exhaustive=False):
+    """The cross-rank half of ``brute_force_search``: this rank searches its classes
+    (``rank_classes``) through ``search_class(w, c, k_max) -> (k, indices or None)``, keeping the
+    smallest accepted size and, at it, the first subset in itertools.combinations order
+    (ref15.class_search: not exhaustive, a class searches only the sizes that can still win on
+    this rank); two all-reduces (MIN of the size, then MAX of the bit-reversed mask as two 32-bit
+    halves) give every rank the global winner (k, indices), or None when no class accepted a
+    subset."""
     import torch.distributed as dist
+
+    from . import ref15
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     tdev = _tdev(group)
-    k_r, key_r = _NONE, 0  # this rank: smallest accepted size, and its max bit-reversed mask
-    for c in range(rank, 1 << w, world):
-        k, idx = search_class(w, c)
-        if k and idx is not None:
-            key = _bitrev64(sum(1 << i for i in idx))
-            if k < k_r or (k == k_r and key > key_r):
-                k_r, key_r = k, key
+    k_r, key_r = ref15.class_search(search_class, n, w, rank_classes(w, rank, world), exhaustive)
+    if k_r is ref15.NO_SIZE:
+        k_r = _NONE
     t = torch.tensor([k_r], dtype=torch.int64, device=tdev)
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     k_min = int(t.item())
@@ -197,7 +207,7 @@ def search_winner(search_class, n, w, group=None):
     lo = torch.tensor([key_r & 0xFFFFFFFF if (k_r == k_min and key_r >> 32 == int(hi.item())) else -1],
                       dtype=torch.int64, device=tdev)
     dist.all_reduce(lo, op=dist.ReduceOp.MAX, group=group)
-    mask = _bitrev64((int(hi.item()) << 32) | int(lo.item()))
+    mask = ref15.bitrev64((int(hi.item()) << 32) | int(lo.item()))
     return k_min, tuple(i for i in range(n) if (mask >> i) & 1)
 
 
@@ -210,10 +220,6 @@ def sum_counts(counts, group=None):
     return t.cpu().numpy()
 
 
-def _bitrev64(v):
-    return int(f'{v & ((1 << 64) - 1):064b}'[::-1], 2)
-
-
 def brute_force_search_ranks(events, start_idx=0, end_idx=None, R_threshold=None, initial_pt=None,
                              initial_state=None, max_combos_in_memory=1 << 22, dtype='f64', device=0, group=None,
                              first_valid=None, finish=None, consts=None):
@@ -222,7 +228,7 @@ def brute_force_search_ranks(events, start_idx=0, end_idx=None, R_threshold=None
     shard_range(C(n, k), r, world) on its GPU (kf_eval_combos), then an all-reduce MIN of the
     first acceptable rank (or "none") decides — the same winner as the single-GPU search (the
     first acceptable subset of the smallest size, in itertools.combinations order).  Every rank
-    returns the reference's result dict (or None).  For searches whose prefix levels do not fit.
+    returns the reference's result dict (or None).  The per-subset cross-check of brute_force_search.
 
     ``first_valid(k, lo, hi)`` / ``finish(k, rank)`` replace the GPU evaluation (tests drive the
     reduction logic with the CPU oracle on gloo)."""

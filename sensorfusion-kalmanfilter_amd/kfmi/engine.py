@@ -425,7 +425,9 @@ class BatchedKF:
         threshold unless ``exhaustive``.  ``n_fixed`` / ``fixed_mask`` restrict it to the subsets
         whose intersection with candidates 0 .. n_fixed - 1 is fixed_mask (one shard of the
         search).  Returns (k_found, winner indices tuple or None, accepted count per size
-        [k_max + 1], subset_max [2^n] or None)."""
+        [k_max + 1], subset_max [2^n] or None).  ``subset_max`` may be a device tensor of 2^n
+        entries of the handle's dtype, which receives this search's subsets (untouched
+        elsewhere: the classes of one search fill one buffer)."""
         if self.model != 'ref15':
             raise ValueError('search_combos needs a ref15 handle')
         ev = np.ascontiguousarray(events, dtype=np.float64)
@@ -437,9 +439,16 @@ class BatchedKF:
         win = ctypes.c_uint64(0)
         kf = ctypes.c_int(0)
         acc = np.zeros(max(k_max, 0) + 1, dtype=np.uint64)
-        sm = self.empty(1 << n) if subset_max else None
-        if sm is not None:
-            sm.fill_(float('nan'))
+        if isinstance(subset_max, torch.Tensor):
+            sm = subset_max
+            if (sm.numel() != 1 << n or sm.dtype != self.torch_dtype or sm.device != self.device
+                    or not sm.is_contiguous()):
+                raise ValueError(f'subset_max must be a contiguous {self.torch_dtype} tensor of 2^{n} entries on '
+                                 f'{self.device}')
+        else:
+            sm = self.empty(1 << n) if subset_max else None
+            if sm is not None:
+                sm.fill_(float('nan'))
         check(_lib.lib().kf_search_combos(self.handle, n, ev.ctypes.data_as(ctypes.c_void_p),
                                           ini.ctypes.data_as(ctypes.c_void_p), float(prev_time), float(target_end),
                                           float(threshold), k_max, int(bool(exhaustive)), int(n_fixed),
@@ -448,6 +457,21 @@ class BatchedKF:
                                           self._stream()))
         combo = tuple(i for i in range(n) if (win.value >> i) & 1) if kf.value else None
         return kf.value, combo, acc, sm
+
+    def search_plan(self, init, n, k_max=None, n_fixed=0, fixed_mask=0):
+        """How search_combos would run over n candidates (kf_search_plan, no device work):
+        dict(sym, workspace_bytes, widest, max_parents, over_cap)."""
+        if self.model != 'ref15':
+            raise ValueError('search_plan needs a ref15 handle')
+        ini = np.ascontiguousarray(init, dtype=np.float64)
+        if ini.shape != (42,):
+            raise ValueError('init must be [42]')
+        out = np.zeros(5, dtype=np.int64)
+        check(_lib.lib().kf_search_plan(self.handle, int(n), ini.ctypes.data_as(ctypes.c_void_p), int(n_fixed),
+                                        int(fixed_mask), int(n if k_max is None else k_max),
+                                        out.ctypes.data_as(ctypes.c_void_p)))
+        return {'sym': bool(out[0]), 'workspace_bytes': int(out[1]), 'widest': int(out[2]),
+                'max_parents': int(out[3]), 'over_cap': int(out[4])}
 
     def search_info(self):
         """How the last search_combos ran (kf_search_info): axis-symmetric or not, the sizes its

@@ -704,10 +704,11 @@ def search_stored_levels(n, k_max=None):
     return list(range(max(K, 1), min(end, k_max)))
 
 
-def search_levels(n, dtype='f64', mem_bytes=32 << 30):
+def search_levels(n, dtype='f64', mem_bytes=32 << 30, sym=False):
     """Largest k_max for which kf_search_combos' level buffers (two of the widest stored level:
     the C(n - 2, k) subsets of size k < k_max whose largest candidate is <= n - 3) fit in
-    ``mem_bytes`` and every level stays below 2^28 stored parents."""
+    ``mem_bytes`` and every level stays below 2^28 stored parents (n = free candidates; sym:
+    the axis-symmetric search's 10-row nodes, kf_search_plan says which the handle runs)."""
     k_max, widest = 0, 0
     for k in range(1, n + 1):
         if k > 1:
@@ -715,10 +716,93 @@ def search_levels(n, dtype='f64', mem_bytes=32 << 30):
             if par >= 1 << 28:
                 break
             widest = max(widest, par)
-        if 2 * search_level_bytes(widest, dtype) + 4096 > mem_bytes:
+        if 2 * search_level_bytes(widest, dtype, sym) + 4096 > mem_bytes:
             break
         k_max = k
     return k_max
+
+
+def search_class_width(n, dtype='f64', mem_bytes=32 << 30, sym=False):
+    """The fewest leading candidates w whose fixed intersections split the search of n
+    candidates into 2^w classes that kf_search_combos runs whole: a class has n - w free
+    candidates, and every size of it fits ``mem_bytes`` and the 2^28-parent cap
+    (search_levels(n - w) = n - w).  n = 40, f64, 32 GiB: 8 axis-symmetric (the widest stored
+    level C(30, 15) nodes, 2 x 15.5 GB), 10 with every chain."""
+    for w in range(n):
+        if search_levels(n - w, dtype, mem_bytes, sym) >= n - w:
+            return w
+    return max(n - 1, 0)
+
+
+NO_SIZE = None
+
+
+def bitrev64(v):
+    return int(f'{v & ((1 << 64) - 1):064b}'[::-1], 2)
+
+
+def class_order(w):
+    """The classes of candidates 0 .. w - 1, fewest fixed members first (the classes that can hold
+    the smallest sizes; a search that is not exhaustive skips the rest once they cannot win)."""
+    return sorted(range(1 << w), key=lambda c: (bin(c).count('1'), c))
+
+
+def class_search(search_class, n, w, classes, exhaustive=False, k_max=None):
+    """Runs ``search_class(w, c, k_max) -> (k, indices or None)`` for each class c in turn (the
+    subsets whose intersection with candidates 0 .. w - 1 is the bit pattern c) and keeps the
+    reference's pick among them (kf_workers.py:1325-1356): the smallest accepted size and, at it,
+    the first subset in itertools.combinations order, i.e. the largest bit-reversed mask.
+    Returns (k, key) or (NO_SIZE, 0).  Not exhaustive, a class searches only the sizes that can
+    still win: up to the best size so far (skipped when its fixed members alone exceed it; one
+    size above when they make exactly it, the least k_max kf_search_combos takes).  ``k_max``
+    caps the sizes searched (the reference's loop over sizes 1 .. n, :1325, cut short)."""
+    k_r, key_r = NO_SIZE, 0
+    cap = n if k_max is None else int(k_max)
+    for c in classes:
+        k_base = bin(c).count('1')
+        lim = cap
+        if not exhaustive and k_r is not NO_SIZE:
+            lim = min(lim, k_r)
+        if k_base > lim:
+            continue
+        k, idx = search_class(w, c, min(n, max(lim, k_base + 1)))
+        if k and idx is not None and k <= cap:
+            key = bitrev64(sum(1 << i for i in idx))
+            if k_r is NO_SIZE or k < k_r or (k == k_r and key > key_r):
+                k_r, key_r = k, key
+    return k_r, key_r
+
+
+def search_combos_classed(kf, ev, init, prev_time, target_end, threshold, w, exhaustive=False, subset_max=False,
+                          classes=None, k_max=None):
+    """kf.search_combos over sizes 1 .. k_max (default n) of the n candidates as 2^w class
+    searches run one after another on this handle's GPU (``class_search``; w from
+    ``search_class_width`` when the whole search does not fit one call).  Returns
+    search_combos' (k_found, winner indices or None, accepted count per size [n + 1],
+    subset_max [2^n] or None): the same winner and counts as one call over those sizes of every
+    subset (not exhaustive: counts past k_found are 0)."""
+    n = int(np.asarray(ev).shape[0])
+    acc = np.zeros(n + 1, dtype=np.uint64)
+    sm = None
+    if subset_max:
+        sm = kf.empty(1 << n)
+        sm.fill_(float('nan'))
+
+    def search_class(nf, c, k_max):
+        k, idx, a, _ = kf.search_combos(ev, init, prev_time, target_end, threshold, k_max=k_max,
+                                        exhaustive=exhaustive, subset_max=sm if sm is not None else False,
+                                        n_fixed=nf, fixed_mask=c)
+        acc[:len(a)] += a
+        return k, idx
+    k, key = class_search(search_class, n, w, class_order(w) if classes is None else classes, exhaustive, k_max)
+    if k_max is not None:
+        acc[int(k_max) + 1:] = 0   # a class whose fixed members make k_max searched one size more
+    if k is NO_SIZE:
+        return 0, None, acc, sm
+    if not exhaustive:
+        acc[k + 1:] = 0
+    mask = bitrev64(key)
+    return k, tuple(i for i in range(n) if (mask >> i) & 1), acc, sm
 
 
 def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end_idx=None, R_threshold=None,
@@ -727,11 +811,14 @@ def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end
                                                        search_mem_bytes=32 << 30, consts=None):
     """kf_workers.py:1218-1392 on the GPU: for k = 1..n, evaluate every k-subset of the candidate
     events and return the first subset, in itertools.combinations order, whose max
-    log-determinant is below R_threshold — the reference's result dict — or None.  Sizes whose
-    prefix levels fit in ``search_mem_bytes`` run as one shared-prefix search
-    (kf_search_combos: one event step per subset); larger sizes evaluate one filter per subset
-    (kf_eval_combos, up to ``max_combos_in_memory`` per launch).  Multi-GPU:
-    kfmi.dist.brute_force_search."""
+    log-determinant is below R_threshold — the reference's result dict — or None.  The subsets
+    run as the shared-prefix search (kf_search_combos: one event step per subset): the sizes
+    whose level buffers fit ``search_mem_bytes`` in one call (k_search), then, if none of those
+    was accepted, every size as 2^w class searches one after another (search_combos_classed;
+    n = 40, the reference's visualizing window, kf_workers_visualizing.py:2293, 2340: 256
+    classes of 32 free candidates).  ``max_combos_in_memory`` is the reference's argument; the
+    search needs no per-subset batch.  One filter per subset stays available as
+    ``first_valid_rank`` (kf_eval_combos).  Multi-GPU: kfmi.dist.brute_force_search."""
     if R_threshold is None:
         raise ValueError('R_threshold must be specified for brute force KF.')
     st = brute_force_setup(events, start_idx, end_idx, initial_pt, initial_state, consts)
@@ -739,30 +826,21 @@ def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end
         return None
     cand, xt, Pt, prev_time, target_end, ev, init = st
     n = len(cand)
-    # sizes 1 .. k_search by the shared-prefix search (kf_search_combos), the rest (if its level
-    # buffers would not fit) one filter per subset (kf_eval_combos)
-    k_search = search_levels(n, dtype, search_mem_bytes)
-    if k_search:
-        kf = BatchedKF('ref15', 1, dtype, device=device, params=_params(consts))
-        try:
-            k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=k_search)
-        finally:
-            kf.close()
-        if k:
-            return brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device, indices=idx,
-                                      consts=consts)
-        if k_search == n:
-            return None
-    width = int(min(max_combos_in_memory, max(math.comb(n, k) for k in range(k_search + 1, n + 1))))
-    kf = BatchedKF('ref15', width, dtype, device=device, params=_params(consts))
+    kf = BatchedKF('ref15', 1, dtype, device=device, params=_params(consts))
     try:
-        for k in range(k_search + 1, n + 1):
-            r = first_valid_rank(kf, ev, init, prev_time, target_end, k, 0, math.comb(n, k), R_threshold)
-            if r is not None:
-                return brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype, device, consts=consts)
+        sym = kf.search_plan(init, n, k_max=1)['sym']
+        k_search = search_levels(n, dtype, search_mem_bytes, sym)
+        k, idx = 0, None
+        if k_search:
+            k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=k_search)
+        if not k and k_search < n:
+            w = search_class_width(n, dtype, search_mem_bytes, sym)
+            k, idx, _, _ = search_combos_classed(kf, ev, init, prev_time, target_end, R_threshold, w)
     finally:
         kf.close()
-    return None
+    if not k:
+        return None
+    return brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device, indices=idx, consts=consts)
 
 
 # --------------------------------------------------------------------------------------------

@@ -59,32 +59,59 @@ def test_bench_world_mismatch_exits_nonzero():
     assert 'WORLD_SIZE=1' in p.stderr
 
 
+def _bench_ranks(gpus, config, extra=()):
+    cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', str(gpus), '--dist-backend', 'gloo',
+           '--config', config, '--no-cpu-baseline'] + list(extra)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec['n_gpus'] == rec['ranks_seen'] == gpus
+    assert rec['failed_filters'] == 0 and rec['value'] > 0
+    return rec
+
+
+def _check_allgather(rec, gpus):
+    ag = rec['allgather']
+    assert ag['checked'].startswith('bitwise') and ag['traj_steps'] > 0
+    assert ag['bytes_gathered'] == gpus * ag['bytes_per_rank'] > 0
+    assert rec['scaling'] == 'weak'
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize('config', ['3', '4', '2', '5', 'ref15', 'sched', 'bf'])
+@pytest.mark.parametrize('config', ['3', '4', '2', '5', 'ref15', 'sched', 'bf', 'bf40'])
 def test_bench_two_ranks_on_the_gpu(config):
     """`python bench.py --gpus 2` end to end on the GPU box, started as a fresh child process:
     two ranks (gloo: they share the box's one GPU; the 8-GPU node's run is RCCL), each owning
     its shard of filters, max-over-ranks timing, and the final all-gather of the final states,
     last log-dets and the decimated trajectory, which every rank checks bitwise against its own
     shard (bench.py's N > 1 path; replaces the reference's Pool(30) fan-out,
-    kf_workers.py:1320-1346).  bf: the brute-force search sharded by subset class across the two
-    ranks with its cross-rank reductions (kfmi.dist.search_winner / sum_counts) gives rank 0's
-    one-rank winner and acceptance counts."""
-    cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--dist-backend', 'gloo', '--config', config,
-           '--batch', '65536', '--steps', '2', '--warmup', '1', '--no-cpu-baseline']
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
-    assert len(lines) == 1, r.stdout[-2000:]
-    rec = json.loads(lines[0])
-    assert rec['n_gpus'] == rec['ranks_seen'] == 2
-    assert rec['failed_filters'] == 0 and rec['value'] > 0
-    if config == 'bf':
+    kf_workers.py:1320-1346).  bf / bf40: ONE search split by subset class across the two ranks,
+    timed with its cross-rank reductions (kfmi.dist.search_winner), value = one search's
+    subsets / the slowest rank's time (strong scaling); after timing, the sharded search at a
+    threshold gives rank 0's one-GPU winner (bf: and, exhaustive, its acceptance counts)."""
+    if config.startswith('bf'):
+        rec = _bench_ranks(2, config, ['--steps', '1', '--warmup', '0' if config == 'bf40' else '1'])
+        assert rec['scaling'] == 'strong' and rec['unit'] == 'subsets/s'
         ds = rec['dist_search']
-        assert ds['one_rank_equal'] and ds['k_found'] > 0 and ds['classes'] >= 2
-        assert ds['winner'] == ds['one_rank']['winner'] and ds['accepted_per_size'] == ds['one_rank']['accepted_per_size']
-        assert sum(ds['accepted_per_size']) > 0
+        assert ds['one_rank_equal'] and ds['k_found'] >= 2 and ds['classes'] >= 8
+        assert ds['winner'] == ds['one_rank']['winner']
+        assert rec['config']['classes'] == ds['classes'] and rec['config']['classes_this_rank'] == ds['classes'] // 2
+        if config == 'bf':
+            ex = ds['exhaustive']
+            assert ex['accepted_per_size'] == ds['one_rank']['accepted_per_size'] and sum(ex['accepted_per_size']) > 0
         return
-    ag = rec['allgather']
-    assert ag['checked'].startswith('bitwise') and ag['traj_steps'] > 0
-    assert ag['bytes_gathered'] == 2 * ag['bytes_per_rank'] > 0
+    rec = _bench_ranks(2, config, ['--batch', '65536', '--steps', '2', '--warmup', '1'])
+    _check_allgather(rec, 2)
+
+
+@pytest.mark.gpu
+def test_bench_eight_ranks_config4_on_the_gpu():
+    """BASELINE config 4's own rank count (8 x 2^20 fp32 filters over 8 GPUs, RCCL all-gather):
+    the launch shape the driver's 8-GPU run uses, eight ranks started by `bench.py --gpus 8`
+    (gloo: here they share the box's one GPU, 65,536 filters each), every rank checking its shard
+    in the all-gathered arrays bitwise."""
+    rec = _bench_ranks(8, '4', ['--batch', '65536', '--steps', '2', '--warmup', '1'])
+    _check_allgather(rec, 8)
+    assert rec['config']['filters_per_gpu'] == 65536

@@ -132,6 +132,38 @@ def test_events_select_sizes(n, p_keep):
             np.testing.assert_array_equal(s_o[:m].cpu().numpy(), k_want)
 
 
+def test_events_select_refuses_capture():
+    """kf_events_select synchronises to return its count, so inside a hipGraph capture it
+    returns KF_EINVAL before queuing anything: the capture stays valid, the graph (holding a
+    torch op captured around the refused call) replays, and the next eager call works."""
+    import ctypes
+    d = torch.device('cuda', 0)
+    n = 5000
+    et_d = (torch.arange(n, device=d) % 3 == 0).to(torch.uint8)
+    t_d = torch.arange(n, dtype=torch.float64, device=d)
+    t_o = torch.empty(n, dtype=torch.float64, device=d)
+    lib = _lib.lib()
+    kept = ctypes.c_int64(-1)
+    x = torch.zeros(4, device=d)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        x += 1
+        rc = lib.kf_events_select(n, ctypes.c_void_p(et_d.data_ptr()), ctypes.c_void_p(t_d.data_ptr()), None, 1,
+                                  ctypes.c_void_p(t_o.data_ptr()), None, None, ctypes.byref(kept),
+                                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        x += 1
+    assert rc == _lib.KF_EINVAL and 'capturable' in _lib.last_error() and kept.value == 0
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(x[0]) == 2.0
+    rc = lib.kf_events_select(n, ctypes.c_void_p(et_d.data_ptr()), ctypes.c_void_p(t_d.data_ptr()), None, 1,
+                              ctypes.c_void_p(t_o.data_ptr()), None, None, ctypes.byref(kept),
+                              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0 and kept.value == (n + 2) // 3
+    np.testing.assert_array_equal(t_o[:kept.value].cpu().numpy(), np.arange(0, n, 3, dtype=float))
+
+
 def test_dead_reckoning_select_and_dt():
     """kf_events_select keeps one type in stream order; kf_events_dt with prev0 = NaN gives the
     first event dt 0 (hw5_2.py:401, 407) and the rest raw differences (no guard)."""

@@ -1,0 +1,167 @@
+"""The class-decomposed brute-force search (kfmi.ref15.search_combos_classed) — needs an MI355X.
+
+The reference's search (kf_workers.py:1218-1392) over n candidates takes every subset, 2^n - 1
+of them; the reference's visualizing run brute-forces a window of n = 40
+(kf_workers_visualizing.py:2293, 2340).  One kf_search_combos call holds its level buffers for
+every size only up to n = 32 (the 2^28-parent cap and the 32 GiB budget), so a larger search runs
+as 2^w classes — the subsets with one fixed intersection with candidates 0 .. w - 1 — one call
+each, reduced to the reference's pick (smallest accepted size, then itertools order).
+
+Checked here: at n = 25 and 28 the classes reproduce the whole search (every subset's score
+through subset_max, winners and acceptance counts, exhaustive and not); at n = 40 the winner
+equals one filter per subset (kf_eval_combos, first_valid_rank) at thresholds whose first
+accepted size is 2 and is past the one-call search's sizes, and acceptance counts of sizes 1-4
+equal the C oracle's (oracle/cpu_kf.c, one filter per subset).
+"""
+import math
+from itertools import combinations
+
+import numpy as np
+import pytest
+import torch
+
+import bench
+import kfmi
+from kfmi import ref15
+from oracle import ref_kf
+from test_gpu_bench_parity import _combo_maxima
+
+pytestmark = pytest.mark.gpu
+
+
+def _thresholds(sm, q):
+    """Thresholds just above the q-quantiles of the finite subset scores (a relative margin of
+    1e-9 keeps every decision away from a score's last bits)."""
+    vals = torch.sort(sm[torch.isfinite(sm)]).values
+    return [float(vals[int(x * (len(vals) - 1))]) * (1 - 1e-9) + 1e-9 for x in q]
+
+
+@pytest.mark.parametrize('n,ws,axis_sym', [(25, (1, 3, 6), 'auto'), (25, (4,), 'off'), (28, (3, 5), 'auto')])
+def test_classed_search_equals_whole_search(n, ws, axis_sym):
+    """Every class split gives the whole search's scores (subset_max, bit for bit), and at
+    thresholds accepting nothing, 0.01 %, 2 % and half of the subsets its winner and acceptance
+    counts, exhaustive and stopping at the first accepted size."""
+    ev, init, _, t0, t_end = bench.bf_events(n)
+    kf = kfmi.BatchedKF('ref15', 1, 'f64', options={'axis_sym': axis_sym})
+    assert kf.search_plan(init, n)['sym'] == (axis_sym == 'auto')
+    _, _, _, whole = kf.search_combos(ev, init, t0, t_end, -1e30, exhaustive=True, subset_max=True)
+    assert kf.search_info()['sym'] == (axis_sym == 'auto')
+    thrs = [-1e30] + _thresholds(whole, (1e-4, 0.02, 0.5))
+    for w in ws:
+        k, idx, acc, sm = ref15.search_combos_classed(kf, ev, init, t0, t_end, -1e30, w, exhaustive=True,
+                                                      subset_max=True)
+        assert k == 0 and idx is None and not acc.any()
+        assert torch.equal(sm.view(torch.int64), whole.view(torch.int64)), (n, w)
+        del sm
+        for thr in thrs:
+            for exhaustive in (True, False):
+                want = kf.search_combos(ev, init, t0, t_end, thr, exhaustive=exhaustive)
+                got = ref15.search_combos_classed(kf, ev, init, t0, t_end, thr, w, exhaustive=exhaustive)
+                assert got[:2] == want[:2], (n, w, thr, exhaustive, got[:2], want[:2])
+                np.testing.assert_array_equal(got[2], want[2])
+    kf.close()
+
+
+def _n40_case():
+    """The bench's 40 candidates (bf_events: 200 Hz IMU, a fix every 20th) with the target 5 s
+    past the last one, so that each subset's score is its final predict's log-det, which falls
+    with every update: the smallest score falls with the size well past the one-call sizes."""
+    n = 40
+    ev, init, Pw, t0, t_end = bench.bf_events(n)
+    return n, ev, init, Pw, t0, t_end + 5.0
+
+
+def _min_scores(kf, n, ev, init, t0, t_end, sizes):
+    """Smallest per-subset score of each size (kf_eval_combos, one filter per subset)."""
+    out = {}
+    for k in sizes:
+        total, best = math.comb(n, k), float('inf')
+        for off in range(0, total, kf.batch):
+            mx, _, _ = kf.eval_combos(ev, init, t0, t_end, k, combo_offset=off, logdets=False)
+            best = min(best, float(mx[:min(kf.batch, total - off)].min()))
+        out[k] = best
+    return out
+
+
+def test_n40_search_vs_per_subset():
+    """The reference's n = 40 window: run_brute_force_kalman_filter_no_sampling_min_usage's
+    winner (one call for sizes 1 .. k_search, then 256 classes) equals the first acceptable
+    subset one filter per subset finds (first_valid_rank, kf_eval_combos over every size in
+    combination order), at a threshold whose first accepted size is 2 and at one whose first
+    accepted size is past k_search."""
+    n, ev, init, Pw, t0, t_far = _n40_case()
+    kfe = kfmi.BatchedKF('ref15', 1 << 22, 'f64')
+    kfs = kfmi.BatchedKF('ref15', 1, 'f64')
+    sym = kfs.search_plan(init, n)['sym']
+    k_search = ref15.search_levels(n, 'f64', 32 << 30, sym)
+    assert sym and k_search == 10 and ref15.search_class_width(n, 'f64', 32 << 30, sym) == 8
+    mins = _min_scores(kfe, n, ev, init, t0, t_far, range(1, k_search + 1))
+    print('n = 40 smallest score per size:', {k: round(v, 6) for k, v in mins.items()})
+    L0 = float(np.linalg.slogdet(Pw)[1])
+    m_lo = min(mins.values())
+    assert mins[2] < mins[1] and m_lo > L0
+    thr_lo = m_lo - 1e-9 * abs(m_lo)      # nothing of sizes 1 .. k_search scores below
+    thr_2 = (mins[1] + mins[2]) / 2        # pairs first
+    # the driver's steps on these arrays (its window's target is the last event's time, so the
+    # far target is set here): sizes 1 .. k_search in one call, then every size by class
+    w = ref15.search_class_width(n, 'f64', 32 << 30, sym)
+    for thr, want_min in ((thr_2, 2), (thr_lo, k_search + 1)):
+        k, idx, _, _ = kfs.search_combos(ev, init, t0, t_far, thr, k_max=k_search)
+        if not k:
+            k, idx, _, _ = ref15.search_combos_classed(kfs, ev, init, t0, t_far, thr, w)
+        assert k == want_min if want_min == 2 else want_min <= k <= want_min + 1, (thr, k)
+        r = None
+        for kk in range(1, k + 1):
+            r = ref15.first_valid_rank(kfe, ev, init, t0, t_far, kk, 0, math.comb(n, kk), thr)
+            if r is not None:
+                break
+        assert r is not None and kk == k, (thr, kk, k)
+        assert tuple(ref15.unrank_combination(n, k, r)) == idx, (thr, k, r, idx)
+        print(f'n = 40, threshold {thr:.9f}: winner of size {k}: {idx}')
+    kfe.close()
+    kfs.close()
+
+
+def test_n40_counts_sizes_1_to_4_vs_oracle():
+    """Acceptance counts of sizes 1-4 summed over the 256 classes of the n = 40 search (size cap
+    4, exhaustive) equal the C oracle's per-subset scores' (every subset of sizes 1-4, 102,090),
+    at thresholds through the size-1, size-2 and size-3 scores; the winner is the oracle's first."""
+    n, ev, init, Pw, t0, t_far = _n40_case()
+    kfs = kfmi.BatchedKF('ref15', 1, 'f64')
+    w = ref15.search_class_width(n, 'f64', 32 << 30, kfs.search_plan(init, n)['sym'])
+    small = {k: np.array(list(combinations(range(n), k))) for k in range(1, 5)}
+    maxima = {k: _combo_maxima(ev, Pw, t0, t_far, c) for k, c in small.items()}
+    for thr in (float(np.median(maxima[1])), float(np.quantile(maxima[2], 0.1)), float(np.median(maxima[3]))):
+        want = [0] + [int((maxima[k] < thr).sum()) for k in range(1, 5)]
+        assert sum(want) > 0
+        k, idx, acc, _ = ref15.search_combos_classed(kfs, ev, init, t0, t_far, thr, w, exhaustive=True, k_max=4)
+        assert [int(v) for v in acc[:5]] == want and not acc[5:].any(), (thr, list(acc[:5]), want)
+        first = next(kk for kk in range(1, 5) if want[kk])
+        assert k == first and idx == tuple(small[first][np.argmax(maxima[first] < thr)])
+        # and not exhaustive: the same winner, counts up to it
+        k2, idx2, acc2, _ = ref15.search_combos_classed(kfs, ev, init, t0, t_far, thr, w)
+        assert (k2, idx2) == (k, idx) and [int(v) for v in acc2[:k + 1]] == want[:k + 1] and not acc2[k + 1:].any()
+    kfs.close()
+
+
+def test_n40_driver_winner_vs_reference_search():
+    """run_brute_force_kalman_filter_no_sampling_min_usage over a 40-event window whose winner
+    has two events equals the NumPy restatement of the reference's search (kf_workers.py:
+    1218-1392, sizes 1 and 2 through the reference's own loop), records and all."""
+    n = 40
+    ev, init, Pw, t0, _ = bench.bf_events(n)
+    t_last = float(ev[-1, 0])
+    events = [(i, 'GPS', ev[i, 0], {'easting': ev[i, 2], 'northing': ev[i, 3], 'altitude': ev[i, 4]})
+              if ev[i, 1] == 0 else (i, 'IMU', ev[i, 0], ['t', *ev[i, 2:]]) for i in range(n)]
+    state0 = (t0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
+    s1 = np.sort(_combo_maxima(ev, Pw, t0, t_last, np.arange(n)[:, None]))
+    L0 = float(np.linalg.slogdet(Pw)[1])
+    thr = (L0 + s1[0]) / 2
+    ref = ref_kf.run_brute_force(events, 0, n, thr, Pw, state0)
+    got = ref15.run_brute_force_kalman_filter_no_sampling_min_usage(events, 0, n, R_threshold=thr, initial_pt=Pw,
+                                                                     initial_state=state0)
+    sel = [e[0] for e in ref['selected_sensors']]
+    assert len(sel) == 2 and [e[0] for e in got['selected_sensors']] == sel
+    for key in ('log_determinants', 'final_state', 'trajectory'):
+        a, b = np.asarray(got[key], np.float64), np.asarray(ref[key], np.float64)
+        assert a.shape == b.shape and np.max(np.abs(a - b) / np.maximum(np.abs(b), 1.0)) <= 1e-6, key

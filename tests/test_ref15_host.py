@@ -201,3 +201,85 @@ def test_device_draws_reproduce_np_random_choice():
     np.testing.assert_array_equal(ref15.legacy_words(3 * len(lens)), words)   # reading does not advance
     np.random.randint(0, 1 << 32, size=taken, dtype=np.uint32)
     assert np.random.random() == after
+
+
+def test_search_class_width_fits_every_size():
+    """ref15.search_class_width: the fewest leading candidates whose 2^w classes kf_search_combos
+    runs whole within the budget and the 2^28-parent cap — the reference's n = 40 window
+    (kf_workers_visualizing.py:2293) takes 256 axis-symmetric classes of 32 free candidates,
+    1024 every-chain classes of 30; n <= 30 needs none."""
+    assert ref15.search_class_width(40, sym=True) == 8 and ref15.search_class_width(40) == 10
+    for n in (12, 25, 30):
+        assert ref15.search_class_width(n) == 0 and ref15.search_levels(n) == n
+    for n in (33, 36, 40, 45):
+        for sym in (False, True):
+            w = ref15.search_class_width(n, sym=sym)
+            assert ref15.search_levels(n - w, sym=sym) == n - w > ref15.search_levels(n - w + 1, sym=sym) - 1
+            assert ref15.search_levels(n - w + 1, sym=sym) < n - w + 1       # one candidate fewer fixed: no
+            m = n - w
+            widest = max(math.comb(m - 2, k) for k in range(1, m - 1))
+            assert 2 * ref15.search_level_bytes(widest, 'f64', sym) + 4096 <= 32 << 30
+            assert all(math.comb(m - 2, k - 1) < 1 << 28 for k in range(2, m + 1))
+    # the sharded plan never goes below the memory rule, nor below 4 classes per rank
+    from kfmi import dist as kdist
+    assert kdist.search_classes(40, 8, sym=True) == 8 and kdist.search_classes(40, 1) == 10
+    assert kdist.search_classes(25, 8) == 5 and kdist.search_classes(25, 1) == 0
+
+
+@pytest.mark.parametrize('w', [0, 1, 3, 5])
+@pytest.mark.parametrize('exhaustive', [True, False])
+def test_class_search_picks_the_reference_winner(w, exhaustive):
+    """ref15.class_search over a random acceptance table: the smallest accepted size, then the
+    first subset in itertools.combinations order (kf_workers.py:1325-1356), whatever the class
+    order; not exhaustive, no class searches sizes that can no longer win and classes whose
+    fixed members alone are too many are skipped."""
+    n = 11
+    rng = np.random.default_rng(5 + w)
+    for trial in range(6):
+        rate = [0.0, 0.001, 0.004, 0.02, 0.05, 0.2][trial]
+        acc = {c: rng.random() < rate * len(c) for k in range(1, n + 1) for c in combinations(range(n), k)}
+        calls = []
+
+        def search_class(nf, c, k_max):
+            calls.append((c, k_max))
+            for k in range(1, k_max + 1):
+                for x in combinations(range(n), k):
+                    if sum(1 << i for i in x if i < nf) == c and acc[x]:
+                        return k, x
+            return 0, None
+        want = next(((k, x) for k in range(1, n + 1) for x in combinations(range(n), k) if acc[x]), None)
+        for order in (ref15.class_order(w), list(range(1 << w))[::-1]):
+            calls.clear()
+            k, key = ref15.class_search(search_class, n, w, order, exhaustive)
+            got = None if k is ref15.NO_SIZE else (k, tuple(i for i in range(n) if (ref15.bitrev64(key) >> i) & 1))
+            assert got == want, (w, trial, got, want)
+            assert sorted(c for c, _ in calls) == (list(range(1 << w)) if exhaustive or want is None
+                                                   else sorted(c for c, _ in calls))
+            if not exhaustive and want:
+                assert all(km >= want[0] for _, km in calls)
+                assert all(bin(c).count('1') < km for c, km in calls)   # a class searched has a size to search
+
+
+@pytest.mark.parametrize('w', [2, 4])
+def test_class_search_size_cap(w):
+    """class_search(k_max=K): the reference's pick among sizes 1..K only; no class is asked for
+    more than one size past K, and none whose fixed members alone exceed K."""
+    n = 10
+    rng = np.random.default_rng(11)
+    acc = {c: rng.random() < 0.01 * len(c) ** 2 for k in range(1, n + 1) for c in combinations(range(n), k)}
+    for K in (1, 2, 3, 6):
+        for exhaustive in (True, False):
+            calls = []
+
+            def search_class(nf, c, k_max):
+                calls.append((c, k_max))
+                for k in range(1, k_max + 1):
+                    for x in combinations(range(n), k):
+                        if sum(1 << i for i in x if i < nf) == c and acc[x]:
+                            return k, x
+                return 0, None
+            want = next(((k, x) for k in range(1, K + 1) for x in combinations(range(n), k) if acc[x]), None)
+            k, key = ref15.class_search(search_class, n, w, ref15.class_order(w), exhaustive, k_max=K)
+            got = None if k is ref15.NO_SIZE else (k, tuple(i for i in range(n) if (ref15.bitrev64(key) >> i) & 1))
+            assert got == want, (K, exhaustive, got, want)
+            assert all(bin(c).count('1') <= K and km <= max(K, bin(c).count('1') + 1) for c, km in calls)
