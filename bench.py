@@ -1165,7 +1165,10 @@ def bf_workload(cfg, args, rank, world, dev):
         pass
     split = (f'{1 << w} classes of {m} free candidates (the subsets split by their intersection with candidates '
              f'0..{w - 1}), {classes_here} on this rank, each a kf_search_combos call' if w else 'one kf_search_combos call')
-    return dict(step=step, units=total_combos, unit='subsets/s', ref_steps=ref_steps, strong=world > 1,
+    par = (f'subset classes x{world}: one search split over the ranks, two all-reduces (MIN size, MAX winner '
+           f'key) per search' if world > 1 else
+           (f'one GPU, {1 << w} class searches in sequence' if w else 'one GPU, one search call'))
+    return dict(step=step, units=total_combos, unit='subsets/s', ref_steps=ref_steps, strong=world > 1, parallelism=par,
                 bytes=lvl_bytes, bytes_per_unit=lvl_bytes / subsets_here,
                 valu_per_launch=valu_per_search if world == 1 else None,
                 kernel=f'ref15_search_head_kernel (sizes 1..{K}) + ref15_search_cm/pm_kernel + '
@@ -1400,7 +1403,8 @@ def main():
             'vs_baseline': None,
             'dtype': cfg['dtype'],
             'data': 'synthetic (GPS+IMU streams per SURVEY.md §8d, generated on the GPU, resident in HBM)',
-            'config': dict({'workload': w['desc'], 'parallelism': f'filter shards x{world} (no data-path collective)'},
+            'config': dict({'workload': w['desc'],
+                            'parallelism': w.get('parallelism', f'filter shards x{world} (no data-path collective)')},
                            **w['extra']),
         }
         if 'valu_per_launch' in w:

@@ -93,35 +93,33 @@ def main():
     if sz is not None:  # the sized count against the probe's known bytes
         res['calibration']['sized_over_known_read'] = sum(sz[0]) / len(sz[0]) / known_read
     for c in cfgs:
-        if c == 'bf':
-            # one search = its level launches (ref15_search_*_kernel), summed
-            n = CONFIGS['bf']['n']
+        if c in ('bf', 'bf40'):
+            # one search = its launches (ref15_search_*_kernel), summed: one kf_search_combos call
+            # (bf), or one per class (bf40: 256 class searches, each with its head launch)
+            with open(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE.log')) as fh:  # the bench line's own count
+                for line in fh:
+                    if line.startswith('{"metric"'):
+                        rec = json.loads(line)
+            alg = rec['roofline']['hbm']['algorithmic_bytes_per_launch']
+            classes = rec['config'].get('classes', 1)
             is_search = lambda k: 'ref15_search' in k  # noqa: E731
             fk = per_kernel(os.path.join(out_dir, f'cfg{c}_FETCH_SIZE'), 'FETCH_SIZE')
             wk = per_kernel(os.path.join(out_dir, f'cfg{c}_WRITE_SIZE'), 'WRITE_SIZE')
             f = [v for k, vs in fk.items() if is_search(k) for v in vs]
             w = [v for k, vs in wk.items() if is_search(k) for v in vs]
-            from kfmi.ref15 import search_launches, search_level_bytes, search_stored_levels
-            import math
-            # launches per search: the head (sizes 1 .. K), the levels with stored parents up to
-            # the end launch, and the end launch
-            nl = search_launches(n)
+            searches = len(pick(fk, 'ref15_search_head')) / classes
             fb, info = fetch(out_dir, f'cfg{c}', is_search, f, read_scale)
-            fb *= nl
+            fb *= len(f) / searches
             if 'fetch_bytes_calibrated' in info:
-                info['fetch_bytes_calibrated'] *= nl
-            write = 1024 * sum(w) / (len(w) / nl)
-            alg = 2 * sum(search_level_bytes(math.comb(n - 2, k), 'f64') for k in search_stored_levels(n))
-            with open(os.path.join(out_dir, 'cfgbf_FETCH_SIZE.log')) as fh:  # the bench line's own count
-                for line in fh:
-                    if line.startswith('{"metric"'):
-                        alg = json.loads(line)['roofline']['algorithmic_bytes_per_launch']
-            res['configbf'] = {
-                'fetch_bytes_raw': 1024 * sum(f) / (len(f) / nl), 'write_bytes_raw': write,
+                info['fetch_bytes_calibrated'] *= len(f) / searches
+            write = 1024 * sum(w) / searches
+            res[f'config{c}'] = {
+                'fetch_bytes_raw': 1024 * sum(f) / searches, 'write_bytes_raw': write,
                 'bytes_per_launch': fb + write * write_scale,
                 'algorithmic_bytes_per_launch': alg,
                 'traffic_over_algorithmic': (fb + write * write_scale) / alg,
-                'launches_profiled': len(f), 'note': f'per search: the sum over its {nl} level launches', **info}
+                'launches_profiled': len(f), 'searches_profiled': searches, 'classes': classes,
+                'note': f'per search: the sum over its {len(f) / searches:.0f} launches', **info}
             continue
         if c == 'sched':
             # the two passes per launch, each against its own bytes; the algorithmic total is the

@@ -22,7 +22,7 @@ for set in $SETS; do
   fi
   timeout -k 10 300 rocprofv3 --pmc $ctrs --output-format csv -d "$OUT/probe_$set" -o p -- "$ROOT/tools/probes/bw_probe" 1048576 64 > "$OUT/probe_$set.log" 2>&1 || { echo "probe $set failed"; tail "$OUT/probe_$set.log"; exit 1; }
   for c in $CFGS; do
-    timeout -k 10 300 rocprofv3 --pmc $ctrs --output-format csv -d "$OUT/cfg${c}_$set" -o k -- python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu-baseline ${PMC_BENCH_ARGS:-} > "$OUT/cfg${c}_$set.log" 2>&1 || { echo "cfg $c $set failed"; tail "$OUT/cfg${c}_$set.log"; exit 1; }
+    timeout -k 10 300 rocprofv3 --pmc $ctrs --output-format csv -d "$OUT/cfg${c}_$set" -o k -- python3 "$ROOT/bench.py" --config $c ${PMC_STEPS:---steps 3 --warmup 1} --no-cpu-baseline ${PMC_BENCH_ARGS:-} > "$OUT/cfg${c}_$set.log" 2>&1 || { echo "cfg $c $set failed"; tail "$OUT/cfg${c}_$set.log"; exit 1; }
   done
 done
 cd "$ROOT"

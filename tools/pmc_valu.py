@@ -39,26 +39,28 @@ def kernel_trace_ms(out_dir, c, kern):
     raise SystemExit(f'no kernel-trace row for {kern!r} under {out_dir}/kt{c}')
 
 
-def search_valu(out_dir, rec):
-    """bf: one search = its head and level launches (every ref15_search_* dispatch), counters and
-    kernel-trace durations summed per search; a unit is one subset."""
+def search_valu(out_dir, rec, c):
+    """bf / bf40: one search = its launches (every ref15_search_* dispatch: one kf_search_combos
+    call, or one per class), counters and kernel-trace durations summed per search; a unit is one
+    subset."""
     import csv
     import glob
-    d = os.path.join(out_dir, 'cfgbf')
-    searches = len(pick(per_kernel(d, 'SQ_WAVES'), 'ref15_search_head'))
+    d = os.path.join(out_dir, f'cfg{c}')
+    classes = rec['config'].get('classes', 1)
+    searches = len(pick(per_kernel(d, 'SQ_WAVES'), 'ref15_search_head')) / classes
     vals = {ctr: sum(v for k, vs in per_kernel(d, ctr).items() if 'ref15_search' in k for v in vs) / searches
             for ctr in COUNTERS}
     tot, heads = 0.0, 0
-    for f in glob.glob(os.path.join(out_dir, 'ktbf', '**', '*kernel_stats.csv'), recursive=True):
+    for f in glob.glob(os.path.join(out_dir, f'kt{c}', '**', '*kernel_stats.csv'), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 if 'ref15_search' in r['Name']:
                     tot += float(r['TotalDurationNs'])
                     heads += int(r['Calls']) if 'search_head' in r['Name'] else 0
-    ms = tot * 1e-6 / heads
+    ms = tot * 1e-6 / (heads / classes)
     wave_units = rec['config']['combinations'] / 64
-    return dict(kernel='ref15_search_head/cm/pm_kernel (one search)', counters_per_launch=vals, kernel_ms=ms,
-                launches_profiled=searches, valu_per_wave_step=vals['SQ_INSTS_VALU'] / wave_units,
+    return dict(kernel='ref15_search_head/cm/pm/end_kernel (one search)', counters_per_launch=vals, kernel_ms=ms,
+                launches_profiled=searches, classes=classes, valu_per_wave_step=vals['SQ_INSTS_VALU'] / wave_units,
                 valu_issue_frac=vals['SQ_INSTS_VALU'] * CYC / (ms * 1e-3 * CLK * SIMDS),
                 wave_cycles_waiting_frac=vals['SQ_WAIT_ANY'] / vals['SQ_WAVE_CYCLES'],
                 wave_cycles_issue_stall_frac=vals['SQ_WAIT_INST_ANY'] / vals['SQ_WAVE_CYCLES'],
@@ -71,8 +73,8 @@ def main():
     for c in cfgs:
         d = os.path.join(out_dir, f'cfg{c}')
         rec = bench_line(os.path.join(out_dir, f'cfg{c}.log'))
-        if c == 'bf':
-            res['configbf'] = search_valu(out_dir, rec)
+        if c in ('bf', 'bf40'):
+            res[f'config{c}'] = search_valu(out_dir, rec, c)
             continue
         units = rec['value'] * rec['ms_per_step'] * 1e-3        # filter-steps (events) per launch
         wave_steps = units / 64

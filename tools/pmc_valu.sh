@@ -10,9 +10,9 @@ export TMPDIR=/tmp
 C="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
 cd /tmp
 for c in $CFGS; do
-  timeout -s KILL 180 rocprofv3 --pmc $C --output-format csv -d "$OUT/cfg$c" -o k -- python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/cfg$c.log" 2>&1 || { echo "cfg $c failed"; tail "$OUT/cfg$c.log"; exit 1; }
+  timeout -s KILL 180 rocprofv3 --pmc $C --output-format csv -d "$OUT/cfg$c" -o k -- python3 "$ROOT/bench.py" --config $c ${PMC_STEPS:---steps 3 --warmup 1} --no-cpu-baseline > "$OUT/cfg$c.log" 2>&1 || { echo "cfg $c failed"; tail "$OUT/cfg$c.log"; exit 1; }
   # per-kernel durations of the same command (configs with more than one kernel per step)
-  timeout -s KILL 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt$c" -o k -- python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/kt$c.log" 2>&1 || { echo "kt $c failed"; tail "$OUT/kt$c.log"; exit 1; }
+  timeout -s KILL 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt$c" -o k -- python3 "$ROOT/bench.py" --config $c ${PMC_STEPS:---steps 3 --warmup 1} --no-cpu-baseline > "$OUT/kt$c.log" 2>&1 || { echo "kt $c failed"; tail "$OUT/kt$c.log"; exit 1; }
   echo "cfg $c ok"
 done
 cd "$ROOT"
