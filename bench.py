@@ -971,14 +971,16 @@ def bf_plan(n, world, sym, mem_bytes=32 << 30):
         r15.search_class_width(n, 'f64', mem_bytes, sym)
 
 
-def bf_level_bytes(n, w, sym):
+def bf_level_bytes(n, w, sym, pair='auto'):
     """Level-buffer bytes of one class search of n - w free candidates: every stored node (the
     C(m-2, k) subsets of size k whose largest free candidate is <= m - 3) written once and read
-    once as a parent; the one-launch head (sizes 1 .. K) stores only its level K, and the end
-    launch (sizes k_end .. m) reads level k_end - 1 and stores none."""
+    once as a parent; the one-launch head (sizes 1 .. K) stores only its level K, a pair launch
+    only its second level (KF_OPT_SEARCH_PAIR), and the end launch (sizes k_end .. m) reads level
+    k_end - 1 and stores none (kfmi.ref15.search_plan)."""
     from kfmi.ref15 import search_level_bytes, search_stored_levels
     m = n - w
-    return 2 * sum(search_level_bytes(math.comb(m - 2, k), 'f64', sym) for k in search_stored_levels(m))
+    return 2 * sum(search_level_bytes(math.comb(m - 2, k), 'f64', sym)
+                   for k in search_stored_levels(m, sym=sym, pair=pair))
 
 
 def bf_workload(cfg, args, rank, world, dev):
@@ -1148,7 +1150,7 @@ def bf_workload(cfg, args, rank, world, dev):
     launches = info['level_launches'] + (1 if K else 0)
     k_end = r15.search_end_size(m)
     classes_here = len(mine)
-    per_class = bf_level_bytes(n, w, sym)
+    per_class = bf_level_bytes(n, w, sym, pair=cfg.get('opts', {}).get('search_pair', 'auto'))
     lvl_bytes = per_class * classes_here
     subsets_here = total_combos if world == 1 else sum(2 ** m for _ in mine) - (1 if 0 in mine else 0)
     chains = ('axis-symmetric: one pva and one aw chain computed and stored for the three of each, '
@@ -1181,8 +1183,9 @@ def bf_workload(cfg, args, rank, world, dev):
                 desc=f'SURVEY 8f row 1: exhaustive brute-force search, n={n} candidate events '
                      f'({"kf_workers.py:2311" if n == 25 else "kf_workers_visualizing.py:2293, 2340"}), '
                      f'all 2^{n}-1 subsets, reference 15-state model, f64, shared-prefix search (one event step + '
-                     f'final predict per subset, sizes 1..{K} in one launch, then one launch per level, sizes '
-                     f'{k_end}..{m} in one: {launches} launches per class search; {chains}); {split}; '
+                     f'final predict per subset, sizes 1..{K} in one launch, then one launch per level or per two '
+                     f'parent-major levels, sizes {k_end}..{m} in one: {launches} launches per class search; {chains}); '
+                     f'{split}; '
                      f'value = subsets/s of ONE search' + (f' split over {world} ranks' if world > 1 else ''),
                 extra={'candidate_events': n, 'combinations': total_combos, 'levels': n, 'search': info,
                        'classes': 1 << w, 'classes_this_rank': classes_here, 'free_candidates_per_class': m})

@@ -153,6 +153,11 @@ const char* kf_version(void);
  *   KF_OPT_SEARCH_END     kf_search_combos: 0 = the last levels (sizes whose subsets need few event
  *                         steps from a stored prefix) in one launch, one lane per subset from its
  *                         stored prefix; 1 = level by level
+ *   KF_OPT_SEARCH_PAIR    kf_search_combos, axis-symmetric: 0 = a parent-major level with at least
+ *                         2^22 stored parents and the next level in one launch (the first level's
+ *                         nodes kept in LDS, never stored: half the level traffic); 1 = one level
+ *                         per launch; 2 = pair every parent-major level; >= 1024 = pair the levels
+ *                         with at least that many stored parents
  *   KF_OPT_AXIS_SYM       0 = where the handle's noise constants are the same on every axis
  *                         (the reference's), work that depends on the constants alone is done
  *                         once for the axes' identical chains: kf_run_stream's covariance maps
@@ -195,7 +200,8 @@ const char* kf_version(void);
 #define KF_OPT_SEARCH_HEAD    15
 #define KF_OPT_AXIS_SYM       16
 #define KF_OPT_SEARCH_END     17
-#define KF_OPT_COUNT          18
+#define KF_OPT_SEARCH_PAIR    18
+#define KF_OPT_COUNT          19
 int kf_set_option(kf_batch* handle, int option, int64_t value);
 int kf_get_option(const kf_batch* handle, int option, int64_t* value);
 

@@ -114,6 +114,10 @@ constexpr uint64_t kSearchHeadSteps = 400000;
 // the end launch covers the last sizes whose subsets' event steps from their stored prefixes add
 // up to at most this many (n = 25: sizes 20 .. 25 from level 19, 86,712 steps for 68,406 subsets)
 constexpr uint64_t kSearchEndSteps = 200000;
+// KF_OPT_SEARCH_PAIR = 0: parent-major levels with at least this many stored parents run paired
+// with the next level (each parent's lane walks its children and their children in sequence, so
+// a pair launch needs many more lanes than a level launch to fill the chip)
+constexpr uint64_t kSearchPairParents = uint64_t(1) << 22;
 
 int64_t opt(const kf_batch* h, int o) { return h->opt[o]; }
 
@@ -413,6 +417,7 @@ int kf_set_option(kf_batch* h, int option, int64_t value) {
         case KF_OPT_SEARCH_PM:
         case KF_OPT_SEARCH_HEAD:
         case KF_OPT_SEARCH_END: ok = value == 0 || value == 1; break;
+        case KF_OPT_SEARCH_PAIR: ok = value == 0 || value == 1 || value == 2 || value >= 1024; break;
         case KF_OPT_AXIS_SYM: ok = value == 0 || value == 1; break;
         case KF_OPT_SCHED_KERNEL: ok = value >= 0 && value <= 4; break;
         case KF_OPT_SCHED_GROUP: ok = value == 0 || value == 1 || value == 4; break;
@@ -1302,6 +1307,7 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
     hipError_t e = ctr_zero ? hipSuccess : hipMemsetAsync(sw, 0, head, st);
     if (e != hipSuccess) return hip_fail(e, "kf_search_combos: clear");
     char* lv[2] = {sw + head, sw + head + level};
+    int cur = 0;  // the buffer holding the last stored level (its children go to the other one)
     uint64_t best[kMaxComboEvents + 1] = {}, acc[kMaxComboEvents + 1] = {};
     int found = 0, last = 0;
     // the head: levels 1 .. K in one launch, one lane per subset (launch_ref15_search_head), K the
@@ -1336,7 +1342,7 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.target_end = target_end;
         a.threshold = threshold;
         kfmi::set_search_band(a, h->dtype == KF_F64);
-        a.child = lv[K & 1];
+        a.child = lv[cur = K & 1];
         a.best = d_best;
         a.n_acc = d_acc;
         a.subset_max = subset_max;
@@ -1374,6 +1380,12 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
     // not exhaustive: the results are peeked after groups of 1, 1, 2, 4, ... level launches, and
     // a launch queued past the first accepted size does nothing (Ref15SearchArgs::stop_best)
     int peek_at = k_first, peek_step = 1;
+    // KF_OPT_SEARCH_PAIR: an axis-symmetric parent-major level k with at least pair_min stored
+    // parents and level k + 1 in one launch (launch_ref15_search_pair), level k never stored;
+    // level k + 1 below the end launch's sizes
+    const int64_t pair_opt = opt(h, KF_OPT_SEARCH_PAIR);
+    const bool pairs = pair_opt != 1 && sym && opt(h, KF_OPT_SEARCH_PM) == 0;
+    const uint64_t pair_min = pair_opt == 0 ? kSearchPairParents : pair_opt == 2 ? 0 : uint64_t(pair_opt);
     for (int k = k_first; k <= kf_max; ++k) {
         kfmi::Ref15SearchArgs a{};
         a.kc = h->kc;
@@ -1393,8 +1405,8 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
         a.target_end = target_end;
         a.threshold = threshold;
         kfmi::set_search_band(a, h->dtype == KF_F64);
-        a.par = k > 1 ? lv[(k - 1) & 1] : nullptr;
-        a.child = k < kf_max ? lv[k & 1] : nullptr;
+        a.par = k > 1 ? lv[cur] : nullptr;
+        a.child = k < kf_max ? lv[1 - cur] : nullptr;
         a.best = d_best;
         a.n_acc = d_acc;
         a.subset_max = subset_max;
@@ -1437,14 +1449,24 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
             break;
         }
         // a level without stored parents was scored whole by the previous launch's tail
-        if (a.n_par) {
+        if (a.n_par && pairs && k >= 2 && k + 1 <= kf_max && k + 1 < k_end0 && a.n_par >= pair_min &&
+            !search_child_major(h, a.n_par)) {
+            // levels k and k + 1: level k + 1 stored (in the other buffer) when it has children
+            a.child = k + 1 < kf_max ? lv[1 - cur] : nullptr;
+            a.tail = k + 1 < kf_max;
+            e = kfmi::launch_ref15_search_pair(h->dtype == KF_F64, a, st);
+            if (e != hipSuccess) return hip_fail(e, "kf_search_combos: pair launch");
+            ++launches;
+            ++k;
+        } else if (a.n_par) {
             a.pm_regs = opt(h, KF_OPT_SEARCH_PM) == 1;
             e = kfmi::launch_ref15_search(h->dtype == KF_F64, a, search_child_major(h, a.n_par), st);
             if (e != hipSuccess) return hip_fail(e, "kf_search_combos: level launch");
             ++launches;
         }
+        if (a.n_par && a.child) cur = 1 - cur;
         last = k_base + k;
-        if (!exhaustive && k == peek_at && k < kf_max) {
+        if (!exhaustive && k >= peek_at && k < kf_max) {
             // the reference stops at the first size with an acceptable subset (the first launch
             // also scores the fixed root itself, size k_base)
             e = kfmi::launch_search_finish(d_best, h->search_host_dev, kMaxComboEvents + 1, false, st);

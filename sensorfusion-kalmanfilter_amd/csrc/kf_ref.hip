@@ -2485,19 +2485,48 @@ struct ParLds {
     __device__ __forceinline__ T operator()(int i) const { return col[i * 64]; }
 };
 
-template <typename T, bool CUSTOM, bool SYM, class PS>
-__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const DetBand<T>& band,
-                                             const SearchNode<T, CUSTOM, SYM>& par, const PS& pp, int j, uint64_t c,
-                                             uint64_t& best, uint64_t& cnt, uint64_t& best1, uint64_t& cnt1) {
+// Where search_child_to puts the child it computed: a level buffer's node (LevelSink: level k,
+// stored for the next launch), or a lane's LDS column and registers (LdsSink: the pair kernel's
+// level k, read back at once as the parent of level k + 1).  Either way the bits are the same.
+template <typename T, bool SYM>
+struct LevelSink {
+    char* cb;
+    uint32_t cl;
+    bool on;
+    __device__ __forceinline__ void row(int i, T v) const { *level_row<T>(cb, cl, i) = v; }
+    __device__ __forceinline__ void node(int nr, const DetV<T>& run, double prev, uint64_t mask) const {
+        *level_row<T>(cb, cl, nr) = run.m;
+        *level_exp<T, SYM>(cb, cl) = run.e;
+        *level_tail<T, SYM>(cb, cl, 0) = prev;
+        *level_tail<T, SYM>(cb, cl, 1) = __builtin_bit_cast(double, mask);
+    }
+};
+template <typename T>
+struct LdsSink {
+    T* col;  // row i at col[i * 64]
+    bool on;
+    DetV<T> run;
+    double prev;
+    uint64_t mask;
+    __device__ __forceinline__ void row(int i, T v) const { col[i * 64] = v; }
+    __device__ __forceinline__ void node(int, const DetV<T>& r, double p, uint64_t m) {
+        run = r;
+        prev = p;
+        mask = m;
+    }
+};
+
+template <typename T, bool CUSTOM, bool SYM, class PS, class SK>
+__device__ __forceinline__ void search_child_to(const Ref15SearchArgs& a, const DetBand<T>& band,
+                                                const SearchNode<T, CUSTOM, SYM>& par, const PS& pp, int j, SK& sk,
+                                                bool tail, uint64_t& best, uint64_t& cnt, uint64_t& best1,
+                                                uint64_t& cnt1) {
     using Node = SearchNode<T, CUSTOM, SYM>;
     constexpr int RP = SYM ? M15::NP : 1, RA = SYM ? M15::NA : 1;  // chains each computed one stands for
     const SearchEvent vs = search_event(a, j, par.prev);
-    const bool store = a.child && j < a.n_events - 2;
-    const bool tail = a.tail && j == a.n_events - 2;  // wave-uniform (j is)
+    const bool store = sk.on;
     SearchEvent vg;
     if (tail) vg = search_event(a, j + 1, vs.prev);
-    char* cb = store ? level_block<T, SYM>(a.child, c) : nullptr;
-    const uint32_t cl = uint32_t(c) & 63u;
     SearchScore<T, CUSTOM> ss, sg;
     ss.kc = sg.kc = a.kc;
 #pragma unroll
@@ -2508,7 +2537,7 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Det
         search_pva<T, CUSTOM>(vs, ch, Pb, ss.ok, a.kc);
         if (store) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) *level_row<T>(cb, cl, 6 * ch + i) = Pb[i];
+            for (int i = 0; i < 6; ++i) sk.row(6 * ch + i, Pb[i]);
         }
         ss.add_pva(vs, Pb, ch, RP);
         if (tail) {
@@ -2525,7 +2554,7 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Det
         search_aw<T, CUSTOM>(vs, ch, Pa, ss.ok, a.kc);
         if (store) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) *level_row<T>(cb, cl, 6 * Node::NP + 3 * ch + i) = Pa[i];
+            for (int i = 0; i < 3; ++i) sk.row(6 * Node::NP + 3 * ch + i, Pa[i]);
         }
         ss.add_aw(vs, Pa, ch, RA);
         if (tail) {
@@ -2537,18 +2566,23 @@ __device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const Det
     DetV<T> fmax;
     const DetV<T> run = ss.finish(vs, par.run, fmax);
     const uint64_t cmask = par.mask | (uint64_t(1) << (j + a.shift));
-    if (store) {
-        *level_row<T>(cb, cl, Node::NR) = run.m;
-        *level_exp<T, SYM>(cb, cl) = run.e;
-        *level_tail<T, SYM>(cb, cl, 0) = vs.prev;
-        *level_tail<T, SYM>(cb, cl, 1) = __builtin_bit_cast(double, cmask);
-    }
+    if (store) sk.node(Node::NR, run, vs.prev, cmask);
     search_score(a, band, cmask, fmax, best, cnt);
     if (tail) {
         DetV<T> gmax;
         (void)sg.finish(vg, run, gmax);
         search_score(a, band, cmask | (uint64_t(1) << (j + 1 + a.shift)), gmax, best1, cnt1);
     }
+}
+
+template <typename T, bool CUSTOM, bool SYM, class PS>
+__device__ __forceinline__ void search_child(const Ref15SearchArgs& a, const DetBand<T>& band,
+                                             const SearchNode<T, CUSTOM, SYM>& par, const PS& pp, int j, uint64_t c,
+                                             uint64_t& best, uint64_t& cnt, uint64_t& best1, uint64_t& cnt1) {
+    const bool store = a.child && j < a.n_events - 2;
+    LevelSink<T, SYM> sk{store ? level_block<T, SYM>(a.child, c) : nullptr, uint32_t(c) & 63u, store};
+    search_child_to<T, CUSTOM, SYM>(a, band, par, pp, j, sk, a.tail && j == a.n_events - 2,  // wave-uniform (j is)
+                                    best, cnt, best1, cnt1);
 }
 
 // one atomic pair per wave, and only from waves with an accepted subset; k = local level
@@ -2629,6 +2663,56 @@ ref15_search_pm_kernel(const Ref15SearchArgs a) {
     }
     search_publish(a, a.k, best, cnt);
     if (a.tail) search_publish(a, a.k + 1, best1, cnt1);
+}
+
+// Two levels per launch (KF_OPT_SEARCH_PAIR, the axis-symmetric search's parent-major levels):
+// lane p's parent (level k - 1, stored), each of its children (level k) computed into the lane's
+// LDS column — not stored — and, at once, that child's children (level k + 1) from the column,
+// stored as the next launch's parents.  Each subset's operations are search_child's and a child
+// reaches its children with the bits a stored node would carry, so every score and every stored
+// node is the one-level search's; level k's nodes (half the level traffic) never reach HBM.  A
+// child holding event n - 2 has one child (it plus n - 1), scored by its tail as size k + 1.
+template <typename T, bool CUSTOM, bool SYM>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KF_SEARCH_SYM_WAVES))) void
+ref15_search_pair_kernel(const Ref15SearchArgs a) {
+    if (search_stopped(a)) return;
+    constexpr int NR = SearchNode<T, CUSTOM, SYM>::NR;
+    const int64_t p = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
+    if (uint64_t(p) >= a.n_par) return;
+    const int n = a.n_events, k = a.k;
+    const DetBand<T> band(a);
+    SearchNode<T, CUSTOM, SYM> par;
+    par.load(a.par, uint64_t(p));
+    const int m = par.max_event(a.shift);
+    const int j0 = wave_uniform(m) + 1;  // colex order: the first lane holds the smallest max
+    __shared__ T sP[NR * 64];
+    __shared__ T sC[NR * 64];
+    T* col = sP + threadIdx.x;
+    T* ccol = sC + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) col[i * 64] = par.P[i];  // read back by this lane only
+    const ParLds<T> pp{col}, cp{ccol};
+    uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0, best2 = 0, cnt2 = 0;
+#pragma unroll 1
+    for (int j = j0; j < n; ++j) {
+        if (j <= m) continue;
+        LdsSink<T> sk{ccol, j < n - 2};
+        search_child_to<T, CUSTOM, SYM>(a, band, par, pp, j, sk, j == n - 2, best, cnt, best1, cnt1);
+        if (j < n - 2) {  // wave-uniform
+            SearchNode<T, CUSTOM, SYM> ch;
+            ch.run = sk.run;
+            ch.prev = sk.prev;
+            ch.mask = sk.mask;
+            const uint64_t c = uint64_t(p) + a.binom[j * (kMaxEvents + 1) + k];  // the child's rank at level k
+#pragma unroll 1
+            for (int j2 = j + 1; j2 < n; ++j2)
+                search_child<T, CUSTOM, SYM>(a, band, ch, cp, j2, c + a.binom[j2 * (kMaxEvents + 1) + k + 1], best1,
+                                             cnt1, best2, cnt2);
+        }
+    }
+    search_publish(a, k, best, cnt);
+    search_publish(a, k + 1, best1, cnt1);
+    if (a.tail) search_publish(a, k + 2, best2, cnt2);
 }
 
 // The head of the search: levels 1 .. K (a.k = K) in ONE launch, one lane per subset of at most
@@ -4140,6 +4224,19 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
                 else ref15_search_pm_kernel<float, false, CUSTOM, false><<<grid, kBlock, 0, stream>>>(a);
             }
         }
+    });
+    return hipGetLastError();
+}
+
+hipError_t launch_ref15_search_pair(bool f64, const Ref15SearchArgs& a, hipStream_t stream) {
+    // levels k and k + 1 < n of the axis-symmetric search, from level k - 1's stored parents
+    if (!a.sym || a.n_events > kMaxEvents || a.k < 2 || a.k + 1 > a.n_events || a.n_par == 0 ||
+        a.n_par >= (1ull << 28) || !a.par)
+        return hipErrorInvalidValue;
+    const dim3 grid(static_cast<unsigned>((a.n_par + 63) / 64));
+    KF_CUSTOM_DISPATCH(a.kc, {
+        if (f64) ref15_search_pair_kernel<double, CUSTOM, true><<<grid, 64, 0, stream>>>(a);
+        else ref15_search_pair_kernel<float, CUSTOM, true><<<grid, 64, 0, stream>>>(a);
     });
     return hipGetLastError();
 }

@@ -55,7 +55,8 @@ KF_OPT_SCHED_REC_TIME = 14
 KF_OPT_SEARCH_HEAD = 15
 KF_OPT_AXIS_SYM = 16
 KF_OPT_SEARCH_END = 17
-KF_OPT_COUNT = 18
+KF_OPT_SEARCH_PAIR = 18
+KF_OPT_COUNT = 19
 
 _ERRNAMES = {KF_EINVAL: 'KF_EINVAL', KF_EHIP: 'KF_EHIP', KF_ENOTSPD: 'KF_ENOTSPD',
              KF_ENODEV: 'KF_ENODEV', KF_ENOMEM: 'KF_ENOMEM'}

@@ -683,25 +683,63 @@ def search_end_size(n, k_max=None, head=True):
     return end
 
 
-def search_launches(n, k_max=None):
-    """Kernel launches of one kf_search_combos over n free candidates: the head (if any), every
-    later level with stored parents (a level with none is scored by the previous tail) up to the
-    end launch, and the end launch (if any)."""
+SEARCH_CM_PARENTS = 200000  # kf_capi.cpp kSearchChildMajorParents: levels with more parents run parent-major
+SEARCH_PAIR_PARENTS = 1 << 22  # kf_capi.cpp kSearchPairParents: KF_OPT_SEARCH_PAIR = 0 pairs levels with as many
+
+
+def _pair_min(pair):
+    """Least stored parents of a paired level for a KF_OPT_SEARCH_PAIR value (None: no pairs)."""
+    pair = {'auto': 0, 'off': 1, 'all': 2, True: 0, False: 1}.get(pair, pair)
+    return None if pair == 1 else SEARCH_PAIR_PARENTS if pair == 0 else 0 if pair == 2 else int(pair)
+
+
+def search_plan(n, k_max=None, sym=False, pair='auto'):
+    """kf_search_combos' launches over n free candidates, exhaustive (kf_capi.cpp): the head
+    (sizes 1 .. K, if any), then per level k with stored parents a level launch, or — axis-
+    symmetric, a parent-major level k (more than SEARCH_CM_PARENTS parents, and at least the pair
+    option's minimum: SEARCH_PAIR_PARENTS by default) whose level k + 1 is below the end launch's
+    sizes — one pair launch for levels k and k + 1 (KF_OPT_SEARCH_PAIR = pair),
+    then the end launch (if any).  Returns (launches [(kind, k)], stored levels: the levels
+    whose nodes a launch writes and the next one reads, once each)."""
     k_max = n if k_max is None else k_max
     K = search_head_size(n, k_max)
     end = search_end_size(n, k_max)
-    levels = [k for k in range(1, min(k_max, end - 1) + 1) if k == 1 or math.comb(n - 2, k - 1) > 0]
-    return (1 if K else 0) + sum(1 for k in levels if k > K) + (1 if end <= k_max else 0)
+    pmin = _pair_min(pair)
+    launches, stored = [], []
+    if K:
+        launches.append(('head', K))
+        stored.append(K)
+    k = K + 1 if K else 1
+    while k <= k_max:
+        if k == end:
+            launches.append(('end', k))
+            break
+        par = 1 if k == 1 else math.comb(n - 2, k - 1)
+        if (par and pmin is not None and sym and k >= 2 and par > SEARCH_CM_PARENTS and par >= pmin
+                and k + 1 <= k_max and k + 1 < end):
+            launches.append(('pair', k))
+            if k + 1 < k_max:
+                stored.append(k + 1)
+            k += 2
+            continue
+        if par:
+            launches.append(('level', k))
+            if k < k_max:
+                stored.append(k)
+        k += 1
+    return launches, stored
 
 
-def search_stored_levels(n, k_max=None):
-    """The levels whose nodes one kf_search_combos writes once and reads once as parents: from
-    the head's last size (or 1) up to the level before the end launch (which reads that level and
-    stores nothing), or to the last level with children."""
-    k_max = n if k_max is None else k_max
-    K = search_head_size(n, k_max)
-    end = search_end_size(n, k_max)
-    return list(range(max(K, 1), min(end, k_max)))
+def search_launches(n, k_max=None, sym=False, pair='auto'):
+    """Kernel launches of one kf_search_combos over n free candidates (search_plan)."""
+    return len(search_plan(n, k_max, sym, pair)[0])
+
+
+def search_stored_levels(n, k_max=None, sym=False, pair='auto'):
+    """The levels whose nodes one kf_search_combos writes once and reads once as parents
+    (search_plan): the head's last size, each level launch's below k_max, each pair launch's
+    second level; the end launch stores none."""
+    return search_plan(n, k_max, sym, pair)[1]
 
 
 def search_levels(n, dtype='f64', mem_bytes=32 << 30, sym=False):

@@ -371,7 +371,7 @@ def test_search_launch_bookkeeping(golden_dir, n):
     info = kf.search_info()
     kf.close()
     assert info['head_sizes'] == ref15.search_head_size(n)
-    assert info['level_launches'] + (1 if info['head_sizes'] else 0) == ref15.search_launches(n)
+    assert info['level_launches'] + (1 if info['head_sizes'] else 0) == ref15.search_launches(n, sym=info['sym'])
 
 
 def test_search_end_random_shapes(golden_dir):

@@ -165,3 +165,37 @@ def test_n40_driver_winner_vs_reference_search():
     for key in ('log_determinants', 'final_state', 'trajectory'):
         a, b = np.asarray(got[key], np.float64), np.asarray(ref[key], np.float64)
         assert a.shape == b.shape and np.max(np.abs(a - b) / np.maximum(np.abs(b), 1.0)) <= 1e-6, key
+
+
+@pytest.mark.parametrize('n,dtype', [(25, 'f64'), (28, 'f64'), (25, 'f32')])
+def test_pair_launches_equal_single_levels(n, dtype):
+    """KF_OPT_SEARCH_PAIR (2: every parent-major level paired): two levels per launch (the first
+    kept in LDS, never stored) give every subset's score bit for bit as one level per launch, and the same winners
+    and acceptance counts, whole and by class, exhaustive and not; the launches are the Python
+    mirror's (ref15.search_plan), and a pair launch stores half the level nodes."""
+    ev, init, _, t0, t_end = bench.bf_events(n)
+    res = {}
+    for pair in ('all', 'off'):
+        kf = kfmi.BatchedKF('ref15', 1, dtype, options={'search_pair': pair})
+        _, _, _, sm = kf.search_combos(ev, init, t0, t_end, -1e30, exhaustive=True, subset_max=True)
+        info = kf.search_info()
+        assert info['sym']
+        plan, stored = ref15.search_plan(n, sym=True, pair=pair)
+        assert info['level_launches'] + (1 if info['head_sizes'] else 0) == len(plan)
+        out = [sm.cpu()]
+        thrs = _thresholds(sm, (1e-4, 0.02, 0.5))
+        for thr in thrs:
+            for exhaustive in (True, False):
+                out.append(kf.search_combos(ev, init, t0, t_end, thr, exhaustive=exhaustive)[:3])
+                out.append(ref15.search_combos_classed(kf, ev, init, t0, t_end, thr, 3, exhaustive=exhaustive)[:3])
+        res[pair] = (out, plan, stored)
+        kf.close()
+    a, b = res['all'][0], res['off'][0]
+    key = torch.int64 if dtype == 'f64' else torch.int32
+    assert torch.equal(a[0].view(key), b[0].view(key))
+    for x, y in zip(a[1:], b[1:]):
+        assert x[:2] == y[:2]
+        np.testing.assert_array_equal(x[2], y[2])
+    assert any(kind == 'pair' for kind, _ in res['all'][1])
+    nodes = lambda st: sum(math.comb(n - 2, k) for k in st)  # noqa: E731
+    assert nodes(res['all'][2]) < 0.6 * nodes(res['off'][2])
