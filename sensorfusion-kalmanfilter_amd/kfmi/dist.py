@@ -107,15 +107,16 @@ _NONE = (1 << 63) - 1
 
 def search_classes(n, world, dtype='f64', mem_bytes=32 << 30, sym=False):
     """Shard plan of the shared-prefix search over ``world`` ranks: the subsets are split by their
-    intersection with the first w candidates (2^w classes of 2^(n-w) subsets each), class c going
-    to rank c % world.  w = the larger of the rank rule (the smallest w with 2^w >= 4 world, at
-    most n - 1; 0 for one rank) and the memory rule (ref15.search_class_width: a class's every
-    size fits ``mem_bytes`` and the 2^28-parent cap), so no rank ever falls back to one filter
-    per subset.  Returns w."""
+    intersection with the first w candidates (2^w classes of 2^(n-w) subsets each, the same
+    work each), class c going to rank c % world.  w = the larger of the rank rule (the fewest
+    classes, at least one per rank, that deal out within 25 % of even: 2^w = world for a power of
+    two, 8 classes for 3 ranks; at most n - 1; 0 for one rank) and the memory rule
+    (ref15.search_class_width: a class's every size fits ``mem_bytes`` and the 2^28-parent cap),
+    so no rank ever falls back to one filter per subset.  Returns w."""
     from . import ref15
     w = 0
     if world > 1:
-        while (1 << w) < 4 * world and w < n - 1:
+        while w < n - 1 and ((1 << w) < world or -(-(1 << w) // world) * world * 4 > 5 * (1 << w)):
             w += 1
     return max(w, ref15.search_class_width(n, dtype, mem_bytes, sym))
 
@@ -125,8 +126,9 @@ def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, init
                        finish=None, search_mem_bytes=32 << 30, consts=None):
     """run_brute_force_kalman_filter_no_sampling_min_usage sharded over the ranks of ``group``
     with the shared-prefix search (kf_search_combos): the subsets are split into 2^w classes by
-    their intersection with the first w candidates (``search_classes``: enough classes for the
-    ranks and small enough for one search call each); each rank searches its classes, keeping
+    their intersection with the first w candidates (``search_classes``: enough classes to deal
+    out evenly over the ranks, each small enough for one search call); each rank searches its
+    classes, keeping
     the first size with an acceptable subset and its first such subset in itertools order, and
     two all-reduces (MIN of the size, then MAX of the bit-reversed subset mask at that size) pick
     the same winner as the single-GPU search.  Every rank returns the reference's result dict

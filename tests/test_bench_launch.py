@@ -95,7 +95,7 @@ def test_bench_two_ranks_on_the_gpu(config):
         rec = _bench_ranks(2, config, ['--steps', '1', '--warmup', '0' if config == 'bf40' else '1'])
         assert rec['scaling'] == 'strong' and rec['unit'] == 'subsets/s'
         ds = rec['dist_search']
-        assert ds['one_rank_equal'] and ds['k_found'] >= 2 and ds['classes'] >= 8
+        assert ds['one_rank_equal'] and ds['k_found'] >= 2 and ds['classes'] >= 2
         assert ds['winner'] == ds['one_rank']['winner']
         assert rec['config']['classes'] == ds['classes'] and rec['config']['classes_this_rank'] == ds['classes'] // 2
         if config == 'bf':

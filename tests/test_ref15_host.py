@@ -220,10 +220,15 @@ def test_search_class_width_fits_every_size():
             widest = max(math.comb(m - 2, k) for k in range(1, m - 1))
             assert 2 * ref15.search_level_bytes(widest, 'f64', sym) + 4096 <= 32 << 30
             assert all(math.comb(m - 2, k - 1) < 1 << 28 for k in range(2, m + 1))
-    # the sharded plan never goes below the memory rule, nor below 4 classes per rank
+    # the sharded plan never goes below the memory rule, nor below one class per rank dealt out
+    # within 25 % of even
     from kfmi import dist as kdist
     assert kdist.search_classes(40, 8, sym=True) == 8 and kdist.search_classes(40, 1) == 10
-    assert kdist.search_classes(25, 8) == 5 and kdist.search_classes(25, 1) == 0
+    assert kdist.search_classes(25, 8) == 3 and kdist.search_classes(25, 1) == 0
+    assert [kdist.search_classes(25, r) for r in (2, 3, 4, 5, 6, 7, 8, 16)] == [1, 3, 2, 3, 4, 5, 3, 4]
+    for r in range(2, 33):
+        c = 1 << kdist.search_classes(25, r)
+        assert c >= r and -(-c // r) <= 1.25 * c / r
 
 
 @pytest.mark.parametrize('w', [0, 1, 3, 5])
