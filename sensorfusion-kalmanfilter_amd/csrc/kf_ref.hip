@@ -2250,53 +2250,8 @@ struct SearchNode {
     double prev;
     uint64_t mask;
 
-    // The root: the search's fixed events (a.root_mask, none for a whole search) applied to the
-    // initial filter in index order as the worker applies a combination's events
-    // (kf_workers.py:36-71); record 0 is the logdet of the initial covariance (:32).  With
-    // `eval`, the root subset itself is also scored (its max log-det with the final predict).
-    __device__ __forceinline__ DetV<T> root(const Ref15SearchArgs& a, bool eval) {
-        Ref15<T, CUSTOM> r;
-        r.kc = a.kc;
-#pragma unroll
-        for (int i = 0; i < 15; ++i) r.x[i] = T(a.init[i]);
-#pragma unroll
-        for (int i = 0; i < 27; ++i) r.blk(i) = T(a.init[15 + i]);
-        run.m = r.det_mant(run.e);
-        if (!run.valid()) run.fail();
-        if (run.m == T(0)) run.e = kNanLoses;
-        prev = a.prev_time;
-        mask = a.root_mask;
-        const T no_gate = T(0);
-        for (uint64_t rest = a.root_mask; rest; rest &= rest - 1) {
-            const double* e = a.ev_all + __builtin_ctzll(rest) * 11;
-            const double dtd = e[0] - prev;
-            if (dtd < 0.0) continue;  // kf_workers.py:38-40
-            T pay[9];
-#pragma unroll
-            for (int i = 0; i < 9; ++i) pay[i] = T(e[2 + i]);
-            bool ok = true;
-            r.event(int(e[1]), T(dtd), pay, false, no_gate, ok);
-            DetV<T> d;
-            d.m = r.det_mant(d.e);
-            d.e = d.valid() && d.m != T(0) ? d.e : kNanLoses;
-            run = dmax(d, run);
-            if (!ok) run.fail();
-            prev = e[0];
-        }
-#pragma unroll
-        for (int i = 0; i < 6 * NP; ++i) P[i] = r.blk(i);
-#pragma unroll
-        for (int i = 0; i < 3 * NA; ++i) P[6 * NP + i] = r.blk(6 * M15::NP + i);
-        DetV<T> fmax = run;
-        if (eval && prev < a.target_end - 1e-8) {  // kf_workers.py:74-82
-            r.predict(T(a.target_end - prev));
-            DetV<T> d;
-            d.m = r.det_mant(d.e);
-            d.e = d.valid() && d.m != T(0) ? d.e : kNanLoses;
-            fmax = dmax(d, run);
-        }
-        return fmax;
-    }
+    // The root (defined after search_child_to, whose operations it applies to the fixed events)
+    __device__ __forceinline__ DetV<T> root(const Ref15SearchArgs& a, bool eval);
     __device__ __forceinline__ void load(const void* level, uint64_t p) {
         char* blk = level_block<T, SYM>(level, p);
         const uint32_t lane = uint32_t(p) & 63u;
@@ -2516,7 +2471,26 @@ struct LdsSink {
     }
 };
 
-template <typename T, bool CUSTOM, bool SYM, class PS, class SK>
+// A class root's prefix nodes (SearchNode::root): the child's rows and scalars in registers,
+// with its score's determinant (fmax) instead of a scoring
+template <typename T, int NR>
+struct RegSink {
+    T P[NR];
+    bool on;
+    DetV<T> run, fmax;
+    double prev;
+    uint64_t mask;
+    __device__ __forceinline__ void row(int i, T v) { P[i] = v; }
+    __device__ __forceinline__ void node(int, const DetV<T>& r, double p, uint64_t m) {
+        run = r;
+        prev = p;
+        mask = m;
+    }
+};
+
+// SCORE = false: the child is not scored (nor is a tail computed); its max with the final predict
+// goes to sk.fmax (RegSink)
+template <typename T, bool CUSTOM, bool SYM, class PS, class SK, bool SCORE = true>
 __device__ __forceinline__ void search_child_to(const Ref15SearchArgs& a, const DetBand<T>& band,
                                                 const SearchNode<T, CUSTOM, SYM>& par, const PS& pp, int j, SK& sk,
                                                 bool tail, uint64_t& best, uint64_t& cnt, uint64_t& best1,
@@ -2567,12 +2541,63 @@ __device__ __forceinline__ void search_child_to(const Ref15SearchArgs& a, const 
     const DetV<T> run = ss.finish(vs, par.run, fmax);
     const uint64_t cmask = par.mask | (uint64_t(1) << (j + a.shift));
     if (store) sk.node(Node::NR, run, vs.prev, cmask);
-    search_score(a, band, cmask, fmax, best, cnt);
-    if (tail) {
-        DetV<T> gmax;
-        (void)sg.finish(vg, run, gmax);
-        search_score(a, band, cmask | (uint64_t(1) << (j + 1 + a.shift)), gmax, best1, cnt1);
+    if constexpr (SCORE) {
+        search_score(a, band, cmask, fmax, best, cnt);
+        if (tail) {
+            DetV<T> gmax;
+            (void)sg.finish(vg, run, gmax);
+            search_score(a, band, cmask | (uint64_t(1) << (j + 1 + a.shift)), gmax, best1, cnt1);
+        }
+    } else {
+        sk.fmax = fmax;
     }
+}
+
+// The root: the search's fixed events (a.root_mask, none for a whole search) applied to the
+// initial filter in index order as the worker applies a combination's events
+// (kf_workers.py:36-71); record 0 is the logdet of the initial covariance (:32).  Each fixed
+// event is applied with search_child_to's operations, from the node its predecessors made, so a
+// class root is bit for bit the node the whole search computes for that subset (its prefixes are
+// not scored: they belong to other classes).  With `eval`, returns the root subset's max log-det
+// with the final predict (as a determinant) for the caller to score.
+template <typename T, bool CUSTOM, bool SYM>
+__device__ __forceinline__ DetV<T> SearchNode<T, CUSTOM, SYM>::root(const Ref15SearchArgs& a, bool eval) {
+    Ref15<T, CUSTOM> r;
+    r.kc = a.kc;
+#pragma unroll
+    for (int i = 0; i < 15; ++i) r.x[i] = T(a.init[i]);
+#pragma unroll
+    for (int i = 0; i < 27; ++i) r.blk(i) = T(a.init[15 + i]);
+    run.m = r.det_mant(run.e);
+    if (!run.valid()) run.fail();
+    if (run.m == T(0)) run.e = kNanLoses;
+    prev = a.prev_time;
+    mask = 0;
+#pragma unroll
+    for (int i = 0; i < 6 * NP; ++i) P[i] = r.blk(i);
+#pragma unroll
+    for (int i = 0; i < 3 * NA; ++i) P[6 * NP + i] = r.blk(6 * M15::NP + i);
+    DetV<T> fmax = run;
+    if (a.root_mask) {
+        const DetBand<T> band(a);
+        for (uint64_t rest = a.root_mask; rest; rest &= rest - 1) {
+            RegSink<T, NR> sk;
+            sk.on = true;
+            uint64_t b0 = 0, c0 = 0, b1 = 0, c1 = 0;
+            // j = the candidate's index relative to the free ones (negative: a.ev + 11 j is the
+            // fixed event's row of a.ev_all)
+            search_child_to<T, CUSTOM, SYM, ParRegs<T>, RegSink<T, NR>, false>(
+                a, band, *this, ParRegs<T>{P}, __builtin_ctzll(rest) - a.shift, sk, false, b0, c0, b1, c1);
+#pragma unroll
+            for (int i = 0; i < NR; ++i) P[i] = sk.P[i];
+            run = sk.run;
+            prev = sk.prev;
+            mask = sk.mask;
+            fmax = sk.fmax;
+        }
+    }
+    (void)eval;
+    return fmax;
 }
 
 template <typename T, bool CUSTOM, bool SYM, class PS>

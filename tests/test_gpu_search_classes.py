@@ -199,3 +199,39 @@ def test_pair_launches_equal_single_levels(n, dtype):
     assert any(kind == 'pair' for kind, _ in res['all'][1])
     nodes = lambda st: sum(math.comb(n - 2, k) for k in st)  # noqa: E731
     assert nodes(res['all'][2]) < 0.6 * nodes(res['off'][2])
+
+
+@pytest.mark.parametrize('case', ['golden_every_chain', 'custom_sym', 'custom_asym_f32'])
+def test_classed_search_other_chains_and_constants(golden_dir, case):
+    """The class split over the reference's own log (candidates out of time order, so negative
+    dt skips) with every chain, and over caller constants (class_args) axis-symmetric and not, f64
+    and f32: every subset's score bitwise the whole search's, and the whole search's winners and
+    counts at three thresholds, exhaustive and not — the pair launches included where they run."""
+    from test_gpu_ref15 import _search_case, _symmetric_consts
+    n = 24
+    if case == 'golden_every_chain':
+        _, ev, init, t0, t_end = _search_case(golden_dir, n)
+        dtype, params, opts = 'f64', None, {'axis_sym': 'off'}
+    else:
+        ev, init, _, t0, t_end = bench.bf_events(n)
+        c = _symmetric_consts(11)
+        if case == 'custom_asym_f32':
+            q = c.q.copy()
+            q[13] *= 1.5   # the y axis's acceleration noise: every chain
+            c = ref15.ModelConsts('ref15', q=q, r_imu=c.r_imu, r_gps=c.r_gps, p0=c.p0)
+        dtype, params, opts = ('f32' if case.endswith('f32') else 'f64'), c.params(), {'search_pair': 'all'}
+    kf = kfmi.BatchedKF('ref15', 1, dtype, params=params, options=opts)
+    _, _, _, whole = kf.search_combos(ev, init, t0, t_end, -1e30, exhaustive=True, subset_max=True)
+    assert kf.search_info()['sym'] == (case == 'custom_sym')
+    key = torch.int64 if dtype == 'f64' else torch.int32
+    for w in (2, 5):
+        _, _, _, sm = ref15.search_combos_classed(kf, ev, init, t0, t_end, -1e30, w, exhaustive=True, subset_max=True)
+        assert torch.equal(sm.view(key), whole.view(key)), (case, w)
+        del sm
+        for thr in _thresholds(whole, (1e-4, 0.02, 0.5)):
+            for exhaustive in (True, False):
+                want = kf.search_combos(ev, init, t0, t_end, thr, exhaustive=exhaustive)
+                got = ref15.search_combos_classed(kf, ev, init, t0, t_end, thr, w, exhaustive=exhaustive)
+                assert got[:2] == want[:2], (case, w, thr, exhaustive)
+                np.testing.assert_array_equal(got[2], want[2])
+    kf.close()
