@@ -2303,8 +2303,18 @@ __device__ __forceinline__ void search_score(const Ref15SearchArgs& a, const Det
 // Event j applied to a node whose last applied event is at prev_in (kf_workers.py:36-82): a
 // negative dt skips the event and keeps the time; the worker's final predict to target_end runs
 // when the new time is before it.
+// The search's read-only tables (events, binomials) read through the constant address space: a
+// wave-uniform entry then becomes a scalar load.  Through a generic pointer the compiler cannot
+// prove that the kernel's level stores leave them alone, so it loads them with vector loads, whose
+// vmcnt wait also waits for every level store issued before them (vmcnt counts both, in order).
+// They are written by the host before the launch and never by a kernel.
+typedef __attribute__((address_space(4))) const double ro_double;
+typedef __attribute__((address_space(4))) const uint64_t ro_u64;
+__device__ __forceinline__ ro_double* ro(const double* p) { return (ro_double*)p; }
+__device__ __forceinline__ ro_u64* ro(const uint64_t* p) { return (ro_u64*)p; }
+
 struct SearchEvent {
-    const double* e;
+    ro_double* e;
     int type;
     bool step, final_predict;
     double dt, dte, prev;  // prev: the time after the event
@@ -2312,7 +2322,7 @@ struct SearchEvent {
 
 __device__ __forceinline__ SearchEvent search_event(const Ref15SearchArgs& a, int j, double prev_in) {
     SearchEvent v;
-    v.e = a.ev + j * 11;
+    v.e = ro(a.ev) + j * 11;
     v.type = int(v.e[1]);
     v.dt = v.e[0] - prev_in;
     v.step = v.dt >= 0.0;  // kf_workers.py:38-40
@@ -2674,7 +2684,7 @@ ref15_search_pm_kernel(const Ref15SearchArgs a) {
 #pragma unroll 1
         for (int j = j0; j < a.n_events; ++j) {
             if (j <= m) continue;
-            search_child<T, CUSTOM, SYM>(a, band, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best,
+            search_child<T, CUSTOM, SYM>(a, band, par, pp, j, uint64_t(p) + ro(a.binom)[j * (kMaxEvents + 1) + a.k], best,
                                          cnt, best1, cnt1);
         }
     } else {
@@ -2682,7 +2692,7 @@ ref15_search_pm_kernel(const Ref15SearchArgs a) {
 #pragma unroll 1
         for (int j = j0; j < a.n_events; ++j) {
             if (j <= m) continue;
-            search_child<T, CUSTOM, SYM>(a, band, par, pp, j, uint64_t(p) + a.binom[j * (kMaxEvents + 1) + a.k], best,
+            search_child<T, CUSTOM, SYM>(a, band, par, pp, j, uint64_t(p) + ro(a.binom)[j * (kMaxEvents + 1) + a.k], best,
                                          cnt, best1, cnt1);
         }
     }
@@ -2728,10 +2738,10 @@ ref15_search_pair_kernel(const Ref15SearchArgs a) {
             ch.run = sk.run;
             ch.prev = sk.prev;
             ch.mask = sk.mask;
-            const uint64_t c = uint64_t(p) + a.binom[j * (kMaxEvents + 1) + k];  // the child's rank at level k
+            const uint64_t c = uint64_t(p) + ro(a.binom)[j * (kMaxEvents + 1) + k];  // the child's rank at level k
 #pragma unroll 1
             for (int j2 = j + 1; j2 < n; ++j2)
-                search_child<T, CUSTOM, SYM>(a, band, ch, cp, j2, c + a.binom[j2 * (kMaxEvents + 1) + k + 1], best1,
+                search_child<T, CUSTOM, SYM>(a, band, ch, cp, j2, c + ro(a.binom)[j2 * (kMaxEvents + 1) + k + 1], best1,
                                              cnt1, best2, cnt2);
         }
     }
@@ -2903,7 +2913,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEA
     const uint64_t ext = a.gblk[lo];
     const int e = __builtin_ctzll(ext);
     const int ex = e == n - 1 ? n - 2 : e;  // E = {n - 1}: the stored prefixes only
-    const uint64_t n_pre = a.binom[ex * (kMaxEvents + 1) + K0 - 1];
+    const uint64_t n_pre = ro(a.binom)[ex * (kMaxEvents + 1) + K0 - 1];
     const uint64_t rp = (w - a.gitem[lo]) * 64 + threadIdx.x;
     const bool live = rp < n_pre;
     uint64_t best = 0, cnt = 0;
@@ -2960,7 +2970,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEA
     const uint64_t item = uint64_t(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
     if (item >= n_items) return;
     const int n = a.n_events, k = a.k;
-    const uint64_t* C = a.binom;
+    ro_u64* C = ro(a.binom);
     auto binom = [&](int x, int y) -> uint64_t { return x < 0 ? (y == 0 ? 1 : 0) : C[x * (kMaxEvents + 1) + y]; };
     // the item's group (the host's table in the kernel arguments: a binary search over
     // constant-cache loads, instead of a walk whose every step waited on a binomial load)
