@@ -29,6 +29,19 @@
 namespace kfmi {
 namespace {
 
+// Read-only device tables (the handle's custom constants, a search's events and binomials) read
+// through the constant address space: a wave-uniform entry then becomes a scalar load.  Through a
+// generic pointer the compiler cannot prove that a kernel's own stores leave them alone, so it
+// loads them with vector loads, whose vmcnt wait also waits for every store issued before them
+// (on gfx950 vmcnt counts loads and stores, in order).  Every such table is written by the host
+// before the launch and never by a kernel.
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(4))) const T* ro(const T* p) {
+    return (__attribute__((address_space(4))) const T*)p;
+}
+typedef __attribute__((address_space(4))) const double ro_double;
+typedef __attribute__((address_space(4))) const uint64_t ro_u64;
+
 using namespace dev;
 
 constexpr int kGps = 0, kImu = 1;  // KF_EVENT_GPS / KF_EVENT_IMU; 2 = predict only, 255 = none
@@ -91,11 +104,11 @@ template <bool CUSTOM, class M, typename T>
 __device__ __forceinline__ void pva_noise(const RefConsts* kc, int c, T (&q)[3], T (&r)[6], T& rg) {
     if constexpr (CUSTOM) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) q[k] = T(kc->q[M::pva(c, k)]);
-        r[0] = T(kc->r_imu[M::pva(c, 0)]);
-        r[3] = T(kc->r_imu[M::pva(c, 1)]);
-        r[5] = T(kc->r_imu[M::pva(c, 2)]);
-        rg = T(kc->r_gps[c]);
+        for (int k = 0; k < 3; ++k) q[k] = T(ro(kc)->q[M::pva(c, k)]);
+        r[0] = T(ro(kc)->r_imu[M::pva(c, 0)]);
+        r[3] = T(ro(kc)->r_imu[M::pva(c, 1)]);
+        r[5] = T(ro(kc)->r_imu[M::pva(c, 2)]);
+        rg = T(ro(kc)->r_gps[c]);
     } else {
         q[0] = T(kQPos);
         q[1] = T(kQVel);
@@ -110,10 +123,10 @@ __device__ __forceinline__ void pva_noise(const RefConsts* kc, int c, T (&q)[3],
 template <bool CUSTOM, class M, typename T>
 __device__ __forceinline__ void aw_noise(const RefConsts* kc, int c, T (&q)[2], T (&r)[3]) {
     if constexpr (CUSTOM) {
-        q[0] = T(kc->q[M::aw(c, 0)]);
-        q[1] = T(kc->q[M::aw(c, 1)]);
-        r[0] = T(kc->r_imu[M::aw(c, 0)]);
-        r[2] = T(kc->r_imu[M::aw(c, 1)]);
+        q[0] = T(ro(kc)->q[M::aw(c, 0)]);
+        q[1] = T(ro(kc)->q[M::aw(c, 1)]);
+        r[0] = T(ro(kc)->r_imu[M::aw(c, 0)]);
+        r[2] = T(ro(kc)->r_imu[M::aw(c, 1)]);
     } else {
         q[0] = T(kQAtt);
         q[1] = T(kQRate);
@@ -306,14 +319,14 @@ struct Chains {
         if constexpr (CUSTOM) {  // P0 = diag(p0) in the model's state order
 #pragma unroll
             for (int c = 0; c < M::NP; ++c) {
-                pva[c][0] = T(kc->p0[M::pva(c, 0)]);
-                pva[c][3] = T(kc->p0[M::pva(c, 1)]);
-                pva[c][5] = T(kc->p0[M::pva(c, 2)]);
+                pva[c][0] = T(ro(kc)->p0[M::pva(c, 0)]);
+                pva[c][3] = T(ro(kc)->p0[M::pva(c, 1)]);
+                pva[c][5] = T(ro(kc)->p0[M::pva(c, 2)]);
             }
 #pragma unroll
             for (int c = 0; c < M::NA; ++c) {
-                aw[c][0] = T(kc->p0[M::aw(c, 0)]);
-                aw[c][2] = T(kc->p0[M::aw(c, 1)]);
+                aw[c][0] = T(ro(kc)->p0[M::aw(c, 0)]);
+                aw[c][2] = T(ro(kc)->p0[M::aw(c, 1)]);
             }
         }
     }
@@ -743,10 +756,10 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
 #pragma unroll
         for (int k = 0; k < 3; ++k)
             if (xi[k] >= 0) {
-                q[k] = T(kc->q[xi[k]]);
-                Rimu[k == 0 ? 0 : k == 1 ? 3 : 5] = T(kc->r_imu[xi[k]]);
+                q[k] = T(ro(kc)->q[xi[k]]);
+                Rimu[k == 0 ? 0 : k == 1 ? 3 : 5] = T(ro(kc)->r_imu[xi[k]]);
             }
-        if (pva) Rgps = T(kc->r_gps[ca]);
+        if (pva) Rgps = T(ro(kc)->r_gps[ca]);
     }
 
     T x[NL][3], P[6];
@@ -1584,10 +1597,10 @@ __device__ __forceinline__ void chain_noise(int ch, double (&q)[3], double (&si_
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const int i = chain_state<M>(ch, k);
-            q[k] = i >= 0 ? kc->q[i] : 0.0;
-            si_imu[k] = i >= 0 ? 1.0 / kc->r_imu[i] : 0.0;
+            q[k] = i >= 0 ? ro(kc)->q[i] : 0.0;
+            si_imu[k] = i >= 0 ? 1.0 / ro(kc)->r_imu[i] : 0.0;
         }
-        si_gps = pva ? 1.0 / kc->r_gps[ch] : 0.0;
+        si_gps = pva ? 1.0 / ro(kc)->r_gps[ch] : 0.0;
         return;
     }
     q[0] = pva ? kQPos : kQAtt;
@@ -2303,16 +2316,7 @@ __device__ __forceinline__ void search_score(const Ref15SearchArgs& a, const Det
 // Event j applied to a node whose last applied event is at prev_in (kf_workers.py:36-82): a
 // negative dt skips the event and keeps the time; the worker's final predict to target_end runs
 // when the new time is before it.
-// The search's read-only tables (events, binomials) read through the constant address space: a
-// wave-uniform entry then becomes a scalar load.  Through a generic pointer the compiler cannot
-// prove that the kernel's level stores leave them alone, so it loads them with vector loads, whose
-// vmcnt wait also waits for every level store issued before them (vmcnt counts both, in order).
-// They are written by the host before the launch and never by a kernel.
-typedef __attribute__((address_space(4))) const double ro_double;
-typedef __attribute__((address_space(4))) const uint64_t ro_u64;
-__device__ __forceinline__ ro_double* ro(const double* p) { return (ro_double*)p; }
-__device__ __forceinline__ ro_u64* ro(const uint64_t* p) { return (ro_u64*)p; }
-
+// the search's events are read through ro() (the table above `ro`): scalar loads in the child loops
 struct SearchEvent {
     ro_double* e;
     int type;
