@@ -1138,6 +1138,7 @@ def bf_workload(cfg, args, rank, world, dev):
             out['one_rank_equal'] = ok
             if not ok:
                 raise SystemExit(f'the {world}-rank search disagrees with the one-rank search: {out}')
+        kf_one.close()
         return out
 
     kf_one = kfmi.BatchedKF('ref15', 64, 'f64', device=dev.index) if world > 1 else None  # scores of the 1-subsets
