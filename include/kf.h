@@ -156,8 +156,10 @@ const char* kf_version(void);
  *   KF_OPT_SEARCH_PAIR    kf_search_combos, axis-symmetric: 0 = a parent-major level with at least
  *                         2^22 stored parents and the next level in one launch (the first level's
  *                         nodes kept in LDS, never stored: half the level traffic); 1 = one level
- *                         per launch; 2 = pair every parent-major level; >= 1024 = pair the levels
- *                         with at least that many stored parents
+ *                         per launch; 2 = pair every parent-major level; 3 = pair every level
+ *                         child-major, a wave per parent block and child event (measured slower;
+ *                         A/B only); >= 1024 = pair the parent-major levels with at least that
+ *                         many stored parents
  *   KF_OPT_AXIS_SYM       0 = where the handle's noise constants are the same on every axis
  *                         (the reference's), work that depends on the constants alone is done
  *                         once for the axes' identical chains: kf_run_stream's covariance maps

@@ -114,9 +114,10 @@ constexpr uint64_t kSearchHeadSteps = 400000;
 // the end launch covers the last sizes whose subsets' event steps from their stored prefixes add
 // up to at most this many (n = 25: sizes 20 .. 25 from level 19, 86,712 steps for 68,406 subsets)
 constexpr uint64_t kSearchEndSteps = 200000;
-// KF_OPT_SEARCH_PAIR = 0: parent-major levels with at least this many stored parents run paired
-// with the next level (each parent's lane walks its children and their children in sequence, so
-// a pair launch needs many more lanes than a level launch to fill the chip)
+// KF_OPT_SEARCH_PAIR = 0: levels with at least this many stored parents pair with the next level
+// parent-major (each parent's lane walks its children and their children in sequence, so such a
+// launch needs many more lanes than a level launch to fill the chip), narrower ones child-major
+// 
 constexpr uint64_t kSearchPairParents = uint64_t(1) << 22;
 
 int64_t opt(const kf_batch* h, int o) { return h->opt[o]; }
@@ -417,7 +418,7 @@ int kf_set_option(kf_batch* h, int option, int64_t value) {
         case KF_OPT_SEARCH_PM:
         case KF_OPT_SEARCH_HEAD:
         case KF_OPT_SEARCH_END: ok = value == 0 || value == 1; break;
-        case KF_OPT_SEARCH_PAIR: ok = value == 0 || value == 1 || value == 2 || value >= 1024; break;
+        case KF_OPT_SEARCH_PAIR: ok = (value >= 0 && value <= 3) || value >= 1024; break;
         case KF_OPT_AXIS_SYM: ok = value == 0 || value == 1; break;
         case KF_OPT_SCHED_KERNEL: ok = value >= 0 && value <= 4; break;
         case KF_OPT_SCHED_GROUP: ok = value == 0 || value == 1 || value == 4; break;
@@ -1380,12 +1381,15 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
     // not exhaustive: the results are peeked after groups of 1, 1, 2, 4, ... level launches, and
     // a launch queued past the first accepted size does nothing (Ref15SearchArgs::stop_best)
     int peek_at = k_first, peek_step = 1;
-    // KF_OPT_SEARCH_PAIR: an axis-symmetric parent-major level k with at least pair_min stored
-    // parents and level k + 1 in one launch (launch_ref15_search_pair), level k never stored;
-    // level k + 1 below the end launch's sizes
+    // KF_OPT_SEARCH_PAIR: in the axis-symmetric search, level k and level k + 1 (below the end
+    // launch's sizes) in one launch (launch_ref15_search_pair), level k never stored: parent-major
+    // (a lane per parent) for a level of at least pm_min stored parents; with 3, every level
+    // child-major instead (a wave per parent block and child event; measured slower: A/B only)
     const int64_t pair_opt = opt(h, KF_OPT_SEARCH_PAIR);
-    const bool pairs = pair_opt != 1 && sym && opt(h, KF_OPT_SEARCH_PM) == 0;
-    const uint64_t pair_min = pair_opt == 0 ? kSearchPairParents : pair_opt == 2 ? 0 : uint64_t(pair_opt);
+    const bool pairs = pair_opt != 1 && sym && opt(h, KF_OPT_SEARCH_PM) == 0 && opt(h, KF_OPT_SEARCH_KERNEL) == 0;
+    const uint64_t pm_min = pair_opt == 0 ? kSearchPairParents : pair_opt == 2 ? 0 : pair_opt == 3 ? ~uint64_t(0)
+                                                                                                   : uint64_t(pair_opt);
+    const bool cm_pairs = pair_opt == 3;
     for (int k = k_first; k <= kf_max; ++k) {
         kfmi::Ref15SearchArgs a{};
         a.kc = h->kc;
@@ -1449,12 +1453,12 @@ int kf_search_combos(kf_batch* h, int n_events, const double* events, const doub
             break;
         }
         // a level without stored parents was scored whole by the previous launch's tail
-        if (a.n_par && pairs && k >= 2 && k + 1 <= kf_max && k + 1 < k_end0 && a.n_par >= pair_min &&
-            !search_child_major(h, a.n_par)) {
+        const bool pm_pair = !search_child_major(h, a.n_par) && a.n_par >= pm_min;
+        if (a.n_par && pairs && k >= 2 && k + 1 <= kf_max && k + 1 < k_end0 && (pm_pair || cm_pairs)) {
             // levels k and k + 1: level k + 1 stored (in the other buffer) when it has children
             a.child = k + 1 < kf_max ? lv[1 - cur] : nullptr;
             a.tail = k + 1 < kf_max;
-            e = kfmi::launch_ref15_search_pair(h->dtype == KF_F64, a, st);
+            e = kfmi::launch_ref15_search_pair(h->dtype == KF_F64, a, !pm_pair, st);
             if (e != hipSuccess) return hip_fail(e, "kf_search_combos: pair launch");
             ++launches;
             ++k;

@@ -356,8 +356,9 @@ hipError_t launch_ref15_combos(bool f64, const Ref15ComboArgs& a, hipStream_t st
 // child_major: one wave per (parent block, child event) instead of one lane per parent
 hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream);
 // levels a.k and a.k + 1 in one launch (axis-symmetric search): level a.k - 1's stored parents,
-// their children computed into LDS and never stored, the children's children stored in a.child
-hipError_t launch_ref15_search_pair(bool f64, const Ref15SearchArgs& a, hipStream_t stream);
+// their children computed into LDS and never stored, the children's children stored in a.child;
+// child_major: one wave per (parent block, child event) item, else one lane per parent
+hipError_t launch_ref15_search_pair(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream);
 // the acceptance band of a search's threshold (Ref15SearchArgs::band_*), for its dtype
 void set_search_band(Ref15SearchArgs& a, bool f64);
 // levels 1 .. a.k of a search in one launch (one lane per subset of at most a.k free events)

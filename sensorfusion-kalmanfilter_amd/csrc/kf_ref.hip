@@ -2966,7 +2966,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEA
 // contiguous ranges, so the items that read one parent block run back to back on one XCD and
 // re-read it from that XCD's L2.  Blocks are grouped by their first parent's largest event v
 // (non-decreasing in colex order); a block of group v has items j = v + 1 .. n - 1.
-template <typename T, bool CUSTOM, bool SYM>
+// PAIR (the axis-symmetric search, KF_OPT_SEARCH_PAIR): levels k and k + 1 in one launch — each
+// lane's child j (level k) computed into its LDS column, never stored, then that child's children
+// j2 > j (level k + 1) from the column, stored as the next launch's parents, as the parent-major
+// pair kernel does; the items keep this kernel's parallelism (a parent block per child event).
+template <typename T, bool CUSTOM, bool SYM, bool PAIR = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEARCH_SYM_WAVES : 3))) void ref15_search_cm_kernel(const Ref15SearchArgs a,
                                                                                                      uint64_t n_items) {
     if (search_stopped(a)) return;
@@ -3008,10 +3012,36 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SYM ? KF_SEA
         par.load(a.par, p);
     }
     uint64_t best = 0, cnt = 0, best1 = 0, cnt1 = 0;
-    if (par.max_event(a.shift) < j)
-        search_child<T, CUSTOM, SYM>(a, band, par, ParRegs<T>{par.P}, j, p + binom(j, k), best, cnt, best1, cnt1);
-    search_publish(a, a.k, best, cnt);
-    if (a.tail) search_publish(a, a.k + 1, best1, cnt1);
+    if constexpr (PAIR) {
+        constexpr int NR = SearchNode<T, CUSTOM, SYM>::NR;
+        __shared__ T sC[NR * 64];
+        T* ccol = sC + threadIdx.x;
+        uint64_t best2 = 0, cnt2 = 0;
+        if (par.max_event(a.shift) < j) {
+            LdsSink<T> sk{ccol, j < n - 2};
+            // a child holding n - 2 has the one child adding n - 1: its tail, size k + 1
+            search_child_to<T, CUSTOM, SYM>(a, band, par, ParRegs<T>{par.P}, j, sk, j == n - 2, best, cnt, best1, cnt1);
+            if (j < n - 2) {  // wave-uniform (j is)
+                SearchNode<T, CUSTOM, SYM> ch;
+                ch.run = sk.run;
+                ch.prev = sk.prev;
+                ch.mask = sk.mask;
+                const uint64_t c = p + binom(j, k);  // the child's rank at level k
+#pragma unroll 1
+                for (int j2 = j + 1; j2 < n; ++j2)
+                    search_child<T, CUSTOM, SYM>(a, band, ch, ParLds<T>{ccol}, j2, c + binom(j2, k + 1), best1, cnt1,
+                                                 best2, cnt2);
+            }
+        }
+        search_publish(a, k, best, cnt);
+        search_publish(a, k + 1, best1, cnt1);
+        if (a.tail) search_publish(a, k + 2, best2, cnt2);
+    } else {
+        if (par.max_event(a.shift) < j)
+            search_child<T, CUSTOM, SYM>(a, band, par, ParRegs<T>{par.P}, j, p + binom(j, k), best, cnt, best1, cnt1);
+        search_publish(a, a.k, best, cnt);
+        if (a.tail) search_publish(a, a.k + 1, best1, cnt1);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -4198,6 +4228,36 @@ hipError_t launch_ref15_search_head(bool f64, const Ref15SearchArgs& a, hipStrea
     return hipGetLastError();
 }
 
+// The child-major kernel's work items: per group v of parent blocks, blocks x (n - 1 - v) child
+// events; group v holds blocks [ceil(C(v, k-1)/64), ceil(C(v+1, k-1)/64)) (the stored parents
+// have largest event <= n - 3).  Fills b's group table; false when the items overflow.
+static bool cm_items(const Ref15SearchArgs& a, Ref15SearchArgs& b, uint64_t& items, uint64_t& waves) {
+    const uint64_t* C = a.binom_host;
+    const int n = a.n_events, k = a.k;
+    b = a;
+    items = 0;
+    if (k == 1) {
+        items = uint64_t(n);
+        b.n_groups = 0;
+    } else {
+        b.v_lo = k - 2;
+        int i = 0;
+        for (int v = k - 2; v <= n - 3; ++v, ++i) {
+            const uint64_t b0 = (C[v * (kMaxEvents + 1) + k - 1] + 63) / 64;
+            const uint64_t b1 = (C[(v + 1) * (kMaxEvents + 1) + k - 1] + 63) / 64;
+            b.gitem[i] = items;
+            b.gblk[i] = b0;
+            const uint64_t span = (b1 - b0) * uint64_t(n - 1 - v);
+            if (span >= (1ull << 31)) return false;  // 32-bit item offsets in a group
+            items += span;
+        }
+        b.n_groups = i;
+        if (i == 0) return false;
+    }
+    waves = (items + 7) / 8 * 8;
+    return waves < (1ull << 31);
+}
+
 hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream) {
     // the stored parents (kf_search_combos' cap); a level's children C(n, k) may be many more
     // (n = 40, k = 10: 8.5e8): child ranks and node addresses are 64-bit, and only the children
@@ -4205,33 +4265,9 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
     if (a.n_events > kMaxEvents || a.k < 1 || a.k > a.n_events || a.n_par == 0 || a.n_par >= (1ull << 28))
         return hipErrorInvalidValue;
     if (child_major) {
-        // work items: per group v of parent blocks, blocks x (n - 1 - v) child events; group v
-        // holds blocks [ceil(C(v, k-1)/64), ceil(C(v+1, k-1)/64)) (the stored parents have
-        // largest event <= n - 3)
-        const uint64_t* C = a.binom_host;
-        const int n = a.n_events, k = a.k;
-        Ref15SearchArgs b = a;
-        uint64_t items = 0;
-        if (k == 1) {
-            items = uint64_t(n);
-            b.n_groups = 0;
-        } else {
-            b.v_lo = k - 2;
-            int i = 0;
-            for (int v = k - 2; v <= n - 3; ++v, ++i) {
-                const uint64_t b0 = (C[v * (kMaxEvents + 1) + k - 1] + 63) / 64;
-                const uint64_t b1 = (C[(v + 1) * (kMaxEvents + 1) + k - 1] + 63) / 64;
-                b.gitem[i] = items;
-                b.gblk[i] = b0;
-                const uint64_t span = (b1 - b0) * uint64_t(n - 1 - v);
-                if (span >= (1ull << 31)) return hipErrorInvalidValue;  // 32-bit item offsets in a group
-                items += span;
-            }
-            b.n_groups = i;
-            if (i == 0) return hipErrorInvalidValue;
-        }
-        const uint64_t waves = (items + 7) / 8 * 8;
-        if (waves >= (1ull << 31)) return hipErrorInvalidValue;
+        Ref15SearchArgs b;
+        uint64_t items = 0, waves = 0;
+        if (!cm_items(a, b, items, waves)) return hipErrorInvalidValue;
         KF_CUSTOM_DISPATCH(a.kc, {
             if (a.sym) {
                 if (f64) ref15_search_cm_kernel<double, CUSTOM, true><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
@@ -4267,11 +4303,21 @@ hipError_t launch_ref15_search(bool f64, const Ref15SearchArgs& a, bool child_ma
     return hipGetLastError();
 }
 
-hipError_t launch_ref15_search_pair(bool f64, const Ref15SearchArgs& a, hipStream_t stream) {
-    // levels k and k + 1 < n of the axis-symmetric search, from level k - 1's stored parents
+hipError_t launch_ref15_search_pair(bool f64, const Ref15SearchArgs& a, bool child_major, hipStream_t stream) {
+    // levels k and k + 1 <= n of the axis-symmetric search, from level k - 1's stored parents
     if (!a.sym || a.n_events > kMaxEvents || a.k < 2 || a.k + 1 > a.n_events || a.n_par == 0 ||
         a.n_par >= (1ull << 28) || !a.par)
         return hipErrorInvalidValue;
+    if (child_major) {
+        Ref15SearchArgs b;
+        uint64_t items = 0, waves = 0;
+        if (!cm_items(a, b, items, waves)) return hipErrorInvalidValue;
+        KF_CUSTOM_DISPATCH(a.kc, {
+            if (f64) ref15_search_cm_kernel<double, CUSTOM, true, true><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
+            else ref15_search_cm_kernel<float, CUSTOM, true, true><<<dim3(unsigned(waves)), 64, 0, stream>>>(b, items);
+        });
+        return hipGetLastError();
+    }
     const dim3 grid(static_cast<unsigned>((a.n_par + 63) / 64));
     KF_CUSTOM_DISPATCH(a.kc, {
         if (f64) ref15_search_pair_kernel<double, CUSTOM, true><<<grid, 64, 0, stream>>>(a);

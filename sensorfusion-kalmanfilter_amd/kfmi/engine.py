@@ -41,7 +41,7 @@ OPTIONS = {
     'search_pm': (_lib.KF_OPT_SEARCH_PM, {'auto': 0, 'lds': 0, 'regs': 1}),
     'search_head': (_lib.KF_OPT_SEARCH_HEAD, {'auto': 0, 'on': 0, 'off': 1}),
     'search_end': (_lib.KF_OPT_SEARCH_END, {'auto': 0, 'on': 0, 'off': 1}),
-    'search_pair': (_lib.KF_OPT_SEARCH_PAIR, {'auto': 0, 'off': 1, 'all': 2}),
+    'search_pair': (_lib.KF_OPT_SEARCH_PAIR, {'auto': 0, 'off': 1, 'all': 2, 'cm': 3}),
     'axis_sym': (_lib.KF_OPT_AXIS_SYM, {'auto': 0, 'on': 0, 'off': 1}),
     'sched_kernel': (_lib.KF_OPT_SCHED_KERNEL, {'auto': 0, 'regs': 1, 'fused': 2, 'two_pass': 3, 'one_launch': 4}),
     'sched_group': (_lib.KF_OPT_SCHED_GROUP, {'auto': 0, 'wave': 1, 'block': 4}),

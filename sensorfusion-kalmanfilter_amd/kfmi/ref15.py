@@ -687,24 +687,29 @@ SEARCH_CM_PARENTS = 200000  # kf_capi.cpp kSearchChildMajorParents: levels with 
 SEARCH_PAIR_PARENTS = 1 << 22  # kf_capi.cpp kSearchPairParents: KF_OPT_SEARCH_PAIR = 0 pairs levels with as many
 
 
-def _pair_min(pair):
-    """Least stored parents of a paired level for a KF_OPT_SEARCH_PAIR value (None: no pairs)."""
-    pair = {'auto': 0, 'off': 1, 'all': 2, True: 0, False: 1}.get(pair, pair)
-    return None if pair == 1 else SEARCH_PAIR_PARENTS if pair == 0 else 0 if pair == 2 else int(pair)
+def _pair_policy(pair):
+    """(least parents of a parent-major pair, child-major pairs for the rest?) of a
+    KF_OPT_SEARCH_PAIR value, or None for no pairs (kf_capi.cpp)."""
+    pair = {'auto': 0, 'off': 1, 'all': 2, 'cm': 3, True: 0, False: 1}.get(pair, pair)
+    if pair == 1:
+        return None
+    pm_min = {0: SEARCH_PAIR_PARENTS, 2: 0, 3: None}.get(pair, int(pair))
+    return pm_min, pair == 3
 
 
 def search_plan(n, k_max=None, sym=False, pair='auto'):
     """kf_search_combos' launches over n free candidates, exhaustive (kf_capi.cpp): the head
-    (sizes 1 .. K, if any), then per level k with stored parents a level launch, or — axis-
-    symmetric, a parent-major level k (more than SEARCH_CM_PARENTS parents, and at least the pair
-    option's minimum: SEARCH_PAIR_PARENTS by default) whose level k + 1 is below the end launch's
-    sizes — one pair launch for levels k and k + 1 (KF_OPT_SEARCH_PAIR = pair),
-    then the end launch (if any).  Returns (launches [(kind, k)], stored levels: the levels
-    whose nodes a launch writes and the next one reads, once each)."""
+    (sizes 1 .. K, if any), then per level k with stored parents a level launch or — axis-
+    symmetric, level k + 1 below the end launch's sizes (KF_OPT_SEARCH_PAIR = pair) — one pair
+    launch for levels k and k + 1: parent-major ('pair') for a parent-major level (more than
+    SEARCH_CM_PARENTS parents) of at least the policy's parent count (SEARCH_PAIR_PARENTS by
+    default), child-major ('pair_cm') otherwise; then the end launch (if any).  Returns
+    (launches [(kind, k)], stored levels: the levels whose nodes a launch writes and the next one
+    reads, once each)."""
     k_max = n if k_max is None else k_max
     K = search_head_size(n, k_max)
     end = search_end_size(n, k_max)
-    pmin = _pair_min(pair)
+    pol = _pair_policy(pair) if sym else None
     launches, stored = [], []
     if K:
         launches.append(('head', K))
@@ -715,13 +720,14 @@ def search_plan(n, k_max=None, sym=False, pair='auto'):
             launches.append(('end', k))
             break
         par = 1 if k == 1 else math.comb(n - 2, k - 1)
-        if (par and pmin is not None and sym and k >= 2 and par > SEARCH_CM_PARENTS and par >= pmin
-                and k + 1 <= k_max and k + 1 < end):
-            launches.append(('pair', k))
-            if k + 1 < k_max:
-                stored.append(k + 1)
-            k += 2
-            continue
+        if par and pol is not None and k >= 2 and k + 1 <= k_max and k + 1 < end:
+            pm_pair = par > SEARCH_CM_PARENTS and pol[0] is not None and par >= pol[0]
+            if pm_pair or pol[1]:
+                launches.append(('pair' if pm_pair else 'pair_cm', k))
+                if k + 1 < k_max:
+                    stored.append(k + 1)
+                k += 2
+                continue
         if par:
             launches.append(('level', k))
             if k < k_max:

@@ -169,13 +169,13 @@ def test_n40_driver_winner_vs_reference_search():
 
 @pytest.mark.parametrize('n,dtype', [(25, 'f64'), (28, 'f64'), (25, 'f32')])
 def test_pair_launches_equal_single_levels(n, dtype):
-    """KF_OPT_SEARCH_PAIR (2: every parent-major level paired): two levels per launch (the first
-    kept in LDS, never stored) give every subset's score bit for bit as one level per launch, and the same winners
+    """KF_OPT_SEARCH_PAIR (auto; 2: every parent-major level paired parent-major; 3: every level
+    child-major): two levels per launch (the first kept in LDS, never stored) give every subset's score bit for bit as one level per launch, and the same winners
     and acceptance counts, whole and by class, exhaustive and not; the launches are the Python
     mirror's (ref15.search_plan), and a pair launch stores half the level nodes."""
     ev, init, _, t0, t_end = bench.bf_events(n)
     res = {}
-    for pair in ('all', 'off'):
+    for pair in ('auto', 'all', 'cm', 'off'):
         kf = kfmi.BatchedKF('ref15', 1, dtype, options={'search_pair': pair})
         _, _, _, sm = kf.search_combos(ev, init, t0, t_end, -1e30, exhaustive=True, subset_max=True)
         info = kf.search_info()
@@ -190,15 +190,20 @@ def test_pair_launches_equal_single_levels(n, dtype):
                 out.append(ref15.search_combos_classed(kf, ev, init, t0, t_end, thr, 3, exhaustive=exhaustive)[:3])
         res[pair] = (out, plan, stored)
         kf.close()
-    a, b = res['all'][0], res['off'][0]
     key = torch.int64 if dtype == 'f64' else torch.int32
-    assert torch.equal(a[0].view(key), b[0].view(key))
-    for x, y in zip(a[1:], b[1:]):
-        assert x[:2] == y[:2]
-        np.testing.assert_array_equal(x[2], y[2])
-    assert any(kind == 'pair' for kind, _ in res['all'][1])
+    b = res['off'][0]
     nodes = lambda st: sum(math.comb(n - 2, k) for k in st)  # noqa: E731
-    assert nodes(res['all'][2]) < 0.6 * nodes(res['off'][2])
+    for pair, kind in (('auto', 'pair'), ('all', 'pair'), ('cm', 'pair_cm')):
+        a = res[pair][0]
+        assert torch.equal(a[0].view(key), b[0].view(key)), pair
+        for x, y in zip(a[1:], b[1:]):
+            assert x[:2] == y[:2], pair
+            np.testing.assert_array_equal(x[2], y[2])
+        if pair == 'auto' and n < 28:  # no level of 2^22 parents: auto runs one level per launch
+            assert res[pair][1] == res['off'][1]
+            continue
+        assert any(kd == kind for kd, _ in res[pair][1]), pair
+        assert nodes(res[pair][2]) < 0.6 * nodes(res['off'][2]), pair
 
 
 @pytest.mark.parametrize('case', ['golden_every_chain', 'custom_sym', 'custom_asym_f32'])
