@@ -185,3 +185,47 @@ def test_scheduled_driver_on_the_ingested_list(csvs, method):
         assert len(st) == len(rs) > 10
         np.testing.assert_array_equal([s[0] for s in st], [r[0] for r in rs])
         assert _rel(st, rs) <= 1e-6 and _rel(ld, rl) <= 1e-6 and _rel(Pf, rP) <= 1e-6
+
+
+def test_visualizing_pipeline_n40_window(csvs):
+    """The reference's visualizing run (kf_workers_visualizing.py:2286-2340) on the synthetic
+    log: the adaptive filter up to start_idx, then the brute-force search over the next
+    start_offset = 40 events from its state and covariance — through the façade, against the
+    oracle's restatement of the reference's adaptive driver and search, at thresholds whose
+    winner has one and two events."""
+    from kfmi import ref15
+    sf = kfw.KF_SensorFusion(*csvs)
+    sf.load_data()
+    sf.gps_to_modified_utm()
+    bw, ba, _ = sf.compute_imu_biases(sf.gps_data, sf.imu_data)
+    sf.unbias_imu_data(bw, ba)
+    sf.combine_sensor_data()
+    events, _, _ = ref_ingest.ingest(*csvs)
+    start_idx, start_offset, r_value = 1200, 40, -10.0
+    st, ld, pt, _, _ = sf.run_adaptive_threshold_kalman_filter(end_idx=start_idx, R_threshold=r_value)
+    rst, rld, rpt, _, _ = ref_kf.run_adaptive_threshold(events, 0, start_idx, R_threshold=r_value)
+    assert _rel(st, rst) <= 1e-6 and _rel(pt, rpt) <= 1e-6
+    # thresholds from the single events' scores over this window (one filter per subset on the GPU)
+    cand, xt, Pt, prev, t_end, ev, init = ref15.brute_force_setup(events, start_idx, start_idx + start_offset,
+                                                                  rpt, tuple(rst[-1]))
+    assert len(cand) == start_offset
+    import kfmi
+    kf1 = kfmi.BatchedKF('ref15', 1024, 'f64')
+    s1 = np.sort(kf1.eval_combos(ev, init, prev, t_end, 1, logdets=False)[0][:start_offset].cpu().numpy())
+    s2 = np.sort(kf1.eval_combos(ev, init, prev, t_end, 2, logdets=False)[0][:780].cpu().numpy())
+    kf1.close()
+    cases = [((s1[2] + s1[3]) / 2, 1)]
+    if s2[0] < s1[0]:   # some pair beats every single event: a winner of two events
+        cases.append(((s2[0] + s1[0]) / 2, 2))
+    print(f'visualizing window at {start_idx}: winner sizes checked {[k for _, k in cases]}')
+    for thr, k_want in cases:
+        got = sf.run_brute_force_kalman_filter_no_sampling_min_usage(start_idx=start_idx,
+                                                                     end_idx=start_idx + start_offset,
+                                                                     initial_pt=pt, initial_state=st[-1],
+                                                                     R_threshold=thr)
+        ref = ref_kf.run_brute_force(events, start_idx, start_idx + start_offset, thr, rpt, tuple(rst[-1]))
+        sel = [e[0] for e in ref['selected_sensors']]
+        assert len(sel) == k_want
+        assert [e[0] for e in got['selected_sensors']] == sel
+        for key in ('log_determinants', 'final_state', 'trajectory'):
+            assert _rel(got[key], ref[key]) <= 1e-6, key
