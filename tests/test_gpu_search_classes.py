@@ -117,6 +117,18 @@ def test_n40_search_vs_per_subset():
                 break
         assert r is not None and kk == k, (thr, kk, k)
         assert tuple(ref15.unrank_combination(n, k, r)) == idx, (thr, k, r, idx)
+        # and against the C oracle (one filter per subset, the reference's dense step): the winner
+        # scores below the threshold, and sampled subsets before it — 4096 of every smaller size
+        # and 4096 of its size earlier in itertools order (ranks below r) — do not
+        rng = np.random.default_rng(k)
+        assert _combo_maxima(ev, Pw, t0, t_far, np.array([idx]))[0] < thr
+        for kk2 in range(1, k + 1):
+            hi = r if kk2 == k else math.comb(n, kk2)
+            ranks = np.unique(rng.integers(0, hi, 4096)) if hi > 4096 else np.arange(hi)
+            if not len(ranks):
+                continue
+            combos = np.array([ref15.unrank_combination(n, kk2, int(x)) for x in ranks])
+            assert (_combo_maxima(ev, Pw, t0, t_far, combos) >= thr).all(), (thr, kk2)
         print(f'n = 40, threshold {thr:.9f}: winner of size {k}: {idx}')
     kfe.close()
     kfs.close()
