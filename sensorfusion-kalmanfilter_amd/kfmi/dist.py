@@ -149,19 +149,32 @@ def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, init
     n = len(cand)
     kf = None
     sym = False
+    if finish is None:
+        def finish(k, idx):
+            return ref15.brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device,
+                                            indices=idx, consts=consts)
     if search_class is None:
         kf = ref15.BatchedKF('ref15', 1, dtype, device=device, params=ref15._params(consts))
         sym = kf.search_plan(init, n, k_max=1)['sym']
+        k_search = ref15.search_levels(n, dtype, search_mem_bytes, sym)
+        if k_search < n:
+            # a search too large for one call (n = 40): first its sizes 1 .. k_search in one call,
+            # the same on every rank (the reference's windows accept within them in milliseconds);
+            # only if none is accepted, every size by class over the ranks
+            try:
+                k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=k_search)
+            except BaseException:
+                kf.close()
+                raise
+            if k:
+                kf.close()
+                return finish(k, idx)
 
         def search_class(n_fixed, fixed_mask, k_max):
             k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=k_max,
                                             n_fixed=n_fixed, fixed_mask=fixed_mask)
             return k, idx
     w = search_classes(n, world, dtype, search_mem_bytes, sym)
-    if finish is None:
-        def finish(k, idx):
-            return ref15.brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device,
-                                            indices=idx, consts=consts)
     try:
         won = search_winner(search_class, n, w, group)
     finally:

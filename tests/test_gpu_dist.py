@@ -101,3 +101,32 @@ def test_brute_force_search_nccl_equals_gloo(groups, golden_dir, thr):
         assert pick(ra) == list(g['selected'])
     for key in ('final_state', 'log_determinants'):
         np.testing.assert_array_equal(np.asarray(ra[key]), np.asarray(rb[key]))
+
+
+def test_brute_force_search_n40_window_nccl(groups):
+    """The reference's 40-event window sharded through RCCL (world 1): the one-call sizes first,
+    then the class split; the same result dict as the one-GPU driver, at a threshold whose winner
+    has two events and at one past the one-call sizes (target far beyond the window, as in
+    tests/test_gpu_search_classes.py, through the events' own target: the window's last event)."""
+    import bench
+    from kfmi import ref15
+    nccl, _ = groups
+    n = 40
+    ev, init, Pw, t0, _ = bench.bf_events(n)
+    events = [(i, 'GPS', ev[i, 0], {'easting': ev[i, 2], 'northing': ev[i, 3], 'altitude': ev[i, 4]})
+              if ev[i, 1] == 0 else (i, 'IMU', ev[i, 0], ['t', *ev[i, 2:]]) for i in range(n)]
+    state0 = (t0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
+    import kfmi
+    kf1 = kfmi.BatchedKF('ref15', 64, 'f64')
+    s1 = np.sort(kf1.eval_combos(ev, init, t0, float(ev[-1, 0]), 1, logdets=False)[0][:n].cpu().numpy())
+    kf1.close()
+    L0 = float(np.linalg.slogdet(Pw)[1])
+    for thr in ((L0 + s1[0]) / 2, L0 - 1.0):   # a pair wins; nothing at all (every size by class)
+        kw = dict(R_threshold=thr, initial_pt=Pw, initial_state=state0)
+        a = kdist.brute_force_search(events, 0, n, group=nccl, **kw)
+        b = ref15.run_brute_force_kalman_filter_no_sampling_min_usage(events, 0, n, **kw)
+        if b is None:
+            assert a is None
+            continue
+        assert [e[0] for e in a['selected_sensors']] == [e[0] for e in b['selected_sensors']]
+        np.testing.assert_array_equal(np.asarray(a['log_determinants']), np.asarray(b['log_determinants']))
