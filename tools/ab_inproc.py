@@ -29,6 +29,7 @@ def main():
     ap.add_argument('--rounds', type=int, default=6)
     ap.add_argument('--rate-block', type=int, default=64, help='config sched: filters per processing rate')
     ap.add_argument('--launches', type=int, default=10)
+    ap.add_argument('--bf-n', type=int, default=None, help='config bf: candidate events (default the row\'s 25)')
     args = ap.parse_args()
     import torch
     import bench
@@ -55,6 +56,8 @@ def main():
             arms.append((a, h, None))
     cfg = dict(bench.CONFIGS[args.config])
     cfg['opts'] = {}
+    if args.bf_n:
+        cfg['n'] = args.bf_n
     ns = argparse.Namespace(ablate='none', gpus=1, no_cpu_baseline=True, rate_block=args.rate_block)
     if args.config in ('ref15', 'ref15f32'):
         w = bench.ref15_workload(cfg, ns, 0, 1, dev)
