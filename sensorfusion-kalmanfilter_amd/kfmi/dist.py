@@ -125,7 +125,9 @@ def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, init
                        max_combos_in_memory=1 << 22, dtype='f64', device=0, group=None, search_class=None,
                        finish=None, search_mem_bytes=32 << 30, consts=None):
     """run_brute_force_kalman_filter_no_sampling_min_usage sharded over the ranks of ``group``
-    with the shared-prefix search (kf_search_combos): the subsets are split into 2^w classes by
+    with the shared-prefix search (kf_search_combos): after the sizes that fit one call (the same
+    on every rank) and, past those, bands of prefix classes dealt over the ranks
+    (ref15.search_bands) while they are the fewer calls, the subsets are split into 2^w classes by
     their intersection with the first w candidates (``search_classes``: enough classes to deal
     out evenly over the ranks, each small enough for one search call); each rank searches its
     classes, keeping
@@ -149,6 +151,7 @@ def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, init
     n = len(cand)
     kf = None
     sym = False
+    k_search = n
     if finish is None:
         def finish(k, idx):
             return ref15.brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device,
@@ -176,7 +179,17 @@ def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, init
             return k, idx
     w = search_classes(n, world, dtype, search_mem_bytes, sym)
     try:
-        won = search_winner(search_class, n, w, group)
+        won = None
+        if kf is not None and k_search < n:
+            # the next sizes by bands of prefix classes dealt over the ranks, while those are
+            # fewer than the sharded fixed-pattern classes (ref15.search_past's order), then
+            # every size by the latter
+            for K, classes in ref15.search_bands(n, k_search, dtype, search_mem_bytes, sym, 1 << w):
+                won = search_winner(search_class, n, 0, group, classes=classes, k_max=K)
+                if won is not None:
+                    break
+        if won is None:
+            won = search_winner(search_class, n, w, group)
     finally:
         if kf is not None:
             kf.close()
@@ -195,20 +208,22 @@ def rank_classes(w, rank, world):
     return [c for c in ref15.class_order(w) if c % world == rank]
 
 
-def search_winner(search_class, n, w, group=None, exhaustive=False):
+def search_winner(search_class, n, w, group=None, exhaustive=False, classes=None, k_max=None):
     """The cross-rank half of ``brute_force_search``: this rank searches its classes
-    (``rank_classes``) through ``search_class(w, c, k_max) -> (k, indices or None)``, keeping the
-    smallest accepted size and, at it, the first subset in itertools.combinations order
-    (ref15.class_search: not exhaustive, a class searches only the sizes that can still win on
-    this rank); two all-reduces (MIN of the size, then MAX of the bit-reversed mask as two 32-bit
-    halves) give every rank the global winner (k, indices), or None when no class accepted a
-    subset."""
+    (``rank_classes``; or every world-th of ``classes``, e.g. ref15.prefix_classes' (n_fixed,
+    mask) pairs) through ``search_class(n_fixed, c, k_max) -> (k, indices or None)``, keeping the
+    smallest accepted size (up to ``k_max``) and, at it, the first subset in
+    itertools.combinations order (ref15.class_search: not exhaustive, a class searches only the
+    sizes that can still win on this rank); two all-reduces (MIN of the size, then MAX of the
+    bit-reversed mask as two 32-bit halves) give every rank the global winner (k, indices), or
+    None when no class accepted a subset."""
     import torch.distributed as dist
 
     from . import ref15
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     tdev = _tdev(group)
-    k_r, key_r = ref15.class_search(search_class, n, w, rank_classes(w, rank, world), exhaustive)
+    mine = rank_classes(w, rank, world) if classes is None else list(classes)[rank::world]
+    k_r, key_r = ref15.class_search(search_class, n, w, mine, exhaustive, k_max)
     if k_r is ref15.NO_SIZE:
         k_r = _NONE
     t = torch.tensor([k_r], dtype=torch.int64, device=tdev)

@@ -791,25 +791,92 @@ def class_order(w):
     return sorted(range(1 << w), key=lambda c: (bin(c).count('1'), c))
 
 
+def prefix_classes(n, k_max, dtype='f64', mem_bytes=32 << 30, sym=False, limit=None):
+    """Classes for the sizes up to ``k_max`` of a search whose levels do not fit one call, when
+    the fixed-pattern classes that fit every size (search_class_width) would be too many (n = 64:
+    2^32).  A class is a prefix P, its members fixed and its free candidates those after max(P):
+    kf_search_combos(n_fixed = max(P) + 1, fixed_mask = P), the subsets P + S, S within
+    max(P) + 1 .. n - 1.  From the whole search (P empty), a class whose free sizes up to
+    k_max - |P| do not fit one call (search_levels) is split by its next member f into the
+    classes P + {f}, f = max(P) + 1 .. n - 1, which hold every subset of the class but P itself
+    (the last, P + {n - 1}, as the class of P with the one free candidate n - 1).  Returns
+    ([(n_fixed, fixed_mask)], fewest fixed members first, and the largest |P| of a split class —
+    that subset is in no class: its size must have been searched already), or None past
+    ``limit`` classes.  n = 64, 32 GiB: 64 classes for sizes up to 8, 532 up to 9, 2623 up to 10."""
+    import functools
+    levels = functools.lru_cache(None)(lambda m: search_levels(m, dtype, mem_bytes, sym))
+    out, split = [], [-1]
+
+    def rec(a, mask, p):
+        if limit is not None and len(out) > limit:
+            return
+        if a == n:  # P + {n - 1}: the class of P over the one free candidate n - 1
+            out.append((n - 1, mask & ~(1 << (n - 1))))
+            return
+        if levels(n - a) >= min(k_max - p, n - a):
+            out.append((a, mask))
+            return
+        split[0] = max(split[0], p)
+        for f in range(a, n):
+            rec(f + 1, mask | (1 << f), p + 1)
+    rec(0, 0, 0)
+    if limit is not None and len(out) > limit:
+        return None
+    out.sort(key=lambda x: (bin(x[1]).count('1'), x[0], x[1]))
+    return out, split[0]
+
+
+def search_bands(n, k_done, dtype='f64', mem_bytes=32 << 30, sym=False, max_classes=None):
+    """The size bands of a search too large for one call whose sizes 1 .. k_done accepted
+    nothing: yields (K, prefix classes of the sizes up to K) for K = k_done + 1, k_done + 2, ...
+    while those are fewer than ``max_classes`` (the fixed-pattern classes that search every
+    size, which then finish the search: 256 at n = 40) and every subset a split leaves out has a
+    size already searched (<= k_done).  Each band searches its sizes again below K; a band holds
+    ~(n - K) / K times the subsets of the one before, so the repeats cost a fraction of the last."""
+    for K in range(k_done + 1, n + 1):
+        got = prefix_classes(n, K, dtype, mem_bytes, sym, limit=max_classes)
+        if got is None:
+            return
+        classes, split = got
+        if (max_classes is not None and len(classes) >= max_classes) or split > k_done:
+            return
+        yield K, classes
+
+
+def search_past(search_class, n, k_done, w, dtype='f64', mem_bytes=32 << 30, sym=False):
+    """The reference's pick (class_search's (k, key)) in a search of n candidates whose sizes
+    1 .. k_done accepted nothing and whose levels do not fit one call: the next sizes by bands of
+    prefix classes (search_bands) while those are fewer than the 2^w classes that fit every size
+    (search_class_width; n = 40: 40 classes for size 11, 151 up to 12, then the 256), then every
+    size by the latter.  ``search_class(n_fixed, fixed_mask, k_max)`` as class_search's."""
+    for K, classes in search_bands(n, k_done, dtype, mem_bytes, sym, 1 << w):
+        k, key = class_search(search_class, n, 0, classes, False, K)
+        if k is not NO_SIZE:
+            return k, key
+    return class_search(search_class, n, w, class_order(w))
+
+
 def class_search(search_class, n, w, classes, exhaustive=False, k_max=None):
-    """Runs ``search_class(w, c, k_max) -> (k, indices or None)`` for each class c in turn (the
-    subsets whose intersection with candidates 0 .. w - 1 is the bit pattern c) and keeps the
-    reference's pick among them (kf_workers.py:1325-1356): the smallest accepted size and, at it,
-    the first subset in itertools.combinations order, i.e. the largest bit-reversed mask.
-    Returns (k, key) or (NO_SIZE, 0).  Not exhaustive, a class searches only the sizes that can
-    still win: up to the best size so far (skipped when its fixed members alone exceed it; one
-    size above when they make exactly it, the least k_max kf_search_combos takes).  ``k_max``
-    caps the sizes searched (the reference's loop over sizes 1 .. n, :1325, cut short)."""
+    """Runs ``search_class(n_fixed, c, k_max) -> (k, indices or None)`` for each class in turn and
+    keeps the reference's pick among them (kf_workers.py:1325-1356): the smallest accepted size
+    and, at it, the first subset in itertools.combinations order, i.e. the largest bit-reversed
+    mask.  A class is a bit pattern c (the subsets whose intersection with candidates 0 .. w - 1
+    is c, n_fixed = w) or a pair (n_fixed, c) (prefix_classes).  Returns (k, key) or
+    (NO_SIZE, 0).  Not exhaustive, a class searches only the sizes that can still win: up to
+    the best size so far (skipped when its fixed members alone exceed it; one size above when
+    they make exactly it, the least k_max kf_search_combos takes).  ``k_max`` caps the sizes
+    searched (the reference's loop over sizes 1 .. n, :1325, cut short)."""
     k_r, key_r = NO_SIZE, 0
     cap = n if k_max is None else int(k_max)
-    for c in classes:
+    for item in classes:
+        nf, c = item if isinstance(item, tuple) else (w, item)
         k_base = bin(c).count('1')
         lim = cap
         if not exhaustive and k_r is not NO_SIZE:
             lim = min(lim, k_r)
         if k_base > lim:
             continue
-        k, idx = search_class(w, c, min(n, max(lim, k_base + 1)))
+        k, idx = search_class(nf, c, min(n, max(lim, k_base + 1)))
         if k and idx is not None and k <= cap:
             key = bitrev64(sum(1 << i for i in idx))
             if k_r is NO_SIZE or k < k_r or (k == k_r and key > key_r):
@@ -858,9 +925,11 @@ def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end
     log-determinant is below R_threshold — the reference's result dict — or None.  The subsets
     run as the shared-prefix search (kf_search_combos: one event step per subset): the sizes
     whose level buffers fit ``search_mem_bytes`` in one call (k_search), then, if none of those
-    was accepted, every size as 2^w class searches one after another (search_combos_classed;
-    n = 40, the reference's visualizing window, kf_workers_visualizing.py:2293, 2340: 256
-    classes of 32 free candidates).  ``max_combos_in_memory`` is the reference's argument; the
+    was accepted, class searches one after another (search_past): bands of the next sizes by
+    prefix classes while they are the fewer calls, then every size as the 2^w fixed-pattern
+    classes (n = 40, the reference's visualizing window, kf_workers_visualizing.py:2293, 2340:
+    size 11 in 40 prefix classes, sizes up to 12 in 151, then 256 classes of 32 free
+    candidates; n = 64: sizes up to 8 in 64 classes, 9 in 532, 10 in 2623).  ``max_combos_in_memory`` is the reference's argument; the
     search needs no per-subset batch.  One filter per subset stays available as
     ``first_valid_rank`` (kf_eval_combos).  Multi-GPU: kfmi.dist.brute_force_search."""
     if R_threshold is None:
@@ -878,8 +947,15 @@ def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end
         if k_search:
             k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=k_search)
         if not k and k_search < n:
+            def search_class(nf, c, k_max):
+                kk, ii, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=k_max,
+                                                n_fixed=nf, fixed_mask=c)
+                return kk, ii
             w = search_class_width(n, dtype, search_mem_bytes, sym)
-            k, idx, _, _ = search_combos_classed(kf, ev, init, prev_time, target_end, R_threshold, w)
+            kr, key = search_past(search_class, n, k_search, w, dtype, search_mem_bytes, sym)
+            if kr is not NO_SIZE:
+                mask = bitrev64(key)
+                k, idx = kr, tuple(i for i in range(n) if (mask >> i) & 1)
     finally:
         kf.close()
     if not k:

@@ -344,3 +344,59 @@ def test_gloo_search_winner_and_counts(world, exhaustive):
     assert won == want_won
     if exhaustive:
         assert total == want
+
+
+def _band_worker(rank, world, port, n, k_done, mem, out_q):
+    """The sharded search past its one-call sizes (kfmi.dist.brute_force_search on the GPU):
+    bands of prefix classes (ref15.search_bands) dealt over the ranks through search_winner,
+    then the fixed-pattern classes — on a random acceptance table shared by every rank that
+    accepts nothing up to k_done."""
+    from itertools import combinations
+
+    from kfmi import ref15
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        res = []
+        for trial, rate in enumerate((0.2, 0.01, 0.0005)):
+            rng = np.random.default_rng(100 + trial)
+            order = [(k, x) for k in range(k_done + 1, n + 1) for x in combinations(range(n), k)
+                     if rng.random() < rate * k]
+
+            def search_class(nf, c, k_max):
+                assert bin(c).count('1') < k_max <= n and c >> nf == 0
+                return next(((k, x) for k, x in order if k <= k_max and sum(1 << i for i in x if i < nf) == c),
+                            (0, None))
+            w = kdist.search_classes(n, world, 'f64', mem, True)
+            won = None
+            for K, classes in ref15.search_bands(n, k_done, 'f64', mem, True, 1 << w):
+                won = kdist.search_winner(search_class, n, 0, classes=classes, k_max=K)
+                if won is not None:
+                    break
+            if won is None:
+                won = kdist.search_winner(search_class, n, w)
+            res.append((won, order[0] if order else None))
+        if rank == 0:
+            out_q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_gloo_banded_search_winner(world):
+    """Bands of prefix classes over the ranks give the reference's pick (the smallest accepted
+    size past the one-call sizes, then the first subset in itertools order), as one rank does."""
+    from kfmi import ref15
+    n, k_done = 15, 2
+    mem = next(m for m in range(8192, 1 << 30, 4096) if ref15.search_levels(n, 'f64', m, True) == k_done)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_band_worker, args=(r, world, port, n, k_done, mem, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    assert [p.exitcode for p in procs] == [0] * world
+    for won, want in q.get(timeout=10):
+        assert won == want

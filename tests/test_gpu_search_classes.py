@@ -134,6 +134,56 @@ def test_n40_search_vs_per_subset():
     kfs.close()
 
 
+@pytest.mark.parametrize('n', [40, 48, 64])
+def test_sizes_past_one_call_by_prefix_bands(n):
+    """Windows past one call's sizes up to kf_search_combos' limit of 64 candidates: with sizes
+    1 .. k_search accepting nothing, the driver's next sizes run as bands of prefix classes
+    (ref15.search_past: n = 40 size 11 in 40 classes, n = 48 size 9 in 48, n = 64 size 8 in 64,
+    where the fixed-pattern classes that fit every size would be 256, 65,536 and 2^32).  The winner
+    equals one filter per subset (first_valid_rank in combination order) and the C oracle's
+    scores: the winner below the threshold, sampled subsets before it not."""
+    ev, init, Pw, t0, t_end = bench.bf_events(n)
+    t_far = t_end + 5.0
+    kfe = kfmi.BatchedKF('ref15', 1 << 22, 'f64')
+    kfs = kfmi.BatchedKF('ref15', 1, 'f64')
+    sym = kfs.search_plan(init, n)['sym']
+    k_lo = ref15.search_levels(n, 'f64', 32 << 30, sym)
+    w = ref15.search_class_width(n, 'f64', 32 << 30, sym)
+    K1, band1 = next(iter(ref15.search_bands(n, k_lo, 'f64', 32 << 30, sym, 1 << w)))
+    assert sym and K1 == k_lo + 1 and len(band1) == n and len(band1) < 1 << w
+    mins = _min_scores(kfe, n, ev, init, t0, t_far, range(1, k_lo + 1))
+    m_lo = min(mins.values())
+    thr = m_lo - 1e-9 * abs(m_lo)          # nothing of sizes 1 .. k_search scores below
+    assert kfs.search_combos(ev, init, t0, t_far, thr, k_max=k_lo)[0] == 0
+    calls = []
+
+    def search_class(nf, c, k_max):
+        calls.append((nf, c, k_max))
+        k, idx, _, _ = kfs.search_combos(ev, init, t0, t_far, thr, k_max=k_max, n_fixed=nf, fixed_mask=c)
+        return k, idx
+    k, key = ref15.search_past(search_class, n, k_lo, w, 'f64', 32 << 30, sym)
+    assert k is not ref15.NO_SIZE and k_lo < k <= k_lo + 2, k
+    idx = tuple(i for i in range(n) if (ref15.bitrev64(key) >> i) & 1)
+    assert all(nf < n and c >> nf == 0 for nf, c, _ in calls)
+    if k == K1:
+        assert len(calls) <= len(band1)    # the first band decided it
+    r = ref15.first_valid_rank(kfe, ev, init, t0, t_far, k, 0, math.comb(n, k), thr)
+    if k > K1:
+        assert ref15.first_valid_rank(kfe, ev, init, t0, t_far, K1, 0, math.comb(n, K1), thr) is None
+    assert r is not None and tuple(ref15.unrank_combination(n, k, r)) == idx, (k, r, idx)
+    rng = np.random.default_rng(n)
+    assert _combo_maxima(ev, Pw, t0, t_far, np.array([idx]))[0] < thr
+    for kk in range(1, k + 1):
+        hi = r if kk == k else math.comb(n, kk)
+        ranks = np.unique(rng.integers(0, hi, 2048)) if hi > 2048 else np.arange(hi)
+        if len(ranks):
+            combos = np.array([ref15.unrank_combination(n, kk, int(x)) for x in ranks])
+            assert (_combo_maxima(ev, Pw, t0, t_far, combos) >= thr).all(), kk
+    print(f'n = {n}: sizes 1 .. {k_lo} in one call, winner of size {k} {idx} from {len(calls)} prefix classes')
+    kfe.close()
+    kfs.close()
+
+
 def test_n40_counts_sizes_1_to_4_vs_oracle():
     """Acceptance counts of sizes 1-4 summed over the 256 classes of the n = 40 search (size cap
     4, exhaustive) equal the C oracle's per-subset scores' (every subset of sizes 1-4, 102,090),

@@ -288,3 +288,67 @@ def test_class_search_size_cap(w):
             got = None if k is ref15.NO_SIZE else (k, tuple(i for i in range(n) if (ref15.bitrev64(key) >> i) & 1))
             assert got == want, (K, exhaustive, got, want)
             assert all(bin(c).count('1') <= K and km <= max(K, bin(c).count('1') + 1) for c, km in calls)
+
+
+def _small_budget(n, want):
+    """A level budget at which one call of n candidates holds sizes 1 .. want exactly."""
+    for mem in range(8192, 1 << 30, 4096):
+        if ref15.search_levels(n, 'f64', mem, True) == want:
+            return mem
+    raise AssertionError((n, want))
+
+
+@pytest.mark.parametrize('n,k_done', [(13, 3), (14, 4), (15, 2), (16, 2)])
+def test_prefix_classes_cover_every_subset_once(n, k_done):
+    """ref15.prefix_classes: for the sizes up to K of a search whose one call holds sizes up to
+    k_done, classes (n_fixed, prefix) that each fit one call for their sizes and hold every subset
+    of sizes k_done + 1 .. K exactly once (the prefixes a split leaves out are of searched sizes);
+    search_bands stops when they are no fewer than the fixed-pattern classes."""
+    mem = _small_budget(n, k_done)
+    for K in range(k_done + 1, min(n, 2 * k_done + 2)):
+        classes, split = ref15.prefix_classes(n, K, 'f64', mem, True)
+        assert split <= k_done and len(set(classes)) == len(classes)
+        for nf, c in classes:
+            p = bin(c).count('1')
+            assert 0 <= nf < n and c >> nf == 0 and p < K
+            assert ref15.search_levels(n - nf, 'f64', mem, True) >= min(K - p, n - nf)
+        for k in range(1, K + 1):
+            for x in combinations(range(n), k):
+                m = sum(1 << i for i in x)
+                hits = sum((m & ((1 << nf) - 1)) == c for nf, c in classes)
+                assert hits == 1 or (k <= split and hits == 0), (K, x, hits)
+    w = ref15.search_class_width(n, 'f64', mem, True)
+    bands = list(ref15.search_bands(n, k_done, 'f64', mem, True, 1 << w))
+    assert [K for K, _ in bands] == list(range(k_done + 1, k_done + 1 + len(bands)))
+    assert all(len(c) < 1 << w for _, c in bands)
+
+
+@pytest.mark.parametrize('n,k_done', [(12, 3), (13, 3), (15, 2), (16, 2)])
+def test_search_past_picks_the_reference_winner(n, k_done):
+    """ref15.search_past over random acceptance tables with nothing accepted up to k_done (what
+    the one-call sizes found): the reference's pick — the smallest accepted size, then the first
+    subset in itertools.combinations order — whether a band of prefix classes or the
+    fixed-pattern classes decide it; every call is one kf_search_combos takes."""
+    mem = _small_budget(n, k_done)
+    w = ref15.search_class_width(n, 'f64', mem, True)
+    rng = np.random.default_rng(n)
+    for trial in range(8):
+        rate = [0.0005, 0.002, 0.01, 0.05, 0.2, 0.0, 0.003, 0.02][trial]
+        # the accepted subsets in the reference's order (size, then itertools order)
+        order = [(k, x) for k in range(k_done + 1, n + 1) for x in combinations(range(n), k)
+                 if rng.random() < rate * k]
+        calls = []
+
+        def search_class(nf, c, k_max):
+            assert 0 <= nf < n and c >> nf == 0 and bin(c).count('1') < k_max <= n
+            calls.append((nf, c, k_max))
+            return next(((k, x) for k, x in order if k <= k_max and sum(1 << i for i in x if i < nf) == c),
+                        (0, None))
+        want = order[0] if order else None
+        k, key = ref15.search_past(search_class, n, k_done, w, 'f64', mem, True)
+        got = None if k is ref15.NO_SIZE else (k, tuple(i for i in range(n) if (ref15.bitrev64(key) >> i) & 1))
+        assert got == want, (trial, got, want)
+        if want and want[0] <= k_done + 2:  # decided by a band: no fixed-pattern class was searched
+            bands = [K for K, _ in ref15.search_bands(n, k_done, 'f64', mem, True, 1 << w)]
+            if want[0] in bands:
+                assert all(nf != w or k_max <= want[0] for nf, _, k_max in calls)
