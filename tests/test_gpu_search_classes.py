@@ -11,7 +11,9 @@ Checked here: at n = 25 and 28 the classes reproduce the whole search (every sub
 through subset_max, winners and acceptance counts, exhaustive and not); at n = 40 the winner
 equals one filter per subset (kf_eval_combos, first_valid_rank) at thresholds whose first
 accepted size is 2 and is past the one-call search's sizes, and acceptance counts of sizes 1-4
-equal the C oracle's (oracle/cpu_kf.c, one filter per subset).
+equal the C oracle's (oracle/cpu_kf.c, one filter per subset); at n = 40, 48 and 64 the first
+size past one call, searched by a band of prefix classes (ref15.search_past), gives one filter
+per subset's winner.
 """
 import math
 from itertools import combinations
