@@ -165,7 +165,8 @@ def brute_force_search(events, start_idx=0, end_idx=None, R_threshold=None, init
             # the same on every rank (the reference's windows accept within them in milliseconds);
             # only if none is accepted, every size by class over the ranks
             try:
-                k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=k_search)
+                k, idx = ref15.one_call_search(kf, ev, init, prev_time, target_end, R_threshold, k_search, dtype,
+                                               search_mem_bytes, sym)
             except BaseException:
                 kf.close()
                 raise

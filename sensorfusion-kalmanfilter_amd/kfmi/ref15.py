@@ -843,6 +843,27 @@ def search_bands(n, k_done, dtype='f64', mem_bytes=32 << 30, sym=False, max_clas
         yield K, classes
 
 
+SEARCH_FIRST_BYTES = 1 << 30  # the first one-call pass's level buffers (one_call_search)
+
+
+def one_call_search(kf, ev, init, prev_time, target_end, threshold, k_search, dtype='f64', mem_bytes=32 << 30,
+                    sym=False):
+    """The sizes 1 .. k_search in one kf_search_combos call each pass, stopping at the first
+    accepted size: first the sizes whose level buffers fit SEARCH_FIRST_BYTES, then, if none was
+    accepted, all k_search (which searches the first ones again).  A handle's level buffers are
+    sized by the call's k_max and freed with the handle, and at n = 40 the sizes up to 10 take
+    2 x 16 GB that a box took up to ~0.7 s to map and free per window; the reference's windows
+    accept within the first pass's sizes (7 at n = 40, 1 GiB).  Returns (k, indices) or (0, None)."""
+    n = int(np.asarray(ev).shape[0])
+    k_first = min(k_search, search_levels(n, dtype, min(mem_bytes, SEARCH_FIRST_BYTES), sym))
+    k, idx = 0, None
+    for k_max in sorted({k_first, k_search} - {0}):
+        k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, threshold, k_max=k_max)
+        if k:
+            break
+    return k, idx
+
+
 def search_past(search_class, n, k_done, w, dtype='f64', mem_bytes=32 << 30, sym=False):
     """The reference's pick (class_search's (k, key)) in a search of n candidates whose sizes
     1 .. k_done accepted nothing and whose levels do not fit one call: the next sizes by bands of
@@ -943,9 +964,8 @@ def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end
     try:
         sym = kf.search_plan(init, n, k_max=1)['sym']
         k_search = search_levels(n, dtype, search_mem_bytes, sym)
-        k, idx = 0, None
-        if k_search:
-            k, idx, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=k_search)
+        k, idx = one_call_search(kf, ev, init, prev_time, target_end, R_threshold, k_search, dtype,
+                                 search_mem_bytes, sym)
         if not k and k_search < n:
             def search_class(nf, c, k_max):
                 kk, ii, _, _ = kf.search_combos(ev, init, prev_time, target_end, R_threshold, k_max=k_max,
