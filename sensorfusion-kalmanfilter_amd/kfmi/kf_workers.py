@@ -264,6 +264,12 @@ _MODEL_RH = {'GPS': (_R_GPS, _H_GPS), 'IMU': (_R_IMU, _H_IMU)}
 # KF_SensorFusion (kf_workers.py:277-1428)
 # ------------------------------------------------------------------------------------------
 
+_GETTERS = ('get_state_transition_matrix', 'get_process_noise_covariance_matrix', 'predict_covariance',
+            'get_gps_observation_matrix', 'get_gps_measurement_noise_covariance_matrix', 'get_imu_observation_matrix',
+            'get_imu_measurement_noise_covariance_matrix', 'calculate_kalman_gain')
+_REFERENCE_CONSTS = None  # KF_SensorFusion._consts of an object with none of _GETTERS replaced
+
+
 class KF_SensorFusion:
     def __init__(self, gps_csv_file, imu_csv_file, dtype='f64', device=0):
         self.gps_csv_file = gps_csv_file
@@ -385,8 +391,17 @@ class KF_SensorFusion:
     # -- drivers ---------------------------------------------------------------------------
     def _consts(self):
         """The model constants the drivers run with, read from this object's getters (which a
-        subclass or a class_args caller may replace, kf_workers.py:1242-1251) and P0."""
-        return _consts_of({'get_state_transition_matrix': self.get_state_transition_matrix,
+        subclass or a class_args caller may replace, kf_workers.py:1242-1251) and P0.  With none
+        of them replaced (the class's and the instance's getters are this class's own and P0 is
+        the reference's) the reference constants, read once (the getters' probes cost ~0.35 ms a
+        driver call)."""
+        global _REFERENCE_CONSTS
+        own = (not any(g in vars(self) for g in _GETTERS)
+               and all(getattr(type(self), g) is getattr(KF_SensorFusion, g) for g in _GETTERS)
+               and np.array_equal(np.asarray(self.P0), ref15.P0))
+        if own and _REFERENCE_CONSTS is not None:
+            return _REFERENCE_CONSTS
+        c = _consts_of({'get_state_transition_matrix': self.get_state_transition_matrix,
                            'get_process_noise_covariance_matrix': self.get_process_noise_covariance_matrix,
                            'predict_covariance': self.predict_covariance,
                            'get_gps_observation_matrix': self.get_gps_observation_matrix,
@@ -396,6 +411,9 @@ class KF_SensorFusion:
                            'get_imu_measurement_noise_covariance_matrix':
                                self.get_imu_measurement_noise_covariance_matrix,
                            'calculate_kalman_gain': self.calculate_kalman_gain}, self.P0)
+        if own:
+            _REFERENCE_CONSTS = c
+        return c
 
     def _ev(self):
         return self.events if self.events is not None else self.indexed_sensor_data

@@ -219,14 +219,16 @@ def event_payload(stype, sdata):
     return [float(v) for v in sdata[1:10]]
 
 
-def _run_streams(streams, x0, P0b, dtype='f64', device=0, threshold=None, model='ref15', cov=False, consts=None):
+def _run_streams(streams, x0, P0b, dtype='f64', device=0, threshold=None, model='ref15', cov=False, consts=None,
+                 kf=None):
     """Run one event list per filter in ONE kf_run_events launch.
 
     streams: list (per filter) of [(type, dt, payload9)]; each stream is preceded by a NONE
     event so row 0 of the outputs holds the initial state and logdet.  x0 [B, n] and P0b
     [B, rows] are the initial states.  Returns traj [T, W, B], logdet [T, B], updated [T, B],
     x [n, B], P blocks [rows, B], status [B] (and cov [T, rows, B] with cov=True) as NumPy
-    arrays.  consts: a ModelConsts (None = the reference's constants)."""
+    arrays.  consts: a ModelConsts (None = the reference's constants).  kf: a handle of this
+    model, batch, dtype and constants to run on (kept open), instead of a new one."""
     B = len(streams)
     T = 1 + max((len(s) for s in streams), default=0)
     etype = np.full((T, B), NONE, np.uint8)
@@ -237,7 +239,9 @@ def _run_streams(streams, x0, P0b, dtype='f64', device=0, threshold=None, model=
             etype[t, f] = ty
             dt[t, f] = d
             pay[t, :, f] = p
-    kf = BatchedKF(model, B, dtype, device=device, params=_params(consts))
+    own = kf is None
+    if own:
+        kf = BatchedKF(model, B, dtype, device=device, params=_params(consts))
     npd = np.float64 if dtype == 'f64' else np.float32
     kf.set_state(np.ascontiguousarray(np.asarray(x0, np.float64).T.astype(npd)),
                  np.ascontiguousarray(np.asarray(P0b, np.float64).T.astype(npd)))
@@ -249,7 +253,8 @@ def _run_streams(streams, x0, P0b, dtype='f64', device=0, threshold=None, model=
            Pb.double().cpu().numpy(), st.cpu().numpy())
     if cov:
         out += (cv.double().cpu().numpy(),)
-    kf.close()
+    if own:
+        kf.close()
     return out
 
 
@@ -540,15 +545,16 @@ def _combo_stream(combo, prev_time, target_end):
     return s, times
 
 
-def evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time, dtype='f64', device=0, consts=None):
+def evaluate_combo_chunk(chunk, xt, Pt, prev_time, target_end_time, dtype='f64', device=0, consts=None, kf=None):
     """evaluate_combo_chunk_worker (kf_workers.py:22-97) for a whole chunk in ONE launch, one
-    filter per combination.  Returns [(0, traj, combo, x_final, None, log_det, k), ...]."""
+    filter per combination.  Returns [(0, traj, combo, x_final, None, log_det, k), ...].  kf: a
+    'ref15' handle of len(chunk) filters with these constants to run on (_run_streams)."""
     if not chunk:
         return []
     built = [_combo_stream(c, prev_time, target_end_time) for c in chunk]
     B = len(chunk)
     tr, ld, _, x, Pb, st = _run_streams([b[0] for b in built], np.broadcast_to(np.asarray(xt, np.float64), (B, 15)),
-                                        np.broadcast_to(to_blocks(Pt), (B, 27)), dtype, device, consts=consts)
+                                        np.broadcast_to(to_blocks(Pt), (B, 27)), dtype, device, consts=consts, kf=kf)
     results = []
     for f, (combo, (s, times)) in enumerate(zip(chunk, built)):
         if st[f] != 0:  # the worker skips a combination that raised (kf_workers.py:88-91)
@@ -626,13 +632,15 @@ def first_valid_rank(kf, ev, init, prev_time, target_end, k, lo, hi, threshold):
     return None
 
 
-def brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype='f64', device=0, indices=None, consts=None):
+def brute_force_result(cand, k, r, xt, Pt, prev_time, target_end, dtype='f64', device=0, indices=None, consts=None,
+                       kf=None):
     """The reference's result dict (kf_workers.py:1358-1367) for combination rank r of size k
-    (or the candidate ``indices`` of the subset)."""
+    (or the candidate ``indices`` of the subset); kf: a one-filter handle to run it on (the
+    search's)."""
     idx = unrank_combination(len(cand), k, r) if indices is None else indices
     combo = tuple(cand[i] for i in idx)
     metric, traj, combo, x_bf, P_bf, log_det, used = evaluate_combo_chunk([combo], xt, Pt, prev_time, target_end,
-                                                                          dtype, device, consts)[0]
+                                                                          dtype, device, consts, kf=kf)[0]
     return {'selected_sensors': combo, 'final_state': x_bf, 'final_covariance': P_bf, 'trajectory': traj,
             'accuracy_metric': metric, 'log_determinants': log_det, 'num_measurements_used': used}
 
@@ -976,11 +984,12 @@ def run_brute_force_kalman_filter_no_sampling_min_usage(events, start_idx=0, end
             if kr is not NO_SIZE:
                 mask = bitrev64(key)
                 k, idx = kr, tuple(i for i in range(n) if (mask >> i) & 1)
+        if not k:
+            return None
+        return brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device, indices=idx,
+                                  consts=consts, kf=kf)
     finally:
         kf.close()
-    if not k:
-        return None
-    return brute_force_result(cand, k, None, xt, Pt, prev_time, target_end, dtype, device, indices=idx, consts=consts)
 
 
 # --------------------------------------------------------------------------------------------

@@ -352,3 +352,29 @@ def test_search_past_picks_the_reference_winner(n, k_done):
             bands = [K for K, _ in ref15.search_bands(n, k_done, 'f64', mem, True, 1 << w)]
             if want[0] in bands:
                 assert all(nf != w or k_max <= want[0] for nf, _, k_max in calls)
+
+
+def test_facade_reference_constants_read_once():
+    """KF_SensorFusion._consts: with no getter replaced (class or instance) and the reference's
+    P0, the drivers get the reference constants read once; a subclass getter, an instance
+    getter or another P0 is read from the object each call, as before."""
+    from kfmi import kf_workers as kfw
+
+    def obj(cls=kfw.KF_SensorFusion):
+        o = cls.__new__(cls)
+        o.P0 = ref15.P0.copy()
+        return o
+    a = obj()
+    c = a._consts()
+    assert c.is_reference() and obj()._consts() is c
+
+    class Sub(kfw.KF_SensorFusion):
+        def get_gps_measurement_noise_covariance_matrix(self):
+            return 5.0 * np.eye(3)
+    assert not obj(Sub)._consts().is_reference()
+    b = obj()
+    b.P0[0, 0] = 7.0
+    assert b._consts() is not c and not b._consts().is_reference()
+    d = obj()
+    d.get_process_noise_covariance_matrix = lambda dt: np.eye(15) * dt
+    assert d._consts() is not c and not d._consts().is_reference()
