@@ -229,3 +229,42 @@ def test_visualizing_pipeline_n40_window(csvs):
         assert [e[0] for e in got['selected_sensors']] == sel
         for key in ('log_determinants', 'final_state', 'trajectory'):
             assert _rel(got[key], ref[key]) <= 1e-6, key
+
+
+@pytest.mark.parametrize('warm', [False, True])
+def test_monotone_drivers_on_the_device_stream(csvs, warm):
+    """run_adaptive_threshold_kalman_filter and run_no_update_kalman_filter over the ingested
+    event list run the window on the device (ref15.run_monotone_stream: kf_events_dt's
+    KF_DT_MONOTONE rule, one kf_run_events launch); their results equal the event-list path's
+    bit for bit (the same dt, the same launch), cold (first fix of the window) and warm, at a
+    threshold that gates some updates; and the adaptive filter equals the NumPy restatement."""
+    from kfmi import ref15
+    sf = kfw.KF_SensorFusion(*csvs)
+    sf.load_data()
+    sf.gps_to_modified_utm()
+    bw, ba, _ = sf.compute_imu_biases(sf.gps_data, sf.imu_data)
+    sf.unbias_imu_data(bw, ba)
+    sf.combine_sensor_data()
+    ev = sf.indexed_sensor_data
+    assert ref15._device_stream(ev) is not None
+    plain = list(ev)
+    kw = {}
+    if warm:
+        st, _, pt, _, _ = ref15.run_adaptive_threshold_kalman_filter(ev, end_idx=1200, R_threshold=-10.0)
+        kw = dict(initial_pt=pt, initial_state=st[-1])
+    for fn, args in ((ref15.run_adaptive_threshold_kalman_filter, dict(R_threshold=-10.0)),
+                     (ref15.run_adaptive_threshold_kalman_filter, dict(R_threshold=float('-inf'))),
+                     (ref15.run_no_update_kalman_filter, {})):
+        a = fn(ev, 1200, 2600, **args, **kw)
+        b = fn(plain, 1200, 2600, **args, **kw)
+        assert len(a[0]) == len(b[0]) > 100
+        np.testing.assert_array_equal(np.array(a[0]), np.array(b[0]))
+        np.testing.assert_array_equal(a[1], b[1])
+        np.testing.assert_array_equal(a[2], b[2])
+        assert a[3] == b[3] and a[4] == b[4]
+    gated = ref15.run_adaptive_threshold_kalman_filter(ev, 1200, 2600, R_threshold=-10.0, **kw)
+    assert 0 < len(gated[4]) < len(gated[0])
+    rs, rl, rP, rprev, rm = ref_kf.run_adaptive_threshold(plain, 1200, 2600, R_threshold=-10.0,
+                                                          initial_pt=kw.get('initial_pt'),
+                                                          initial_state=kw.get('initial_state'))
+    assert _rel(gated[0], rs) <= 1e-9 and _rel(gated[1], rl) <= 1e-9 and gated[4] == list(rm)

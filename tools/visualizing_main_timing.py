@@ -1,0 +1,112 @@
+"""The reference's visualizing __main__ without its plots (kf_workers_visualizing.py:2256-2340),
+end to end through the kfmi façade, step by step beside the oracle's NumPy restatement of the
+reference (diagnostic): on the synthetic drive log of bench config 1 (the reference's
+gps_data.csv shape; its IMU log is absent), ingest, start_idx = 134 s in, the adaptive filter up
+to it, the 40-event window's adaptive and full filters, and the window's brute-force search
+(r_value = -10).  The NumPy brute force runs in a child process under --numpy-budget seconds.
+
+    python tools/visualizing_main_timing.py [--numpy-budget 120]
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, 'sensorfusion-kalmanfilter_amd')]
+
+
+def _numpy_bf(q, events, s, e, r, P, state):
+    from oracle import ref_kf
+    t = time.perf_counter()
+    ref = ref_kf.run_brute_force(events, s, e, r, P, state)
+    q.put(([x[0] for x in ref['selected_sensors']] if ref else None, time.perf_counter() - t))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--numpy-budget', type=float, default=120.0)
+    ap.add_argument('--offset', type=float, default=134.0, help='find_start_idx_for_time_offset seconds')
+    ap.add_argument('--r', type=float, default=-10.0)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import bench
+    from kfmi import kf_workers as kfw
+    from oracle import ref_ingest, ref_kf
+    d = tempfile.mkdtemp()
+    gp, ip = bench.synth_log(bench.CONFIGS['1'], d)
+    g, c = {}, {}
+
+    def timed(store, key, fn):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize()
+        store[key] = round(time.perf_counter() - t, 5)
+        return out
+
+    # --- the façade (GPU) ---
+    def ingest_gpu():
+        sf = kfw.KF_SensorFusion(gp, ip)
+        sf.load_data()
+        sf.gps_to_modified_utm()
+        bw, ba, _ = sf.compute_imu_biases(sf.gps_data, sf.imu_data)
+        sf.unbias_imu_data(bw, ba)
+        sf.combine_sensor_data()
+        return sf
+    sf = timed(g, 'ingest', ingest_gpu)
+    s = kfw.find_start_idx_for_time_offset(sf, args.offset)
+    e = s + 40
+    st, _, pt, _, _ = timed(g, 'adaptive_to_start', lambda: sf.run_adaptive_threshold_kalman_filter(
+        end_idx=s, R_threshold=args.r))
+    aw = timed(g, 'adaptive_window', lambda: sf.run_adaptive_threshold_kalman_filter(
+        start_idx=s, end_idx=e, initial_pt=pt, initial_state=st[-1], R_threshold=args.r))
+    fw = timed(g, 'full_window', lambda: sf.run_kalman_filter_full(start_idx=s, end_idx=e, initial_pt=pt,
+                                                                   initial_state=st[-1]))
+    bf = timed(g, 'brute_force_window', lambda: sf.run_brute_force_kalman_filter_no_sampling_min_usage(
+        start_idx=s, end_idx=e, initial_pt=pt, initial_state=st[-1], R_threshold=args.r))
+    g['total'] = round(sum(v for v in g.values()), 5)
+
+    # --- the oracle's NumPy restatement of the reference, one process ---
+    t = time.perf_counter()
+    events, _, _ = ref_ingest.ingest(gp, ip)
+    c['ingest'] = round(time.perf_counter() - t, 5)
+    rst, _, rpt, _, _ = timed(c, 'adaptive_to_start', lambda: ref_kf.run_adaptive_threshold(
+        events, 0, s, R_threshold=args.r))
+    raw = timed(c, 'adaptive_window', lambda: ref_kf.run_adaptive_threshold(
+        events, s, e, R_threshold=args.r, initial_pt=rpt, initial_state=tuple(rst[-1])))
+    rfw = timed(c, 'full_window', lambda: ref_kf.run_kalman_filter_full(events, s, e, initial_pt=rpt,
+                                                                        initial_state=tuple(rst[-1])))
+    q = mp.get_context('spawn').Queue()
+    p = mp.get_context('spawn').Process(target=_numpy_bf, args=(q, events, s, e, args.r, rpt, tuple(rst[-1])))
+    p.start()
+    p.join(args.numpy_budget)
+    if p.is_alive():
+        p.kill()
+        p.join()
+        c['brute_force_window'] = f'> {args.numpy_budget}'
+        ref_win = 'not finished'
+    else:
+        ref_win, c['brute_force_window'] = q.get(timeout=10)
+        c['brute_force_window'] = round(c['brute_force_window'], 3)
+    win = [x[0] for x in bf['selected_sensors']] if bf else None
+
+    def rel(a, b):
+        a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+        return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1.0)))
+    out = {'log': 'bench config 1 synthetic drive log (616,322 IMU rows at 200 Hz, 30,758 GPS rows)',
+           'start_idx': s, 'window': 40, 'R_threshold': args.r, 'gpu_s': g, 'numpy_s': c,
+           'agree': {'adaptive_to_start_state': rel(st[-1], rst[-1]), 'adaptive_window_logdet': rel(aw[1], raw[1]),
+                     'full_window_logdet': rel(fw[1], rfw[1]),
+                     'brute_force_winner_size': len(win) if win else 0,
+                     'brute_force_winner_equal': (ref_win == win) if isinstance(ref_win, list) or ref_win is None
+                     else ref_win}}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == '__main__':
+    main()
