@@ -331,7 +331,7 @@ int kf_run_events_seq(kf_batch* handle, int T, const uint8_t* etype, const doubl
                       void* stream);
 
 /* One filter over a long event stream, parallel over time: kf_run_events for a handle of ONE
- * filter (B = 1, no gate), with the same arguments, outputs and final state, computed as
+ * filter (B = 1, here without a gate), with the same arguments, outputs and final state, computed as
  * chunks of `chunk` events run as filters of one launch (chunk <= 0: max(128, T / 2048)).
  * Each chunk's start covariance comes from the covariance recursion's linear-fractional maps
  * (per chain and piece of <= 160 events), iterated over all chunks at once from the handle's
@@ -347,9 +347,11 @@ int kf_run_events_seq(kf_batch* handle, int T, const uint8_t* etype, const doubl
  * state must be finite (final pass: every chunk's end state its successor's start, 1e-9 /
  * 1e-4), and no chunk filter may fail; otherwise the sequential kernel runs the stream as one
  * filter from the handle's state and rewrites every record.  Asynchronous on `stream` either
- * way.  kf_run_events takes this route by itself for B = 1, gate = 0 and T >= 65536
- * (KF_OPT_STREAM = 1 disables it).  The run of run_kalman_filter_full (kf_workers.py:623-728)
- * over a whole drive log. */
+ * way.  kf_run_events takes this route by itself for B = 1 and T >= 65536 (KF_OPT_STREAM = 1
+ * disables it); with its gate (the adaptive threshold, kf_workers.py:959-1058) the chunk starts
+ * come from 2048 events of warm-up that apply the gate (the maps cannot carry it) and every
+ * pass and the fallback apply it too, the seam check deciding as above.  The run of
+ * run_kalman_filter_full (kf_workers.py:623-728) over a whole drive log. */
 int kf_run_stream(kf_batch* handle, int T, const uint8_t* etype, const double* dt, const void* payload,
                   void* traj, void* cov, void* logdet, uint8_t* updated, int chunk, int warmup,
                   void* stream);

@@ -876,6 +876,10 @@ int run_events_launch(kf_batch* h, int T, const uint8_t* etype, const double* dt
 
 // kf_run_events routes one-filter runs of at least this many events through kf_run_stream
 constexpr int kStreamMinEvents = 65536;
+// a gated run (the adaptive threshold) takes its chunk starts from this many events of warm-up:
+// the gate makes the covariance recursion's map depend on the covariance, so the
+// linear-fractional maps cannot carry it; the seam check decides whether the warm-up converged
+constexpr int kStreamGateWarmup = 2048;
 // default (warmup < 0): covariance maps iterated to cover this many events, then kStreamPolish
 // chunks of event warm-up
 constexpr int64_t kStreamLftEvents = 2048;
@@ -915,15 +919,23 @@ int check_events_args(const kf_batch* h, int T, const uint8_t* etype, const doub
 }
 }  // namespace
 
+namespace {
+int run_stream_impl(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload, void* traj,
+                    void* cov, void* logdet, uint8_t* updated, int chunk, int warmup, int gate, double threshold,
+                    void* stream);
+}  // namespace
+
 int kf_run_events(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload,
                   void* traj, void* cov, void* logdet, uint8_t* updated, int gate, double threshold,
                   void* stream) {
     int rc = KF_OK;
     if (!check_events_args(h, T, etype, dt, payload, "kf_run_events", &rc)) return rc;
     // one filter over a long stream: parallel over time (checked, with a sequential fallback);
-    // KF_OPT_STREAM = 1 turns the route off for the handle, kf_run_events_seq for one call
-    if (h->B == 1 && !gate && T >= kStreamMinEvents && opt(h, KF_OPT_STREAM) == 0)
-        return kf_run_stream(h, T, etype, dt, payload, traj, cov, logdet, updated, 0, -1, stream);
+    // gated (the adaptive threshold) from an event warm-up; KF_OPT_STREAM = 1 turns the route
+    // off for the handle, kf_run_events_seq for one call
+    if (h->B == 1 && T >= kStreamMinEvents && opt(h, KF_OPT_STREAM) == 0)
+        return run_stream_impl(h, T, etype, dt, payload, traj, cov, logdet, updated, 0, gate ? kStreamGateWarmup : -1,
+                               gate, threshold, stream);
     return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, gate, threshold, nullptr, stream);
 }
 
@@ -937,7 +949,18 @@ int kf_run_events_seq(kf_batch* h, int T, const uint8_t* etype, const double* dt
 
 int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload, void* traj,
                   void* cov, void* logdet, uint8_t* updated, int chunk, int warmup, void* stream) {
+    return run_stream_impl(h, T, etype, dt, payload, traj, cov, logdet, updated, chunk, warmup, 0, 0.0, stream);
+}
+
+namespace {
+// kf_run_stream, and with gate != 0 kf_run_events' gated one-filter route: every chain pass and
+// the fallback apply the gate, and the chunk starts come from an event warm-up (warmup < 0
+// becomes kStreamGateWarmup)
+int run_stream_impl(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload, void* traj,
+                    void* cov, void* logdet, uint8_t* updated, int chunk, int warmup, int gate, double threshold,
+                    void* stream) {
     if (int rc = check_handle(h)) return rc;
+    if (gate && warmup < 0) warmup = kStreamGateWarmup;
     if (!is_ref(h)) return fail(KF_EINVAL, "kf_run_stream: needs a KF_MODEL_REF15 or KF_MODEL_REF8 handle");
     if (h->B != 1) return fail(KF_EINVAL, "kf_run_stream: needs a handle of one filter (B = %lld)", (long long)h->B);
     if (T < 0) return fail(KF_EINVAL, "kf_run_stream: T = %d < 0", T);
@@ -963,7 +986,8 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     h->s_warm = W;
     if (C < 2 || !fits || L > INT32_MAX || W > INT32_MAX) {
         h->s_chunks = 1;
-        return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, 0, 0.0, nullptr, stream);
+        return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, gate, threshold, nullptr,
+                                 stream);
     }
     h->s_chunks = C;
     // workspace: check | banks W (C), M (4C), F (C) | maps | starts
@@ -1074,6 +1098,8 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
             a.logdet = logdet;
             a.updated = updated;
         }
+        a.gate = gate;
+        a.threshold = threshold;
         a.s_len = T;
         a.s_chunk = L;
         a.s_shift = shift;
@@ -1127,8 +1153,10 @@ int kf_run_stream(kf_batch* h, int T, const uint8_t* etype, const double* dt, co
     }
     if (e != hipSuccess) return hip_fail(e, "kf_run_stream");
     // the sequential run, which does nothing unless a check failed
-    return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, 0, 0.0, &sa.check->ok, stream);
+    return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, gate, threshold, &sa.check->ok,
+                             stream);
 }
+}  // namespace
 
 int kf_stream_check(kf_batch* h, double* out, void* stream) {
     if (int rc = check_handle(h)) return rc;

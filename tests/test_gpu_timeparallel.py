@@ -320,3 +320,40 @@ def test_stream_run_replays_as_a_hip_graph():
         np.testing.assert_array_equal(a, b)
     assert kf.stream_check()['ok']
     kf.close()
+
+
+def _gated(et, dt, pay, x0, thr, sequential):
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    kf.set_state(x0[:, None], ref15.to_blocks(ref15.P0)[:, None])
+    tr, ld, up, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None], updated=True, cov=True, threshold=thr,
+                                   sequential=sequential)
+    chk = None if sequential else kf.stream_check()
+    x, P = kf.state()
+    out = tuple(v.double().cpu().numpy() for v in (tr[:, :, 0], ld[:, 0], x[:, 0], P[:, 0], cv[:, :, 0]))
+    flags = up[:, 0].cpu().numpy()
+    kf.close()
+    return out, flags, chk
+
+
+@pytest.mark.parametrize('offset,stands', [(0.5, True), (1.0, True), (2.0, False), (None, False)])
+def test_gated_route_equals_single_filter(offset, stands):
+    """kf_run_events' route for one long GATED filter (the adaptive threshold, kf_workers.py:
+    959-1058): chunk starts from 2048 events of warm-up that apply the gate, every pass gated.
+    Where the gate blocks few updates (thresholds 0.5 / 1.0 above the median record: 2 % / 7 %
+    blocked) the warm-up meets the covariance and the chunked records stand; where it blocks many
+    (2.0 above: 20 %; the reference's r_value = -10: 97 %) the gated covariance's sawtooth keeps
+    the phase it started with, the seam check fails and the sequential fallback rewrites every
+    record.  Either way: the sequential gated filter's records, update flags and final state."""
+    et, dt, pay, x0 = _stream(70000, seed=11)
+    base, _, _ = _gated(et, dt, pay, x0, None, True)
+    thr = -10.0 if offset is None else float(np.median(base[1])) + offset
+    seq, f_seq, _ = _gated(et, dt, pay, x0, thr, True)
+    par, f_par, chk = _gated(et, dt, pay, x0, thr, False)
+    assert chk['chunks'] > 1 and chk['warmup'] == 2048 and chk['ok'] == stands, chk
+    assert 0 < f_seq.mean() < 1 or offset == 0.5
+    np.testing.assert_array_equal(f_par, f_seq)
+    for a, b in zip(par, seq):
+        assert a.shape == b.shape and _rel(a, b) <= 1e-9
+    if not stands:
+        for a, b in zip(par, seq):
+            assert np.array_equal(a, b)   # the fallback is the sequential kernel
