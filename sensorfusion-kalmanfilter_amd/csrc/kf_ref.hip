@@ -695,6 +695,51 @@ __device__ __forceinline__ void atomic_max_pos(double* p, double v) {
     atomicMax(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v));
 }
 
+// The adaptive gate logdet(P_pred) > threshold (kf_workers.py:1023-1025) of the chain kernel,
+// decided on the group's determinant product (mantissa, binary exponent) against
+// exp(threshold) (1 -+ eps); only inside that band are the logs taken, as
+// group_sum(chain_log_det) > threshold, so every decision is the logs' (eps far above the logs'
+// and the products' rounding: 1e-10 in f64, 1e-4 in f32).  The log is the longest part of a
+// gated event's dependent chain, and a gated filter with few updates runs little else.
+// Non-finite or huge thresholds take the logs every event.
+template <typename T>
+struct GateBand {
+    T lo_m = T(0), hi_m = T(0);
+    int lo_e = 0, hi_e = 0;
+    bool banded = false;
+    __device__ __forceinline__ void init(double thr) {
+        banded = thr == thr && thr > -1e6 && thr < 1e6;
+        if (!banded) return;
+        const double eps = sizeof(T) == 8 ? 1e-10 : 1e-4;
+        const double k = floor(thr * 1.4426950408889634);  // exp(thr) = 2^k exp(r), r in [0, ln 2)
+        const double r = thr - k * 0.6931471805599453;
+        int e1, e2;
+        const double lo = frexp(exp(r) * (1.0 - eps), &e1), hi = frexp(exp(r) * (1.0 + eps), &e2);
+        lo_m = T(lo);
+        hi_m = T(hi);
+        lo_e = int(k) + e1;
+        hi_e = int(k) + e2;
+    }
+    // the gate for this lane's chain covariance P (live: a chain lane of the group)
+    __device__ __forceinline__ bool open(const T (&P)[6], bool live, T thr) const {
+        if (banded) {
+            T m;
+            int ex;
+            chain_det_mant(P, m, ex);
+            m = live ? m : T(1);
+            ex = live ? ex : 0;
+            group_prod(m, ex);
+            int e;
+            m = frexp(m, &e);
+            ex += e;
+            if (!(m > T(0))) return false;                           // NaN (a failed block) or 0: log -inf
+            if (ex < lo_e || (ex == lo_e && m < lo_m)) return false;  // the logs' sum below thr
+            if (ex > hi_e || (ex == hi_e && m > hi_m)) return true;   // above
+        }
+        return group_sum(live ? chain_log_det(P) : T(0)) > thr;
+    }
+};
+
 // Inputs of one event for one lane.
 template <typename T>
 struct ChainIn {
@@ -794,6 +839,8 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
     }
     int32_t st = a.status[f];
     const bool need_ld = a.logdet != nullptr;
+    GateBand<T> gate;
+    if (a.gate) gate.init(a.threshold);
     constexpr bool kLdBatch = STREAM && NV == 4 && kStreamLdBatch;
     T bm = T(1);  // kLdBatch: the group's determinant product of event (t - t mod 8 + c)
     int bex = 0;
@@ -878,7 +925,7 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
                     P[tri<3>(i, j)] = (i == j) ? s + q[i] * dt : s;
                 }
             applied = (type == kGps || type == kImu);
-            if (a.gate && applied) applied = group_sum(live ? chain_log_det(P) : T(0)) > T(a.threshold);
+            if (a.gate && applied) applied = gate.open(P, live, T(a.threshold));
             bool ok = true;
             if (applied) {
                 if (type == kGps) {
