@@ -139,7 +139,10 @@ const char* kf_version(void);
  *   KF_OPT_BLOCKS_PER_CU  kf_run: cap resident workgroups per CU at 2..8 (reserving unused LDS);
  *                         0 = no cap
  *   KF_OPT_EVENTS_KERNEL  kf_run_events: 0 = auto, 1 = one lane per filter (inputs in registers),
- *                         2 = one lane per axis chain, 3 = LDS-staged inputs (where legal)
+ *                         2 = one lane per axis chain, 3 = LDS-staged inputs (where legal),
+ *                         4 = one gated f64 filter (B = 1, gate) with closed-form look-ahead
+ *                         over runs of predict-only events (8 events per wave step; opt-in:
+ *                         2.3x the chain kernel at 3 % updated, slower from about 20 %)
  *   KF_OPT_STREAM         kf_run_events: 0 = route one long filter through kf_run_stream,
  *                         1 = never (every filter in sequence)
  *   KF_OPT_STREAM_CHUNKS  kf_run_stream: target chunk count (>= 2); 0 = 8192

@@ -426,7 +426,7 @@ int kf_set_option(kf_batch* h, int option, int64_t value) {
         case KF_OPT_SCHED_REC_TIME: ok = value == 0 || value == 1; break;
         case KF_OPT_CV_KERNEL: ok = value == 0 || value == 1 || value == 2 || value == 4 || value == 8; break;
         case KF_OPT_BLOCKS_PER_CU: ok = value == 0 || (value >= 2 && value <= 8); break;
-        case KF_OPT_EVENTS_KERNEL: ok = value >= 0 && value <= 3; break;
+        case KF_OPT_EVENTS_KERNEL: ok = value >= 0 && value <= 4; break;
         case KF_OPT_STREAM_CHUNKS: ok = value == 0 || (value >= 2 && value <= (int64_t(1) << 24)); break;
         case KF_OPT_START_THREADS: ok = value == 0 || (value >= 1 && value <= kfmi::kBlock); break;
         case KF_OPT_SEARCH_KERNEL: ok = value >= 0 && value <= 2; break;
@@ -856,7 +856,9 @@ int run_events_launch(kf_batch* h, int T, const uint8_t* etype, const double* dt
     // Few filters cannot fill the chip one lane each: give every axis chain its own lane
     // (8 lanes per filter).  Otherwise one lane per filter, with the inputs staged through LDS
     // by DMA where its layout conditions hold.  KF_OPT_EVENTS_KERNEL = 1 | 2 | 3 (lane, chain,
-    // lds) forces a variant (tests, A/B) where it is legal.
+    // lds) forces a variant (tests, A/B) where it is legal; 4 picks the look-ahead kernel for one
+    // gated f64 filter (in f32 its closed-form predicts round differently enough to move gate
+    // decisions: 8 of 70,000 flags at r_value = -10, profiles/r06_lookahead)
     const uint64_t span = static_cast<uint64_t>(h->B) * elem(h);
     // the chain kernel addresses up to 27 [B] rows through one descriptor (32-bit byte count);
     // the LDS kernel moves 16-B chunks (B % 16 == 0: none straddles B) of a 9-row payload span
@@ -869,7 +871,9 @@ int run_events_launch(kf_batch* h, int T, const uint8_t* etype, const double* dt
     if (v == 2 && chain_ok) variant = kfmi::kEventsChain;
     else if (v == 1) variant = kfmi::kEventsLane;
     else if (v == 3 && lds_ok) variant = kfmi::kEventsLds;
-    if (skip && variant != kfmi::kEventsChain) return fail(KF_EINVAL, "kf_run_stream: fallback needs the chain kernel");
+    else if (v == 4 && h->B == 1 && gate && h->dtype == KF_F64) variant = kfmi::kEventsGated;
+    if (skip && variant != kfmi::kEventsChain && variant != kfmi::kEventsGated)
+        return fail(KF_EINVAL, "kf_run_stream: fallback needs the chain kernel");
     hipError_t e = kfmi::launch_ref_events(h->model, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream), variant);
     return e == hipSuccess ? KF_OK : hip_fail(e, "kf_run_events");
 }

@@ -346,7 +346,7 @@ hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t str
 // chain = true: the chain-parallel kernel (kGroup lanes per filter), for few filters.
 // kf_run_events kernel variants: one lane per filter (inputs loaded to registers), one lane
 // per axis chain (few filters), one lane per filter with inputs staged through LDS by DMA
-constexpr int kEventsLane = 0, kEventsChain = 1, kEventsLds = 2;
+constexpr int kEventsLane = 0, kEventsChain = 1, kEventsLds = 2, kEventsGated = 3;  // gated: B = 1 look-ahead
 hipError_t launch_ref_events(int model, bool f64, const RefArgs& a, hipStream_t stream, int variant);
 // the chain kernel in stream mode (a.s_len > 0); nv = 4: the map pass, four state variants per
 // filter sharing its covariance (state bank of 4 B columns)

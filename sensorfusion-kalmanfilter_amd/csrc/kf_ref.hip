@@ -1145,6 +1145,270 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// ONE gated filter (B = 1, the adaptive threshold, kf_workers.py:959-1058) whose gate blocks
+// most updates, on one wave: lane c + 8 j is chain c (the chain kernel's lane layout) of event
+// slot j.  Every event that applies an update runs as the chain kernel's event (its arithmetic,
+// term for term).  After an event that did not, the wave looks ahead over the next 8 events at
+// once: between two updates the filter only predicts, and with the model's additive F (F(a) F(b)
+// = F(a + b)) and diagonal Q(dt) a run of predicts has a closed form,
+//   P_m = F(tau_m) (P + S_m) F(tau_m)^T,  S_m = sum_{i <= m} F(-tau_i) Q(dt_i) F(-tau_i)^T,
+// tau the time since the last event run (prefix sums over the slots), x_m = F(tau_m) x.  Slot j
+// takes event t + j; the first slot whose event would open the gate (GateBand on its closed-form
+// P_pred, a ballot over the slots) ends the run: the slots before it write their records at
+// once and hand their state on, and that event runs next as a chain-kernel event.  The closed
+// form rounds differently from one predict after another (records within ~1e-15 relative of the
+// sequential kernel's); a gate decision could only differ within that distance of the threshold.
+// KF_OPT_EVENTS_KERNEL = 4 (and kf_run_events' gated one-filter route, when the chunked run
+// falls back) runs it.
+// ------------------------------------------------------------------------------------
+template <typename T, class M, bool CUSTOM>
+__global__ __launch_bounds__(64) void ref_chain_gated_kernel(const RefArgs a) {
+    if (a.skip && *a.skip) return;
+    const int lane = int(threadIdx.x);
+    const int c = lane & (kGroup - 1);  // chain
+    const int slot = lane / kGroup;     // event slot of the look-ahead
+    const bool pva = c < M::NP;
+    const bool live = c < M::NP + M::NA;
+    const int ca = pva ? c : (live ? c - M::NP : 0);
+    int xi[3], pr[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) xi[k] = !live ? -1 : pva ? M::pva(ca, k) : (k < 2 ? M::aw(ca, k) : -1);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int aw_row = k == 0 ? 0 : k == 1 ? 1 : k == 3 ? 2 : -1;
+        pr[k] = !live ? -1 : pva ? 6 * ca + k : (aw_row < 0 ? -1 : 6 * M::NP + 3 * ca + aw_row);
+    }
+    const int ia = pva ? ca : M::imu_att(ca);
+    const int ib = pva ? M::imu_acc(ca) : M::imu_rate(ca);
+    T q[3] = {T(pva ? kQPos : kQAtt), T(pva ? kQVel : kQRate), T(pva ? kQAcc : 0.0)};
+    T Rimu[6] = {T(pva ? kRPos : kRAtt), T(0), T(0), T(pva ? kRVel : kRRate), T(0), T(pva ? kRAcc : 1.0)};
+    T Rgps = T(kRGps);
+    if constexpr (CUSTOM) {
+        const RefConsts* kc = a.kc;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            if (xi[k] >= 0) {
+                q[k] = T(ro(kc)->q[xi[k]]);
+                Rimu[k == 0 ? 0 : k == 1 ? 3 : 5] = T(ro(kc)->r_imu[xi[k]]);
+            }
+        if (pva) Rgps = T(ro(kc)->r_gps[ca]);
+    }
+    const T* hx = static_cast<const T*>(a.x);
+    const T* hP = static_cast<const T*>(a.P);
+    T x[1][3], P[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) x[0][k] = xi[k] >= 0 ? hx[xi[k]] : T(0);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) P[k] = pr[k] >= 0 ? hP[pr[k]] : T(k == 0 || k == 3 || k == 5 ? 1 : 0);
+    int32_t st = a.status[0];
+    GateBand<T> gate;
+    gate.init(a.threshold);
+    const T thr = T(a.threshold);
+    const T* pay = static_cast<const T*>(a.payload);
+    T* traj = static_cast<T*>(a.traj);
+    T* cov = static_cast<T*>(a.cov);
+    T* ldo = static_cast<T*>(a.logdet);
+    const int T_ = a.T;
+    // the records of event t from this lane's chain state (slot `writer`'s lanes write; plain
+    // stores under the writer branch measured faster here than dropped buffer stores, which the
+    // seven non-writing slots would issue too)
+    auto record = [&](int t, const T (&xr)[3], const T (&Pr)[6], bool applied, bool writer) {
+        if (writer && traj && xi[0] >= 0 && xi[0] < M::NTRAJ) traj[int64_t(t) * M::NTRAJ + xi[0]] = xr[0];
+        if (writer && cov) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                if (pr[k] >= 0) cov[int64_t(t) * M::NBLK + pr[k]] = Pr[k];
+        }
+        if (ldo) {
+            const T ld = group_sum(live ? chain_log_det(Pr) : T(0));
+            st = (ld == ld) ? st : kNotSpd;
+            if (writer && c == 0) ldo[t] = ld;
+        }
+        if (writer && c == 0 && a.updated) a.updated[t] = applied ? 1 : 0;
+    };
+    int t = 0;
+    // a look-ahead after an event that did not update, unless the last one found its run over at
+    // once (then only after `cool` more such events: a regime of frequent updates stays on the
+    // chain kernel's event step)
+    int cool = 0, backoff = 0;
+    // event t's inputs, loaded one event ahead (t + 1 while t runs; a look-ahead that moves t
+    // reloads)
+    int nt = 0;
+    int ntype = T_ > 0 ? int(a.etype[0]) : 255;
+    double ndt = T_ > 0 ? a.dt[0] : 0.0;
+    T nva = T_ > 0 ? pay[ia] : T(0), nvb = T_ > 0 ? pay[ib] : T(0);
+    while (t < T_) {  // wave-uniform
+        // ---- event t as the chain kernel runs it (every slot the same arithmetic) ----
+        if (nt != t) {
+            ntype = int(a.etype[t]);
+            ndt = a.dt[t];
+            nva = pay[int64_t(t) * 9 + ia];
+            nvb = pay[int64_t(t) * 9 + ib];
+        }
+        const int type = ntype;
+        const T dt = T(ndt);
+        const T va = nva, vb = nvb;
+        nt = t + 1;
+        if (nt < T_) {
+            ntype = int(a.etype[nt]);
+            ndt = a.dt[nt];
+            nva = pay[int64_t(nt) * 9 + ia];
+            nvb = pay[int64_t(nt) * 9 + ib];
+        }
+        bool applied = false;
+        if (type != 255) {
+            const T c02 = pva ? T(0.5) * dt * dt : T(0);
+            const T c12 = pva ? dt : T(0);
+            {
+                const T xn0 = fmaT(c02, x[0][2], fmaT(dt, x[0][1], x[0][0]));
+                const T xn1 = fmaT(c12, x[0][2], x[0][1]);
+                x[0][0] = xn0;
+                x[0][1] = xn1;
+            }
+            T FP[3][3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                FP[0][j] = fmaT(c02, P[tri<3>(2, j)], fmaT(dt, P[tri<3>(1, j)], P[tri<3>(0, j)]));
+                FP[1][j] = fmaT(c12, P[tri<3>(2, j)], P[tri<3>(1, j)]);
+                FP[2][j] = P[tri<3>(2, j)];
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = i; j < 3; ++j) {
+                    T s = FP[i][j];
+                    if (j == 0) s = fmaT(FP[i][2], c02, fmaT(FP[i][1], dt, s));
+                    if (j == 1) s = fmaT(FP[i][2], c12, s);
+                    P[tri<3>(i, j)] = (i == j) ? s + q[i] * dt : s;
+                }
+            applied = (type == kGps || type == kImu);
+            if (applied) applied = gate.open(P, live, thr);
+            bool ok = true;
+            if (applied) {
+                if (type == kGps) {
+                    if (pva) {
+                        T zb[1][1] = {{va}};
+                        const T R[1] = {Rgps};
+                        ok = sel_update_nv<3, 1, true, T, kRefNewton, true, 1, kRefJoseph<T>, kRefGainR>(x, P, zb, R);
+                    }
+                } else {
+                    const T V = fmaT(vb, dt, x[0][1]);
+                    const T X = fmaT(V, dt, x[0][0]);
+                    T zb[1][3] = {{pva ? X : va, pva ? V : vb, pva ? vb : T(0)}};
+                    ok = sel_update_nv<3, 3, true, T, kRefNewton, true, 1, kRefJoseph<T>, kRefGainR>(x, P, zb, Rimu);
+                    if (!pva) {
+                        x[0][2] = T(0);
+                        P[5] = T(1);
+                    }
+                }
+            }
+            if (group_any(!ok)) {
+                st = kNotSpd;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) x[0][k] = quiet_nan<T>();
+#pragma unroll
+                for (int k = 0; k < 6; ++k) P[k] = quiet_nan<T>();
+            }
+        }
+        record(t, x[0], P, applied, slot == 0);
+        ++t;
+        if (applied || t >= T_) continue;  // wave-uniform (the gate's group ops give every slot the decision)
+        if (cool > 0) {
+            --cool;
+            continue;
+        }
+        for (;;) {  // look-aheads until a run ends (or the stream does)
+        // ---- look-ahead: slot j predicts to event t + j in closed form ----
+        const int e = t + slot;
+        const bool valid = e < T_;
+        const int ty = valid ? int(a.etype[e]) : 255;
+        const bool pred = valid && ty != 255;
+        const T dte = pred ? T(a.dt[e]) : T(0);
+        // tau: time since event t - 1 up to and including slot j's event (prefix over slots)
+        T tau = dte;
+#pragma unroll
+        for (int o = 1; o < 8; o *= 2) {
+            const T u = __shfl_up(tau, o * kGroup, 64);
+            tau += slot >= o ? u : T(0);
+        }
+        // this slot's term F(-tau) Q(dt) F(-tau)^T (G = F(-tau): rows (1, -tau, h'), (0, 1, g'), (0, 0, 1))
+        const T hm = pva ? T(0.5) * tau * tau : T(0), gm = pva ? -tau : T(0);
+        const T d0 = q[0] * dte, d1 = q[1] * dte, d2 = q[2] * dte;
+        T Sx[6];
+        Sx[0] = fmaT(hm * hm, d2, fmaT(tau * tau, d1, d0));
+        Sx[1] = fmaT(hm * gm, d2, -tau * d1);
+        Sx[2] = hm * d2;
+        Sx[3] = fmaT(gm * gm, d2, d1);
+        Sx[4] = gm * d2;
+        Sx[5] = d2;
+#pragma unroll
+        for (int o = 1; o < 8; o *= 2)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const T u = __shfl_up(Sx[k], o * kGroup, 64);
+                Sx[k] += slot >= o ? u : T(0);
+            }
+        // P_pred = F(tau) (P + S) F(tau)^T, F = [[1, tau, h], [0, 1, g], [0, 0, 1]]
+        const T h = pva ? T(0.5) * tau * tau : T(0), g = pva ? tau : T(0);
+        T A[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) A[k] = P[k] + Sx[k];
+        T B[3][3];  // F A
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            B[0][j] = fmaT(h, A[tri<3>(2, j)], fmaT(tau, A[tri<3>(1, j)], A[tri<3>(0, j)]));
+            B[1][j] = fmaT(g, A[tri<3>(2, j)], A[tri<3>(1, j)]);
+            B[2][j] = A[tri<3>(2, j)];
+        }
+        T Pp[6];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = i; j < 3; ++j) {
+                T s = B[i][j];
+                if (j == 0) s = fmaT(B[i][2], h, fmaT(B[i][1], tau, s));
+                if (j == 1) s = fmaT(B[i][2], g, s);
+                Pp[tri<3>(i, j)] = s;
+            }
+        if (!pva) Pp[5] = P[5];  // the inert state of an aw lane
+        T xp[3] = {fmaT(h, x[0][2], fmaT(tau, x[0][1], x[0][0])), fmaT(g, x[0][2], x[0][1]), x[0][2]};
+        const bool opens = valid && (ty == kGps || ty == kImu) && gate.open(Pp, live, thr);
+        const uint64_t om = __builtin_amdgcn_ballot_w64(opens && c == 0);
+        const int nvalid = T_ - t < 8 ? T_ - t : 8;
+        const int n = om ? int(__builtin_ctzll(om)) / kGroup : nvalid;  // events of the predict run
+        if (slot < n) record(e, xp, Pp, false, true);
+        st = __builtin_amdgcn_ballot_w64(st == kNotSpd) ? kNotSpd : st;  // a failed record in any slot
+        if (n > 0) {
+            const int src = (n - 1) * kGroup + c;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) x[0][k] = __shfl(xp[k], src, 64);
+#pragma unroll
+            for (int k = 0; k < 6; ++k) P[k] = __shfl(Pp[k], src, 64);
+            t += n;
+        }
+        if (n < 4 && om) {  // a short run: look-aheads do not pay here, back off
+            backoff = backoff ? (backoff < 32 ? 2 * backoff : 32) : 1;
+            cool = backoff;
+        } else if (n >= 4) {
+            backoff = 0;
+        }
+        if (om || n < 8 || t >= T_) break;  // the run ended (its opening event runs next) or the stream did
+        }
+    }
+    if (slot == 0) {
+        T* ox = static_cast<T*>(a.x);
+        T* oP = static_cast<T*>(a.P);
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            if (xi[k] >= 0) ox[xi[k]] = x[0][k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            if (pr[k] >= 0) oP[pr[k]] = P[k];
+        if (c == 0) a.status[0] = st;
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Time-parallel run of ONE filter over a long event stream (kf_run_stream; the reference's own
 // use of run_kalman_filter_full, kf_workers.py:623-728, is one filter over a whole drive log).
 // The stream is cut into C chunks of L events that run as filters of the chain kernel:
@@ -4063,6 +4327,8 @@ void ref_events_t(const RefArgs& a, hipStream_t stream, int variant) {
     } else if (variant == kEventsChain) {
         const dim3 cgrid(static_cast<unsigned>((a.B * kGroup + kBlock - 1) / kBlock));
         ref_chain_kernel<T, M, false, CUSTOM><<<cgrid, kBlock, 0, stream>>>(a);
+    } else if (variant == kEventsGated) {
+        ref_chain_gated_kernel<T, M, CUSTOM><<<1, 64, 0, stream>>>(a);
     } else {
         const dim3 grid(static_cast<unsigned>((a.B + kBlock - 1) / kBlock));
         ref_events_kernel<T, M, CUSTOM><<<grid, kBlock, 0, stream>>>(a);

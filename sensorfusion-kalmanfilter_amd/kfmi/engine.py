@@ -32,7 +32,7 @@ OPTIONS = {
     'predict': (_lib.KF_OPT_PREDICT, {'auto': 0, 'deferred': 0, 'eager': 1}),
     'cv_kernel': (_lib.KF_OPT_CV_KERNEL, {'auto': 0, 'general': 1, 'block2': 2, 'block4': 4, 'block8': 8}),
     'blocks_per_cu': (_lib.KF_OPT_BLOCKS_PER_CU, {'auto': 0}),
-    'events_kernel': (_lib.KF_OPT_EVENTS_KERNEL, {'auto': 0, 'lane': 1, 'chain': 2, 'lds': 3}),
+    'events_kernel': (_lib.KF_OPT_EVENTS_KERNEL, {'auto': 0, 'lane': 1, 'chain': 2, 'lds': 3, 'gated': 4}),
     'stream': (_lib.KF_OPT_STREAM, {'auto': 0, 'off': 1}),
     'stream_chunks': (_lib.KF_OPT_STREAM_CHUNKS, {'auto': 0}),
     'stream_final': (_lib.KF_OPT_STREAM_FINAL, {'auto': 0, 'off': 0, 'on': 1}),

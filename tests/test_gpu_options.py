@@ -11,14 +11,14 @@ pytestmark = pytest.mark.gpu
 
 # include/kf.h: the values each option takes besides 0
 VALID = {
-    'predict': [1], 'cv_kernel': [1, 2, 4, 8], 'blocks_per_cu': [2, 5, 8], 'events_kernel': [1, 2, 3],
+    'predict': [1], 'cv_kernel': [1, 2, 4, 8], 'blocks_per_cu': [2, 5, 8], 'events_kernel': [1, 2, 3, 4],
     'stream': [1], 'stream_chunks': [2, 8192, 1 << 24], 'stream_final': [1], 'start_threads': [1, 64, 256],
     'search_kernel': [1, 2], 'search_pm': [1], 'sched_kernel': [1, 2, 3, 4], 'sched_group': [1, 4],
     'sched_order': [1], 'sched_rec_time': [1], 'search_head': [1], 'axis_sym': [1], 'search_end': [1],
     'search_pair': [1, 2, 3, 1024, 1 << 22],
 }
 INVALID = {
-    'predict': [2, -1], 'cv_kernel': [3, 16], 'blocks_per_cu': [1, 9], 'events_kernel': [4],
+    'predict': [2, -1], 'cv_kernel': [3, 16], 'blocks_per_cu': [1, 9], 'events_kernel': [5],
     'stream': [2], 'stream_chunks': [1, (1 << 24) + 1], 'stream_final': [2], 'start_threads': [257, -1],
     'search_kernel': [3], 'search_pm': [2], 'sched_kernel': [5, -1], 'sched_group': [2, 3], 'sched_order': [2],
     'sched_rec_time': [2, -1], 'search_head': [2], 'axis_sym': [2], 'search_end': [2, -1],
