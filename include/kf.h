@@ -141,8 +141,9 @@ const char* kf_version(void);
  *   KF_OPT_EVENTS_KERNEL  kf_run_events: 0 = auto, 1 = one lane per filter (inputs in registers),
  *                         2 = one lane per axis chain, 3 = LDS-staged inputs (where legal),
  *                         4 = one gated f64 filter (B = 1, gate) with closed-form look-ahead
- *                         over runs of predict-only events (8 events per wave step; opt-in:
- *                         2.3x the chain kernel at 3 % updated, slower from about 20 %)
+ *                         over runs of predict-only events (8 events per wave step: 2.3x
+ *                         the chain kernel at 3 % updated, slower from about 20 %; the
+ *                         gated stream fallback picks it by itself, see kf_run_stream)
  *   KF_OPT_STREAM         kf_run_events: 0 = route one long filter through kf_run_stream,
  *                         1 = never (every filter in sequence)
  *   KF_OPT_STREAM_CHUNKS  kf_run_stream: target chunk count (>= 2); 0 = 8192
@@ -353,7 +354,11 @@ int kf_run_events_seq(kf_batch* handle, int T, const uint8_t* etype, const doubl
  * way.  kf_run_events takes this route by itself for B = 1 and T >= 65536 (KF_OPT_STREAM = 1
  * disables it); with its gate (the adaptive threshold, kf_workers.py:959-1058) the chunk starts
  * come from 2048 events of warm-up that apply the gate (the maps cannot carry it) and every
- * pass and the fallback apply it too, the seam check deciding as above.  The run of
+ * pass and the fallback apply it too, the seam check deciding as above; in f64 with update
+ * flags requested, a fallback whose chunked pass updated at most 1 event in 8 runs the
+ * look-ahead kernel (KF_OPT_EVENTS_KERNEL = 4: same flags, records to rounding, 1.8e-12
+ * relative measured), chosen on the device (KF_OPT_EVENTS_KERNEL = 2 keeps the chain
+ * kernel).  The run of
  * run_kalman_filter_full (kf_workers.py:623-728) over a whole drive log. */
 int kf_run_stream(kf_batch* handle, int T, const uint8_t* etype, const double* dt, const void* payload,
                   void* traj, void* cov, void* logdet, uint8_t* updated, int chunk, int warmup,
@@ -364,7 +369,10 @@ int kf_run_stream(kf_batch* handle, int T, const uint8_t* etype, const double* d
  * failed, out[2] = covariance seam gap, out[3] = state seam gap (final pass only; records from
  * the map pass: NaN = not measured, the chunk starts being the composed maps' values, or inf for
  * a non-finite chunk start), out[4] = chunks (1: the stream was too short to split
- * and ran sequentially), out[5] = chunk length, out[6] = events of event warm-up. */
+ * and ran sequentially), out[5] = chunk length, out[6] = events of event warm-up, out[7] = the
+ * sequential fallback's kernel (0 = none, the chunked records stood; 2 = the chain kernel; 4 =
+ * the look-ahead kernel, which a gated f64 run takes when its chunked pass updated at most 1
+ * event in 8).  out: 8 doubles. */
 int kf_stream_check(kf_batch* handle, double* out, void* stream);
 
 /* KF_MODEL_REF15 brute-force search: filter f of the handle evaluates combination number

@@ -837,10 +837,11 @@ int kf_synth(kf_batch* h, uint64_t seed, int64_t filter_offset, int T, double dt
 
 namespace {
 
-// kf_run_events' kernel choice and launch (skip: device flag, see RefArgs::skip)
+// kf_run_events' kernel choice and launch (skip: device flag, see RefArgs::skip; variant >= 0:
+// that kernel, for the stream fallback's device-side choice)
 int run_events_launch(kf_batch* h, int T, const uint8_t* etype, const double* dt, const void* payload, void* traj,
                       void* cov, void* logdet, uint8_t* updated, int gate, double threshold, const int32_t* skip,
-                      void* stream) {
+                      void* stream, int forced = -1) {
     kfmi::RefArgs a = ref_args(h);
     a.T = T;
     a.etype = etype;
@@ -872,6 +873,7 @@ int run_events_launch(kf_batch* h, int T, const uint8_t* etype, const double* dt
     else if (v == 1) variant = kfmi::kEventsLane;
     else if (v == 3 && lds_ok) variant = kfmi::kEventsLds;
     else if (v == 4 && h->B == 1 && gate && h->dtype == KF_F64) variant = kfmi::kEventsGated;
+    if (forced >= 0) variant = forced;
     if (skip && variant != kfmi::kEventsChain && variant != kfmi::kEventsGated)
         return fail(KF_EINVAL, "kf_run_stream: fallback needs the chain kernel");
     hipError_t e = kfmi::launch_ref_events(h->model, h->dtype == KF_F64, a, static_cast<hipStream_t>(stream), variant);
@@ -884,6 +886,10 @@ constexpr int kStreamMinEvents = 65536;
 // the gate makes the covariance recursion's map depend on the covariance, so the
 // linear-fractional maps cannot carry it; the seam check decides whether the warm-up converged
 constexpr int kStreamGateWarmup = 2048;
+// the gated fallback takes the look-ahead kernel when at most 1 in this many events updated in
+// the chunked pass (70,000 events: 1.4x the chain kernel at 11 %, 0.74x at 22 %;
+// profiles/r06_lookahead/ab_f64.log)
+constexpr int kStreamLookaheadShare = 8;
 // default (warmup < 0): covariance maps iterated to cover this many events, then kStreamPolish
 // chunks of event warm-up
 constexpr int64_t kStreamLftEvents = 2048;
@@ -1156,7 +1162,19 @@ int run_stream_impl(kf_batch* h, int T, const uint8_t* etype, const double* dt, 
         if (e == hipSuccess) e = kfmi::launch_stream_phase(h->model, f64, kfmi::kStreamPhaseFinish, sa, st);
     }
     if (e != hipSuccess) return hip_fail(e, "kf_run_stream");
-    // the sequential run, which does nothing unless a check failed
+    // the sequential run, which does nothing unless a check failed.  A gated f64 run whose
+    // chunked pass updated at most 1 event in kStreamLookaheadShare runs it with the look-ahead
+    // kernel (2.3x the chain kernel at 3 % updated, slower from about 20 %), chosen
+    // on the device: both launches are queued and each returns on its flag
+    if (gate && f64 && updated && opt(h, KF_OPT_EVENTS_KERNEL) == 0) {
+        e = kfmi::launch_stream_choose(sa.check, updated, T, kStreamLookaheadShare, st);
+        if (e != hipSuccess) return hip_fail(e, "kf_run_stream");
+        int rc = run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, gate, threshold,
+                                   &sa.check->skip_gated, stream, kfmi::kEventsGated);
+        if (rc != KF_OK) return rc;
+        return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, gate, threshold,
+                                 &sa.check->skip_chain, stream, kfmi::kEventsChain);
+    }
     return run_events_launch(h, T, etype, dt, payload, traj, cov, logdet, updated, gate, threshold, &sa.check->ok,
                              stream);
 }
@@ -1179,6 +1197,8 @@ int kf_stream_check(kf_batch* h, double* out, void* stream) {
     out[4] = double(h->s_chunks);
     out[5] = double(h->s_len);
     out[6] = double(h->s_warm);
+    // the sequential fallback's kernel: 0 none (the chunked records stood), 2 chain, 4 look-ahead
+    out[7] = h->s_chunks > 1 && k.ok ? 0.0 : k.skip_chain ? 4.0 : 2.0;
     return KF_OK;
 }
 

@@ -109,6 +109,11 @@ struct StreamCheck {
     double state_gap;        // max over chunk seams of |end state - next start| / max(|start|, 1)
     int32_t done;            // chain blocks of the scan phase that have finished (the last decides)
     int32_t pad;
+    // the sequential fallback's kernel of a gated f64 run (launch_stream_choose): each kernel
+    // returns at once when its flag is set.  The start phases zero skip_chain only (no choice:
+    // the chain kernel runs on ok alone)
+    int32_t skip_chain;      // ok, or the look-ahead kernel takes the fallback
+    int32_t skip_gated;      // ok, or the chain kernel takes the fallback
 };
 struct StreamArgs {
     int64_t C;               // chunks
@@ -163,6 +168,11 @@ struct StreamArgs {
 // the map pass the verdict); 5: state seam check, verdict, and (if it passed) the handle's
 // final state after a final pass
 hipError_t launch_stream_phase(int model, bool f64, int phase, const StreamArgs& a, hipStream_t stream);
+// after the verdict of a gated f64 stream run: the sequential fallback goes to the look-ahead
+// kernel (ref_chain_gated_kernel) when at most 1 in `share_den` of the chunked run's update flags
+// is set (a sample of up to 64K of them), else to the chain kernel (check->skip_chain / skip_gated)
+hipError_t launch_stream_choose(StreamCheck* check, const uint8_t* updated, int64_t T, int share_den,
+                                hipStream_t stream);
 // the linear-fractional covariance warm-up: phase 6 = every chunk's covariance map, phase 7 =
 // every chunk's start covariance from the maps (and the warm-up / map banks, the zeroed check)
 constexpr int kStreamPhaseLftMaps = 6, kStreamPhaseLftStart = 7;

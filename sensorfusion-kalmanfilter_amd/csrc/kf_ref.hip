@@ -1459,6 +1459,7 @@ __global__ __launch_bounds__(kBlock) void stream_init_kernel(const StreamArgs a)
         a.check->cov_gap = 0.0;
         a.check->state_gap = 0.0;
         a.check->done = 0;
+        a.check->skip_chain = 0;
     }
     if (c >= a.C) return;
     const T* hx = static_cast<const T*>(a.hx);
@@ -2159,6 +2160,7 @@ __global__ __launch_bounds__(kBlock) void stream_lft_start_kernel(const StreamAr
         a.check->cov_gap = 0.0;
         a.check->state_gap = 0.0;
         a.check->done = 0;
+        a.check->skip_chain = 0;
     }
     const int64_t gt = LDS ? a.g : 1;                  // chunks per thread
     const int64_t BC = LDS ? a.G : int64_t(blockDim.x);  // chunks per block
@@ -4445,6 +4447,42 @@ hipError_t launch_stream_phase(int model, bool f64, int phase, const StreamArgs&
     } else {
         return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+namespace {
+// launch_stream_choose (kf_internal.h): one block; 64 segments of 1024 consecutive flags spread
+// evenly over the stream (or every flag of a shorter one), coalesced byte loads, an LDS count
+__global__ void __launch_bounds__(1024) stream_choose_kernel(StreamCheck* k, const uint8_t* up, int64_t T,
+                                                             int share_den) {
+    __shared__ int total;
+    const int tid = int(threadIdx.x);
+    if (tid == 0) total = 0;
+    __syncthreads();
+    constexpr int kSeg = 64, kSegLen = 1024;
+    int cnt = 0;
+    int64_t seen = 0;
+    if (T <= int64_t(kSeg) * kSegLen) {
+        for (int64_t i = tid; i < T; i += kSegLen) cnt += up[i] != 0;
+        seen = T;
+    } else {
+        for (int j = 0; j < kSeg; ++j) cnt += up[(T - kSegLen) * j / (kSeg - 1) + tid] != 0;
+        seen = int64_t(kSeg) * kSegLen;
+    }
+    atomicAdd(&total, cnt);
+    __syncthreads();
+    if (tid != 0) return;
+    const int ok = k->ok;
+    const bool look = int64_t(total) * share_den <= seen;
+    k->skip_chain = (ok || look) ? 1 : 0;
+    k->skip_gated = (ok || !look) ? 1 : 0;
+}
+}  // namespace
+
+hipError_t launch_stream_choose(StreamCheck* check, const uint8_t* updated, int64_t T, int share_den,
+                                hipStream_t stream) {
+    if (!check || !updated || T <= 0 || share_den < 1) return hipErrorInvalidValue;
+    stream_choose_kernel<<<1, 1024, 0, stream>>>(check, updated, T, share_den);
     return hipGetLastError();
 }
 

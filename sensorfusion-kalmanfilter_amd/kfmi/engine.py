@@ -393,10 +393,11 @@ class BatchedKF:
 
     def stream_check(self):
         """The checks of the last run_stream (kf_stream_check; synchronises the stream)."""
-        out = (ctypes.c_double * 7)()
+        out = (ctypes.c_double * 8)()
         check(_lib.lib().kf_stream_check(self.handle, out, self._stream()))
         return dict(ok=bool(out[0]), failed_chunk=bool(out[1]), cov_gap=out[2], state_gap=out[3],
-                    chunks=int(out[4]), chunk=int(out[5]), warmup=int(out[6]))
+                    chunks=int(out[4]), chunk=int(out[5]), warmup=int(out[6]),
+                    fallback={0: None, 2: 'chain', 4: 'gated'}[int(out[7])])
 
     def eval_combos(self, events, init, prev_time, target_end, k, combo_offset=0, logdets=True):
         """KF_MODEL_REF15 brute force (kf_eval_combos): filter f evaluates combination

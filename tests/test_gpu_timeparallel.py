@@ -335,26 +335,33 @@ def _gated(et, dt, pay, x0, thr, sequential):
     return out, flags, chk
 
 
-@pytest.mark.parametrize('offset,stands', [(0.5, True), (1.0, True), (2.0, False), (None, False)])
-def test_gated_route_equals_single_filter(offset, stands):
+@pytest.mark.parametrize('offset,absolute,stands,fallback', [(0.5, None, True, None), (1.0, None, True, None),
+                                                             (2.0, None, False, 'chain'), (None, -30.0, False, 'chain'),
+                                                             (None, -20.0, False, 'gated'),
+                                                             (None, -10.0, False, 'gated')])
+def test_gated_route_equals_single_filter(offset, absolute, stands, fallback):
     """kf_run_events' route for one long GATED filter (the adaptive threshold, kf_workers.py:
     959-1058): chunk starts from 2048 events of warm-up that apply the gate, every pass gated.
     Where the gate blocks few updates (thresholds 0.5 / 1.0 above the median record: 2 % / 7 %
     blocked) the warm-up meets the covariance and the chunked records stand; where it blocks many
-    (2.0 above: 20 %; the reference's r_value = -10: 97 %) the gated covariance's sawtooth keeps
-    the phase it started with, the seam check fails and the sequential fallback rewrites every
-    record.  Either way: the sequential gated filter's records, update flags and final state."""
+    (2.0 above: 20 %; -30: 58 %; -20: 89 %; the reference's r_value = -10: 97 %) the gated
+    covariance's sawtooth keeps the phase it started with, the seam check fails and the
+    sequential fallback rewrites every record: the chain kernel (bitwise the sequential filter)
+    or, where the chunked pass updated at most 1 event in 8, the look-ahead kernel (flags equal,
+    records to rounding).  Either way: the sequential gated filter's records, update flags and
+    final state."""
     et, dt, pay, x0 = _stream(70000, seed=11)
     base, _, _ = _gated(et, dt, pay, x0, None, True)
-    thr = -10.0 if offset is None else float(np.median(base[1])) + offset
+    thr = absolute if offset is None else float(np.median(base[1])) + offset
     seq, f_seq, _ = _gated(et, dt, pay, x0, thr, True)
     par, f_par, chk = _gated(et, dt, pay, x0, thr, False)
     assert chk['chunks'] > 1 and chk['warmup'] == 2048 and chk['ok'] == stands, chk
+    assert chk['fallback'] == fallback, chk
     assert 0 < f_seq.mean() < 1 or offset == 0.5
     np.testing.assert_array_equal(f_par, f_seq)
     for a, b in zip(par, seq):
         assert a.shape == b.shape and _rel(a, b) <= 1e-9
-    if not stands:
+    if fallback == 'chain':
         for a, b in zip(par, seq):
             assert np.array_equal(a, b)   # the fallback is the sequential kernel
 
