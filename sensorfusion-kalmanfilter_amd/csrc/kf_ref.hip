@@ -1205,26 +1205,52 @@ __global__ __launch_bounds__(64) void ref_chain_gated_kernel(const RefArgs a) {
     gate.init(a.threshold);
     const T thr = T(a.threshold);
     const T* pay = static_cast<const T*>(a.payload);
-    T* traj = static_cast<T*>(a.traj);
-    T* cov = static_cast<T*>(a.cov);
-    T* ldo = static_cast<T*>(a.logdet);
+    const bool cov = a.cov != nullptr, ldo = a.logdet != nullptr;
     const int T_ = a.T;
-    // the records of event t from this lane's chain state (slot `writer`'s lanes write; plain
-    // stores under the writer branch measured faster here than dropped buffer stores, which the
-    // seven non-writing slots would issue too)
-    auto record = [&](int t, const T (&xr)[3], const T (&Pr)[6], bool applied, bool writer) {
-        if (writer && traj && xi[0] >= 0 && xi[0] < M::NTRAJ) traj[int64_t(t) * M::NTRAJ + xi[0]] = xr[0];
-        if (writer && cov) {
+    // an event step's records (t wave-uniform): slot 0's lanes write, through buffer stores whose
+    // offsets drop the other slots' and the absent rows' stores (the chain kernel's form)
+    constexpr uint32_t rb = uint32_t(sizeof(T));
+    const uint32_t v_tr0 = slot == 0 && xi[0] >= 0 && xi[0] < M::NTRAJ ? uint32_t(xi[0]) * rb : kDropOffset;
+    uint32_t vp0[6];
 #pragma unroll
-            for (int k = 0; k < 6; ++k)
-                if (pr[k] >= 0) cov[int64_t(t) * M::NBLK + pr[k]] = Pr[k];
+    for (int k = 0; k < 6; ++k) vp0[k] = slot == 0 && pr[k] >= 0 ? uint32_t(pr[k]) * rb : kDropOffset;
+    const uint32_t v_ld0 = slot == 0 && c == 0 ? 0u : kDropOffset;
+    auto record_step = [&](int t, bool applied) {
+        stv(span_rsrc(a.traj, int64_t(t) * M::NTRAJ, rb, M::NTRAJ), v_tr0, x[0][0]);
+        if (cov) {
+            const auto rc = span_rsrc(a.cov, int64_t(t) * M::NBLK, rb, M::NBLK);
+#pragma unroll
+            for (int k = 0; k < 6; ++k) stv(rc, vp0[k], P[k]);
+        }
+        if (ldo) {
+            const T ld = group_sum(live ? chain_log_det(P) : T(0));
+            st = (ld == ld) ? st : kNotSpd;
+            stv(span_rsrc(a.logdet, t, rb, 1), v_ld0, ld);
+        }
+        if (slot == 0 && c == 0 && a.updated) a.updated[t] = applied ? 1 : 0;
+    };
+    // a look-ahead run's records (events t0 + slot for the slots < n; t0 wave-uniform): one
+    // descriptor over the run's rows, each slot's lanes at their row, the other stores dropped
+    const uint32_t v_trr = xi[0] >= 0 && xi[0] < M::NTRAJ ? uint32_t(slot * M::NTRAJ + xi[0]) * rb : kDropOffset;
+    uint32_t vpr[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) vpr[k] = pr[k] >= 0 ? uint32_t(slot * M::NBLK + pr[k]) * rb : kDropOffset;
+    const uint32_t v_ldr = c == 0 ? uint32_t(slot) * rb : kDropOffset;
+    auto record_run = [&](int t0, int n, const T (&xr)[3], const T (&Pr)[6]) {
+        const uint32_t wm = slot < n ? 0u : kDropOffset;
+        const uint32_t rows = uint32_t(T_ - t0 < 8 ? T_ - t0 : 8);
+        stv(span_rsrc(a.traj, int64_t(t0) * M::NTRAJ, rb, rows * M::NTRAJ), v_trr | wm, xr[0]);
+        if (cov) {
+            const auto rc = span_rsrc(a.cov, int64_t(t0) * M::NBLK, rb, rows * M::NBLK);
+#pragma unroll
+            for (int k = 0; k < 6; ++k) stv(rc, vpr[k] | wm, Pr[k]);
         }
         if (ldo) {
             const T ld = group_sum(live ? chain_log_det(Pr) : T(0));
-            st = (ld == ld) ? st : kNotSpd;
-            if (writer && c == 0) ldo[t] = ld;
+            st = (ld == ld || slot >= n) ? st : kNotSpd;
+            stv(span_rsrc(a.logdet, t0, rb, rows), v_ldr | wm, ld);
         }
-        if (writer && c == 0 && a.updated) a.updated[t] = applied ? 1 : 0;
+        if (slot < n && c == 0 && a.updated) a.updated[t0 + slot] = 0;
     };
     int t = 0;
     // a look-ahead after an event that did not update, unless the last one found its run over at
@@ -1310,9 +1336,12 @@ __global__ __launch_bounds__(64) void ref_chain_gated_kernel(const RefArgs a) {
                 for (int k = 0; k < 6; ++k) P[k] = quiet_nan<T>();
             }
         }
-        record(t, x[0], P, applied, slot == 0);
+        record_step(t, applied);
         ++t;
-        if (applied || t >= T_) continue;  // wave-uniform (the gate's group ops give every slot the decision)
+        // every lane holds the same decision (the gate's group ops, every slot the same event), but
+        // the compiler cannot know it: taken from lane 0, so that t and the loop stay scalar (a
+        // per-lane `continue` made t divergent, and with it every event's type branches)
+        if (__builtin_amdgcn_readfirstlane(int(applied)) || t >= T_) continue;
         if (cool > 0) {
             --cool;
             continue;
@@ -1376,7 +1405,7 @@ __global__ __launch_bounds__(64) void ref_chain_gated_kernel(const RefArgs a) {
         const uint64_t om = __builtin_amdgcn_ballot_w64(opens && c == 0);
         const int nvalid = T_ - t < 8 ? T_ - t : 8;
         const int n = om ? int(__builtin_ctzll(om)) / kGroup : nvalid;  // events of the predict run
-        if (slot < n) record(e, xp, Pp, false, true);
+        record_run(t, n, xp, Pp);
         st = __builtin_amdgcn_ballot_w64(st == kNotSpd) ? kNotSpd : st;  // a failed record in any slot
         if (n > 0) {
             const int src = (n - 1) * kGroup + c;

@@ -1,7 +1,9 @@
 """Reduce tools/search_stalls.sh's passes: per search kernel, the SQ counters summed over its
 dispatches, per 64 subsets where that is meaningful, and the shares of the wave cycles.
 
-usage: python tools/search_stalls.py OUTDIR   -> prints and writes OUTDIR/search_stalls.json
+usage: python tools/search_stalls.py OUTDIR [KERNEL_REGEX]   -> prints and writes OUTDIR/search_stalls.json
+(KERNEL_REGEX: group 1 the kernel's stem, group 2 its template arguments; default the search
+kernels; tools/gated_stalls.sh passes the chain and look-ahead kernels')
 """
 import collections
 import csv
@@ -12,19 +14,25 @@ import re
 import sys
 
 
+KERNELS = r'(ref15_search_\w+?)_kernel<([^>]*)>'
+
+
 def sums(d):
     out = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                m = re.search(r'(ref15_search_\w+?)_kernel<([^>]*)>', r['Kernel_Name'])
+                m = re.search(KERNELS, r['Kernel_Name'])
                 if m:
                     out[f'{m.group(1)}<{m.group(2)}>'][r['Counter_Name']] += float(r['Counter_Value'])
     return out
 
 
 def main():
+    global KERNELS
     d = sys.argv[1]
+    if len(sys.argv) > 2:
+        KERNELS = sys.argv[2]
     tot = collections.defaultdict(dict)
     for p in ('p1', 'p2', 'p3'):
         for k, cs in sums(os.path.join(d, p)).items():
@@ -33,7 +41,7 @@ def main():
     for f in glob.glob(os.path.join(d, 'kt', '**', '*kernel_stats.csv'), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                m = re.search(r'(ref15_search_\w+?)_kernel<([^>]*)>', r['Name'])
+                m = re.search(KERNELS, r['Name'])
                 if m:
                     kt[f'{m.group(1)}<{m.group(2)}>'] = float(r['TotalDurationNs']) * 1e-6
     rep = {}
