@@ -416,3 +416,43 @@ def test_lookahead_gated_kernel_is_f64_only():
         return out
     for a, b in zip(run('gated'), run('chain')):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize('consts', ['reference', 'custom'])
+@pytest.mark.parametrize('model', ['ref15', 'ref8'])
+def test_lookahead_gated_kernel_models_and_constants(model, consts):
+    """The look-ahead kernel on both reference models, with the reference's constants (the
+    compiled literals) and a caller's (kf_params: its CUSTOM instantiation reads Q, R, P0 from
+    the handle), against the chain kernel: flags equal, records within 1e-9 relative.  The
+    threshold sits far enough above the ungated filter's log-dets that most updates are blocked
+    (2-50 % applied) and the look-ahead runs are long."""
+    T = 20000
+    et, dt, pay, x0 = _stream(T, seed=31, skips=40)
+    n = 15 if model == 'ref15' else 8
+    params = _symmetric_params(model, 5) if consts == 'custom' else None
+
+    def run(kernel, thr):
+        kf = kfmi.BatchedKF(model, 1, 'f64', options={'events_kernel': kernel}, params=params)
+        P0 = kf.state()[1].cpu().numpy()
+        xs = np.zeros((n, 1))
+        xs[0:2, 0] = x0[0:2]
+        kf.set_state(xs, P0)
+        tr, ld, up, cv = kf.run_events(et[:, None], dt[:, None], pay[:, :, None], updated=True, cov=True,
+                                       threshold=thr, sequential=True)
+        x, P = kf.state()
+        out = tuple(v.double().cpu().numpy() for v in (tr, ld, cv, x, P))
+        flags, st = up.cpu().numpy(), int(kf.status().sum().item())
+        kf.close()
+        return out, flags, st
+    base, _, _ = run('chain', None)
+    for above in (40.0, 20.0, 10.0, 5.0, 2.5):  # the gate opens above the threshold: from rare to frequent
+        thr = float(np.median(base[1])) + above
+        c, fc, sc = run('chain', thr)
+        if fc.mean() >= 0.02:
+            break
+    assert 0.02 <= fc.mean() < 0.5, (above, fc.mean())
+    g, fg, sg = run('gated', thr)
+    assert sg == sc == 0
+    np.testing.assert_array_equal(fg, fc)
+    for a, b in zip(g, c):
+        assert a.shape == b.shape and _rel(a, b) <= 1e-9
