@@ -322,6 +322,48 @@ def test_stream_run_replays_as_a_hip_graph():
     kf.close()
 
 
+
+def test_gated_stream_route_replays_as_a_hip_graph():
+    """The gated one-filter route with the look-ahead fallback (r_value = -10: the seam check
+    fails, the chunked pass updated ~3 % of events) captured into a hipGraph after an eager call:
+    the device choice and both queued fallback kernels replay as they are, and the replay gives
+    the eager records, flags and final state."""
+    et, dt, pay, x0 = _stream(70000, seed=11)
+    dev = torch.device('cuda', 0)
+    kf = kfmi.BatchedKF('ref15', 1, 'f64')
+    P0b = torch.as_tensor(ref15.to_blocks(ref15.P0)[:, None], device=dev)
+    x0d = torch.as_tensor(x0[:, None], device=dev)
+    etd, dtd, payd = (torch.as_tensor(v, device=dev) for v in (et[:, None], dt[:, None], pay[:, :, None]))
+    T = len(et)
+    tr, ld = kf.empty(T, 6, 1), kf.empty(T, 1)
+    up = torch.empty(T, 1, dtype=torch.uint8, device=dev)
+
+    def run():
+        kf.set_state(x0d, P0b)
+        out = kf.run_events(etd, dtd, payd, updated=True, threshold=-10.0)
+        tr.copy_(out[0])
+        ld.copy_(out[1])
+        up.copy_(out[2])
+
+    run()
+    torch.cuda.synchronize()
+    eager = (tr.cpu().numpy().copy(), ld.cpu().numpy().copy(), up.cpu().numpy().copy(), kf.state()[0].cpu().numpy())
+    chk = kf.stream_check()
+    assert not chk['ok'] and chk['fallback'] == 'gated', chk
+    tr.zero_()
+    ld.zero_()
+    up.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        run()
+    g.replay()
+    torch.cuda.synchronize()
+    replay = (tr.cpu().numpy(), ld.cpu().numpy(), up.cpu().numpy(), kf.state()[0].cpu().numpy())
+    for a, b in zip(replay, eager):
+        np.testing.assert_array_equal(a, b)
+    assert kf.stream_check()['fallback'] == 'gated'
+    kf.close()
+
 def _gated(et, dt, pay, x0, thr, sequential):
     kf = kfmi.BatchedKF('ref15', 1, 'f64')
     kf.set_state(x0[:, None], ref15.to_blocks(ref15.P0)[:, None])
