@@ -1156,10 +1156,11 @@ __global__ __launch_bounds__(kBlock) void ref_chain_kernel(const RefArgs a) {
 // takes event t + j; the first slot whose event would open the gate (GateBand on its closed-form
 // P_pred, a ballot over the slots) ends the run: the slots before it write their records at
 // once and hand their state on, and that event runs next as a chain-kernel event.  The closed
-// form rounds differently from one predict after another (records within ~1e-15 relative of the
-// sequential kernel's); a gate decision could only differ within that distance of the threshold.
-// KF_OPT_EVENTS_KERNEL = 4 (and kf_run_events' gated one-filter route, when the chunked run
-// falls back) runs it.
+// form rounds differently from one predict after another (records within 1.8e-12 relative of the
+// chain kernel's over 70,000 events, every flag equal); a gate decision could only differ within
+// that distance of the threshold (in f32 it does: f64 only).  KF_OPT_EVENTS_KERNEL = 4 runs it,
+// and kf_run_events' gated one-filter route when the chunked run falls back after updating at
+// most 1 event in 8 (launch_stream_choose).
 // ------------------------------------------------------------------------------------
 template <typename T, class M, bool CUSTOM>
 __global__ __launch_bounds__(64) void ref_chain_gated_kernel(const RefArgs a) {
